@@ -1,0 +1,332 @@
+// Graph-level kernels of U2GNN on gfx950: sum pooling (+dropout), the per-layer linear
+// head, the label-smoothed cross-entropy, the fused clip_grad_norm_ + Adam sweep, and the
+// sampled-softmax loss of the unsupervised model.
+#include "u2gnn_common.h"
+
+namespace {
+
+// ------------------------------------------------------------------------------------------
+// a5/a6 pooling: torch.spmm(graph_pool, output_Tr) with graph_pool in CSR form
+// (pytorch_U2GNN_Sup.py:41) followed by dropout (:42).  Block = one graph x 256 columns.
+// ------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) pool_fwd_kernel(const float *X, int64_t ldx, const int64_t *rowptr,
+                                                       const int64_t *colidx, const float *vals, float *G, int64_t ldg,
+                                                       int64_t d, float p, uint64_t seed) {
+    const int64_t b = blockIdx.x;
+    const int64_t c = (int64_t)blockIdx.y * 256 + threadIdx.x;
+    if (c >= d) return;
+    const int64_t e0 = rowptr[b], e1 = rowptr[b + 1];
+    float s = 0.f;
+    for (int64_t e = e0; e < e1; ++e) s += vals[e] * X[colidx[e] * ldx + c];
+    if (p > 0.f) s = u2gnn_keep(seed, (uint32_t)b, (uint32_t)c, p) ? s * (1.f / (1.f - p)) : 0.f;
+    G[b * ldg + c] = s;
+}
+
+__global__ void __launch_bounds__(256) pool_bwd_kernel(const float *dGd, int64_t ldg, const int64_t *rowptr,
+                                                       const int64_t *colidx, const float *vals, float *dX,
+                                                       int64_t ldx, int64_t d, float p, uint64_t seed) {
+    const int64_t b = blockIdx.x;
+    const int64_t c = (int64_t)blockIdx.y * 256 + threadIdx.x;
+    if (c >= d) return;
+    float g = dGd[b * ldg + c];
+    if (p > 0.f) g = u2gnn_keep(seed, (uint32_t)b, (uint32_t)c, p) ? g * (1.f / (1.f - p)) : 0.f;
+    const int64_t e0 = rowptr[b], e1 = rowptr[b + 1];
+    for (int64_t e = e0; e < e1; ++e) atomicAdd(dX + colidx[e] * ldx + c, vals[e] * g);
+}
+
+// head: scores[b, k] (+)= G[b,:] . W[k,:] + bias[k];  one wave per (b, k)
+__global__ void __launch_bounds__(256) head_fwd_kernel(const float *G, int64_t ldg, const float *W, const float *bias,
+                                                       float *scores, int64_t B, int64_t C, int64_t d, int accumulate) {
+    const int64_t o = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (o >= B * C) return;
+    const int64_t b = o / C, k = o - b * C;
+    float s = 0.f;
+    for (int64_t j = lane; j < d; j += 64) s += G[b * ldg + j] * W[k * d + j];
+    s = wave_sum(s);
+    if (lane == 0) scores[o] = (accumulate ? scores[o] : 0.f) + s + bias[k];
+}
+
+// head backward: thread per feature j computes dG[:, j] and dW[:, j]; block 0 also db.
+__global__ void __launch_bounds__(256) head_bwd_kernel(const float *dS, const float *G, int64_t ldg, const float *W,
+                                                       float *dG, int64_t lddg, float *dW, float *db, int64_t B,
+                                                       int64_t C, int64_t d, int accumulate) {
+    const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (j < d) {
+        for (int64_t b = 0; b < B; ++b) {
+            float s = 0.f;
+            for (int64_t k = 0; k < C; ++k) s += dS[b * C + k] * W[k * d + j];
+            dG[b * lddg + j] = s;
+        }
+        for (int64_t k = 0; k < C; ++k) {
+            float s = 0.f;
+            for (int64_t b = 0; b < B; ++b) s += dS[b * C + k] * G[b * ldg + j];
+            dW[k * d + j] = accumulate ? dW[k * d + j] + s : s;
+        }
+    }
+    if (blockIdx.x == 0 && threadIdx.x < C) {
+        float s = 0.f;
+        for (int64_t b = 0; b < B; ++b) s += dS[b * C + threadIdx.x];
+        db[threadIdx.x] = accumulate ? db[threadIdx.x] + s : s;
+    }
+}
+
+// a7: label smoothing (0.9 / 0.1/(C-1)) + mean soft cross-entropy; single block.
+__global__ void __launch_bounds__(256) smoothed_ce_kernel(const float *scores, const int64_t *labels, int64_t B,
+                                                          int64_t C, float smoothing, float *loss, float *dscores) {
+    __shared__ float red[256];
+    float acc = 0.f;
+    const float off = smoothing / (float)(C - 1), on = 1.f - smoothing;
+    for (int64_t b = threadIdx.x; b < B; b += 256) {
+        const float *s = scores + b * C;
+        float m = -INFINITY;
+        for (int64_t k = 0; k < C; ++k) m = fmaxf(m, s[k]);
+        float z = 0.f;
+        for (int64_t k = 0; k < C; ++k) z += expf(s[k] - m);
+        const float lz = logf(z);
+        const int64_t y = labels[b];
+        for (int64_t k = 0; k < C; ++k) {
+            const float t = (k == y) ? on : off;
+            const float ls = s[k] - m - lz;
+            acc += -t * ls;
+            dscores[b * C + k] = (expf(ls) - t) / (float)B;
+        }
+    }
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) loss[0] = red[0] / (float)B;
+}
+
+// ------------------------------------------------------------------------------------------
+// a9: clip_grad_norm_ + Adam over one flat fp32 buffer
+// ------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) sqnorm_partial_kernel(const float *g, int64_t n, double *ws) {
+    __shared__ double red[4];
+    double s = 0.0;
+    const int64_t n4 = n >> 2;
+    const float4 *g4 = reinterpret_cast<const float4 *>(g);
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+        const float4 v = g4[i];
+        s += (double)v.x * v.x + (double)v.y * v.y + (double)v.z * v.z + (double)v.w * v.w;
+    }
+    if (blockIdx.x == 0)
+        for (int64_t i = (n4 << 2) + threadIdx.x; i < n; i += 256) s += (double)g[i] * g[i];
+    s = wave_sum_d(s);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) ws[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+__global__ void __launch_bounds__(256) sqnorm_final_kernel(const double *ws, int nb, float *out) {
+    __shared__ double red[4];
+    double s = 0.0;
+    for (int i = threadIdx.x; i < nb; i += 256) s += ws[i];
+    s = wave_sum_d(s);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) out[0] = (float)(red[0] + red[1] + red[2] + red[3]);
+}
+
+// torch.optim.Adam (_single_tensor_adam, no weight decay / amsgrad):
+//   m.lerp_(g, 1-b1); v = v*b2 + (1-b2) g*g; denom = sqrt(v)/bc2_sqrt + eps; p -= step_size*m/denom
+__global__ void __launch_bounds__(256) adam_kernel(float *param, const float *grad, float *m, float *v, int64_t n,
+                                                   const float *sqnorm, float max_norm, float b1, float b2, float eps,
+                                                   float step_size, float bc2_sqrt) {
+    float coef = 1.f;
+    if (sqnorm) {
+        const float total = sqrtf(sqnorm[0]);
+        coef = fminf(1.f, max_norm / (total + 1e-6f));
+    }
+    const float w1 = 1.f - b1, w2 = 1.f - b2;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        const float g = grad[i] * coef;
+        float mi = m[i];
+        mi = mi + w1 * (g - mi);
+        float vi = v[i] * b2 + w2 * g * g;
+        m[i] = mi;
+        v[i] = vi;
+        const float denom = sqrtf(vi) / bc2_sqrt + eps;
+        param[i] = param[i] - step_size * (mi / denom);
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// a10 sampled softmax (sampled_softmax.py:36-56).  One block per input row; the sampled
+// rows of W are read straight from HBM/L2 (S = 512 rows of D floats, shared by every row).
+// ------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) ss_fwd_kernel(const float *X, int64_t ldx, const int64_t *labels,
+                                                     const int64_t *sids, int64_t S, const float *W, int64_t ldw,
+                                                     float *loss, float *prob, int64_t D) {
+    __shared__ float xs[1024];
+    __shared__ float red[8];
+    const int64_t i = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    for (int64_t c = tid; c < D; c += 256) xs[c] = X[i * ldx + c];
+    __syncthreads();
+    float m = -INFINITY, s = 0.f;
+    float *pr = prob + i * S;
+    for (int64_t j = tid; j < S; j += 256) {
+        const float *wr = W + sids[j] * ldw;
+        float dot = 0.f;
+        for (int64_t c = 0; c < D; ++c) dot += xs[c] * wr[c];
+        pr[j] = dot;  // logits, normalised below
+        const float mn = fmaxf(m, dot);
+        s = s * expf(m - mn) + expf(dot - mn);
+        m = mn;
+    }
+    const float mw = wave_max(m);
+    s = (m == -INFINITY) ? 0.f : s * expf(m - mw);
+    s = wave_sum(s);
+    if (lane == 0) {
+        red[w] = mw;
+        red[4 + w] = s;
+    }
+    __syncthreads();
+    const float M = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    float tot = 0.f;
+    for (int k = 0; k < 4; ++k) tot += red[k] == -INFINITY ? 0.f : red[4 + k] * expf(red[k] - M);
+    const float lse = M + logf(tot);
+    for (int64_t j = tid; j < S; j += 256) pr[j] = expf(pr[j] - lse);
+    if (tid == 0) {
+        const float *wy = W + labels[i] * ldw;
+        float t = 0.f;
+        for (int64_t c = 0; c < D; ++c) t += xs[c] * wy[c];
+        loss[i] = lse - t;
+    }
+}
+
+// dX[i, c] = g_i (sum_j prob_ij W[s_j, c] - W[y_i, c]); dW[y_i, c] -= g_i X[i, c]
+__global__ void __launch_bounds__(256) ss_bwd_x_kernel(const float *X, int64_t ldx, const int64_t *labels,
+                                                       const int64_t *sids, int64_t S, const float *W, int64_t ldw,
+                                                       const float *prob, const float *dloss, float *dX, int64_t lddx,
+                                                       float *dW, int64_t lddw, int64_t D) {
+    const int64_t i = blockIdx.x;
+    const float g = dloss ? dloss[i] : 1.f;
+    const float *pr = prob + i * S;
+    for (int64_t c = threadIdx.x; c < D; c += 256) {
+        float s = 0.f;
+        for (int64_t j = 0; j < S; ++j) s += pr[j] * W[sids[j] * ldw + c];
+        dX[i * lddx + c] = g * (s - W[labels[i] * ldw + c]);
+        atomicAdd(dW + labels[i] * lddw + c, -g * X[i * ldx + c]);
+    }
+}
+
+// dW[s_j, c] += sum_i g_i prob_ij X[i, c]; block per sample j
+__global__ void __launch_bounds__(256) ss_bwd_w_kernel(const float *X, int64_t ldx, const int64_t *sids, int64_t S,
+                                                       const float *prob, const float *dloss, float *dW, int64_t lddw,
+                                                       int64_t n_rows, int64_t D) {
+    __shared__ float red[4][256];
+    const int64_t j = blockIdx.x;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int64_t c0 = 0; c0 < D; c0 += 64) {
+        const int64_t c = c0 + lane;
+        float s = 0.f;
+        if (c < D)
+            for (int64_t i = w; i < n_rows; i += 4) s += (dloss ? dloss[i] : 1.f) * prob[i * S + j] * X[i * ldx + c];
+        red[w][lane] = s;
+        __syncthreads();
+        if (w == 0 && c < D) atomicAdd(dW + sids[j] * lddw + c, red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane]);
+        __syncthreads();
+    }
+}
+
+inline unsigned grid_for(int64_t n, int64_t per_block, int64_t cap = 8192) {
+    int64_t g = (n + per_block - 1) / per_block;
+    if (g < 1) g = 1;
+    if (g > cap) g = cap;
+    return (unsigned)g;
+}
+
+}  // namespace
+
+extern "C" {
+
+int u2gnn_pool_fwd(const float *X, int64_t ldx, const int64_t *rowptr, const int64_t *colidx, const float *vals,
+                   float *G, int64_t ldg, int64_t B, int64_t d, float p, uint64_t seed, void *stream) {
+    if (!X || !rowptr || !colidx || !vals || !G || B < 1 || d < 1) return U2GNN_E_ARG;
+    hipLaunchKernelGGL(pool_fwd_kernel, dim3((unsigned)B, (unsigned)((d + 255) / 256)), dim3(256), 0,
+                       u2gnn_stream(stream), X, ldx, rowptr, colidx, vals, G, ldg, d, p, seed);
+    return u2gnn_launch_status();
+}
+
+int u2gnn_pool_bwd(const float *dGd, int64_t ldg, const int64_t *rowptr, const int64_t *colidx, const float *vals,
+                   float *dX, int64_t ldx, int64_t B, int64_t d, float p, uint64_t seed, void *stream) {
+    if (!dGd || !rowptr || !colidx || !vals || !dX || B < 1 || d < 1) return U2GNN_E_ARG;
+    hipLaunchKernelGGL(pool_bwd_kernel, dim3((unsigned)B, (unsigned)((d + 255) / 256)), dim3(256), 0,
+                       u2gnn_stream(stream), dGd, ldg, rowptr, colidx, vals, dX, ldx, d, p, seed);
+    return u2gnn_launch_status();
+}
+
+int u2gnn_head_fwd(const float *G, int64_t ldg, const float *W, const float *bias, float *scores, int64_t B, int64_t C,
+                   int64_t d, int32_t accumulate, void *stream) {
+    if (!G || !W || !bias || !scores || B < 1 || C < 1) return U2GNN_E_ARG;
+    hipLaunchKernelGGL(head_fwd_kernel, dim3(grid_for(B * C, 4, 1 << 30)), dim3(256), 0, u2gnn_stream(stream), G, ldg,
+                       W, bias, scores, B, C, d, accumulate);
+    return u2gnn_launch_status();
+}
+
+int u2gnn_head_bwd(const float *dscores, const float *G, int64_t ldg, const float *W, float *dG, int64_t lddg,
+                   float *dW, float *db, int64_t B, int64_t C, int64_t d, int32_t accumulate, void *stream) {
+    if (!dscores || !G || !W || !dG || !dW || !db || C > 256) return U2GNN_E_ARG;
+    hipLaunchKernelGGL(head_bwd_kernel, dim3(grid_for(d, 256, 1 << 30)), dim3(256), 0, u2gnn_stream(stream), dscores,
+                       G, ldg, W, dG, lddg, dW, db, B, C, d, accumulate);
+    return u2gnn_launch_status();
+}
+
+int u2gnn_smoothed_ce(const float *scores, const int64_t *labels, int64_t B, int64_t C, float smoothing, float *loss,
+                      float *dscores, void *stream) {
+    if (!scores || !labels || !loss || !dscores || B < 1 || C < 2) return U2GNN_E_ARG;
+    hipLaunchKernelGGL(smoothed_ce_kernel, dim3(1), dim3(256), 0, u2gnn_stream(stream), scores, labels, B, C,
+                       smoothing, loss, dscores);
+    return u2gnn_launch_status();
+}
+
+int u2gnn_sqnorm(const float *g, int64_t n, float *ws, float *sqnorm, void *stream) {
+    if (!g || !ws || !sqnorm || (reinterpret_cast<uintptr_t>(g) & 15)) return U2GNN_E_ARG;
+    const unsigned nb = grid_for(n, 256 * 8, 512);
+    hipStream_t st = u2gnn_stream(stream);
+    double *wsd = reinterpret_cast<double *>(ws);
+    hipLaunchKernelGGL(sqnorm_partial_kernel, dim3(nb), dim3(256), 0, st, g, n, wsd);
+    hipLaunchKernelGGL(sqnorm_final_kernel, dim3(1), dim3(256), 0, st, wsd, (int)nb, sqnorm);
+    return u2gnn_launch_status();
+}
+
+int u2gnn_adam(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, int64_t n, const float *sqnorm,
+               float max_norm, float beta1, float beta2, float eps, float step_size, float bc2_sqrt, void *stream) {
+    if (!param || !grad || !exp_avg || !exp_avg_sq) return U2GNN_E_ARG;
+    if (n == 0) return U2GNN_OK;
+    hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n, 256, 4096)), dim3(256), 0, u2gnn_stream(stream), param, grad,
+                       exp_avg, exp_avg_sq, n, sqnorm, max_norm, beta1, beta2, eps, step_size, bc2_sqrt);
+    return u2gnn_launch_status();
+}
+
+int u2gnn_sampled_softmax_fwd(const float *X, int64_t ldx, const int64_t *labels, const int64_t *sample_ids, int64_t S,
+                              const float *W, int64_t ldw, float *loss, float *prob, int64_t n_rows, int64_t D,
+                              void *stream) {
+    if (!X || !labels || !sample_ids || !W || !loss || !prob || D > 1024 || S < 1) return U2GNN_E_ARG;
+    if (n_rows == 0) return U2GNN_OK;
+    hipLaunchKernelGGL(ss_fwd_kernel, dim3((unsigned)n_rows), dim3(256), 0, u2gnn_stream(stream), X, ldx, labels,
+                       sample_ids, S, W, ldw, loss, prob, D);
+    return u2gnn_launch_status();
+}
+
+int u2gnn_sampled_softmax_bwd(const float *X, int64_t ldx, const int64_t *labels, const int64_t *sample_ids, int64_t S,
+                              const float *W, int64_t ldw, const float *prob, const float *dloss, float *dX,
+                              int64_t lddx, float *dW, int64_t lddw, int64_t n_rows, int64_t D, void *stream) {
+    if (!X || !labels || !sample_ids || !W || !prob || !dX || !dW || S < 1) return U2GNN_E_ARG;
+    if (n_rows == 0) return U2GNN_OK;
+    hipStream_t st = u2gnn_stream(stream);
+    hipLaunchKernelGGL(ss_bwd_x_kernel, dim3((unsigned)n_rows), dim3(256), 0, st, X, ldx, labels, sample_ids, S, W, ldw,
+                       prob, dloss, dX, lddx, dW, lddw, D);
+    hipLaunchKernelGGL(ss_bwd_w_kernel, dim3((unsigned)S), dim3(256), 0, st, X, ldx, sample_ids, S, prob, dloss, dW,
+                       lddw, n_rows, D);
+    return u2gnn_launch_status();
+}
+
+int u2gnn_abi_version(void) { return U2GNN_ABI_VERSION; }
+
+}  // extern "C"

@@ -1,0 +1,140 @@
+"""ctypes binding of the two native libraries (C ABI: include/u2gnn_hip.h, include/u2gnn_lus.h).
+
+The product path has no CPU fallback: if ``libu2gnn_hip.so`` is missing or cannot be
+loaded, every kernel entry point raises ``U2GNNNativeError`` (build it with
+``make -C graph-transformer_amd/csrc`` or ``python -c 'import __graft_entry__ as g; g.build()'``).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+from ctypes import POINTER, c_float, c_int32, c_int64, c_size_t, c_uint8, c_uint32, c_uint64, c_void_p
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO_ROOT = os.path.dirname(PKG_ROOT)
+LIB_DIR = os.path.join(PKG_ROOT, "lib")
+INCLUDE_DIR = os.path.join(REPO_ROOT, "include")
+HIP_LIB_PATH = os.path.join(LIB_DIR, "libu2gnn_hip.so")
+LUS_LIB_PATH = os.path.join(LIB_DIR, "libu2gnn_lus.so")
+
+
+class U2GNNNativeError(RuntimeError):
+    pass
+
+
+# error codes (u2gnn_hip.h)
+U2GNN_OK = 0
+ERRORS = {-1: "bad argument", -2: "misaligned pointer / leading dimension", -3: "shape not a tile multiple"}
+
+EPI_STORE, EPI_BIAS, EPI_BIAS_DROP_RESID, EPI_BIAS_RELU_DROP, EPI_RELU_DROP_BWD, EPI_ACCUM, EPI_ATTN_DS = range(7)
+PREC_F32, PREC_BF16X3, PREC_BF16 = 0, 1, 2
+
+
+class GemmArgs(ctypes.Structure):
+    _fields_ = [
+        ("A", c_void_p), ("B", c_void_p), ("C", c_void_p),
+        ("M", c_int64), ("N", c_int64), ("K", c_int64),
+        ("lda", c_int64), ("ldb", c_int64), ("ldc", c_int64),
+        ("trans_a", c_int32), ("trans_b", c_int32),
+        ("epilogue", c_int32), ("split_k", c_int32),
+        ("slab_stride", c_int64),
+        ("bias", c_void_p), ("aux0", c_void_p), ("aux1", c_void_p), ("rowvec", c_void_p),
+        ("ld_aux", c_int64),
+        ("alpha", c_float),
+        ("scale_cols", c_int64),
+        ("p_drop", c_float),
+        ("seed", c_uint64),
+        ("precision", c_int32),
+        ("tile", c_int32),
+    ]
+
+
+I64, F32, VP, I32 = c_int64, c_float, c_void_p, c_int32
+
+_HIP_SIGS = {
+    "u2gnn_abi_version": ([], c_int32),
+    "u2gnn_gather_rows": ([VP, I64, I64, VP, I64, VP, I64, I64, I64, I64, I64, VP, VP], c_int32),
+    "u2gnn_scatter_add_rows": ([VP, I64, VP, I64, VP, I64, I64, I64, VP], c_int32),
+    "u2gnn_gemm": ([POINTER(GemmArgs), VP], c_int32),
+    "u2gnn_slab_reduce": ([VP, I32, I64, I64, I64, I64, I64, I64, I64, I64, VP, I64, F32, I32, VP], c_int32),
+    "u2gnn_pack_padded": ([VP, I64, I64, I64, I64, I64, I64, I64, VP, I64, VP], c_int32),
+    "u2gnn_colsum": ([VP, I64, I64, I64, I64, I64, VP, I32, VP, VP], c_int32),
+    "u2gnn_attn_softmax_fwd": ([VP, I64, VP, VP, I64, I64, I64, I64, I64, F32, c_uint64, VP], c_int32),
+    "u2gnn_rowdot": ([VP, I64, VP, I64, VP, I64, I64, VP], c_int32),
+    "u2gnn_layernorm_fwd": ([VP, I64, VP, VP, VP, I64, VP, VP, I64, I64, I64, I64, F32, VP], c_int32),
+    "u2gnn_layernorm_bwd": ([VP, I64, VP, I64, VP, VP, VP, VP, I64, VP, I64, F32, c_uint64, VP, I64, I64, I64, I64,
+                             VP], c_int32),
+    "u2gnn_layernorm_param_reduce": ([VP, I64, I64, I64, VP, VP, I32, VP], c_int32),
+    "u2gnn_pool_fwd": ([VP, I64, VP, VP, VP, VP, I64, I64, I64, F32, c_uint64, VP], c_int32),
+    "u2gnn_pool_bwd": ([VP, I64, VP, VP, VP, VP, I64, I64, I64, F32, c_uint64, VP], c_int32),
+    "u2gnn_head_fwd": ([VP, I64, VP, VP, VP, I64, I64, I64, I32, VP], c_int32),
+    "u2gnn_head_bwd": ([VP, VP, I64, VP, VP, I64, VP, VP, I64, I64, I64, I32, VP], c_int32),
+    "u2gnn_smoothed_ce": ([VP, VP, I64, I64, F32, VP, VP, VP], c_int32),
+    "u2gnn_sqnorm": ([VP, I64, VP, VP, VP], c_int32),
+    "u2gnn_adam": ([VP, VP, VP, VP, I64, VP, F32, F32, F32, F32, F32, F32, VP], c_int32),
+    "u2gnn_sampled_softmax_fwd": ([VP, I64, VP, VP, I64, VP, I64, VP, VP, I64, I64, VP], c_int32),
+    "u2gnn_sampled_softmax_bwd": ([VP, I64, VP, VP, I64, VP, I64, VP, VP, VP, I64, VP, I64, I64, I64, VP], c_int32),
+    "u2gnn_dropout_mask": ([c_uint64, I64, I64, F32, VP, VP], c_int32),
+}
+
+_LUS_SIGS = {
+    "u2gnn_lus_create": ([I64, c_uint32], VP),
+    "u2gnn_lus_destroy": ([VP], None),
+    "u2gnn_lus_sample": ([VP, c_size_t, VP, POINTER(c_int32)], c_int32),
+    "u2gnn_lus_expected_count": ([VP, c_int32, VP, c_size_t, VP], c_int32),
+    "u2gnn_lus_probability": ([VP, I64], c_float),
+    "u2gnn_lus_sample_unique": ([VP, c_size_t, VP, c_size_t, VP], c_int32),
+    "u2gnn_lus_accidental_matches": ([VP, c_size_t, VP, c_size_t, VP, c_size_t, POINTER(c_size_t)], c_int32),
+}
+
+_hip = None
+_lus = None
+
+
+def _bind(lib, sigs):
+    for name, (args, res) in sigs.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = res
+    return lib
+
+
+def hip_lib():
+    """The gfx950 kernel library; raises if it is not built (no CPU fallback exists)."""
+    global _hip
+    if _hip is None:
+        if not os.path.exists(HIP_LIB_PATH):
+            raise U2GNNNativeError(f"{HIP_LIB_PATH} not built: run `make -C graph-transformer_amd/csrc` "
+                                   "(the U2GNN hot path has no CPU fallback)")
+        try:
+            lib = ctypes.CDLL(HIP_LIB_PATH)
+        except OSError as e:  # pragma: no cover
+            raise U2GNNNativeError(f"cannot load {HIP_LIB_PATH}: {e}") from e
+        _hip = _bind(lib, _HIP_SIGS)
+        v = _hip.u2gnn_abi_version()
+        if v != 1:
+            raise U2GNNNativeError(f"ABI mismatch: library {v}, binding 1")
+    return _hip
+
+
+def lus_lib():
+    global _lus
+    if _lus is None:
+        if not os.path.exists(LUS_LIB_PATH):
+            raise U2GNNNativeError(f"{LUS_LIB_PATH} not built: run `make -C graph-transformer_amd/csrc`")
+        _lus = _bind(ctypes.CDLL(LUS_LIB_PATH), _LUS_SIGS)
+    return _lus
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = ERRORS.get(rc, f"hipError {rc}")
+        raise U2GNNNativeError(f"{what} failed: {msg} (rc={rc})")
+
+
+def header_symbols(header: str):
+    """Function names declared in include/<header> (used by the ABI export test)."""
+    txt = open(os.path.join(INCLUDE_DIR, header)).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(u2gnn_[a-z0-9_]+)\s*\(", txt)))

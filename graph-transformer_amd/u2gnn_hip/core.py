@@ -1,0 +1,207 @@
+"""Model-level orchestration of the U2GNN hot path on the gfx950 kernels.
+
+* ``DeviceBatch``   — one mini-batch resident in HBM (input_x, X_concat, pooling CSR, labels).
+* ``SupCore``       — forward / backward of pytorch_U2GNN_Sup.TransformerU2GNN (:30-46):
+                      gather -> L x (T encoder layers -> sum-pool -> dropout -> Linear, summed).
+* ``FlatParams``    — all parameters (and grads, Adam moments) in single flat fp32 buffers,
+                      so clip_grad_norm_ + Adam are two sweeps (train_pytorch_U2GNN_Sup.py:160-161).
+* ``FusedAdam``     — torch.optim.Adam semantics with the clip coefficient applied on device.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import List, Optional
+
+import numpy as np
+import torch
+
+from . import kernels as K
+from .engine import (SITE_ATTN, SITE_DROP1, SITE_DROP2, SITE_DROPFF, SITE_HEAD, Dims, LayerParams, PackedLayer,
+                     encoder_layer_backward, encoder_layer_forward, rup, site_seed)
+
+
+@dataclass
+class DeviceBatch:
+    N: int
+    B: int
+    input_x: torch.Tensor           # int64 [N, k+1] (only column 0 is read: the slot-0 gather)
+    X_concat: torch.Tensor          # f32 [N, d]
+    rowptr: torch.Tensor            # int64 [B+1]   pooling CSR (graph_pool rows)
+    colidx: torch.Tensor            # int64 [nnz]
+    vals: torch.Tensor              # f32 [nnz]
+    labels: Optional[torch.Tensor] = None   # int64 [B]
+    input_y: Optional[torch.Tensor] = None  # int64 [N] (UnSup softmax labels)
+
+    @property
+    def idx_stride(self):
+        return self.input_x.stride(0)
+
+    @staticmethod
+    def from_offsets(input_x, offsets, X_concat, labels=None, device="cuda", input_y=None):
+        """Host arrays (numpy / torch CPU) -> HBM.  Block-diagonal graph_pool of ones given by
+        node offsets (train_pytorch_U2GNN_Sup.py:73-89)."""
+        dev = torch.device(device)
+        ix = torch.as_tensor(input_x, dtype=torch.int64).to(dev, non_blocking=True).contiguous()
+        X = torch.as_tensor(X_concat, dtype=torch.float32).to(dev, non_blocking=True).contiguous()
+        off = torch.as_tensor(np.asarray(offsets), dtype=torch.int64)
+        N = int(off[-1])
+        B = off.numel() - 1
+        lab = None if labels is None else torch.as_tensor(labels, dtype=torch.int64).to(dev, non_blocking=True)
+        iy = None if input_y is None else torch.as_tensor(input_y, dtype=torch.int64).to(dev, non_blocking=True)
+        return DeviceBatch(N, B, ix, X, off.to(dev), torch.arange(N, device=dev, dtype=torch.int64),
+                           torch.ones(N, device=dev, dtype=torch.float32), lab, iy)
+
+    @staticmethod
+    def from_reference_inputs(input_x, graph_pool, X_concat, labels=None):
+        """The reference forward() inputs: input_x int64 [N,k+1], graph_pool sparse COO [B,N],
+        X_concat f32 [N,d] (pytorch_U2GNN_Sup.py:30)."""
+        dev = X_concat.device
+        gp = graph_pool.coalesce()
+        B, N = gp.shape
+        rows, cols = gp.indices()
+        vals = gp.values().to(torch.float32)
+        rowptr = torch.zeros(B + 1, dtype=torch.int64, device=dev)
+        rowptr[1:] = torch.cumsum(torch.bincount(rows, minlength=B), 0)
+        return DeviceBatch(int(N), int(B), input_x.to(dev).contiguous(), X_concat.to(torch.float32).contiguous(),
+                           rowptr, cols.contiguous(), vals.contiguous(), labels)
+
+
+class SupCore:
+    """Forward/backward of the supervised TransformerU2GNN on the HIP kernels."""
+
+    def __init__(self, module, precision: str = "fp32"):
+        self.m = module
+        self.prec = precision
+        self.d = module.feature_dim_size
+        self.ff = module.ff_hidden_size
+        self.C = module.num_classes
+        self.L = module.num_U2GNN_layers
+        self.T = module.num_self_att_layers
+        self.p_enc = 0.5                      # hard-coded in pytorch_U2GNN_Sup.py:20
+        self.p_head = module.dropout_p        # args.dropout, pytorch_U2GNN_Sup.py:28
+        self.packed = None
+
+    def layer_params(self, l, t) -> LayerParams:
+        return LayerParams.from_encoder_layer(self.m.u2gnn_layers[l].layers[t])
+
+    def _pack(self, device):
+        if self.packed is None:
+            self.packed = [[PackedLayer(self.d, self.ff, device) for _ in range(self.T)] for _ in range(self.L)]
+        for l in range(self.L):
+            for t in range(self.T):
+                self.packed[l][t].pack(self.layer_params(l, t))
+
+    def forward(self, b: DeviceBatch, train: bool, need_ctx: bool, seed: int):
+        dev = b.X_concat.device
+        d, dp = self.d, rup(self.d, 64)
+        dims = Dims(b.N, d, self.ff)
+        Np = dims.Np
+        self._pack(dev)
+        X = torch.empty(Np, dp, device=dev, dtype=torch.float32)
+        K.gather_rows(b.X_concat, b.input_x, b.idx_stride, X, b.N, Np, d, dp)
+        scores = torch.empty(b.B, self.C, device=dev, dtype=torch.float32)
+        ph = self.p_head if train else 0.0
+        ctx = {"dims": dims, "layers": [], "batch": b, "seed": seed, "ph": ph}
+        for l in range(self.L):
+            lctx = []
+            for t in range(self.T):
+                seeds = {s: site_seed(seed, l, t, s) for s in (SITE_ATTN, SITE_DROP1, SITE_DROPFF, SITE_DROP2)}
+                X, c = encoder_layer_forward(X, self.packed[l][t], self.layer_params(l, t), dims, train, seeds,
+                                             need_ctx, self.prec, self.p_enc)
+                lctx.append(c)
+            G = torch.empty(b.B, dp, device=dev, dtype=torch.float32)
+            hs = site_seed(seed, l, 0, SITE_HEAD)
+            K.pool_fwd(X, dp, b.rowptr, b.colidx, b.vals, G, dp, b.B, d, ph, hs)
+            pw, pb = self.m.predictions[l].weight, self.m.predictions[l].bias
+            K.head_fwd(G, dp, pw, pb, scores, b.B, self.C, d, accumulate=l > 0)
+            ctx["layers"].append((lctx, G, hs))
+            if l + 1 < self.L:
+                Xn = torch.empty(Np, dp, device=dev, dtype=torch.float32)
+                K.gather_rows(X, b.input_x, b.idx_stride, Xn, b.N, Np, d, dp)
+                X = Xn
+        ctx["out"] = X
+        return scores, ctx
+
+    def backward(self, ctx, dscores: torch.Tensor, grads: dict):
+        """grads: name -> real-shaped tensor (reference state_dict key names)."""
+        b: DeviceBatch = ctx["batch"]
+        dims: Dims = ctx["dims"]
+        dev = dscores.device
+        d, dp, Np = self.d, dims.dp, dims.Np
+        dnext = None
+        for l in reversed(range(self.L)):
+            lctx, G, hs = ctx["layers"][l]
+            dG = torch.empty(b.B, dp, device=dev, dtype=torch.float32)
+            K.head_bwd(dscores, G, dp, self.m.predictions[l].weight, dG, dp, grads[f"predictions.{l}.weight"],
+                       grads[f"predictions.{l}.bias"], b.B, self.C, d)
+            dX = torch.zeros(Np, dp, device=dev, dtype=torch.float32)
+            K.pool_bwd(dG, dp, b.rowptr, b.colidx, b.vals, dX, dp, b.B, d, ctx["ph"], hs)
+            if dnext is not None:
+                K.scatter_add_rows(dnext, b.input_x, b.idx_stride, dX, b.N, d)
+            for t in reversed(range(self.T)):
+                pre = f"u2gnn_layers.{l}.layers.{t}."
+                g = LayerParams(*[grads[pre + k] for k in LAYER_KEYS])
+                dX = encoder_layer_backward(dX, lctx[t], self.packed[l][t], self.layer_params(l, t), g, dims,
+                                            self.prec)
+            dnext = dX
+        return dnext
+
+
+LAYER_KEYS = ["self_attn.in_proj_weight", "self_attn.in_proj_bias", "self_attn.out_proj.weight",
+              "self_attn.out_proj.bias", "linear1.weight", "linear1.bias", "linear2.weight", "linear2.bias",
+              "norm1.weight", "norm1.bias", "norm2.weight", "norm2.bias"]
+
+
+class FlatParams:
+    """Re-homes every parameter of ``module`` into one flat fp32 device buffer (params become
+    views, keeping their reference shapes and state_dict keys) with a matching flat grad buffer."""
+
+    def __init__(self, module: torch.nn.Module):
+        self.names, self.params = zip(*[(n, p) for n, p in module.named_parameters()])
+        dev = self.params[0].device
+        sizes = [p.numel() for p in self.params]
+        # 16-byte aligned offsets for the float4 sweeps
+        offs, o = [], 0
+        for s in sizes:
+            offs.append(o)
+            o += rup(s, 4)
+        self.n = o
+        self.flat = torch.zeros(o, device=dev, dtype=torch.float32)
+        self.gflat = torch.zeros(o, device=dev, dtype=torch.float32)
+        self.grads = {}
+        for name, p, off, s in zip(self.names, self.params, offs, sizes):
+            self.flat[off:off + s].copy_(p.detach().reshape(-1))
+            p.data = self.flat[off:off + s].view(p.shape)
+            gv = self.gflat[off:off + s].view(p.shape)
+            p.grad = gv
+            self.grads[name] = gv
+
+
+class FusedAdam:
+    """torch.optim.Adam (lr, betas=(0.9, 0.999), eps=1e-8, no weight decay) preceded by
+    clip_grad_norm_(max_norm) — both on device over the flat buffers, no host sync."""
+
+    def __init__(self, flat: FlatParams, lr: float, max_norm: Optional[float] = 0.5, betas=(0.9, 0.999),
+                 eps: float = 1e-8):
+        self.f = flat
+        self.lr, self.max_norm, self.betas, self.eps = lr, max_norm, betas, eps
+        dev = flat.flat.device
+        self.m = torch.zeros_like(flat.flat)
+        self.v = torch.zeros_like(flat.flat)
+        self.ws = torch.empty(1024, device=dev, dtype=torch.float32)
+        self.sq = torch.zeros(1, device=dev, dtype=torch.float32)
+        self.step_count = 0
+
+    def step(self):
+        self.step_count += 1
+        b1, b2 = self.betas
+        bc1 = 1 - b1 ** self.step_count
+        bc2 = 1 - b2 ** self.step_count
+        if self.max_norm is not None:
+            K.sqnorm(self.f.gflat, self.f.n, self.ws, self.sq)
+        K.adam(self.f.flat, self.f.gflat, self.m, self.v, self.f.n, self.sq if self.max_norm is not None else None,
+               self.max_norm or 0.0, b1, b2, self.eps, self.lr / bc1, math.sqrt(bc2))
+
+    def grad_norm(self) -> float:
+        return float(self.sq.sqrt().item())

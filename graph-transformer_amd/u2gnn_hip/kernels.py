@@ -1,0 +1,196 @@
+"""Thin torch-tensor wrappers over the C ABI of libu2gnn_hip.so.
+
+Tensors are only used for device memory and stream plumbing: every wrapper passes raw
+device pointers + sizes and the current HIP stream to the native entry point, and checks
+its status code.  Nothing here computes on the CPU.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import check, hip_lib
+
+PREC = {"fp32": _lib.PREC_F32, "bf16x3": _lib.PREC_BF16X3, "bf16": _lib.PREC_BF16}
+
+
+def _p(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _s():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _dev(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise _lib.U2GNNNativeError("U2GNN kernels need device tensors (no CPU fallback)")
+
+
+def gemm(A, B, C, M, N, K, lda, ldb, ldc, trans_a=False, trans_b=False, epilogue=_lib.EPI_STORE, split_k=1,
+         slab_stride=0, bias=None, aux0=None, aux1=None, rowvec=None, ld_aux=0, alpha=1.0, scale_cols=0, p_drop=0.0,
+         seed=0, precision="fp32", tile=0):
+    """C[M,N] (epilogue) sum_k A(m,k) B(k,n).  A/B/C may be views (pointer arithmetic via
+    storage offsets is done by torch's data_ptr())."""
+    _dev(A, B, C)
+    a = _lib.GemmArgs()
+    a.A, a.B, a.C = A.data_ptr(), B.data_ptr(), C.data_ptr()
+    a.M, a.N, a.K = int(M), int(N), int(K)
+    a.lda, a.ldb, a.ldc = int(lda), int(ldb), int(ldc)
+    a.trans_a, a.trans_b = int(bool(trans_a)), int(bool(trans_b))
+    a.epilogue, a.split_k, a.slab_stride = int(epilogue), int(split_k), int(slab_stride)
+    a.bias = bias.data_ptr() if bias is not None else None
+    a.aux0 = aux0.data_ptr() if aux0 is not None else None
+    a.aux1 = aux1.data_ptr() if aux1 is not None else None
+    a.rowvec = rowvec.data_ptr() if rowvec is not None else None
+    a.ld_aux = int(ld_aux)
+    a.alpha = float(alpha)
+    a.scale_cols = int(scale_cols)
+    a.p_drop = float(p_drop)
+    a.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+    a.precision = PREC[precision] if isinstance(precision, str) else int(precision)
+    a.tile = int(tile)
+    check(hip_lib().u2gnn_gemm(ctypes.byref(a), _s()), "u2gnn_gemm")
+
+
+def gather_rows(src, idx, idx_stride, dst, n_rows, n_rows_pad, d, d_pad, err=None):
+    _dev(src, idx, dst)
+    check(hip_lib().u2gnn_gather_rows(_p(src), src.stride(0), src.shape[0], _p(idx), int(idx_stride), _p(dst),
+                                      dst.stride(0), int(n_rows), int(n_rows_pad), int(d), int(d_pad), _p(err),
+                                      _s()), "u2gnn_gather_rows")
+
+
+def scatter_add_rows(src, idx, idx_stride, dst, n_rows, d):
+    _dev(src, idx, dst)
+    check(hip_lib().u2gnn_scatter_add_rows(_p(src), src.stride(0), _p(idx), int(idx_stride), _p(dst), dst.stride(0),
+                                           int(n_rows), int(d), _s()), "u2gnn_scatter_add_rows")
+
+
+def slab_reduce(src, n_slab, slab_stride, rows_pad, cols_pad, ld_src, rblk, cblk, dst, ld_dst, alpha=1.0,
+                accumulate=False):
+    """rblk/cblk = (blk_pad, blk_real) block maps from padded to real indices."""
+    _dev(src, dst)
+    check(hip_lib().u2gnn_slab_reduce(_p(src), int(n_slab), int(slab_stride), int(rows_pad), int(cols_pad),
+                                      int(ld_src), int(rblk[0]), int(rblk[1]), int(cblk[0]), int(cblk[1]), _p(dst),
+                                      int(ld_dst), float(alpha), int(accumulate), _s()), "u2gnn_slab_reduce")
+
+
+def pack_padded(src, ld_src, rows_pad, cols_pad, rblk, cblk, dst, ld_dst):
+    _dev(src, dst)
+    check(hip_lib().u2gnn_pack_padded(_p(src), int(ld_src), int(rows_pad), int(cols_pad), int(rblk[0]),
+                                      int(rblk[1]), int(cblk[0]), int(cblk[1]), _p(dst), int(ld_dst), _s()),
+          "u2gnn_pack_padded")
+
+
+def colsum(X, rows, cols_pad, ld, cblk, out, ws, accumulate=False):
+    _dev(X, out, ws)
+    check(hip_lib().u2gnn_colsum(_p(X), int(rows), int(cols_pad), int(ld), int(cblk[0]), int(cblk[1]), _p(out),
+                                 int(accumulate), _p(ws), _s()), "u2gnn_colsum")
+
+
+def attn_softmax_fwd(S, lds, P, Pd, ldp, rows_valid, rows_pad, n_valid, n_pad, p, seed):
+    _dev(S, P, Pd)
+    check(hip_lib().u2gnn_attn_softmax_fwd(_p(S), int(lds), _p(P), _p(Pd), int(ldp), int(rows_valid), int(rows_pad),
+                                           int(n_valid), int(n_pad), float(p), int(seed), _s()),
+          "u2gnn_attn_softmax_fwd")
+
+
+def rowdot(A, lda, B, ldb, out, rows, cols):
+    _dev(A, B, out)
+    check(hip_lib().u2gnn_rowdot(_p(A), int(lda), _p(B), int(ldb), _p(out), int(rows), int(cols), _s()),
+          "u2gnn_rowdot")
+
+
+def layernorm_fwd(Z, ldz, gamma, beta, Y, ldy, mean, rstd, rows_valid, rows_pad, d, d_pad, eps=1e-5):
+    _dev(Z, gamma, beta, Y, mean, rstd)
+    check(hip_lib().u2gnn_layernorm_fwd(_p(Z), int(ldz), _p(gamma), _p(beta), _p(Y), int(ldy), _p(mean), _p(rstd),
+                                        int(rows_valid), int(rows_pad), int(d), int(d_pad), float(eps), _s()),
+          "u2gnn_layernorm_fwd")
+
+
+LNB_ROWS = 32
+
+
+def ln_part_blocks(rows_pad):
+    return (rows_pad + LNB_ROWS - 1) // LNB_ROWS
+
+
+def layernorm_bwd(dY, ldy, Z, ldz, mean, rstd, gamma, dZ, lddz, dZdrop, lddrop, p, seed, part, rows_valid, rows_pad,
+                  d, d_pad):
+    _dev(dY, Z, mean, rstd, gamma, dZ, part)
+    check(hip_lib().u2gnn_layernorm_bwd(_p(dY), int(ldy), _p(Z), int(ldz), _p(mean), _p(rstd), _p(gamma), _p(dZ),
+                                        int(lddz), _p(dZdrop), int(lddrop), float(p), int(seed), _p(part),
+                                        int(rows_valid), int(rows_pad), int(d), int(d_pad), _s()),
+          "u2gnn_layernorm_bwd")
+
+
+def layernorm_param_reduce(part, n_blocks, d, d_pad, dgamma, dbeta, accumulate=False):
+    _dev(part, dgamma, dbeta)
+    check(hip_lib().u2gnn_layernorm_param_reduce(_p(part), int(n_blocks), int(d), int(d_pad), _p(dgamma), _p(dbeta),
+                                                 int(accumulate), _s()), "u2gnn_layernorm_param_reduce")
+
+
+def pool_fwd(X, ldx, rowptr, colidx, vals, G, ldg, B, d, p, seed):
+    _dev(X, rowptr, colidx, vals, G)
+    check(hip_lib().u2gnn_pool_fwd(_p(X), int(ldx), _p(rowptr), _p(colidx), _p(vals), _p(G), int(ldg), int(B),
+                                   int(d), float(p), int(seed), _s()), "u2gnn_pool_fwd")
+
+
+def pool_bwd(dG, ldg, rowptr, colidx, vals, dX, ldx, B, d, p, seed):
+    _dev(dG, rowptr, colidx, vals, dX)
+    check(hip_lib().u2gnn_pool_bwd(_p(dG), int(ldg), _p(rowptr), _p(colidx), _p(vals), _p(dX), int(ldx), int(B),
+                                   int(d), float(p), int(seed), _s()), "u2gnn_pool_bwd")
+
+
+def head_fwd(G, ldg, W, bias, scores, B, C, d, accumulate):
+    _dev(G, W, bias, scores)
+    check(hip_lib().u2gnn_head_fwd(_p(G), int(ldg), _p(W), _p(bias), _p(scores), int(B), int(C), int(d),
+                                   int(accumulate), _s()), "u2gnn_head_fwd")
+
+
+def head_bwd(dscores, G, ldg, W, dG, lddg, dW, db, B, C, d, accumulate=False):
+    _dev(dscores, G, W, dG, dW, db)
+    check(hip_lib().u2gnn_head_bwd(_p(dscores), _p(G), int(ldg), _p(W), _p(dG), int(lddg), _p(dW), _p(db), int(B),
+                                   int(C), int(d), int(accumulate), _s()), "u2gnn_head_bwd")
+
+
+def smoothed_ce(scores, labels, B, C, smoothing, loss, dscores):
+    _dev(scores, labels, loss, dscores)
+    check(hip_lib().u2gnn_smoothed_ce(_p(scores), _p(labels), int(B), int(C), float(smoothing), _p(loss),
+                                      _p(dscores), _s()), "u2gnn_smoothed_ce")
+
+
+def sqnorm(g, n, ws, out):
+    _dev(g, ws, out)
+    check(hip_lib().u2gnn_sqnorm(_p(g), int(n), _p(ws), _p(out), _s()), "u2gnn_sqnorm")
+
+
+def adam(param, grad, m, v, n, sqnorm_t, max_norm, beta1, beta2, eps, step_size, bc2_sqrt):
+    _dev(param, grad, m, v)
+    check(hip_lib().u2gnn_adam(_p(param), _p(grad), _p(m), _p(v), int(n), _p(sqnorm_t), float(max_norm),
+                               float(beta1), float(beta2), float(eps), float(step_size), float(bc2_sqrt), _s()),
+          "u2gnn_adam")
+
+
+def sampled_softmax_fwd(X, ldx, labels, sample_ids, S, W, ldw, loss, prob, n_rows, D):
+    _dev(X, labels, sample_ids, W, loss, prob)
+    check(hip_lib().u2gnn_sampled_softmax_fwd(_p(X), int(ldx), _p(labels), _p(sample_ids), int(S), _p(W), int(ldw),
+                                              _p(loss), _p(prob), int(n_rows), int(D), _s()),
+          "u2gnn_sampled_softmax_fwd")
+
+
+def sampled_softmax_bwd(X, ldx, labels, sample_ids, S, W, ldw, prob, dloss, dX, lddx, dW, lddw, n_rows, D):
+    _dev(X, labels, sample_ids, W, prob, dX, dW)
+    check(hip_lib().u2gnn_sampled_softmax_bwd(_p(X), int(ldx), _p(labels), _p(sample_ids), int(S), _p(W), int(ldw),
+                                              _p(prob), _p(dloss), _p(dX), int(lddx), _p(dW), int(lddw), int(n_rows),
+                                              int(D), _s()), "u2gnn_sampled_softmax_bwd")
+
+
+def dropout_mask(seed, rows, cols, p, device="cuda"):
+    out = torch.empty(rows, cols, dtype=torch.uint8, device=device)
+    check(hip_lib().u2gnn_dropout_mask(int(seed), int(rows), int(cols), float(p), _p(out), _s()),
+          "u2gnn_dropout_mask")
+    return out

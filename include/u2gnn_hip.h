@@ -1,0 +1,191 @@
+/*
+ * u2gnn_hip.h — C ABI of libu2gnn_hip.so, the MI355X (gfx950) kernels of the U2GNN hot path.
+ *
+ * The reference (shaginhekvs/Graph-Transformer, PyTorch) has no native kernels: every op
+ * below replaces ATen calls made from the reference's Python.  Each entry point cites the
+ * reference line whose computation it takes over (paths relative to the reference root).
+ *
+ * Conventions (all entry points):
+ *   - plain pointers to DEVICE memory allocated by the caller; no allocation inside,
+ *     no host synchronisation, so every call can be captured into a hipGraph;
+ *   - `stream` is a hipStream_t passed as void* (NULL = the default stream);
+ *   - fp32 row-major matrices with explicit leading dimensions (elements);
+ *   - "padded" layouts: node rows padded to Np (multiple of 128), feature columns padded
+ *     to a multiple of 64; padding columns are kept at zero by the producers;
+ *   - return value: 0 on success, a negative U2GNN_E* code for argument errors, or a
+ *     positive hipError_t from the launch.
+ *   - dropout: keep(i,j) = hash(seed, i, j) >= p (counter-based; the same mask is
+ *     regenerated in backward from (seed, i, j) — nothing is stored).
+ */
+#ifndef U2GNN_HIP_H
+#define U2GNN_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define U2GNN_ABI_VERSION 1
+
+#define U2GNN_OK 0
+#define U2GNN_E_ARG (-1)    /* bad size / null pointer */
+#define U2GNN_E_ALIGN (-2)  /* pointer or leading dimension not 16-byte aligned */
+#define U2GNN_E_SHAPE (-3)  /* dimension not a multiple of the kernel tile */
+
+/* GEMM epilogues (u2gnn_gemm_args.epilogue). acc = sum_k A(m,k) B(k,n). */
+#define U2GNN_EPI_STORE 0           /* C = alpha*acc                                     */
+#define U2GNN_EPI_BIAS 1            /* C = (acc + bias[n]) * (n < scale_cols ? alpha : 1) */
+#define U2GNN_EPI_BIAS_DROP_RESID 2 /* C = aux0[m,n] + drop(acc + bias[n])               */
+#define U2GNN_EPI_BIAS_RELU_DROP 3  /* C = drop(relu(acc + bias[n]))                      */
+#define U2GNN_EPI_RELU_DROP_BWD 4   /* C = acc * (aux0[m,n] > 0 ? 1/(1-p) : 0)            */
+#define U2GNN_EPI_ACCUM 5           /* C = C + alpha*acc                                  */
+#define U2GNN_EPI_ATTN_DS 6         /* C = aux1[m,n]*acc - aux0[m,n]*rowvec[m]            */
+
+/* Matrix-core precision of a GEMM (u2gnn_gemm_args.precision). */
+#define U2GNN_PREC_F32 0    /* v_mfma_f32_32x32x2_f32: exact fp32 fma chains            */
+#define U2GNN_PREC_BF16X3 1 /* split-bf16 (hi*hi+hi*lo+lo*hi) on bf16 MFMA, fp32 accum  */
+#define U2GNN_PREC_BF16 2   /* plain bf16 operands on bf16 MFMA, fp32 accum             */
+
+typedef struct u2gnn_gemm_args {
+    const float *A;       /* trans_a=0: A[m*lda+k]   trans_a=1: A[k*lda+m] */
+    const float *B;       /* trans_b=0: B[k*ldb+n]   trans_b=1: B[n*ldb+k] */
+    float *C;             /* C[m*ldc+n]; with split_k>1: slab z at C + z*slab_stride */
+    int64_t M, N, K;
+    int64_t lda, ldb, ldc;
+    int32_t trans_a, trans_b;
+    int32_t epilogue;     /* U2GNN_EPI_*; split_k>1 requires STORE */
+    int32_t split_k;      /* >= 1; K must split into multiples of the K tile */
+    int64_t slab_stride;
+    const float *bias;    /* [N] */
+    const float *aux0;    /* residual / saved relu-dropout output / P */
+    const float *aux1;    /* Pd (dropped probabilities) */
+    const float *rowvec;  /* [M] (delta of the attention backward) */
+    int64_t ld_aux;
+    float alpha;
+    int64_t scale_cols;
+    float p_drop;
+    uint64_t seed;
+    int32_t precision;    /* U2GNN_PREC_* */
+    int32_t tile;         /* 0 = auto, else 64 / 128 (square block tile) */
+} u2gnn_gemm_args;
+
+/* ---- library ------------------------------------------------------------------ */
+int u2gnn_abi_version(void);
+
+/* ---- a2: neighbour gather  (pytorch_U2GNN_Sup.py:32,39; pytorch_U2GNN_UnSup.py:54) --------
+ * dst[i, 0:d] = src[idx[i*idx_stride], 0:d] for i < n_rows; dst[i, d:d_pad] = 0;
+ * rows n_rows..n_rows_pad-1 = 0.  Out-of-range indices write zeros and set *err = 1. */
+int u2gnn_gather_rows(const float *src, int64_t ld_src, int64_t src_rows, const int64_t *idx,
+                      int64_t idx_stride, float *dst, int64_t ld_dst, int64_t n_rows,
+                      int64_t n_rows_pad, int64_t d, int64_t d_pad, int32_t *err, void *stream);
+/* backward of the gather: dst[idx[i*idx_stride], 0:d] += src[i, 0:d] (fp32 atomics) */
+int u2gnn_scatter_add_rows(const float *src, int64_t ld_src, const int64_t *idx, int64_t idx_stride,
+                           float *dst, int64_t ld_dst, int64_t n_rows, int64_t d, void *stream);
+
+/* ---- a3.x: every dense contraction of the encoder (in-proj, Q.K^T, P.V, out-proj, FFN)
+ * and of its backward  (torch TransformerEncoderLayer at pytorch_U2GNN_Sup.py:19-21,35;
+ * pytorch_U2GNN_UnSup.py:37-40,57) -------------------------------------------------- */
+int u2gnn_gemm(const u2gnn_gemm_args *args, void *stream);
+
+/* split-K / padded -> real unpack:  dst[map(r), map(c)] (+)= alpha * sum_z src[z*slab_stride + r*ld_src + c]
+ * for r < rows_pad, c < cols_pad whose in-block index is < the real block size; the map
+ * packs blocks of size (blk_pad) to (blk_real): r -> (r / rblk_pad) * rblk_real + r % rblk_pad. */
+int u2gnn_slab_reduce(const float *src, int32_t n_slab, int64_t slab_stride, int64_t rows_pad,
+                      int64_t cols_pad, int64_t ld_src, int64_t rblk_pad, int64_t rblk_real,
+                      int64_t cblk_pad, int64_t cblk_real, float *dst, int64_t ld_dst, float alpha,
+                      int32_t accumulate, void *stream);
+
+/* pack real-shaped parameters into padded device buffers (same block map as above, inverse);
+ * padding entries of dst are written with 0. */
+int u2gnn_pack_padded(const float *src, int64_t ld_src, int64_t rows_pad, int64_t cols_pad,
+                      int64_t rblk_pad, int64_t rblk_real, int64_t cblk_pad, int64_t cblk_real,
+                      float *dst, int64_t ld_dst, void *stream);
+
+/* column sums (bias gradients):  out[map(c)] (+)= sum_{r<rows} X[r*ld + c], c < cols_pad.
+ * ws must hold ceil(rows/256) * cols_pad floats. */
+int u2gnn_colsum(const float *X, int64_t rows, int64_t cols_pad, int64_t ld, int64_t cblk_pad,
+                 int64_t cblk_real, float *out, int32_t accumulate, float *ws, void *stream);
+
+/* ---- a3.2: attention row softmax + dropout(p) on probabilities (MHA core) ----------
+ * P[i,j] = softmax_j(S[i,j], j < n_valid); Pd = P * keep / (1-p); rows >= rows_valid -> 0.
+ * Pd may alias P when p == 0. */
+int u2gnn_attn_softmax_fwd(const float *S, int64_t lds, float *P, float *Pd, int64_t ldp,
+                           int64_t rows_valid, int64_t rows_pad, int64_t n_valid, int64_t n_pad,
+                           float p, uint64_t seed, void *stream);
+/* delta[i] = sum_c A[i,c]*B[i,c]  (rowsum(dO * O) of the attention backward) */
+int u2gnn_rowdot(const float *A, int64_t lda, const float *B, int64_t ldb, float *out, int64_t rows,
+                 int64_t cols, void *stream);
+
+/* ---- a3.3 / a3.4: post-LN  (norm1/norm2, eps 1e-5) -------------------------------------
+ * Y = LN(Z) over the first d columns; Y[:, d:d_pad] = 0; rows >= rows_valid -> 0. */
+int u2gnn_layernorm_fwd(const float *Z, int64_t ldz, const float *gamma, const float *beta, float *Y,
+                        int64_t ldy, float *mean, float *rstd, int64_t rows_valid, int64_t rows_pad,
+                        int64_t d, int64_t d_pad, float eps, void *stream);
+/* dZ = LN'(dY); dZdrop = dZ * keep/(1-p) (may be NULL); per-block partial sums of
+ * dY*xhat and dY written to part[blk*2*d_pad + c] / part[blk*2*d_pad + d_pad + c];
+ * n_part_blocks = ceil(rows_pad / 32). */
+int u2gnn_layernorm_bwd(const float *dY, int64_t ldy, const float *Z, int64_t ldz, const float *mean,
+                        const float *rstd, const float *gamma, float *dZ, int64_t lddz, float *dZdrop,
+                        int64_t lddrop, float p, uint64_t seed, float *part, int64_t rows_valid,
+                        int64_t rows_pad, int64_t d, int64_t d_pad, void *stream);
+/* dgamma[c] (+)= sum_blk part[blk][0][c]; dbeta[c] (+)= sum_blk part[blk][1][c], c < d */
+int u2gnn_layernorm_param_reduce(const float *part, int64_t n_blocks, int64_t d, int64_t d_pad,
+                                 float *dgamma, float *dbeta, int32_t accumulate, void *stream);
+
+/* ---- a5/a6: sum pooling + dropout + per-layer head  (pytorch_U2GNN_Sup.py:41-44) ------
+ * G[b, c] = drop(sum_{e in [rowptr[b], rowptr[b+1])} vals[e] * X[colidx[e], c]), c < d;
+ * G[b, d:ldg] untouched. */
+int u2gnn_pool_fwd(const float *X, int64_t ldx, const int64_t *rowptr, const int64_t *colidx,
+                   const float *vals, float *G, int64_t ldg, int64_t B, int64_t d, float p,
+                   uint64_t seed, void *stream);
+/* dX[colidx[e], c] += vals[e] * dGd[b, c] * keep/(1-p)   (fp32 atomics) */
+int u2gnn_pool_bwd(const float *dGd, int64_t ldg, const int64_t *rowptr, const int64_t *colidx,
+                   const float *vals, float *dX, int64_t ldx, int64_t B, int64_t d, float p,
+                   uint64_t seed, void *stream);
+/* scores[b, c] (+)= sum_j G[b, j] W[c, j] + bias[c]   (W real [C, d]) */
+int u2gnn_head_fwd(const float *G, int64_t ldg, const float *W, const float *bias, float *scores,
+                   int64_t B, int64_t C, int64_t d, int32_t accumulate, void *stream);
+/* dG[b, j] = sum_c dS[b,c] W[c,j];  dW[c,j] (+)= sum_b dS[b,c] G[b,j];  db[c] (+)= sum_b dS[b,c] */
+int u2gnn_head_bwd(const float *dscores, const float *G, int64_t ldg, const float *W, float *dG,
+                   int64_t lddg, float *dW, float *db, int64_t B, int64_t C, int64_t d,
+                   int32_t accumulate, void *stream);
+
+/* ---- a7: label smoothing + soft cross-entropy  (pytorch_U2GNN_Sup.py:48-60;
+ * train_pytorch_U2GNN_Sup.py:140-142,158) -----------------------------------------------
+ * loss[0] = mean_b sum_c -t_bc log_softmax(s_b)_c ; dscores = (softmax - t) / B */
+int u2gnn_smoothed_ce(const float *scores, const int64_t *labels, int64_t B, int64_t C,
+                      float smoothing, float *loss, float *dscores, void *stream);
+
+/* ---- a9: clip_grad_norm_(max_norm) + Adam  (train_pytorch_U2GNN_Sup.py:145,160-161) ----
+ * sqnorm[0] = sum g^2 (double accumulation, fp32 result); ws >= 1024 floats. */
+int u2gnn_sqnorm(const float *g, int64_t n, float *ws, float *sqnorm, void *stream);
+/* torch.optim.Adam single-tensor step on a flat buffer with the clip coefficient
+ * min(1, max_norm/(sqrt(*sqnorm)+1e-6)) applied to g on the fly (sqnorm NULL: no clip).
+ * step_size = lr / (1 - beta1^t), bc2_sqrt = sqrt(1 - beta2^t), computed by the caller. */
+int u2gnn_adam(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, int64_t n,
+               const float *sqnorm, float max_norm, float beta1, float beta2, float eps,
+               float step_size, float bc2_sqrt, void *stream);
+
+/* ---- a10: sampled softmax  (sampled_softmax.py:36-56) --------------------------------------
+ * loss_i = log sum_s exp(x_i . w_s) - x_i . w_{y_i}   (== the reference -log(exp(t)/sum exp(s))
+ * whenever the reference is finite); prob[i, s] = softmax over samples (saved for backward). */
+int u2gnn_sampled_softmax_fwd(const float *X, int64_t ldx, const int64_t *labels,
+                              const int64_t *sample_ids, int64_t S, const float *W, int64_t ldw,
+                              float *loss, float *prob, int64_t n_rows, int64_t D, void *stream);
+/* with upstream dloss[i] (NULL = all ones): dX[i] = dloss_i (sum_s prob_is w_s - w_{y_i});
+ * dW[y_i] -= dloss_i x_i;  dW[s] += sum_i dloss_i prob_is x_i   (dW accumulated, atomics) */
+int u2gnn_sampled_softmax_bwd(const float *X, int64_t ldx, const int64_t *labels,
+                              const int64_t *sample_ids, int64_t S, const float *W, int64_t ldw,
+                              const float *prob, const float *dloss, float *dX, int64_t lddx,
+                              float *dW, int64_t lddw, int64_t n_rows, int64_t D, void *stream);
+
+/* ---- debugging / tests ---------------------------------------------------------------- */
+/* out[i*cols + j] = keep(seed, i, j) ? 1 : 0   (the exact dropout mask the kernels apply) */
+int u2gnn_dropout_mask(uint64_t seed, int64_t rows, int64_t cols, float p, uint8_t *out, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* U2GNN_HIP_H */

@@ -59,6 +59,7 @@ def sup_case(name, dataset, deg_tag, bs, k, T, ff, L, lr=0.0005, n_batches=3, fo
         out[f"b{i}_input_x"] = ix
         out[f"b{i}_offsets"] = off
         out[f"b{i}_labels"] = y
+        out[f"b{i}_X"] = X
     # batch 0: eval-mode forward, loss, grads, one clip+Adam step (reference modules)
     sel, ix, off, X, y = batches[0]
     Nn = int(off[-1])
@@ -152,7 +153,7 @@ def unsup_case(name="ptc_unsup", dataset="PTC", bs=4, k=4, T=2, ff=1024, L=1, lr
     loss = logits.sum()
     loss.backward()
     out = {"meta": np.array([bs, k, T, ff, L, d, V], np.int64), "lr": np.float32(lr),
-           "sel": sel.astype(np.int64), "input_x": ix, "offsets": off, "input_y": iy,
+           "sel": sel.astype(np.int64), "input_x": ix, "offsets": off, "input_y": iy, "X": X,
            "sample_ids": np.asarray(sv[0], np.int64), "logits": logits.detach().numpy(),
            "loss": np.float32(loss.item())}
     sd0 = {}

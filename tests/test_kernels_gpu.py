@@ -1,0 +1,196 @@
+"""Per-kernel numerics of libu2gnn_hip.so against plain torch fp32 references (GPU)."""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from u2gnn_hip import _lib  # noqa: E402
+from u2gnn_hip import kernels as K  # noqa: E402
+
+DEV = "cuda"
+
+
+def rel_err(a, b):
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-6)).item()
+
+
+def _mk(*s, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(*s, generator=g).to(DEV)
+
+
+@pytest.mark.parametrize("tile", [64, 128])
+@pytest.mark.parametrize("layout", ["NT", "NN", "TN"])
+def test_gemm_layouts_exact_fp32(tile, layout):
+    M, N, Kd = 256, 384, 192
+    ta, tb = layout[0] == "T", layout[1] == "T"
+    A = _mk(Kd, M, seed=1) if ta else _mk(M, Kd, seed=1)
+    B = _mk(N, Kd, seed=2) if tb else _mk(Kd, N, seed=2)
+    C = torch.empty(M, N, device=DEV)
+    K.gemm(A, B, C, M, N, Kd, A.shape[1], B.shape[1], N, trans_a=ta, trans_b=tb, tile=tile)
+    ref = (A.t() if ta else A).double() @ (B.t() if tb else B).double()
+    assert rel_err(C.double(), ref) < 1e-5
+
+
+def test_gemm_asymmetric_identity():
+    """A = I with an asymmetric B catches a transposed C/D map."""
+    M = N = Kd = 128
+    A = torch.eye(M, device=DEV)
+    B = torch.arange(Kd * N, device=DEV, dtype=torch.float32).view(Kd, N) / 1000.0
+    C = torch.empty(M, N, device=DEV)
+    K.gemm(A, B, C, M, N, Kd, Kd, N, N)
+    assert torch.equal(C, B)
+
+
+def test_gemm_split_k_slabs_and_views():
+    M, N, Kd = 128, 192, 1024
+    A = _mk(Kd, M, seed=3)     # trans_a
+    B = _mk(Kd, 3 * N, seed=4)[:, N:2 * N]   # column-slice view, ld 3N
+    slabs = torch.empty(4, M, N, device=DEV)
+    K.gemm(A, B, slabs, M, N, Kd, M, 3 * N, N, trans_a=True, split_k=4, slab_stride=M * N, tile=64)
+    out = torch.empty(M, N, device=DEV)
+    K.slab_reduce(slabs, 4, M * N, M, N, N, (M, M), (N, N), out, N)
+    ref = A.t().double() @ B.double()
+    assert rel_err(out.double(), ref) < 1e-5
+
+
+def test_gemm_epilogues():
+    M, N, Kd = 128, 128, 64
+    A, B = _mk(M, Kd, seed=5), _mk(N, Kd, seed=6)
+    bias, R = _mk(N, seed=7), _mk(M, N, seed=8)
+    acc = A @ B.t()
+    C = torch.empty(M, N, device=DEV)
+    K.gemm(A, B, C, M, N, Kd, Kd, Kd, N, trans_b=True, epilogue=_lib.EPI_BIAS, bias=bias, alpha=0.5, scale_cols=64)
+    ref = acc + bias
+    ref[:, :64] *= 0.5
+    assert rel_err(C, ref) < 1e-5
+    # dropout epilogues against the kernel's own mask
+    p, seed = 0.5, 1234
+    mask = K.dropout_mask(seed, M, N, p).float()
+    assert 0.45 < mask.mean().item() < 0.55
+    K.gemm(A, B, C, M, N, Kd, Kd, Kd, N, trans_b=True, epilogue=_lib.EPI_BIAS_DROP_RESID, bias=bias, aux0=R,
+           ld_aux=N, p_drop=p, seed=seed)
+    assert rel_err(C, R + (acc + bias) * mask * 2) < 1e-5
+    K.gemm(A, B, C, M, N, Kd, Kd, Kd, N, trans_b=True, epilogue=_lib.EPI_BIAS_RELU_DROP, bias=bias, p_drop=p,
+           seed=seed)
+    H = torch.relu(acc + bias) * mask * 2
+    assert rel_err(C, H) < 1e-5
+    G = torch.empty(M, N, device=DEV)
+    K.gemm(A, B, G, M, N, Kd, Kd, Kd, N, trans_b=True, epilogue=_lib.EPI_RELU_DROP_BWD, aux0=H, ld_aux=N, p_drop=p)
+    assert rel_err(G, acc * (H > 0).float() * 2) < 1e-5
+    C2 = R.clone()
+    K.gemm(A, B, C2, M, N, Kd, Kd, Kd, N, trans_b=True, epilogue=_lib.EPI_ACCUM, alpha=1.0)
+    assert rel_err(C2, R + acc) < 1e-5
+    P, Pd, dl = torch.rand(M, N, device=DEV), torch.rand(M, N, device=DEV), _mk(M, seed=9)
+    K.gemm(A, B, C, M, N, Kd, Kd, Kd, N, trans_b=True, epilogue=_lib.EPI_ATTN_DS, aux0=P, aux1=Pd, rowvec=dl,
+           ld_aux=N)
+    assert rel_err(C, Pd * acc - P * dl[:, None]) < 1e-5
+
+
+def test_attn_softmax_masking_and_dropout():
+    Np, N = 256, 200
+    S = _mk(Np, Np, seed=10) * 3
+    P = torch.empty(Np, Np, device=DEV)
+    K.attn_softmax_fwd(S, Np, P, P, Np, N, Np, N, Np, 0.0, 0)
+    ref = torch.softmax(S[:N, :N], dim=1)
+    assert rel_err(P[:N, :N], ref) < 1e-5
+    assert P[:, N:].abs().max().item() == 0 and P[N:].abs().max().item() == 0
+    Pd = torch.empty_like(P)
+    K.attn_softmax_fwd(S, Np, P, Pd, Np, N, Np, N, Np, 0.5, 77)
+    mask = K.dropout_mask(77, Np, Np, 0.5).float()
+    assert rel_err(Pd[:N, :N], ref * mask[:N, :N] * 2) < 1e-5
+
+
+def test_layernorm_fwd_bwd():
+    Np, N, d, dp = 128, 100, 67, 128
+    Z = _mk(Np, dp, seed=11)
+    gam, bet = _mk(d, seed=12), _mk(d, seed=13)
+    Y = torch.empty(Np, dp, device=DEV)
+    mu, rs = torch.empty(Np, device=DEV), torch.empty(Np, device=DEV)
+    K.layernorm_fwd(Z, dp, gam, bet, Y, dp, mu, rs, N, Np, d, dp)
+    z = Z[:N, :d].clone().requires_grad_(True)
+    g_, b_ = gam.clone().requires_grad_(True), bet.clone().requires_grad_(True)
+    ref = torch.nn.functional.layer_norm(z, (d,), g_, b_, 1e-5)
+    assert rel_err(Y[:N, :d], ref) < 1e-5
+    assert Y[:, d:].abs().max().item() == 0 and Y[N:].abs().max().item() == 0
+    dY = torch.zeros(Np, dp, device=DEV)
+    dY[:N, :d] = _mk(N, d, seed=14)
+    ref.backward(dY[:N, :d])
+    dZ, dZd = torch.empty(Np, dp, device=DEV), torch.empty(Np, dp, device=DEV)
+    nb = K.ln_part_blocks(Np)
+    part = torch.empty(nb, 2 * dp, device=DEV)
+    K.layernorm_bwd(dY, dp, Z, dp, mu, rs, gam, dZ, dp, dZd, dp, 0.5, 99, part, N, Np, d, dp)
+    dg, db = torch.empty(d, device=DEV), torch.empty(d, device=DEV)
+    K.layernorm_param_reduce(part, nb, d, dp, dg, db)
+    assert rel_err(dZ[:N, :d], z.grad) < 1e-4
+    mask = K.dropout_mask(99, Np, dp, 0.5).float()
+    assert rel_err(dZd[:N, :d], z.grad * mask[:N, :d] * 2) < 1e-4
+    assert rel_err(dg, g_.grad) < 1e-4 and rel_err(db, b_.grad) < 1e-4
+    assert dZ[N:].abs().max().item() == 0 and dZ[:, d:].abs().max().item() == 0
+
+
+def test_gather_pack_colsum():
+    src = _mk(50, 7, seed=15)
+    idx = torch.randint(0, 50, (30, 5), device=DEV)
+    dst = torch.full((64, 64), 7.0, device=DEV)
+    err = torch.zeros(1, dtype=torch.int32, device=DEV)
+    K.gather_rows(src, idx, 5, dst, 30, 64, 7, 64, err)
+    assert torch.equal(dst[:30, :7], src[idx[:, 0]]) and dst[30:].abs().max() == 0 and dst[:, 7:].abs().max() == 0
+    assert err.item() == 0
+    W = _mk(3 * 7, 7, seed=16)
+    Wp = torch.empty(3 * 64, 64, device=DEV)
+    K.pack_padded(W, 7, 3 * 64, 64, (64, 7), (64, 7), Wp, 64)
+    for q in range(3):
+        assert torch.equal(Wp[q * 64:q * 64 + 7, :7], W[q * 7:(q + 1) * 7])
+    X = _mk(300, 192, seed=17)
+    out = torch.empty(3 * 7, device=DEV)
+    ws = torch.empty(2 * 192, device=DEV)
+    K.colsum(X, 300, 192, 192, (64, 7), out, ws)
+    ref = X.sum(0).view(3, 64)[:, :7].reshape(-1)
+    assert rel_err(out, ref) < 1e-5
+
+
+def test_pool_head_ce():
+    Np, d, dp, B, C = 128, 10, 64, 4, 3
+    X = _mk(Np, dp, seed=18)
+    off = torch.tensor([0, 5, 9, 20, 31], device=DEV)
+    col = torch.arange(31, device=DEV)
+    vals = torch.ones(31, device=DEV)
+    G = torch.zeros(B, dp, device=DEV)
+    K.pool_fwd(X, dp, off, col, vals, G, dp, B, d, 0.0, 0)
+    ref = torch.stack([X[off[b]:off[b + 1], :d].sum(0) for b in range(B)])
+    assert rel_err(G[:, :d], ref) < 1e-5
+    W, bias = _mk(C, d, seed=19), _mk(C, seed=20)
+    sc = torch.empty(B, C, device=DEV)
+    K.head_fwd(G, dp, W, bias, sc, B, C, d, False)
+    assert rel_err(sc, ref @ W.t() + bias) < 1e-5
+    labels = torch.tensor([0, 2, 1, 2], device=DEV)
+    loss, ds = torch.empty(1, device=DEV), torch.empty(B, C, device=DEV)
+    K.smoothed_ce(sc, labels, B, C, 0.1, loss, ds)
+    s = sc.clone().requires_grad_(True)
+    t = torch.full((B, C), 0.05, device=DEV)
+    t.scatter_(1, labels[:, None], 0.9)
+    lref = torch.mean(torch.sum(-t * torch.log_softmax(s, 1), 1))
+    lref.backward()
+    assert abs(loss.item() - lref.item()) < 1e-5 and rel_err(ds, s.grad) < 1e-5
+
+
+def test_adam_matches_torch():
+    n = 1000
+    p0 = _mk(n, seed=21)
+    g = _mk(n, seed=22) * 3
+    p1 = p0.clone()
+    m, v = torch.zeros(n, device=DEV), torch.zeros(n, device=DEV)
+    ws, sq = torch.empty(1024, device=DEV), torch.empty(1, device=DEV)
+    tp = p0.clone().requires_grad_(True)
+    opt = torch.optim.Adam([tp], lr=0.01)
+    for step in range(1, 4):
+        K.sqnorm(g, n, ws, sq)
+        K.adam(p1, g, m, v, n, sq, 0.5, 0.9, 0.999, 1e-8, 0.01 / (1 - 0.9 ** step), math.sqrt(1 - 0.999 ** step))
+        tp.grad = g.clone()
+        torch.nn.utils.clip_grad_norm_([tp], 0.5)
+        opt.step()
+    assert abs(sq.item() - (g.double() ** 2).sum().item()) / sq.item() < 1e-5
+    assert rel_err(p1, tp.detach()) < 1e-5

@@ -1,0 +1,197 @@
+#!/usr/bin/env python
+"""U2GNN-Sup training throughput on MI355X — BASELINE.json metric
+"graphs/sec (fwd+bwd) U2GNN-Sup COLLAB k=16 T=4 at 1/2/4/8 MI355X".
+
+Workload: COLLAB supervised, batch_size=64 graphs per GPU, num_neighbors=16,
+num_timesteps=4, ff_hidden_size=1024, d=367 (degree-as-tag one-hot), 3 classes, dropout 0.5,
+Adam lr 5e-4 + clip_grad_norm_(0.5).  COLLAB itself is not in the image, so the graphs are the
+synthetic COLLAB-like set of u2gnn_hip.synthetic (published statistics); weights random-init.
+
+A step = forward + smoothed-CE loss + backward + (DP: gradient all-reduce over RCCL) + clip + Adam
+over one 64-graph batch per rank; batches are pre-assembled and resident in HBM before timing.
+Data-parallel: one process per GPU, each rank trains its own 64-graph batch (weak scaling; the
+attention couples all graphs of a batch, so a batch never splits across GPUs).
+
+Usage: python bench.py [--gpus N --steps K --warmup W]   (N>1 under torch.distributed.run)
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [os.path.join(REPO, "graph-transformer_amd"), REPO]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+METRIC = "graphs/sec (fwd+bwd) U2GNN-Sup COLLAB k=16 T=4 at 1/2/4/8 MI355X"
+PEAK = {"fp32": 157.3}     # TFLOP/s dense matrix-core peak per dtype (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch-size", type=int, default=64)
+    ap.add_argument("--num-neighbors", type=int, default=16)
+    ap.add_argument("--num-timesteps", type=int, default=4)
+    ap.add_argument("--ff-hidden-size", type=int, default=1024)
+    ap.add_argument("--num-hidden-layers", type=int, default=1)
+    ap.add_argument("--precision", default="fp32", choices=["fp32"])
+    ap.add_argument("--lr", type=float, default=5e-4)
+    ap.add_argument("--distinct-batches", type=int, default=8)
+    ap.add_argument("--cpu-baseline", type=int, default=1, help="1 = time the CPU oracle on rank 0 at N=1")
+    ap.add_argument("--cpu-steps", type=int, default=1)
+    ap.add_argument("--no-roofline", action="store_true")
+    return ap.parse_args()
+
+
+def model_step_flops(N, d, ff, T, L):
+    """Algorithmic FLOPs of one fwd+bwd step, slot 0 only."""
+    return 3.0 * L * T * (8.0 * N * d * d + 4.0 * N * N * d + 4.0 * N * d * ff)
+
+
+def cpu_baseline(hb, sd, args, d, C):
+    """The oracle restatement (reference semantics incl. all k+1 slots and p=0.5 dropout,
+    i.e. the reference's cost) timed on the host cores: forward + loss + backward + clip + Adam."""
+    from oracle import u2gnn_oracle as O
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
+    threads = max(1, min(threads, os.cpu_count()))
+    torch.set_num_threads(threads)
+    params = {k: v.detach().cpu().clone().requires_grad_(True) for k, v in sd.items()}
+    plist = list(params.values())
+    opt = torch.optim.Adam(plist, lr=args.lr)
+    ix = torch.from_numpy(hb.input_x)
+    X = torch.from_numpy(hb.X_concat)
+    lab = torch.from_numpy(hb.labels)
+    times = []
+    for _ in range(args.cpu_steps):
+        t0 = time.perf_counter()
+        opt.zero_grad()
+        scores = O.sup_forward(params, ix, hb.offsets, X, args.num_hidden_layers, args.num_timesteps,
+                               train=True, dropout=0.5)
+        loss = O.soft_cross_entropy(scores, O.label_smoothing(lab, C))
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(plist, 0.5)
+        opt.step()
+        times.append(time.perf_counter() - t0)
+    t = float(np.median(times))
+    return {"value": hb.labels.shape[0] / t, "unit": "graphs/s", "cores": threads, "kind": "port",
+            "sample": f"{args.cpu_steps} full training step(s) of one {hb.labels.shape[0]}-graph batch "
+                      f"(N={hb.N} nodes, all {args.num_neighbors + 1} neighbour slots, dropout on) "
+                      f"= {t:.1f} s/step, oracle/u2gnn_oracle.py on torch CPU"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    from pytorch_U2GNN_Sup import TransformerU2GNN
+    from u2gnn_hip.batching import BatchLoader
+    from u2gnn_hip.core import DeviceBatch
+    from u2gnn_hip.engine import TIMER
+    from u2gnn_hip.synthetic import collab_like
+    from u2gnn_hip.train import SupTrainer
+
+    d, C = 367, 3
+    store = collab_like(seed=0)
+    np.random.seed(123)
+    loader = BatchLoader(store, args.batch_size, args.num_neighbors)
+    # rank r keeps batch r of every group of `world` consecutive batches of the single
+    # reference numpy stream (the others are replayed to keep the stream aligned)
+    host = []
+    for _ in range(args.distinct_batches):
+        for g in range(world):
+            if g == rank:
+                host.append(loader())
+            else:
+                loader.replay()
+    batches = [DeviceBatch.from_offsets(h.input_x, h.offsets, h.X_concat, h.labels, device=dev) for h in host]
+    torch.manual_seed(123)
+    model = TransformerU2GNN(feature_dim_size=d, ff_hidden_size=args.ff_hidden_size, num_classes=C,
+                             num_self_att_layers=args.num_timesteps, dropout=0.5,
+                             num_U2GNN_layers=args.num_hidden_layers, precision=args.precision)
+    sd0 = {k: v.clone() for k, v in model.state_dict().items()}
+    model = model.to(dev).train()
+    trainer = SupTrainer(model, lr=args.lr, max_norm=0.5, seed=123 + rank)
+    if dist is not None:
+        dist.broadcast(trainer.flat.flat, 0)
+
+        def sync(flat):
+            dist.all_reduce(flat.gflat)
+            flat.gflat.mul_(1.0 / world)
+        trainer.grad_sync = sync
+
+    nb = len(batches)
+    for i in range(args.warmup):
+        trainer.step(batches[i % nb])
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    TIMER.records.clear()
+    TIMER.enabled = not args.no_roofline
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        trainer.step(batches[(args.warmup + i) % nb])
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    TIMER.enabled = False
+    if dist is not None:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    loss = float(trainer.loss.item())
+    graphs = args.steps * args.batch_size * world
+    value = graphs / elapsed
+    used = [batches[(args.warmup + i) % nb] for i in range(args.steps)]
+    mean_N = float(np.mean([b.N for b in used]))
+    step_flops = float(np.mean([model_step_flops(b.N, d, args.ff_hidden_size, args.num_timesteps,
+                                                 args.num_hidden_layers) for b in used]))
+
+    roof = None
+    if TIMER.records:
+        fl = sum(r[1] for r in TIMER.records)
+        ms = sum(r[2].elapsed_time(r[3]) for r in TIMER.records)
+        ach = fl / (ms * 1e-3) / 1e12
+        peak = PEAK[args.precision]
+        roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
+                "frac": round(ach / peak, 4), "traffic": None,
+                "kernel": "gemm_f32_kernel on the attention products (Q.K^T, P.V, dO.V^T->dS, Pd^T.dO, dS.K, "
+                          "dS^T.Q); algorithmic 2*N*N*d FLOP per launch, real N and d",
+                "launches": len(TIMER.records), "avg_launch_us": round(1e3 * ms / len(TIMER.records), 1),
+                "step_tflops": round(step_flops / (elapsed / args.steps * world / world) / 1e12, 2)}
+    out = {"metric": METRIC, "value": round(value, 2), "unit": "graphs/s", "n_gpus": world, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 3), "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": args.precision,
+           "data": "synthetic COLLAB-like graphs (5000 graphs, mean 74.49 nodes, degree-tag one-hot d=367, "
+                   "3 classes); random-init weights",
+           "config": {"workload": "U2GNN-Sup COLLAB (C4): batch_size=64/GPU, num_neighbors=16, num_timesteps=4, "
+                                  "ff_hidden_size=1024, num_hidden_layers=1, d=367",
+                      "global_batch": args.batch_size * world, "mean_nodes_per_batch": round(mean_N, 1),
+                      "parallelism": f"dp{world}", "precision": args.precision},
+           "final_loss": round(loss, 5), "roofline": roof, "cpu_baseline": None}
+    if rank == 0 and world == 1 and args.cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(host[args.warmup % nb], sd0, args, d, C)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -337,6 +337,17 @@ __global__ void __launch_bounds__(256) dropout_mask_kernel(uint64_t seed, int64_
     }
 }
 
+__global__ void __launch_bounds__(256) dropout_kernel(const float *X, int64_t ldx, float *Y, int64_t ldy, int64_t rows,
+                                                      int64_t cols, float p, uint64_t seed) {
+    const int64_t total = rows * cols;
+    const float ks = 1.f / (1.f - p);
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+        const int64_t r = i / cols, c = i - r * cols;
+        const float v = X[r * ldx + c];
+        Y[r * ldy + c] = u2gnn_keep(seed, (uint32_t)r, (uint32_t)c, p) ? v * ks : 0.f;
+    }
+}
+
 inline unsigned grid_for(int64_t n, int64_t per_block, int64_t cap = 8192) {
     int64_t g = (n + per_block - 1) / per_block;
     if (g < 1) g = 1;
@@ -444,6 +455,15 @@ int u2gnn_layernorm_param_reduce(const float *part, int64_t n_blocks, int64_t d,
     if (!part || !dgamma || !dbeta) return U2GNN_E_ARG;
     hipLaunchKernelGGL(ln_param_reduce_kernel, dim3(grid_for(d, 256, 1 << 30)), dim3(256), 0, u2gnn_stream(stream),
                        part, n_blocks, d, d_pad, dgamma, dbeta, accumulate);
+    return u2gnn_launch_status();
+}
+
+int u2gnn_dropout(const float *X, int64_t ldx, float *Y, int64_t ldy, int64_t rows, int64_t cols, float p,
+                  uint64_t seed, void *stream) {
+    if (!X || !Y || p < 0.f || p >= 1.f) return U2GNN_E_ARG;
+    if (rows * cols == 0) return U2GNN_OK;
+    hipLaunchKernelGGL(dropout_kernel, dim3(grid_for(rows * cols, 256)), dim3(256), 0, u2gnn_stream(stream), X, ldx, Y,
+                       ldy, rows, cols, p, seed);
     return u2gnn_launch_status();
 }
 

@@ -76,6 +76,7 @@ _HIP_SIGS = {
     "u2gnn_sampled_softmax_fwd": ([VP, I64, VP, VP, I64, VP, I64, VP, VP, I64, I64, VP], c_int32),
     "u2gnn_sampled_softmax_bwd": ([VP, I64, VP, VP, I64, VP, I64, VP, VP, VP, I64, VP, I64, I64, I64, VP], c_int32),
     "u2gnn_dropout_mask": ([c_uint64, I64, I64, F32, VP, VP], c_int32),
+    "u2gnn_dropout": ([VP, I64, VP, I64, I64, I64, F32, c_uint64, VP], c_int32),
 }
 
 _LUS_SIGS = {

@@ -65,6 +65,9 @@ class GraphStore:
         np.cumsum(deg_all, out=self.nbr_start[1:])
         self.d = self.X.shape[1]
 
+    def degrees_of(self, ids) -> np.ndarray:
+        return np.concatenate([self.deg[self.node_start[i]:self.node_start[i + 1]] for i in ids])
+
     def assemble(self, graph_ids: Sequence[int], num_neighbors: int, rng=np.random,
                  with_input_y: bool = False) -> HostBatch:
         """get_batch_data for the graphs ``graph_ids`` (in that order)."""
@@ -107,7 +110,7 @@ class BatchLoader:
         """Consume exactly the numpy draws of one batch without building it (data-parallel
         ranks skip the batches of other ranks this way)."""
         sel = self.rng.permutation(len(self.store.graphs))[:self.bs]
-        deg = np.concatenate([self.store.deg[self.store.node_start[i]:self.store.node_start[i + 1]] for i in sel])
+        deg = self.store.degrees_of(sel)
         live = deg[deg > 0]
         if len(live):
             self.rng.randint(0, live[:, None], size=(len(live), self.k))

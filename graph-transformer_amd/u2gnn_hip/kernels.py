@@ -189,6 +189,12 @@ def sampled_softmax_bwd(X, ldx, labels, sample_ids, S, W, ldw, prob, dloss, dX, 
                                               int(D), _s()), "u2gnn_sampled_softmax_bwd")
 
 
+def dropout(X, ldx, Y, ldy, rows, cols, p, seed):
+    _dev(X, Y)
+    check(hip_lib().u2gnn_dropout(_p(X), int(ldx), _p(Y), int(ldy), int(rows), int(cols), float(p), int(seed), _s()),
+          "u2gnn_dropout")
+
+
 def dropout_mask(seed, rows, cols, p, device="cuda"):
     out = torch.empty(rows, cols, dtype=torch.uint8, device=device)
     check(hip_lib().u2gnn_dropout_mask(int(seed), int(rows), int(cols), float(p), _p(out), _s()),

@@ -181,6 +181,12 @@ int u2gnn_sampled_softmax_bwd(const float *X, int64_t ldx, const int64_t *labels
                               const float *prob, const float *dloss, float *dX, int64_t lddx,
                               float *dW, int64_t lddw, int64_t n_rows, int64_t D, void *stream);
 
+/* ---- a12: dropout on the concatenated UnSup node embeddings (model_U2GNN_Unsup_multi.py:56) --
+ * Y[i, j] = X[i, j] * keep(seed, i, j) / (1-p) for i < rows, j < cols.  The backward is the same
+ * call on the upstream gradient with the same seed.  Y may alias X. */
+int u2gnn_dropout(const float *X, int64_t ldx, float *Y, int64_t ldy, int64_t rows, int64_t cols, float p,
+                  uint64_t seed, void *stream);
+
 /* ---- debugging / tests ---------------------------------------------------------------- */
 /* out[i*cols + j] = keep(seed, i, j) ? 1 : 0   (the exact dropout mask the kernels apply) */
 int u2gnn_dropout_mask(uint64_t seed, int64_t rows, int64_t cols, float p, uint8_t *out, void *stream);

@@ -46,9 +46,15 @@ class LogUniformSampler(object):
             raise IndexError("id out of range")
         return out
 
+    def sample_set_order(self, size):
+        """ids in the order the reference returns them: its Cython binding converts the C++
+        unordered_set into a Python set (inserting in C++ iteration order) before list()."""
+        ids, nt = self.sample_ids(size)
+        return np.asarray(list(set(ids.tolist())), dtype=np.int64), nt
+
     def sample(self, size, labels):
         """log_uniform.pyx:29-34: (sample ids, true expected counts, sample expected counts)."""
-        ids, nt = self.sample_ids(size)
+        ids, nt = self.sample_set_order(size)
         true_freq = self.expected_count(nt, np.asarray(labels)).tolist()
         sample_freq = self.expected_count(nt, ids).tolist()
         return ids.tolist(), true_freq, sample_freq

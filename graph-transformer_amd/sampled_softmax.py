@@ -59,7 +59,7 @@ class SampledSoftmax(nn.Module):
         self.weight.data.uniform_(-stdv, stdv)
 
     def draw_samples(self):
-        ids, _ = self.sampler.sample_ids(self.nsampled)
+        ids, _ = self.sampler.sample_set_order(self.nsampled)
         return ids
 
     def forward(self, inputs, labels):

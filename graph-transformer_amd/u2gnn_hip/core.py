@@ -67,8 +67,70 @@ class DeviceBatch:
                            rowptr, cols.contiguous(), vals.contiguous(), labels)
 
 
+class EncoderStack:
+    """L U2GNN layers x T post-LN encoder layers on slot-0 rows, with the re-gather between
+    U2GNN layers (pytorch_U2GNN_Sup.py:33-39; pytorch_U2GNN_UnSup.py:55-64)."""
+
+    def __init__(self, u2gnn_layers, d: int, ff: int, T: int, L: int, prec: str = "fp32", p_enc: float = 0.5):
+        self.layers, self.d, self.ff, self.T, self.L, self.prec, self.p_enc = u2gnn_layers, d, ff, T, L, prec, p_enc
+        self.packed = None
+
+    def layer_params(self, l, t) -> LayerParams:
+        return LayerParams.from_encoder_layer(self.layers[l].layers[t])
+
+    def _pack(self, device):
+        if self.packed is None:
+            self.packed = [[PackedLayer(self.d, self.ff, device) for _ in range(self.T)] for _ in range(self.L)]
+        for l in range(self.L):
+            for t in range(self.T):
+                self.packed[l][t].pack(self.layer_params(l, t))
+
+    def forward(self, b: "DeviceBatch", train: bool, need_ctx: bool, seed: int):
+        """Returns (outs, ctx): outs[l] = padded [Np, dp] slot-0 output of U2GNN layer l."""
+        dev = b.X_concat.device
+        d, dp = self.d, rup(self.d, 64)
+        dims = Dims(b.N, d, self.ff)
+        Np = dims.Np
+        self._pack(dev)
+        X = torch.empty(Np, dp, device=dev, dtype=torch.float32)
+        K.gather_rows(b.X_concat, b.input_x, b.idx_stride, X, b.N, Np, d, dp)
+        outs, lctxs = [], []
+        for l in range(self.L):
+            lctx = []
+            for t in range(self.T):
+                seeds = {s: site_seed(seed, l, t, s) for s in (SITE_ATTN, SITE_DROP1, SITE_DROPFF, SITE_DROP2)}
+                X, c = encoder_layer_forward(X, self.packed[l][t], self.layer_params(l, t), dims, train, seeds,
+                                             need_ctx, self.prec, self.p_enc)
+                lctx.append(c)
+            outs.append(X)
+            lctxs.append(lctx)
+            if l + 1 < self.L:
+                Xn = torch.empty(Np, dp, device=dev, dtype=torch.float32)
+                K.gather_rows(X, b.input_x, b.idx_stride, Xn, b.N, Np, d, dp)
+                X = Xn
+        return outs, {"dims": dims, "layers": lctxs, "batch": b}
+
+    def backward(self, ctx, ext_grad, grads: dict, prefix: str = "u2gnn_layers"):
+        """ext_grad(l) -> fresh padded gradient of outs[l] from outside the stack (head / loss).
+        Writes encoder parameter gradients into grads[<reference key>]."""
+        b = ctx["batch"]
+        dims = ctx["dims"]
+        dnext = None
+        for l in reversed(range(self.L)):
+            dX = ext_grad(l)
+            if dnext is not None:
+                K.scatter_add_rows(dnext, b.input_x, b.idx_stride, dX, b.N, self.d)
+            for t in reversed(range(self.T)):
+                pre = f"{prefix}.{l}.layers.{t}."
+                g = LayerParams(*[grads[pre + k] for k in LAYER_KEYS])
+                dX = encoder_layer_backward(dX, ctx["layers"][l][t], self.packed[l][t], self.layer_params(l, t), g,
+                                            dims, self.prec)
+            dnext = dX
+        return dnext
+
+
 class SupCore:
-    """Forward/backward of the supervised TransformerU2GNN on the HIP kernels."""
+    """Forward/backward of the supervised TransformerU2GNN (pytorch_U2GNN_Sup.py:30-46)."""
 
     def __init__(self, module, precision: str = "fp32"):
         self.m = module
@@ -78,74 +140,42 @@ class SupCore:
         self.C = module.num_classes
         self.L = module.num_U2GNN_layers
         self.T = module.num_self_att_layers
-        self.p_enc = 0.5                      # hard-coded in pytorch_U2GNN_Sup.py:20
         self.p_head = module.dropout_p        # args.dropout, pytorch_U2GNN_Sup.py:28
-        self.packed = None
-
-    def layer_params(self, l, t) -> LayerParams:
-        return LayerParams.from_encoder_layer(self.m.u2gnn_layers[l].layers[t])
-
-    def _pack(self, device):
-        if self.packed is None:
-            self.packed = [[PackedLayer(self.d, self.ff, device) for _ in range(self.T)] for _ in range(self.L)]
-        for l in range(self.L):
-            for t in range(self.T):
-                self.packed[l][t].pack(self.layer_params(l, t))
+        # encoder dropout is hard-coded to 0.5 (pytorch_U2GNN_Sup.py:20)
+        self.stack = EncoderStack(module.u2gnn_layers, self.d, self.ff, self.T, self.L, precision, 0.5)
 
     def forward(self, b: DeviceBatch, train: bool, need_ctx: bool, seed: int):
         dev = b.X_concat.device
         d, dp = self.d, rup(self.d, 64)
-        dims = Dims(b.N, d, self.ff)
-        Np = dims.Np
-        self._pack(dev)
-        X = torch.empty(Np, dp, device=dev, dtype=torch.float32)
-        K.gather_rows(b.X_concat, b.input_x, b.idx_stride, X, b.N, Np, d, dp)
+        outs, sctx = self.stack.forward(b, train, need_ctx, seed)
         scores = torch.empty(b.B, self.C, device=dev, dtype=torch.float32)
         ph = self.p_head if train else 0.0
-        ctx = {"dims": dims, "layers": [], "batch": b, "seed": seed, "ph": ph}
+        heads = []
         for l in range(self.L):
-            lctx = []
-            for t in range(self.T):
-                seeds = {s: site_seed(seed, l, t, s) for s in (SITE_ATTN, SITE_DROP1, SITE_DROPFF, SITE_DROP2)}
-                X, c = encoder_layer_forward(X, self.packed[l][t], self.layer_params(l, t), dims, train, seeds,
-                                             need_ctx, self.prec, self.p_enc)
-                lctx.append(c)
             G = torch.empty(b.B, dp, device=dev, dtype=torch.float32)
             hs = site_seed(seed, l, 0, SITE_HEAD)
-            K.pool_fwd(X, dp, b.rowptr, b.colidx, b.vals, G, dp, b.B, d, ph, hs)
-            pw, pb = self.m.predictions[l].weight, self.m.predictions[l].bias
-            K.head_fwd(G, dp, pw, pb, scores, b.B, self.C, d, accumulate=l > 0)
-            ctx["layers"].append((lctx, G, hs))
-            if l + 1 < self.L:
-                Xn = torch.empty(Np, dp, device=dev, dtype=torch.float32)
-                K.gather_rows(X, b.input_x, b.idx_stride, Xn, b.N, Np, d, dp)
-                X = Xn
-        ctx["out"] = X
-        return scores, ctx
+            K.pool_fwd(outs[l], dp, b.rowptr, b.colidx, b.vals, G, dp, b.B, d, ph, hs)
+            K.head_fwd(G, dp, self.m.predictions[l].weight, self.m.predictions[l].bias, scores, b.B, self.C, d,
+                       accumulate=l > 0)
+            heads.append((G, hs))
+        return scores, {"stack": sctx, "heads": heads, "ph": ph, "batch": b}
 
     def backward(self, ctx, dscores: torch.Tensor, grads: dict):
         """grads: name -> real-shaped tensor (reference state_dict key names)."""
         b: DeviceBatch = ctx["batch"]
-        dims: Dims = ctx["dims"]
+        dims: Dims = ctx["stack"]["dims"]
         dev = dscores.device
         d, dp, Np = self.d, dims.dp, dims.Np
-        dnext = None
-        for l in reversed(range(self.L)):
-            lctx, G, hs = ctx["layers"][l]
+
+        def ext(l):
+            G, hs = ctx["heads"][l]
             dG = torch.empty(b.B, dp, device=dev, dtype=torch.float32)
             K.head_bwd(dscores, G, dp, self.m.predictions[l].weight, dG, dp, grads[f"predictions.{l}.weight"],
                        grads[f"predictions.{l}.bias"], b.B, self.C, d)
             dX = torch.zeros(Np, dp, device=dev, dtype=torch.float32)
             K.pool_bwd(dG, dp, b.rowptr, b.colidx, b.vals, dX, dp, b.B, d, ctx["ph"], hs)
-            if dnext is not None:
-                K.scatter_add_rows(dnext, b.input_x, b.idx_stride, dX, b.N, d)
-            for t in reversed(range(self.T)):
-                pre = f"u2gnn_layers.{l}.layers.{t}."
-                g = LayerParams(*[grads[pre + k] for k in LAYER_KEYS])
-                dX = encoder_layer_backward(dX, lctx[t], self.packed[l][t], self.layer_params(l, t), g, dims,
-                                            self.prec)
-            dnext = dX
-        return dnext
+            return dX
+        return self.stack.backward(ctx["stack"], ext, grads)
 
 
 LAYER_KEYS = ["self_attn.in_proj_weight", "self_attn.in_proj_bias", "self_attn.out_proj.weight",
@@ -157,8 +187,9 @@ class FlatParams:
     """Re-homes every parameter of ``module`` into one flat fp32 device buffer (params become
     views, keeping their reference shapes and state_dict keys) with a matching flat grad buffer."""
 
-    def __init__(self, module: torch.nn.Module):
-        self.names, self.params = zip(*[(n, p) for n, p in module.named_parameters()])
+    def __init__(self, module: torch.nn.Module, names=None):
+        sel = None if names is None else set(names)
+        self.names, self.params = zip(*[(n, p) for n, p in module.named_parameters() if sel is None or n in sel])
         dev = self.params[0].device
         sizes = [p.numel() for p in self.params]
         # 16-byte aligned offsets for the float4 sweeps

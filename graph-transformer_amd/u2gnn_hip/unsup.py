@@ -1,0 +1,122 @@
+"""Unsupervised U2GNN on the gfx950 kernels.
+
+Working semantics of the fork's UnSup model (the shipped file cannot run):
+per-U2GNN-layer slot-0 outputs concatenated to [N, d*L] (pytorch_U2GNN_UnSup.py:52-69,
+U2GNN_tf/model_U2GNN_Unsup_multi.py:43-55) -> dropout (:56 of the TF model) -> SampledSoftmax
+over the node vocabulary with 512 log-uniform samples (sampled_softmax.py:36-56); the training
+loss is the SUM of the per-node losses (train_pytorch_U2GNN_UnSup.py:156).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import numpy as np
+import torch
+
+from . import kernels as K
+from .core import DeviceBatch, EncoderStack, FlatParams, FusedAdam
+from .engine import rup, site_seed
+
+SITE_SS_DROP = 6
+
+
+class UnSupCore:
+    def __init__(self, module, precision: str = "fp32"):
+        self.m = module
+        self.d = module.feature_dim_size
+        self.ff = module.ff_hidden_size
+        self.L = module.num_U2GNN_layers
+        self.T = module.num_self_att_layers
+        self.p_out = module.dropout_p
+        self.stack = EncoderStack(module.u2gnn_layers, self.d, self.ff, self.T, self.L, precision, 0.5)
+
+    def encode(self, b: DeviceBatch, train: bool, need_ctx: bool, seed: int):
+        """-> (OV f32 [N, d*L] real layout, ctx)."""
+        outs, sctx = self.stack.forward(b, train, need_ctx, seed)
+        d, dp, L = self.d, rup(self.d, 64), self.L
+        N = b.N
+        OV = torch.empty(N, d * L, device=b.X_concat.device, dtype=torch.float32)
+        for l in range(L):
+            # padded [Np, dp] -> real columns l*d .. (l+1)*d of OV
+            K.slab_reduce(outs[l], 1, 0, N, dp, dp, (N, N), (dp, d), OV[:, l * d:], d * L)
+        return OV, sctx
+
+    def encode_backward(self, sctx, dOV: torch.Tensor, grads: dict):
+        d, dp, L = self.d, rup(self.d, 64), self.L
+        dims = sctx["dims"]
+        Np = dims.Np
+
+        def ext(l):
+            dX = torch.empty(Np, dp, device=dOV.device, dtype=torch.float32)
+            K.pack_padded(dOV[:, l * d:], d * L, Np, dp, (Np, dims.N), (dp, d), dX, dp)
+            return dX
+        return self.stack.backward(sctx, ext, grads)
+
+
+class UnSupTrainer:
+    """One iteration of train() in train_pytorch_U2GNN_UnSup.py:152-160, fused on device:
+    encode -> dropout -> sampled softmax (sum loss) -> backward -> clip(0.5) -> Adam (dense over
+    the whole embedding table, like torch.optim.Adam on a dense gradient)."""
+
+    def __init__(self, model, lr: float, max_norm: Optional[float] = 0.5, seed: int = 123):
+        self.m = model
+        self.core: UnSupCore = model.core
+        self.flat = FlatParams(model, names=model.trainable_names())
+        self.opt = FusedAdam(self.flat, lr, max_norm)
+        dev = self.flat.flat.device
+        self.loss = torch.zeros(1, device=dev)
+        self.ws = torch.empty(1024, device=dev)
+        self.gen = torch.Generator().manual_seed(seed)
+        self.grad_sync = None
+
+    def next_seed(self) -> int:
+        return int(torch.randint(0, 2 ** 62, (1,), generator=self.gen).item())
+
+    def forward_backward(self, b: DeviceBatch, sample_ids: torch.Tensor, train: bool = True):
+        core, ss = self.core, self.m.ss
+        seed = self.next_seed()
+        OV, sctx = core.encode(b, train, True, seed)
+        N, D = OV.shape
+        p = core.p_out if train else 0.0
+        ds = site_seed(seed, 0, 0, SITE_SS_DROP)
+        if p > 0:
+            OVd = torch.empty_like(OV)
+            K.dropout(OV, D, OVd, D, N, D, p, ds)
+        else:
+            OVd = OV
+        W = ss.weight
+        S = sample_ids.numel()
+        lrow = torch.empty(N, device=OV.device)
+        prob = torch.empty(N, S, device=OV.device)
+        K.sampled_softmax_fwd(OVd, D, b.input_y, sample_ids, S, W, W.stride(0), lrow, prob, N, D)
+        K.colsum(lrow.view(N, 1), N, 1, 1, (1, 1), self.loss, self.ws)
+        gW = self.flat.grads["ss.weight"]
+        gW.zero_()
+        dOV = torch.empty_like(OV)
+        K.sampled_softmax_bwd(OVd, D, b.input_y, sample_ids, S, W, W.stride(0), prob, None, dOV, D, gW, gW.stride(0),
+                              N, D)
+        if p > 0:
+            K.dropout(dOV, D, dOV, D, N, D, p, ds)
+        core.encode_backward(sctx, dOV, self.flat.grads)
+        return self.loss
+
+    def step(self, b: DeviceBatch, sample_ids: torch.Tensor, train: bool = True):
+        loss = self.forward_backward(b, sample_ids, train)
+        if self.grad_sync is not None:
+            self.grad_sync(self.flat)
+        self.opt.step()
+        return loss
+
+
+def graph_embeddings(weight: torch.Tensor, node_start: np.ndarray) -> torch.Tensor:
+    """evaluate() of train_pytorch_U2GNN_UnSup.py:167-169: spmm(graph_pool, ss.weight), i.e. the
+    per-graph sum of the learned node embeddings (graph_pool over ALL graphs, nodes contiguous)."""
+    dev = weight.device
+    G = len(node_start) - 1
+    V, D = weight.shape
+    out = torch.empty(G, D, device=dev)
+    rowptr = torch.as_tensor(np.asarray(node_start), dtype=torch.int64, device=dev)
+    col = torch.arange(V, device=dev, dtype=torch.int64)
+    vals = torch.ones(V, device=dev)
+    K.pool_fwd(weight, D, rowptr, col, vals, out, D, G, D, 0.0, 0)
+    return out

@@ -1,0 +1,75 @@
+"""Parity of the HIP sampled-softmax loss and the unsupervised U2GNN (C3 PTC composite) against
+golden fixtures generated from the REFERENCE encoder + REFERENCE SampledSoftmax + REFERENCE sampler.
+Tolerance: max|ours-ref| / max(1, |ref|) <= 1e-3."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def close(a, b, tol=1e-3):
+    a = torch.as_tensor(a).double().cpu()
+    b = torch.as_tensor(b).double().cpu()
+    return ((a - b).abs().max() / max(1.0, b.abs().max().item())).item() <= tol
+
+
+def test_sampled_softmax_vs_reference(golden_dir):
+    from sampled_softmax import SampledSoftmax
+    z = dict(np.load(os.path.join(golden_dir, "sampled_softmax.npz")))
+    V, D = z["weight"].shape
+    ss = SampledSoftmax(V, 512, D, DEV).to(DEV)
+    ss.weight.data.copy_(torch.from_numpy(z["weight"]))
+    x = torch.from_numpy(z["inputs"]).to(DEV).requires_grad_(True)
+    labels = torch.from_numpy(z["labels"]).to(DEV)
+    logits = ss.sampled(x, labels, (z["sample_ids"], None, None))
+    assert close(logits.detach(), z["logits"])
+    logits.sum().backward()
+    assert close(x.grad, z["grad_inputs"])
+    assert close(ss.weight.grad, z["grad_weight"])
+
+
+def _unsup_model(z):
+    from pytorch_U2GNN_UnSup import TransformerU2GNN
+    bs, k, T, ff, L, d, V = [int(x) for x in z["meta"]]
+    m = TransformerU2GNN(vocab_size=V, feature_dim_size=d, ff_hidden_size=ff, sampled_num=512, num_self_att_layers=T,
+                         num_U2GNN_layers=L, dropout=0.5, device=DEV)
+    sd = m.state_dict()
+    for kk in list(sd):
+        if "init." + kk in z:
+            sd[kk] = torch.from_numpy(z["init." + kk])
+    m.load_state_dict(sd)
+    return m.to(DEV).eval(), (bs, k, T, ff, L, d, V)
+
+
+def test_unsup_module_forward_backward(golden_dir):
+    from u2gnn_hip.core import DeviceBatch
+    z = dict(np.load(os.path.join(golden_dir, "ptc_unsup.npz")))
+    m, _ = _unsup_model(z)
+    b = DeviceBatch.from_offsets(z["input_x"], z["offsets"], z["X"], input_y=z["input_y"], device=DEV)
+    m.ss.draw_samples = lambda: z["sample_ids"]
+    logits, _ = m(b, None, None)
+    assert close(logits.detach(), z["logits"])
+    logits.sum().backward()
+    for n, p in m.named_parameters():
+        if "grad." + n in z:
+            assert close(p.grad, z["grad." + n]), n
+
+
+def test_unsup_fused_trainer_step(golden_dir):
+    from u2gnn_hip.core import DeviceBatch
+    from u2gnn_hip.unsup import UnSupTrainer
+    z = dict(np.load(os.path.join(golden_dir, "ptc_unsup.npz")))
+    m, _ = _unsup_model(z)
+    tr = UnSupTrainer(m, lr=float(z["lr"]))
+    b = DeviceBatch.from_offsets(z["input_x"], z["offsets"], z["X"], input_y=z["input_y"], device=DEV)
+    sid = torch.from_numpy(z["sample_ids"]).to(DEV)
+    loss = tr.step(b, sid, train=False)
+    assert abs(loss.item() - float(z["loss"])) <= 1e-3 * max(1.0, abs(float(z["loss"])))
+    assert abs(tr.opt.grad_norm() - float(z["grad_norm"])) <= 1e-3 * float(z["grad_norm"])
+    for n, p in m.named_parameters():
+        if "after." + n in z:
+            assert close(p.detach(), z["after." + n]), n

@@ -4,6 +4,8 @@
 // one wave64 per row, coalesced lane-contiguous accesses, fp32 throughout.
 #include "u2gnn_common.h"
 
+#include <algorithm>
+
 namespace {
 
 // ------------------------------------------------------------------------------------------
@@ -78,21 +80,50 @@ __global__ void __launch_bounds__(256) pack_padded_kernel(const float *src, int6
     }
 }
 
-// column sums, stage 1: block (64 columns x 256 rows) -> ws[chunk][col]
+// many pack jobs in one launch: the descriptors travel by value in the kernel arguments
+constexpr int PACK_MAX = 32;
+struct PackBatch {
+    u2gnn_pack_desc d[PACK_MAX];
+};
+
+__global__ void __launch_bounds__(256) pack_multi_kernel(PackBatch pb) {
+    const u2gnn_pack_desc &D = pb.d[blockIdx.y];
+    const int64_t total = D.rows_pad * D.cols_pad;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+        const int64_t r = i / D.cols_pad, c = i - r * D.cols_pad;
+        bool vr, vc;
+        const int64_t rr = blk_map(r, D.rblk_pad, D.rblk_real, &vr);
+        const int64_t cc = blk_map(c, D.cblk_pad, D.cblk_real, &vc);
+        D.dst[r * D.ld_dst + c] = (vr && vc) ? D.src[rr * D.ld_src + cc] : 0.f;
+    }
+}
+
+// column sums, stage 1: block (64 columns x CS_ROWS rows) -> ws[chunk][col].  Each wave owns 32
+// consecutive rows and keeps 8 independent loads in flight (latency, not bandwidth, bounds this).
+constexpr int CS_ROWS = 128;
+
 __global__ void __launch_bounds__(256) colsum_partial_kernel(const float *X, int64_t rows, int64_t cols_pad,
                                                              int64_t ld, float *ws) {
     __shared__ float red[4][64];
-    const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-    const int w = threadIdx.x >> 6;
-    const int64_t r0 = (int64_t)blockIdx.y * 256;
-    float s = 0.f;
-    if (c < cols_pad)
-        for (int64_t r = r0 + w; r < min(r0 + 256, rows); r += 4) s += X[r * ld + c];
-    red[w][threadIdx.x & 63] = s;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t c = (int64_t)blockIdx.x * 64 + lane;
+    const int64_t r0 = (int64_t)blockIdx.y * CS_ROWS + w * (CS_ROWS / 4);
+    float s[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s[j] = 0.f;
+    if (c < cols_pad) {
+#pragma unroll
+        for (int i = 0; i < CS_ROWS / 4; i += 8)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int64_t r = r0 + i + j;
+                if (r < rows) s[j] += X[r * ld + c];
+            }
+    }
+    red[w][lane] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
     __syncthreads();
     if (w == 0 && c < cols_pad)
-        ws[(int64_t)blockIdx.y * cols_pad + c] = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] +
-                                                 red[3][threadIdx.x];
+        ws[(int64_t)blockIdx.y * cols_pad + c] = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
 }
 
 __global__ void __launch_bounds__(256) colsum_final_kernel(const float *ws, int64_t n_chunks, int64_t cols_pad,
@@ -102,9 +133,14 @@ __global__ void __launch_bounds__(256) colsum_final_kernel(const float *ws, int6
     bool v;
     const int64_t cc = blk_map(c, cbp, cbr, &v);
     if (!v) return;
-    float s = 0.f;
-    for (int64_t k = 0; k < n_chunks; ++k) s += ws[k * cols_pad + c];
-    out[cc] = accumulate ? out[cc] + s : s;
+    float s[4] = {0.f, 0.f, 0.f, 0.f};
+    int64_t k = 0;
+    for (; k + 4 <= n_chunks; k += 4)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) s[j] += ws[(k + j) * cols_pad + c];
+    for (; k < n_chunks; ++k) s[0] += ws[k * cols_pad + c];
+    const float t = (s[0] + s[1]) + (s[2] + s[3]);
+    out[cc] = accumulate ? out[cc] + t : t;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -236,96 +272,118 @@ __global__ void __launch_bounds__(256) layernorm_fwd_kernel(const float *Z, int6
     }
 }
 
-constexpr int LNB_ROWS = 32;  // rows per block in the backward (8 per wave)
-
+// LN backward, row part: one wave per row (4 rows per block, fully parallel over rows).
 __global__ void __launch_bounds__(256) layernorm_bwd_kernel(const float *dY, int64_t ldy, const float *Z, int64_t ldz,
                                                             const float *mean, const float *rstd, const float *gamma,
                                                             float *dZ, int64_t lddz, float *dZd, int64_t lddrop,
-                                                            float p, uint64_t seed, float *part, int64_t rows_valid,
+                                                            float p, uint64_t seed, int64_t rows_valid,
                                                             int64_t rows_pad, int64_t d, int64_t d_pad) {
-    __shared__ float red[4][2][LN_MAXV * 64];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    float pg[LN_MAXV], pb[LN_MAXV];
-#pragma unroll
-    for (int i = 0; i < LN_MAXV; ++i) pg[i] = pb[i] = 0.f;
-    const float ks = p > 0.f ? 1.f / (1.f - p) : 1.f;
-    for (int rr = 0; rr < LNB_ROWS / 4; ++rr) {
-        const int64_t row = (int64_t)blockIdx.x * LNB_ROWS + w * (LNB_ROWS / 4) + rr;
-        if (row >= rows_pad) break;
-        float *dz = dZ + row * lddz;
-        float *dzd = dZd ? dZd + row * lddrop : nullptr;
-        if (row >= rows_valid) {
-            for (int64_t c = lane; c < d_pad; c += 64) {
-                dz[c] = 0.f;
-                if (dzd) dzd[c] = 0.f;
-            }
-            continue;
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (row >= rows_pad) return;
+    float *dz = dZ + row * lddz;
+    float *dzd = dZd ? dZd + row * lddrop : nullptr;
+    if (row >= rows_valid) {
+        for (int64_t c = lane; c < d_pad; c += 64) {
+            dz[c] = 0.f;
+            if (dzd) dzd[c] = 0.f;
         }
-        const float mu = mean[row], rs = rstd[row];
-        const float *dy = dY + row * ldy;
-        const float *z = Z + row * ldz;
-        float xh[LN_MAXV], g[LN_MAXV];
-        float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-        for (int i = 0; i < LN_MAXV; ++i) {
-            const int64_t c = lane + 64 * i;
-            if (c < d) {
-                const float dyv = dy[c];
-                xh[i] = (z[c] - mu) * rs;
-                g[i] = dyv * gamma[c];
-                pg[i] += dyv * xh[i];
-                pb[i] += dyv;
-            } else {
-                xh[i] = 0.f;
-                g[i] = 0.f;
-            }
-            s1 += g[i];
-            s2 += g[i] * xh[i];
-        }
-        const float m1 = wave_sum(s1) / (float)d;
-        const float m2 = wave_sum(s2) / (float)d;
-#pragma unroll
-        for (int i = 0; i < LN_MAXV; ++i) {
-            const int64_t c = lane + 64 * i;
-            if (c < d) {
-                const float v = rs * (g[i] - m1 - xh[i] * m2);
-                dz[c] = v;
-                if (dzd) dzd[c] = (p > 0.f) ? (u2gnn_keep(seed, (uint32_t)row, (uint32_t)c, p) ? v * ks : 0.f) : v;
-            } else if (c < d_pad) {
-                dz[c] = 0.f;
-                if (dzd) dzd[c] = 0.f;
-            }
-        }
+        return;
     }
+    const float ks = p > 0.f ? 1.f / (1.f - p) : 1.f;
+    const float mu = mean[row], rs = rstd[row];
+    const float *dy = dY + row * ldy;
+    const float *z = Z + row * ldz;
+    float xh[LN_MAXV], g[LN_MAXV];
+    float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int i = 0; i < LN_MAXV; ++i) {
-        red[w][0][lane + 64 * i] = pg[i];
-        red[w][1][lane + 64 * i] = pb[i];
-    }
-    __syncthreads();
-    for (int64_t c = threadIdx.x; c < d_pad; c += 256) {
-        float a = 0.f, b = 0.f;
-        if (c < LN_MAXV * 64) {
-            a = red[0][0][c] + red[1][0][c] + red[2][0][c] + red[3][0][c];
-            b = red[0][1][c] + red[1][1][c] + red[2][1][c] + red[3][1][c];
+        const int64_t c = lane + 64 * i;
+        if (c < d) {
+            xh[i] = (z[c] - mu) * rs;
+            g[i] = dy[c] * gamma[c];
+        } else {
+            xh[i] = 0.f;
+            g[i] = 0.f;
         }
-        part[(int64_t)blockIdx.x * 2 * d_pad + c] = a;
-        part[(int64_t)blockIdx.x * 2 * d_pad + d_pad + c] = b;
+        s1 += g[i];
+        s2 += g[i] * xh[i];
+    }
+    const float m1 = wave_sum(s1) / (float)d;
+    const float m2 = wave_sum(s2) / (float)d;
+#pragma unroll
+    for (int i = 0; i < LN_MAXV; ++i) {
+        const int64_t c = lane + 64 * i;
+        if (c < d) {
+            const float v = rs * (g[i] - m1 - xh[i] * m2);
+            dz[c] = v;
+            if (dzd) dzd[c] = (p > 0.f) ? (u2gnn_keep(seed, (uint32_t)row, (uint32_t)c, p) ? v * ks : 0.f) : v;
+        } else if (c < d_pad) {
+            dz[c] = 0.f;
+            if (dzd) dzd[c] = 0.f;
+        }
     }
 }
 
-__global__ void __launch_bounds__(256) ln_param_reduce_kernel(const float *part, int64_t n_blocks, int64_t d,
-                                                              int64_t d_pad, float *dgamma, float *dbeta,
-                                                              int accumulate) {
+// LN backward, column part: per 128-row chunk, sums over rows of dY*xhat (dgamma), dY (dbeta)
+// and dZd (the bias gradient of the dropout branch feeding this LN) -> ws[chunk][3][d_pad].
+__global__ void __launch_bounds__(256) ln_colstats_kernel(const float *dY, int64_t ldy, const float *Z, int64_t ldz,
+                                                          const float *mean, const float *rstd, const float *dZd,
+                                                          int64_t lddrop, int64_t rows, int64_t d, int64_t d_pad,
+                                                          float *ws) {
+    __shared__ float red[4][3][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t c = (int64_t)blockIdx.x * 64 + lane;
+    const int64_t r0 = (int64_t)blockIdx.y * CS_ROWS + w * (CS_ROWS / 4);
+    float sg[4] = {0.f, 0.f, 0.f, 0.f}, sb[4] = {0.f, 0.f, 0.f, 0.f}, sd[4] = {0.f, 0.f, 0.f, 0.f};
+    if (c < d) {
+#pragma unroll
+        for (int i = 0; i < CS_ROWS / 4; i += 4)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int64_t r = r0 + i + j;
+                if (r < rows) {
+                    const float dy = dY[r * ldy + c];
+                    sg[j] += dy * ((Z[r * ldz + c] - mean[r]) * rstd[r]);
+                    sb[j] += dy;
+                    if (dZd) sd[j] += dZd[r * lddrop + c];
+                }
+            }
+    }
+    red[w][0][lane] = (sg[0] + sg[1]) + (sg[2] + sg[3]);
+    red[w][1][lane] = (sb[0] + sb[1]) + (sb[2] + sb[3]);
+    red[w][2][lane] = (sd[0] + sd[1]) + (sd[2] + sd[3]);
+    __syncthreads();
+    if (w < 3 && c < d_pad)
+        ws[((int64_t)blockIdx.y * 3 + w) * d_pad + c] = red[0][w][lane] + red[1][w][lane] + red[2][w][lane] +
+                                                      red[3][w][lane];
+}
+
+__global__ void __launch_bounds__(256) ln_param_reduce_kernel(const float *ws, int64_t n_chunks, int64_t d,
+                                                              int64_t d_pad, float *dgamma, float *dbeta, float *dbias) {
     const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (c >= d) return;
-    float a = 0.f, b = 0.f;
-    for (int64_t k = 0; k < n_blocks; ++k) {
-        a += part[k * 2 * d_pad + c];
-        b += part[k * 2 * d_pad + d_pad + c];
+    float a[4] = {0.f, 0.f, 0.f, 0.f};
+    float b[4] = {0.f, 0.f, 0.f, 0.f};
+    float e[4] = {0.f, 0.f, 0.f, 0.f};
+    int64_t k = 0;
+    for (; k + 4 <= n_chunks; k += 4)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float *q = ws + (k + j) * 3 * d_pad + c;
+            a[j] += q[0];
+            b[j] += q[d_pad];
+            e[j] += q[2 * d_pad];
+        }
+    for (; k < n_chunks; ++k) {
+        const float *q = ws + k * 3 * d_pad + c;
+        a[0] += q[0];
+        b[0] += q[d_pad];
+        e[0] += q[2 * d_pad];
     }
-    dgamma[c] = accumulate ? dgamma[c] + a : a;
-    dbeta[c] = accumulate ? dbeta[c] + b : b;
+    dgamma[c] = (a[0] + a[1]) + (a[2] + a[3]);
+    dbeta[c] = (b[0] + b[1]) + (b[2] + b[3]);
+    if (dbias) dbias[c] = (e[0] + e[1]) + (e[2] + e[3]);
 }
 
 __global__ void __launch_bounds__(256) dropout_mask_kernel(uint64_t seed, int64_t rows, int64_t cols, float p,
@@ -398,10 +456,27 @@ int u2gnn_pack_padded(const float *src, int64_t ld_src, int64_t rows_pad, int64_
     return u2gnn_launch_status();
 }
 
+int u2gnn_pack_padded_multi(const u2gnn_pack_desc *descs, int32_t n, void *stream) {
+    if (n < 0 || (n && !descs)) return U2GNN_E_ARG;
+    for (int32_t o = 0; o < n; o += PACK_MAX) {
+        PackBatch pb;
+        const int32_t m = n - o < PACK_MAX ? n - o : PACK_MAX;
+        int64_t biggest = 1;
+        for (int32_t i = 0; i < m; ++i) {
+            pb.d[i] = descs[o + i];
+            if (!pb.d[i].src || !pb.d[i].dst || pb.d[i].rblk_pad < 1 || pb.d[i].cblk_pad < 1) return U2GNN_E_ARG;
+            biggest = std::max<int64_t>(biggest, pb.d[i].rows_pad * pb.d[i].cols_pad);
+        }
+        hipLaunchKernelGGL(pack_multi_kernel, dim3(grid_for(biggest, 256, 2048), (unsigned)m), dim3(256), 0,
+                           u2gnn_stream(stream), pb);
+    }
+    return u2gnn_launch_status();
+}
+
 int u2gnn_colsum(const float *X, int64_t rows, int64_t cols_pad, int64_t ld, int64_t cblk_pad, int64_t cblk_real,
                  float *out, int32_t accumulate, float *ws, void *stream) {
     if (!X || !out || !ws || cblk_pad < 1) return U2GNN_E_ARG;
-    const int64_t chunks = (rows + 255) / 256;
+    const int64_t chunks = (rows + CS_ROWS - 1) / CS_ROWS;
     hipStream_t st = u2gnn_stream(stream);
     hipLaunchKernelGGL(colsum_partial_kernel, dim3((unsigned)((cols_pad + 63) / 64), (unsigned)(chunks > 0 ? chunks : 1)),
                        dim3(256), 0, st, X, rows, cols_pad, ld, ws);
@@ -440,21 +515,27 @@ int u2gnn_layernorm_fwd(const float *Z, int64_t ldz, const float *gamma, const f
 
 int u2gnn_layernorm_bwd(const float *dY, int64_t ldy, const float *Z, int64_t ldz, const float *mean,
                         const float *rstd, const float *gamma, float *dZ, int64_t lddz, float *dZdrop, int64_t lddrop,
-                        float p, uint64_t seed, float *part, int64_t rows_valid, int64_t rows_pad, int64_t d,
-                        int64_t d_pad, void *stream) {
-    if (!dY || !Z || !mean || !rstd || !gamma || !dZ || !part || d < 1 || d > d_pad || d_pad > LN_MAXV * 64)
+                        float p, uint64_t seed, int64_t rows_valid, int64_t rows_pad, int64_t d, int64_t d_pad,
+                        void *stream) {
+    if (!dY || !Z || !mean || !rstd || !gamma || !dZ || d < 1 || d > d_pad || d_pad > LN_MAXV * 64)
         return U2GNN_E_ARG;
-    hipLaunchKernelGGL(layernorm_bwd_kernel, dim3(grid_for(rows_pad, LNB_ROWS, 1 << 30)), dim3(256), 0,
-                       u2gnn_stream(stream), dY, ldy, Z, ldz, mean, rstd, gamma, dZ, lddz, dZdrop, lddrop, p, seed,
-                       part, rows_valid, rows_pad, d, d_pad);
+    hipLaunchKernelGGL(layernorm_bwd_kernel, dim3(grid_for(rows_pad, 4, 1 << 30)), dim3(256), 0, u2gnn_stream(stream),
+                       dY, ldy, Z, ldz, mean, rstd, gamma, dZ, lddz, dZdrop, lddrop, p, seed, rows_valid, rows_pad, d,
+                       d_pad);
     return u2gnn_launch_status();
 }
 
-int u2gnn_layernorm_param_reduce(const float *part, int64_t n_blocks, int64_t d, int64_t d_pad, float *dgamma,
-                                 float *dbeta, int32_t accumulate, void *stream) {
-    if (!part || !dgamma || !dbeta) return U2GNN_E_ARG;
-    hipLaunchKernelGGL(ln_param_reduce_kernel, dim3(grid_for(d, 256, 1 << 30)), dim3(256), 0, u2gnn_stream(stream),
-                       part, n_blocks, d, d_pad, dgamma, dbeta, accumulate);
+int u2gnn_layernorm_bwd_params(const float *dY, int64_t ldy, const float *Z, int64_t ldz, const float *mean,
+                               const float *rstd, const float *dZdrop, int64_t lddrop, int64_t rows_valid, int64_t d,
+                               int64_t d_pad, float *ws, float *dgamma, float *dbeta, float *dbias, void *stream) {
+    if (!dY || !Z || !mean || !rstd || !ws || !dgamma || !dbeta || d < 1 || d > d_pad) return U2GNN_E_ARG;
+    if (dbias && !dZdrop) return U2GNN_E_ARG;
+    const int64_t chunks = rows_valid > 0 ? (rows_valid + CS_ROWS - 1) / CS_ROWS : 1;
+    hipStream_t st = u2gnn_stream(stream);
+    hipLaunchKernelGGL(ln_colstats_kernel, dim3((unsigned)((d + 63) / 64), (unsigned)chunks), dim3(256), 0, st, dY,
+                       ldy, Z, ldz, mean, rstd, dbias ? dZdrop : nullptr, lddrop, rows_valid, d, d_pad, ws);
+    hipLaunchKernelGGL(ln_param_reduce_kernel, dim3(grid_for(d, 256, 1 << 30)), dim3(256), 0, st, ws, chunks, d, d_pad,
+                       dgamma, dbeta, dbias);
     return u2gnn_launch_status();
 }
 

@@ -12,26 +12,45 @@ namespace {
 __global__ void __launch_bounds__(256) pool_fwd_kernel(const float *X, int64_t ldx, const int64_t *rowptr,
                                                        const int64_t *colidx, const float *vals, float *G, int64_t ldg,
                                                        int64_t d, float p, uint64_t seed) {
+    // block = one graph; the 4 waves split the graph's rows, lanes cover 64 columns at a time
+    __shared__ float red[4][64];
     const int64_t b = blockIdx.x;
-    const int64_t c = (int64_t)blockIdx.y * 256 + threadIdx.x;
-    if (c >= d) return;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int64_t e0 = rowptr[b], e1 = rowptr[b + 1];
-    float s = 0.f;
-    for (int64_t e = e0; e < e1; ++e) s += vals[e] * X[colidx[e] * ldx + c];
-    if (p > 0.f) s = u2gnn_keep(seed, (uint32_t)b, (uint32_t)c, p) ? s * (1.f / (1.f - p)) : 0.f;
-    G[b * ldg + c] = s;
+    for (int64_t c0 = 0; c0 < d; c0 += 64) {
+        const int64_t c = c0 + lane;
+        float s[4] = {0.f, 0.f, 0.f, 0.f};
+        if (c < d) {
+            int64_t e = e0 + w;
+            for (; e + 12 < e1; e += 16)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) s[j] += vals[e + 4 * j] * X[colidx[e + 4 * j] * ldx + c];
+            for (; e < e1; e += 4) s[0] += vals[e] * X[colidx[e] * ldx + c];
+        }
+        red[w][lane] = (s[0] + s[1]) + (s[2] + s[3]);
+        __syncthreads();
+        if (w == 0 && c < d) {
+            float v = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+            if (p > 0.f) v = u2gnn_keep(seed, (uint32_t)b, (uint32_t)c, p) ? v * (1.f / (1.f - p)) : 0.f;
+            G[b * ldg + c] = v;
+        }
+        __syncthreads();
+    }
 }
 
 __global__ void __launch_bounds__(256) pool_bwd_kernel(const float *dGd, int64_t ldg, const int64_t *rowptr,
                                                        const int64_t *colidx, const float *vals, float *dX,
                                                        int64_t ldx, int64_t d, float p, uint64_t seed) {
+    // block = (graph, 4-row slice); lanes over columns; one atomic per (row, column)
     const int64_t b = blockIdx.x;
-    const int64_t c = (int64_t)blockIdx.y * 256 + threadIdx.x;
-    if (c >= d) return;
-    float g = dGd[b * ldg + c];
-    if (p > 0.f) g = u2gnn_keep(seed, (uint32_t)b, (uint32_t)c, p) ? g * (1.f / (1.f - p)) : 0.f;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int64_t e0 = rowptr[b], e1 = rowptr[b + 1];
-    for (int64_t e = e0; e < e1; ++e) atomicAdd(dX + colidx[e] * ldx + c, vals[e] * g);
+    for (int64_t c = lane; c < d; c += 64) {
+        float g = dGd[b * ldg + c];
+        if (p > 0.f) g = u2gnn_keep(seed, (uint32_t)b, (uint32_t)c, p) ? g * (1.f / (1.f - p)) : 0.f;
+        for (int64_t e = e0 + (int64_t)blockIdx.y * 4 + w; e < e1; e += (int64_t)gridDim.y * 4)
+            atomicAdd(dX + colidx[e] * ldx + c, vals[e] * g);
+    }
 }
 
 // head: scores[b, k] (+)= G[b,:] . W[k,:] + bias[k];  one wave per (b, k)
@@ -47,27 +66,31 @@ __global__ void __launch_bounds__(256) head_fwd_kernel(const float *G, int64_t l
     if (lane == 0) scores[o] = (accumulate ? scores[o] : 0.f) + s + bias[k];
 }
 
-// head backward: thread per feature j computes dG[:, j] and dW[:, j]; block 0 also db.
+// head backward, one thread per output element: dG[b, j] (B*d), dW[k, j] (C*d), db[k] (C)
 __global__ void __launch_bounds__(256) head_bwd_kernel(const float *dS, const float *G, int64_t ldg, const float *W,
                                                        float *dG, int64_t lddg, float *dW, float *db, int64_t B,
                                                        int64_t C, int64_t d, int accumulate) {
-    const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (j < d) {
-        for (int64_t b = 0; b < B; ++b) {
-            float s = 0.f;
-            for (int64_t k = 0; k < C; ++k) s += dS[b * C + k] * W[k * d + j];
-            dG[b * lddg + j] = s;
-        }
-        for (int64_t k = 0; k < C; ++k) {
-            float s = 0.f;
-            for (int64_t b = 0; b < B; ++b) s += dS[b * C + k] * G[b * ldg + j];
-            dW[k * d + j] = accumulate ? dW[k * d + j] + s : s;
-        }
-    }
-    if (blockIdx.x == 0 && threadIdx.x < C) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t < B * d) {
+        const int64_t b = t / d, j = t - b * d;
         float s = 0.f;
-        for (int64_t b = 0; b < B; ++b) s += dS[b * C + threadIdx.x];
-        db[threadIdx.x] = accumulate ? db[threadIdx.x] + s : s;
+        for (int64_t k = 0; k < C; ++k) s += dS[b * C + k] * W[k * d + j];
+        dG[b * lddg + j] = s;
+    } else if (t < B * d + C * d) {
+        const int64_t u = t - B * d, k = u / d, j = u - k * d;
+        float s[4] = {0.f, 0.f, 0.f, 0.f};
+        int64_t b = 0;
+        for (; b + 4 <= B; b += 4)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) s[q] += dS[(b + q) * C + k] * G[(b + q) * ldg + j];
+        for (; b < B; ++b) s[0] += dS[b * C + k] * G[b * ldg + j];
+        const float v = (s[0] + s[1]) + (s[2] + s[3]);
+        dW[k * d + j] = accumulate ? dW[k * d + j] + v : v;
+    } else if (t < B * d + C * d + C) {
+        const int64_t k = t - B * d - C * d;
+        float s = 0.f;
+        for (int64_t b = 0; b < B; ++b) s += dS[b * C + k];
+        db[k] = accumulate ? db[k] + s : s;
     }
 }
 
@@ -248,7 +271,7 @@ extern "C" {
 int u2gnn_pool_fwd(const float *X, int64_t ldx, const int64_t *rowptr, const int64_t *colidx, const float *vals,
                    float *G, int64_t ldg, int64_t B, int64_t d, float p, uint64_t seed, void *stream) {
     if (!X || !rowptr || !colidx || !vals || !G || B < 1 || d < 1) return U2GNN_E_ARG;
-    hipLaunchKernelGGL(pool_fwd_kernel, dim3((unsigned)B, (unsigned)((d + 255) / 256)), dim3(256), 0,
+    hipLaunchKernelGGL(pool_fwd_kernel, dim3((unsigned)B), dim3(256), 0,
                        u2gnn_stream(stream), X, ldx, rowptr, colidx, vals, G, ldg, d, p, seed);
     return u2gnn_launch_status();
 }
@@ -256,7 +279,7 @@ int u2gnn_pool_fwd(const float *X, int64_t ldx, const int64_t *rowptr, const int
 int u2gnn_pool_bwd(const float *dGd, int64_t ldg, const int64_t *rowptr, const int64_t *colidx, const float *vals,
                    float *dX, int64_t ldx, int64_t B, int64_t d, float p, uint64_t seed, void *stream) {
     if (!dGd || !rowptr || !colidx || !vals || !dX || B < 1 || d < 1) return U2GNN_E_ARG;
-    hipLaunchKernelGGL(pool_bwd_kernel, dim3((unsigned)B, (unsigned)((d + 255) / 256)), dim3(256), 0,
+    hipLaunchKernelGGL(pool_bwd_kernel, dim3((unsigned)B, 8), dim3(256), 0,
                        u2gnn_stream(stream), dGd, ldg, rowptr, colidx, vals, dX, ldx, d, p, seed);
     return u2gnn_launch_status();
 }
@@ -271,8 +294,8 @@ int u2gnn_head_fwd(const float *G, int64_t ldg, const float *W, const float *bia
 
 int u2gnn_head_bwd(const float *dscores, const float *G, int64_t ldg, const float *W, float *dG, int64_t lddg,
                    float *dW, float *db, int64_t B, int64_t C, int64_t d, int32_t accumulate, void *stream) {
-    if (!dscores || !G || !W || !dG || !dW || !db || C > 256) return U2GNN_E_ARG;
-    hipLaunchKernelGGL(head_bwd_kernel, dim3(grid_for(d, 256, 1 << 30)), dim3(256), 0, u2gnn_stream(stream), dscores,
+    if (!dscores || !G || !W || !dG || !dW || !db) return U2GNN_E_ARG;
+    hipLaunchKernelGGL(head_bwd_kernel, dim3(grid_for(B * d + C * d + C, 256, 1 << 30)), dim3(256), 0, u2gnn_stream(stream), dscores,
                        G, ldg, W, dG, lddg, dW, db, B, C, d, accumulate);
     return u2gnn_launch_status();
 }

@@ -50,6 +50,12 @@ class GemmArgs(ctypes.Structure):
     ]
 
 
+class PackDesc(ctypes.Structure):
+    _fields_ = [("src", c_void_p), ("dst", c_void_p), ("ld_src", c_int64), ("rows_pad", c_int64),
+                ("cols_pad", c_int64), ("rblk_pad", c_int64), ("rblk_real", c_int64), ("cblk_pad", c_int64),
+                ("cblk_real", c_int64), ("ld_dst", c_int64)]
+
+
 I64, F32, VP, I32 = c_int64, c_float, c_void_p, c_int32
 
 _HIP_SIGS = {
@@ -63,9 +69,10 @@ _HIP_SIGS = {
     "u2gnn_attn_softmax_fwd": ([VP, I64, VP, VP, I64, I64, I64, I64, I64, F32, c_uint64, VP], c_int32),
     "u2gnn_rowdot": ([VP, I64, VP, I64, VP, I64, I64, VP], c_int32),
     "u2gnn_layernorm_fwd": ([VP, I64, VP, VP, VP, I64, VP, VP, I64, I64, I64, I64, F32, VP], c_int32),
-    "u2gnn_layernorm_bwd": ([VP, I64, VP, I64, VP, VP, VP, VP, I64, VP, I64, F32, c_uint64, VP, I64, I64, I64, I64,
-                             VP], c_int32),
-    "u2gnn_layernorm_param_reduce": ([VP, I64, I64, I64, VP, VP, I32, VP], c_int32),
+    "u2gnn_layernorm_bwd": ([VP, I64, VP, I64, VP, VP, VP, VP, I64, VP, I64, F32, c_uint64, I64, I64, I64, I64, VP],
+                            c_int32),
+    "u2gnn_layernorm_bwd_params": ([VP, I64, VP, I64, VP, VP, VP, I64, I64, I64, I64, VP, VP, VP, VP, VP], c_int32),
+    "u2gnn_pack_padded_multi": ([VP, I32, VP], c_int32),
     "u2gnn_pool_fwd": ([VP, I64, VP, VP, VP, VP, I64, I64, I64, F32, c_uint64, VP], c_int32),
     "u2gnn_pool_bwd": ([VP, I64, VP, VP, VP, VP, I64, I64, I64, F32, c_uint64, VP], c_int32),
     "u2gnn_head_fwd": ([VP, I64, VP, VP, VP, I64, I64, I64, I32, VP], c_int32),

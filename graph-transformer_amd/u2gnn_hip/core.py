@@ -81,9 +81,11 @@ class EncoderStack:
     def _pack(self, device):
         if self.packed is None:
             self.packed = [[PackedLayer(self.d, self.ff, device) for _ in range(self.T)] for _ in range(self.L)]
+        jobs = []
         for l in range(self.L):
             for t in range(self.T):
-                self.packed[l][t].pack(self.layer_params(l, t))
+                jobs += self.packed[l][t].jobs(self.layer_params(l, t))
+        K.pack_padded_multi(jobs)      # one launch per 32 tensors
 
     def forward(self, b: "DeviceBatch", train: bool, need_ctx: bool, seed: int):
         """Returns (outs, ctx): outs[l] = padded [Np, dp] slot-0 output of U2GNN layer l."""

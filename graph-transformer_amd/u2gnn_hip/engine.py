@@ -111,16 +111,20 @@ class PackedLayer:
         self.W1, self.b1 = z(ffp, dp), z(ffp)
         self.W2, self.b2 = z(dp, ffp), z(dp)
 
-    def pack(self, p: LayerParams):
+    def jobs(self, p: LayerParams):
+        """pack_padded_multi jobs refreshing the padded copies from the real parameters."""
         d, ff, dp, ffp = self.d, self.ff, self.dp, self.ffp
-        K.pack_padded(p.in_w, d, 3 * dp, dp, (dp, d), (dp, d), self.W_in, dp)
-        K.pack_padded(p.in_b, 3 * d, 1, 3 * dp, (1, 1), (dp, d), self.b_in, 3 * dp)
-        K.pack_padded(p.out_w, d, dp, dp, (dp, d), (dp, d), self.W_o, dp)
-        K.pack_padded(p.out_b, d, 1, dp, (1, 1), (dp, d), self.b_o, dp)
-        K.pack_padded(p.l1_w, d, ffp, dp, (ffp, ff), (dp, d), self.W1, dp)
-        K.pack_padded(p.l1_b, ff, 1, ffp, (1, 1), (ffp, ff), self.b1, ffp)
-        K.pack_padded(p.l2_w, ff, dp, ffp, (dp, d), (ffp, ff), self.W2, ffp)
-        K.pack_padded(p.l2_b, d, 1, dp, (1, 1), (dp, d), self.b2, dp)
+        return [(p.in_w, d, 3 * dp, dp, (dp, d), (dp, d), self.W_in, dp),
+                (p.in_b, 3 * d, 1, 3 * dp, (1, 1), (dp, d), self.b_in, 3 * dp),
+                (p.out_w, d, dp, dp, (dp, d), (dp, d), self.W_o, dp),
+                (p.out_b, d, 1, dp, (1, 1), (dp, d), self.b_o, dp),
+                (p.l1_w, d, ffp, dp, (ffp, ff), (dp, d), self.W1, dp),
+                (p.l1_b, ff, 1, ffp, (1, 1), (ffp, ff), self.b1, ffp),
+                (p.l2_w, ff, dp, ffp, (dp, d), (ffp, ff), self.W2, ffp),
+                (p.l2_b, d, 1, dp, (1, 1), (dp, d), self.b2, dp)]
+
+    def pack(self, p: LayerParams):
+        K.pack_padded_multi(self.jobs(p))
 
 
 class GemmTimer:
@@ -163,8 +167,26 @@ def _wgrad(dY, ld_dy, X, ld_x, m_pad, n_pad, rows_pad, dst, rblk, cblk, prec):
 
 
 def _bias_grad(dY, rows, cols_pad, ld, cblk, out):
-    ws = torch.empty((rows + 255) // 256 * cols_pad, device=dY.device, dtype=torch.float32)
+    ws = torch.empty(K.colstat_ws_floats(rows, cols_pad), device=dY.device, dtype=torch.float32)
     K.colsum(dY, rows, cols_pad, ld, cblk, out, ws)
+
+
+def _gemm_nodes_k(A, B, C, M, N, Kd, lda, ldb, ldc, trans_a=False, alpha=1.0, prec="fp32"):
+    """C[M, N] = alpha * op(A) . B for the skinny attention products whose depth is the node
+    dimension (P.V, Pd^T.dO, dS.K, dS^T.Q: N = dp, K = Np).  A 128x128 tile grid has only
+    (Np/128)*(dp/128) ~ 114 workgroups for 256 CUs, so the depth is split into deterministic fp32
+    slabs (>= ~1.5 workgroups per CU), reduced (and scaled by alpha) by one streaming pass."""
+    tiles = (M // 128) * (N // 128) if (M % 128 == 0 and N % 128 == 0) else 0
+    if tiles == 0 or tiles >= 384:
+        K.gemm(A, B, C, M, N, Kd, lda, ldb, ldc, trans_a=trans_a, alpha=alpha, precision=prec)
+        return
+    split = 1
+    while split < 8 and tiles * split < 400 and Kd % (16 * split * 2) == 0:
+        split *= 2
+    slabs = torch.empty(split, M, N, device=C.device, dtype=torch.float32)
+    K.gemm(A, B, slabs, M, N, Kd, lda, ldb, N, trans_a=trans_a, split_k=split, slab_stride=M * N, precision=prec,
+           tile=128)
+    K.slab_reduce(slabs, split, M * N, M, N, N, (M, M), (N, N), C, ldc, alpha=alpha)
 
 
 def encoder_layer_forward(X: torch.Tensor, w: PackedLayer, p: LayerParams, dims: Dims, train: bool,
@@ -189,7 +211,7 @@ def encoder_layer_forward(X: torch.Tensor, w: PackedLayer, p: LayerParams, dims:
     del S
     O = torch.empty(Np, dp, device=dev, dtype=f32)
     TIMER.wrap("pv", 2.0 * N * N * d,
-               lambda: K.gemm(Pd, V, O, Np, dp, Np, Np, 3 * dp, dp, precision=prec))
+               lambda: _gemm_nodes_k(Pd, V, O, Np, dp, Np, Np, 3 * dp, dp, prec=prec))
     Z1 = torch.empty(Np, dp, device=dev, dtype=f32)
     K.gemm(O, w.W_o, Z1, Np, dp, dp, dp, dp, dp, trans_b=True, epilogue=E.EPI_BIAS_DROP_RESID, bias=w.b_o,
            aux0=X, ld_aux=dp, p_drop=pd, seed=seeds.get(SITE_DROP1, 0), precision=prec)
@@ -225,20 +247,18 @@ def encoder_layer_backward(dX2: torch.Tensor, ctx: EncoderLayerCtx, w: PackedLay
     pd, seeds = ctx.seeds
     dev = dX2.device
     f32 = torch.float32
-    nblk = K.ln_part_blocks(Np)
-    part = torch.empty(nblk, 2 * dp, device=dev, dtype=f32)
-    # LN2 backward -> dX1 (residual branch), dF (dropout2 branch)
+    ws = torch.empty(K.colstat_ws_floats(N, dp), device=dev, dtype=f32)
+    # LN2 backward -> dX1 (residual branch), dF (dropout2 branch); norm2 + linear2.bias grads
     dX1 = torch.empty(Np, dp, device=dev, dtype=f32)
     dF = torch.empty(Np, dp, device=dev, dtype=f32)
     K.layernorm_bwd(dX2, dp, ctx.Z2, dp, ctx.mean2, ctx.rstd2, p.n2_w, dX1, dp, dF, dp, pd,
-                    seeds.get(SITE_DROP2, 0), part, N, Np, d, dp)
-    K.layernorm_param_reduce(part, nblk, d, dp, g.n2_w, g.n2_b)
+                    seeds.get(SITE_DROP2, 0), N, Np, d, dp)
+    K.layernorm_bwd_params(dX2, dp, ctx.Z2, dp, ctx.mean2, ctx.rstd2, dF, dp, N, d, dp, ws, g.n2_w, g.n2_b, g.l2_b)
     # FFN: Z2 = X1 + drop(Hd W2^T + b2), Hd = drop(relu(X1 W1^T + b1))
     dH = torch.empty(Np, ffp, device=dev, dtype=f32)
     K.gemm(dF, w.W2, dH, Np, ffp, dp, dp, ffp, ffp, epilogue=E.EPI_RELU_DROP_BWD, aux0=ctx.Hd, ld_aux=ffp,
            p_drop=pd, precision=prec)
     _wgrad(dF, dp, ctx.Hd, ffp, dp, ffp, Np, g.l2_w, (dp, d), (ffp, ff), prec)
-    _bias_grad(dF, Np, dp, dp, (dp, d), g.l2_b)
     K.gemm(dH, w.W1, dX1, Np, dp, ffp, ffp, dp, dp, epilogue=E.EPI_ACCUM, precision=prec)
     _wgrad(dH, ffp, ctx.X1, dp, ffp, dp, Np, g.l1_w, (ffp, ff), (dp, d), prec)
     _bias_grad(dH, Np, ffp, ffp, (ffp, ff), g.l1_b)
@@ -247,14 +267,13 @@ def encoder_layer_backward(dX2: torch.Tensor, ctx: EncoderLayerCtx, w: PackedLay
     dX = torch.empty(Np, dp, device=dev, dtype=f32)
     dA = torch.empty(Np, dp, device=dev, dtype=f32)
     K.layernorm_bwd(dX1, dp, ctx.Z1, dp, ctx.mean1, ctx.rstd1, p.n1_w, dX, dp, dA, dp, pd,
-                    seeds.get(SITE_DROP1, 0), part, N, Np, d, dp)
-    K.layernorm_param_reduce(part, nblk, d, dp, g.n1_w, g.n1_b)
+                    seeds.get(SITE_DROP1, 0), N, Np, d, dp)
+    K.layernorm_bwd_params(dX1, dp, ctx.Z1, dp, ctx.mean1, ctx.rstd1, dA, dp, N, d, dp, ws, g.n1_w, g.n1_b, g.out_b)
     del dX1
     # out-projection
     dO = torch.empty(Np, dp, device=dev, dtype=f32)
     K.gemm(dA, w.W_o, dO, Np, dp, dp, dp, dp, dp, precision=prec)
     _wgrad(dA, dp, ctx.O, dp, dp, dp, Np, g.out_w, (dp, d), (dp, d), prec)
-    _bias_grad(dA, Np, dp, dp, (dp, d), g.out_b)
     del dA
     # attention core
     QKV = ctx.QKV
@@ -267,14 +286,14 @@ def encoder_layer_backward(dX2: torch.Tensor, ctx: EncoderLayerCtx, w: PackedLay
                               aux0=ctx.P, aux1=ctx.Pd, rowvec=delta, ld_aux=Np, precision=prec))
     dQKV = torch.empty(Np, 3 * dp, device=dev, dtype=f32)
     TIMER.wrap("dv", 2.0 * N * N * d,
-               lambda: K.gemm(ctx.Pd, dO, dQKV[:, 2 * dp:], Np, dp, Np, Np, dp, 3 * dp, trans_a=True,
-                              precision=prec))
+               lambda: _gemm_nodes_k(ctx.Pd, dO, dQKV[:, 2 * dp:], Np, dp, Np, Np, dp, 3 * dp, trans_a=True,
+                                     prec=prec))
     TIMER.wrap("dq", 2.0 * N * N * d,
-               lambda: K.gemm(dS, Kt, dQKV[:, :dp], Np, dp, Np, Np, 3 * dp, 3 * dp, alpha=1.0 / math.sqrt(d),
-                              precision=prec))
+               lambda: _gemm_nodes_k(dS, Kt, dQKV[:, :dp], Np, dp, Np, Np, 3 * dp, 3 * dp,
+                                     alpha=1.0 / math.sqrt(d), prec=prec))
     TIMER.wrap("dk", 2.0 * N * N * d,
-               lambda: K.gemm(dS, Q, dQKV[:, dp:2 * dp], Np, dp, Np, Np, 3 * dp, 3 * dp, trans_a=True,
-                              precision=prec))
+               lambda: _gemm_nodes_k(dS, Q, dQKV[:, dp:2 * dp], Np, dp, Np, Np, 3 * dp, 3 * dp, trans_a=True,
+                                     prec=prec))
     del dS, dO
     # in-projection
     K.gemm(dQKV, w.W_in, dX, Np, dp, 3 * dp, 3 * dp, dp, dp, epilogue=E.EPI_ACCUM, precision=prec)

@@ -111,26 +111,38 @@ def layernorm_fwd(Z, ldz, gamma, beta, Y, ldy, mean, rstd, rows_valid, rows_pad,
           "u2gnn_layernorm_fwd")
 
 
-LNB_ROWS = 32
+CS_ROWS = 128
 
 
-def ln_part_blocks(rows_pad):
-    return (rows_pad + LNB_ROWS - 1) // LNB_ROWS
+def colstat_ws_floats(rows, cols):
+    """Workspace of the two-pass column reductions (colsum, LN parameter gradients)."""
+    return max(1, (rows + CS_ROWS - 1) // CS_ROWS) * 3 * cols
 
 
-def layernorm_bwd(dY, ldy, Z, ldz, mean, rstd, gamma, dZ, lddz, dZdrop, lddrop, p, seed, part, rows_valid, rows_pad,
-                  d, d_pad):
-    _dev(dY, Z, mean, rstd, gamma, dZ, part)
+def layernorm_bwd(dY, ldy, Z, ldz, mean, rstd, gamma, dZ, lddz, dZdrop, lddrop, p, seed, rows_valid, rows_pad, d,
+                  d_pad):
+    _dev(dY, Z, mean, rstd, gamma, dZ)
     check(hip_lib().u2gnn_layernorm_bwd(_p(dY), int(ldy), _p(Z), int(ldz), _p(mean), _p(rstd), _p(gamma), _p(dZ),
-                                        int(lddz), _p(dZdrop), int(lddrop), float(p), int(seed), _p(part),
-                                        int(rows_valid), int(rows_pad), int(d), int(d_pad), _s()),
-          "u2gnn_layernorm_bwd")
+                                        int(lddz), _p(dZdrop), int(lddrop), float(p), int(seed), int(rows_valid),
+                                        int(rows_pad), int(d), int(d_pad), _s()), "u2gnn_layernorm_bwd")
 
 
-def layernorm_param_reduce(part, n_blocks, d, d_pad, dgamma, dbeta, accumulate=False):
-    _dev(part, dgamma, dbeta)
-    check(hip_lib().u2gnn_layernorm_param_reduce(_p(part), int(n_blocks), int(d), int(d_pad), _p(dgamma), _p(dbeta),
-                                                 int(accumulate), _s()), "u2gnn_layernorm_param_reduce")
+def layernorm_bwd_params(dY, ldy, Z, ldz, mean, rstd, dZdrop, lddrop, rows_valid, d, d_pad, ws, dgamma, dbeta,
+                         dbias=None):
+    _dev(dY, Z, mean, rstd, ws, dgamma, dbeta)
+    check(hip_lib().u2gnn_layernorm_bwd_params(_p(dY), int(ldy), _p(Z), int(ldz), _p(mean), _p(rstd), _p(dZdrop),
+                                               int(lddrop), int(rows_valid), int(d), int(d_pad), _p(ws), _p(dgamma),
+                                               _p(dbeta), _p(dbias), _s()), "u2gnn_layernorm_bwd_params")
+
+
+def pack_padded_multi(jobs):
+    """jobs: list of (src, ld_src, rows_pad, cols_pad, rblk, cblk, dst, ld_dst)."""
+    arr = (_lib.PackDesc * len(jobs))()
+    for i, (src, ld_src, rp, cp, rb, cb, dst, ld_dst) in enumerate(jobs):
+        _dev(src, dst)
+        arr[i] = _lib.PackDesc(src.data_ptr(), dst.data_ptr(), int(ld_src), int(rp), int(cp), int(rb[0]), int(rb[1]),
+                               int(cb[0]), int(cb[1]), int(ld_dst))
+    check(hip_lib().u2gnn_pack_padded_multi(arr, len(jobs), _s()), "u2gnn_pack_padded_multi")
 
 
 def pool_fwd(X, ldx, rowptr, colidx, vals, G, ldg, B, d, p, seed):

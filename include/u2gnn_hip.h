@@ -103,8 +103,17 @@ int u2gnn_pack_padded(const float *src, int64_t ld_src, int64_t rows_pad, int64_
                       int64_t rblk_pad, int64_t rblk_real, int64_t cblk_pad, int64_t cblk_real,
                       float *dst, int64_t ld_dst, void *stream);
 
+/* many u2gnn_pack_padded jobs in one launch (the descriptor array is a HOST array; up to 32 jobs
+ * per launch, more are split into several launches). */
+typedef struct u2gnn_pack_desc {
+    const float *src;
+    float *dst;
+    int64_t ld_src, rows_pad, cols_pad, rblk_pad, rblk_real, cblk_pad, cblk_real, ld_dst;
+} u2gnn_pack_desc;
+int u2gnn_pack_padded_multi(const u2gnn_pack_desc *descs, int32_t n, void *stream);
+
 /* column sums (bias gradients):  out[map(c)] (+)= sum_{r<rows} X[r*ld + c], c < cols_pad.
- * ws must hold ceil(rows/256) * cols_pad floats. */
+ * ws must hold ceil(rows/128) * cols_pad floats. */
 int u2gnn_colsum(const float *X, int64_t rows, int64_t cols_pad, int64_t ld, int64_t cblk_pad,
                  int64_t cblk_real, float *out, int32_t accumulate, float *ws, void *stream);
 
@@ -123,16 +132,20 @@ int u2gnn_rowdot(const float *A, int64_t lda, const float *B, int64_t ldb, float
 int u2gnn_layernorm_fwd(const float *Z, int64_t ldz, const float *gamma, const float *beta, float *Y,
                         int64_t ldy, float *mean, float *rstd, int64_t rows_valid, int64_t rows_pad,
                         int64_t d, int64_t d_pad, float eps, void *stream);
-/* dZ = LN'(dY); dZdrop = dZ * keep/(1-p) (may be NULL); per-block partial sums of
- * dY*xhat and dY written to part[blk*2*d_pad + c] / part[blk*2*d_pad + d_pad + c];
- * n_part_blocks = ceil(rows_pad / 32). */
+/* dZ = LN'(dY) (rows >= rows_valid and columns >= d written 0); dZdrop = dZ * keep/(1-p)
+ * (may be NULL): the gradient of the dropout branch that fed this LN's residual sum. */
 int u2gnn_layernorm_bwd(const float *dY, int64_t ldy, const float *Z, int64_t ldz, const float *mean,
                         const float *rstd, const float *gamma, float *dZ, int64_t lddz, float *dZdrop,
-                        int64_t lddrop, float p, uint64_t seed, float *part, int64_t rows_valid,
-                        int64_t rows_pad, int64_t d, int64_t d_pad, void *stream);
-/* dgamma[c] (+)= sum_blk part[blk][0][c]; dbeta[c] (+)= sum_blk part[blk][1][c], c < d */
-int u2gnn_layernorm_param_reduce(const float *part, int64_t n_blocks, int64_t d, int64_t d_pad,
-                                 float *dgamma, float *dbeta, int32_t accumulate, void *stream);
+                        int64_t lddrop, float p, uint64_t seed, int64_t rows_valid, int64_t rows_pad,
+                        int64_t d, int64_t d_pad, void *stream);
+/* LN parameter gradients: dgamma[c] = sum_r dY*xhat, dbeta[c] = sum_r dY (c < d) and, when
+ * dbias != NULL, dbias[c] = sum_r dZdrop[r, c] (bias of the linear whose output was dropped into
+ * the residual: out_proj.bias for norm1, linear2.bias for norm2).  Deterministic two-pass column
+ * reduction; ws >= ceil(rows_valid/128) * 3 * d_pad floats. */
+int u2gnn_layernorm_bwd_params(const float *dY, int64_t ldy, const float *Z, int64_t ldz,
+                               const float *mean, const float *rstd, const float *dZdrop,
+                               int64_t lddrop, int64_t rows_valid, int64_t d, int64_t d_pad, float *ws,
+                               float *dgamma, float *dbeta, float *dbias, void *stream);
 
 /* ---- a5/a6: sum pooling + dropout + per-layer head  (pytorch_U2GNN_Sup.py:41-44) ------
  * G[b, c] = drop(sum_{e in [rowptr[b], rowptr[b+1])} vals[e] * X[colidx[e], c]), c < d;

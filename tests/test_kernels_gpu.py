@@ -119,15 +119,15 @@ def test_layernorm_fwd_bwd():
     dY[:N, :d] = _mk(N, d, seed=14)
     ref.backward(dY[:N, :d])
     dZ, dZd = torch.empty(Np, dp, device=DEV), torch.empty(Np, dp, device=DEV)
-    nb = K.ln_part_blocks(Np)
-    part = torch.empty(nb, 2 * dp, device=DEV)
-    K.layernorm_bwd(dY, dp, Z, dp, mu, rs, gam, dZ, dp, dZd, dp, 0.5, 99, part, N, Np, d, dp)
-    dg, db = torch.empty(d, device=DEV), torch.empty(d, device=DEV)
-    K.layernorm_param_reduce(part, nb, d, dp, dg, db)
+    K.layernorm_bwd(dY, dp, Z, dp, mu, rs, gam, dZ, dp, dZd, dp, 0.5, 99, N, Np, d, dp)
+    dg, db, dbias = torch.empty(d, device=DEV), torch.empty(d, device=DEV), torch.empty(d, device=DEV)
+    ws = torch.empty(K.colstat_ws_floats(N, dp), device=DEV)
+    K.layernorm_bwd_params(dY, dp, Z, dp, mu, rs, dZd, dp, N, d, dp, ws, dg, db, dbias)
     assert rel_err(dZ[:N, :d], z.grad) < 1e-4
     mask = K.dropout_mask(99, Np, dp, 0.5).float()
     assert rel_err(dZd[:N, :d], z.grad * mask[:N, :d] * 2) < 1e-4
     assert rel_err(dg, g_.grad) < 1e-4 and rel_err(db, b_.grad) < 1e-4
+    assert rel_err(dbias, (z.grad * mask[:N, :d] * 2).sum(0)) < 1e-4
     assert dZ[N:].abs().max().item() == 0 and dZ[:, d:].abs().max().item() == 0
 
 
@@ -144,6 +144,12 @@ def test_gather_pack_colsum():
     K.pack_padded(W, 7, 3 * 64, 64, (64, 7), (64, 7), Wp, 64)
     for q in range(3):
         assert torch.equal(Wp[q * 64:q * 64 + 7, :7], W[q * 7:(q + 1) * 7])
+    Wm = torch.full_like(Wp, 3.0)
+    bsrc = _mk(21, seed=23)
+    bm = torch.full((3 * 64,), 5.0, device=DEV)
+    K.pack_padded_multi([(W, 7, 3 * 64, 64, (64, 7), (64, 7), Wm, 64), (bsrc, 21, 1, 3 * 64, (1, 1), (64, 7), bm, 192)])
+    assert torch.equal(Wm, Wp) and bm.view(3, 64)[:, 7:].abs().max() == 0
+    assert torch.equal(bm.view(3, 64)[:, :7].reshape(-1), bsrc)
     X = _mk(300, 192, seed=17)
     out = torch.empty(3 * 7, device=DEV)
     ws = torch.empty(2 * 192, device=DEV)
@@ -155,9 +161,9 @@ def test_gather_pack_colsum():
 def test_pool_head_ce():
     Np, d, dp, B, C = 128, 10, 64, 4, 3
     X = _mk(Np, dp, seed=18)
-    off = torch.tensor([0, 5, 9, 20, 31], device=DEV)
-    col = torch.arange(31, device=DEV)
-    vals = torch.ones(31, device=DEV)
+    off = torch.tensor([0, 5, 9, 70, 128], device=DEV)
+    col = torch.arange(128, device=DEV)
+    vals = torch.ones(128, device=DEV)
     G = torch.zeros(B, dp, device=DEV)
     K.pool_fwd(X, dp, off, col, vals, G, dp, B, d, 0.0, 0)
     ref = torch.stack([X[off[b]:off[b + 1], :d].sum(0) for b in range(B)])

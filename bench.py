@@ -28,7 +28,9 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 METRIC = "graphs/sec (fwd+bwd) U2GNN-Sup COLLAB k=16 T=4 at 1/2/4/8 MI355X"
-PEAK = {"fp32": 157.3}     # TFLOP/s dense matrix-core peak per dtype (MI355X_MICROARCH.md)
+PEAK = {"fp32": 157.3,     # TFLOP/s dense f32-input MFMA peak (MI355X_MICROARCH.md)
+        "bf16x3": 2500.0 / 3,  # 2.5 PF dense bf16 MFMA / 3 MFMAs per fp32-accurate product
+        "bf16": 2500.0}
 
 
 def parse():
@@ -41,7 +43,7 @@ def parse():
     ap.add_argument("--num-timesteps", type=int, default=4)
     ap.add_argument("--ff-hidden-size", type=int, default=1024)
     ap.add_argument("--num-hidden-layers", type=int, default=1)
-    ap.add_argument("--precision", default="fp32", choices=["fp32"])
+    ap.add_argument("--precision", default="bf16x3", choices=["fp32", "bf16x3", "bf16"])
     ap.add_argument("--lr", type=float, default=5e-4)
     ap.add_argument("--distinct-batches", type=int, default=8)
     ap.add_argument("--cpu-baseline", type=int, default=1, help="1 = time the CPU oracle on rank 0 at N=1")
@@ -162,7 +164,8 @@ def main():
         peak = PEAK[args.precision]
         roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
                 "frac": round(ach / peak, 4), "traffic": None,
-                "kernel": "gemm_f32_kernel on the attention products (Q.K^T, P.V, dO.V^T->dS, Pd^T.dO, dS.K, "
+                "kernel": ("gemm_f32_kernel" if args.precision == "fp32" else "gemm_bf16_kernel") +
+                          " on the attention products (Q.K^T, P.V, dO.V^T->dS, Pd^T.dO, dS.K, "
                           "dS^T.Q); algorithmic 2*N*N*d FLOP per launch, real N and d",
                 "launches": len(TIMER.records), "avg_launch_us": round(1e3 * ms / len(TIMER.records), 1),
                 "step_tflops_per_gpu": round(step_flops / (elapsed / args.steps) / 1e12, 2)}

@@ -227,13 +227,196 @@ __global__ void __launch_bounds__(256) gemm_f32_kernel(GemmP P) {
             }
 }
 
-template <int BM, int BN, bool TA, bool TB>
+// ------------------------------------------------------------------------------------
+// split-bf16 MFMA kernel (U2GNN_PREC_BF16X3) and plain bf16 (U2GNN_PREC_BF16)
+//
+// x = hi + lo with hi = bf16(x), lo = bf16(x - hi) (|x - hi - lo| <= 2^-17 |x|); the product is
+// hi*hi + hi*lo + lo*hi on v_mfma_f32_32x32x16_bf16 with fp32 accumulation, i.e. ~2^-16
+// relative error per product at 3 bf16 MFMAs (5.3x the fp32-MFMA rate).  fp32 operands are
+// split once per block while staging into LDS (register staging; the split is VALU work that
+// runs beside the matrix pipe), so HBM/L2 traffic is the fp32 operands themselves.
+// LDS holds both operands k-contiguous ([rows][BK+8] bf16: 80-byte rows make the
+// ds_read_b128 fragment reads conflict-free); [K][rows] layouts are transposed in registers
+// (4k x 4m micro-tiles) on the way in.
+// ------------------------------------------------------------------------------------
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+template <int R, int BK, bool T>
+__device__ __forceinline__ void g2r_bf(const float *base, int64_t ld, int kt, int tid, float4 (&v)[R * BK / 1024]) {
+    constexpr int NF = R * BK / 1024;
+    if constexpr (!T) {  // global [R][K]
+#pragma unroll
+        for (int i = 0; i < NF; ++i) {
+            const int idx = tid + i * 256;
+            const int r = idx / (BK / 4), kq = idx % (BK / 4);
+            v[i] = *reinterpret_cast<const float4 *>(base + (int64_t)r * ld + kt * BK + kq * 4);
+        }
+    } else {  // global [K][R]: NF k-rows x 4 columns per thread
+        const int mg = tid % (R / 4), kg = tid / (R / 4);
+#pragma unroll
+        for (int q = 0; q < NF; ++q)
+            v[q] = *reinterpret_cast<const float4 *>(base + (int64_t)(kt * BK + kg * NF + q) * ld + mg * 4);
+    }
+}
+
+template <int R, int BK, int LDK, bool T, bool SPLIT>
+__device__ __forceinline__ void r2s_bf(__bf16 *hi, __bf16 *lo, int tid, const float4 (&v)[R * BK / 1024]) {
+    constexpr int NF = R * BK / 1024;
+    if constexpr (!T) {
+#pragma unroll
+        for (int i = 0; i < NF; ++i) {
+            const int idx = tid + i * 256;
+            const int r = idx / (BK / 4), kq = idx % (BK / 4);
+            const float x[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+            bf16x4 h, l;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                h[c] = (__bf16)x[c];
+                l[c] = (__bf16)(x[c] - (float)h[c]);
+            }
+            *reinterpret_cast<bf16x4 *>(hi + r * LDK + kq * 4) = h;
+            if constexpr (SPLIT) *reinterpret_cast<bf16x4 *>(lo + r * LDK + kq * 4) = l;
+        }
+    } else {
+        const int mg = tid % (R / 4), kg = tid / (R / 4);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            float x[NF];
+#pragma unroll
+            for (int q = 0; q < NF; ++q) x[q] = c == 0 ? v[q].x : c == 1 ? v[q].y : c == 2 ? v[q].z : v[q].w;
+            __bf16 *dh = hi + (mg * 4 + c) * LDK + kg * NF;
+            __bf16 *dl = lo + (mg * 4 + c) * LDK + kg * NF;
+            if constexpr (NF == 4) {
+                bf16x4 h, l;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    h[q] = (__bf16)x[q];
+                    l[q] = (__bf16)(x[q] - (float)h[q]);
+                }
+                *reinterpret_cast<bf16x4 *>(dh) = h;
+                if constexpr (SPLIT) *reinterpret_cast<bf16x4 *>(dl) = l;
+            } else {
+                static_assert(NF == 2, "bf16 staging supports 64- and 128-row tiles");
+                bf16x2 h, l;
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    h[q] = (__bf16)x[q];
+                    l[q] = (__bf16)(x[q] - (float)h[q]);
+                }
+                *reinterpret_cast<bf16x2 *>(dh) = h;
+                if constexpr (SPLIT) *reinterpret_cast<bf16x2 *>(dl) = l;
+            }
+        }
+    }
+}
+
+template <int BM, int BN, bool TA, bool TB, int EPI, bool SPLIT>
+__global__ void __launch_bounds__(256) gemm_bf16_kernel(GemmP P) {
+    constexpr int BK = 32;
+    constexpr int LDK = BK + 8;
+    constexpr int WTM = BM / 2, WTN = BN / 2;
+    constexpr int TM = WTM / 32, TN = WTN / 32;
+    constexpr int NFA = BM * BK / 1024, NFB = BN * BK / 1024;
+    constexpr int AE = BM * LDK, BE = BN * LDK;
+    constexpr int STAGE = 2 * (AE + BE);  // hi + lo of A and B
+    __shared__ __attribute__((aligned(16))) __bf16 smem[2 * STAGE];
+
+    const int tid = threadIdx.x;
+    int tmi, tni;
+    tile_coords(P.gm, P.gn, tmi, tni);
+    const int m0 = tmi * BM, n0 = tni * BN;
+    const int64_t kbase = (int64_t)blockIdx.z * P.K;
+    const float *Ab = TA ? P.A + kbase * P.lda + m0 : P.A + (int64_t)m0 * P.lda + kbase;
+    const float *Bb = TB ? P.B + (int64_t)n0 * P.ldb + kbase : P.B + kbase * P.ldb + n0;
+
+    float4 ra[NFA], rb[NFB];
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    const int wave = tid >> 6, lane = tid & 63;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int kh = lane >> 5, li = lane & 31;
+    const int nk = P.K / BK;
+
+    auto stage = [&](int s) { return smem + s * STAGE; };
+    g2r_bf<BM, BK, TA>(Ab, P.lda, 0, tid, ra);
+    g2r_bf<BN, BK, !TB>(Bb, P.ldb, 0, tid, rb);
+    r2s_bf<BM, BK, LDK, TA, SPLIT>(stage(0), stage(0) + AE, tid, ra);
+    r2s_bf<BN, BK, LDK, !TB, SPLIT>(stage(0) + 2 * AE, stage(0) + 2 * AE + BE, tid, rb);
+    __syncthreads();
+    for (int t = 0; t < nk; ++t) {
+        const int tn = min(t + 1, nk - 1);
+        g2r_bf<BM, BK, TA>(Ab, P.lda, tn, tid, ra);
+        g2r_bf<BN, BK, !TB>(Bb, P.ldb, tn, tid, rb);
+        const __bf16 *Ah = stage(t & 1), *Al = Ah + AE, *Bh = Ah + 2 * AE, *Bl = Bh + BE;
+#pragma unroll
+        for (int ks = 0; ks < BK / 16; ++ks) {
+            bf16x8 ah[TM], al[TM], bh[TN], bl[TN];
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                const int o = (wm * WTM + i * 32 + li) * LDK + ks * 16 + kh * 8;
+                ah[i] = *reinterpret_cast<const bf16x8 *>(Ah + o);
+                if constexpr (SPLIT) al[i] = *reinterpret_cast<const bf16x8 *>(Al + o);
+            }
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const int o = (wn * WTN + j * 32 + li) * LDK + ks * 16 + kh * 8;
+                bh[j] = *reinterpret_cast<const bf16x8 *>(Bh + o);
+                if constexpr (SPLIT) bl[j] = *reinterpret_cast<const bf16x8 *>(Bl + o);
+            }
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    if constexpr (SPLIT) {
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+                    }
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+                }
+        }
+        __bf16 *ns = stage((t + 1) & 1);
+        r2s_bf<BM, BK, LDK, TA, SPLIT>(ns, ns + AE, tid, ra);
+        r2s_bf<BN, BK, LDK, !TB, SPLIT>(ns + 2 * AE, ns + 2 * AE + BE, tid, rb);
+        __syncthreads();
+    }
+
+    float *C = P.C + (int64_t)blockIdx.z * P.slab_stride;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = m0 + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
+                const int col = n0 + wn * WTN + j * 32 + li;
+                C[(int64_t)row * P.ldc + col] = epilogue<EPI>(P, row, col, acc[i][j][r]);
+            }
+}
+
+template <int KIND, int BM, int BN, bool TA, bool TB, int EPI>
+void launch_kernel(const GemmP &P, dim3 grid, hipStream_t st) {
+    if constexpr (KIND == U2GNN_PREC_F32)
+        hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, TA, TB, EPI>), grid, dim3(256), 0, st, P);
+    else
+        hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, TA, TB, EPI, KIND == U2GNN_PREC_BF16X3>), grid, dim3(256), 0, st,
+                           P);
+}
+
+template <int KIND, int BM, int BN, bool TA, bool TB>
 int launch_epi(const GemmP &P, int epi, int split, hipStream_t st) {
-    dim3 grid(P.gm * P.gn, 1, split), block(256);
+    dim3 grid(P.gm * P.gn, 1, split);
     switch (epi) {
-#define U2GNN_CASE(E)                                                                 \
-    case E:                                                                           \
-        hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, TA, TB, E>), grid, block, 0, st, P); \
+#define U2GNN_CASE(E)                                          \
+    case E:                                                    \
+        launch_kernel<KIND, BM, BN, TA, TB, E>(P, grid, st);   \
         break;
         U2GNN_CASE(U2GNN_EPI_STORE)
         U2GNN_CASE(U2GNN_EPI_BIAS)
@@ -249,12 +432,18 @@ int launch_epi(const GemmP &P, int epi, int split, hipStream_t st) {
     return u2gnn_launch_status();
 }
 
-template <int BM, int BN>
+template <int KIND, int BM, int BN>
 int launch_layout(const GemmP &P, bool ta, bool tb, int epi, int split, hipStream_t st) {
-    if (!ta && tb) return launch_epi<BM, BN, false, true>(P, epi, split, st);
-    if (!ta && !tb) return launch_epi<BM, BN, false, false>(P, epi, split, st);
-    if (ta && !tb) return launch_epi<BM, BN, true, false>(P, epi, split, st);
+    if (!ta && tb) return launch_epi<KIND, BM, BN, false, true>(P, epi, split, st);
+    if (!ta && !tb) return launch_epi<KIND, BM, BN, false, false>(P, epi, split, st);
+    if (ta && !tb) return launch_epi<KIND, BM, BN, true, false>(P, epi, split, st);
     return U2GNN_E_ARG;  // A^T B^T is never needed by the encoder
+}
+
+template <int KIND>
+int launch_tile(const GemmP &P, int tile, bool ta, bool tb, int epi, int split, hipStream_t st) {
+    if (tile == 128) return launch_layout<KIND, 128, 128>(P, ta, tb, epi, split, st);
+    return launch_layout<KIND, 64, 64>(P, ta, tb, epi, split, st);
 }
 
 inline bool al16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
@@ -265,11 +454,13 @@ extern "C" int u2gnn_gemm(const u2gnn_gemm_args *a, void *stream) {
     if (!a || !a->A || !a->B || !a->C) return U2GNN_E_ARG;
     if (a->M <= 0 || a->N <= 0 || a->K <= 0) return U2GNN_E_ARG;
     if (a->epilogue < 0 || a->epilogue > U2GNN_EPI_ATTN_DS) return U2GNN_E_ARG;
-    if (a->precision != U2GNN_PREC_F32) return U2GNN_E_ARG;
+    const int prec = a->precision;
+    if (prec != U2GNN_PREC_F32 && prec != U2GNN_PREC_BF16X3 && prec != U2GNN_PREC_BF16) return U2GNN_E_ARG;
     const int split = a->split_k < 1 ? 1 : a->split_k;
     if (split > 1 && a->epilogue != U2GNN_EPI_STORE) return U2GNN_E_ARG;
     if (!al16(a->A) || !al16(a->B) || (a->lda & 3) || (a->ldb & 3)) return U2GNN_E_ALIGN;
-    if (a->K % (16 * split)) return U2GNN_E_SHAPE;
+    const int bk = prec == U2GNN_PREC_F32 ? 16 : 32;
+    if (a->K % (bk * split)) return U2GNN_E_SHAPE;
     const int e = a->epilogue;
     if ((e == U2GNN_EPI_BIAS || e == U2GNN_EPI_BIAS_DROP_RESID || e == U2GNN_EPI_BIAS_RELU_DROP) && !a->bias)
         return U2GNN_E_ARG;
@@ -307,6 +498,8 @@ extern "C" int u2gnn_gemm(const u2gnn_gemm_args *a, void *stream) {
     P.p = a->p_drop;
     P.seed = a->seed;
     hipStream_t st = u2gnn_stream(stream);
-    if (tile == 128) return launch_layout<128, 128>(P, a->trans_a, a->trans_b, e, split, st);
-    return launch_layout<64, 64>(P, a->trans_a, a->trans_b, e, split, st);
+    const bool ta = a->trans_a != 0, tb = a->trans_b != 0;
+    if (prec == U2GNN_PREC_BF16X3) return launch_tile<U2GNN_PREC_BF16X3>(P, tile, ta, tb, e, split, st);
+    if (prec == U2GNN_PREC_BF16) return launch_tile<U2GNN_PREC_BF16>(P, tile, ta, tb, e, split, st);
+    return launch_tile<U2GNN_PREC_F32>(P, tile, ta, tb, e, split, st);
 }

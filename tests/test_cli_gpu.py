@@ -27,7 +27,7 @@ def test_sup_cli_mutag(tmp_path, autograd):
                                                    "--num_timesteps", "1"] + (["--autograd"] if autograd else []),
                     tmp_path)
     assert "| epoch   1 |" in out and "test acc" in out
-    acc = run.parent.parent / "runs_pytorch_U2GNN_Sup" / "MUTAG" / "checkpoints" / "model_acc.txt"
+    acc = run.parent / "runs_pytorch_U2GNN_Sup" / "MUTAG" / "checkpoints" / "model_acc.txt"
     assert acc.read_text().startswith("epoch 1 fold 1 acc ")
 
 
@@ -35,5 +35,5 @@ def test_unsup_cli_ptc(tmp_path):
     out, run = _run("train_pytorch_U2GNN_UnSup.py", ["--dataset", "PTC", "--model_name", "PTC", "--num_timesteps", "2",
                                                      "--max_steps", "20"], tmp_path)
     assert "| epoch   1 |" in out and "mean" in out
-    acc = run.parent.parent / "runs_pytorch_U2GNN_UnSup" / "PTC" / "checkpoints" / "model_acc.txt"
+    acc = run.parent / "runs_pytorch_U2GNN_UnSup" / "PTC" / "checkpoints" / "model_acc.txt"
     assert acc.read_text().startswith("epoch 1 mean: ")

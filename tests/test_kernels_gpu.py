@@ -34,6 +34,35 @@ def test_gemm_layouts_exact_fp32(tile, layout):
     assert rel_err(C.double(), ref) < 1e-5
 
 
+@pytest.mark.parametrize("prec,tol", [("bf16x3", 3e-5), ("bf16", 2e-2)])
+@pytest.mark.parametrize("tile", [64, 128])
+@pytest.mark.parametrize("layout", ["NT", "NN", "TN"])
+def test_gemm_split_bf16_layouts(prec, tol, tile, layout):
+    M, N, Kd = 256, 384, 320
+    ta, tb = layout[0] == "T", layout[1] == "T"
+    A = _mk(Kd, M, seed=11) if ta else _mk(M, Kd, seed=11)
+    B = _mk(N, Kd, seed=12) if tb else _mk(Kd, N, seed=12)
+    C = torch.empty(M, N, device=DEV)
+    K.gemm(A, B, C, M, N, Kd, A.shape[1], B.shape[1], N, trans_a=ta, trans_b=tb, tile=tile, precision=prec)
+    ref = (A.t() if ta else A).double() @ (B.t() if tb else B).double()
+    assert rel_err(C.double(), ref) < tol
+
+
+@pytest.mark.parametrize("prec", ["bf16x3", "bf16"])
+def test_gemm_split_bf16_identity_and_epilogue(prec):
+    M = N = Kd = 128
+    A = torch.eye(M, device=DEV)
+    B = (torch.arange(Kd * N, device=DEV, dtype=torch.float32).view(Kd, N) % 251) / 8.0   # exact in bf16
+    C = torch.empty(M, N, device=DEV)
+    K.gemm(A, B, C, M, N, Kd, Kd, N, N, precision=prec)
+    assert torch.equal(C, B)
+    Bt = B.t().contiguous()
+    P, Pd, dl = torch.rand(M, N, device=DEV), torch.rand(M, N, device=DEV), _mk(M, seed=9)
+    K.gemm(A, Bt, C, M, N, Kd, Kd, Kd, N, trans_b=True, epilogue=_lib.EPI_ATTN_DS, aux0=P, aux1=Pd, rowvec=dl,
+           ld_aux=N, precision=prec)
+    assert rel_err(C, Pd * B - P * dl[:, None]) < 1e-6
+
+
 def test_gemm_asymmetric_identity():
     """A = I with an asymmetric B catches a transposed C/D map."""
     M = N = Kd = 128

@@ -25,22 +25,23 @@ def _load(golden_dir, name):
     return dict(np.load(os.path.join(golden_dir, name + ".npz")))
 
 
-def _model(z):
+def _model(z, precision="fp32"):
     from pytorch_U2GNN_Sup import TransformerU2GNN
     bs, k, T, ff, L, d, C, fold = [int(x) for x in z["meta"]]
     m = TransformerU2GNN(feature_dim_size=d, ff_hidden_size=ff, num_classes=C, num_self_att_layers=T, dropout=0.5,
-                         num_U2GNN_layers=L)
+                         num_U2GNN_layers=L, precision=precision)
     sd = {kk[5:]: torch.from_numpy(v) for kk, v in z.items() if kk.startswith("init.")}
     m.load_state_dict(sd)
     return m.to(DEV), (bs, k, T, ff, L, d, C)
 
 
+@pytest.mark.parametrize("precision", ["fp32", "bf16x3"])
 @pytest.mark.parametrize("name", ["mutag_sup", "mutag_sup_L2T2", "imdbb_sup"])
-def test_sup_forward_backward_adam_vs_reference(golden_dir, name):
+def test_sup_forward_backward_adam_vs_reference(golden_dir, name, precision):
     from pytorch_U2GNN_Sup import label_smoothing
     from u2gnn_hip.core import DeviceBatch, FusedAdam
     z = _load(golden_dir, name)
-    m, (bs, k, T, ff, L, d, C) = _model(z)
+    m, (bs, k, T, ff, L, d, C) = _model(z, precision)
     m.eval()
     b = DeviceBatch.from_offsets(z["b0_input_x"], z["b0_offsets"], z["b0_X"], z["b0_labels"])
     # reference-signature path with a sparse graph_pool
@@ -69,6 +70,40 @@ def test_sup_forward_backward_adam_vs_reference(golden_dir, name):
     assert abs(opt.grad_norm() - float(z["grad_norm"])) <= TOL * max(1.0, float(z["grad_norm"]))
     for n, p in m.named_parameters():
         assert close(p.detach(), z["after." + n]), n
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16x3"])
+def test_collab_c4_full_batch_vs_oracle(precision):
+    """The benchmark configuration itself (C4: d=367, ff=1024, T=4, k=16, a full 64-graph batch,
+    N ~ 4.7K nodes) against the oracle restatement (slot 0, eval mode): scores, loss, grads."""
+    from oracle import u2gnn_oracle as O
+    from pytorch_U2GNN_Sup import TransformerU2GNN
+    from u2gnn_hip.batching import BatchLoader
+    from u2gnn_hip.core import DeviceBatch
+    from u2gnn_hip.synthetic import collab_like
+    np.random.seed(123)
+    hb = BatchLoader(collab_like(), 64, 16)()
+    torch.manual_seed(123)
+    m = TransformerU2GNN(367, 1024, 3, 4, 0.5, 1, precision=precision)
+    sd = {k: v.detach().clone().requires_grad_(True) for k, v in m.state_dict().items()}
+    m = m.to(DEV).eval()
+    flat = m.flatten_parameters()
+    b = DeviceBatch.from_offsets(hb.input_x, hb.offsets, hb.X_concat, hb.labels, device=DEV)
+    from u2gnn_hip import kernels as K
+    scores, ctx = m.core.forward(b, train=False, need_ctx=True, seed=0)
+    dsc = torch.empty_like(scores)
+    loss = torch.zeros(1, device=DEV)
+    K.smoothed_ce(scores, b.labels, b.B, 3, 0.1, loss, dsc)
+    m.core.backward(ctx, dsc, flat.grads)
+    torch.set_num_threads(min(16, os.cpu_count()))
+    ref = O.sup_forward(sd, torch.from_numpy(hb.input_x), hb.offsets, torch.from_numpy(hb.X_concat), 1, 4,
+                        train=False, slots=1)
+    lref = O.soft_cross_entropy(ref, O.label_smoothing(torch.from_numpy(hb.labels), 3))
+    lref.backward()
+    assert close(scores, ref.detach())
+    assert abs(loss.item() - lref.item()) <= TOL * max(1.0, abs(lref.item()))
+    for n, _ in m.named_parameters():
+        assert close(flat.grads[n], sd[n].grad), n
 
 
 def test_sup_fused_step_matches_autograd(golden_dir):

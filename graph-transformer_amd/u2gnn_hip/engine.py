@@ -158,7 +158,7 @@ def _wgrad(dY, ld_dy, X, ld_x, m_pad, n_pad, rows_pad, dst, rblk, cblk, prec):
     Split-K over the node dimension into deterministic fp32 slabs, then one reduce+unpack."""
     tiles = (m_pad // 64) * (n_pad // 64)
     split = 1
-    while split < 8 and tiles * split < 512 and rows_pad % (16 * split * 2) == 0:
+    while split < 8 and tiles * split < 512 and rows_pad % (32 * split * 2) == 0:
         split *= 2
     slabs = torch.empty(split, m_pad, n_pad, device=dY.device, dtype=torch.float32)
     K.gemm(dY, X, slabs, m_pad, n_pad, rows_pad, ld_dy, ld_x, n_pad, trans_a=True, trans_b=False,
@@ -181,7 +181,7 @@ def _gemm_nodes_k(A, B, C, M, N, Kd, lda, ldb, ldc, trans_a=False, alpha=1.0, pr
         K.gemm(A, B, C, M, N, Kd, lda, ldb, ldc, trans_a=trans_a, alpha=alpha, precision=prec)
         return
     split = 1
-    while split < 8 and tiles * split < 400 and Kd % (16 * split * 2) == 0:
+    while split < 8 and tiles * split < 400 and Kd % (32 * split * 2) == 0:
         split *= 2
     slabs = torch.empty(split, M, N, device=C.device, dtype=torch.float32)
     K.gemm(A, B, slabs, M, N, Kd, lda, ldb, N, trans_a=trans_a, split_k=split, slab_stride=M * N, precision=prec,

@@ -29,7 +29,8 @@ struct GemmP {
     const float *B;
     float *C;
     int64_t lda, ldb, ldc;
-    int32_t M, N, K;  // K = per-split depth
+    int32_t M, N, K;  // K = per-split depth (multiple of the K tile)
+    int32_t Ktot;     // full depth; split z covers [z*K, min((z+1)*K, Ktot))
     int32_t gm, gn;
     int64_t slab_stride;
     const float *bias;
@@ -185,11 +186,14 @@ __global__ void __launch_bounds__(256) gemm_f32_kernel(GemmP P) {
     const int wave = tid >> 6, lane = tid & 63;
     const int wm = wave >> 1, wn = wave & 1;
     const int kh = lane >> 5, li = lane & 31;
-    const int nk = P.K / BK;
+    const int64_t klen = min((int64_t)P.K, (int64_t)P.Ktot - kbase);
+    const int nk = klen > 0 ? (int)(klen / BK) : 0;   // ragged last split; empty splits write 0
 
-    g2r<BM, BN, BK, TA, TB>(Ab, Bb, P.lda, P.ldb, 0, tid, ra, rb);
-    r2s<BM, BN, BK, SA, SB, TA, TB>(As0, Bs0, tid, ra, rb);
-    __syncthreads();
+    if (nk > 0) {
+        g2r<BM, BN, BK, TA, TB>(Ab, Bb, P.lda, P.ldb, 0, tid, ra, rb);
+        r2s<BM, BN, BK, SA, SB, TA, TB>(As0, Bs0, tid, ra, rb);
+        __syncthreads();
+    }
     for (int t = 0; t < nk; ++t) {
         // unconditional prefetch (the last iteration re-reads the final tile; harmless) keeps
         // the staging registers out of scratch
@@ -328,10 +332,11 @@ __global__ void __launch_bounds__(256) gemm_bf16_kernel(GemmP P) {
     tile_coords(P.gm, P.gn, tmi, tni);
     const int m0 = tmi * BM, n0 = tni * BN;
     const int64_t kbase = (int64_t)blockIdx.z * P.K;
+    const int64_t klen = min((int64_t)P.K, (int64_t)P.Ktot - kbase);
+    const int nk = klen > 0 ? (int)(klen / BK) : 0;   // ragged last split; empty splits write 0
     const float *Ab = TA ? P.A + kbase * P.lda + m0 : P.A + (int64_t)m0 * P.lda + kbase;
     const float *Bb = TB ? P.B + (int64_t)n0 * P.ldb + kbase : P.B + kbase * P.ldb + n0;
 
-    float4 ra[NFA], rb[NFB];
     f32x16 acc[TM][TN];
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -343,19 +348,10 @@ __global__ void __launch_bounds__(256) gemm_bf16_kernel(GemmP P) {
     const int wave = tid >> 6, lane = tid & 63;
     const int wm = wave >> 1, wn = wave & 1;
     const int kh = lane >> 5, li = lane & 31;
-    const int nk = P.K / BK;
 
     auto stage = [&](int s) { return smem + s * STAGE; };
-    g2r_bf<BM, BK, TA>(Ab, P.lda, 0, tid, ra);
-    g2r_bf<BN, BK, !TB>(Bb, P.ldb, 0, tid, rb);
-    r2s_bf<BM, BK, LDK, TA, SPLIT>(stage(0), stage(0) + AE, tid, ra);
-    r2s_bf<BN, BK, LDK, !TB, SPLIT>(stage(0) + 2 * AE, stage(0) + 2 * AE + BE, tid, rb);
-    __syncthreads();
-    for (int t = 0; t < nk; ++t) {
-        const int tn = min(t + 1, nk - 1);
-        g2r_bf<BM, BK, TA>(Ab, P.lda, tn, tid, ra);
-        g2r_bf<BN, BK, !TB>(Bb, P.ldb, tn, tid, rb);
-        const __bf16 *Ah = stage(t & 1), *Al = Ah + AE, *Bh = Ah + 2 * AE, *Bl = Bh + BE;
+    auto compute = [&](const __bf16 *Ah) {
+        const __bf16 *Al = Ah + AE, *Bh = Ah + 2 * AE, *Bl = Bh + BE;
 #pragma unroll
         for (int ks = 0; ks < BK / 16; ++ks) {
             bf16x8 ah[TM], al[TM], bh[TN], bl[TN];
@@ -382,10 +378,35 @@ __global__ void __launch_bounds__(256) gemm_bf16_kernel(GemmP P) {
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
                 }
         }
-        __bf16 *ns = stage((t + 1) & 1);
-        r2s_bf<BM, BK, LDK, TA, SPLIT>(ns, ns + AE, tid, ra);
-        r2s_bf<BN, BK, LDK, !TB, SPLIT>(ns + 2 * AE, ns + 2 * AE + BE, tid, rb);
+    };
+
+    if (nk > 0) {
+        // two register stages: every tile's global loads are in flight across TWO compute phases
+        // (a single phase of 24 MFMAs does not cover an L2/LLC miss at 2 waves per SIMD)
+        float4 ra0[NFA], rb0[NFB], ra1[NFA], rb1[NFB];
+        g2r_bf<BM, BK, TA>(Ab, P.lda, 0, tid, ra0);
+        g2r_bf<BN, BK, !TB>(Bb, P.ldb, 0, tid, rb0);
+        g2r_bf<BM, BK, TA>(Ab, P.lda, min(1, nk - 1), tid, ra1);
+        g2r_bf<BN, BK, !TB>(Bb, P.ldb, min(1, nk - 1), tid, rb1);
+        r2s_bf<BM, BK, LDK, TA, SPLIT>(stage(0), stage(0) + AE, tid, ra0);
+        r2s_bf<BN, BK, LDK, !TB, SPLIT>(stage(0) + 2 * AE, stage(0) + 2 * AE + BE, tid, rb0);
         __syncthreads();
+        for (int t = 0; t < nk; t += 2) {
+            g2r_bf<BM, BK, TA>(Ab, P.lda, min(t + 2, nk - 1), tid, ra0);
+            g2r_bf<BN, BK, !TB>(Bb, P.ldb, min(t + 2, nk - 1), tid, rb0);
+            compute(stage(0));
+            r2s_bf<BM, BK, LDK, TA, SPLIT>(stage(1), stage(1) + AE, tid, ra1);
+            r2s_bf<BN, BK, LDK, !TB, SPLIT>(stage(1) + 2 * AE, stage(1) + 2 * AE + BE, tid, rb1);
+            __syncthreads();
+            if (t + 1 < nk) {
+                g2r_bf<BM, BK, TA>(Ab, P.lda, min(t + 3, nk - 1), tid, ra1);
+                g2r_bf<BN, BK, !TB>(Bb, P.ldb, min(t + 3, nk - 1), tid, rb1);
+                compute(stage(1));
+                r2s_bf<BM, BK, LDK, TA, SPLIT>(stage(0), stage(0) + AE, tid, ra0);
+                r2s_bf<BN, BK, LDK, !TB, SPLIT>(stage(0) + 2 * AE, stage(0) + 2 * AE + BE, tid, rb0);
+                __syncthreads();
+            }
+        }
     }
 
     float *C = P.C + (int64_t)blockIdx.z * P.slab_stride;
@@ -460,7 +481,7 @@ extern "C" int u2gnn_gemm(const u2gnn_gemm_args *a, void *stream) {
     if (split > 1 && a->epilogue != U2GNN_EPI_STORE) return U2GNN_E_ARG;
     if (!al16(a->A) || !al16(a->B) || (a->lda & 3) || (a->ldb & 3)) return U2GNN_E_ALIGN;
     const int bk = prec == U2GNN_PREC_F32 ? 16 : 32;
-    if (a->K % (bk * split)) return U2GNN_E_SHAPE;
+    if (a->K % bk) return U2GNN_E_SHAPE;
     const int e = a->epilogue;
     if ((e == U2GNN_EPI_BIAS || e == U2GNN_EPI_BIAS_DROP_RESID || e == U2GNN_EPI_BIAS_RELU_DROP) && !a->bias)
         return U2GNN_E_ARG;
@@ -484,7 +505,10 @@ extern "C" int u2gnn_gemm(const u2gnn_gemm_args *a, void *stream) {
     P.ldc = a->ldc;
     P.M = (int32_t)a->M;
     P.N = (int32_t)a->N;
-    P.K = (int32_t)(a->K / split);
+    // split z covers k in [z*Kc, min((z+1)*Kc, K)), Kc a multiple of the K tile (the last
+    // splits may be short or empty; an empty split writes a zero slab)
+    P.K = (int32_t)((a->K + (int64_t)split * bk - 1) / ((int64_t)split * bk) * bk);
+    P.Ktot = (int32_t)a->K;
     P.gm = (int32_t)(a->M / tile);
     P.gn = (int32_t)(a->N / tile);
     P.slab_stride = a->slab_stride;

@@ -153,17 +153,33 @@ class EncoderLayerCtx:
     __slots__ = ("X", "QKV", "P", "Pd", "O", "Z1", "X1", "mean1", "rstd1", "Hd", "Z2", "mean2", "rstd2", "seeds")
 
 
+def _gemm_split(A, B, C, M, N, Kd, lda, ldb, ldc, trans_a=False, trans_b=False, alpha=1.0, accumulate=False,
+                prec="fp32", rblk=None, cblk=None, target=448):
+    """C (+)= alpha * op(A) . op(B) with deterministic split-K: when the tile grid alone would
+    leave most of the 256 CUs idle (skinny outputs with a deep node dimension: P.V, Pd^T.dO,
+    dS.K, dS^T.Q, the weight gradients, dH.W1, dQKV.W_in), the depth is cut into fp32 slabs
+    (>= 4 K-tiles each, ~target workgroups) and one streaming pass sums them into C — applying
+    alpha, accumulation and an optional padded->real block map (rblk, cblk)."""
+    t = 128 if (M % 128 == 0 and N % 128 == 0) else 64
+    tiles = (M // t) * (N // t)
+    bk = 16 if prec == "fp32" else 32
+    split = max(1, min(target // max(tiles, 1), Kd // (4 * bk)))
+    mapped = rblk is not None
+    if split == 1 and not mapped:
+        K.gemm(A, B, C, M, N, Kd, lda, ldb, ldc, trans_a=trans_a, trans_b=trans_b, alpha=alpha,
+               epilogue=E.EPI_ACCUM if accumulate else E.EPI_STORE, precision=prec, tile=t)
+        return
+    slabs = torch.empty(split, M, N, device=C.device, dtype=torch.float32)
+    K.gemm(A, B, slabs, M, N, Kd, lda, ldb, N, trans_a=trans_a, trans_b=trans_b, split_k=split, slab_stride=M * N,
+           precision=prec, tile=t)
+    K.slab_reduce(slabs, split, M * N, M, N, N, rblk or (M, M), cblk or (N, N), C, ldc, alpha=alpha,
+                  accumulate=accumulate)
+
+
 def _wgrad(dY, ld_dy, X, ld_x, m_pad, n_pad, rows_pad, dst, rblk, cblk, prec):
-    """dst(real) = unpack(dY^T X) with dY [rows_pad, m_pad] (ld_dy), X [rows_pad, n_pad] (ld_x).
-    Split-K over the node dimension into deterministic fp32 slabs, then one reduce+unpack."""
-    tiles = (m_pad // 64) * (n_pad // 64)
-    split = 1
-    while split < 8 and tiles * split < 512 and rows_pad % (32 * split * 2) == 0:
-        split *= 2
-    slabs = torch.empty(split, m_pad, n_pad, device=dY.device, dtype=torch.float32)
-    K.gemm(dY, X, slabs, m_pad, n_pad, rows_pad, ld_dy, ld_x, n_pad, trans_a=True, trans_b=False,
-           epilogue=E.EPI_STORE, split_k=split, slab_stride=m_pad * n_pad, precision=prec, tile=64)
-    K.slab_reduce(slabs, split, m_pad * n_pad, m_pad, n_pad, n_pad, rblk, cblk, dst, dst.shape[-1] if dst.dim() > 1 else dst.numel())
+    """dst(real) = unpack(dY^T X) with dY [rows_pad, m_pad] (ld_dy), X [rows_pad, n_pad] (ld_x)."""
+    _gemm_split(dY, X, dst, m_pad, n_pad, rows_pad, ld_dy, ld_x, dst.shape[-1] if dst.dim() > 1 else dst.numel(),
+                trans_a=True, prec=prec, rblk=rblk, cblk=cblk)
 
 
 def _bias_grad(dY, rows, cols_pad, ld, cblk, out):
@@ -172,21 +188,8 @@ def _bias_grad(dY, rows, cols_pad, ld, cblk, out):
 
 
 def _gemm_nodes_k(A, B, C, M, N, Kd, lda, ldb, ldc, trans_a=False, alpha=1.0, prec="fp32"):
-    """C[M, N] = alpha * op(A) . B for the skinny attention products whose depth is the node
-    dimension (P.V, Pd^T.dO, dS.K, dS^T.Q: N = dp, K = Np).  A 128x128 tile grid has only
-    (Np/128)*(dp/128) ~ 114 workgroups for 256 CUs, so the depth is split into deterministic fp32
-    slabs (>= ~1.5 workgroups per CU), reduced (and scaled by alpha) by one streaming pass."""
-    tiles = (M // 128) * (N // 128) if (M % 128 == 0 and N % 128 == 0) else 0
-    if tiles == 0 or tiles >= 384:
-        K.gemm(A, B, C, M, N, Kd, lda, ldb, ldc, trans_a=trans_a, alpha=alpha, precision=prec)
-        return
-    split = 1
-    while split < 8 and tiles * split < 400 and Kd % (32 * split * 2) == 0:
-        split *= 2
-    slabs = torch.empty(split, M, N, device=C.device, dtype=torch.float32)
-    K.gemm(A, B, slabs, M, N, Kd, lda, ldb, N, trans_a=trans_a, split_k=split, slab_stride=M * N, precision=prec,
-           tile=128)
-    K.slab_reduce(slabs, split, M * N, M, N, N, (M, M), (N, N), C, ldc, alpha=alpha)
+    """The skinny attention products whose depth is the node dimension (N = dp, K = Np)."""
+    _gemm_split(A, B, C, M, N, Kd, lda, ldb, ldc, trans_a=trans_a, alpha=alpha, prec=prec)
 
 
 def encoder_layer_forward(X: torch.Tensor, w: PackedLayer, p: LayerParams, dims: Dims, train: bool,
@@ -259,7 +262,7 @@ def encoder_layer_backward(dX2: torch.Tensor, ctx: EncoderLayerCtx, w: PackedLay
     K.gemm(dF, w.W2, dH, Np, ffp, dp, dp, ffp, ffp, epilogue=E.EPI_RELU_DROP_BWD, aux0=ctx.Hd, ld_aux=ffp,
            p_drop=pd, precision=prec)
     _wgrad(dF, dp, ctx.Hd, ffp, dp, ffp, Np, g.l2_w, (dp, d), (ffp, ff), prec)
-    K.gemm(dH, w.W1, dX1, Np, dp, ffp, ffp, dp, dp, epilogue=E.EPI_ACCUM, precision=prec)
+    _gemm_split(dH, w.W1, dX1, Np, dp, ffp, ffp, dp, dp, accumulate=True, prec=prec)
     _wgrad(dH, ffp, ctx.X1, dp, ffp, dp, Np, g.l1_w, (ffp, ff), (dp, d), prec)
     _bias_grad(dH, Np, ffp, ffp, (ffp, ff), g.l1_b)
     del dH, dF
@@ -296,7 +299,7 @@ def encoder_layer_backward(dX2: torch.Tensor, ctx: EncoderLayerCtx, w: PackedLay
                                      prec=prec))
     del dS, dO
     # in-projection
-    K.gemm(dQKV, w.W_in, dX, Np, dp, 3 * dp, 3 * dp, dp, dp, epilogue=E.EPI_ACCUM, precision=prec)
+    _gemm_split(dQKV, w.W_in, dX, Np, dp, 3 * dp, 3 * dp, dp, dp, accumulate=True, prec=prec)
     _wgrad(dQKV, 3 * dp, ctx.X, dp, 3 * dp, dp, Np, g.in_w, (dp, d), (dp, d), prec)
     _bias_grad(dQKV, Np, 3 * dp, 3 * dp, (dp, d), g.in_b)
     return dX

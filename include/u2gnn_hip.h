@@ -56,7 +56,9 @@ typedef struct u2gnn_gemm_args {
     int64_t lda, ldb, ldc;
     int32_t trans_a, trans_b;
     int32_t epilogue;     /* U2GNN_EPI_*; split_k>1 requires STORE */
-    int32_t split_k;      /* >= 1; K must split into multiples of the K tile */
+    int32_t split_k;      /* >= 1; K (a multiple of the K tile: 16 fp32, 32 bf16 modes) is cut into
+                             split_k chunks of Kc = ceil(K/(split_k*tile))*tile; slab z holds the
+                             partial sum over [z*Kc, min((z+1)*Kc, K)) (zeros when empty) */
     int64_t slab_stride;
     const float *bias;    /* [N] */
     const float *aux0;    /* residual / saved relu-dropout output / P */

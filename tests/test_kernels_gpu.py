@@ -85,6 +85,19 @@ def test_gemm_split_k_slabs_and_views():
     assert rel_err(out.double(), ref) < 1e-5
 
 
+@pytest.mark.parametrize("prec,Kd,split", [("fp32", 208, 5), ("fp32", 64, 8), ("bf16x3", 352, 4),
+                                           ("bf16x3", 96, 8)])
+def test_gemm_ragged_and_empty_splits(prec, Kd, split):
+    """split z covers [z*Kc, min((z+1)*Kc, K)); trailing splits may be short or empty (zero slab)."""
+    M, N = 128, 128
+    A, B = _mk(Kd, M, seed=31), _mk(Kd, N, seed=32)
+    slabs = torch.full((split, M, N), float("nan"), device=DEV)
+    K.gemm(A, B, slabs, M, N, Kd, M, N, N, trans_a=True, split_k=split, slab_stride=M * N, tile=128, precision=prec)
+    assert torch.isfinite(slabs).all()
+    ref = A.t().double() @ B.double()
+    assert rel_err(slabs.sum(0).double(), ref) < (1e-5 if prec == "fp32" else 3e-5)
+
+
 def test_gemm_epilogues():
     M, N, Kd = 128, 128, 64
     A, B = _mk(M, Kd, seed=5), _mk(N, Kd, seed=6)

@@ -52,6 +52,21 @@ def parse():
     return ap.parse_args()
 
 
+def pmc_traffic(symbol):
+    """HBM bytes per launch of `symbol` from the committed PMC pass (profiles/<round>/pmc_traffic.json,
+    written by tools/pmc_traffic.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs with
+    the gfx950 FETCH_SIZE x2 correction).  None when no pass covers this kernel."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*", "pmc_traffic.json")), reverse=True):
+        try:
+            table = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if symbol in table.get("kernels", {}):
+            return table["kernels"][symbol]["hbm_bytes_per_launch"]
+    return None
+
+
 def model_step_flops(N, d, ff, T, L):
     """Algorithmic FLOPs of one fwd+bwd step, slot 0 only."""
     return 3.0 * L * T * (8.0 * N * d * d + 4.0 * N * N * d + 4.0 * N * d * ff)
@@ -104,7 +119,7 @@ def main():
     from u2gnn_hip.batching import BatchLoader
     from u2gnn_hip.dp import GradAllReduce, broadcast_params, rank_batches
     from u2gnn_hip.core import DeviceBatch
-    from u2gnn_hip.engine import TIMER
+    from u2gnn_hip import kernels as K
     from u2gnn_hip.synthetic import collab_like
     from u2gnn_hip.train import SupTrainer
 
@@ -133,8 +148,8 @@ def main():
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
-    TIMER.records.clear()
-    TIMER.enabled = not args.no_roofline
+    K.REC.records.clear()
+    K.REC.enabled = not args.no_roofline
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
@@ -143,7 +158,7 @@ def main():
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    TIMER.enabled = False
+    K.REC.enabled = False
     if dist is not None:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -157,17 +172,22 @@ def main():
                                                  args.num_hidden_layers) for b in used]))
 
     roof = None
-    if TIMER.records:
-        fl = sum(r[1] for r in TIMER.records)
-        ms = sum(r[2].elapsed_time(r[3]) for r in TIMER.records)
+    summ = K.REC.summary()
+    if summ:
+        # the dominant kernel = the GEMM template instance with the most device time in the timed
+        # region; achieved = its launches' algorithmic FLOPs (real, unpadded dims) / their time
+        dom = max(summ, key=lambda k: summ[k][2])
+        n, fl, ms = summ[dom]
         ach = fl / (ms * 1e-3) / 1e12
         peak = PEAK[args.precision]
-        roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
-                "frac": round(ach / peak, 4), "traffic": None,
-                "kernel": ("gemm_f32_kernel" if args.precision == "fp32" else "gemm_bf16_kernel") +
-                          " on the attention products (Q.K^T, P.V, dO.V^T->dS, Pd^T.dO, dS.K, "
-                          "dS^T.Q); algorithmic 2*N*N*d FLOP per launch, real N and d",
-                "launches": len(TIMER.records), "avg_launch_us": round(1e3 * ms / len(TIMER.records), 1),
+        fam = sorted(summ.items(), key=lambda kv: -kv[1][2])
+        roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
+                "frac": round(ach / peak, 4), "traffic": pmc_traffic(dom),
+                "kernel": dom, "launches": n, "avg_launch_us": round(1e3 * ms / n, 1),
+                "algorithmic_flop_per_launch": round(fl / n),
+                "gemm_share_of_step": round(sum(v[2] for v in summ.values()) / (1e3 * elapsed), 3),
+                "gemm_family": {k: {"launches": v[0], "ms": round(v[2], 2),
+                                    "tflops": round(v[1] / (v[2] * 1e-3) / 1e12, 1)} for k, v in fam[:8]},
                 "step_tflops_per_gpu": round(step_flops / (elapsed / args.steps) / 1e12, 2)}
     out = {"metric": METRIC, "value": round(value, 2), "unit": "graphs/s", "n_gpus": world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 3), "higher_is_better": True,

@@ -127,34 +127,12 @@ class PackedLayer:
         K.pack_padded_multi(self.jobs(p))
 
 
-class GemmTimer:
-    """Optional HIP-event bracketing of selected launches (bench roofline)."""
-
-    def __init__(self):
-        self.records = []  # (name, flops, start_event, end_event)
-        self.enabled = False
-
-    def wrap(self, name, flops, fn):
-        if not self.enabled:
-            fn()
-            return
-        s = torch.cuda.Event(enable_timing=True)
-        e = torch.cuda.Event(enable_timing=True)
-        s.record()
-        fn()
-        e.record()
-        self.records.append((name, flops, s, e))
-
-
-TIMER = GemmTimer()
-
-
 class EncoderLayerCtx:
     __slots__ = ("X", "QKV", "P", "Pd", "O", "Z1", "X1", "mean1", "rstd1", "Hd", "Z2", "mean2", "rstd2", "seeds")
 
 
 def _gemm_split(A, B, C, M, N, Kd, lda, ldb, ldc, trans_a=False, trans_b=False, alpha=1.0, accumulate=False,
-                prec="fp32", rblk=None, cblk=None, target=448):
+                prec="fp32", rblk=None, cblk=None, target=448, flops=None):
     """C (+)= alpha * op(A) . op(B) with deterministic split-K: when the tile grid alone would
     leave most of the 256 CUs idle (skinny outputs with a deep node dimension: P.V, Pd^T.dO,
     dS.K, dS^T.Q, the weight gradients, dH.W1, dQKV.W_in), the depth is cut into fp32 slabs
@@ -167,19 +145,19 @@ def _gemm_split(A, B, C, M, N, Kd, lda, ldb, ldc, trans_a=False, trans_b=False, 
     mapped = rblk is not None
     if split == 1 and not mapped:
         K.gemm(A, B, C, M, N, Kd, lda, ldb, ldc, trans_a=trans_a, trans_b=trans_b, alpha=alpha,
-               epilogue=E.EPI_ACCUM if accumulate else E.EPI_STORE, precision=prec, tile=t)
+               epilogue=E.EPI_ACCUM if accumulate else E.EPI_STORE, precision=prec, tile=t, flops=flops)
         return
     slabs = torch.empty(split, M, N, device=C.device, dtype=torch.float32)
     K.gemm(A, B, slabs, M, N, Kd, lda, ldb, N, trans_a=trans_a, trans_b=trans_b, split_k=split, slab_stride=M * N,
-           precision=prec, tile=t)
+           precision=prec, tile=t, flops=flops)
     K.slab_reduce(slabs, split, M * N, M, N, N, rblk or (M, M), cblk or (N, N), C, ldc, alpha=alpha,
                   accumulate=accumulate)
 
 
-def _wgrad(dY, ld_dy, X, ld_x, m_pad, n_pad, rows_pad, dst, rblk, cblk, prec):
+def _wgrad(dY, ld_dy, X, ld_x, m_pad, n_pad, rows_pad, dst, rblk, cblk, prec, n_real):
     """dst(real) = unpack(dY^T X) with dY [rows_pad, m_pad] (ld_dy), X [rows_pad, n_pad] (ld_x)."""
     _gemm_split(dY, X, dst, m_pad, n_pad, rows_pad, ld_dy, ld_x, dst.shape[-1] if dst.dim() > 1 else dst.numel(),
-                trans_a=True, prec=prec, rblk=rblk, cblk=cblk)
+                trans_a=True, prec=prec, rblk=rblk, cblk=cblk, flops=2.0 * dst.numel() * n_real)
 
 
 def _bias_grad(dY, rows, cols_pad, ld, cblk, out):
@@ -187,9 +165,9 @@ def _bias_grad(dY, rows, cols_pad, ld, cblk, out):
     K.colsum(dY, rows, cols_pad, ld, cblk, out, ws)
 
 
-def _gemm_nodes_k(A, B, C, M, N, Kd, lda, ldb, ldc, trans_a=False, alpha=1.0, prec="fp32"):
+def _gemm_nodes_k(A, B, C, M, N, Kd, lda, ldb, ldc, trans_a=False, alpha=1.0, prec="fp32", flops=None):
     """The skinny attention products whose depth is the node dimension (N = dp, K = Np)."""
-    _gemm_split(A, B, C, M, N, Kd, lda, ldb, ldc, trans_a=trans_a, alpha=alpha, prec=prec)
+    _gemm_split(A, B, C, M, N, Kd, lda, ldb, ldc, trans_a=trans_a, alpha=alpha, prec=prec, flops=flops)
 
 
 def encoder_layer_forward(X: torch.Tensor, w: PackedLayer, p: LayerParams, dims: Dims, train: bool,
@@ -197,37 +175,36 @@ def encoder_layer_forward(X: torch.Tensor, w: PackedLayer, p: LayerParams, dims:
                           p_drop: float = 0.5) -> (torch.Tensor, Optional[EncoderLayerCtx]):
     """One torch TransformerEncoderLayer(d, nhead=1, ff, dropout=0.5) forward, post-LN, on the
     slot-0 rows X [Np, dp] (pytorch_U2GNN_Sup.py:19-21,35)."""
-    N, Np, d, dp, ffp = dims.N, dims.Np, dims.d, dims.dp, dims.ffp
+    N, Np, d, dp, ff, ffp = dims.N, dims.Np, dims.d, dims.dp, dims.ff, dims.ffp
     pd = p_drop if train else 0.0
+    att = 2.0 * N * N * d          # algorithmic FLOPs of one attention product (real N, d)
     dev = X.device
     f32 = torch.float32
     QKV = torch.empty(Np, 3 * dp, device=dev, dtype=f32)
     K.gemm(X, w.W_in, QKV, Np, 3 * dp, dp, dp, dp, 3 * dp, trans_b=True, epilogue=E.EPI_BIAS, bias=w.b_in,
-           alpha=1.0 / math.sqrt(d), scale_cols=dp, precision=prec)
+           alpha=1.0 / math.sqrt(d), scale_cols=dp, precision=prec, flops=6.0 * N * d * d)
     Q, Kt, V = QKV[:, :dp], QKV[:, dp:2 * dp], QKV[:, 2 * dp:]
     S = torch.empty(Np, Np, device=dev, dtype=f32)
-    TIMER.wrap("qk", 2.0 * N * N * d,
-               lambda: K.gemm(Q, Kt, S, Np, Np, dp, 3 * dp, 3 * dp, Np, trans_b=True, precision=prec))
+    K.gemm(Q, Kt, S, Np, Np, dp, 3 * dp, 3 * dp, Np, trans_b=True, precision=prec, flops=att)
     P = torch.empty(Np, Np, device=dev, dtype=f32)
     Pd = torch.empty(Np, Np, device=dev, dtype=f32) if pd > 0 else P
     K.attn_softmax_fwd(S, Np, P, Pd, Np, N, Np, N, Np, pd, seeds.get(SITE_ATTN, 0))
     del S
     O = torch.empty(Np, dp, device=dev, dtype=f32)
-    TIMER.wrap("pv", 2.0 * N * N * d,
-               lambda: _gemm_nodes_k(Pd, V, O, Np, dp, Np, Np, 3 * dp, dp, prec=prec))
+    _gemm_nodes_k(Pd, V, O, Np, dp, Np, Np, 3 * dp, dp, prec=prec, flops=att)
     Z1 = torch.empty(Np, dp, device=dev, dtype=f32)
     K.gemm(O, w.W_o, Z1, Np, dp, dp, dp, dp, dp, trans_b=True, epilogue=E.EPI_BIAS_DROP_RESID, bias=w.b_o,
-           aux0=X, ld_aux=dp, p_drop=pd, seed=seeds.get(SITE_DROP1, 0), precision=prec)
+           aux0=X, ld_aux=dp, p_drop=pd, seed=seeds.get(SITE_DROP1, 0), precision=prec, flops=2.0 * N * d * d)
     X1 = torch.empty(Np, dp, device=dev, dtype=f32)
     mean1 = torch.empty(Np, device=dev, dtype=f32)
     rstd1 = torch.empty(Np, device=dev, dtype=f32)
     K.layernorm_fwd(Z1, dp, p.n1_w, p.n1_b, X1, dp, mean1, rstd1, N, Np, d, dp)
     Hd = torch.empty(Np, ffp, device=dev, dtype=f32)
     K.gemm(X1, w.W1, Hd, Np, ffp, dp, dp, dp, ffp, trans_b=True, epilogue=E.EPI_BIAS_RELU_DROP, bias=w.b1,
-           p_drop=pd, seed=seeds.get(SITE_DROPFF, 0), precision=prec)
+           p_drop=pd, seed=seeds.get(SITE_DROPFF, 0), precision=prec, flops=2.0 * N * d * ff)
     Z2 = torch.empty(Np, dp, device=dev, dtype=f32)
     K.gemm(Hd, w.W2, Z2, Np, dp, ffp, ffp, ffp, dp, trans_b=True, epilogue=E.EPI_BIAS_DROP_RESID, bias=w.b2,
-           aux0=X1, ld_aux=dp, p_drop=pd, seed=seeds.get(SITE_DROP2, 0), precision=prec)
+           aux0=X1, ld_aux=dp, p_drop=pd, seed=seeds.get(SITE_DROP2, 0), precision=prec, flops=2.0 * N * d * ff)
     X2 = torch.empty(Np, dp, device=dev, dtype=f32)
     mean2 = torch.empty(Np, device=dev, dtype=f32)
     rstd2 = torch.empty(Np, device=dev, dtype=f32)
@@ -248,6 +225,7 @@ def encoder_layer_backward(dX2: torch.Tensor, ctx: EncoderLayerCtx, w: PackedLay
     ``g`` (tensors shaped like the params) and returns dX [Np, dp]."""
     N, Np, d, dp, ff, ffp = dims.N, dims.Np, dims.d, dims.dp, dims.ff, dims.ffp
     pd, seeds = ctx.seeds
+    att = 2.0 * N * N * d
     dev = dX2.device
     f32 = torch.float32
     ws = torch.empty(K.colstat_ws_floats(N, dp), device=dev, dtype=f32)
@@ -260,10 +238,10 @@ def encoder_layer_backward(dX2: torch.Tensor, ctx: EncoderLayerCtx, w: PackedLay
     # FFN: Z2 = X1 + drop(Hd W2^T + b2), Hd = drop(relu(X1 W1^T + b1))
     dH = torch.empty(Np, ffp, device=dev, dtype=f32)
     K.gemm(dF, w.W2, dH, Np, ffp, dp, dp, ffp, ffp, epilogue=E.EPI_RELU_DROP_BWD, aux0=ctx.Hd, ld_aux=ffp,
-           p_drop=pd, precision=prec)
-    _wgrad(dF, dp, ctx.Hd, ffp, dp, ffp, Np, g.l2_w, (dp, d), (ffp, ff), prec)
-    _gemm_split(dH, w.W1, dX1, Np, dp, ffp, ffp, dp, dp, accumulate=True, prec=prec)
-    _wgrad(dH, ffp, ctx.X1, dp, ffp, dp, Np, g.l1_w, (ffp, ff), (dp, d), prec)
+           p_drop=pd, precision=prec, flops=2.0 * N * d * ff)
+    _wgrad(dF, dp, ctx.Hd, ffp, dp, ffp, Np, g.l2_w, (dp, d), (ffp, ff), prec, N)
+    _gemm_split(dH, w.W1, dX1, Np, dp, ffp, ffp, dp, dp, accumulate=True, prec=prec, flops=2.0 * N * d * ff)
+    _wgrad(dH, ffp, ctx.X1, dp, ffp, dp, Np, g.l1_w, (ffp, ff), (dp, d), prec, N)
     _bias_grad(dH, Np, ffp, ffp, (ffp, ff), g.l1_b)
     del dH, dF
     # LN1 backward -> dX (residual), dA (dropout1 branch)
@@ -275,8 +253,8 @@ def encoder_layer_backward(dX2: torch.Tensor, ctx: EncoderLayerCtx, w: PackedLay
     del dX1
     # out-projection
     dO = torch.empty(Np, dp, device=dev, dtype=f32)
-    K.gemm(dA, w.W_o, dO, Np, dp, dp, dp, dp, dp, precision=prec)
-    _wgrad(dA, dp, ctx.O, dp, dp, dp, Np, g.out_w, (dp, d), (dp, d), prec)
+    K.gemm(dA, w.W_o, dO, Np, dp, dp, dp, dp, dp, precision=prec, flops=2.0 * N * d * d)
+    _wgrad(dA, dp, ctx.O, dp, dp, dp, Np, g.out_w, (dp, d), (dp, d), prec, N)
     del dA
     # attention core
     QKV = ctx.QKV
@@ -284,22 +262,17 @@ def encoder_layer_backward(dX2: torch.Tensor, ctx: EncoderLayerCtx, w: PackedLay
     delta = torch.empty(Np, device=dev, dtype=f32)
     K.rowdot(dO, dp, ctx.O, dp, delta, Np, dp)
     dS = torch.empty(Np, Np, device=dev, dtype=f32)
-    TIMER.wrap("dpv", 2.0 * N * N * d,
-               lambda: K.gemm(dO, V, dS, Np, Np, dp, dp, 3 * dp, Np, trans_b=True, epilogue=E.EPI_ATTN_DS,
-                              aux0=ctx.P, aux1=ctx.Pd, rowvec=delta, ld_aux=Np, precision=prec))
+    K.gemm(dO, V, dS, Np, Np, dp, dp, 3 * dp, Np, trans_b=True, epilogue=E.EPI_ATTN_DS, aux0=ctx.P, aux1=ctx.Pd,
+           rowvec=delta, ld_aux=Np, precision=prec, flops=att)
     dQKV = torch.empty(Np, 3 * dp, device=dev, dtype=f32)
-    TIMER.wrap("dv", 2.0 * N * N * d,
-               lambda: _gemm_nodes_k(ctx.Pd, dO, dQKV[:, 2 * dp:], Np, dp, Np, Np, dp, 3 * dp, trans_a=True,
-                                     prec=prec))
-    TIMER.wrap("dq", 2.0 * N * N * d,
-               lambda: _gemm_nodes_k(dS, Kt, dQKV[:, :dp], Np, dp, Np, Np, 3 * dp, 3 * dp,
-                                     alpha=1.0 / math.sqrt(d), prec=prec))
-    TIMER.wrap("dk", 2.0 * N * N * d,
-               lambda: _gemm_nodes_k(dS, Q, dQKV[:, dp:2 * dp], Np, dp, Np, Np, 3 * dp, 3 * dp, trans_a=True,
-                                     prec=prec))
+    _gemm_nodes_k(ctx.Pd, dO, dQKV[:, 2 * dp:], Np, dp, Np, Np, dp, 3 * dp, trans_a=True, prec=prec, flops=att)
+    _gemm_nodes_k(dS, Kt, dQKV[:, :dp], Np, dp, Np, Np, 3 * dp, 3 * dp, alpha=1.0 / math.sqrt(d), prec=prec,
+                  flops=att)
+    _gemm_nodes_k(dS, Q, dQKV[:, dp:2 * dp], Np, dp, Np, Np, 3 * dp, 3 * dp, trans_a=True, prec=prec, flops=att)
     del dS, dO
     # in-projection
-    _gemm_split(dQKV, w.W_in, dX, Np, dp, 3 * dp, 3 * dp, dp, dp, accumulate=True, prec=prec)
-    _wgrad(dQKV, 3 * dp, ctx.X, dp, 3 * dp, dp, Np, g.in_w, (dp, d), (dp, d), prec)
+    _gemm_split(dQKV, w.W_in, dX, Np, dp, 3 * dp, 3 * dp, dp, dp, accumulate=True, prec=prec,
+                flops=6.0 * N * d * d)
+    _wgrad(dQKV, 3 * dp, ctx.X, dp, 3 * dp, dp, Np, g.in_w, (dp, d), (dp, d), prec, N)
     _bias_grad(dQKV, Np, 3 * dp, 3 * dp, (dp, d), g.in_b)
     return dX

@@ -30,12 +30,51 @@ def _dev(*ts):
             raise _lib.U2GNNNativeError("U2GNN kernels need device tensors (no CPU fallback)")
 
 
+class LaunchRecorder:
+    """HIP-event bracketing of GEMM launches, keyed by the kernel symbol the launch runs, with the
+    launch's ALGORITHMIC FLOPs (real, unpadded dims) supplied by the caller (bench roofline)."""
+
+    def __init__(self):
+        self.enabled = False
+        self.records = []   # (symbol, flops, start_event, end_event)
+
+    def summary(self):
+        """{symbol: (launches, algorithmic flops, milliseconds)} after a synchronize."""
+        out = {}
+        for sym, fl, s, e in self.records:
+            n, f, ms = out.get(sym, (0, 0.0, 0.0))
+            out[sym] = (n + 1, f + fl, ms + s.elapsed_time(e))
+        return out
+
+
+REC = LaunchRecorder()
+_EPI_NAMES = ["STORE", "BIAS", "BIAS_DROP_RESID", "BIAS_RELU_DROP", "RELU_DROP_BWD", "ACCUM", "ATTN_DS"]
+
+
+def gemm_symbol(precision, M, N, split_k, tile, trans_a, trans_b, epilogue):
+    """Mirror of the C dispatcher's kernel choice (gemm.hip u2gnn_gemm) -> template symbol."""
+    if tile == 0:
+        can128 = M % 128 == 0 and N % 128 == 0
+        tile = 128 if (can128 and (M // 128) * (N // 128) * max(split_k, 1) >= 480) else 64
+    b = lambda x: "true" if x else "false"  # noqa: E731
+    if precision == "fp32":
+        return f"gemm_f32_kernel<{tile}, {tile}, {b(trans_a)}, {b(trans_b)}, {int(epilogue)}>"
+    return (f"gemm_bf16_kernel<{tile}, {tile}, {b(trans_a)}, {b(trans_b)}, {int(epilogue)}, "
+            f"{b(precision == 'bf16x3')}>")   # the C++ template instance as rocprofv3 names it
+
+
 def gemm(A, B, C, M, N, K, lda, ldb, ldc, trans_a=False, trans_b=False, epilogue=_lib.EPI_STORE, split_k=1,
          slab_stride=0, bias=None, aux0=None, aux1=None, rowvec=None, ld_aux=0, alpha=1.0, scale_cols=0, p_drop=0.0,
-         seed=0, precision="fp32", tile=0):
+         seed=0, precision="fp32", tile=0, flops=None):
     """C[M,N] (epilogue) sum_k A(m,k) B(k,n).  A/B/C may be views (pointer arithmetic via
-    storage offsets is done by torch's data_ptr())."""
+    storage offsets is done by torch's data_ptr()).  ``flops``: algorithmic FLOPs of the
+    launch for the roofline recorder (None = not recorded)."""
     _dev(A, B, C)
+    rec = REC.enabled and flops is not None
+    if rec:
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev0.record()
     a = _lib.GemmArgs()
     a.A, a.B, a.C = A.data_ptr(), B.data_ptr(), C.data_ptr()
     a.M, a.N, a.K = int(M), int(N), int(K)
@@ -54,6 +93,10 @@ def gemm(A, B, C, M, N, K, lda, ldb, ldc, trans_a=False, trans_b=False, epilogue
     a.precision = PREC[precision] if isinstance(precision, str) else int(precision)
     a.tile = int(tile)
     check(hip_lib().u2gnn_gemm(ctypes.byref(a), _s()), "u2gnn_gemm")
+    if rec:
+        ev1.record()
+        REC.records.append((gemm_symbol(precision, M, N, split_k, tile, trans_a, trans_b, epilogue), float(flops),
+                            ev0, ev1))
 
 
 def gather_rows(src, idx, idx_stride, dst, n_rows, n_rows_pad, d, d_pad, err=None):

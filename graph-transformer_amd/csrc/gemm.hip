@@ -44,43 +44,73 @@ struct GemmP {
     uint64_t seed;
 };
 
+// four consecutive columns (col % 4 == 0) of one row; every vector operand is 16-byte aligned
+// with a leading dimension that is a multiple of 4 (checked by u2gnn_gemm)
+__device__ __forceinline__ float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
+
 template <int EPI>
-__device__ __forceinline__ float epilogue(const GemmP &P, int row, int col, float acc) {
+__device__ __forceinline__ float4 epilogue4(const GemmP &P, int row, int col, float4 v) {
     if constexpr (EPI == U2GNN_EPI_STORE) {
-        return P.alpha * acc;
-    } else if constexpr (EPI == U2GNN_EPI_BIAS) {
-        float v = acc + P.bias[col];
-        return col < P.scale_cols ? v * P.alpha : v;
-    } else if constexpr (EPI == U2GNN_EPI_BIAS_DROP_RESID) {
-        float v = acc + P.bias[col];
-        if (P.p > 0.f) v = u2gnn_keep(P.seed, row, col, P.p) ? v * (1.f / (1.f - P.p)) : 0.f;
-        return P.aux0[(int64_t)row * P.ld_aux + col] + v;
-    } else if constexpr (EPI == U2GNN_EPI_BIAS_RELU_DROP) {
-        float v = fmaxf(acc + P.bias[col], 0.f);
-        if (P.p > 0.f) v = u2gnn_keep(P.seed, row, col, P.p) ? v * (1.f / (1.f - P.p)) : 0.f;
-        return v;
-    } else if constexpr (EPI == U2GNN_EPI_RELU_DROP_BWD) {
-        const float h = P.aux0[(int64_t)row * P.ld_aux + col];
-        return h > 0.f ? acc * (1.f / (1.f - P.p)) : 0.f;
-    } else if constexpr (EPI == U2GNN_EPI_ACCUM) {
-        return P.C[(int64_t)row * P.ldc + col] + P.alpha * acc;
-    } else {  // U2GNN_EPI_ATTN_DS
+        return make_float4(P.alpha * v.x, P.alpha * v.y, P.alpha * v.z, P.alpha * v.w);
+    } else if constexpr (EPI == U2GNN_EPI_ATTN_DS) {
         const int64_t o = (int64_t)row * P.ld_aux + col;
-        return P.aux1[o] * acc - P.aux0[o] * P.rowvec[row];
+        const float4 pd = ld4(P.aux1 + o), pr = ld4(P.aux0 + o);
+        const float dl = P.rowvec[row];
+        return make_float4(pd.x * v.x - pr.x * dl, pd.y * v.y - pr.y * dl, pd.z * v.z - pr.z * dl,
+                           pd.w * v.w - pr.w * dl);
+    } else if constexpr (EPI == U2GNN_EPI_ACCUM) {
+        const float4 c = ld4(P.C + (int64_t)row * P.ldc + col);
+        return make_float4(c.x + P.alpha * v.x, c.y + P.alpha * v.y, c.z + P.alpha * v.z, c.w + P.alpha * v.w);
+    } else if constexpr (EPI == U2GNN_EPI_RELU_DROP_BWD) {
+        const float4 h = ld4(P.aux0 + (int64_t)row * P.ld_aux + col);
+        const float s = 1.f / (1.f - P.p);
+        return make_float4(h.x > 0.f ? v.x * s : 0.f, h.y > 0.f ? v.y * s : 0.f, h.z > 0.f ? v.z * s : 0.f,
+                           h.w > 0.f ? v.w * s : 0.f);
+    } else {  // bias epilogues: per-column dropout hash
+        const float4 b = ld4(P.bias + col);
+        float x[4] = {v.x + b.x, v.y + b.y, v.z + b.z, v.w + b.w};
+        if constexpr (EPI == U2GNN_EPI_BIAS) {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) x[c] = col + c < P.scale_cols ? x[c] * P.alpha : x[c];
+        } else {
+            if constexpr (EPI == U2GNN_EPI_BIAS_RELU_DROP) {
+#pragma unroll
+                for (int c = 0; c < 4; ++c) x[c] = fmaxf(x[c], 0.f);
+            }
+            if (P.p > 0.f) {
+                const float s = 1.f / (1.f - P.p);
+#pragma unroll
+                for (int c = 0; c < 4; ++c) x[c] = u2gnn_keep(P.seed, row, col + c, P.p) ? x[c] * s : 0.f;
+            }
+            if constexpr (EPI == U2GNN_EPI_BIAS_DROP_RESID) {
+                const float4 r = ld4(P.aux0 + (int64_t)row * P.ld_aux + col);
+                x[0] += r.x, x[1] += r.y, x[2] += r.z, x[3] += r.w;
+            }
+        }
+        return make_float4(x[0], x[1], x[2], x[3]);
     }
 }
 
-__device__ __forceinline__ void tile_coords(int gm, int gn, int &tm, int &tn) {
-    const int nwg = gm * gn;
+// 1-D grid over gm * gn * split blocks.  The hardware deals workgroups to the 8 XCDs round-robin
+// by linear id, so the bijective remap gives each XCD one contiguous range of logical ids; the
+// logical order is split-slowest, then 8-row-tile groups with the row tile fastest inside a
+// group.  Blocks that share an A row-panel or a B column-panel of the same K range therefore run
+// on the same XCD (one L2), and the large N^2 operands of the skinny attention products are
+// fetched from HBM once.
+__device__ __forceinline__ void tile_coords(int gm, int gn, int &tm, int &tn, int &z) {
+    const int ntile = gm * gn;
     const int bid = blockIdx.x;
-    const int q = nwg >> 3, r = nwg & 7, xcd = bid & 7, loc = bid >> 3;
+    const int total = (int)gridDim.x;
+    const int q = total >> 3, r = total & 7, xcd = bid & 7, loc = bid >> 3;
     const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+    z = wgid / ntile;
+    const int t = wgid - z * ntile;
     constexpr int GROUP = 8;
     const int per_group = GROUP * gn;
-    const int g = wgid / per_group;
+    const int g = t / per_group;
     const int first_m = g * GROUP;
     const int gsz = min(gm - first_m, GROUP);
-    const int in_g = wgid - g * per_group;
+    const int in_g = t - g * per_group;
     tm = first_m + in_g % gsz;
     tn = in_g / gsz;
 }
@@ -167,9 +197,10 @@ __global__ void __launch_bounds__(256) gemm_f32_kernel(GemmP P) {
 
     const int tid = threadIdx.x;
     int tmi, tni;
-    tile_coords(P.gm, P.gn, tmi, tni);
+    int zi;
+    tile_coords(P.gm, P.gn, tmi, tni, zi);
     const int m0 = tmi * BM, n0 = tni * BN;
-    const int64_t kbase = (int64_t)blockIdx.z * P.K;
+    const int64_t kbase = (int64_t)zi * P.K;
 
     const float *Ab = TA ? P.A + kbase * P.lda + m0 : P.A + (int64_t)m0 * P.lda + kbase;
     const float *Bb = TB ? P.B + (int64_t)n0 * P.ldb + kbase : P.B + kbase * P.ldb + n0;
@@ -212,22 +243,25 @@ __global__ void __launch_bounds__(256) gemm_f32_kernel(GemmP P) {
             for (int i = 0; i < TM; ++i)
 #pragma unroll
                 for (int j = 0; j < TN; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(b[j], a[i], acc[i][j], 0, 0, 0);  // C^T map
         }
         r2s<BM, BN, BK, SA, SB, TA, TB>(As0 + ((t + 1) & 1) * BK * SA, Bs0 + ((t + 1) & 1) * BK * SB, tid, ra, rb);
         __syncthreads();
     }
 
-    float *C = P.C + (int64_t)blockIdx.z * P.slab_stride;
+    // lane (li, kh) of tile (i, j) holds C[row = li][cols 8g + 4kh .. +3] in acc[4g .. 4g+3]
+    float *C = P.C + (int64_t)zi * P.slab_stride;
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int row = m0 + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
-                const int col = n0 + wn * WTN + j * 32 + li;
-                C[(int64_t)row * P.ldc + col] = epilogue<EPI>(P, row, col, acc[i][j][r]);
+            for (int g = 0; g < 4; ++g) {
+                const int row = m0 + wm * WTM + i * 32 + li;
+                const int col = n0 + wn * WTN + j * 32 + 8 * g + 4 * kh;
+                const float4 v = make_float4(acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2],
+                                             acc[i][j][4 * g + 3]);
+                *reinterpret_cast<float4 *>(C + (int64_t)row * P.ldc + col) = epilogue4<EPI>(P, row, col, v);
             }
 }
 
@@ -239,103 +273,172 @@ __global__ void __launch_bounds__(256) gemm_f32_kernel(GemmP P) {
 // relative error per product at 3 bf16 MFMAs (5.3x the fp32-MFMA rate).  fp32 operands are
 // split once per block while staging into LDS (register staging; the split is VALU work that
 // runs beside the matrix pipe), so HBM/L2 traffic is the fp32 operands themselves.
-// LDS holds both operands k-contiguous ([rows][BK+8] bf16: 80-byte rows make the
-// ds_read_b128 fragment reads conflict-free); [K][rows] layouts are transposed in registers
-// (4k x 4m micro-tiles) on the way in.
+// LDS images: an operand stored [rows][K] in HBM is staged k-contiguous ([rows][BK+8] bf16: 80-byte
+// rows make the ds_read_b128 fragment reads conflict-free); an operand stored [K][rows] is
+// staged as it lies, k-major ([BK][rows+32] bf16), and its MFMA fragments are gathered with the
+// gfx950 transpose read ds_read_b64_tr_b16 (two per fragment), so neither layout needs a
+// register transpose and both keep 16-byte-per-lane coalesced global loads.
 // ------------------------------------------------------------------------------------
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 
-template <int R, int BK, bool T>
-__device__ __forceinline__ void g2r_bf(const float *base, int64_t ld, int kt, int tid, float4 (&v)[R * BK / 1024]) {
-    constexpr int NF = R * BK / 1024;
+// LDS bank map of the staging stores (banks = dword mod 32 for ds_write):
+//  * [R][K] operands: 8 lanes x 16 B cover one row's 32 k; LDK = 40 bf16 = 20 dwords per row, so
+//    the 8 rows of a wave instruction are permuted (0,4,1,5,2,6,3,7): each 16-lane ds_write_b64
+//    group then pairs rows 4 apart (16 banks apart), 32 distinct banks;
+//  * [K][R] operands: 16 consecutive lanes store 16 x 8 B of one k-row, contiguous.
+// Transpose reads: a 32-lane half reads 4 k-rows x 32 columns; a row pitch of R+32 bf16 puts the
+// 4 rows 16 dwords apart mod 64, so the 64 dwords of the half hit 64 distinct banks.
+template <int BK, int NT>
+__device__ __forceinline__ void stage_rk(int tid, int i, int &r, int &kq) {
+    const int idx = tid + i * NT;
+    const int j = (idx / (BK / 4)) & 7;
+    r = (idx / (BK / 4)) - j + ((j >> 1) | ((j & 1) << 2));
+    kq = idx % (BK / 4);
+}
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+#ifdef U2GNN_EXP_NOSTAGE
+#define U2GNN_LOOP_SYNC() ((void)0)
+#else
+#define U2GNN_LOOP_SYNC() __syncthreads()
+#endif
+
+// Global->register staging through raw buffer loads: the per-thread byte offsets (voff) are
+// loop-invariant VGPRs, the K-tile advance is one scalar soffset (kt * kstep bytes), so a load
+// costs no 64-bit VALU address arithmetic.  The descriptor is built from the block's operand
+// base (kernarg + blockIdx only: wave-uniform, no waterfall).
+template <int R, int BK, bool T, int NT>
+__device__ __forceinline__ void g2r_init(int tid, int64_t ld, int (&voff)[R * BK / (4 * NT)]) {
+    constexpr int NF = R * BK / (4 * NT);
     if constexpr (!T) {  // global [R][K]
 #pragma unroll
         for (int i = 0; i < NF; ++i) {
-            const int idx = tid + i * 256;
-            const int r = idx / (BK / 4), kq = idx % (BK / 4);
-            v[i] = *reinterpret_cast<const float4 *>(base + (int64_t)r * ld + kt * BK + kq * 4);
+            int r, kq;
+            stage_rk<BK, NT>(tid, i, r, kq);
+            voff[i] = (int)(((int64_t)r * ld + kq * 4) * 4);
         }
-    } else {  // global [K][R]: NF k-rows x 4 columns per thread
+    } else {  // global [K][R]: NF k-rows x 4 columns per thread, columns fastest across lanes
         const int mg = tid % (R / 4), kg = tid / (R / 4);
 #pragma unroll
-        for (int q = 0; q < NF; ++q)
-            v[q] = *reinterpret_cast<const float4 *>(base + (int64_t)(kt * BK + kg * NF + q) * ld + mg * 4);
+        for (int q = 0; q < NF; ++q) voff[q] = (int)(((int64_t)(kg * NF + q) * ld + mg * 4) * 4);
     }
 }
 
-template <int R, int BK, int LDK, bool T, bool SPLIT>
-__device__ __forceinline__ void r2s_bf(__bf16 *hi, __bf16 *lo, int tid, const float4 (&v)[R * BK / 1024]) {
-    constexpr int NF = R * BK / 1024;
+template <int NF>
+__device__ __forceinline__ void g2r_bf(__amdgpu_buffer_rsrc_t rs, const int (&voff)[NF], int soff,
+                                       float4 (&v)[NF]) {
+#ifdef U2GNN_EXP_NOLOAD
+    if (soff > 0) return;
+#endif
+#pragma unroll
+    for (int i = 0; i < NF; ++i) {
+        const u32x4 u = __builtin_amdgcn_raw_buffer_load_b128(rs, voff[i], soff, 0);
+        v[i] = make_float4(__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w));
+    }
+}
+
+// (x0, x1) -> packed bf16 hi pair and, for SPLIT, the packed bf16 residual pair:
+// one v_cvt_pk_bf16_f32, two bit ops, two subtractions, one more cvt_pk (3 VALU / element).
+template <bool SPLIT>
+__device__ __forceinline__ void split2(float x0, float x1, unsigned &h, unsigned &l) {
+    // opaque to the optimizer: otherwise it re-derives bf16(x0) with a second cvt instead of
+    // shifting the packed pair
+#ifdef U2GNN_EXP_NOSPLIT
+    h = __float_as_uint(x0) ^ __float_as_uint(x1); l = h; return;
+#endif
+    asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(h) : "v"(x0), "v"(x1));
+    if constexpr (SPLIT) {
+        const float l0 = x0 - __uint_as_float(h << 16), l1 = x1 - __uint_as_float(h & 0xffff0000u);
+        l = __builtin_bit_cast(unsigned, bf16x2{(__bf16)l0, (__bf16)l1});
+    }
+}
+
+template <int R, int BK, int LDK, bool T, bool SPLIT, int NT>
+__device__ __forceinline__ void r2s_bf(__bf16 *hi, __bf16 *lo, int tid, const float4 (&v)[R * BK / (4 * NT)]) {
+    constexpr int NF = R * BK / (4 * NT);
+#ifdef U2GNN_EXP_NOSTAGE
+    return;
+#endif
     if constexpr (!T) {
 #pragma unroll
         for (int i = 0; i < NF; ++i) {
-            const int idx = tid + i * 256;
-            const int r = idx / (BK / 4), kq = idx % (BK / 4);
-            const float x[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
-            bf16x4 h, l;
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                h[c] = (__bf16)x[c];
-                l[c] = (__bf16)(x[c] - (float)h[c]);
-            }
-            *reinterpret_cast<bf16x4 *>(hi + r * LDK + kq * 4) = h;
-            if constexpr (SPLIT) *reinterpret_cast<bf16x4 *>(lo + r * LDK + kq * 4) = l;
+            int r, kq;
+            stage_rk<BK, NT>(tid, i, r, kq);
+            uint2 h, l;
+            split2<SPLIT>(v[i].x, v[i].y, h.x, l.x);
+            split2<SPLIT>(v[i].z, v[i].w, h.y, l.y);
+            *reinterpret_cast<uint2 *>(hi + r * LDK + kq * 4) = h;
+            if constexpr (SPLIT) *reinterpret_cast<uint2 *>(lo + r * LDK + kq * 4) = l;
         }
-    } else {
+    } else {  // k-major image [BK][R + 32]
+        constexpr int S = R + 32;
         const int mg = tid % (R / 4), kg = tid / (R / 4);
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            float x[NF];
-#pragma unroll
-            for (int q = 0; q < NF; ++q) x[q] = c == 0 ? v[q].x : c == 1 ? v[q].y : c == 2 ? v[q].z : v[q].w;
-            __bf16 *dh = hi + (mg * 4 + c) * LDK + kg * NF;
-            __bf16 *dl = lo + (mg * 4 + c) * LDK + kg * NF;
-            if constexpr (NF == 4) {
-                bf16x4 h, l;
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    h[q] = (__bf16)x[q];
-                    l[q] = (__bf16)(x[q] - (float)h[q]);
-                }
-                *reinterpret_cast<bf16x4 *>(dh) = h;
-                if constexpr (SPLIT) *reinterpret_cast<bf16x4 *>(dl) = l;
-            } else {
-                static_assert(NF == 2, "bf16 staging supports 64- and 128-row tiles");
-                bf16x2 h, l;
-#pragma unroll
-                for (int q = 0; q < 2; ++q) {
-                    h[q] = (__bf16)x[q];
-                    l[q] = (__bf16)(x[q] - (float)h[q]);
-                }
-                *reinterpret_cast<bf16x2 *>(dh) = h;
-                if constexpr (SPLIT) *reinterpret_cast<bf16x2 *>(dl) = l;
-            }
+        for (int q = 0; q < NF; ++q) {
+            uint2 h, l;
+            split2<SPLIT>(v[q].x, v[q].y, h.x, l.x);
+            split2<SPLIT>(v[q].z, v[q].w, h.y, l.y);
+            const int o = (kg * NF + q) * S + mg * 4;
+            *reinterpret_cast<uint2 *>(hi + o) = h;
+            if constexpr (SPLIT) *reinterpret_cast<uint2 *>(lo + o) = l;
         }
     }
 }
 
-template <int BM, int BN, bool TA, bool TB, int EPI, bool SPLIT>
-__global__ void __launch_bounds__(256) gemm_bf16_kernel(GemmP P) {
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+// One 32x32x16 MFMA operand fragment (lane l: row r0 + l%32, k = ks*16 + 8*(l/32) .. +7).
+template <int R, int LDK, bool T>
+__device__ __forceinline__ bf16x8 ld_frag(const __bf16 *img, int r0, int ks, int lane) {
+    if constexpr (!T) {
+        return *reinterpret_cast<const bf16x8 *>(img + (r0 + (lane & 31)) * LDK + ks * 16 + (lane >> 5) * 8);
+    } else {
+        // ds_read_b64_tr_b16: within each 16-lane group, lane 4q+p addresses k-row q, columns
+        // 4p..4p+3 of a 4 x 16 block and receives column (lane % 16) of the 4 rows
+        constexpr int S = R + 32;
+        const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+        const __bf16 *a = img + (ks * 16 + (g >> 1) * 8 + q) * S + r0 + (g & 1) * 16 + 4 * p;
+        const s16x4 x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)a);
+        const s16x4 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(a + 4 * S));
+        const s16x4 v[2] = {x0, x1};
+        return __builtin_bit_cast(bf16x8, v);
+    }
+}
+
+template <int BM, int BN, int WM, int WN, bool TA, bool TB, int EPI, bool SPLIT>
+__global__ void __launch_bounds__(64 * WM * WN) gemm_bf16_kernel(GemmP P) {
+    constexpr int NT = 64 * WM * WN;
     constexpr int BK = 32;
     constexpr int LDK = BK + 8;
-    constexpr int WTM = BM / 2, WTN = BN / 2;
+    constexpr int WTM = BM / WM, WTN = BN / WN;
     constexpr int TM = WTM / 32, TN = WTN / 32;
-    constexpr int NFA = BM * BK / 1024, NFB = BN * BK / 1024;
-    constexpr int AE = BM * LDK, BE = BN * LDK;
+    constexpr int NFA = BM * BK / (4 * NT), NFB = BN * BK / (4 * NT);
+    constexpr int AE = TA ? BK * (BM + 32) : BM * LDK;    // elements per plane, per operand
+    constexpr int BE = !TB ? BK * (BN + 32) : BN * LDK;
     constexpr int STAGE = 2 * (AE + BE);  // hi + lo of A and B
     __shared__ __attribute__((aligned(16))) __bf16 smem[2 * STAGE];
 
     const int tid = threadIdx.x;
     int tmi, tni;
-    tile_coords(P.gm, P.gn, tmi, tni);
+    int zi;
+    tile_coords(P.gm, P.gn, tmi, tni, zi);
     const int m0 = tmi * BM, n0 = tni * BN;
-    const int64_t kbase = (int64_t)blockIdx.z * P.K;
+    const int64_t kbase = (int64_t)zi * P.K;
     const int64_t klen = min((int64_t)P.K, (int64_t)P.Ktot - kbase);
     const int nk = klen > 0 ? (int)(klen / BK) : 0;   // ragged last split; empty splits write 0
     const float *Ab = TA ? P.A + kbase * P.lda + m0 : P.A + (int64_t)m0 * P.lda + kbase;
     const float *Bb = TB ? P.B + (int64_t)n0 * P.ldb + kbase : P.B + kbase * P.ldb + n0;
+    const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void *)Ab, 0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void *)Bb, 0, 0x7fffffff, 0x00020000);
+    const int kstepA = TA ? (int)(BK * P.lda * 4) : BK * 4;   // bytes per K tile
+    const int kstepB = TB ? BK * 4 : (int)(BK * P.ldb * 4);
+    int voA[NFA], voB[NFB];
+    g2r_init<BM, BK, TA, NT>(tid, P.lda, voA);
+    g2r_init<BN, BK, !TB, NT>(tid, P.ldb, voB);
 
     f32x16 acc[TM][TN];
 #pragma unroll
@@ -346,7 +449,7 @@ __global__ void __launch_bounds__(256) gemm_bf16_kernel(GemmP P) {
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
     const int wave = tid >> 6, lane = tid & 63;
-    const int wm = wave >> 1, wn = wave & 1;
+    const int wm = wave / WN, wn = wave % WN;
     const int kh = lane >> 5, li = lane & 31;
 
     auto stage = [&](int s) { return smem + s * STAGE; };
@@ -357,25 +460,25 @@ __global__ void __launch_bounds__(256) gemm_bf16_kernel(GemmP P) {
             bf16x8 ah[TM], al[TM], bh[TN], bl[TN];
 #pragma unroll
             for (int i = 0; i < TM; ++i) {
-                const int o = (wm * WTM + i * 32 + li) * LDK + ks * 16 + kh * 8;
-                ah[i] = *reinterpret_cast<const bf16x8 *>(Ah + o);
-                if constexpr (SPLIT) al[i] = *reinterpret_cast<const bf16x8 *>(Al + o);
+                ah[i] = ld_frag<BM, LDK, TA>(Ah, wm * WTM + i * 32, ks, lane);
+                if constexpr (SPLIT) al[i] = ld_frag<BM, LDK, TA>(Al, wm * WTM + i * 32, ks, lane);
             }
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
-                const int o = (wn * WTN + j * 32 + li) * LDK + ks * 16 + kh * 8;
-                bh[j] = *reinterpret_cast<const bf16x8 *>(Bh + o);
-                if constexpr (SPLIT) bl[j] = *reinterpret_cast<const bf16x8 *>(Bl + o);
+                bh[j] = ld_frag<BN, LDK, !TB>(Bh, wn * WTN + j * 32, ks, lane);
+                if constexpr (SPLIT) bl[j] = ld_frag<BN, LDK, !TB>(Bl, wn * WTN + j * 32, ks, lane);
             }
 #pragma unroll
             for (int i = 0; i < TM; ++i)
 #pragma unroll
                 for (int j = 0; j < TN; ++j) {
+                    // B fragment first: the accumulator holds the tile transposed, so each lane
+                    // owns 4 consecutive output columns of one row (16-byte epilogue accesses)
                     if constexpr (SPLIT) {
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bh[j], al[i], acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bl[j], ah[i], acc[i][j], 0, 0, 0);
                     }
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bh[j], ah[i], acc[i][j], 0, 0, 0);
                 }
         }
     };
@@ -384,56 +487,61 @@ __global__ void __launch_bounds__(256) gemm_bf16_kernel(GemmP P) {
         // two register stages: every tile's global loads are in flight across TWO compute phases
         // (a single phase of 24 MFMAs does not cover an L2/LLC miss at 2 waves per SIMD)
         float4 ra0[NFA], rb0[NFB], ra1[NFA], rb1[NFB];
-        g2r_bf<BM, BK, TA>(Ab, P.lda, 0, tid, ra0);
-        g2r_bf<BN, BK, !TB>(Bb, P.ldb, 0, tid, rb0);
-        g2r_bf<BM, BK, TA>(Ab, P.lda, min(1, nk - 1), tid, ra1);
-        g2r_bf<BN, BK, !TB>(Bb, P.ldb, min(1, nk - 1), tid, rb1);
-        r2s_bf<BM, BK, LDK, TA, SPLIT>(stage(0), stage(0) + AE, tid, ra0);
-        r2s_bf<BN, BK, LDK, !TB, SPLIT>(stage(0) + 2 * AE, stage(0) + 2 * AE + BE, tid, rb0);
+        g2r_bf<NFA>(rsA, voA, (0) * kstepA, ra0);
+        g2r_bf<NFB>(rsB, voB, (0) * kstepB, rb0);
+        g2r_bf<NFA>(rsA, voA, (min(1, nk - 1)) * kstepA, ra1);
+        g2r_bf<NFB>(rsB, voB, (min(1, nk - 1)) * kstepB, rb1);
+        r2s_bf<BM, BK, LDK, TA, SPLIT, NT>(stage(0), stage(0) + AE, tid, ra0);
+        r2s_bf<BN, BK, LDK, !TB, SPLIT, NT>(stage(0) + 2 * AE, stage(0) + 2 * AE + BE, tid, rb0);
         __syncthreads();
         for (int t = 0; t < nk; t += 2) {
-            g2r_bf<BM, BK, TA>(Ab, P.lda, min(t + 2, nk - 1), tid, ra0);
-            g2r_bf<BN, BK, !TB>(Bb, P.ldb, min(t + 2, nk - 1), tid, rb0);
+            g2r_bf<NFA>(rsA, voA, (min(t + 2, nk - 1)) * kstepA, ra0);
+            g2r_bf<NFB>(rsB, voB, (min(t + 2, nk - 1)) * kstepB, rb0);
             compute(stage(0));
-            r2s_bf<BM, BK, LDK, TA, SPLIT>(stage(1), stage(1) + AE, tid, ra1);
-            r2s_bf<BN, BK, LDK, !TB, SPLIT>(stage(1) + 2 * AE, stage(1) + 2 * AE + BE, tid, rb1);
-            __syncthreads();
+            r2s_bf<BM, BK, LDK, TA, SPLIT, NT>(stage(1), stage(1) + AE, tid, ra1);
+            r2s_bf<BN, BK, LDK, !TB, SPLIT, NT>(stage(1) + 2 * AE, stage(1) + 2 * AE + BE, tid, rb1);
+            U2GNN_LOOP_SYNC();
             if (t + 1 < nk) {
-                g2r_bf<BM, BK, TA>(Ab, P.lda, min(t + 3, nk - 1), tid, ra1);
-                g2r_bf<BN, BK, !TB>(Bb, P.ldb, min(t + 3, nk - 1), tid, rb1);
+                g2r_bf<NFA>(rsA, voA, (min(t + 3, nk - 1)) * kstepA, ra1);
+                g2r_bf<NFB>(rsB, voB, (min(t + 3, nk - 1)) * kstepB, rb1);
                 compute(stage(1));
-                r2s_bf<BM, BK, LDK, TA, SPLIT>(stage(0), stage(0) + AE, tid, ra0);
-                r2s_bf<BN, BK, LDK, !TB, SPLIT>(stage(0) + 2 * AE, stage(0) + 2 * AE + BE, tid, rb0);
-                __syncthreads();
+                r2s_bf<BM, BK, LDK, TA, SPLIT, NT>(stage(0), stage(0) + AE, tid, ra0);
+                r2s_bf<BN, BK, LDK, !TB, SPLIT, NT>(stage(0) + 2 * AE, stage(0) + 2 * AE + BE, tid, rb0);
+                U2GNN_LOOP_SYNC();
             }
         }
     }
 
-    float *C = P.C + (int64_t)blockIdx.z * P.slab_stride;
+    // lane (li, kh) of tile (i, j) holds C[row = li][cols 8g + 4kh .. +3] in acc[4g .. 4g+3]
+    float *C = P.C + (int64_t)zi * P.slab_stride;
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int row = m0 + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
-                const int col = n0 + wn * WTN + j * 32 + li;
-                C[(int64_t)row * P.ldc + col] = epilogue<EPI>(P, row, col, acc[i][j][r]);
+            for (int g = 0; g < 4; ++g) {
+                const int row = m0 + wm * WTM + i * 32 + li;
+                const int col = n0 + wn * WTN + j * 32 + 8 * g + 4 * kh;
+                const float4 v = make_float4(acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2],
+                                             acc[i][j][4 * g + 3]);
+                *reinterpret_cast<float4 *>(C + (int64_t)row * P.ldc + col) = epilogue4<EPI>(P, row, col, v);
             }
 }
 
 template <int KIND, int BM, int BN, bool TA, bool TB, int EPI>
 void launch_kernel(const GemmP &P, dim3 grid, hipStream_t st) {
-    if constexpr (KIND == U2GNN_PREC_F32)
+    if constexpr (KIND == U2GNN_PREC_F32) {
         hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, TA, TB, EPI>), grid, dim3(256), 0, st, P);
-    else
-        hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, TA, TB, EPI, KIND == U2GNN_PREC_BF16X3>), grid, dim3(256), 0, st,
-                           P);
+    } else {
+        constexpr int WM = BM == 256 ? 4 : 2, WN = 2;   // 256x128 tiles run 8 waves (4x2)
+        hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, WM, WN, TA, TB, EPI, KIND == U2GNN_PREC_BF16X3>), grid,
+                           dim3(64 * WM * WN), 0, st, P);
+    }
 }
 
 template <int KIND, int BM, int BN, bool TA, bool TB>
 int launch_epi(const GemmP &P, int epi, int split, hipStream_t st) {
-    dim3 grid(P.gm * P.gn, 1, split);
+    dim3 grid(P.gm * P.gn * split);
     switch (epi) {
 #define U2GNN_CASE(E)                                          \
     case E:                                                    \
@@ -463,6 +571,8 @@ int launch_layout(const GemmP &P, bool ta, bool tb, int epi, int split, hipStrea
 
 template <int KIND>
 int launch_tile(const GemmP &P, int tile, bool ta, bool tb, int epi, int split, hipStream_t st) {
+    if constexpr (KIND != U2GNN_PREC_F32)
+        if (tile == 256) return launch_layout<KIND, 256, 128>(P, ta, tb, epi, split, st);
     if (tile == 128) return launch_layout<KIND, 128, 128>(P, ta, tb, epi, split, st);
     return launch_layout<KIND, 64, 64>(P, ta, tb, epi, split, st);
 }
@@ -482,6 +592,15 @@ extern "C" int u2gnn_gemm(const u2gnn_gemm_args *a, void *stream) {
     if (!al16(a->A) || !al16(a->B) || (a->lda & 3) || (a->ldb & 3)) return U2GNN_E_ALIGN;
     const int bk = prec == U2GNN_PREC_F32 ? 16 : 32;
     if (a->K % bk) return U2GNN_E_SHAPE;
+    if (prec != U2GNN_PREC_F32) {   // bf16 staging addresses operands by 32-bit buffer offsets
+        const int64_t span = ((int64_t)a->K + 256) * (a->lda > a->ldb ? a->lda : a->ldb) * 4;
+        if (span >= (int64_t)INT32_MAX) return U2GNN_E_SHAPE;
+    }
+    // 16-byte epilogue: C, bias and aux rows are read/written as float4
+    if (!al16(a->C) || (a->ldc & 3) || (split > 1 && (a->slab_stride & 3))) return U2GNN_E_ALIGN;
+    if ((a->bias && !al16(a->bias)) || (a->aux0 && !al16(a->aux0)) || (a->aux1 && !al16(a->aux1)) ||
+        ((a->aux0 || a->aux1) && (a->ld_aux & 3)))
+        return U2GNN_E_ALIGN;
     const int e = a->epilogue;
     if ((e == U2GNN_EPI_BIAS || e == U2GNN_EPI_BIAS_DROP_RESID || e == U2GNN_EPI_BIAS_RELU_DROP) && !a->bias)
         return U2GNN_E_ARG;
@@ -494,8 +613,10 @@ extern "C" int u2gnn_gemm(const u2gnn_gemm_args *a, void *stream) {
         const int64_t blocks128 = can128 ? (a->M / 128) * (a->N / 128) * split : 0;
         tile = (can128 && blocks128 >= 480) ? 128 : 64;
     }
-    if (tile != 64 && tile != 128) return U2GNN_E_ARG;
-    if (a->M % tile || a->N % tile) return U2GNN_E_SHAPE;
+    if (tile != 64 && tile != 128 && tile != 256) return U2GNN_E_ARG;
+    if (tile == 256 && prec == U2GNN_PREC_F32) return U2GNN_E_ARG;
+    const int tile_n = tile == 256 ? 128 : tile;   // "256" = 256x128 block (bf16 modes)
+    if (a->M % tile || a->N % tile_n) return U2GNN_E_SHAPE;
     GemmP P;
     P.A = a->A;
     P.B = a->B;
@@ -510,7 +631,7 @@ extern "C" int u2gnn_gemm(const u2gnn_gemm_args *a, void *stream) {
     P.K = (int32_t)((a->K + (int64_t)split * bk - 1) / ((int64_t)split * bk) * bk);
     P.Ktot = (int32_t)a->K;
     P.gm = (int32_t)(a->M / tile);
-    P.gn = (int32_t)(a->N / tile);
+    P.gn = (int32_t)(a->N / tile_n);
     P.slab_stride = a->slab_stride;
     P.bias = a->bias;
     P.aux0 = a->aux0;

@@ -15,7 +15,8 @@ PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REPO_ROOT = os.path.dirname(PKG_ROOT)
 LIB_DIR = os.path.join(PKG_ROOT, "lib")
 INCLUDE_DIR = os.path.join(REPO_ROOT, "include")
-HIP_LIB_PATH = os.path.join(LIB_DIR, "libu2gnn_hip.so")
+# U2GNN_HIP_LIB: an alternative build of the same kernels (tools/ experiments)
+HIP_LIB_PATH = os.environ.get("U2GNN_HIP_LIB") or os.path.join(LIB_DIR, "libu2gnn_hip.so")
 LUS_LIB_PATH = os.path.join(LIB_DIR, "libu2gnn_lus.so")
 
 

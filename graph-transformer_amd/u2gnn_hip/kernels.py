@@ -59,7 +59,8 @@ def gemm_symbol(precision, M, N, split_k, tile, trans_a, trans_b, epilogue):
     b = lambda x: "true" if x else "false"  # noqa: E731
     if precision == "fp32":
         return f"gemm_f32_kernel<{tile}, {tile}, {b(trans_a)}, {b(trans_b)}, {int(epilogue)}>"
-    return (f"gemm_bf16_kernel<{tile}, {tile}, {b(trans_a)}, {b(trans_b)}, {int(epilogue)}, "
+    bm, bn, wm = (256, 128, 4) if tile == 256 else (tile, tile, 2)   # "256" = 256x128 block, 4x2 waves
+    return (f"gemm_bf16_kernel<{bm}, {bn}, {wm}, 2, {b(trans_a)}, {b(trans_b)}, {int(epilogue)}, "
             f"{b(precision == 'bf16x3')}>")   # the C++ template instance as rocprofv3 names it
 
 

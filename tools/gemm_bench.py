@@ -1,5 +1,5 @@
-"""GEMM micro-benchmark on the C4 attention / weight-gradient shapes (device time via HIP events).
-Usage: python tools/gemm_bench.py [precision ...]"""
+"""GEMM micro-benchmark on the C4 attention / projection / weight-gradient shapes: device time of
+u2gnn_gemm per (precision, tile, split) via HIP events.  Usage: python tools/gemm_bench.py [prec ...]"""
 import os
 import sys
 
@@ -9,38 +9,58 @@ import torch  # noqa: E402
 from u2gnn_hip import kernels as K  # noqa: E402
 
 Np, dp, ffp = 4864, 384, 1024
-SHAPES = [  # name, M, N, K, ta, tb, split, tile
-    ("QK^T  NT", Np, Np, dp, False, True, 1, 128),
-    ("P.V   NN", Np, dp, Np, False, False, 4, 128),
-    ("dV    TN", Np, dp, Np, True, False, 4, 128),
-    ("dWin  TN", 3 * dp, dp, Np, True, False, 16, 128),
-    ("dW1   TN", ffp, dp, Np, True, False, 16, 128),
-    ("QKV   NT", Np, 3 * dp, dp, False, True, 1, 64),
-    ("FFN1  NT", Np, ffp, dp, False, True, 1, 64),
-    ("FFN2  NT", Np, dp, ffp, False, True, 1, 64),
+SHAPES = [  # name, M, N, K, ta, tb, [(split, tile), ...]
+    ("QK^T  NT", Np, Np, dp, False, True, [(1, 128), (1, 256)]),
+    ("dS    NT", Np, Np, dp, False, True, [(1, 128), (1, 256)], 6),   # dO.V^T with the attention-dS epilogue
+    ("P.V   NN", Np, dp, Np, False, False, [(4, 128), (8, 256), (4, 256)]),
+    ("dV    TN", Np, dp, Np, True, False, [(4, 128), (8, 256), (4, 256)]),
+    ("dWin  TN", 3 * dp, dp, Np, True, False, [(16, 128), (8, 128)]),
+    ("dW1   TN", ffp, dp, Np, True, False, [(16, 128), (8, 256)]),
+    ("QKV   NT", Np, 3 * dp, dp, False, True, [(1, 64), (1, 128), (1, 256)]),
+    ("FFN1  NT", Np, ffp, dp, False, True, [(1, 64), (1, 128), (1, 256)]),
+    ("FFN2  NT", Np, dp, ffp, False, True, [(1, 64), (1, 128)]),
 ]
+
+
+ONLY = os.environ.get("GB_ONLY")  # e.g. "QK^T,dV": restrict to shapes whose name starts with one of these
+REPS = int(os.environ.get("GB_REPS", "20"))
 
 
 def run(prec):
     g = torch.Generator(device="cuda").manual_seed(0)
-    for name, M, N, Kd, ta, tb, split, tile in SHAPES:
+    for name, M, N, Kd, ta, tb, cfgs, *epi in SHAPES:
+        epi = epi[0] if epi else 0
+        ext = {}
+        if epi == 6:
+            ext = dict(epilogue=6, aux0=torch.rand(M, N, device="cuda", generator=g),
+                       aux1=torch.rand(M, N, device="cuda", generator=g),
+                       rowvec=torch.randn(M, device="cuda", generator=g), ld_aux=N)
+        if ONLY and not any(name.startswith(o) for o in ONLY.split(",")):
+            continue
         A = torch.randn(Kd, M, device="cuda", generator=g) if ta else torch.randn(M, Kd, device="cuda", generator=g)
         B = torch.randn(N, Kd, device="cuda", generator=g) if tb else torch.randn(Kd, N, device="cuda", generator=g)
-        C = torch.empty(split, M, N, device="cuda")
-        f = lambda: K.gemm(A, B, C, M, N, Kd, A.shape[1], B.shape[1], N, trans_a=ta, trans_b=tb, split_k=split,  # noqa
-                           slab_stride=M * N, tile=tile, precision=prec)
-        for _ in range(3):
-            f()
-        torch.cuda.synchronize()
-        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        s.record()
-        for _ in range(20):
-            f()
-        e.record()
-        torch.cuda.synchronize()
-        us = s.elapsed_time(e) / 20 * 1e3
-        print(f"{prec:7s} {name}  M={M:5d} N={N:5d} K={Kd:5d} split={split:2d} tile={tile:3d}: {us:8.1f} us "
-              f"{2.0 * M * N * Kd / us / 1e6:7.1f} TF/s")
+        for split, tile in cfgs:
+            if prec == "fp32" and tile == 256:
+                continue
+            C = torch.empty(split, M, N, device="cuda")
+            f = lambda: K.gemm(A, B, C, M, N, Kd, A.shape[1], B.shape[1], N, trans_a=ta, trans_b=tb,  # noqa: E731
+                               split_k=split, slab_stride=M * N, tile=tile, precision=prec, **ext)
+            for _ in range(3):
+                f()
+            torch.cuda.synchronize()
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(REPS):
+                f()
+            e.record()
+            torch.cuda.synchronize()
+            us = s.elapsed_time(e) / REPS * 1e3
+            ref = (A.t() if ta else A).double() @ (B.t() if tb else B).double()
+            if epi == 6:
+                ref = ext["aux1"].double() * ref - ext["aux0"].double() * ext["rowvec"].double()[:, None]
+            err = ((C.sum(0).double() - ref).abs().max() / ref.abs().max()).item()
+            print(f"{prec:7s} {name}  M={M:5d} N={N:5d} K={Kd:5d} split={split:2d} tile={tile:3d}: {us:8.1f} us "
+                  f"{2.0 * M * N * Kd / us / 1e6:7.1f} TF/s  relerr {err:.1e}")
 
 
 if __name__ == "__main__":

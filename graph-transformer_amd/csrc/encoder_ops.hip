@@ -48,22 +48,51 @@ __global__ void __launch_bounds__(256) scatter_add_rows_kernel(const float *src,
 // ------------------------------------------------------------------------------------------
 // split-K slab reduce + padded->real unpack; pack real->padded
 // ------------------------------------------------------------------------------------------
+__device__ __forceinline__ float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
+__device__ __forceinline__ float4 add4(float4 a, float4 b) { return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); }
+
+// One wave per padded row, a float4 of columns per lane; the slab loop keeps 4 independent
+// 16-byte loads in flight.  Rows/columns outside the real blocks are skipped; the real
+// destination is written with 16-byte stores when the column map is the identity and aligned.
 __global__ void __launch_bounds__(256) slab_reduce_kernel(const float *src, int n_slab, int64_t slab_stride,
                                                           int64_t rows_pad, int64_t cols_pad, int64_t ld_src,
                                                           int64_t rbp, int64_t rbr, int64_t cbp, int64_t cbr,
-                                                          float *dst, int64_t ld_dst, float alpha, int accumulate) {
-    const int64_t total = rows_pad * cols_pad;
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
-        const int64_t r = i / cols_pad, c = i - r * cols_pad;
-        bool vr, vc;
-        const int64_t rr = blk_map(r, rbp, rbr, &vr);
-        const int64_t cc = blk_map(c, cbp, cbr, &vc);
-        if (!vr || !vc) continue;
-        float s = 0.f;
+                                                          float *dst, int64_t ld_dst, float alpha, int accumulate,
+                                                          int vec_store) {
+    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (r >= rows_pad) return;
+    bool vr;
+    const int64_t rr = blk_map(r, rbp, rbr, &vr);
+    if (!vr) return;
+    for (int64_t c = (int64_t)lane * 4; c < cols_pad; c += 256) {
         const float *p = src + r * ld_src + c;
-        for (int z = 0; z < n_slab; ++z) s += p[(int64_t)z * slab_stride];
-        float *o = dst + rr * ld_dst + cc;
-        *o = accumulate ? *o + alpha * s : alpha * s;
+        float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a, e = a, f = a;
+        int z = 0;
+        for (; z + 4 <= n_slab; z += 4) {
+            a = add4(a, ld4(p + (int64_t)z * slab_stride));
+            b = add4(b, ld4(p + (int64_t)(z + 1) * slab_stride));
+            e = add4(e, ld4(p + (int64_t)(z + 2) * slab_stride));
+            f = add4(f, ld4(p + (int64_t)(z + 3) * slab_stride));
+        }
+        for (; z < n_slab; ++z) a = add4(a, ld4(p + (int64_t)z * slab_stride));
+        const float4 t = add4(add4(a, b), add4(e, f));
+        if (vec_store) {
+            float *o = dst + rr * ld_dst + c;
+            float4 v = make_float4(alpha * t.x, alpha * t.y, alpha * t.z, alpha * t.w);
+            if (accumulate) v = add4(v, ld4(o));
+            *reinterpret_cast<float4 *>(o) = v;
+        } else {
+            const float x[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                bool vc;
+                const int64_t cc = blk_map(c + q, cbp, cbr, &vc);
+                if (!vc) continue;
+                float *o = dst + rr * ld_dst + cc;
+                *o = accumulate ? *o + alpha * x[q] : alpha * x[q];
+            }
+        }
     }
 }
 
@@ -98,48 +127,72 @@ __global__ void __launch_bounds__(256) pack_multi_kernel(PackBatch pb) {
     }
 }
 
-// column sums, stage 1: block (64 columns x CS_ROWS rows) -> ws[chunk][col].  Each wave owns 32
-// consecutive rows and keeps 8 independent loads in flight (latency, not bandwidth, bounds this).
-constexpr int CS_ROWS = 128;
+// column sums, stage 1: block = CS_ROWS rows x 256 columns; each lane owns a float4 of columns,
+// each wave CS_ROWS/4 rows (all its loads in flight at once), ws[chunk][col] via LDS.  Small row
+// chunks give ~Np/16 x cols/256 blocks, enough waves to cover HBM latency.
+constexpr int CS_ROWS = 16;
 
 __global__ void __launch_bounds__(256) colsum_partial_kernel(const float *X, int64_t rows, int64_t cols_pad,
                                                              int64_t ld, float *ws) {
+    __shared__ float4 red[4][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t c = ((int64_t)blockIdx.x * 64 + lane) * 4;
+    const int64_t r0 = (int64_t)blockIdx.y * CS_ROWS + w * (CS_ROWS / 4);
+    float4 v[CS_ROWS / 4];
+#pragma unroll
+    for (int j = 0; j < CS_ROWS / 4; ++j)
+        v[j] = (c < cols_pad && r0 + j < rows) ? ld4(X + (r0 + j) * ld + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    red[w][lane] = add4(add4(v[0], v[1]), add4(v[2], v[3]));
+    __syncthreads();
+    if (w == 0 && c < cols_pad)
+        *reinterpret_cast<float4 *>(ws + (int64_t)blockIdx.y * cols_pad + c) =
+            add4(add4(red[0][lane], red[1][lane]), add4(red[2][lane], red[3][lane]));
+}
+
+// the same partial sums for operands that are not float4-addressable (e.g. a column vector):
+// lane = column, wave w sums rows r0 + w*CS_ROWS/4 ...
+__global__ void __launch_bounds__(256) colsum_partial_scalar_kernel(const float *X, int64_t rows, int64_t cols_pad,
+                                                                    int64_t ld, float *ws) {
     __shared__ float red[4][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int64_t c = (int64_t)blockIdx.x * 64 + lane;
     const int64_t r0 = (int64_t)blockIdx.y * CS_ROWS + w * (CS_ROWS / 4);
-    float s[8];
+    float v[CS_ROWS / 4];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) s[j] = 0.f;
-    if (c < cols_pad) {
-#pragma unroll
-        for (int i = 0; i < CS_ROWS / 4; i += 8)
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int64_t r = r0 + i + j;
-                if (r < rows) s[j] += X[r * ld + c];
-            }
-    }
-    red[w][lane] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+    for (int j = 0; j < CS_ROWS / 4; ++j) v[j] = (c < cols_pad && r0 + j < rows) ? X[(r0 + j) * ld + c] : 0.f;
+    red[w][lane] = (v[0] + v[1]) + (v[2] + v[3]);
     __syncthreads();
     if (w == 0 && c < cols_pad)
-        ws[(int64_t)blockIdx.y * cols_pad + c] = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+        ws[(int64_t)blockIdx.y * cols_pad + c] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
 }
+
+// stage 2: block = 16 columns x 16 chunk strides (thread t: column t%16, chunks t/16, t/16+16, ...),
+// then a fixed-order LDS combine (deterministic).  ~cols/16 blocks keep the serial chain short.
+constexpr int FIN_COLS = 16;
 
 __global__ void __launch_bounds__(256) colsum_final_kernel(const float *ws, int64_t n_chunks, int64_t cols_pad,
                                                            int64_t cbp, int64_t cbr, float *out, int accumulate) {
-    const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (c >= cols_pad) return;
+    __shared__ float red[16][FIN_COLS + 1];
+    const int cl = threadIdx.x % FIN_COLS, kg = threadIdx.x / FIN_COLS;
+    const int64_t c = (int64_t)blockIdx.x * FIN_COLS + cl;
+    float s[2] = {0.f, 0.f};
+    if (c < cols_pad) {
+        int64_t k = kg;
+        for (; k + 16 < n_chunks; k += 32) {
+            s[0] += ws[k * cols_pad + c];
+            s[1] += ws[(k + 16) * cols_pad + c];
+        }
+        for (; k < n_chunks; k += 16) s[0] += ws[k * cols_pad + c];
+    }
+    red[kg][cl] = s[0] + s[1];
+    __syncthreads();
+    if (kg != 0 || c >= cols_pad) return;
     bool v;
     const int64_t cc = blk_map(c, cbp, cbr, &v);
     if (!v) return;
-    float s[4] = {0.f, 0.f, 0.f, 0.f};
-    int64_t k = 0;
-    for (; k + 4 <= n_chunks; k += 4)
+    float t = 0.f;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) s[j] += ws[(k + j) * cols_pad + c];
-    for (; k < n_chunks; ++k) s[0] += ws[k * cols_pad + c];
-    const float t = (s[0] + s[1]) + (s[2] + s[3]);
+    for (int j = 0; j < 16; ++j) t += red[j][cl];
     out[cc] = accumulate ? out[cc] + t : t;
 }
 
@@ -219,74 +272,90 @@ __global__ void __launch_bounds__(256) rowdot_kernel(const float *A, int64_t lda
 }
 
 // ------------------------------------------------------------------------------------------
-// a3.3/a3.4 post-LN (eps 1e-5). One wave per row, row cached in registers (d_pad <= 1024).
+// a3.3/a3.4 post-LN (eps 1e-5).  One half-wave (32 lanes) per row, a float4 of columns per lane,
+// the row cached in registers (d_pad <= 1024): 16-byte loads/stores, 8 rows per block.
 // ------------------------------------------------------------------------------------------
-constexpr int LN_MAXV = 16;  // d_pad / 64 upper bound
+constexpr int LN_V4 = 8;       // d_pad / 128 upper bound
+constexpr int LN_MAXV = 16;    // d_pad / 64 upper bound (host check)
+
+__device__ __forceinline__ float half_sum(float v) {
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
 
 __global__ void __launch_bounds__(256) layernorm_fwd_kernel(const float *Z, int64_t ldz, const float *gamma,
                                                             const float *beta, float *Y, int64_t ldy, float *mean,
                                                             float *rstd, int64_t rows_valid, int64_t rows_pad,
                                                             int64_t d, int64_t d_pad, float eps) {
-    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
+    const int64_t row = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 5);
+    const int hl = threadIdx.x & 31;
     if (row >= rows_pad) return;
     float *y = Y + row * ldy;
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
     if (row >= rows_valid) {
-        for (int64_t c = lane; c < d_pad; c += 64) y[c] = 0.f;
-        if (lane == 0) {
+        for (int64_t c = hl * 4; c < d_pad; c += 128) *reinterpret_cast<float4 *>(y + c) = z4;
+        if (hl == 0) {
             mean[row] = 0.f;
             rstd[row] = 0.f;
         }
         return;
     }
     const float *z = Z + row * ldz;
-    float v[LN_MAXV];
+    float v[LN_V4][4];
     float s = 0.f;
 #pragma unroll
-    for (int i = 0; i < LN_MAXV; ++i) {
-        const int64_t c = lane + 64 * i;
-        v[i] = (c < d) ? z[c] : 0.f;
-        s += v[i];
-    }
-    const float mu = wave_sum(s) / (float)d;
-    float q = 0.f;
+    for (int i = 0; i < LN_V4; ++i) {
+        const int64_t c = 4 * (hl + 32 * i);
+        const float4 t = c < d_pad ? ld4(z + c) : z4;
+        const float x[4] = {t.x, t.y, t.z, t.w};
 #pragma unroll
-    for (int i = 0; i < LN_MAXV; ++i) {
-        const int64_t c = lane + 64 * i;
-        const float t = (c < d) ? v[i] - mu : 0.f;
-        q += t * t;
+        for (int q = 0; q < 4; ++q) {
+            v[i][q] = c + q < d ? x[q] : 0.f;
+            s += v[i][q];
+        }
     }
-    const float var = wave_sum(q) / (float)d;
-    const float rs = rsqrtf(var + eps);
+    const float mu = half_sum(s) / (float)d;
+    float sq = 0.f;
 #pragma unroll
-    for (int i = 0; i < LN_MAXV; ++i) {
-        const int64_t c = lane + 64 * i;
-        if (c < d)
-            y[c] = (v[i] - mu) * rs * gamma[c] + beta[c];
-        else if (c < d_pad)
-            y[c] = 0.f;
+    for (int i = 0; i < LN_V4; ++i)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const float t = 4 * (hl + 32 * i) + q < d ? v[i][q] - mu : 0.f;
+            sq += t * t;
+        }
+    const float rs = rsqrtf(half_sum(sq) / (float)d + eps);
+#pragma unroll
+    for (int i = 0; i < LN_V4; ++i) {
+        const int64_t c = 4 * (hl + 32 * i);
+        if (c >= d_pad) continue;
+        float o[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o[q] = c + q < d ? (v[i][q] - mu) * rs * gamma[c + q] + beta[c + q] : 0.f;
+        *reinterpret_cast<float4 *>(y + c) = make_float4(o[0], o[1], o[2], o[3]);
     }
-    if (lane == 0) {
+    if (hl == 0) {
         mean[row] = mu;
         rstd[row] = rs;
     }
 }
 
-// LN backward, row part: one wave per row (4 rows per block, fully parallel over rows).
+// LN backward, row part: one half-wave per row (8 rows per block).
 __global__ void __launch_bounds__(256) layernorm_bwd_kernel(const float *dY, int64_t ldy, const float *Z, int64_t ldz,
                                                             const float *mean, const float *rstd, const float *gamma,
                                                             float *dZ, int64_t lddz, float *dZd, int64_t lddrop,
                                                             float p, uint64_t seed, int64_t rows_valid,
                                                             int64_t rows_pad, int64_t d, int64_t d_pad) {
-    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
+    const int64_t row = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 5);
+    const int hl = threadIdx.x & 31;
     if (row >= rows_pad) return;
     float *dz = dZ + row * lddz;
     float *dzd = dZd ? dZd + row * lddrop : nullptr;
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
     if (row >= rows_valid) {
-        for (int64_t c = lane; c < d_pad; c += 64) {
-            dz[c] = 0.f;
-            if (dzd) dzd[c] = 0.f;
+        for (int64_t c = hl * 4; c < d_pad; c += 128) {
+            *reinterpret_cast<float4 *>(dz + c) = z4;
+            if (dzd) *reinterpret_cast<float4 *>(dzd + c) = z4;
         }
         return;
     }
@@ -294,96 +363,114 @@ __global__ void __launch_bounds__(256) layernorm_bwd_kernel(const float *dY, int
     const float mu = mean[row], rs = rstd[row];
     const float *dy = dY + row * ldy;
     const float *z = Z + row * ldz;
-    float xh[LN_MAXV], g[LN_MAXV];
+    float xh[LN_V4][4], g[LN_V4][4];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-    for (int i = 0; i < LN_MAXV; ++i) {
-        const int64_t c = lane + 64 * i;
-        if (c < d) {
-            xh[i] = (z[c] - mu) * rs;
-            g[i] = dy[c] * gamma[c];
-        } else {
-            xh[i] = 0.f;
-            g[i] = 0.f;
-        }
-        s1 += g[i];
-        s2 += g[i] * xh[i];
-    }
-    const float m1 = wave_sum(s1) / (float)d;
-    const float m2 = wave_sum(s2) / (float)d;
+    for (int i = 0; i < LN_V4; ++i) {
+        const int64_t c = 4 * (hl + 32 * i);
+        const float4 a = c < d_pad ? ld4(dy + c) : z4, b = c < d_pad ? ld4(z + c) : z4;
+        const float av[4] = {a.x, a.y, a.z, a.w}, bv[4] = {b.x, b.y, b.z, b.w};
 #pragma unroll
-    for (int i = 0; i < LN_MAXV; ++i) {
-        const int64_t c = lane + 64 * i;
-        if (c < d) {
-            const float v = rs * (g[i] - m1 - xh[i] * m2);
-            dz[c] = v;
-            if (dzd) dzd[c] = (p > 0.f) ? (u2gnn_keep(seed, (uint32_t)row, (uint32_t)c, p) ? v * ks : 0.f) : v;
-        } else if (c < d_pad) {
-            dz[c] = 0.f;
-            if (dzd) dzd[c] = 0.f;
+        for (int q = 0; q < 4; ++q) {
+            const bool ok = c + q < d;
+            xh[i][q] = ok ? (bv[q] - mu) * rs : 0.f;
+            g[i][q] = ok ? av[q] * gamma[c + q] : 0.f;
+            s1 += g[i][q];
+            s2 += g[i][q] * xh[i][q];
         }
+    }
+    const float m1 = half_sum(s1) / (float)d;
+    const float m2 = half_sum(s2) / (float)d;
+#pragma unroll
+    for (int i = 0; i < LN_V4; ++i) {
+        const int64_t c = 4 * (hl + 32 * i);
+        if (c >= d_pad) continue;
+        float o[4], od[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const bool ok = c + q < d;
+            o[q] = ok ? rs * (g[i][q] - m1 - xh[i][q] * m2) : 0.f;
+            od[q] = (ok && p > 0.f) ? (u2gnn_keep(seed, (uint32_t)row, (uint32_t)(c + q), p) ? o[q] * ks : 0.f) : o[q];
+        }
+        *reinterpret_cast<float4 *>(dz + c) = make_float4(o[0], o[1], o[2], o[3]);
+        if (dzd) *reinterpret_cast<float4 *>(dzd + c) = make_float4(od[0], od[1], od[2], od[3]);
     }
 }
 
-// LN backward, column part: per 128-row chunk, sums over rows of dY*xhat (dgamma), dY (dbeta)
-// and dZd (the bias gradient of the dropout branch feeding this LN) -> ws[chunk][3][d_pad].
+// LN backward, column part: per CS_ROWS-row chunk, sums over rows of dY*xhat (dgamma), dY (dbeta)
+// and dZd (the bias gradient of the dropout branch feeding this LN) -> ws[chunk][3][d_pad];
+// float4 columns per lane, CS_ROWS/4 rows per wave (all loads in flight).
 __global__ void __launch_bounds__(256) ln_colstats_kernel(const float *dY, int64_t ldy, const float *Z, int64_t ldz,
                                                           const float *mean, const float *rstd, const float *dZd,
                                                           int64_t lddrop, int64_t rows, int64_t d, int64_t d_pad,
                                                           float *ws) {
-    __shared__ float red[4][3][64];
+    __shared__ float4 red[4][3][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int64_t c = (int64_t)blockIdx.x * 64 + lane;
+    const int64_t c = ((int64_t)blockIdx.x * 64 + lane) * 4;
     const int64_t r0 = (int64_t)blockIdx.y * CS_ROWS + w * (CS_ROWS / 4);
-    float sg[4] = {0.f, 0.f, 0.f, 0.f}, sb[4] = {0.f, 0.f, 0.f, 0.f}, sd[4] = {0.f, 0.f, 0.f, 0.f};
-    if (c < d) {
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 sg = z4, sb = z4, sd = z4;
+    if (c < d_pad) {
+        float4 dy[CS_ROWS / 4], zz[CS_ROWS / 4], dd[CS_ROWS / 4];
+        float mu[CS_ROWS / 4], rs[CS_ROWS / 4];
 #pragma unroll
-        for (int i = 0; i < CS_ROWS / 4; i += 4)
+        for (int j = 0; j < CS_ROWS / 4; ++j) {
+            const int64_t r = r0 + j;
+            const bool ok = r < rows;
+            dy[j] = ok ? ld4(dY + r * ldy + c) : z4;
+            zz[j] = ok ? ld4(Z + r * ldz + c) : z4;
+            dd[j] = (ok && dZd) ? ld4(dZd + r * lddrop + c) : z4;
+            mu[j] = ok ? mean[r] : 0.f;
+            rs[j] = ok ? rstd[r] : 0.f;
+        }
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int64_t r = r0 + i + j;
-                if (r < rows) {
-                    const float dy = dY[r * ldy + c];
-                    sg[j] += dy * ((Z[r * ldz + c] - mean[r]) * rstd[r]);
-                    sb[j] += dy;
-                    if (dZd) sd[j] += dZd[r * lddrop + c];
-                }
-            }
+        for (int j = 0; j < CS_ROWS / 4; ++j) {
+            sg.x += dy[j].x * ((zz[j].x - mu[j]) * rs[j]);
+            sg.y += dy[j].y * ((zz[j].y - mu[j]) * rs[j]);
+            sg.z += dy[j].z * ((zz[j].z - mu[j]) * rs[j]);
+            sg.w += dy[j].w * ((zz[j].w - mu[j]) * rs[j]);
+            sb = add4(sb, dy[j]);
+            sd = add4(sd, dd[j]);
+        }
     }
-    red[w][0][lane] = (sg[0] + sg[1]) + (sg[2] + sg[3]);
-    red[w][1][lane] = (sb[0] + sb[1]) + (sb[2] + sb[3]);
-    red[w][2][lane] = (sd[0] + sd[1]) + (sd[2] + sd[3]);
+    red[w][0][lane] = sg;
+    red[w][1][lane] = sb;
+    red[w][2][lane] = sd;
     __syncthreads();
     if (w < 3 && c < d_pad)
-        ws[((int64_t)blockIdx.y * 3 + w) * d_pad + c] = red[0][w][lane] + red[1][w][lane] + red[2][w][lane] +
-                                                      red[3][w][lane];
+        *reinterpret_cast<float4 *>(ws + ((int64_t)blockIdx.y * 3 + w) * d_pad + c) =
+            add4(add4(red[0][w][lane], red[1][w][lane]), add4(red[2][w][lane], red[3][w][lane]));
 }
 
+// block = 16 columns x 16 chunk strides (as colsum_final), fixed-order LDS combine
 __global__ void __launch_bounds__(256) ln_param_reduce_kernel(const float *ws, int64_t n_chunks, int64_t d,
                                                               int64_t d_pad, float *dgamma, float *dbeta, float *dbias) {
-    const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (c >= d) return;
-    float a[4] = {0.f, 0.f, 0.f, 0.f};
-    float b[4] = {0.f, 0.f, 0.f, 0.f};
-    float e[4] = {0.f, 0.f, 0.f, 0.f};
-    int64_t k = 0;
-    for (; k + 4 <= n_chunks; k += 4)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const float *q = ws + (k + j) * 3 * d_pad + c;
-            a[j] += q[0];
-            b[j] += q[d_pad];
-            e[j] += q[2 * d_pad];
+    __shared__ float red[3][16][FIN_COLS + 1];
+    const int cl = threadIdx.x % FIN_COLS, kg = threadIdx.x / FIN_COLS;
+    const int64_t c = (int64_t)blockIdx.x * FIN_COLS + cl;
+    float a = 0.f, b = 0.f, e = 0.f;
+    if (c < d)
+        for (int64_t k = kg; k < n_chunks; k += 16) {
+            const float *q = ws + k * 3 * d_pad + c;
+            a += q[0];
+            b += q[d_pad];
+            e += q[2 * d_pad];
         }
-    for (; k < n_chunks; ++k) {
-        const float *q = ws + k * 3 * d_pad + c;
-        a[0] += q[0];
-        b[0] += q[d_pad];
-        e[0] += q[2 * d_pad];
+    red[0][kg][cl] = a;
+    red[1][kg][cl] = b;
+    red[2][kg][cl] = e;
+    __syncthreads();
+    if (kg != 0 || c >= d) return;
+    float t[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        t[0] += red[0][j][cl];
+        t[1] += red[1][j][cl];
+        t[2] += red[2][j][cl];
     }
-    dgamma[c] = (a[0] + a[1]) + (a[2] + a[3]);
-    dbeta[c] = (b[0] + b[1]) + (b[2] + b[3]);
-    if (dbias) dbias[c] = (e[0] + e[1]) + (e[2] + e[3]);
+    dgamma[c] = t[0];
+    dbeta[c] = t[1];
+    if (dbias) dbias[c] = t[2];
 }
 
 __global__ void __launch_bounds__(256) dropout_mask_kernel(uint64_t seed, int64_t rows, int64_t cols, float p,
@@ -405,6 +492,8 @@ __global__ void __launch_bounds__(256) dropout_kernel(const float *X, int64_t ld
         Y[r * ldy + c] = u2gnn_keep(seed, (uint32_t)r, (uint32_t)c, p) ? v * ks : 0.f;
     }
 }
+
+inline bool al16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 inline unsigned grid_for(int64_t n, int64_t per_block, int64_t cap = 8192) {
     int64_t g = (n + per_block - 1) / per_block;
@@ -440,9 +529,12 @@ int u2gnn_slab_reduce(const float *src, int32_t n_slab, int64_t slab_stride, int
                       int64_t ld_src, int64_t rblk_pad, int64_t rblk_real, int64_t cblk_pad, int64_t cblk_real,
                       float *dst, int64_t ld_dst, float alpha, int32_t accumulate, void *stream) {
     if (!src || !dst || n_slab < 1 || rblk_pad < 1 || cblk_pad < 1) return U2GNN_E_ARG;
-    hipLaunchKernelGGL(slab_reduce_kernel, dim3(grid_for(rows_pad * cols_pad, 256)), dim3(256), 0,
+    if (!al16(src) || (cols_pad & 3) || (ld_src & 3) || (slab_stride & 3)) return U2GNN_E_ALIGN;
+    if (rows_pad == 0 || cols_pad == 0) return U2GNN_OK;
+    const int vec_store = cblk_pad == cblk_real && al16(dst) && (ld_dst & 3) == 0;
+    hipLaunchKernelGGL(slab_reduce_kernel, dim3(grid_for(rows_pad, 4, 1 << 30)), dim3(256), 0,
                        u2gnn_stream(stream), src, n_slab, slab_stride, rows_pad, cols_pad, ld_src, rblk_pad, rblk_real,
-                       cblk_pad, cblk_real, dst, ld_dst, alpha, accumulate);
+                       cblk_pad, cblk_real, dst, ld_dst, alpha, accumulate, vec_store);
     return u2gnn_launch_status();
 }
 
@@ -476,11 +568,17 @@ int u2gnn_pack_padded_multi(const u2gnn_pack_desc *descs, int32_t n, void *strea
 int u2gnn_colsum(const float *X, int64_t rows, int64_t cols_pad, int64_t ld, int64_t cblk_pad, int64_t cblk_real,
                  float *out, int32_t accumulate, float *ws, void *stream) {
     if (!X || !out || !ws || cblk_pad < 1) return U2GNN_E_ARG;
+    if (cols_pad == 0) return U2GNN_OK;
     const int64_t chunks = (rows + CS_ROWS - 1) / CS_ROWS;
     hipStream_t st = u2gnn_stream(stream);
-    hipLaunchKernelGGL(colsum_partial_kernel, dim3((unsigned)((cols_pad + 63) / 64), (unsigned)(chunks > 0 ? chunks : 1)),
-                       dim3(256), 0, st, X, rows, cols_pad, ld, ws);
-    hipLaunchKernelGGL(colsum_final_kernel, dim3(grid_for(cols_pad, 256, 1 << 30)), dim3(256), 0, st, ws,
+    const unsigned nch = (unsigned)(chunks > 0 ? chunks : 1);
+    if (al16(X) && al16(ws) && (ld & 3) == 0 && (cols_pad & 3) == 0)
+        hipLaunchKernelGGL(colsum_partial_kernel, dim3((unsigned)((cols_pad + 255) / 256), nch), dim3(256), 0, st, X,
+                           rows, cols_pad, ld, ws);
+    else
+        hipLaunchKernelGGL(colsum_partial_scalar_kernel, dim3((unsigned)((cols_pad + 63) / 64), nch), dim3(256), 0, st,
+                           X, rows, cols_pad, ld, ws);
+    hipLaunchKernelGGL(colsum_final_kernel, dim3((unsigned)((cols_pad + FIN_COLS - 1) / FIN_COLS)), dim3(256), 0, st, ws,
                        chunks > 0 ? chunks : 1, cols_pad, cblk_pad, cblk_real, out, accumulate);
     return u2gnn_launch_status();
 }
@@ -508,7 +606,8 @@ int u2gnn_layernorm_fwd(const float *Z, int64_t ldz, const float *gamma, const f
                         float eps, void *stream) {
     if (!Z || !gamma || !beta || !Y || !mean || !rstd || d < 1 || d > d_pad || d_pad > LN_MAXV * 64)
         return U2GNN_E_ARG;
-    hipLaunchKernelGGL(layernorm_fwd_kernel, dim3(grid_for(rows_pad, 4, 1 << 30)), dim3(256), 0, u2gnn_stream(stream),
+    if (!al16(Z) || !al16(Y) || (ldz & 3) || (ldy & 3) || (d_pad & 3)) return U2GNN_E_ALIGN;
+    hipLaunchKernelGGL(layernorm_fwd_kernel, dim3(grid_for(rows_pad, 8, 1 << 30)), dim3(256), 0, u2gnn_stream(stream),
                        Z, ldz, gamma, beta, Y, ldy, mean, rstd, rows_valid, rows_pad, d, d_pad, eps);
     return u2gnn_launch_status();
 }
@@ -519,7 +618,10 @@ int u2gnn_layernorm_bwd(const float *dY, int64_t ldy, const float *Z, int64_t ld
                         void *stream) {
     if (!dY || !Z || !mean || !rstd || !gamma || !dZ || d < 1 || d > d_pad || d_pad > LN_MAXV * 64)
         return U2GNN_E_ARG;
-    hipLaunchKernelGGL(layernorm_bwd_kernel, dim3(grid_for(rows_pad, 4, 1 << 30)), dim3(256), 0, u2gnn_stream(stream),
+    if (!al16(dY) || !al16(Z) || !al16(dZ) || (ldy & 3) || (ldz & 3) || (lddz & 3) || (d_pad & 3) ||
+        (dZdrop && (!al16(dZdrop) || (lddrop & 3))))
+        return U2GNN_E_ALIGN;
+    hipLaunchKernelGGL(layernorm_bwd_kernel, dim3(grid_for(rows_pad, 8, 1 << 30)), dim3(256), 0, u2gnn_stream(stream),
                        dY, ldy, Z, ldz, mean, rstd, gamma, dZ, lddz, dZdrop, lddrop, p, seed, rows_valid, rows_pad, d,
                        d_pad);
     return u2gnn_launch_status();
@@ -530,11 +632,15 @@ int u2gnn_layernorm_bwd_params(const float *dY, int64_t ldy, const float *Z, int
                                int64_t d_pad, float *ws, float *dgamma, float *dbeta, float *dbias, void *stream) {
     if (!dY || !Z || !mean || !rstd || !ws || !dgamma || !dbeta || d < 1 || d > d_pad) return U2GNN_E_ARG;
     if (dbias && !dZdrop) return U2GNN_E_ARG;
+    if (!al16(dY) || !al16(Z) || !al16(ws) || (ldy & 3) || (ldz & 3) || (d_pad & 3) ||
+        (dbias && (!al16(dZdrop) || (lddrop & 3))))
+        return U2GNN_E_ALIGN;
     const int64_t chunks = rows_valid > 0 ? (rows_valid + CS_ROWS - 1) / CS_ROWS : 1;
     hipStream_t st = u2gnn_stream(stream);
-    hipLaunchKernelGGL(ln_colstats_kernel, dim3((unsigned)((d + 63) / 64), (unsigned)chunks), dim3(256), 0, st, dY,
+    hipLaunchKernelGGL(ln_colstats_kernel, dim3((unsigned)((d_pad + 255) / 256), (unsigned)chunks), dim3(256), 0, st, dY,
                        ldy, Z, ldz, mean, rstd, dbias ? dZdrop : nullptr, lddrop, rows_valid, d, d_pad, ws);
-    hipLaunchKernelGGL(ln_param_reduce_kernel, dim3(grid_for(d, 256, 1 << 30)), dim3(256), 0, st, ws, chunks, d, d_pad,
+    hipLaunchKernelGGL(ln_param_reduce_kernel, dim3((unsigned)((d + FIN_COLS - 1) / FIN_COLS)), dim3(256), 0, st, ws,
+                       chunks, d, d_pad,
                        dgamma, dbeta, dbias);
     return u2gnn_launch_status();
 }

@@ -138,9 +138,13 @@ def _gemm_split(A, B, C, M, N, Kd, lda, ldb, ldc, trans_a=False, trans_b=False, 
     dS.K, dS^T.Q, the weight gradients, dH.W1, dQKV.W_in), the depth is cut into fp32 slabs
     (>= 4 K-tiles each, ~target workgroups) and one streaming pass sums them into C — applying
     alpha, accumulation and an optional padded->real block map (rblk, cblk)."""
-    t = 128 if (M % 128 == 0 and N % 128 == 0) else 64
-    tiles = (M // t) * (N // t)
     bk = 16 if prec == "fp32" else 32
+    if prec != "fp32" and M % 256 == 0 and N % 128 == 0 and (M // 256) * (N // 128) >= 32:
+        # 256x128 blocks (8 waves, one block per CU): the skinny attention products
+        t, tiles, target = 256, (M // 256) * (N // 128), 240
+    else:
+        t = 128 if (M % 128 == 0 and N % 128 == 0) else 64
+        tiles = (M // t) * (N // t)
     split = max(1, min(target // max(tiles, 1), Kd // (4 * bk)))
     mapped = rblk is not None
     if split == 1 and not mapped:
@@ -185,7 +189,8 @@ def encoder_layer_forward(X: torch.Tensor, w: PackedLayer, p: LayerParams, dims:
            alpha=1.0 / math.sqrt(d), scale_cols=dp, precision=prec, flops=6.0 * N * d * d)
     Q, Kt, V = QKV[:, :dp], QKV[:, dp:2 * dp], QKV[:, 2 * dp:]
     S = torch.empty(Np, Np, device=dev, dtype=f32)
-    K.gemm(Q, Kt, S, Np, Np, dp, 3 * dp, 3 * dp, Np, trans_b=True, precision=prec, flops=att)
+    K.gemm(Q, Kt, S, Np, Np, dp, 3 * dp, 3 * dp, Np, trans_b=True, precision=prec, flops=att,
+           tile=256 if (prec != "fp32" and Np % 256 == 0) else 0)
     P = torch.empty(Np, Np, device=dev, dtype=f32)
     Pd = torch.empty(Np, Np, device=dev, dtype=f32) if pd > 0 else P
     K.attn_softmax_fwd(S, Np, P, Pd, Np, N, Np, N, Np, pd, seeds.get(SITE_ATTN, 0))

@@ -155,7 +155,7 @@ def layernorm_fwd(Z, ldz, gamma, beta, Y, ldy, mean, rstd, rows_valid, rows_pad,
           "u2gnn_layernorm_fwd")
 
 
-CS_ROWS = 128
+CS_ROWS = 16   # rows per partial chunk of the column reductions (encoder_ops.hip)
 
 
 def colstat_ws_floats(rows, cols):

@@ -115,7 +115,8 @@ typedef struct u2gnn_pack_desc {
 int u2gnn_pack_padded_multi(const u2gnn_pack_desc *descs, int32_t n, void *stream);
 
 /* column sums (bias gradients):  out[map(c)] (+)= sum_{r<rows} X[r*ld + c], c < cols_pad.
- * ws must hold ceil(rows/128) * cols_pad floats. */
+ * ws must hold ceil(rows/16) * cols_pad floats (kernels.colstat_ws_floats allocates 3x that); 16-byte
+ * loads when X, ws are 16-byte aligned with ld and cols_pad multiples of 4, scalar loads otherwise. */
 int u2gnn_colsum(const float *X, int64_t rows, int64_t cols_pad, int64_t ld, int64_t cblk_pad,
                  int64_t cblk_real, float *out, int32_t accumulate, float *ws, void *stream);
 
@@ -143,7 +144,8 @@ int u2gnn_layernorm_bwd(const float *dY, int64_t ldy, const float *Z, int64_t ld
 /* LN parameter gradients: dgamma[c] = sum_r dY*xhat, dbeta[c] = sum_r dY (c < d) and, when
  * dbias != NULL, dbias[c] = sum_r dZdrop[r, c] (bias of the linear whose output was dropped into
  * the residual: out_proj.bias for norm1, linear2.bias for norm2).  Deterministic two-pass column
- * reduction; ws >= ceil(rows_valid/128) * 3 * d_pad floats. */
+ * reduction; ws >= ceil(rows_valid/16) * 3 * d_pad floats; dY, Z, dZdrop, ws 16-byte aligned with
+ * leading dimensions and d_pad multiples of 4. */
 int u2gnn_layernorm_bwd_params(const float *dY, int64_t ldy, const float *Z, int64_t ldz,
                                const float *mean, const float *rstd, const float *dZdrop,
                                int64_t lddrop, int64_t rows_valid, int64_t d, int64_t d_pad, float *ws,

@@ -409,10 +409,9 @@ __device__ __forceinline__ bf16x8 ld_frag(const __bf16 *img, int r0, int ks, int
     }
 }
 
-template <int BM, int BN, int WM, int WN, bool TA, bool TB, int EPI, bool SPLIT>
+template <int BM, int BN, int WM, int WN, int BK, bool TA, bool TB, int EPI, bool SPLIT>
 __global__ void __launch_bounds__(64 * WM * WN) gemm_bf16_kernel(GemmP P) {
     constexpr int NT = 64 * WM * WN;
-    constexpr int BK = 32;
     constexpr int LDK = BK + 8;
     constexpr int WTM = BM / WM, WTN = BN / WN;
     constexpr int TM = WTM / 32, TN = WTN / 32;
@@ -528,24 +527,31 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_bf16_kernel(GemmP P) {
             }
 }
 
-template <int KIND, int BM, int BN, bool TA, bool TB, int EPI>
+// bf16 K-step variants: 0 = BK 32 (2 blocks/CU at 128x128), 1 = BK 16 (40 KB LDS, 140-152
+// VGPRs: 3 blocks/CU; the skinny weight-gradient products run faster at that occupancy).
+// Measured and not kept (tools/gemm_bench.py, round 1): BK 64 at one block per CU (-30..-45 %),
+// staging written after the barrier from one register set (+-2 %).
+template <int VAR> constexpr int CFG_BK = VAR == 1 ? 16 : 32;
+
+template <int KIND, int BM, int BN, int VAR, bool TA, bool TB, int EPI>
 void launch_kernel(const GemmP &P, dim3 grid, hipStream_t st) {
     if constexpr (KIND == U2GNN_PREC_F32) {
         hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, TA, TB, EPI>), grid, dim3(256), 0, st, P);
     } else {
         constexpr int WM = BM == 256 ? 4 : 2, WN = 2;   // 256x128 tiles run 8 waves (4x2)
-        hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, WM, WN, TA, TB, EPI, KIND == U2GNN_PREC_BF16X3>), grid,
-                           dim3(64 * WM * WN), 0, st, P);
+        hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, WM, WN, CFG_BK<VAR>, TA, TB, EPI,
+                                             KIND == U2GNN_PREC_BF16X3>),
+                           grid, dim3(64 * WM * WN), 0, st, P);
     }
 }
 
-template <int KIND, int BM, int BN, bool TA, bool TB>
+template <int KIND, int BM, int BN, int VAR, bool TA, bool TB>
 int launch_epi(const GemmP &P, int epi, int split, hipStream_t st) {
     dim3 grid(P.gm * P.gn * split);
     switch (epi) {
 #define U2GNN_CASE(E)                                          \
     case E:                                                    \
-        launch_kernel<KIND, BM, BN, TA, TB, E>(P, grid, st);   \
+        launch_kernel<KIND, BM, BN, VAR, TA, TB, E>(P, grid, st);   \
         break;
         U2GNN_CASE(U2GNN_EPI_STORE)
         U2GNN_CASE(U2GNN_EPI_BIAS)
@@ -561,18 +567,20 @@ int launch_epi(const GemmP &P, int epi, int split, hipStream_t st) {
     return u2gnn_launch_status();
 }
 
-template <int KIND, int BM, int BN>
+template <int KIND, int BM, int BN, int VAR = 0>
 int launch_layout(const GemmP &P, bool ta, bool tb, int epi, int split, hipStream_t st) {
-    if (!ta && tb) return launch_epi<KIND, BM, BN, false, true>(P, epi, split, st);
-    if (!ta && !tb) return launch_epi<KIND, BM, BN, false, false>(P, epi, split, st);
-    if (ta && !tb) return launch_epi<KIND, BM, BN, true, false>(P, epi, split, st);
+    if (!ta && tb) return launch_epi<KIND, BM, BN, VAR, false, true>(P, epi, split, st);
+    if (!ta && !tb) return launch_epi<KIND, BM, BN, VAR, false, false>(P, epi, split, st);
+    if (ta && !tb) return launch_epi<KIND, BM, BN, VAR, true, false>(P, epi, split, st);
     return U2GNN_E_ARG;  // A^T B^T is never needed by the encoder
 }
 
 template <int KIND>
 int launch_tile(const GemmP &P, int tile, bool ta, bool tb, int epi, int split, hipStream_t st) {
-    if constexpr (KIND != U2GNN_PREC_F32)
+    if constexpr (KIND != U2GNN_PREC_F32) {
         if (tile == 256) return launch_layout<KIND, 256, 128>(P, ta, tb, epi, split, st);
+        if (tile == 129) return launch_layout<KIND, 128, 128, 1>(P, ta, tb, epi, split, st);
+    }
     if (tile == 128) return launch_layout<KIND, 128, 128>(P, ta, tb, epi, split, st);
     return launch_layout<KIND, 64, 64>(P, ta, tb, epi, split, st);
 }
@@ -590,7 +598,7 @@ extern "C" int u2gnn_gemm(const u2gnn_gemm_args *a, void *stream) {
     const int split = a->split_k < 1 ? 1 : a->split_k;
     if (split > 1 && a->epilogue != U2GNN_EPI_STORE) return U2GNN_E_ARG;
     if (!al16(a->A) || !al16(a->B) || (a->lda & 3) || (a->ldb & 3)) return U2GNN_E_ALIGN;
-    const int bk = prec == U2GNN_PREC_F32 ? 16 : 32;
+    const int bk = (prec == U2GNN_PREC_F32 || a->tile == 129) ? 16 : 32;   // K step of the kernel
     if (a->K % bk) return U2GNN_E_SHAPE;
     if (prec != U2GNN_PREC_F32) {   // bf16 staging addresses operands by 32-bit buffer offsets
         const int64_t span = ((int64_t)a->K + 256) * (a->lda > a->ldb ? a->lda : a->ldb) * 4;
@@ -613,10 +621,12 @@ extern "C" int u2gnn_gemm(const u2gnn_gemm_args *a, void *stream) {
         const int64_t blocks128 = can128 ? (a->M / 128) * (a->N / 128) * split : 0;
         tile = (can128 && blocks128 >= 480) ? 128 : 64;
     }
-    if (tile != 64 && tile != 128 && tile != 256) return U2GNN_E_ARG;
-    if (tile == 256 && prec == U2GNN_PREC_F32) return U2GNN_E_ARG;
-    const int tile_n = tile == 256 ? 128 : tile;   // "256" = 256x128 block (bf16 modes)
-    if (a->M % tile || a->N % tile_n) return U2GNN_E_SHAPE;
+    // tile codes: 64, 128 (square), 256 (256x128, 8 waves), 129 (128x128 with a 16-deep K step)
+    if (tile != 64 && tile != 128 && tile != 256 && tile != 129) return U2GNN_E_ARG;
+    if ((tile == 256 || tile == 129) && prec == U2GNN_PREC_F32) return U2GNN_E_ARG;
+    const int tm_ = tile == 129 ? 128 : tile;
+    const int tile_n = tm_ == 256 ? 128 : tm_;
+    if (a->M % tm_ || a->N % tile_n) return U2GNN_E_SHAPE;
     GemmP P;
     P.A = a->A;
     P.B = a->B;
@@ -628,9 +638,10 @@ extern "C" int u2gnn_gemm(const u2gnn_gemm_args *a, void *stream) {
     P.N = (int32_t)a->N;
     // split z covers k in [z*Kc, min((z+1)*Kc, K)), Kc a multiple of the K tile (the last
     // splits may be short or empty; an empty split writes a zero slab)
-    P.K = (int32_t)((a->K + (int64_t)split * bk - 1) / ((int64_t)split * bk) * bk);
+    const int kq = bk;   // K granule of one split
+    P.K = (int32_t)((a->K + (int64_t)split * kq - 1) / ((int64_t)split * kq) * kq);
     P.Ktot = (int32_t)a->K;
-    P.gm = (int32_t)(a->M / tile);
+    P.gm = (int32_t)(a->M / tm_);
     P.gn = (int32_t)(a->N / tile_n);
     P.slab_stride = a->slab_stride;
     P.bias = a->bias;

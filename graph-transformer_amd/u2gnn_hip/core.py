@@ -18,7 +18,7 @@ import torch
 
 from . import kernels as K
 from .engine import (SITE_ATTN, SITE_DROP1, SITE_DROP2, SITE_DROPFF, SITE_HEAD, Dims, LayerParams, PackedLayer,
-                     encoder_layer_backward, encoder_layer_forward, rup, site_seed)
+                     OffPath, encoder_layer_backward, encoder_layer_forward, rup, site_seed)
 
 
 @dataclass
@@ -118,6 +118,7 @@ class EncoderStack:
         b = ctx["batch"]
         dims = ctx["dims"]
         dnext = None
+        off = OffPath(b.input_x.device)
         for l in reversed(range(self.L)):
             dX = ext_grad(l)
             if dnext is not None:
@@ -126,8 +127,9 @@ class EncoderStack:
                 pre = f"{prefix}.{l}.layers.{t}."
                 g = LayerParams(*[grads[pre + k] for k in LAYER_KEYS])
                 dX = encoder_layer_backward(dX, ctx["layers"][l][t], self.packed[l][t], self.layer_params(l, t), g,
-                                            dims, self.prec)
+                                            dims, self.prec, off=off)
             dnext = dX
+        off.join()   # parameter gradients complete before the caller's optimizer reads them
         return dnext
 
 

@@ -18,6 +18,7 @@ Padding rows/columns hold zeros in every activation and gradient the encoder pro
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
 
@@ -131,8 +132,47 @@ class EncoderLayerCtx:
     __slots__ = ("X", "QKV", "P", "Pd", "O", "Z1", "X1", "mean1", "rstd1", "Hd", "Z2", "mean2", "rstd2", "seeds")
 
 
+# weight gradients on the 16-deep-K 128x128 tile (-1 % step time, A/B on one box);
+# U2GNN_DEEP_WGRAD=0 selects the 32-deep tile
+_DEEP_WGRAD = os.environ.get("U2GNN_DEEP_WGRAD", "1") == "1"
+
+
+# Gradient work off the backward's critical path (weight, bias and LayerNorm-parameter gradients)
+# runs on a second HIP stream, overlapping the dX chain; U2GNN_OVERLAP=0 serialises it.
+_OVERLAP = os.environ.get("U2GNN_OVERLAP", "1") == "1"
+_SIDE: Dict[int, "torch.cuda.Stream"] = {}
+
+
+class OffPath:
+    """Enqueue closures on the side stream after everything already issued on the current
+    stream; tensors they read are record_stream'ed so the caching allocator cannot recycle
+    them early.  join() makes the current stream wait for all of it."""
+
+    def __init__(self, dev: torch.device):
+        self.side = None
+        if _OVERLAP and dev.type == "cuda":
+            s = _SIDE.get(dev.index)
+            if s is None:
+                s = _SIDE[dev.index] = torch.cuda.Stream(device=dev)
+            self.side = s
+
+    def run(self, fn, *uses: torch.Tensor):
+        if self.side is None:
+            fn()
+            return
+        self.side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(self.side):
+            fn()
+        for t in uses:
+            t.record_stream(self.side)
+
+    def join(self):
+        if self.side is not None:
+            torch.cuda.current_stream().wait_stream(self.side)
+
+
 def _gemm_split(A, B, C, M, N, Kd, lda, ldb, ldc, trans_a=False, trans_b=False, alpha=1.0, accumulate=False,
-                prec="fp32", rblk=None, cblk=None, target=448, flops=None):
+                prec="fp32", rblk=None, cblk=None, target=448, flops=None, deep=False):
     """C (+)= alpha * op(A) . op(B) with deterministic split-K: when the tile grid alone would
     leave most of the 256 CUs idle (skinny outputs with a deep node dimension: P.V, Pd^T.dO,
     dS.K, dS^T.Q, the weight gradients, dH.W1, dQKV.W_in), the depth is cut into fp32 slabs
@@ -146,6 +186,10 @@ def _gemm_split(A, B, C, M, N, Kd, lda, ldb, ldc, trans_a=False, trans_b=False, 
         t = 128 if (M % 128 == 0 and N % 128 == 0) else 64
         tiles = (M // t) * (N // t)
     split = max(1, min(target // max(tiles, 1), Kd // (4 * bk)))
+    if deep and _DEEP_WGRAD and prec != "fp32" and t == 128:
+        # weight gradients (a few dozen 128x128 output tiles, K = Np): the 16-deep K step runs 3
+        # blocks per CU; <= 16 slabs keeps the reduce pass short
+        t, split = 129, max(1, min(16, target // max(tiles, 1)))
     mapped = rblk is not None
     if split == 1 and not mapped:
         K.gemm(A, B, C, M, N, Kd, lda, ldb, ldc, trans_a=trans_a, trans_b=trans_b, alpha=alpha,
@@ -161,7 +205,7 @@ def _gemm_split(A, B, C, M, N, Kd, lda, ldb, ldc, trans_a=False, trans_b=False, 
 def _wgrad(dY, ld_dy, X, ld_x, m_pad, n_pad, rows_pad, dst, rblk, cblk, prec, n_real):
     """dst(real) = unpack(dY^T X) with dY [rows_pad, m_pad] (ld_dy), X [rows_pad, n_pad] (ld_x)."""
     _gemm_split(dY, X, dst, m_pad, n_pad, rows_pad, ld_dy, ld_x, dst.shape[-1] if dst.dim() > 1 else dst.numel(),
-                trans_a=True, prec=prec, rblk=rblk, cblk=cblk, flops=2.0 * dst.numel() * n_real)
+                trans_a=True, prec=prec, rblk=rblk, cblk=cblk, flops=2.0 * dst.numel() * n_real, deep=True)
 
 
 def _bias_grad(dY, rows, cols_pad, ld, cblk, out):
@@ -225,41 +269,51 @@ def encoder_layer_forward(X: torch.Tensor, w: PackedLayer, p: LayerParams, dims:
 
 
 def encoder_layer_backward(dX2: torch.Tensor, ctx: EncoderLayerCtx, w: PackedLayer, p: LayerParams,
-                           g: LayerParams, dims: Dims, prec: str = "fp32") -> torch.Tensor:
+                           g: LayerParams, dims: Dims, prec: str = "fp32",
+                           off: Optional[OffPath] = None) -> torch.Tensor:
     """Backward of encoder_layer_forward.  Writes the real-shaped parameter gradients into
-    ``g`` (tensors shaped like the params) and returns dX [Np, dp]."""
+    ``g`` (tensors shaped like the params) and returns dX [Np, dp].  Parameter-gradient work is
+    enqueued on ``off``'s side stream (joined here unless the caller passes its own OffPath)."""
     N, Np, d, dp, ff, ffp = dims.N, dims.Np, dims.d, dims.dp, dims.ff, dims.ffp
     pd, seeds = ctx.seeds
     att = 2.0 * N * N * d
     dev = dX2.device
     f32 = torch.float32
+    own = off is None
+    if own:
+        off = OffPath(dev)
     ws = torch.empty(K.colstat_ws_floats(N, dp), device=dev, dtype=f32)
     # LN2 backward -> dX1 (residual branch), dF (dropout2 branch); norm2 + linear2.bias grads
     dX1 = torch.empty(Np, dp, device=dev, dtype=f32)
     dF = torch.empty(Np, dp, device=dev, dtype=f32)
     K.layernorm_bwd(dX2, dp, ctx.Z2, dp, ctx.mean2, ctx.rstd2, p.n2_w, dX1, dp, dF, dp, pd,
                     seeds.get(SITE_DROP2, 0), N, Np, d, dp)
-    K.layernorm_bwd_params(dX2, dp, ctx.Z2, dp, ctx.mean2, ctx.rstd2, dF, dp, N, d, dp, ws, g.n2_w, g.n2_b, g.l2_b)
+    off.run(lambda: K.layernorm_bwd_params(dX2, dp, ctx.Z2, dp, ctx.mean2, ctx.rstd2, dF, dp, N, d, dp, ws, g.n2_w,
+                                           g.n2_b, g.l2_b), dX2, ctx.Z2, ctx.mean2, ctx.rstd2, dF, ws)
     # FFN: Z2 = X1 + drop(Hd W2^T + b2), Hd = drop(relu(X1 W1^T + b1))
     dH = torch.empty(Np, ffp, device=dev, dtype=f32)
     K.gemm(dF, w.W2, dH, Np, ffp, dp, dp, ffp, ffp, epilogue=E.EPI_RELU_DROP_BWD, aux0=ctx.Hd, ld_aux=ffp,
            p_drop=pd, precision=prec, flops=2.0 * N * d * ff)
-    _wgrad(dF, dp, ctx.Hd, ffp, dp, ffp, Np, g.l2_w, (dp, d), (ffp, ff), prec, N)
+    off.run(lambda: _wgrad(dF, dp, ctx.Hd, ffp, dp, ffp, Np, g.l2_w, (dp, d), (ffp, ff), prec, N), dF, ctx.Hd)
     _gemm_split(dH, w.W1, dX1, Np, dp, ffp, ffp, dp, dp, accumulate=True, prec=prec, flops=2.0 * N * d * ff)
-    _wgrad(dH, ffp, ctx.X1, dp, ffp, dp, Np, g.l1_w, (ffp, ff), (dp, d), prec, N)
-    _bias_grad(dH, Np, ffp, ffp, (ffp, ff), g.l1_b)
+
+    def ffn1_grads(dH=dH):
+        _wgrad(dH, ffp, ctx.X1, dp, ffp, dp, Np, g.l1_w, (ffp, ff), (dp, d), prec, N)
+        _bias_grad(dH, Np, ffp, ffp, (ffp, ff), g.l1_b)
+    off.run(ffn1_grads, dH, ctx.X1)
     del dH, dF
     # LN1 backward -> dX (residual), dA (dropout1 branch)
     dX = torch.empty(Np, dp, device=dev, dtype=f32)
     dA = torch.empty(Np, dp, device=dev, dtype=f32)
     K.layernorm_bwd(dX1, dp, ctx.Z1, dp, ctx.mean1, ctx.rstd1, p.n1_w, dX, dp, dA, dp, pd,
                     seeds.get(SITE_DROP1, 0), N, Np, d, dp)
-    K.layernorm_bwd_params(dX1, dp, ctx.Z1, dp, ctx.mean1, ctx.rstd1, dA, dp, N, d, dp, ws, g.n1_w, g.n1_b, g.out_b)
+    off.run(lambda: K.layernorm_bwd_params(dX1, dp, ctx.Z1, dp, ctx.mean1, ctx.rstd1, dA, dp, N, d, dp, ws, g.n1_w,
+                                           g.n1_b, g.out_b), dX1, ctx.Z1, ctx.mean1, ctx.rstd1, dA)
     del dX1
     # out-projection
     dO = torch.empty(Np, dp, device=dev, dtype=f32)
     K.gemm(dA, w.W_o, dO, Np, dp, dp, dp, dp, dp, precision=prec, flops=2.0 * N * d * d)
-    _wgrad(dA, dp, ctx.O, dp, dp, dp, Np, g.out_w, (dp, d), (dp, d), prec, N)
+    off.run(lambda: _wgrad(dA, dp, ctx.O, dp, dp, dp, Np, g.out_w, (dp, d), (dp, d), prec, N), dA, ctx.O)
     del dA
     # attention core
     QKV = ctx.QKV
@@ -278,6 +332,11 @@ def encoder_layer_backward(dX2: torch.Tensor, ctx: EncoderLayerCtx, w: PackedLay
     # in-projection
     _gemm_split(dQKV, w.W_in, dX, Np, dp, 3 * dp, 3 * dp, dp, dp, accumulate=True, prec=prec,
                 flops=6.0 * N * d * d)
-    _wgrad(dQKV, 3 * dp, ctx.X, dp, 3 * dp, dp, Np, g.in_w, (dp, d), (dp, d), prec, N)
-    _bias_grad(dQKV, Np, 3 * dp, 3 * dp, (dp, d), g.in_b)
+
+    def in_proj_grads(dQKV=dQKV):
+        _wgrad(dQKV, 3 * dp, ctx.X, dp, 3 * dp, dp, Np, g.in_w, (dp, d), (dp, d), prec, N)
+        _bias_grad(dQKV, Np, 3 * dp, 3 * dp, (dp, d), g.in_b)
+    off.run(in_proj_grads, dQKV, ctx.X)
+    if own:
+        off.join()
     return dX

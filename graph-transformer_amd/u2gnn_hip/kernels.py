@@ -59,8 +59,9 @@ def gemm_symbol(precision, M, N, split_k, tile, trans_a, trans_b, epilogue):
     b = lambda x: "true" if x else "false"  # noqa: E731
     if precision == "fp32":
         return f"gemm_f32_kernel<{tile}, {tile}, {b(trans_a)}, {b(trans_b)}, {int(epilogue)}>"
-    bm, bn, wm = (256, 128, 4) if tile == 256 else (tile, tile, 2)   # "256" = 256x128 block, 4x2 waves
-    return (f"gemm_bf16_kernel<{bm}, {bn}, {wm}, 2, {b(trans_a)}, {b(trans_b)}, {int(epilogue)}, "
+    # "256" = 256x128 block (4x2 waves); "129" = 128x128 block with a 16-deep K step
+    bm, bn, wm, bk = {256: (256, 128, 4, 32), 129: (128, 128, 2, 16)}.get(tile, (tile, tile, 2, 32))
+    return (f"gemm_bf16_kernel<{bm}, {bn}, {wm}, 2, {bk}, {b(trans_a)}, {b(trans_b)}, {int(epilogue)}, "
             f"{b(precision == 'bf16x3')}>")   # the C++ template instance as rocprofv3 names it
 
 

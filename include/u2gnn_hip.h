@@ -70,7 +70,9 @@ typedef struct u2gnn_gemm_args {
     float p_drop;
     uint64_t seed;
     int32_t precision;    /* U2GNN_PREC_* */
-    int32_t tile;         /* 0 = auto, else 64 / 128 (square block tile) */
+    int32_t tile;         /* 0 = auto; 64 / 128 square block tiles; bf16 modes also 256 (256x128
+                             block, 8 waves) and 129 (128x128 block with a 16-deep K step, 3
+                             blocks per CU: skinny weight-gradient products) */
 } u2gnn_gemm_args;
 
 /* ---- library ------------------------------------------------------------------ */

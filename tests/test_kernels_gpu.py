@@ -35,7 +35,7 @@ def test_gemm_layouts_exact_fp32(tile, layout):
 
 
 @pytest.mark.parametrize("prec,tol", [("bf16x3", 3e-5), ("bf16", 2e-2)])
-@pytest.mark.parametrize("tile", [64, 128, 256])
+@pytest.mark.parametrize("tile", [64, 128, 256, 129])
 @pytest.mark.parametrize("layout", ["NT", "NN", "TN"])
 def test_gemm_split_bf16_layouts(prec, tol, tile, layout):
     M, N, Kd = 512, 384, 320
@@ -86,7 +86,8 @@ def test_gemm_split_k_slabs_and_views():
 
 
 @pytest.mark.parametrize("prec,Kd,split,tile", [("fp32", 208, 5, 128), ("fp32", 64, 8, 128), ("bf16x3", 352, 4, 128),
-                                                ("bf16x3", 96, 8, 128), ("bf16x3", 352, 4, 256), ("bf16", 96, 8, 256)])
+                                                ("bf16x3", 96, 8, 128), ("bf16x3", 352, 4, 256), ("bf16", 96, 8, 256),
+                                                ("bf16x3", 336, 5, 129)])
 def test_gemm_ragged_and_empty_splits(prec, Kd, split, tile):
     """split z covers [z*Kc, min((z+1)*Kc, K)); trailing splits may be short or empty (zero slab)."""
     M, N = 256, 128

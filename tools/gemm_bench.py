@@ -9,16 +9,16 @@ import torch  # noqa: E402
 from u2gnn_hip import kernels as K  # noqa: E402
 
 Np, dp, ffp = 4864, 384, 1024
-SHAPES = [  # name, M, N, K, ta, tb, [(split, tile), ...]
-    ("QK^T  NT", Np, Np, dp, False, True, [(1, 128), (1, 256)]),
-    ("dS    NT", Np, Np, dp, False, True, [(1, 128), (1, 256)], 6),   # dO.V^T with the attention-dS epilogue
-    ("P.V   NN", Np, dp, Np, False, False, [(4, 128), (8, 256), (4, 256)]),
-    ("dV    TN", Np, dp, Np, True, False, [(4, 128), (8, 256), (4, 256)]),
-    ("dWin  TN", 3 * dp, dp, Np, True, False, [(16, 128), (8, 128)]),
-    ("dW1   TN", ffp, dp, Np, True, False, [(16, 128), (8, 256)]),
-    ("QKV   NT", Np, 3 * dp, dp, False, True, [(1, 64), (1, 128), (1, 256)]),
-    ("FFN1  NT", Np, ffp, dp, False, True, [(1, 64), (1, 128), (1, 256)]),
-    ("FFN2  NT", Np, dp, ffp, False, True, [(1, 64), (1, 128)]),
+SHAPES = [  # name, M, N, K, ta, tb, [(split, tile), ...] (tile 129-132/257: experimental pipelines)
+    ("QK^T  NT", Np, Np, dp, False, True, [(1, 128), (1, 256), (1, 131), (1, 132)]),
+    ("dS    NT", Np, Np, dp, False, True, [(1, 128), (1, 131), (1, 132)], 6),   # dO.V^T with the attention-dS epilogue
+    ("P.V   NN", Np, dp, Np, False, False, [(4, 128), (4, 256), (4, 131), (4, 132), (6, 131), (6, 132)]),
+    ("dV    TN", Np, dp, Np, True, False, [(4, 128), (4, 256), (4, 131), (4, 132), (6, 131), (6, 132)]),
+    ("dWin  TN", 3 * dp, dp, Np, True, False, [(8, 128), (8, 131), (8, 132), (16, 131)]),
+    ("dW1   TN", ffp, dp, Np, True, False, [(16, 128), (16, 131), (16, 132), (8, 131)]),
+    ("QKV   NT", Np, 3 * dp, dp, False, True, [(1, 64), (1, 256), (1, 131), (1, 132)]),
+    ("FFN1  NT", Np, ffp, dp, False, True, [(1, 64), (1, 256), (1, 131), (1, 132)]),
+    ("FFN2  NT", Np, dp, ffp, False, True, [(1, 64), (1, 131), (1, 132), (2, 131)]),
 ]
 
 

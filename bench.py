@@ -162,6 +162,8 @@ def main():
     K.REC.records.clear()
     rec_elapsed = None
     if not args.no_roofline:
+        from u2gnn_hip.engine import set_overlap
+        set_overlap(False)   # serial: each GEMM's events time that kernel alone
         K.REC.enabled = True
         torch.cuda.synchronize()
         t1 = time.perf_counter()

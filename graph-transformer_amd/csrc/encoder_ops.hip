@@ -201,20 +201,33 @@ __global__ void __launch_bounds__(256) colsum_final_kernel(const float *ws, int6
 // probabilities (torch SDPA math path: dropout AFTER softmax, 1/(1-p) scaling).
 // One 256-thread block per row; online max/sum pass, then normalise + mask pass.
 // ------------------------------------------------------------------------------------------
+// 8 bits -> bit 4i for bit i (the keep decisions of 8 lanes x 4 columns -> one 32-bit word)
+__device__ __forceinline__ uint32_t spread4(uint32_t x) {
+    x &= 0xFFu;
+    x = (x | (x << 12)) & 0x000F000Fu;
+    x = (x | (x << 6)) & 0x03030303u;
+    x = (x | (x << 3)) & 0x11111111u;
+    return x;
+}
+
 __global__ void __launch_bounds__(256) attn_softmax_kernel(const float *S, int64_t lds, float *P, float *Pd,
                                                            int64_t ldp, int64_t rows_valid, int64_t n_valid,
-                                                           int64_t n_pad, float p, uint64_t seed) {
+                                                           int64_t n_pad, float p, uint64_t seed, uint32_t *keep,
+                                                           int64_t ld_keep) {
     __shared__ float red_m[4], red_s[4];
     const int64_t row = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     float *prow = P + row * ldp;
     float *pdrow = Pd + row * ldp;
+    uint32_t *krow = keep ? keep + row * ld_keep : nullptr;
     const bool write_pd = Pd != P;
     if (row >= rows_valid) {
         for (int64_t c = tid * 4; c < n_pad; c += 1024) {
             *reinterpret_cast<float4 *>(prow + c) = make_float4(0.f, 0.f, 0.f, 0.f);
             if (write_pd) *reinterpret_cast<float4 *>(pdrow + c) = make_float4(0.f, 0.f, 0.f, 0.f);
         }
+        if (krow)
+            for (int64_t k = tid; k < n_pad / 32; k += 256) krow[k] = 0u;
         return;
     }
     const float *srow = S + row * lds;
@@ -246,17 +259,36 @@ __global__ void __launch_bounds__(256) attn_softmax_kernel(const float *S, int64
     for (int i = 0; i < 4; ++i) tot += red_m[i] == -INFINITY ? 0.f : red_s[i] * expf(red_m[i] - M);
     const float inv = 1.f / tot;
     const float ks = p > 0.f ? 1.f / (1.f - p) : 1.f;
-    for (int64_t c = tid * 4; c < n_pad; c += 1024) {
-        const float4 v = *reinterpret_cast<const float4 *>(srow + c);
+    // every wave runs the same trip count (n_pad % 1024 may leave the last trip partial) so the
+    // keep-bit ballots below see all 64 lanes
+    for (int64_t cb = 0; cb < n_pad; cb += 1024) {
+        const int64_t c = cb + tid * 4;
+        const bool in = c < n_pad;
+        const float4 v = in ? *reinterpret_cast<const float4 *>(srow + c) : make_float4(0.f, 0.f, 0.f, 0.f);
         const float x[4] = {v.x, v.y, v.z, v.w};
         float e[4], ed[4];
+        bool kp[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             e[j] = (c + j < n_valid) ? expf(x[j] - M) * inv : 0.f;
-            ed[j] = (p > 0.f) ? (u2gnn_keep(seed, (uint32_t)row, (uint32_t)(c + j), p) ? e[j] * ks : 0.f) : e[j];
+            kp[j] = (p > 0.f) ? u2gnn_keep(seed, (uint32_t)row, (uint32_t)(c + j), p) : true;
+            ed[j] = kp[j] ? e[j] * ks : 0.f;
         }
-        *reinterpret_cast<float4 *>(prow + c) = make_float4(e[0], e[1], e[2], e[3]);
-        if (write_pd) *reinterpret_cast<float4 *>(pdrow + c) = make_float4(ed[0], ed[1], ed[2], ed[3]);
+        if (in) {
+            *reinterpret_cast<float4 *>(prow + c) = make_float4(e[0], e[1], e[2], e[3]);
+            if (write_pd) *reinterpret_cast<float4 *>(pdrow + c) = make_float4(ed[0], ed[1], ed[2], ed[3]);
+        }
+        if (krow) {
+            // lanes 8k..8k+7 cover columns 32k..32k+31 of this wave's 256: word k from 4 ballots
+            uint32_t word = 0u;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint64_t b = __ballot(in && kp[j] && c + j < n_valid);
+                word |= spread4((uint32_t)(b >> (8 * (lane & 7)))) << j;
+            }
+            const int64_t wi = (cb + w * 256) / 32 + lane;
+            if (lane < 8 && (cb + w * 256 + 32 * lane) < n_pad) krow[wi] = word;
+        }
     }
 }
 
@@ -584,11 +616,13 @@ int u2gnn_colsum(const float *X, int64_t rows, int64_t cols_pad, int64_t ld, int
 }
 
 int u2gnn_attn_softmax_fwd(const float *S, int64_t lds, float *P, float *Pd, int64_t ldp, int64_t rows_valid,
-                           int64_t rows_pad, int64_t n_valid, int64_t n_pad, float p, uint64_t seed, void *stream) {
+                           int64_t rows_pad, int64_t n_valid, int64_t n_pad, float p, uint64_t seed, uint32_t *keep,
+                           int64_t ld_keep, void *stream) {
     if (!S || !P || !Pd || (n_pad & 3) || (lds & 3) || (ldp & 3) || n_valid > n_pad || n_valid < 1) return U2GNN_E_ARG;
     if (Pd == P && p > 0.f) return U2GNN_E_ARG;
+    if (keep && ((n_pad & 31) || ld_keep < n_pad / 32)) return U2GNN_E_ARG;
     hipLaunchKernelGGL(attn_softmax_kernel, dim3((unsigned)rows_pad), dim3(256), 0, u2gnn_stream(stream), S, lds, P,
-                       Pd, ldp, rows_valid, n_valid, n_pad, p, seed);
+                       Pd, ldp, rows_valid, n_valid, n_pad, p, seed, keep, ld_keep);
     return u2gnn_launch_status();
 }
 

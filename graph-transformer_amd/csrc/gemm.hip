@@ -42,6 +42,8 @@ struct GemmP {
     int32_t scale_cols;
     float p;
     uint64_t seed;
+    const uint32_t *keep;
+    int64_t ld_keep;
 };
 
 // four consecutive columns (col % 4 == 0) of one row; every vector operand is 16-byte aligned
@@ -54,8 +56,15 @@ __device__ __forceinline__ float4 epilogue4(const GemmP &P, int row, int col, fl
         return make_float4(P.alpha * v.x, P.alpha * v.y, P.alpha * v.z, P.alpha * v.w);
     } else if constexpr (EPI == U2GNN_EPI_ATTN_DS) {
         const int64_t o = (int64_t)row * P.ld_aux + col;
-        const float4 pd = ld4(P.aux1 + o), pr = ld4(P.aux0 + o);
+        const float4 pr = ld4(P.aux0 + o);
         const float dl = P.rowvec[row];
+        if (P.keep) {   // dS = P * (keep * dPd / (1-p) - delta): 4 keep bits instead of 16 B of Pd
+            const uint32_t kb = P.keep[(int64_t)row * P.ld_keep + (col >> 5)] >> (col & 31);
+            const float s = 1.f / (1.f - P.p);
+            return make_float4(pr.x * (((kb & 1u) ? v.x * s : 0.f) - dl), pr.y * (((kb & 2u) ? v.y * s : 0.f) - dl),
+                               pr.z * (((kb & 4u) ? v.z * s : 0.f) - dl), pr.w * (((kb & 8u) ? v.w * s : 0.f) - dl));
+        }
+        const float4 pd = ld4(P.aux1 + o);
         return make_float4(pd.x * v.x - pr.x * dl, pd.y * v.y - pr.y * dl, pd.z * v.z - pr.z * dl,
                            pd.w * v.w - pr.w * dl);
     } else if constexpr (EPI == U2GNN_EPI_ACCUM) {
@@ -614,7 +623,8 @@ extern "C" int u2gnn_gemm(const u2gnn_gemm_args *a, void *stream) {
         return U2GNN_E_ARG;
     if ((e == U2GNN_EPI_BIAS_DROP_RESID || e == U2GNN_EPI_RELU_DROP_BWD || e == U2GNN_EPI_ATTN_DS) && !a->aux0)
         return U2GNN_E_ARG;
-    if (e == U2GNN_EPI_ATTN_DS && (!a->aux1 || !a->rowvec)) return U2GNN_E_ARG;
+    if (e == U2GNN_EPI_ATTN_DS && ((!a->aux1 && !a->keep) || !a->rowvec)) return U2GNN_E_ARG;
+    if (e == U2GNN_EPI_ATTN_DS && a->keep && (a->ld_keep * 32 < a->N || !(a->p_drop < 1.f))) return U2GNN_E_ARG;
     int tile = a->tile;
     if (tile == 0) {
         const bool can128 = (a->M % 128 == 0) && (a->N % 128 == 0);
@@ -653,6 +663,8 @@ extern "C" int u2gnn_gemm(const u2gnn_gemm_args *a, void *stream) {
     P.scale_cols = (int32_t)a->scale_cols;
     P.p = a->p_drop;
     P.seed = a->seed;
+    P.keep = e == U2GNN_EPI_ATTN_DS ? a->keep : nullptr;
+    P.ld_keep = a->ld_keep;
     hipStream_t st = u2gnn_stream(stream);
     const bool ta = a->trans_a != 0, tb = a->trans_b != 0;
     if (prec == U2GNN_PREC_BF16X3) return launch_tile<U2GNN_PREC_BF16X3>(P, tile, ta, tb, e, split, st);

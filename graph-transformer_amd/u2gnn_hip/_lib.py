@@ -48,6 +48,7 @@ class GemmArgs(ctypes.Structure):
         ("seed", c_uint64),
         ("precision", c_int32),
         ("tile", c_int32),
+        ("keep", c_void_p), ("ld_keep", c_int64),
     ]
 
 
@@ -67,7 +68,7 @@ _HIP_SIGS = {
     "u2gnn_slab_reduce": ([VP, I32, I64, I64, I64, I64, I64, I64, I64, I64, VP, I64, F32, I32, VP], c_int32),
     "u2gnn_pack_padded": ([VP, I64, I64, I64, I64, I64, I64, I64, VP, I64, VP], c_int32),
     "u2gnn_colsum": ([VP, I64, I64, I64, I64, I64, VP, I32, VP, VP], c_int32),
-    "u2gnn_attn_softmax_fwd": ([VP, I64, VP, VP, I64, I64, I64, I64, I64, F32, c_uint64, VP], c_int32),
+    "u2gnn_attn_softmax_fwd": ([VP, I64, VP, VP, I64, I64, I64, I64, I64, F32, c_uint64, VP, I64, VP], c_int32),
     "u2gnn_rowdot": ([VP, I64, VP, I64, VP, I64, I64, VP], c_int32),
     "u2gnn_layernorm_fwd": ([VP, I64, VP, VP, VP, I64, VP, VP, I64, I64, I64, I64, F32, VP], c_int32),
     "u2gnn_layernorm_bwd": ([VP, I64, VP, I64, VP, VP, VP, VP, I64, VP, I64, F32, c_uint64, I64, I64, I64, I64, VP],

@@ -129,7 +129,8 @@ class PackedLayer:
 
 
 class EncoderLayerCtx:
-    __slots__ = ("X", "QKV", "P", "Pd", "O", "Z1", "X1", "mean1", "rstd1", "Hd", "Z2", "mean2", "rstd2", "seeds")
+    __slots__ = ("X", "QKV", "P", "Pd", "O", "keep", "Z1", "X1", "mean1", "rstd1", "Hd", "Z2", "mean2", "rstd2",
+                 "seeds")
 
 
 # weight gradients on the 16-deep-K 128x128 tile (-1 % step time, A/B on one box);
@@ -139,8 +140,16 @@ _DEEP_WGRAD = os.environ.get("U2GNN_DEEP_WGRAD", "1") == "1"
 
 # Gradient work off the backward's critical path (weight, bias and LayerNorm-parameter gradients)
 # runs on a second HIP stream, overlapping the dX chain; U2GNN_OVERLAP=0 serialises it.
-_OVERLAP = os.environ.get("U2GNN_OVERLAP", "1") == "1"
+_OVERLAP = [os.environ.get("U2GNN_OVERLAP", "1") == "1"]
 _SIDE: Dict[int, "torch.cuda.Stream"] = {}
+
+
+def set_overlap(on: bool) -> bool:
+    """Enable/disable the side stream (bench.py serialises its per-kernel timing pass, where
+    concurrent kernels would inflate each other's event times); returns the previous setting."""
+    prev = _OVERLAP[0]
+    _OVERLAP[0] = bool(on)
+    return prev
 
 
 class OffPath:
@@ -150,7 +159,7 @@ class OffPath:
 
     def __init__(self, dev: torch.device):
         self.side = None
-        if _OVERLAP and dev.type == "cuda":
+        if _OVERLAP[0] and dev.type == "cuda":
             s = _SIDE.get(dev.index)
             if s is None:
                 s = _SIDE[dev.index] = torch.cuda.Stream(device=dev)
@@ -237,7 +246,9 @@ def encoder_layer_forward(X: torch.Tensor, w: PackedLayer, p: LayerParams, dims:
            tile=256 if (prec != "fp32" and Np % 256 == 0) else 0)
     P = torch.empty(Np, Np, device=dev, dtype=f32)
     Pd = torch.empty(Np, Np, device=dev, dtype=f32) if pd > 0 else P
-    K.attn_softmax_fwd(S, Np, P, Pd, Np, N, Np, N, Np, pd, seeds.get(SITE_ATTN, 0))
+    # keep bits for the backward's dS epilogue (3 MB instead of re-reading the 95 MB Pd)
+    keep = torch.empty(Np, Np // 32, device=dev, dtype=torch.int32) if (pd > 0 and need_ctx) else None
+    K.attn_softmax_fwd(S, Np, P, Pd, Np, N, Np, N, Np, pd, seeds.get(SITE_ATTN, 0), keep=keep)
     del S
     O = torch.empty(Np, dp, device=dev, dtype=f32)
     _gemm_nodes_k(Pd, V, O, Np, dp, Np, Np, 3 * dp, dp, prec=prec, flops=att)
@@ -261,7 +272,7 @@ def encoder_layer_forward(X: torch.Tensor, w: PackedLayer, p: LayerParams, dims:
     ctx = None
     if need_ctx:
         ctx = EncoderLayerCtx()
-        ctx.X, ctx.QKV, ctx.P, ctx.Pd, ctx.O = X, QKV, P, Pd, O
+        ctx.X, ctx.QKV, ctx.P, ctx.Pd, ctx.O, ctx.keep = X, QKV, P, Pd, O, keep
         ctx.Z1, ctx.X1, ctx.mean1, ctx.rstd1, ctx.Hd = Z1, X1, mean1, rstd1, Hd
         ctx.Z2, ctx.mean2, ctx.rstd2 = Z2, mean2, rstd2
         ctx.seeds = (pd, dict(seeds))
@@ -321,8 +332,9 @@ def encoder_layer_backward(dX2: torch.Tensor, ctx: EncoderLayerCtx, w: PackedLay
     delta = torch.empty(Np, device=dev, dtype=f32)
     K.rowdot(dO, dp, ctx.O, dp, delta, Np, dp)
     dS = torch.empty(Np, Np, device=dev, dtype=f32)
-    K.gemm(dO, V, dS, Np, Np, dp, dp, 3 * dp, Np, trans_b=True, epilogue=E.EPI_ATTN_DS, aux0=ctx.P, aux1=ctx.Pd,
-           rowvec=delta, ld_aux=Np, precision=prec, flops=att)
+    K.gemm(dO, V, dS, Np, Np, dp, dp, 3 * dp, Np, trans_b=True, epilogue=E.EPI_ATTN_DS, aux0=ctx.P,
+           aux1=ctx.Pd if ctx.keep is None else None, keep=ctx.keep, p_drop=pd, rowvec=delta, ld_aux=Np,
+           precision=prec, flops=att)
     dQKV = torch.empty(Np, 3 * dp, device=dev, dtype=f32)
     _gemm_nodes_k(ctx.Pd, dO, dQKV[:, 2 * dp:], Np, dp, Np, Np, dp, 3 * dp, trans_a=True, prec=prec, flops=att)
     _gemm_nodes_k(dS, Kt, dQKV[:, :dp], Np, dp, Np, Np, 3 * dp, 3 * dp, alpha=1.0 / math.sqrt(d), prec=prec,

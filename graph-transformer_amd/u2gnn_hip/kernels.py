@@ -67,7 +67,7 @@ def gemm_symbol(precision, M, N, split_k, tile, trans_a, trans_b, epilogue):
 
 def gemm(A, B, C, M, N, K, lda, ldb, ldc, trans_a=False, trans_b=False, epilogue=_lib.EPI_STORE, split_k=1,
          slab_stride=0, bias=None, aux0=None, aux1=None, rowvec=None, ld_aux=0, alpha=1.0, scale_cols=0, p_drop=0.0,
-         seed=0, precision="fp32", tile=0, flops=None):
+         seed=0, precision="fp32", tile=0, flops=None, keep=None):
     """C[M,N] (epilogue) sum_k A(m,k) B(k,n).  A/B/C may be views (pointer arithmetic via
     storage offsets is done by torch's data_ptr()).  ``flops``: algorithmic FLOPs of the
     launch for the roofline recorder (None = not recorded)."""
@@ -94,6 +94,9 @@ def gemm(A, B, C, M, N, K, lda, ldb, ldc, trans_a=False, trans_b=False, epilogue
     a.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
     a.precision = PREC[precision] if isinstance(precision, str) else int(precision)
     a.tile = int(tile)
+    if keep is not None:   # ATTN_DS: dropout keep bits (attn_softmax_fwd) instead of Pd
+        _dev(keep)
+        a.keep, a.ld_keep = keep.data_ptr(), keep.stride(0)
     check(hip_lib().u2gnn_gemm(ctypes.byref(a), _s()), "u2gnn_gemm")
     if rec:
         ev1.record()
@@ -136,10 +139,12 @@ def colsum(X, rows, cols_pad, ld, cblk, out, ws, accumulate=False):
                                  int(accumulate), _p(ws), _s()), "u2gnn_colsum")
 
 
-def attn_softmax_fwd(S, lds, P, Pd, ldp, rows_valid, rows_pad, n_valid, n_pad, p, seed):
-    _dev(S, P, Pd)
+def attn_softmax_fwd(S, lds, P, Pd, ldp, rows_valid, rows_pad, n_valid, n_pad, p, seed, keep=None):
+    """keep: optional int32 [rows_pad, >= n_pad/32] receiving the dropout keep bits."""
+    _dev(S, P, Pd, *([keep] if keep is not None else []))
     check(hip_lib().u2gnn_attn_softmax_fwd(_p(S), int(lds), _p(P), _p(Pd), int(ldp), int(rows_valid), int(rows_pad),
-                                           int(n_valid), int(n_pad), float(p), int(seed), _s()),
+                                           int(n_valid), int(n_pad), float(p), int(seed), _p(keep),
+                                           int(keep.stride(0)) if keep is not None else 0, _s()),
           "u2gnn_attn_softmax_fwd")
 
 

@@ -41,7 +41,8 @@ extern "C" {
 #define U2GNN_EPI_BIAS_RELU_DROP 3  /* C = drop(relu(acc + bias[n]))                      */
 #define U2GNN_EPI_RELU_DROP_BWD 4   /* C = acc * (aux0[m,n] > 0 ? 1/(1-p) : 0)            */
 #define U2GNN_EPI_ACCUM 5           /* C = C + alpha*acc                                  */
-#define U2GNN_EPI_ATTN_DS 6         /* C = aux1[m,n]*acc - aux0[m,n]*rowvec[m]            */
+#define U2GNN_EPI_ATTN_DS 6         /* C = aux1[m,n]*acc - aux0[m,n]*rowvec[m]; with keep:
+                                       C = aux0[m,n]*(keep(m,n) ? acc/(1-p_drop) : 0 - rowvec[m]) */
 
 /* Matrix-core precision of a GEMM (u2gnn_gemm_args.precision). */
 #define U2GNN_PREC_F32 0    /* v_mfma_f32_32x32x2_f32: exact fp32 fma chains            */
@@ -73,6 +74,10 @@ typedef struct u2gnn_gemm_args {
     int32_t tile;         /* 0 = auto; 64 / 128 square block tiles; bf16 modes also 256 (256x128
                              block, 8 waves) and 129 (128x128 block with a 16-deep K step, 3
                              blocks per CU: skinny weight-gradient products) */
+    const uint32_t *keep; /* ATTN_DS: dropout keep bits of the probabilities (bit n%32 of
+                             keep[m*ld_keep + n/32]) written by u2gnn_attn_softmax_fwd, or NULL
+                             (then aux1 = Pd is read) */
+    int64_t ld_keep;      /* words per row of keep */
 } u2gnn_gemm_args;
 
 /* ---- library ------------------------------------------------------------------ */
@@ -124,10 +129,12 @@ int u2gnn_colsum(const float *X, int64_t rows, int64_t cols_pad, int64_t ld, int
 
 /* ---- a3.2: attention row softmax + dropout(p) on probabilities (MHA core) ----------
  * P[i,j] = softmax_j(S[i,j], j < n_valid); Pd = P * keep / (1-p); rows >= rows_valid -> 0.
- * Pd may alias P when p == 0. */
+ * Pd may alias P when p == 0.  keep (optional, n_pad % 32 == 0): the keep decisions as bits,
+ * bit j%32 of keep[i*ld_keep + j/32] (0 for j >= n_valid and padded rows), for the ATTN_DS
+ * epilogue of the backward. */
 int u2gnn_attn_softmax_fwd(const float *S, int64_t lds, float *P, float *Pd, int64_t ldp,
                            int64_t rows_valid, int64_t rows_pad, int64_t n_valid, int64_t n_pad,
-                           float p, uint64_t seed, void *stream);
+                           float p, uint64_t seed, uint32_t *keep, int64_t ld_keep, void *stream);
 /* delta[i] = sum_c A[i,c]*B[i,c]  (rowsum(dO * O) of the attention backward) */
 int u2gnn_rowdot(const float *A, int64_t lda, const float *B, int64_t ldb, float *out, int64_t rows,
                  int64_t cols, void *stream);

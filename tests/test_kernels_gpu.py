@@ -146,6 +146,49 @@ def test_attn_softmax_masking_and_dropout():
     assert rel_err(Pd[:N, :N], ref * mask[:N, :N] * 2) < 1e-5
 
 
+def _unpack_bits(kb, cols):
+    w = kb.to(torch.int64) & 0xFFFFFFFF
+    bits = (w[:, :, None] >> torch.arange(32, device=kb.device)) & 1
+    return bits.reshape(kb.shape[0], -1)[:, :cols]
+
+
+@pytest.mark.parametrize("Np,N", [(1280, 1100), (256, 256), (2048, 1999)])
+def test_attn_softmax_keep_bits(Np, N):
+    """keep bits == the dropout mask on the valid block, 0 on padded rows/columns (n_pad not a
+    multiple of the 1024-column trip included)."""
+    S = _mk(Np, Np, seed=21)
+    P, Pd = torch.empty(Np, Np, device=DEV), torch.empty(Np, Np, device=DEV)
+    kb = torch.full((Np, Np // 32), -1, device=DEV, dtype=torch.int32)
+    K.attn_softmax_fwd(S, Np, P, Pd, Np, N, Np, N, Np, 0.5, 99, keep=kb)
+    bits = _unpack_bits(kb, Np)
+    mask = K.dropout_mask(99, Np, Np, 0.5).to(torch.int64)
+    assert torch.equal(bits[:N, :N], mask[:N, :N])
+    assert bits[:, N:].sum().item() == 0 and bits[N:].sum().item() == 0
+    assert torch.equal((Pd[:N, :N] != 0), (bits[:N, :N] == 1) & (P[:N, :N] != 0))
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16x3"])
+def test_attn_ds_epilogue_with_keep_bits(prec):
+    M = N = 256
+    Kd = 64
+    A, B = _mk(M, Kd, seed=31), _mk(N, Kd, seed=32)
+    acc = A @ B.t()
+    S = _mk(M, N, seed=33)
+    P, Pd = torch.empty(M, N, device=DEV), torch.empty(M, N, device=DEV)
+    kb = torch.empty(M, N // 32, device=DEV, dtype=torch.int32)
+    K.attn_softmax_fwd(S, N, P, Pd, N, 230, M, 230, N, 0.5, 5, keep=kb)
+    dl = _mk(M, seed=34)
+    C1, C2 = torch.empty(M, N, device=DEV), torch.empty(M, N, device=DEV)
+    K.gemm(A, B, C1, M, N, Kd, Kd, Kd, N, trans_b=True, epilogue=_lib.EPI_ATTN_DS, aux0=P, aux1=Pd, rowvec=dl,
+           ld_aux=N, precision=prec)
+    K.gemm(A, B, C2, M, N, Kd, Kd, Kd, N, trans_b=True, epilogue=_lib.EPI_ATTN_DS, aux0=P, keep=kb, p_drop=0.5,
+           rowvec=dl, ld_aux=N, precision=prec)
+    keep = _unpack_bits(kb, N).float()
+    ref = P * (keep * acc * 2 - dl[:, None])
+    assert rel_err(C2, ref) < (1e-5 if prec == "fp32" else 3e-5)
+    assert rel_err(C2, C1) < 1e-5
+
+
 def test_layernorm_fwd_bwd():
     Np, N, d, dp = 128, 100, 67, 128
     Z = _mk(Np, dp, seed=11)

@@ -9,16 +9,17 @@ import torch  # noqa: E402
 from u2gnn_hip import kernels as K  # noqa: E402
 
 Np, dp, ffp = 4864, 384, 1024
-SHAPES = [  # name, M, N, K, ta, tb, [(split, tile), ...] (tile 129-132/257: experimental pipelines)
-    ("QK^T  NT", Np, Np, dp, False, True, [(1, 128), (1, 256), (1, 131), (1, 132)]),
-    ("dS    NT", Np, Np, dp, False, True, [(1, 128), (1, 131), (1, 132)], 6),   # dO.V^T with the attention-dS epilogue
-    ("P.V   NN", Np, dp, Np, False, False, [(4, 128), (4, 256), (4, 131), (4, 132), (6, 131), (6, 132)]),
-    ("dV    TN", Np, dp, Np, True, False, [(4, 128), (4, 256), (4, 131), (4, 132), (6, 131), (6, 132)]),
-    ("dWin  TN", 3 * dp, dp, Np, True, False, [(8, 128), (8, 131), (8, 132), (16, 131)]),
-    ("dW1   TN", ffp, dp, Np, True, False, [(16, 128), (16, 131), (16, 132), (8, 131)]),
-    ("QKV   NT", Np, 3 * dp, dp, False, True, [(1, 64), (1, 256), (1, 131), (1, 132)]),
-    ("FFN1  NT", Np, ffp, dp, False, True, [(1, 64), (1, 256), (1, 131), (1, 132)]),
-    ("FFN2  NT", Np, dp, ffp, False, True, [(1, 64), (1, 131), (1, 132), (2, 131)]),
+SHAPES = [  # name, M, N, K, ta, tb, [(split, tile), ...] (tile 129 = 128x128 with a 16-deep K step)
+    ("QK^T  NT", Np, Np, dp, False, True, [(1, 128), (1, 256), (1, 129)]),
+    ("dS    NT", Np, Np, dp, False, True, [(1, 128), (1, 256)], 6),   # dO.V^T, attention-dS epilogue (Pd)
+    ("dSkb  NT", Np, Np, dp, False, True, [(1, 128), (1, 256)], 7),   # same, dropout keep bits instead of Pd
+    ("P.V   NN", Np, dp, Np, False, False, [(4, 128), (4, 256), (4, 129)]),
+    ("dV    TN", Np, dp, Np, True, False, [(4, 128), (4, 256), (4, 129)]),
+    ("dWin  TN", 3 * dp, dp, Np, True, False, [(8, 128), (8, 129), (16, 129)]),
+    ("dW1   TN", ffp, dp, Np, True, False, [(16, 128), (16, 129)]),
+    ("QKV   NT", Np, 3 * dp, dp, False, True, [(1, 64), (1, 128), (1, 256)]),
+    ("FFN1  NT", Np, ffp, dp, False, True, [(1, 64), (1, 128), (1, 256)]),
+    ("FFN2  NT", Np, dp, ffp, False, True, [(1, 64), (1, 128), (2, 129)]),
 ]
 
 
@@ -34,6 +35,11 @@ def run(prec):
         if epi == 6:
             ext = dict(epilogue=6, aux0=torch.rand(M, N, device="cuda", generator=g),
                        aux1=torch.rand(M, N, device="cuda", generator=g),
+                       rowvec=torch.randn(M, device="cuda", generator=g), ld_aux=N)
+        elif epi == 7:
+            ext = dict(epilogue=6, aux0=torch.rand(M, N, device="cuda", generator=g), p_drop=0.5,
+                       keep=torch.randint(-2**31, 2**31 - 1, (M, N // 32), device="cuda", dtype=torch.int32,
+                                          generator=g),
                        rowvec=torch.randn(M, device="cuda", generator=g), ld_aux=N)
         if ONLY and not any(name.startswith(o) for o in ONLY.split(",")):
             continue
@@ -58,6 +64,10 @@ def run(prec):
             ref = (A.t() if ta else A).double() @ (B.t() if tb else B).double()
             if epi == 6:
                 ref = ext["aux1"].double() * ref - ext["aux0"].double() * ext["rowvec"].double()[:, None]
+            elif epi == 7:
+                w = ext["keep"].to(torch.int64) & 0xFFFFFFFF
+                kb = ((w[:, :, None] >> torch.arange(32, device="cuda")) & 1).reshape(M, -1).double()
+                ref = ext["aux0"].double() * (kb * ref * 2 - ext["rowvec"].double()[:, None])
             err = ((C.sum(0).double() - ref).abs().max() / ref.abs().max()).item()
             print(f"{prec:7s} {name}  M={M:5d} N={N:5d} K={Kd:5d} split={split:2d} tile={tile:3d}: {us:8.1f} us "
                   f"{2.0 * M * N * Kd / us / 1e6:7.1f} TF/s  relerr {err:.1e}")

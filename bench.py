@@ -163,7 +163,9 @@ def main():
     rec_elapsed = None
     if not args.no_roofline:
         from u2gnn_hip.engine import set_overlap
+        from u2gnn_hip import native
         set_overlap(False)   # serial: each GEMM's events time that kernel alone
+        native.set_enabled(False)   # the same kernel sequence, launched from the evented wrappers
         K.REC.enabled = True
         torch.cuda.synchronize()
         t1 = time.perf_counter()

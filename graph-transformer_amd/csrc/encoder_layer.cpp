@@ -1,0 +1,377 @@
+// Native executor of one U2GNN encoder layer (torch TransformerEncoderLayer(d, nhead=1, ff,
+// dropout), post-LN, slot-0 rows) — forward and backward issued from C++ straight onto HIP
+// streams, one C-ABI call per layer instead of ~40 Python-side launches.
+//
+// Reference: pytorch_U2GNN_Sup.py:19-21,35 (UnSup: pytorch_U2GNN_UnSup.py:37-40,57) reach this
+// through torch.nn.TransformerEncoder; the Python orchestration of the same kernels is
+// u2gnn_hip/engine.py (encoder_layer_forward / encoder_layer_backward), which this file mirrors
+// launch for launch (same tiles, split counts and reduction order, hence bit-identical results:
+// tests/test_native_layer_gpu.py).
+//
+// Memory: every buffer is caller-allocated.  The forward writes the tensors saved for the
+// backward into a "ctx" arena and uses a scratch workspace for S and split-K slabs; the backward
+// carves all of its temporaries from one workspace with a bump allocator that never reuses a
+// byte within a call, so work left running on the side stream cannot be overwritten by the main
+// stream.  Sizes come from the same code run in planning mode (no launches).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+
+#include "u2gnn_hip.h"
+
+namespace {
+
+inline int64_t rup(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+
+struct Dims {
+    int64_t N, d, ff, Np, dp, ffp;
+    int prec;
+    bool deep_wgrad;
+};
+
+Dims make_dims(const u2gnn_layer_dims *a) {
+    Dims D;
+    D.N = a->N;
+    D.d = a->d;
+    D.ff = a->ff;
+    D.Np = rup(a->N, 128);
+    D.dp = rup(a->d, 64);
+    D.ffp = rup(a->ff, 64);
+    D.prec = a->precision;
+    D.deep_wgrad = (a->flags & U2GNN_LAYER_DEEP_WGRAD) != 0;
+    return D;
+}
+
+// bump allocator over a caller buffer; plan mode (base == nullptr) only counts
+struct Arena {
+    char *base;
+    int64_t used = 0, cap;
+    bool overflow = false;
+    Arena(void *b, int64_t c) : base(static_cast<char *>(b)), cap(c) {}
+    template <typename T>
+    T *take(int64_t n) {
+        const int64_t bytes = rup(n * (int64_t)sizeof(T), 256);
+        T *p = base ? reinterpret_cast<T *>(base + used) : nullptr;
+        used += bytes;
+        if (base && used > cap) overflow = true;
+        return p;
+    }
+    bool plan() const { return base == nullptr; }
+};
+
+#define U2GNN_TRY(x)                     \
+    do {                                 \
+        const int rc_ = (x);             \
+        if (rc_ != U2GNN_OK) return rc_; \
+    } while (0)
+
+struct Ctx {   // tensors saved by the forward for the backward
+    float *QKV, *P, *Pd, *O, *Z1, *X1, *mean1, *rstd1, *Hd, *Z2, *mean2, *rstd2;
+    uint32_t *keep;
+};
+
+Ctx carve_ctx(Arena &A, const Dims &D, bool drop) {
+    Ctx c;
+    c.QKV = A.take<float>(D.Np * 3 * D.dp);
+    c.P = A.take<float>(D.Np * D.Np);
+    c.Pd = drop ? A.take<float>(D.Np * D.Np) : c.P;
+    c.keep = drop ? A.take<uint32_t>(D.Np * (D.Np / 32)) : nullptr;
+    c.O = A.take<float>(D.Np * D.dp);
+    c.Z1 = A.take<float>(D.Np * D.dp);
+    c.X1 = A.take<float>(D.Np * D.dp);
+    c.mean1 = A.take<float>(D.Np);
+    c.rstd1 = A.take<float>(D.Np);
+    c.Hd = A.take<float>(D.Np * D.ffp);
+    c.Z2 = A.take<float>(D.Np * D.dp);
+    c.mean2 = A.take<float>(D.Np);
+    c.rstd2 = A.take<float>(D.Np);
+    return c;
+}
+
+struct G {   // one GEMM launch (defaults = plain store)
+    u2gnn_gemm_args a;
+    G(const float *A, const float *B, float *C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
+      int64_t ldc, int prec) {
+        std::memset(&a, 0, sizeof(a));
+        a.A = A, a.B = B, a.C = C, a.M = M, a.N = N, a.K = K, a.lda = lda, a.ldb = ldb, a.ldc = ldc;
+        a.epilogue = U2GNN_EPI_STORE;
+        a.split_k = 1;
+        a.alpha = 1.f;
+        a.precision = prec;
+    }
+    G &ta() { a.trans_a = 1; return *this; }
+    G &tb() { a.trans_b = 1; return *this; }
+    G &epi(int e) { a.epilogue = e; return *this; }
+    G &tile(int t) { a.tile = t; return *this; }
+    int run(hipStream_t st, bool plan) { return plan ? U2GNN_OK : u2gnn_gemm(&a, st); }
+};
+
+// engine._gemm_split: deterministic split-K into fp32 slabs + one reduce pass (alpha, accumulate,
+// padded->real block map).  deep = weight gradient (16-deep K step, <= 16 slabs).
+int gemm_split(Arena &W, const Dims &D, const float *A, const float *B, float *C, int64_t M, int64_t N, int64_t Kd,
+               int64_t lda, int64_t ldb, int64_t ldc, bool ta, float alpha, bool accumulate, const int64_t *rblk,
+               const int64_t *cblk, bool deep, hipStream_t st) {
+    const bool f32 = D.prec == U2GNN_PREC_F32;
+    const int64_t bk = f32 ? 16 : 32;
+    int t;
+    int64_t tiles, target = 448;
+    if (!f32 && M % 256 == 0 && N % 128 == 0 && (M / 256) * (N / 128) >= 32) {
+        t = 256, tiles = (M / 256) * (N / 128), target = 240;
+    } else {
+        t = (M % 128 == 0 && N % 128 == 0) ? 128 : 64;
+        tiles = (M / t) * (N / t);
+    }
+    int64_t split = target / (tiles > 0 ? tiles : 1);
+    if (Kd / (4 * bk) < split) split = Kd / (4 * bk);
+    if (split < 1) split = 1;
+    if (deep && D.deep_wgrad && !f32 && t == 128) {
+        t = 129;
+        split = target / (tiles > 0 ? tiles : 1);
+        if (split > 16) split = 16;
+        if (split < 1) split = 1;
+    }
+    const bool plan = W.plan();
+    const bool mapped = rblk != nullptr;
+    if (split == 1 && !mapped) {
+        G g(A, B, C, M, N, Kd, lda, ldb, ldc, D.prec);
+        if (ta) g.ta();
+        g.a.alpha = alpha;
+        g.epi(accumulate ? U2GNN_EPI_ACCUM : U2GNN_EPI_STORE).tile(t);
+        return g.run(st, plan);
+    }
+    float *slabs = W.take<float>(split * M * N);
+    G g(A, B, slabs, M, N, Kd, lda, ldb, N, D.prec);
+    if (ta) g.ta();
+    g.a.split_k = (int32_t)split;
+    g.a.slab_stride = M * N;
+    g.tile(t);
+    U2GNN_TRY(g.run(st, plan));
+    if (plan) return U2GNN_OK;
+    const int64_t rb0 = rblk ? rblk[0] : M, rb1 = rblk ? rblk[1] : M;
+    const int64_t cb0 = cblk ? cblk[0] : N, cb1 = cblk ? cblk[1] : N;
+    return u2gnn_slab_reduce(slabs, (int32_t)split, M * N, M, N, N, rb0, rb1, cb0, cb1, C, ldc, alpha,
+                             accumulate ? 1 : 0, st);
+}
+
+// engine._wgrad: dst(real) = unpack(dY^T X)
+int wgrad(Arena &W, const Dims &D, const float *dY, int64_t ld_dy, const float *X, int64_t ld_x, int64_t m_pad,
+          int64_t n_pad, float *dst, int64_t ld_dst, const int64_t *rblk, const int64_t *cblk, hipStream_t st) {
+    return gemm_split(W, D, dY, X, dst, m_pad, n_pad, D.Np, ld_dy, ld_x, ld_dst, true, 1.f, false, rblk, cblk, true,
+                      st);
+}
+
+int64_t colstat_ws_floats(int64_t rows, int64_t cols) { return ((rows + 15) / 16 > 0 ? (rows + 15) / 16 : 1) * 3 * cols; }
+
+int bias_grad(Arena &W, const float *dY, int64_t rows, int64_t cols_pad, int64_t ld, int64_t cb0, int64_t cb1,
+              float *out, hipStream_t st) {
+    float *ws = W.take<float>(colstat_ws_floats(rows, cols_pad));
+    if (W.plan()) return U2GNN_OK;
+    return u2gnn_colsum(dY, rows, cols_pad, ld, cb0, cb1, out, 0, ws, st);
+}
+
+// side-stream hand-off: the side stream waits for everything issued on main so far
+struct Side {
+    hipStream_t main, side;
+    bool plan;
+    int fork() {
+        if (plan || side == main) return U2GNN_OK;
+        hipEvent_t ev;
+        hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+        if (e != hipSuccess) return (int)e;
+        e = hipEventRecord(ev, main);
+        if (e == hipSuccess) e = hipStreamWaitEvent(side, ev, 0);
+        const hipError_t e2 = hipEventDestroy(ev);   // resources released once the recorded work completes
+        if (e == hipSuccess) e = e2;
+        return e == hipSuccess ? U2GNN_OK : (int)e;
+    }
+};
+
+int layer_fwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seeds *s, const float *X, float *X2,
+              Arena &CA, Arena &W, bool need_ctx, hipStream_t st) {
+    const int64_t N = D.N, Np = D.Np, d = D.d, dp = D.dp, ffp = D.ffp;
+    const int prec = D.prec;
+    const float pd = s->p_drop;
+    const bool drop = pd > 0.f;
+    const bool plan = W.plan();
+    Ctx c = carve_ctx(need_ctx ? CA : W, D, drop);
+    if (!need_ctx) c.keep = nullptr;
+    // a3.1 in-projection (+bias, Q scaled by 1/sqrt(d))
+    {
+        G g(X, w->W_in, c.QKV, Np, 3 * dp, dp, dp, dp, 3 * dp, prec);
+        g.tb().epi(U2GNN_EPI_BIAS);
+        g.a.bias = w->b_in;
+        g.a.alpha = (float)(1.0 / std::sqrt((double)d));
+        g.a.scale_cols = dp;
+        U2GNN_TRY(g.run(st, plan));
+    }
+    const float *Q = c.QKV, *Kt = c.QKV + dp, *V = c.QKV + 2 * dp;
+    // a3.2 scores, softmax + dropout, P.V
+    float *S = W.take<float>(Np * Np);
+    {
+        G g(Q, Kt, S, Np, Np, dp, 3 * dp, 3 * dp, Np, prec);
+        g.tb().tile((prec != U2GNN_PREC_F32 && Np % 256 == 0) ? 256 : 0);
+        U2GNN_TRY(g.run(st, plan));
+    }
+    if (!plan)
+        U2GNN_TRY(u2gnn_attn_softmax_fwd(S, Np, c.P, c.Pd, Np, N, Np, N, Np, pd, s->attn, c.keep, Np / 32, st));
+    U2GNN_TRY(gemm_split(W, D, c.Pd, V, c.O, Np, dp, Np, Np, 3 * dp, dp, false, 1.f, false, nullptr, nullptr, false,
+                         st));
+    // a3.3 out-projection + dropout1 + residual, LayerNorm1
+    {
+        G g(c.O, w->W_o, c.Z1, Np, dp, dp, dp, dp, dp, prec);
+        g.tb().epi(U2GNN_EPI_BIAS_DROP_RESID);
+        g.a.bias = w->b_o, g.a.aux0 = X, g.a.ld_aux = dp, g.a.p_drop = pd, g.a.seed = s->drop1;
+        U2GNN_TRY(g.run(st, plan));
+    }
+    if (!plan) U2GNN_TRY(u2gnn_layernorm_fwd(c.Z1, dp, w->n1_w, w->n1_b, c.X1, dp, c.mean1, c.rstd1, N, Np, d, dp, 1e-5f, st));
+    // a3.4 FFN + dropout2 + residual, LayerNorm2
+    {
+        G g(c.X1, w->W1, c.Hd, Np, ffp, dp, dp, dp, ffp, prec);
+        g.tb().epi(U2GNN_EPI_BIAS_RELU_DROP);
+        g.a.bias = w->b1, g.a.p_drop = pd, g.a.seed = s->dropff;
+        U2GNN_TRY(g.run(st, plan));
+    }
+    {
+        G g(c.Hd, w->W2, c.Z2, Np, dp, ffp, ffp, ffp, dp, prec);
+        g.tb().epi(U2GNN_EPI_BIAS_DROP_RESID);
+        g.a.bias = w->b2, g.a.aux0 = c.X1, g.a.ld_aux = dp, g.a.p_drop = pd, g.a.seed = s->drop2;
+        U2GNN_TRY(g.run(st, plan));
+    }
+    if (!plan) U2GNN_TRY(u2gnn_layernorm_fwd(c.Z2, dp, w->n2_w, w->n2_b, X2, dp, c.mean2, c.rstd2, N, Np, d, dp, 1e-5f, st));
+    return (W.overflow || CA.overflow) ? U2GNN_E_ARG : U2GNN_OK;
+}
+
+int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seeds *s, const float *X, Arena &CA,
+              const float *dX2, float *dX, const u2gnn_layer_grads *g, Arena &W, hipStream_t st, hipStream_t side_st) {
+    const int64_t N = D.N, Np = D.Np, d = D.d, dp = D.dp, ff = D.ff, ffp = D.ffp;
+    const int prec = D.prec;
+    const float pd = s->p_drop;
+    const bool drop = pd > 0.f;
+    const bool plan = W.plan();
+    Ctx c = carve_ctx(CA, D, drop);
+    Side sd{st, side_st ? side_st : st, plan};
+    hipStream_t so = sd.side;
+    const int64_t blk_d[2] = {dp, d}, blk_ff[2] = {ffp, ff};
+    float *ws = W.take<float>(colstat_ws_floats(N, dp));
+    // LN2 backward -> dX1 (residual), dF (dropout2 branch); norm2 + linear2.bias grads (side)
+    float *dX1 = W.take<float>(Np * dp), *dF = W.take<float>(Np * dp);
+    if (!plan)
+        U2GNN_TRY(u2gnn_layernorm_bwd(dX2, dp, c.Z2, dp, c.mean2, c.rstd2, w->n2_w, dX1, dp, dF, dp, pd, s->drop2, N,
+                                      Np, d, dp, st));
+    U2GNN_TRY(sd.fork());
+    if (!plan)
+        U2GNN_TRY(u2gnn_layernorm_bwd_params(dX2, dp, c.Z2, dp, c.mean2, c.rstd2, dF, dp, N, d, dp, ws, g->n2_w,
+                                             g->n2_b, g->l2_b, so));
+    // FFN
+    float *dH = W.take<float>(Np * ffp);
+    {
+        G gg(dF, w->W2, dH, Np, ffp, dp, dp, ffp, ffp, prec);
+        gg.epi(U2GNN_EPI_RELU_DROP_BWD);
+        gg.a.aux0 = c.Hd, gg.a.ld_aux = ffp, gg.a.p_drop = pd;
+        U2GNN_TRY(gg.run(st, plan));
+    }
+    U2GNN_TRY(wgrad(W, D, dF, dp, c.Hd, ffp, dp, ffp, g->l2_w, ff, blk_d, blk_ff, so));   // side (forked above)
+    U2GNN_TRY(gemm_split(W, D, dH, w->W1, dX1, Np, dp, ffp, ffp, dp, dp, false, 1.f, true, nullptr, nullptr, false,
+                         st));
+    U2GNN_TRY(sd.fork());
+    U2GNN_TRY(wgrad(W, D, dH, ffp, c.X1, dp, ffp, dp, g->l1_w, d, blk_ff, blk_d, so));
+    U2GNN_TRY(bias_grad(W, dH, Np, ffp, ffp, ffp, ff, g->l1_b, so));
+    // LN1 backward -> dX (residual), dA (dropout1 branch); norm1 + out_proj.bias grads (side)
+    float *dA = W.take<float>(Np * dp);
+    if (!plan)
+        U2GNN_TRY(u2gnn_layernorm_bwd(dX1, dp, c.Z1, dp, c.mean1, c.rstd1, w->n1_w, dX, dp, dA, dp, pd, s->drop1, N,
+                                      Np, d, dp, st));
+    U2GNN_TRY(sd.fork());
+    if (!plan)
+        U2GNN_TRY(u2gnn_layernorm_bwd_params(dX1, dp, c.Z1, dp, c.mean1, c.rstd1, dA, dp, N, d, dp, ws, g->n1_w,
+                                             g->n1_b, g->out_b, so));
+    // out-projection
+    float *dO = W.take<float>(Np * dp);
+    {
+        G gg(dA, w->W_o, dO, Np, dp, dp, dp, dp, dp, prec);
+        U2GNN_TRY(gg.run(st, plan));
+    }
+    U2GNN_TRY(wgrad(W, D, dA, dp, c.O, dp, dp, dp, g->out_w, d, blk_d, blk_d, so));   // side (forked above)
+    // attention core
+    const float *Q = c.QKV, *Kt = c.QKV + dp, *V = c.QKV + 2 * dp;
+    float *delta = W.take<float>(Np);
+    if (!plan) U2GNN_TRY(u2gnn_rowdot(dO, dp, c.O, dp, delta, Np, dp, st));
+    float *dS = W.take<float>(Np * Np);
+    {
+        G gg(dO, V, dS, Np, Np, dp, dp, 3 * dp, Np, prec);
+        gg.tb().epi(U2GNN_EPI_ATTN_DS);
+        gg.a.aux0 = c.P, gg.a.rowvec = delta, gg.a.ld_aux = Np, gg.a.p_drop = pd;
+        if (c.keep) {
+            gg.a.keep = c.keep, gg.a.ld_keep = Np / 32;
+        } else {
+            gg.a.aux1 = c.Pd;
+        }
+        U2GNN_TRY(gg.run(st, plan));
+    }
+    float *dQKV = W.take<float>(Np * 3 * dp);
+    U2GNN_TRY(gemm_split(W, D, c.Pd, dO, dQKV + 2 * dp, Np, dp, Np, Np, dp, 3 * dp, true, 1.f, false, nullptr,
+                         nullptr, false, st));
+    U2GNN_TRY(gemm_split(W, D, dS, Kt, dQKV, Np, dp, Np, Np, 3 * dp, 3 * dp, false, (float)(1.0 / std::sqrt((double)d)), false,
+                         nullptr, nullptr, false, st));
+    U2GNN_TRY(gemm_split(W, D, dS, Q, dQKV + dp, Np, dp, Np, Np, 3 * dp, 3 * dp, true, 1.f, false, nullptr, nullptr,
+                         false, st));
+    // in-projection
+    U2GNN_TRY(gemm_split(W, D, dQKV, w->W_in, dX, Np, dp, 3 * dp, 3 * dp, dp, dp, false, 1.f, true, nullptr, nullptr,
+                         false, st));
+    U2GNN_TRY(sd.fork());
+    U2GNN_TRY(wgrad(W, D, dQKV, 3 * dp, X, dp, 3 * dp, dp, g->in_w, d, blk_d, blk_d, so));
+    U2GNN_TRY(bias_grad(W, dQKV, Np, 3 * dp, 3 * dp, dp, d, g->in_b, so));
+    return (W.overflow || CA.overflow) ? U2GNN_E_ARG : U2GNN_OK;
+}
+
+bool dims_ok(const u2gnn_layer_dims *a) {
+    return a && a->N >= 1 && a->d >= 1 && a->ff >= 1 && rup(a->d, 64) <= 1024 &&
+           (a->precision == U2GNN_PREC_F32 || a->precision == U2GNN_PREC_BF16X3 || a->precision == U2GNN_PREC_BF16);
+}
+
+}  // namespace
+
+extern "C" {
+
+int u2gnn_layer_sizes(const u2gnn_layer_dims *dims, float p_drop, int64_t *ctx_bytes, int64_t *fwd_ws_bytes,
+                      int64_t *bwd_ws_bytes) {
+    if (!dims_ok(dims) || !ctx_bytes || !fwd_ws_bytes || !bwd_ws_bytes) return U2GNN_E_ARG;
+    const Dims D = make_dims(dims);
+    u2gnn_layer_seeds s;
+    std::memset(&s, 0, sizeof(s));
+    s.p_drop = p_drop;
+    u2gnn_layer_params w;
+    std::memset(&w, 0, sizeof(w));
+    u2gnn_layer_grads g;
+    std::memset(&g, 0, sizeof(g));
+    Arena C(nullptr, 0), Wf(nullptr, 0), Wb(nullptr, 0), Cb(nullptr, 0);
+    layer_fwd(D, &w, &s, nullptr, nullptr, C, Wf, true, nullptr);
+    layer_bwd(D, &w, &s, nullptr, Cb, nullptr, nullptr, &g, Wb, nullptr, nullptr);
+    *ctx_bytes = C.used;
+    *fwd_ws_bytes = Wf.used;
+    *bwd_ws_bytes = Wb.used;
+    return U2GNN_OK;
+}
+
+int u2gnn_layer_fwd(const u2gnn_layer_dims *dims, const u2gnn_layer_params *w, const u2gnn_layer_seeds *s,
+                    const float *X, float *X2, void *ctx, int64_t ctx_bytes, void *ws, int64_t ws_bytes,
+                    void *stream) {
+    if (!dims_ok(dims) || !w || !s || !X || !X2 || !ws) return U2GNN_E_ARG;
+    const Dims D = make_dims(dims);
+    Arena C(ctx, ctx_bytes), W(ws, ws_bytes);
+    return layer_fwd(D, w, s, X, X2, C, W, ctx != nullptr, reinterpret_cast<hipStream_t>(stream));
+}
+
+int u2gnn_layer_bwd(const u2gnn_layer_dims *dims, const u2gnn_layer_params *w, const u2gnn_layer_seeds *s,
+                    const float *X, const void *ctx, int64_t ctx_bytes, const float *dX2, float *dX,
+                    const u2gnn_layer_grads *g, void *ws, int64_t ws_bytes, void *stream, void *side_stream) {
+    if (!dims_ok(dims) || !w || !s || !X || !ctx || !dX2 || !dX || !g || !ws) return U2GNN_E_ARG;
+    const Dims D = make_dims(dims);
+    Arena C(const_cast<void *>(ctx), ctx_bytes), W(ws, ws_bytes);
+    return layer_bwd(D, w, s, X, C, dX2, dX, g, W, reinterpret_cast<hipStream_t>(stream),
+                     reinterpret_cast<hipStream_t>(side_stream));
+}
+
+}  // extern "C"

@@ -58,6 +58,29 @@ class PackDesc(ctypes.Structure):
                 ("cblk_real", c_int64), ("ld_dst", c_int64)]
 
 
+class LayerDims(ctypes.Structure):
+    _fields_ = [("N", c_int64), ("d", c_int64), ("ff", c_int64), ("precision", c_int32), ("flags", c_int32)]
+
+
+_PKEYS = ("in_w", "in_b", "out_w", "out_b", "l1_w", "l1_b", "l2_w", "l2_b", "n1_w", "n1_b", "n2_w", "n2_b")
+
+
+class LayerParamsC(ctypes.Structure):
+    _fields_ = [(k, c_void_p) for k in ("W_in", "b_in", "W_o", "b_o", "W1", "b1", "W2", "b2",
+                                        "n1_w", "n1_b", "n2_w", "n2_b")]
+
+
+class LayerSeeds(ctypes.Structure):
+    _fields_ = [("p_drop", c_float), ("attn", c_uint64), ("drop1", c_uint64), ("dropff", c_uint64),
+                ("drop2", c_uint64)]
+
+
+class LayerGrads(ctypes.Structure):
+    _fields_ = [(k, c_void_p) for k in _PKEYS]
+
+
+LAYER_DEEP_WGRAD = 1
+
 I64, F32, VP, I32 = c_int64, c_float, c_void_p, c_int32
 
 _HIP_SIGS = {
@@ -65,6 +88,11 @@ _HIP_SIGS = {
     "u2gnn_gather_rows": ([VP, I64, I64, VP, I64, VP, I64, I64, I64, I64, I64, VP, VP], c_int32),
     "u2gnn_scatter_add_rows": ([VP, I64, VP, I64, VP, I64, I64, I64, VP], c_int32),
     "u2gnn_gemm": ([POINTER(GemmArgs), VP], c_int32),
+    "u2gnn_layer_sizes": ([POINTER(LayerDims), F32, POINTER(c_int64), POINTER(c_int64), POINTER(c_int64)], c_int32),
+    "u2gnn_layer_fwd": ([POINTER(LayerDims), POINTER(LayerParamsC), POINTER(LayerSeeds), VP, VP, VP, I64, VP, I64,
+                         VP], c_int32),
+    "u2gnn_layer_bwd": ([POINTER(LayerDims), POINTER(LayerParamsC), POINTER(LayerSeeds), VP, VP, I64, VP, VP,
+                         POINTER(LayerGrads), VP, I64, VP, VP], c_int32),
     "u2gnn_slab_reduce": ([VP, I32, I64, I64, I64, I64, I64, I64, I64, I64, VP, I64, F32, I32, VP], c_int32),
     "u2gnn_pack_padded": ([VP, I64, I64, I64, I64, I64, I64, I64, VP, I64, VP], c_int32),
     "u2gnn_colsum": ([VP, I64, I64, I64, I64, I64, VP, I32, VP, VP], c_int32),

@@ -17,6 +17,8 @@ import numpy as np
 import torch
 
 from . import kernels as K
+from . import native
+from .engine import deep_wgrad as engine_deep_wgrad
 from .engine import (SITE_ATTN, SITE_DROP1, SITE_DROP2, SITE_DROPFF, SITE_HEAD, Dims, LayerParams, PackedLayer,
                      OffPath, encoder_layer_backward, encoder_layer_forward, rup, site_seed)
 
@@ -101,8 +103,12 @@ class EncoderStack:
             lctx = []
             for t in range(self.T):
                 seeds = {s: site_seed(seed, l, t, s) for s in (SITE_ATTN, SITE_DROP1, SITE_DROPFF, SITE_DROP2)}
-                X, c = encoder_layer_forward(X, self.packed[l][t], self.layer_params(l, t), dims, train, seeds,
-                                             need_ctx, self.prec, self.p_enc)
+                if native.enabled():
+                    X, c = native.layer_forward(X, self.packed[l][t], self.layer_params(l, t), dims, train, seeds,
+                                                need_ctx, self.prec, self.p_enc, deep_wgrad=engine_deep_wgrad())
+                else:
+                    X, c = encoder_layer_forward(X, self.packed[l][t], self.layer_params(l, t), dims, train, seeds,
+                                                 need_ctx, self.prec, self.p_enc)
                 lctx.append(c)
             outs.append(X)
             lctxs.append(lctx)
@@ -126,8 +132,13 @@ class EncoderStack:
             for t in reversed(range(self.T)):
                 pre = f"{prefix}.{l}.layers.{t}."
                 g = LayerParams(*[grads[pre + k] for k in LAYER_KEYS])
-                dX = encoder_layer_backward(dX, ctx["layers"][l][t], self.packed[l][t], self.layer_params(l, t), g,
-                                            dims, self.prec, off=off)
+                lc = ctx["layers"][l][t]
+                if isinstance(lc, native.NativeCtx):
+                    dX = native.layer_backward(dX, lc, self.packed[l][t], self.layer_params(l, t), g, dims,
+                                               self.prec, side=off.side, deep_wgrad=engine_deep_wgrad())
+                else:
+                    dX = encoder_layer_backward(dX, lc, self.packed[l][t], self.layer_params(l, t), g, dims,
+                                                self.prec, off=off)
             dnext = dX
         off.join()   # parameter gradients complete before the caller's optimizer reads them
         return dnext

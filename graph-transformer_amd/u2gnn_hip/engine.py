@@ -138,6 +138,10 @@ class EncoderLayerCtx:
 _DEEP_WGRAD = os.environ.get("U2GNN_DEEP_WGRAD", "1") == "1"
 
 
+def deep_wgrad() -> bool:
+    return _DEEP_WGRAD
+
+
 # Gradient work off the backward's critical path (weight, bias and LayerNorm-parameter gradients)
 # runs on a second HIP stream, overlapping the dX chain; U2GNN_OVERLAP=0 serialises it.
 _OVERLAP = [os.environ.get("U2GNN_OVERLAP", "1") == "1"]

@@ -1,0 +1,112 @@
+"""Python handle on the native encoder-layer executor (csrc/encoder_layer.cpp,
+include/u2gnn_hip.h u2gnn_layer_*): one C-ABI call per layer forward / backward.
+
+engine.py issues the same kernel sequence launch by launch from Python (kept as the readable
+reference orchestration and for per-GEMM event timing); this module is the production path.
+Buffers come from the torch caching allocator: the forward's saved tensors live in one uint8
+"ctx" tensor per layer, workspaces are allocated per call.  Memory read by the backward's
+side stream is record_stream'ed so the allocator cannot recycle it early.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Dict, Optional
+
+import torch
+
+from . import _lib
+from ._lib import LayerDims, LayerGrads, LayerParamsC, LayerSeeds, check, hip_lib
+from .kernels import PREC
+
+_SIZES: Dict[tuple, tuple] = {}
+
+
+_ENABLED = [os.environ.get("U2GNN_NATIVE_LAYER", "1") == "1"]
+
+
+def enabled() -> bool:
+    """U2GNN_NATIVE_LAYER=0 routes layers through the Python orchestration (engine.py)."""
+    return _ENABLED[0]
+
+
+def set_enabled(on: bool) -> bool:
+    """bench.py's per-GEMM timing pass runs the Python orchestration (its wrappers carry the HIP
+    events); returns the previous setting."""
+    prev = _ENABLED[0]
+    _ENABLED[0] = bool(on)
+    return prev
+
+
+def _dims(N: int, d: int, ff: int, prec: str, deep_wgrad: bool) -> LayerDims:
+    return LayerDims(int(N), int(d), int(ff), PREC[prec], _lib.LAYER_DEEP_WGRAD if deep_wgrad else 0)
+
+
+def sizes(N: int, d: int, ff: int, prec: str, p_drop: float, deep_wgrad: bool = True):
+    key = (N, d, ff, prec, p_drop > 0, deep_wgrad)
+    r = _SIZES.get(key)
+    if r is None:
+        c, f, b = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        dims = _dims(N, d, ff, prec, deep_wgrad)
+        check(hip_lib().u2gnn_layer_sizes(ctypes.byref(dims), float(p_drop), ctypes.byref(c), ctypes.byref(f),
+                                          ctypes.byref(b)), "u2gnn_layer_sizes")
+        r = _SIZES[key] = (c.value, f.value, b.value)
+    return r
+
+
+def _params(packed, p) -> LayerParamsC:
+    return LayerParamsC(packed.W_in.data_ptr(), packed.b_in.data_ptr(), packed.W_o.data_ptr(), packed.b_o.data_ptr(),
+                        packed.W1.data_ptr(), packed.b1.data_ptr(), packed.W2.data_ptr(), packed.b2.data_ptr(),
+                        p.n1_w.data_ptr(), p.n1_b.data_ptr(), p.n2_w.data_ptr(), p.n2_b.data_ptr())
+
+
+def _seeds(p_drop: float, seeds: Dict[int, int]) -> LayerSeeds:
+    from .engine import SITE_ATTN, SITE_DROP1, SITE_DROP2, SITE_DROPFF
+    return LayerSeeds(float(p_drop), seeds.get(SITE_ATTN, 0), seeds.get(SITE_DROP1, 0), seeds.get(SITE_DROPFF, 0),
+                      seeds.get(SITE_DROP2, 0))
+
+
+class NativeCtx:
+    """What the backward needs from one layer's forward."""
+    __slots__ = ("X", "buf", "p_drop", "seeds")
+
+
+def _stream(s=None):
+    return ctypes.c_void_p((s or torch.cuda.current_stream()).cuda_stream)
+
+
+def layer_forward(X: torch.Tensor, packed, p, dims, train: bool, seeds: Dict[int, int], need_ctx: bool,
+                  prec: str, p_enc: float, deep_wgrad: bool = True):
+    pd = p_enc if train else 0.0
+    cb, fb, _ = sizes(dims.N, dims.d, dims.ff, prec, pd, deep_wgrad)
+    dev = X.device
+    X2 = torch.empty(dims.Np, dims.dp, device=dev, dtype=torch.float32)
+    buf = torch.empty(cb, device=dev, dtype=torch.uint8) if need_ctx else None
+    ws = torch.empty(fb + (0 if need_ctx else cb), device=dev, dtype=torch.uint8)
+    dd, pp, ss = _dims(dims.N, dims.d, dims.ff, prec, deep_wgrad), _params(packed, p), _seeds(pd, seeds)
+    check(hip_lib().u2gnn_layer_fwd(ctypes.byref(dd), ctypes.byref(pp), ctypes.byref(ss), X.data_ptr(),
+                                    X2.data_ptr(), buf.data_ptr() if buf is not None else None, cb,
+                                    ws.data_ptr(), ws.numel(), _stream()), "u2gnn_layer_fwd")
+    ctx = None
+    if need_ctx:
+        ctx = NativeCtx()
+        ctx.X, ctx.buf, ctx.p_drop, ctx.seeds = X, buf, pd, dict(seeds)
+    return X2, ctx
+
+
+def layer_backward(dX2: torch.Tensor, ctx: NativeCtx, packed, p, g, dims, prec: str,
+                   side: Optional["torch.cuda.Stream"] = None, deep_wgrad: bool = True) -> torch.Tensor:
+    cb, _, bb = sizes(dims.N, dims.d, dims.ff, prec, ctx.p_drop, deep_wgrad)
+    dev = dX2.device
+    dX = torch.empty(dims.Np, dims.dp, device=dev, dtype=torch.float32)
+    ws = torch.empty(bb, device=dev, dtype=torch.uint8)
+    dd, pp, ss = _dims(dims.N, dims.d, dims.ff, prec, deep_wgrad), _params(packed, p), _seeds(ctx.p_drop, ctx.seeds)
+    gg = LayerGrads(*[getattr(g, k).data_ptr() for k in _lib._PKEYS])
+    check(hip_lib().u2gnn_layer_bwd(ctypes.byref(dd), ctypes.byref(pp), ctypes.byref(ss), ctx.X.data_ptr(),
+                                    ctx.buf.data_ptr(), cb, dX2.data_ptr(), dX.data_ptr(), ctypes.byref(gg),
+                                    ws.data_ptr(), ws.numel(), _stream(), _stream(side) if side is not None else None),
+          "u2gnn_layer_bwd")
+    if side is not None:
+        for t in (ws, ctx.buf, ctx.X, dX2):
+            t.record_stream(side)
+    return dX

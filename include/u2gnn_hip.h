@@ -217,6 +217,44 @@ int u2gnn_dropout(const float *X, int64_t ldx, float *Y, int64_t ldy, int64_t ro
 /* out[i*cols + j] = keep(seed, i, j) ? 1 : 0   (the exact dropout mask the kernels apply) */
 int u2gnn_dropout_mask(uint64_t seed, int64_t rows, int64_t cols, float p, uint8_t *out, void *stream);
 
+/* ---- a3: one encoder layer (TransformerEncoderLayer(d, nhead=1, ff, dropout), post-LN, slot-0
+ * rows) issued natively: forward and backward of pytorch_U2GNN_Sup.py:19-21,35 /
+ * pytorch_U2GNN_UnSup.py:37-40,57, launch-for-launch the sequence of u2gnn_hip/engine.py.
+ * Padded layouts: Np = roundup(N,128) rows, dp = roundup(d,64), ffp = roundup(ff,64) columns.
+ * All buffers are caller-allocated; u2gnn_layer_sizes gives the three sizes (ctx = tensors
+ * saved for the backward, fwd/bwd workspaces).  The backward's parameter-gradient work goes to
+ * side_stream (NULL: same stream) after the main-stream results it reads; the caller joins the
+ * streams before reading grads and must keep X, ctx, dX2 and ws alive until side_stream drains. */
+#define U2GNN_LAYER_DEEP_WGRAD 1   /* weight gradients on the 16-deep-K 128x128 tile */
+typedef struct u2gnn_layer_dims {
+    int64_t N, d, ff;      /* real nodes, model width, FFN width */
+    int32_t precision;     /* U2GNN_PREC_* */
+    int32_t flags;         /* U2GNN_LAYER_* */
+} u2gnn_layer_dims;
+typedef struct u2gnn_layer_params {
+    const float *W_in, *b_in, *W_o, *b_o, *W1, *b1, *W2, *b2;   /* padded copies ([3dp,dp], [3dp], ...) */
+    const float *n1_w, *n1_b, *n2_w, *n2_b;                      /* LayerNorm affine, real [d] */
+} u2gnn_layer_params;
+typedef struct u2gnn_layer_seeds {
+    float p_drop;          /* 0 in eval mode */
+    uint64_t attn, drop1, dropff, drop2;   /* per-site dropout seeds */
+} u2gnn_layer_seeds;
+typedef struct u2gnn_layer_grads {  /* real-shaped parameter gradients, overwritten */
+    float *in_w, *in_b, *out_w, *out_b, *l1_w, *l1_b, *l2_w, *l2_b, *n1_w, *n1_b, *n2_w, *n2_b;
+} u2gnn_layer_grads;
+int u2gnn_layer_sizes(const u2gnn_layer_dims *dims, float p_drop, int64_t *ctx_bytes,
+                      int64_t *fwd_ws_bytes, int64_t *bwd_ws_bytes);
+/* X, X2: [Np, dp]; ctx may be NULL when no backward follows (the saved tensors then live in ws,
+ * which must be ctx_bytes + fwd_ws_bytes large). */
+int u2gnn_layer_fwd(const u2gnn_layer_dims *dims, const u2gnn_layer_params *w,
+                    const u2gnn_layer_seeds *s, const float *X, float *X2, void *ctx,
+                    int64_t ctx_bytes, void *ws, int64_t ws_bytes, void *stream);
+/* dX2, dX: [Np, dp]; X is the forward's input. */
+int u2gnn_layer_bwd(const u2gnn_layer_dims *dims, const u2gnn_layer_params *w,
+                    const u2gnn_layer_seeds *s, const float *X, const void *ctx, int64_t ctx_bytes,
+                    const float *dX2, float *dX, const u2gnn_layer_grads *g, void *ws,
+                    int64_t ws_bytes, void *stream, void *side_stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -210,73 +210,92 @@ __device__ __forceinline__ uint32_t spread4(uint32_t x) {
     return x;
 }
 
+// One 256-thread block per row.  The row (n_pad <= 1024 * RV columns) is read ONCE into
+// registers: block max, then e = exp(s - max) and its block sum (one exp per element), then P,
+// Pd and the keep bits are written from the registers.  RV = float4 per thread: 8, 16 or 32
+// (rows of up to 8192 / 16384 / 32768 keys).
+constexpr int SM_RV_MAX = 32;
+
+__device__ __forceinline__ float block_max4(float v, float *red, int lane, int w) {
+    v = wave_max(v);
+    __syncthreads();
+    if (lane == 0) red[w] = v;
+    __syncthreads();
+    return fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+}
+
+__device__ __forceinline__ float block_sum4(float v, float *red, int lane, int w) {
+    v = wave_sum(v);
+    __syncthreads();
+    if (lane == 0) red[w] = v;
+    __syncthreads();
+    return (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+template <int SM_RV>
 __global__ void __launch_bounds__(256) attn_softmax_kernel(const float *S, int64_t lds, float *P, float *Pd,
                                                            int64_t ldp, int64_t rows_valid, int64_t n_valid,
                                                            int64_t n_pad, float p, uint64_t seed, uint32_t *keep,
                                                            int64_t ld_keep) {
-    __shared__ float red_m[4], red_s[4];
+    __shared__ float red[4];
     const int64_t row = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     float *prow = P + row * ldp;
     float *pdrow = Pd + row * ldp;
     uint32_t *krow = keep ? keep + row * ld_keep : nullptr;
     const bool write_pd = Pd != P;
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
     if (row >= rows_valid) {
         for (int64_t c = tid * 4; c < n_pad; c += 1024) {
-            *reinterpret_cast<float4 *>(prow + c) = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (write_pd) *reinterpret_cast<float4 *>(pdrow + c) = make_float4(0.f, 0.f, 0.f, 0.f);
+            *reinterpret_cast<float4 *>(prow + c) = z4;
+            if (write_pd) *reinterpret_cast<float4 *>(pdrow + c) = z4;
         }
         if (krow)
             for (int64_t k = tid; k < n_pad / 32; k += 256) krow[k] = 0u;
         return;
     }
     const float *srow = S + row * lds;
-    float m = -INFINITY, s = 0.f;
-    for (int64_t c = tid * 4; c < n_pad; c += 1024) {
-        const float4 v = *reinterpret_cast<const float4 *>(srow + c);
+    float e[SM_RV][4];
+    float m = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < SM_RV; ++i) {
+        const int64_t c = (int64_t)i * 1024 + tid * 4;
+        const float4 v = c < n_pad ? *reinterpret_cast<const float4 *>(srow + c) : z4;
         const float x[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            if (c + j < n_valid) {
-                const float mn = fmaxf(m, x[j]);
-                s = s * expf(m - mn) + expf(x[j] - mn);
-                m = mn;
-            }
+            e[i][j] = c + j < n_valid ? x[j] : -INFINITY;
+            m = fmaxf(m, e[i][j]);
         }
     }
-    // combine (m, s) across the wave, then across the 4 waves
-    const float mw = wave_max(m);
-    s = (m == -INFINITY) ? 0.f : s * expf(m - mw);
-    s = wave_sum(s);
-    if (lane == 0) {
-        red_m[w] = mw;
-        red_s[w] = s;
-    }
-    __syncthreads();
-    const float M = fmaxf(fmaxf(red_m[0], red_m[1]), fmaxf(red_m[2], red_m[3]));
-    float tot = 0.f;
+    const float M = block_max4(m, red, lane, w);
+    float s = 0.f;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) tot += red_m[i] == -INFINITY ? 0.f : red_s[i] * expf(red_m[i] - M);
-    const float inv = 1.f / tot;
+    for (int i = 0; i < SM_RV; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            e[i][j] = expf(e[i][j] - M);   // exp(-inf) = 0 for masked / padded keys
+            s += e[i][j];
+        }
+    const float inv = 1.f / block_sum4(s, red, lane, w);
     const float ks = p > 0.f ? 1.f / (1.f - p) : 1.f;
-    // every wave runs the same trip count (n_pad % 1024 may leave the last trip partial) so the
-    // keep-bit ballots below see all 64 lanes
-    for (int64_t cb = 0; cb < n_pad; cb += 1024) {
+#pragma unroll
+    for (int i = 0; i < SM_RV; ++i) {
+        const int64_t cb = (int64_t)i * 1024;
+        if (cb >= n_pad) break;   // block-uniform
         const int64_t c = cb + tid * 4;
         const bool in = c < n_pad;
-        const float4 v = in ? *reinterpret_cast<const float4 *>(srow + c) : make_float4(0.f, 0.f, 0.f, 0.f);
-        const float x[4] = {v.x, v.y, v.z, v.w};
-        float e[4], ed[4];
+        float pv[4], pdv[4];
         bool kp[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            e[j] = (c + j < n_valid) ? expf(x[j] - M) * inv : 0.f;
+            pv[j] = e[i][j] * inv;
             kp[j] = (p > 0.f) ? u2gnn_keep(seed, (uint32_t)row, (uint32_t)(c + j), p) : true;
-            ed[j] = kp[j] ? e[j] * ks : 0.f;
+            pdv[j] = kp[j] ? pv[j] * ks : 0.f;
         }
         if (in) {
-            *reinterpret_cast<float4 *>(prow + c) = make_float4(e[0], e[1], e[2], e[3]);
-            if (write_pd) *reinterpret_cast<float4 *>(pdrow + c) = make_float4(ed[0], ed[1], ed[2], ed[3]);
+            *reinterpret_cast<float4 *>(prow + c) = make_float4(pv[0], pv[1], pv[2], pv[3]);
+            if (write_pd) *reinterpret_cast<float4 *>(pdrow + c) = make_float4(pdv[0], pdv[1], pdv[2], pdv[3]);
         }
         if (krow) {
             // lanes 8k..8k+7 cover columns 32k..32k+31 of this wave's 256: word k from 4 ballots
@@ -286,8 +305,7 @@ __global__ void __launch_bounds__(256) attn_softmax_kernel(const float *S, int64
                 const uint64_t b = __ballot(in && kp[j] && c + j < n_valid);
                 word |= spread4((uint32_t)(b >> (8 * (lane & 7)))) << j;
             }
-            const int64_t wi = (cb + w * 256) / 32 + lane;
-            if (lane < 8 && (cb + w * 256 + 32 * lane) < n_pad) krow[wi] = word;
+            if (lane < 8 && (cb + w * 256 + 32 * lane) < n_pad) krow[(cb + w * 256) / 32 + lane] = word;
         }
     }
 }
@@ -621,8 +639,17 @@ int u2gnn_attn_softmax_fwd(const float *S, int64_t lds, float *P, float *Pd, int
     if (!S || !P || !Pd || (n_pad & 3) || (lds & 3) || (ldp & 3) || n_valid > n_pad || n_valid < 1) return U2GNN_E_ARG;
     if (Pd == P && p > 0.f) return U2GNN_E_ARG;
     if (keep && ((n_pad & 31) || ld_keep < n_pad / 32)) return U2GNN_E_ARG;
-    hipLaunchKernelGGL(attn_softmax_kernel, dim3((unsigned)rows_pad), dim3(256), 0, u2gnn_stream(stream), S, lds, P,
-                       Pd, ldp, rows_valid, n_valid, n_pad, p, seed, keep, ld_keep);
+    if (n_pad > 1024 * SM_RV_MAX) return U2GNN_E_SHAPE;   // rows are held in registers
+    hipStream_t st = u2gnn_stream(stream);
+    if (n_pad <= 8192)
+        hipLaunchKernelGGL(attn_softmax_kernel<8>, dim3((unsigned)rows_pad), dim3(256), 0, st, S, lds, P, Pd, ldp,
+                           rows_valid, n_valid, n_pad, p, seed, keep, ld_keep);
+    else if (n_pad <= 16384)
+        hipLaunchKernelGGL(attn_softmax_kernel<16>, dim3((unsigned)rows_pad), dim3(256), 0, st, S, lds, P, Pd, ldp,
+                           rows_valid, n_valid, n_pad, p, seed, keep, ld_keep);
+    else
+        hipLaunchKernelGGL(attn_softmax_kernel<32>, dim3((unsigned)rows_pad), dim3(256), 0, st, S, lds, P, Pd, ldp,
+                           rows_valid, n_valid, n_pad, p, seed, keep, ld_keep);
     return u2gnn_launch_status();
 }
 

@@ -131,7 +131,7 @@ int u2gnn_colsum(const float *X, int64_t rows, int64_t cols_pad, int64_t ld, int
  * P[i,j] = softmax_j(S[i,j], j < n_valid); Pd = P * keep / (1-p); rows >= rows_valid -> 0.
  * Pd may alias P when p == 0.  keep (optional, n_pad % 32 == 0): the keep decisions as bits,
  * bit j%32 of keep[i*ld_keep + j/32] (0 for j >= n_valid and padded rows), for the ATTN_DS
- * epilogue of the backward. */
+ * epilogue of the backward.  Rows are held in registers: n_pad <= 32768 (else U2GNN_E_SHAPE). */
 int u2gnn_attn_softmax_fwd(const float *S, int64_t lds, float *P, float *Pd, int64_t ldp,
                            int64_t rows_valid, int64_t rows_pad, int64_t n_valid, int64_t n_pad,
                            float p, uint64_t seed, uint32_t *keep, int64_t ld_keep, void *stream);

@@ -132,8 +132,8 @@ def test_gemm_epilogues():
     assert rel_err(C, Pd * acc - P * dl[:, None]) < 1e-5
 
 
-def test_attn_softmax_masking_and_dropout():
-    Np, N = 256, 200
+@pytest.mark.parametrize("Np,N", [(256, 200), (17408, 17000)])
+def test_attn_softmax_masking_and_dropout(Np, N):
     S = _mk(Np, Np, seed=10) * 3
     P = torch.empty(Np, Np, device=DEV)
     K.attn_softmax_fwd(S, Np, P, P, Np, N, Np, N, Np, 0.0, 0)
@@ -152,7 +152,7 @@ def _unpack_bits(kb, cols):
     return bits.reshape(kb.shape[0], -1)[:, :cols]
 
 
-@pytest.mark.parametrize("Np,N", [(1280, 1100), (256, 256), (2048, 1999)])
+@pytest.mark.parametrize("Np,N", [(1280, 1100), (256, 256), (2048, 1999), (9216, 9000)])
 def test_attn_softmax_keep_bits(Np, N):
     """keep bits == the dropout mask on the valid block, 0 on padded rows/columns (n_pad not a
     multiple of the 1024-column trip included)."""

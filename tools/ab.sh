@@ -1,0 +1,20 @@
+#!/usr/bin/env bash
+# A/B kernel variants in ONE GPU session (box-to-box clock differences are ~5-7 %):
+#   bash tools/ab.sh "base exp_oldloop exp_nosb" [GB_ONLY shapes]
+# base = the default library; others = graph-transformer_amd/lib/<name>.so.  Each variant runs
+# the GEMM micro-benchmark (optional shapes) and bench.py twice, interleaved.
+set -o pipefail
+VARS=$1
+ONLY=${2:-}
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$R"; mkdir -p gpurun_out
+for rep in 1 2; do
+  for v in $VARS; do
+    if [ "$v" = base ]; then L=""; else L="$R/graph-transformer_amd/lib/$v.so"; fi
+    if [ -n "$ONLY" ] && [ $rep = 1 ]; then
+      U2GNN_HIP_LIB=$L GB_ONLY="$ONLY" timeout -k 10 200 python tools/gemm_bench.py bf16x3 2>/dev/null | sed "s/^/$v /" || exit 1
+    fi
+    U2GNN_HIP_LIB=$L timeout -k 10 200 python bench.py --steps 30 --warmup 5 --cpu-baseline 0 --no-roofline > gpurun_out/ab_$v.json 2>/dev/null || exit 1
+    python -c "import json;d=json.load(open('gpurun_out/ab_$v.json'));print('$v', 'step_ms', d['ms_per_step'], d['final_loss'])"
+  done
+done

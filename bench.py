@@ -49,6 +49,8 @@ def parse():
     ap.add_argument("--cpu-baseline", type=int, default=1, help="1 = time the CPU oracle on rank 0 at N=1")
     ap.add_argument("--cpu-steps", type=int, default=1)
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--attention", default="nodes", choices=["nodes", "neighbors"],
+                    help="nodes = the fork's semantics (the headline metric); neighbors = paper semantics")
     ap.add_argument("--workload", default="c4", choices=["c4", "c5"],
                     help="c4 = U2GNN-Sup COLLAB (the headline metric); c5 = U2GNN-UnSup REDDIT-M5K (HBM-bound)")
     return ap.parse_args()
@@ -212,7 +214,8 @@ def main():
     torch.manual_seed(123)
     model = TransformerU2GNN(feature_dim_size=d, ff_hidden_size=args.ff_hidden_size, num_classes=C,
                              num_self_att_layers=args.num_timesteps, dropout=0.5,
-                             num_U2GNN_layers=args.num_hidden_layers, precision=args.precision)
+                             num_U2GNN_layers=args.num_hidden_layers, precision=args.precision,
+                             attention=args.attention)
     sd0 = {k: v.clone() for k, v in model.state_dict().items()}
     model = model.to(dev).train()
     trainer = SupTrainer(model, lr=args.lr, max_norm=0.5, seed=123 + rank)
@@ -289,7 +292,7 @@ def main():
            "config": {"workload": "U2GNN-Sup COLLAB (C4): batch_size=64/GPU, num_neighbors=16, num_timesteps=4, "
                                   "ff_hidden_size=1024, num_hidden_layers=1, d=367",
                       "global_batch": args.batch_size * world, "mean_nodes_per_batch": round(mean_N, 1),
-                      "parallelism": f"dp{world}", "precision": args.precision},
+                      "parallelism": f"dp{world}", "precision": args.precision, "attention": args.attention},
            "final_loss": round(loss, 5), "host_issue_ms_per_step": round(1e3 * t_issue / args.steps, 3),
            "roofline": roof, "cpu_baseline": None}
     if rank == 0 and world == 1 and args.cpu_baseline:

@@ -17,6 +17,8 @@
 
 #include <cmath>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "u2gnn_hip.h"
@@ -29,6 +31,7 @@ struct Dims {
     int64_t N, d, ff, Np, dp, ffp;
     int prec;
     bool deep_wgrad;
+    int window;   // 0: attention over all N rows; W: within windows of W rows (N % W == 0)
 };
 
 Dims make_dims(const u2gnn_layer_dims *a) {
@@ -41,6 +44,7 @@ Dims make_dims(const u2gnn_layer_dims *a) {
     D.ffp = rup(a->ff, 64);
     D.prec = a->precision;
     D.deep_wgrad = (a->flags & U2GNN_LAYER_DEEP_WGRAD) != 0;
+    D.window = a->window;
     return D;
 }
 
@@ -61,23 +65,43 @@ struct Arena {
     bool plan() const { return base == nullptr; }
 };
 
-#define U2GNN_TRY(x)                     \
-    do {                                 \
-        const int rc_ = (x);             \
-        if (rc_ != U2GNN_OK) return rc_; \
+// U2GNN_DEBUG=1 in the environment names the failing call on stderr
+bool debug_on() {
+    static const int on = [] {
+        const char *e = std::getenv("U2GNN_DEBUG");
+        return e && e[0] == '1' ? 1 : 0;
+    }();
+    return on != 0;
+}
+
+#define U2GNN_TRY(x)                                                                                \
+    do {                                                                                            \
+        const int rc_ = (x);                                                                        \
+        if (rc_ != U2GNN_OK) {                                                                      \
+            if (debug_on()) std::fprintf(stderr, "u2gnn: %s:%d: %s -> %d\n", __FILE__, __LINE__, #x, rc_); \
+            return rc_;                                                                             \
+        }                                                                                           \
     } while (0)
 
 struct Ctx {   // tensors saved by the forward for the backward
     float *QKV, *P, *Pd, *O, *Z1, *X1, *mean1, *rstd1, *Hd, *Z2, *mean2, *rstd2;
     uint32_t *keep;
+    float *Psave;   // window mode: [N/W, W, W] probabilities
 };
 
 Ctx carve_ctx(Arena &A, const Dims &D, bool drop) {
     Ctx c;
     c.QKV = A.take<float>(D.Np * 3 * D.dp);
-    c.P = A.take<float>(D.Np * D.Np);
-    c.Pd = drop ? A.take<float>(D.Np * D.Np) : c.P;
-    c.keep = drop ? A.take<uint32_t>(D.Np * (D.Np / 32)) : nullptr;
+    if (D.window) {
+        c.P = c.Pd = nullptr;
+        c.keep = nullptr;
+        c.Psave = A.take<float>(D.N * D.window);
+    } else {
+        c.Psave = nullptr;
+        c.P = A.take<float>(D.Np * D.Np);
+        c.Pd = drop ? A.take<float>(D.Np * D.Np) : c.P;
+        c.keep = drop ? A.take<uint32_t>(D.Np * (D.Np / 32)) : nullptr;
+    }
     c.O = A.take<float>(D.Np * D.dp);
     c.Z1 = A.take<float>(D.Np * D.dp);
     c.X1 = A.take<float>(D.Np * D.dp);
@@ -207,17 +231,24 @@ int layer_fwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
         U2GNN_TRY(g.run(st, plan));
     }
     const float *Q = c.QKV, *Kt = c.QKV + dp, *V = c.QKV + 2 * dp;
-    // a3.2 scores, softmax + dropout, P.V
-    float *S = W.take<float>(Np * Np);
-    {
-        G g(Q, Kt, S, Np, Np, dp, 3 * dp, 3 * dp, Np, prec);
-        g.tb().tile((prec != U2GNN_PREC_F32 && Np % 256 == 0) ? 256 : 0);
-        U2GNN_TRY(g.run(st, plan));
+    if (D.window) {
+        // paper semantics: attention inside each node's window of W neighbour tokens
+        if (!plan)
+            U2GNN_TRY(u2gnn_window_attn_fwd(c.QKV, 3 * dp, D.window, (int32_t)dp, c.O, dp, c.Psave, pd, s->attn,
+                                            N / D.window, Np, st));
+    } else {
+        // a3.2 scores, softmax + dropout, P.V
+        float *S = W.take<float>(Np * Np);
+        {
+            G g(Q, Kt, S, Np, Np, dp, 3 * dp, 3 * dp, Np, prec);
+            g.tb().tile((prec != U2GNN_PREC_F32 && Np % 256 == 0) ? 256 : 0);
+            U2GNN_TRY(g.run(st, plan));
+        }
+        if (!plan)
+            U2GNN_TRY(u2gnn_attn_softmax_fwd(S, Np, c.P, c.Pd, Np, N, Np, N, Np, pd, s->attn, c.keep, Np / 32, st));
+        U2GNN_TRY(gemm_split(W, D, c.Pd, V, c.O, Np, dp, Np, Np, 3 * dp, dp, false, 1.f, false, nullptr, nullptr,
+                             false, st));
     }
-    if (!plan)
-        U2GNN_TRY(u2gnn_attn_softmax_fwd(S, Np, c.P, c.Pd, Np, N, Np, N, Np, pd, s->attn, c.keep, Np / 32, st));
-    U2GNN_TRY(gemm_split(W, D, c.Pd, V, c.O, Np, dp, Np, Np, 3 * dp, dp, false, 1.f, false, nullptr, nullptr, false,
-                         st));
     // a3.3 out-projection + dropout1 + residual, LayerNorm1
     {
         G g(c.O, w->W_o, c.Z1, Np, dp, dp, dp, dp, dp, prec);
@@ -240,6 +271,9 @@ int layer_fwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
         U2GNN_TRY(g.run(st, plan));
     }
     if (!plan) U2GNN_TRY(u2gnn_layernorm_fwd(c.Z2, dp, w->n2_w, w->n2_b, X2, dp, c.mean2, c.rstd2, N, Np, d, dp, 1e-5f, st));
+    if ((W.overflow || CA.overflow) && debug_on())
+        std::fprintf(stderr, "u2gnn: layer_fwd arena overflow (ws %lld/%lld, ctx %lld/%lld)\n", (long long)W.used,
+                     (long long)W.cap, (long long)CA.used, (long long)CA.cap);
     return (W.overflow || CA.overflow) ? U2GNN_E_ARG : U2GNN_OK;
 }
 
@@ -296,27 +330,36 @@ int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
     U2GNN_TRY(wgrad(W, D, dA, dp, c.O, dp, dp, dp, g->out_w, d, blk_d, blk_d, so));   // side (forked above)
     // attention core
     const float *Q = c.QKV, *Kt = c.QKV + dp, *V = c.QKV + 2 * dp;
-    float *delta = W.take<float>(Np);
-    if (!plan) U2GNN_TRY(u2gnn_rowdot(dO, dp, c.O, dp, delta, Np, dp, st));
-    float *dS = W.take<float>(Np * Np);
-    {
-        G gg(dO, V, dS, Np, Np, dp, dp, 3 * dp, Np, prec);
-        gg.tb().epi(U2GNN_EPI_ATTN_DS);
-        gg.a.aux0 = c.P, gg.a.rowvec = delta, gg.a.ld_aux = Np, gg.a.p_drop = pd;
-        if (c.keep) {
-            gg.a.keep = c.keep, gg.a.ld_keep = Np / 32;
-        } else {
-            gg.a.aux1 = c.Pd;
+    const float q_scale = (float)(1.0 / std::sqrt((double)d));
+    float *dQKV;
+    if (D.window) {
+        dQKV = W.take<float>(Np * 3 * dp);
+        if (!plan)
+            U2GNN_TRY(u2gnn_window_attn_bwd(c.QKV, 3 * dp, D.window, (int32_t)dp, dO, dp, c.Psave, pd, s->attn,
+                                            q_scale, dQKV, 3 * dp, N / D.window, Np, st));
+    } else {
+        float *delta = W.take<float>(Np);
+        if (!plan) U2GNN_TRY(u2gnn_rowdot(dO, dp, c.O, dp, delta, Np, dp, st));
+        float *dS = W.take<float>(Np * Np);
+        {
+            G gg(dO, V, dS, Np, Np, dp, dp, 3 * dp, Np, prec);
+            gg.tb().epi(U2GNN_EPI_ATTN_DS);
+            gg.a.aux0 = c.P, gg.a.rowvec = delta, gg.a.ld_aux = Np, gg.a.p_drop = pd;
+            if (c.keep) {
+                gg.a.keep = c.keep, gg.a.ld_keep = Np / 32;
+            } else {
+                gg.a.aux1 = c.Pd;
+            }
+            U2GNN_TRY(gg.run(st, plan));
         }
-        U2GNN_TRY(gg.run(st, plan));
+        dQKV = W.take<float>(Np * 3 * dp);
+        U2GNN_TRY(gemm_split(W, D, c.Pd, dO, dQKV + 2 * dp, Np, dp, Np, Np, dp, 3 * dp, true, 1.f, false, nullptr,
+                             nullptr, false, st));
+        U2GNN_TRY(gemm_split(W, D, dS, Kt, dQKV, Np, dp, Np, Np, 3 * dp, 3 * dp, false, q_scale, false, nullptr, nullptr,
+                             false, st));
+        U2GNN_TRY(gemm_split(W, D, dS, Q, dQKV + dp, Np, dp, Np, Np, 3 * dp, 3 * dp, true, 1.f, false, nullptr, nullptr,
+                             false, st));
     }
-    float *dQKV = W.take<float>(Np * 3 * dp);
-    U2GNN_TRY(gemm_split(W, D, c.Pd, dO, dQKV + 2 * dp, Np, dp, Np, Np, dp, 3 * dp, true, 1.f, false, nullptr,
-                         nullptr, false, st));
-    U2GNN_TRY(gemm_split(W, D, dS, Kt, dQKV, Np, dp, Np, Np, 3 * dp, 3 * dp, false, (float)(1.0 / std::sqrt((double)d)), false,
-                         nullptr, nullptr, false, st));
-    U2GNN_TRY(gemm_split(W, D, dS, Q, dQKV + dp, Np, dp, Np, Np, 3 * dp, 3 * dp, true, 1.f, false, nullptr, nullptr,
-                         false, st));
     // in-projection
     U2GNN_TRY(gemm_split(W, D, dQKV, w->W_in, dX, Np, dp, 3 * dp, 3 * dp, dp, dp, false, 1.f, true, nullptr, nullptr,
                          false, st));
@@ -328,7 +371,8 @@ int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
 
 bool dims_ok(const u2gnn_layer_dims *a) {
     return a && a->N >= 1 && a->d >= 1 && a->ff >= 1 && rup(a->d, 64) <= 1024 &&
-           (a->precision == U2GNN_PREC_F32 || a->precision == U2GNN_PREC_BF16X3 || a->precision == U2GNN_PREC_BF16);
+           (a->precision == U2GNN_PREC_F32 || a->precision == U2GNN_PREC_BF16X3 || a->precision == U2GNN_PREC_BF16) &&
+           a->window >= 0 && a->window <= 32 && (a->window == 0 || a->N % a->window == 0);
 }
 
 }  // namespace
@@ -358,18 +402,20 @@ int u2gnn_layer_sizes(const u2gnn_layer_dims *dims, float p_drop, int64_t *ctx_b
 int u2gnn_layer_fwd(const u2gnn_layer_dims *dims, const u2gnn_layer_params *w, const u2gnn_layer_seeds *s,
                     const float *X, float *X2, void *ctx, int64_t ctx_bytes, void *ws, int64_t ws_bytes,
                     void *stream) {
-    if (!dims_ok(dims) || !w || !s || !X || !X2 || !ws) return U2GNN_E_ARG;
+    if (!dims_ok(dims) || !w || !s || !X || !X2 || (!ws && ws_bytes > 0)) return U2GNN_E_ARG;
     const Dims D = make_dims(dims);
-    Arena C(ctx, ctx_bytes), W(ws, ws_bytes);
+    static char empty_ws alignas(256)[256];   // a null base would mean "plan only"
+    Arena C(ctx, ctx_bytes), W(ws ? ws : empty_ws, ws ? ws_bytes : 0);
     return layer_fwd(D, w, s, X, X2, C, W, ctx != nullptr, reinterpret_cast<hipStream_t>(stream));
 }
 
 int u2gnn_layer_bwd(const u2gnn_layer_dims *dims, const u2gnn_layer_params *w, const u2gnn_layer_seeds *s,
                     const float *X, const void *ctx, int64_t ctx_bytes, const float *dX2, float *dX,
                     const u2gnn_layer_grads *g, void *ws, int64_t ws_bytes, void *stream, void *side_stream) {
-    if (!dims_ok(dims) || !w || !s || !X || !ctx || !dX2 || !dX || !g || !ws) return U2GNN_E_ARG;
+    if (!dims_ok(dims) || !w || !s || !X || !ctx || !dX2 || !dX || !g || (!ws && ws_bytes > 0)) return U2GNN_E_ARG;
     const Dims D = make_dims(dims);
-    Arena C(const_cast<void *>(ctx), ctx_bytes), W(ws, ws_bytes);
+    static char empty_ws alignas(256)[256];
+    Arena C(const_cast<void *>(ctx), ctx_bytes), W(ws ? ws : empty_ws, ws ? ws_bytes : 0);
     return layer_bwd(D, w, s, X, C, dX2, dX, g, W, reinterpret_cast<hipStream_t>(stream),
                      reinterpret_cast<hipStream_t>(side_stream));
 }

@@ -7,8 +7,10 @@ are only parameter containers here: the computation runs on the gfx950 kernels o
 libu2gnn_hip.so through ``u2gnn_hip.core.SupCore`` (no CPU fallback — the forward raises if
 the HIP library or a GPU is missing).
 
-Extra keyword (not in the reference): ``precision`` = "fp32" (exact fp32 matrix cores,
-the parity path).
+Extra keywords (not in the reference): ``precision`` = "fp32" (exact fp32 matrix cores,
+the parity path); ``attention`` = "nodes" (the fork's semantics: the encoder's sequence axis is
+the node axis, pytorch_U2GNN_Sup.py:35) or "neighbors" (the paper / TF semantics: each node
+attends over its own k+1 sampled neighbours, U2GNN_tf/model_U2GNN_Sup_multi.py:14-45).
 """
 import torch
 import torch.nn as nn
@@ -36,7 +38,7 @@ class _SupFunction(torch.autograd.Function):
 class TransformerU2GNN(nn.Module):
 
     def __init__(self, feature_dim_size, ff_hidden_size, num_classes,
-                 num_self_att_layers, dropout, num_U2GNN_layers, precision="fp32"):
+                 num_self_att_layers, dropout, num_U2GNN_layers, precision="fp32", attention="nodes"):
         super(TransformerU2GNN, self).__init__()
         self.feature_dim_size = feature_dim_size
         self.ff_hidden_size = ff_hidden_size
@@ -45,6 +47,9 @@ class TransformerU2GNN(nn.Module):
         self.num_U2GNN_layers = num_U2GNN_layers
         self.dropout_p = dropout
         self.precision = precision
+        if attention not in ("nodes", "neighbors"):
+            raise ValueError(f"attention must be 'nodes' or 'neighbors', got {attention!r}")
+        self.attention = attention
         # parameter containers built in the reference's order (identical init under a seed)
         self.u2gnn_layers = torch.nn.ModuleList()
         for _ in range(self.num_U2GNN_layers):

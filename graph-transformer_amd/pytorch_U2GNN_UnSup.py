@@ -62,12 +62,15 @@ class TransformerU2GNN(nn.Module):
 
     def __init__(self, vocab_size, feature_dim_size, ff_hidden_size, sampled_num,
                  num_self_att_layers, num_U2GNN_layers, dropout, device, sampler_type='default',
-                 loss_type='default', adj_mat=None, single_layer_only=True, precision="fp32"):
+                 loss_type='default', adj_mat=None, single_layer_only=True, precision="fp32", attention="nodes"):
         super(TransformerU2GNN, self).__init__()
         if sampler_type != 'default' or loss_type != 'default':
             raise NotImplementedError("only sampler_type='default', loss_type='default' (graph-level U2GNN) "
                                       "are on the MI355X path; neighbour/contrastive/gae are node-level research")
         self.feature_dim_size = feature_dim_size
+        if attention not in ("nodes", "neighbors"):
+            raise ValueError(f"attention must be 'nodes' or 'neighbors', got {attention!r}")
+        self.attention = attention
         self.self_attn = nn.MultiheadAttention(self.feature_dim_size, 1, dropout=dropout)
         self.ff_hidden_size = ff_hidden_size
         self.num_self_att_layers = num_self_att_layers

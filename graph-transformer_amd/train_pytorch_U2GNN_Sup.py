@@ -10,7 +10,7 @@ Execution: the default trainer is the fused HIP step (u2gnn_hip.train.SupTrainer
 backward into a flat grad buffer, device-side clip + Adam, no per-step host sync except the loss
 readout the reference also does).  ``--autograd`` runs the reference's exact loop instead
 (model(), cross_entropy, loss.backward(), clip_grad_norm_, torch Adam, StepLR) — on the same kernels.
-Extra flags: --precision, --autograd, --max_steps (0 = full epochs).
+Extra flags: --precision, --attention, --autograd, --max_steps (0 = full epochs).
 """
 import math
 import os
@@ -52,7 +52,11 @@ parser.add_argument("--num_timesteps", default=1, type=int, help="Timestep T ~ N
 parser.add_argument("--ff_hidden_size", default=1024, type=int, help="The hidden size for the feedforward layer")
 parser.add_argument("--num_neighbors", default=4, type=int, help="")
 parser.add_argument('--fold_idx', type=int, default=1, help='The fold index. 0-9.')
-parser.add_argument("--precision", default="fp32", choices=["fp32"], help="matrix-core precision (MI355X)")
+parser.add_argument("--precision", default="fp32", choices=["fp32", "bf16x3", "bf16"],
+                    help="matrix-core precision (MI355X): fp32 exact, bf16x3 split-bf16 (~fp32), bf16")
+parser.add_argument("--attention", default="nodes", choices=["nodes", "neighbors"],
+                    help="nodes = the fork's attention over all nodes of the batch; neighbors = the paper's "
+                         "attention over each node's k+1 sampled neighbours")
 parser.add_argument("--autograd", action="store_true", help="reference loop: autograd + torch Adam/StepLR")
 parser.add_argument("--max_steps", default=0, type=int, help="stop after this many train steps (0 = no limit)")
 args = parser.parse_args()
@@ -74,7 +78,8 @@ print("Loading data... finished!")
 
 model = TransformerU2GNN(feature_dim_size=feature_dim_size, ff_hidden_size=args.ff_hidden_size,
                          num_classes=num_classes, dropout=args.dropout, num_self_att_layers=args.num_timesteps,
-                         num_U2GNN_layers=args.num_hidden_layers, precision=args.precision).to(device)
+                         num_U2GNN_layers=args.num_hidden_layers, precision=args.precision,
+                         attention=args.attention).to(device)
 num_batches_per_epoch = int((len(train_graphs) - 1) / args.batch_size) + 1
 
 

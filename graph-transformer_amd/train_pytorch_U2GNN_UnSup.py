@@ -9,7 +9,7 @@ LogisticRegression(liblinear, tol=1e-3) (:164-188), stdout line (:207) and acc f
 (<run_folder>/../runs_pytorch_U2GNN_UnSup/<model_name>/checkpoints/model_acc.txt).
 
 The fork's file cannot run as shipped; this runs its working semantics
-(pytorch_U2GNN_UnSup.TransformerU2GNN of this package).  Extra flags: --precision, --max_steps,
+(pytorch_U2GNN_UnSup.TransformerU2GNN of this package).  Extra flags: --precision, --attention, --max_steps,
 --eval_every (0 = evaluate every epoch like the reference).
 """
 import os
@@ -52,7 +52,11 @@ parser.add_argument("--num_timesteps", default=1, type=int, help="Timestep T ~ N
 parser.add_argument("--ff_hidden_size", default=1024, type=int, help="The hidden size for the feedforward layer")
 parser.add_argument("--num_neighbors", default=4, type=int, help="")
 parser.add_argument('--fold_idx', type=int, default=1, help='The fold index. 0-9.')
-parser.add_argument("--precision", default="fp32", choices=["fp32"], help="matrix-core precision (MI355X)")
+parser.add_argument("--precision", default="fp32", choices=["fp32", "bf16x3", "bf16"],
+                    help="matrix-core precision (MI355X): fp32 exact, bf16x3 split-bf16 (~fp32), bf16")
+parser.add_argument("--attention", default="nodes", choices=["nodes", "neighbors"],
+                    help="nodes = the fork's attention over all nodes of the batch; neighbors = the paper's "
+                         "attention over each node's k+1 sampled neighbours")
 parser.add_argument("--max_steps", default=0, type=int, help="stop after this many train steps (0 = no limit)")
 args = parser.parse_args()
 
@@ -74,7 +78,8 @@ print("Loading data... finished!")
 model = TransformerU2GNN(feature_dim_size=feature_dim_size, ff_hidden_size=args.ff_hidden_size,
                          dropout=args.dropout, num_self_att_layers=args.num_timesteps,
                          vocab_size=vocab_size, sampled_num=args.sampled_num,
-                         num_U2GNN_layers=args.num_hidden_layers, device=device, precision=args.precision).to(device)
+                         num_U2GNN_layers=args.num_hidden_layers, device=device, precision=args.precision,
+                         attention=args.attention).to(device)
 trainer = UnSupTrainer(model, lr=args.learning_rate, max_norm=0.5)
 num_batches_per_epoch = int((len(graphs) - 1) / args.batch_size) + 1
 sched_steps = 0

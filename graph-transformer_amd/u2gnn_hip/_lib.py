@@ -59,7 +59,8 @@ class PackDesc(ctypes.Structure):
 
 
 class LayerDims(ctypes.Structure):
-    _fields_ = [("N", c_int64), ("d", c_int64), ("ff", c_int64), ("precision", c_int32), ("flags", c_int32)]
+    _fields_ = [("N", c_int64), ("d", c_int64), ("ff", c_int64), ("precision", c_int32), ("flags", c_int32),
+                ("window", c_int32), ("reserved", c_int32)]
 
 
 _PKEYS = ("in_w", "in_b", "out_w", "out_b", "l1_w", "l1_b", "l2_w", "l2_b", "n1_w", "n1_b", "n2_w", "n2_b")
@@ -88,6 +89,8 @@ _HIP_SIGS = {
     "u2gnn_gather_rows": ([VP, I64, I64, VP, I64, VP, I64, I64, I64, I64, I64, VP, VP], c_int32),
     "u2gnn_scatter_add_rows": ([VP, I64, VP, I64, VP, I64, I64, I64, VP], c_int32),
     "u2gnn_gemm": ([POINTER(GemmArgs), VP], c_int32),
+    "u2gnn_window_attn_fwd": ([VP, I64, I32, I32, VP, I64, VP, F32, c_uint64, I64, I64, VP], c_int32),
+    "u2gnn_window_attn_bwd": ([VP, I64, I32, I32, VP, I64, VP, F32, c_uint64, F32, VP, I64, I64, I64, VP], c_int32),
     "u2gnn_layer_sizes": ([POINTER(LayerDims), F32, POINTER(c_int64), POINTER(c_int64), POINTER(c_int64)], c_int32),
     "u2gnn_layer_fwd": ([POINTER(LayerDims), POINTER(LayerParamsC), POINTER(LayerSeeds), VP, VP, VP, I64, VP, I64,
                          VP], c_int32),

@@ -73,8 +73,12 @@ class EncoderStack:
     """L U2GNN layers x T post-LN encoder layers on slot-0 rows, with the re-gather between
     U2GNN layers (pytorch_U2GNN_Sup.py:33-39; pytorch_U2GNN_UnSup.py:55-64)."""
 
-    def __init__(self, u2gnn_layers, d: int, ff: int, T: int, L: int, prec: str = "fp32", p_enc: float = 0.5):
+    def __init__(self, u2gnn_layers, d: int, ff: int, T: int, L: int, prec: str = "fp32", p_enc: float = 0.5,
+                 attention: str = "nodes"):
         self.layers, self.d, self.ff, self.T, self.L, self.prec, self.p_enc = u2gnn_layers, d, ff, T, L, prec, p_enc
+        if attention not in ("nodes", "neighbors"):
+            raise ValueError(f"attention must be 'nodes' or 'neighbors', got {attention!r}")
+        self.attention = attention
         self.packed = None
 
     def layer_params(self, l, t) -> LayerParams:
@@ -91,6 +95,8 @@ class EncoderStack:
 
     def forward(self, b: "DeviceBatch", train: bool, need_ctx: bool, seed: int):
         """Returns (outs, ctx): outs[l] = padded [Np, dp] slot-0 output of U2GNN layer l."""
+        if self.attention == "neighbors":
+            return self._forward_neighbors(b, train, need_ctx, seed)
         dev = b.X_concat.device
         d, dp = self.d, rup(self.d, 64)
         dims = Dims(b.N, d, self.ff)
@@ -118,9 +124,68 @@ class EncoderStack:
                 X = Xn
         return outs, {"dims": dims, "layers": lctxs, "batch": b}
 
+    # ---- paper semantics (U2GNN_tf/model_U2GNN_Sup_multi.py:14-45): every
+    # node attends over its own k+1 gathered neighbour tokens.  Token rows are node-major
+    # (row n*W + s = slot s of node n, W = k+1); each layer runs on all N*W tokens through the native
+    # executor's window mode; slot 0 of the last layer is the node's output.
+    def _forward_neighbors(self, b: "DeviceBatch", train: bool, need_ctx: bool, seed: int):
+        if not native.enabled():
+            raise NotImplementedError("neighbour attention runs on the native layer executor (U2GNN_NATIVE_LAYER=1)")
+        dev = b.X_concat.device
+        d, dp = self.d, rup(self.d, 64)
+        if not b.input_x.is_contiguous():
+            raise ValueError("input_x must be contiguous [N, k+1]")
+        W = b.input_x.shape[1]
+        dims, tdims = Dims(b.N, d, self.ff), Dims(b.N * W, d, self.ff)
+        Np, R, Rp = dims.Np, b.N * W, tdims.Np
+        self._pack(dev)
+        slot0 = torch.arange(b.N, device=dev, dtype=torch.int64) * W
+        X = torch.empty(Rp, dp, device=dev, dtype=torch.float32)
+        K.gather_rows(b.X_concat, b.input_x, 1, X, R, Rp, d, dp)
+        outs, lctxs = [], []
+        for l in range(self.L):
+            lctx = []
+            for t in range(self.T):
+                seeds = {s: site_seed(seed, l, t, s) for s in (SITE_ATTN, SITE_DROP1, SITE_DROPFF, SITE_DROP2)}
+                X, c = native.layer_forward(X, self.packed[l][t], self.layer_params(l, t), tdims, train, seeds,
+                                            need_ctx, self.prec, self.p_enc, deep_wgrad=engine_deep_wgrad(), window=W)
+                lctx.append(c)
+            out = torch.empty(Np, dp, device=dev, dtype=torch.float32)
+            K.gather_rows(X, slot0, 1, out, b.N, Np, d, dp)
+            outs.append(out)
+            lctxs.append(lctx)
+            if l + 1 < self.L:
+                X = torch.empty(Rp, dp, device=dev, dtype=torch.float32)
+                K.gather_rows(out, b.input_x, 1, X, R, Rp, d, dp)
+        return outs, {"dims": dims, "tdims": tdims, "window": W, "slot0": slot0, "layers": lctxs, "batch": b}
+
+    def _backward_neighbors(self, ctx, ext_grad, grads: dict, prefix: str):
+        b = ctx["batch"]
+        tdims, W, slot0 = ctx["tdims"], ctx["window"], ctx["slot0"]
+        d, dp = self.d, rup(self.d, 64)
+        R = b.N * W
+        off = OffPath(b.input_x.device)
+        dnext = None
+        for l in reversed(range(self.L)):
+            dOut = ext_grad(l)                                   # [Np, dp] node rows
+            if dnext is not None:                                # re-gather of the next U2GNN layer
+                K.scatter_add_rows(dnext, b.input_x, 1, dOut, R, d)
+            dX = torch.zeros(tdims.Np, dp, device=dOut.device, dtype=torch.float32)
+            K.scatter_add_rows(dOut, slot0, 1, dX, b.N, d)       # slot 0 of every node
+            for t in reversed(range(self.T)):
+                pre = f"{prefix}.{l}.layers.{t}."
+                g = LayerParams(*[grads[pre + k] for k in LAYER_KEYS])
+                dX = native.layer_backward(dX, ctx["layers"][l][t], self.packed[l][t], self.layer_params(l, t), g,
+                                           tdims, self.prec, side=off.side, deep_wgrad=engine_deep_wgrad())
+            dnext = dX
+        off.join()
+        return dnext
+
     def backward(self, ctx, ext_grad, grads: dict, prefix: str = "u2gnn_layers"):
         """ext_grad(l) -> fresh padded gradient of outs[l] from outside the stack (head / loss).
         Writes encoder parameter gradients into grads[<reference key>]."""
+        if "window" in ctx:
+            return self._backward_neighbors(ctx, ext_grad, grads, prefix)
         b = ctx["batch"]
         dims = ctx["dims"]
         dnext = None
@@ -157,7 +222,8 @@ class SupCore:
         self.T = module.num_self_att_layers
         self.p_head = module.dropout_p        # args.dropout, pytorch_U2GNN_Sup.py:28
         # encoder dropout is hard-coded to 0.5 (pytorch_U2GNN_Sup.py:20)
-        self.stack = EncoderStack(module.u2gnn_layers, self.d, self.ff, self.T, self.L, precision, 0.5)
+        self.stack = EncoderStack(module.u2gnn_layers, self.d, self.ff, self.T, self.L, precision, 0.5,
+                                  getattr(module, "attention", "nodes"))
 
     def forward(self, b: DeviceBatch, train: bool, need_ctx: bool, seed: int):
         dev = b.X_concat.device

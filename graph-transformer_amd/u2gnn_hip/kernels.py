@@ -148,6 +148,21 @@ def attn_softmax_fwd(S, lds, P, Pd, ldp, rows_valid, rows_pad, n_valid, n_pad, p
           "u2gnn_attn_softmax_fwd")
 
 
+def window_attn_fwd(QKV, W, dp, O, Psave, p, seed, n_nodes, rows_pad):
+    """Per-node attention over windows of W token rows (paper semantics); QKV [rows_pad, >=3dp]."""
+    _dev(QKV, O, Psave)
+    check(hip_lib().u2gnn_window_attn_fwd(_p(QKV), QKV.stride(0), int(W), int(dp), _p(O), O.stride(0), _p(Psave),
+                                          float(p), int(seed), int(n_nodes), int(rows_pad), _s()),
+          "u2gnn_window_attn_fwd")
+
+
+def window_attn_bwd(QKV, W, dp, dO, Psave, p, seed, q_scale, dQKV, n_nodes, rows_pad):
+    _dev(QKV, dO, Psave, dQKV)
+    check(hip_lib().u2gnn_window_attn_bwd(_p(QKV), QKV.stride(0), int(W), int(dp), _p(dO), dO.stride(0), _p(Psave),
+                                          float(p), int(seed), float(q_scale), _p(dQKV), dQKV.stride(0),
+                                          int(n_nodes), int(rows_pad), _s()), "u2gnn_window_attn_bwd")
+
+
 def rowdot(A, lda, B, ldb, out, rows, cols):
     _dev(A, B, out)
     check(hip_lib().u2gnn_rowdot(_p(A), int(lda), _p(B), int(ldb), _p(out), int(rows), int(cols), _s()),

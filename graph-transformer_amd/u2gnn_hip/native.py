@@ -38,16 +38,16 @@ def set_enabled(on: bool) -> bool:
     return prev
 
 
-def _dims(N: int, d: int, ff: int, prec: str, deep_wgrad: bool) -> LayerDims:
-    return LayerDims(int(N), int(d), int(ff), PREC[prec], _lib.LAYER_DEEP_WGRAD if deep_wgrad else 0)
+def _dims(N: int, d: int, ff: int, prec: str, deep_wgrad: bool, window: int = 0) -> LayerDims:
+    return LayerDims(int(N), int(d), int(ff), PREC[prec], _lib.LAYER_DEEP_WGRAD if deep_wgrad else 0, int(window), 0)
 
 
-def sizes(N: int, d: int, ff: int, prec: str, p_drop: float, deep_wgrad: bool = True):
-    key = (N, d, ff, prec, p_drop > 0, deep_wgrad)
+def sizes(N: int, d: int, ff: int, prec: str, p_drop: float, deep_wgrad: bool = True, window: int = 0):
+    key = (N, d, ff, prec, p_drop > 0, deep_wgrad, window)
     r = _SIZES.get(key)
     if r is None:
         c, f, b = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
-        dims = _dims(N, d, ff, prec, deep_wgrad)
+        dims = _dims(N, d, ff, prec, deep_wgrad, window)
         check(hip_lib().u2gnn_layer_sizes(ctypes.byref(dims), float(p_drop), ctypes.byref(c), ctypes.byref(f),
                                           ctypes.byref(b)), "u2gnn_layer_sizes")
         r = _SIZES[key] = (c.value, f.value, b.value)
@@ -68,7 +68,7 @@ def _seeds(p_drop: float, seeds: Dict[int, int]) -> LayerSeeds:
 
 class NativeCtx:
     """What the backward needs from one layer's forward."""
-    __slots__ = ("X", "buf", "p_drop", "seeds")
+    __slots__ = ("X", "buf", "p_drop", "seeds", "window")
 
 
 def _stream(s=None):
@@ -76,31 +76,34 @@ def _stream(s=None):
 
 
 def layer_forward(X: torch.Tensor, packed, p, dims, train: bool, seeds: Dict[int, int], need_ctx: bool,
-                  prec: str, p_enc: float, deep_wgrad: bool = True):
+                  prec: str, p_enc: float, deep_wgrad: bool = True, window: int = 0):
+    """window = 0: attention over all dims.N rows; W: within each node's window of W token rows
+    (dims.N = nodes * W)."""
     pd = p_enc if train else 0.0
-    cb, fb, _ = sizes(dims.N, dims.d, dims.ff, prec, pd, deep_wgrad)
+    cb, fb, _ = sizes(dims.N, dims.d, dims.ff, prec, pd, deep_wgrad, window)
     dev = X.device
     X2 = torch.empty(dims.Np, dims.dp, device=dev, dtype=torch.float32)
     buf = torch.empty(cb, device=dev, dtype=torch.uint8) if need_ctx else None
-    ws = torch.empty(fb + (0 if need_ctx else cb), device=dev, dtype=torch.uint8)
-    dd, pp, ss = _dims(dims.N, dims.d, dims.ff, prec, deep_wgrad), _params(packed, p), _seeds(pd, seeds)
+    ws = torch.empty(max(256, fb + (0 if need_ctx else cb)), device=dev, dtype=torch.uint8)
+    dd, pp, ss = _dims(dims.N, dims.d, dims.ff, prec, deep_wgrad, window), _params(packed, p), _seeds(pd, seeds)
     check(hip_lib().u2gnn_layer_fwd(ctypes.byref(dd), ctypes.byref(pp), ctypes.byref(ss), X.data_ptr(),
                                     X2.data_ptr(), buf.data_ptr() if buf is not None else None, cb,
                                     ws.data_ptr(), ws.numel(), _stream()), "u2gnn_layer_fwd")
     ctx = None
     if need_ctx:
         ctx = NativeCtx()
-        ctx.X, ctx.buf, ctx.p_drop, ctx.seeds = X, buf, pd, dict(seeds)
+        ctx.X, ctx.buf, ctx.p_drop, ctx.seeds, ctx.window = X, buf, pd, dict(seeds), window
     return X2, ctx
 
 
 def layer_backward(dX2: torch.Tensor, ctx: NativeCtx, packed, p, g, dims, prec: str,
                    side: Optional["torch.cuda.Stream"] = None, deep_wgrad: bool = True) -> torch.Tensor:
-    cb, _, bb = sizes(dims.N, dims.d, dims.ff, prec, ctx.p_drop, deep_wgrad)
+    cb, _, bb = sizes(dims.N, dims.d, dims.ff, prec, ctx.p_drop, deep_wgrad, ctx.window)
     dev = dX2.device
     dX = torch.empty(dims.Np, dims.dp, device=dev, dtype=torch.float32)
-    ws = torch.empty(bb, device=dev, dtype=torch.uint8)
-    dd, pp, ss = _dims(dims.N, dims.d, dims.ff, prec, deep_wgrad), _params(packed, p), _seeds(ctx.p_drop, ctx.seeds)
+    ws = torch.empty(max(256, bb), device=dev, dtype=torch.uint8)
+    dd = _dims(dims.N, dims.d, dims.ff, prec, deep_wgrad, ctx.window)
+    pp, ss = _params(packed, p), _seeds(ctx.p_drop, ctx.seeds)
     gg = LayerGrads(*[getattr(g, k).data_ptr() for k in _lib._PKEYS])
     check(hip_lib().u2gnn_layer_bwd(ctypes.byref(dd), ctypes.byref(pp), ctypes.byref(ss), ctx.X.data_ptr(),
                                     ctx.buf.data_ptr(), cb, dX2.data_ptr(), dX.data_ptr(), ctypes.byref(gg),

@@ -28,7 +28,8 @@ class UnSupCore:
         self.L = module.num_U2GNN_layers
         self.T = module.num_self_att_layers
         self.p_out = module.dropout_p
-        self.stack = EncoderStack(module.u2gnn_layers, self.d, self.ff, self.T, self.L, precision, 0.5)
+        self.stack = EncoderStack(module.u2gnn_layers, self.d, self.ff, self.T, self.L, precision, 0.5,
+                                  getattr(module, "attention", "nodes"))
 
     def encode(self, b: DeviceBatch, train: bool, need_ctx: bool, seed: int):
         """-> (OV f32 [N, d*L] real layout, ctx)."""

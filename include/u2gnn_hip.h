@@ -217,6 +217,20 @@ int u2gnn_dropout(const float *X, int64_t ldx, float *Y, int64_t ldy, int64_t ro
 /* out[i*cols + j] = keep(seed, i, j) ? 1 : 0   (the exact dropout mask the kernels apply) */
 int u2gnn_dropout_mask(uint64_t seed, int64_t rows, int64_t cols, float p, uint8_t *out, void *stream);
 
+/* ---- paper-semantics neighbourhood attention ---------------------
+ * Token rows node-major (row n*W + s = slot s of node n, W = k+1 <= 32); QKV [rows_pad, ldq >= 3dp]
+ * = [Q/sqrt(d) | K | V].  Per node: P = softmax(Qs K^T) over the node's W keys, Pd = dropout(P)
+ * (keep(seed, n*W+i, j)), O = Pd V.  Psave [n_nodes, W, W] holds P for the backward.  Rows
+ * n_nodes*W .. rows_pad-1 of O (resp. dQKV) are zeroed.  LDS bound: (3W*dp + W(W+1))*4 B (fwd),
+ * (4W*dp + 2W(W+1))*4 B (bwd) <= 160 KiB, else U2GNN_E_SHAPE. */
+int u2gnn_window_attn_fwd(const float *QKV, int64_t ldq, int32_t W, int32_t dp, float *O, int64_t ldo,
+                          float *Psave, float p, uint64_t seed, int64_t n_nodes, int64_t rows_pad,
+                          void *stream);
+/* dQKV = [q_scale * dL/dQs | dL/dK | dL/dV] from dO [rows_pad, ldo] and Psave. */
+int u2gnn_window_attn_bwd(const float *QKV, int64_t ldq, int32_t W, int32_t dp, const float *dO,
+                          int64_t ldo, const float *Psave, float p, uint64_t seed, float q_scale,
+                          float *dQKV, int64_t ldg, int64_t n_nodes, int64_t rows_pad, void *stream);
+
 /* ---- a3: one encoder layer (TransformerEncoderLayer(d, nhead=1, ff, dropout), post-LN, slot-0
  * rows) issued natively: forward and backward of pytorch_U2GNN_Sup.py:19-21,35 /
  * pytorch_U2GNN_UnSup.py:37-40,57, launch-for-launch the sequence of u2gnn_hip/engine.py.
@@ -227,9 +241,12 @@ int u2gnn_dropout_mask(uint64_t seed, int64_t rows, int64_t cols, float p, uint8
  * streams before reading grads and must keep X, ctx, dX2 and ws alive until side_stream drains. */
 #define U2GNN_LAYER_DEEP_WGRAD 1   /* weight gradients on the 16-deep-K 128x128 tile */
 typedef struct u2gnn_layer_dims {
-    int64_t N, d, ff;      /* real nodes, model width, FFN width */
+    int64_t N, d, ff;      /* real rows (nodes; window mode: nodes * window tokens), model width, FFN width */
     int32_t precision;     /* U2GNN_PREC_* */
     int32_t flags;         /* U2GNN_LAYER_* */
+    int32_t window;        /* 0: attention over all N rows (the fork's semantics); W >= 1: attention
+                              within consecutive windows of W rows (paper semantics, N % W == 0) */
+    int32_t reserved;
 } u2gnn_layer_dims;
 typedef struct u2gnn_layer_params {
     const float *W_in, *b_in, *W_o, *b_o, *W1, *b1, *W2, *b2;   /* padded copies ([3dp,dp], [3dp], ...) */

@@ -242,21 +242,26 @@ def layer_params(sd: Dict[str, torch.Tensor], l: int, t: int) -> Dict[str, torch
 def sup_forward(sd: Dict[str, torch.Tensor], input_x: torch.Tensor, offsets: np.ndarray,
                 X_concat: torch.Tensor, num_layers: int, num_timesteps: int, train: bool,
                 dropout: float = 0.5, slots: Optional[int] = None,
-                masks: Optional[dict] = None) -> torch.Tensor:
+                masks: Optional[dict] = None, attention: str = "nodes") -> torch.Tensor:
     """pytorch_U2GNN_Sup.py:30-46.  ``sd`` uses the reference state_dict keys.
     ``masks[(l, t)]`` feeds encoder_layer; ``masks[('head', l)]`` is the [B,d] mask of
-    the graph-embedding dropout (pytorch_U2GNN_Sup.py:42)."""
+    the graph-embedding dropout (pytorch_U2GNN_Sup.py:42).
+    attention="neighbors": the paper semantics (U2GNN_tf/model_U2GNN_Sup_multi.py:14-45) restated
+    on the same torch encoder by feeding the gathered window transposed, [k+1, N, d], so each node
+    attends over its own k+1 tokens (no TF oracle here, parity of this mode is
+    unpinned by the reference)."""
     if slots is not None:
         input_x = input_x[:, :slots]
     P = pool_matrix(offsets)
     scores = 0
     inp = F.embedding(input_x, X_concat)                   # [N, k+1, d]
+    nb = attention == "neighbors"
     for l in range(num_layers):
-        x = inp
+        x = inp.transpose(0, 1) if nb else inp
         for t in range(num_timesteps):
             x = encoder_layer(x, layer_params(sd, l, t), train, 0.5,
                               None if masks is None else masks[(l, t)])
-        out = x[:, 0, :]                                  # slot 0
+        out = x[0] if nb else x[:, 0, :]                  # slot 0
         inp = F.embedding(input_x, out)
         ge = P @ out
         hm = None if masks is None else masks.get(("head", l))

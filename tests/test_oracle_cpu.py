@@ -94,3 +94,32 @@ def test_c_oracle_sampler_vs_reference_sets(golden_dir):
             lib.lus_oracle_expected_count(h, nt.value, ref.ctypes.data, 512, ec.ctypes.data)
             assert np.array_equal(ec, z[f"V{V}_c{c}_sample_freq"])
         lib.lus_oracle_destroy(h)
+
+
+def test_oracle_neighbors_mode_matches_torch_encoder_on_transposed_window():
+    """Paper semantics restated: the oracle's encoder on the transposed window [k+1, N, d] equals
+    torch.nn.TransformerEncoder (the reference's module, eval mode) fed the same tensor, and the
+    attention="neighbors" forward uses exactly that (slot 0 = sequence position 0)."""
+    import torch
+    from oracle import u2gnn_oracle as O
+    torch.manual_seed(3)
+    d, ff, T, N, k = 12, 32, 2, 9, 4
+    enc = torch.nn.TransformerEncoder(torch.nn.TransformerEncoderLayer(d, 1, ff, 0.5), T,
+                                      enable_nested_tensor=False).eval()
+    x = torch.randn(N, k + 1, d)
+    ref = enc(x.transpose(0, 1))
+    sd = {f"u2gnn_layers.0.{kk}": v for kk, v in enc.state_dict().items()}
+    y = x.transpose(0, 1)
+    for t in range(T):
+        y = O.encoder_layer(y, O.layer_params(sd, 0, t), train=False)
+    assert torch.allclose(y, ref, atol=1e-5)
+    # full forward: pooled slot-0 rows through the head
+    input_x = torch.randint(0, N, (N, k + 1))
+    input_x[:, 0] = torch.arange(N)
+    X = torch.randn(N, d)
+    sd["predictions.0.weight"], sd["predictions.0.bias"] = torch.randn(3, d), torch.randn(3)
+    offsets = np.array([0, 4, N])
+    scores = O.sup_forward(sd, input_x, offsets, X, 1, T, train=False, attention="neighbors")
+    out = enc(torch.nn.functional.embedding(input_x, X).transpose(0, 1))[0]
+    exp = O.pool_matrix(offsets) @ out @ sd["predictions.0.weight"].t() + sd["predictions.0.bias"]
+    assert torch.allclose(scores, exp, atol=1e-5)

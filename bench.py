@@ -242,7 +242,7 @@ def main():
     # roofline pass: the same K steps again with per-GEMM HIP events (kept out of the timed region)
     K.REC.records.clear()
     rec_elapsed = None
-    if not args.no_roofline:
+    if not args.no_roofline and args.attention == "nodes":   # per-GEMM events: Python orchestration
         from u2gnn_hip.engine import set_overlap
         from u2gnn_hip import native
         set_overlap(False)   # serial: each GEMM's events time that kernel alone

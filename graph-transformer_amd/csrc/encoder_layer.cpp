@@ -27,6 +27,10 @@ namespace {
 
 inline int64_t rup(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 
+// padded rows: multiples of 256 from 1024 rows on (the N^2 products always get 256x128 blocks),
+// else of 128 (mirrors engine.row_pad)
+inline int64_t rows_pad(int64_t N) { return N >= 1024 ? rup(N, 256) : rup(N, 128); }
+
 struct Dims {
     int64_t N, d, ff, Np, dp, ffp;
     int prec;
@@ -39,7 +43,7 @@ Dims make_dims(const u2gnn_layer_dims *a) {
     D.N = a->N;
     D.d = a->d;
     D.ff = a->ff;
-    D.Np = rup(a->N, 128);
+    D.Np = rows_pad(a->N);
     D.dp = rup(a->d, 64);
     D.ffp = rup(a->ff, 64);
     D.prec = a->precision;

@@ -9,7 +9,8 @@ computes exactly the slot-0 path — gather(X_concat, input_x[:,0]) -> T post-LN
 layers with single-head attention over all N nodes -> pooling/head — which is equal to the
 reference output (slots 1..k never reach the output) at 1/(k+1) of the reference's work.
 
-Layouts in HBM (fp32, row-major): node rows padded to Np = roundup(N, 128), feature columns
+Layouts in HBM (fp32, row-major): node rows padded to Np = row_pad(N) (a multiple of 128, of 256
+from 1024 rows on), feature columns
 to dp = roundup(d, 64), FFN width to ffp = roundup(ff, 64); QKV is one [Np, 3*dp] buffer
 (Q pre-scaled by 1/sqrt(d)); attention probabilities P and the dropped Pd are [Np, Np].
 Padding rows/columns hold zeros in every activation and gradient the encoder produces
@@ -32,6 +33,12 @@ E = _lib
 
 def rup(x: int, m: int) -> int:
     return (x + m - 1) // m * m
+
+
+def row_pad(N: int) -> int:
+    """Padded node rows: multiples of 256 from 1024 rows on (the N^2 products then always run on
+    256x128 blocks), else of 128.  Mirrors rows_pad() in csrc/encoder_layer.cpp."""
+    return rup(N, 256) if N >= 1024 else rup(N, 128)
 
 
 def _mix64(z: int) -> int:
@@ -61,7 +68,7 @@ class Dims:
 
     @property
     def Np(self):
-        return rup(self.N, 128)
+        return row_pad(self.N)
 
     @property
     def dp(self):

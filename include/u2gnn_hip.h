@@ -234,7 +234,8 @@ int u2gnn_window_attn_bwd(const float *QKV, int64_t ldq, int32_t W, int32_t dp, 
 /* ---- a3: one encoder layer (TransformerEncoderLayer(d, nhead=1, ff, dropout), post-LN, slot-0
  * rows) issued natively: forward and backward of pytorch_U2GNN_Sup.py:19-21,35 /
  * pytorch_U2GNN_UnSup.py:37-40,57, launch-for-launch the sequence of u2gnn_hip/engine.py.
- * Padded layouts: Np = roundup(N,128) rows, dp = roundup(d,64), ffp = roundup(ff,64) columns.
+ * Padded layouts: Np = roundup(N,256) rows for N >= 1024, else roundup(N,128); dp = roundup(d,64),
+ * ffp = roundup(ff,64) columns.
  * All buffers are caller-allocated; u2gnn_layer_sizes gives the three sizes (ctx = tensors
  * saved for the backward, fwd/bwd workspaces).  The backward's parameter-gradient work goes to
  * side_stream (NULL: same stream) after the main-stream results it reads; the caller joins the

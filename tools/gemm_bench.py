@@ -20,6 +20,13 @@ SHAPES = [  # name, M, N, K, ta, tb, [(split, tile), ...] (tile 129 = 128x128 wi
     ("QKV   NT", Np, 3 * dp, dp, False, True, [(1, 64), (1, 128), (1, 256)]),
     ("FFN1  NT", Np, ffp, dp, False, True, [(1, 64), (1, 128), (1, 256)]),
     ("FFN2  NT", Np, dp, ffp, False, True, [(1, 64), (1, 128), (2, 129)]),
+    # epilogue GEMMs of the layer as the executor issues them (dropout p = 0.5 where it applies)
+    ("QKVb  NT", Np, 3 * dp, dp, False, True, [(1, 64), (1, 128), (1, 256)], 1),
+    ("FFN1d NT", Np, ffp, dp, False, True, [(1, 64), (1, 128), (1, 256)], 3),
+    ("outpr NT", Np, dp, dp, False, True, [(1, 64), (1, 128), (1, 256)], 2),
+    ("FFN2r NT", Np, dp, ffp, False, True, [(1, 64), (1, 128), (1, 256)], 2),
+    ("dH    NN", Np, ffp, dp, False, False, [(1, 64), (1, 128), (1, 256)], 4),
+    ("dO    NN", Np, dp, dp, False, False, [(1, 64), (1, 128), (1, 256)]),
 ]
 
 
@@ -41,6 +48,12 @@ def run(prec):
                        keep=torch.randint(-2**31, 2**31 - 1, (M, N // 32), device="cuda", dtype=torch.int32,
                                           generator=g),
                        rowvec=torch.randn(M, device="cuda", generator=g), ld_aux=N)
+        if epi in (1, 2, 3, 4):
+            ext = dict(epilogue=epi, p_drop=0.5 if epi != 1 else 0.0, seed=7, ld_aux=N, alpha=0.05, scale_cols=dp)
+            if epi in (1, 2, 3):
+                ext["bias"] = torch.randn(N, device="cuda", generator=g)
+            if epi in (2, 4):
+                ext["aux0"] = torch.randn(M, N, device="cuda", generator=g)
         if ONLY and not any(name.startswith(o) for o in ONLY.split(",")):
             continue
         A = torch.randn(Kd, M, device="cuda", generator=g) if ta else torch.randn(M, Kd, device="cuda", generator=g)
@@ -62,13 +75,15 @@ def run(prec):
             torch.cuda.synchronize()
             us = s.elapsed_time(e) / REPS * 1e3
             ref = (A.t() if ta else A).double() @ (B.t() if tb else B).double()
-            if epi == 6:
+            if epi in (1, 2, 3, 4):   # dropout epilogues: timing only
+                ref = None
+            elif epi == 6:
                 ref = ext["aux1"].double() * ref - ext["aux0"].double() * ext["rowvec"].double()[:, None]
             elif epi == 7:
                 w = ext["keep"].to(torch.int64) & 0xFFFFFFFF
                 kb = ((w[:, :, None] >> torch.arange(32, device="cuda")) & 1).reshape(M, -1).double()
                 ref = ext["aux0"].double() * (kb * ref * 2 - ext["rowvec"].double()[:, None])
-            err = ((C.sum(0).double() - ref).abs().max() / ref.abs().max()).item()
+            err = float("nan") if ref is None else ((C.sum(0).double() - ref).abs().max() / ref.abs().max()).item()
             print(f"{prec:7s} {name}  M={M:5d} N={N:5d} K={Kd:5d} split={split:2d} tile={tile:3d}: {us:8.1f} us "
                   f"{2.0 * M * N * Kd / us / 1e6:7.1f} TF/s  relerr {err:.1e}")
 

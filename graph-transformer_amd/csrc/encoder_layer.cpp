@@ -228,7 +228,9 @@ int layer_fwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
     // a3.1 in-projection (+bias, Q scaled by 1/sqrt(d))
     {
         G g(X, w->W_in, c.QKV, Np, 3 * dp, dp, dp, dp, 3 * dp, prec);
-        g.tb().epi(U2GNN_EPI_BIAS);
+        // 256x128 blocks once they fill the chip (C4: 19 x 9); the 64 tile below that
+        g.tb().epi(U2GNN_EPI_BIAS).tile(prec != U2GNN_PREC_F32 && Np % 256 == 0 && (Np / 256) * (3 * dp / 128) >= 128
+                                            ? 256 : 0);
         g.a.bias = w->b_in;
         g.a.alpha = (float)(1.0 / std::sqrt((double)d));
         g.a.scale_cols = dp;

@@ -50,34 +50,56 @@ struct GemmP {
 // with a leading dimension that is a multiple of 4 (checked by u2gnn_gemm)
 __device__ __forceinline__ float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
 
+// The epilogue runs in two passes per 32-row slice of a wave's tile: epi_fetch issues every
+// auxiliary load (P, keep words, residual, bias, C) first, then epilogue4 combines and stores.
+// Interleaved in one loop, each load would sit behind the previous store (the compiler cannot
+// prove C distinct from the aux operands) and the slice would pay one memory round trip per
+// 4 columns.
 template <int EPI>
-__device__ __forceinline__ float4 epilogue4(const GemmP &P, int row, int col, float4 v) {
+__device__ __forceinline__ void epi_fetch(const GemmP &P, int row, int col, float4 &a, float4 &b, uint32_t &kb) {
+    if constexpr (EPI == U2GNN_EPI_ATTN_DS) {
+        const int64_t o = (int64_t)row * P.ld_aux + col;
+        a = ld4(P.aux0 + o);
+        if (P.keep)
+            kb = P.keep[(int64_t)row * P.ld_keep + (col >> 5)] >> (col & 31);
+        else
+            b = ld4(P.aux1 + o);
+    } else if constexpr (EPI == U2GNN_EPI_ACCUM) {
+        a = ld4(P.C + (int64_t)row * P.ldc + col);
+    } else if constexpr (EPI == U2GNN_EPI_RELU_DROP_BWD) {
+        a = ld4(P.aux0 + (int64_t)row * P.ld_aux + col);
+    } else if constexpr (EPI != U2GNN_EPI_STORE) {
+        a = ld4(P.bias + col);
+        if constexpr (EPI == U2GNN_EPI_BIAS_DROP_RESID) b = ld4(P.aux0 + (int64_t)row * P.ld_aux + col);
+    }
+}
+
+// four consecutive columns (col % 4 == 0) of one row; a, b, kb, dl = what epi_fetch loaded
+template <int EPI>
+__device__ __forceinline__ float4 epilogue4(const GemmP &P, int row, int col, float4 v, float4 a, float4 b,
+                                            uint32_t kb, float dl) {
     if constexpr (EPI == U2GNN_EPI_STORE) {
         return make_float4(P.alpha * v.x, P.alpha * v.y, P.alpha * v.z, P.alpha * v.w);
     } else if constexpr (EPI == U2GNN_EPI_ATTN_DS) {
-        const int64_t o = (int64_t)row * P.ld_aux + col;
-        const float4 pr = ld4(P.aux0 + o);
-        const float dl = P.rowvec[row];
+        const float4 pr = a;
         if (P.keep) {   // dS = P * (keep * dPd / (1-p) - delta): 4 keep bits instead of 16 B of Pd
-            const uint32_t kb = P.keep[(int64_t)row * P.ld_keep + (col >> 5)] >> (col & 31);
             const float s = 1.f / (1.f - P.p);
             return make_float4(pr.x * (((kb & 1u) ? v.x * s : 0.f) - dl), pr.y * (((kb & 2u) ? v.y * s : 0.f) - dl),
                                pr.z * (((kb & 4u) ? v.z * s : 0.f) - dl), pr.w * (((kb & 8u) ? v.w * s : 0.f) - dl));
         }
-        const float4 pd = ld4(P.aux1 + o);
+        const float4 pd = b;
         return make_float4(pd.x * v.x - pr.x * dl, pd.y * v.y - pr.y * dl, pd.z * v.z - pr.z * dl,
                            pd.w * v.w - pr.w * dl);
     } else if constexpr (EPI == U2GNN_EPI_ACCUM) {
-        const float4 c = ld4(P.C + (int64_t)row * P.ldc + col);
+        const float4 c = a;
         return make_float4(c.x + P.alpha * v.x, c.y + P.alpha * v.y, c.z + P.alpha * v.z, c.w + P.alpha * v.w);
     } else if constexpr (EPI == U2GNN_EPI_RELU_DROP_BWD) {
-        const float4 h = ld4(P.aux0 + (int64_t)row * P.ld_aux + col);
+        const float4 h = a;
         const float s = 1.f / (1.f - P.p);
         return make_float4(h.x > 0.f ? v.x * s : 0.f, h.y > 0.f ? v.y * s : 0.f, h.z > 0.f ? v.z * s : 0.f,
                            h.w > 0.f ? v.w * s : 0.f);
     } else {  // bias epilogues: per-column dropout hash
-        const float4 b = ld4(P.bias + col);
-        float x[4] = {v.x + b.x, v.y + b.y, v.z + b.z, v.w + b.w};
+        float x[4] = {v.x + a.x, v.y + a.y, v.z + a.z, v.w + a.w};
         if constexpr (EPI == U2GNN_EPI_BIAS) {
 #pragma unroll
             for (int c = 0; c < 4; ++c) x[c] = col + c < P.scale_cols ? x[c] * P.alpha : x[c];
@@ -92,11 +114,91 @@ __device__ __forceinline__ float4 epilogue4(const GemmP &P, int row, int col, fl
                 for (int c = 0; c < 4; ++c) x[c] = u2gnn_keep(P.seed, row, col + c, P.p) ? x[c] * s : 0.f;
             }
             if constexpr (EPI == U2GNN_EPI_BIAS_DROP_RESID) {
-                const float4 r = ld4(P.aux0 + (int64_t)row * P.ld_aux + col);
-                x[0] += r.x, x[1] += r.y, x[2] += r.z, x[3] += r.w;
+                x[0] += b.x, x[1] += b.y, x[2] += b.z, x[3] += b.w;
             }
         }
         return make_float4(x[0], x[1], x[2], x[3]);
+    }
+}
+
+// lane (li, kh) of MFMA tile (i, j) holds C[row = li][cols 8g + 4kh .. +3] in acc[i][j][4g .. 4g+3].
+// One 32-row slice (fixed i) of a wave's tile: its auxiliary operands, then its stores.
+template <int EPI, int TN>
+struct EpiSlice {
+    float4 a[TN][4], b[TN][4];
+    uint32_t kb[TN][4];
+    float dl;
+};
+
+template <int EPI, int TN>
+__device__ __forceinline__ void fetch_slice(const GemmP &P, int row, int c0, int kh, EpiSlice<EPI, TN> &e) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            e.a[j][g] = e.b[j][g] = make_float4(0.f, 0.f, 0.f, 0.f);
+            e.kb[j][g] = 0;
+            epi_fetch<EPI>(P, row, c0 + j * 32 + 8 * g + 4 * kh, e.a[j][g], e.b[j][g], e.kb[j][g]);
+        }
+    e.dl = EPI == U2GNN_EPI_ATTN_DS ? P.rowvec[row] : 0.f;
+}
+
+template <int EPI, int TM, int TN>
+__device__ __forceinline__ void store_slice(const GemmP &P, float *C, const f32x16 (&acc)[TM][TN], int i, int row,
+                                            int c0, int kh, const EpiSlice<EPI, TN> &e) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int col = c0 + j * 32 + 8 * g + 4 * kh;
+            const float4 v = make_float4(acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2],
+                                         acc[i][j][4 * g + 3]);
+            *reinterpret_cast<float4 *>(C + (int64_t)row * P.ldc + col) =
+                epilogue4<EPI>(P, row, col, v, e.a[j][g], e.b[j][g], e.kb[j][g], e.dl);
+        }
+}
+
+// Attention dS with keep bits: slice 0's P tile, keep words and delta fetched before the main loop
+// (TN*16 + TN + 1 VGPRs), so they land under the MFMAs and the epilogue pays one round trip less.
+template <int TN>
+struct PreDS {
+    float4 p[TN][4];
+    uint32_t kw[TN];
+    float dl;
+};
+
+template <int EPI, int TN>
+__device__ __forceinline__ void prefetch_ds(const GemmP &P, int row, int c0, int kh, PreDS<TN> &f) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        f.kw[j] = P.keep[(int64_t)row * P.ld_keep + ((c0 + j * 32) >> 5)];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) f.p[j][g] = ld4(P.aux0 + (int64_t)row * P.ld_aux + c0 + j * 32 + 8 * g + 4 * kh);
+    }
+    f.dl = P.rowvec[row];
+}
+
+template <int EPI, int TM, int TN>
+__device__ __forceinline__ void store_tile(const GemmP &P, float *C, const f32x16 (&acc)[TM][TN], int r0, int c0,
+                                           int li, int kh, const PreDS<TN> *pre) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+        const int row = r0 + i * 32 + li;
+        EpiSlice<EPI, TN> e;
+        if (i == 0 && pre) {
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    e.a[j][g] = pre->p[j][g];
+                    e.b[j][g] = make_float4(0.f, 0.f, 0.f, 0.f);
+                    e.kb[j][g] = pre->kw[j] >> ((8 * g + 4 * kh) & 31);
+                }
+            e.dl = pre->dl;
+        } else {
+            fetch_slice<EPI>(P, row, c0, kh, e);
+        }
+        store_slice<EPI>(P, C, acc, i, row, c0, kh, e);
     }
 }
 
@@ -258,20 +360,8 @@ __global__ void __launch_bounds__(256) gemm_f32_kernel(GemmP P) {
         __syncthreads();
     }
 
-    // lane (li, kh) of tile (i, j) holds C[row = li][cols 8g + 4kh .. +3] in acc[4g .. 4g+3]
-    float *C = P.C + (int64_t)zi * P.slab_stride;
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const int row = m0 + wm * WTM + i * 32 + li;
-                const int col = n0 + wn * WTN + j * 32 + 8 * g + 4 * kh;
-                const float4 v = make_float4(acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2],
-                                             acc[i][j][4 * g + 3]);
-                *reinterpret_cast<float4 *>(C + (int64_t)row * P.ldc + col) = epilogue4<EPI>(P, row, col, v);
-            }
+    store_tile<EPI>(P, P.C + (int64_t)zi * P.slab_stride, acc, m0 + wm * WTM, n0 + wn * WTN, li, kh,
+                    (const PreDS<TN> *)nullptr);
 }
 
 // ------------------------------------------------------------------------------------
@@ -308,6 +398,17 @@ __device__ __forceinline__ void stage_rk(int tid, int i, int &r, int &kq) {
 }
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+#ifdef U2GNN_EXP_NOSTAGE_A   // experiment: A staged once (upper bound of pre-split A planes)
+constexpr bool kStageA = false;
+#else
+constexpr bool kStageA = true;
+#endif
+#ifdef U2GNN_EXP_NOSTAGE_B
+constexpr bool kStageB = false;
+#else
+constexpr bool kStageB = true;
+#endif
 
 #ifdef U2GNN_EXP_NOSTAGE
 #define U2GNN_LOOP_SYNC() ((void)0)
@@ -491,6 +592,9 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_bf16_kernel(GemmP P) {
         }
     };
 
+    PreDS<TN> pre;
+    const bool use_pre = EPI == U2GNN_EPI_ATTN_DS && P.keep != nullptr;
+    if (use_pre) prefetch_ds<EPI>(P, m0 + wm * WTM + li, n0 + wn * WTN, kh, pre);
     if (nk > 0) {
         // two register stages: every tile's global loads are in flight across TWO compute phases
         // (a single phase of 24 MFMAs does not cover an L2/LLC miss at 2 waves per SIMD)
@@ -503,37 +607,25 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_bf16_kernel(GemmP P) {
         r2s_bf<BN, BK, LDK, !TB, SPLIT, NT>(stage(0) + 2 * AE, stage(0) + 2 * AE + BE, tid, rb0);
         __syncthreads();
         for (int t = 0; t < nk; t += 2) {
-            g2r_bf<NFA>(rsA, voA, (min(t + 2, nk - 1)) * kstepA, ra0);
-            g2r_bf<NFB>(rsB, voB, (min(t + 2, nk - 1)) * kstepB, rb0);
+            if constexpr (kStageA) g2r_bf<NFA>(rsA, voA, (min(t + 2, nk - 1)) * kstepA, ra0);
+            if constexpr (kStageB) g2r_bf<NFB>(rsB, voB, (min(t + 2, nk - 1)) * kstepB, rb0);
             compute(stage(0));
-            r2s_bf<BM, BK, LDK, TA, SPLIT, NT>(stage(1), stage(1) + AE, tid, ra1);
-            r2s_bf<BN, BK, LDK, !TB, SPLIT, NT>(stage(1) + 2 * AE, stage(1) + 2 * AE + BE, tid, rb1);
+            if constexpr (kStageA) r2s_bf<BM, BK, LDK, TA, SPLIT, NT>(stage(1), stage(1) + AE, tid, ra1);
+            if constexpr (kStageB) r2s_bf<BN, BK, LDK, !TB, SPLIT, NT>(stage(1) + 2 * AE, stage(1) + 2 * AE + BE, tid, rb1);
             U2GNN_LOOP_SYNC();
             if (t + 1 < nk) {
-                g2r_bf<NFA>(rsA, voA, (min(t + 3, nk - 1)) * kstepA, ra1);
-                g2r_bf<NFB>(rsB, voB, (min(t + 3, nk - 1)) * kstepB, rb1);
+                if constexpr (kStageA) g2r_bf<NFA>(rsA, voA, (min(t + 3, nk - 1)) * kstepA, ra1);
+                if constexpr (kStageB) g2r_bf<NFB>(rsB, voB, (min(t + 3, nk - 1)) * kstepB, rb1);
                 compute(stage(1));
-                r2s_bf<BM, BK, LDK, TA, SPLIT, NT>(stage(0), stage(0) + AE, tid, ra0);
-                r2s_bf<BN, BK, LDK, !TB, SPLIT, NT>(stage(0) + 2 * AE, stage(0) + 2 * AE + BE, tid, rb0);
+                if constexpr (kStageA) r2s_bf<BM, BK, LDK, TA, SPLIT, NT>(stage(0), stage(0) + AE, tid, ra0);
+                if constexpr (kStageB) r2s_bf<BN, BK, LDK, !TB, SPLIT, NT>(stage(0) + 2 * AE, stage(0) + 2 * AE + BE, tid, rb0);
                 U2GNN_LOOP_SYNC();
             }
         }
     }
 
-    // lane (li, kh) of tile (i, j) holds C[row = li][cols 8g + 4kh .. +3] in acc[4g .. 4g+3]
-    float *C = P.C + (int64_t)zi * P.slab_stride;
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const int row = m0 + wm * WTM + i * 32 + li;
-                const int col = n0 + wn * WTN + j * 32 + 8 * g + 4 * kh;
-                const float4 v = make_float4(acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2],
-                                             acc[i][j][4 * g + 3]);
-                *reinterpret_cast<float4 *>(C + (int64_t)row * P.ldc + col) = epilogue4<EPI>(P, row, col, v);
-            }
+    store_tile<EPI>(P, P.C + (int64_t)zi * P.slab_stride, acc, m0 + wm * WTM, n0 + wn * WTN, li, kh,
+                    use_pre ? &pre : nullptr);
 }
 
 // bf16 K-step variants: 0 = BK 32 (2 blocks/CU at 128x128), 1 = BK 16 (40 KB LDS, 140-152

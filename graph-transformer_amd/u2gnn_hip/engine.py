@@ -250,7 +250,8 @@ def encoder_layer_forward(X: torch.Tensor, w: PackedLayer, p: LayerParams, dims:
     f32 = torch.float32
     QKV = torch.empty(Np, 3 * dp, device=dev, dtype=f32)
     K.gemm(X, w.W_in, QKV, Np, 3 * dp, dp, dp, dp, 3 * dp, trans_b=True, epilogue=E.EPI_BIAS, bias=w.b_in,
-           alpha=1.0 / math.sqrt(d), scale_cols=dp, precision=prec, flops=6.0 * N * d * d)
+           alpha=1.0 / math.sqrt(d), scale_cols=dp, precision=prec, flops=6.0 * N * d * d,
+           tile=256 if (prec != "fp32" and Np % 256 == 0 and (Np // 256) * (3 * dp // 128) >= 128) else 0)
     Q, Kt, V = QKV[:, :dp], QKV[:, dp:2 * dp], QKV[:, 2 * dp:]
     S = torch.empty(Np, Np, device=dev, dtype=f32)
     K.gemm(Q, Kt, S, Np, Np, dp, 3 * dp, 3 * dp, Np, trans_b=True, precision=prec, flops=att,

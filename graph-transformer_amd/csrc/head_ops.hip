@@ -7,17 +7,18 @@ namespace {
 
 // ------------------------------------------------------------------------------------------
 // a5/a6 pooling: torch.spmm(graph_pool, output_Tr) with graph_pool in CSR form
-// (pytorch_U2GNN_Sup.py:41) followed by dropout (:42).  Block = one graph x 256 columns.
+// (pytorch_U2GNN_Sup.py:41) followed by dropout (:42).  Block = one graph x 64 columns.
 // ------------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) pool_fwd_kernel(const float *X, int64_t ldx, const int64_t *rowptr,
                                                        const int64_t *colidx, const float *vals, float *G, int64_t ldg,
                                                        int64_t d, float p, uint64_t seed) {
-    // block = one graph; the 4 waves split the graph's rows, lanes cover 64 columns at a time
+    // block = (graph, 64-column chunk); the 4 waves split the graph's rows
     __shared__ float red[4][64];
     const int64_t b = blockIdx.x;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int64_t e0 = rowptr[b], e1 = rowptr[b + 1];
-    for (int64_t c0 = 0; c0 < d; c0 += 64) {
+    {
+        const int64_t c0 = (int64_t)blockIdx.y * 64;
         const int64_t c = c0 + lane;
         float s[4] = {0.f, 0.f, 0.f, 0.f};
         if (c < d) {
@@ -34,18 +35,19 @@ __global__ void __launch_bounds__(256) pool_fwd_kernel(const float *X, int64_t l
             if (p > 0.f) v = u2gnn_keep(seed, (uint32_t)b, (uint32_t)c, p) ? v * (1.f / (1.f - p)) : 0.f;
             G[b * ldg + c] = v;
         }
-        __syncthreads();
     }
 }
 
 __global__ void __launch_bounds__(256) pool_bwd_kernel(const float *dGd, int64_t ldg, const int64_t *rowptr,
                                                        const int64_t *colidx, const float *vals, float *dX,
                                                        int64_t ldx, int64_t d, float p, uint64_t seed) {
-    // block = (graph, 4-row slice); lanes over columns; one atomic per (row, column)
+    // block = (graph, row slice, 64-column chunk); one atomic per (row, column)
     const int64_t b = blockIdx.x;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int64_t e0 = rowptr[b], e1 = rowptr[b + 1];
-    for (int64_t c = lane; c < d; c += 64) {
+    {
+        const int64_t c = (int64_t)blockIdx.z * 64 + lane;
+        if (c >= d) return;
         float g = dGd[b * ldg + c];
         if (p > 0.f) g = u2gnn_keep(seed, (uint32_t)b, (uint32_t)c, p) ? g * (1.f / (1.f - p)) : 0.f;
         for (int64_t e = e0 + (int64_t)blockIdx.y * 4 + w; e < e1; e += (int64_t)gridDim.y * 4)
@@ -271,7 +273,7 @@ extern "C" {
 int u2gnn_pool_fwd(const float *X, int64_t ldx, const int64_t *rowptr, const int64_t *colidx, const float *vals,
                    float *G, int64_t ldg, int64_t B, int64_t d, float p, uint64_t seed, void *stream) {
     if (!X || !rowptr || !colidx || !vals || !G || B < 1 || d < 1) return U2GNN_E_ARG;
-    hipLaunchKernelGGL(pool_fwd_kernel, dim3((unsigned)B), dim3(256), 0,
+    hipLaunchKernelGGL(pool_fwd_kernel, dim3((unsigned)B, (unsigned)((d + 63) / 64)), dim3(256), 0,
                        u2gnn_stream(stream), X, ldx, rowptr, colidx, vals, G, ldg, d, p, seed);
     return u2gnn_launch_status();
 }
@@ -279,7 +281,7 @@ int u2gnn_pool_fwd(const float *X, int64_t ldx, const int64_t *rowptr, const int
 int u2gnn_pool_bwd(const float *dGd, int64_t ldg, const int64_t *rowptr, const int64_t *colidx, const float *vals,
                    float *dX, int64_t ldx, int64_t B, int64_t d, float p, uint64_t seed, void *stream) {
     if (!dGd || !rowptr || !colidx || !vals || !dX || B < 1 || d < 1) return U2GNN_E_ARG;
-    hipLaunchKernelGGL(pool_bwd_kernel, dim3((unsigned)B, 8), dim3(256), 0,
+    hipLaunchKernelGGL(pool_bwd_kernel, dim3((unsigned)B, 8, (unsigned)((d + 63) / 64)), dim3(256), 0,
                        u2gnn_stream(stream), dGd, ldg, rowptr, colidx, vals, dX, ldx, d, p, seed);
     return u2gnn_launch_status();
 }

@@ -1,5 +1,5 @@
 """Summarise a rocprofv3 kernel trace (rocpd .db -> per-kernel totals).  Usage:
-   python tools/kstats.py <run_results.db> [out.txt] [title]"""
+   python tools/kstats.py <run_results.db> [out.txt] [title] [trace_copy.csv]"""
 import collections
 import csv
 import os
@@ -13,6 +13,9 @@ title = sys.argv[3] if len(sys.argv) > 3 else ""
 tmp = tempfile.mkdtemp()
 subprocess.run(["rocpd2csv", "-i", db, "-d", tmp], check=True, capture_output=True)
 rows = list(csv.DictReader(open(os.path.join(tmp, "out_kernel_trace.csv"))))
+if len(sys.argv) > 4:   # keep the raw trace (timeline analysis: tools/timeline.py)
+    import shutil
+    shutil.copy(os.path.join(tmp, "out_kernel_trace.csv"), sys.argv[4])
 agg = collections.defaultdict(lambda: [0, 0.0])
 for r in rows:
     d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3

@@ -88,23 +88,21 @@ bool debug_on() {
     } while (0)
 
 struct Ctx {   // tensors saved by the forward for the backward
-    float *QKV, *P, *Pd, *O, *Z1, *X1, *mean1, *rstd1, *Hd, *Z2, *mean2, *rstd2;
-    uint32_t *keep;
+    // Pd: with dropout the signed probability image (P/(1-p) where kept, -P where dropped), else P
+    float *QKV, *Pd, *O, *Z1, *X1, *mean1, *rstd1, *Hd, *Z2, *mean2, *rstd2;
     float *Psave;   // window mode: [N/W, W, W] probabilities
 };
 
 Ctx carve_ctx(Arena &A, const Dims &D, bool drop) {
     Ctx c;
     c.QKV = A.take<float>(D.Np * 3 * D.dp);
+    (void)drop;
     if (D.window) {
-        c.P = c.Pd = nullptr;
-        c.keep = nullptr;
+        c.Pd = nullptr;
         c.Psave = A.take<float>(D.N * D.window);
     } else {
         c.Psave = nullptr;
-        c.P = A.take<float>(D.Np * D.Np);
-        c.Pd = drop ? A.take<float>(D.Np * D.Np) : c.P;
-        c.keep = drop ? A.take<uint32_t>(D.Np * (D.Np / 32)) : nullptr;
+        c.Pd = A.take<float>(D.Np * D.Np);
     }
     c.O = A.take<float>(D.Np * D.dp);
     c.Z1 = A.take<float>(D.Np * D.dp);
@@ -140,7 +138,7 @@ struct G {   // one GEMM launch (defaults = plain store)
 // padded->real block map).  deep = weight gradient (16-deep K step, <= 16 slabs).
 int gemm_split(Arena &W, const Dims &D, const float *A, const float *B, float *C, int64_t M, int64_t N, int64_t Kd,
                int64_t lda, int64_t ldb, int64_t ldc, bool ta, float alpha, bool accumulate, const int64_t *rblk,
-               const int64_t *cblk, bool deep, hipStream_t st) {
+               const int64_t *cblk, bool deep, hipStream_t st, bool clamp_a = false) {
     const bool f32 = D.prec == U2GNN_PREC_F32;
     const int64_t bk = f32 ? 16 : 32;
     int t;
@@ -166,6 +164,7 @@ int gemm_split(Arena &W, const Dims &D, const float *A, const float *B, float *C
         G g(A, B, C, M, N, Kd, lda, ldb, ldc, D.prec);
         if (ta) g.ta();
         g.a.alpha = alpha;
+        g.a.clamp_a = clamp_a;
         g.epi(accumulate ? U2GNN_EPI_ACCUM : U2GNN_EPI_STORE).tile(t);
         return g.run(st, plan);
     }
@@ -174,6 +173,7 @@ int gemm_split(Arena &W, const Dims &D, const float *A, const float *B, float *C
     if (ta) g.ta();
     g.a.split_k = (int32_t)split;
     g.a.slab_stride = M * N;
+    g.a.clamp_a = clamp_a;
     g.tile(t);
     U2GNN_TRY(g.run(st, plan));
     if (plan) return U2GNN_OK;
@@ -224,7 +224,6 @@ int layer_fwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
     const bool drop = pd > 0.f;
     const bool plan = W.plan();
     Ctx c = carve_ctx(need_ctx ? CA : W, D, drop);
-    if (!need_ctx) c.keep = nullptr;
     // a3.1 in-projection (+bias, Q scaled by 1/sqrt(d))
     {
         G g(X, w->W_in, c.QKV, Np, 3 * dp, dp, dp, dp, 3 * dp, prec);
@@ -251,9 +250,10 @@ int layer_fwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
             U2GNN_TRY(g.run(st, plan));
         }
         if (!plan)
-            U2GNN_TRY(u2gnn_attn_softmax_fwd(S, Np, c.P, c.Pd, Np, N, Np, N, Np, pd, s->attn, c.keep, Np / 32, st));
+            U2GNN_TRY(u2gnn_attn_softmax_fwd(S, Np, drop ? nullptr : c.Pd, c.Pd, Np, N, Np, N, Np, pd, s->attn,
+                                             nullptr, 0, st));
         U2GNN_TRY(gemm_split(W, D, c.Pd, V, c.O, Np, dp, Np, Np, 3 * dp, dp, false, 1.f, false, nullptr, nullptr,
-                             false, st));
+                             false, st, drop));
     }
     // a3.3 out-projection + dropout1 + residual, LayerNorm1
     {
@@ -349,18 +349,13 @@ int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
         float *dS = W.take<float>(Np * Np);
         {
             G gg(dO, V, dS, Np, Np, dp, dp, 3 * dp, Np, prec);
-            gg.tb().epi(U2GNN_EPI_ATTN_DS);
-            gg.a.aux0 = c.P, gg.a.rowvec = delta, gg.a.ld_aux = Np, gg.a.p_drop = pd;
-            if (c.keep) {
-                gg.a.keep = c.keep, gg.a.ld_keep = Np / 32;
-            } else {
-                gg.a.aux1 = c.Pd;
-            }
+            gg.tb().epi(U2GNN_EPI_ATTN_DS_SIGNED);
+            gg.a.aux0 = c.Pd, gg.a.rowvec = delta, gg.a.ld_aux = Np, gg.a.p_drop = pd;
             U2GNN_TRY(gg.run(st, plan));
         }
         dQKV = W.take<float>(Np * 3 * dp);
         U2GNN_TRY(gemm_split(W, D, c.Pd, dO, dQKV + 2 * dp, Np, dp, Np, Np, dp, 3 * dp, true, 1.f, false, nullptr,
-                             nullptr, false, st));
+                             nullptr, false, st, pd > 0.f));
         U2GNN_TRY(gemm_split(W, D, dS, Kt, dQKV, Np, dp, Np, Np, 3 * dp, 3 * dp, false, q_scale, false, nullptr, nullptr,
                              false, st));
         U2GNN_TRY(gemm_split(W, D, dS, Q, dQKV + dp, Np, dp, Np, Np, 3 * dp, 3 * dp, true, 1.f, false, nullptr, nullptr,

@@ -240,14 +240,16 @@ __global__ void __launch_bounds__(256) attn_softmax_kernel(const float *S, int64
     __shared__ float red[4];
     const int64_t row = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    float *prow = P + row * ldp;
+    // P == nullptr: signed image only, Pd = kept ? P/(1-p) : -P (the sign bit is the keep bit)
+    const bool sgn = P == nullptr;
+    float *prow = sgn ? nullptr : P + row * ldp;
     float *pdrow = Pd + row * ldp;
     uint32_t *krow = keep ? keep + row * ld_keep : nullptr;
     const bool write_pd = Pd != P;
     const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
     if (row >= rows_valid) {
         for (int64_t c = tid * 4; c < n_pad; c += 1024) {
-            *reinterpret_cast<float4 *>(prow + c) = z4;
+            if (!sgn) *reinterpret_cast<float4 *>(prow + c) = z4;
             if (write_pd) *reinterpret_cast<float4 *>(pdrow + c) = z4;
         }
         if (krow)
@@ -291,10 +293,10 @@ __global__ void __launch_bounds__(256) attn_softmax_kernel(const float *S, int64
         for (int j = 0; j < 4; ++j) {
             pv[j] = e[i][j] * inv;
             kp[j] = (p > 0.f) ? u2gnn_keep(seed, (uint32_t)row, (uint32_t)(c + j), p) : true;
-            pdv[j] = kp[j] ? pv[j] * ks : 0.f;
+            pdv[j] = kp[j] ? pv[j] * ks : (sgn ? -pv[j] : 0.f);
         }
         if (in) {
-            *reinterpret_cast<float4 *>(prow + c) = make_float4(pv[0], pv[1], pv[2], pv[3]);
+            if (!sgn) *reinterpret_cast<float4 *>(prow + c) = make_float4(pv[0], pv[1], pv[2], pv[3]);
             if (write_pd) *reinterpret_cast<float4 *>(pdrow + c) = make_float4(pdv[0], pdv[1], pdv[2], pdv[3]);
         }
         if (krow) {
@@ -636,8 +638,9 @@ int u2gnn_colsum(const float *X, int64_t rows, int64_t cols_pad, int64_t ld, int
 int u2gnn_attn_softmax_fwd(const float *S, int64_t lds, float *P, float *Pd, int64_t ldp, int64_t rows_valid,
                            int64_t rows_pad, int64_t n_valid, int64_t n_pad, float p, uint64_t seed, uint32_t *keep,
                            int64_t ld_keep, void *stream) {
-    if (!S || !P || !Pd || (n_pad & 3) || (lds & 3) || (ldp & 3) || n_valid > n_pad || n_valid < 1) return U2GNN_E_ARG;
+    if (!S || !Pd || (n_pad & 3) || (lds & 3) || (ldp & 3) || n_valid > n_pad || n_valid < 1) return U2GNN_E_ARG;
     if (Pd == P && p > 0.f) return U2GNN_E_ARG;
+    if (!P && keep) return U2GNN_E_ARG;   // signed image: the sign bit is the keep bit
     if (keep && ((n_pad & 31) || ld_keep < n_pad / 32)) return U2GNN_E_ARG;
     if (n_pad > 1024 * SM_RV_MAX) return U2GNN_E_SHAPE;   // rows are held in registers
     hipStream_t st = u2gnn_stream(stream);

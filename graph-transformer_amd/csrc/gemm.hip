@@ -57,7 +57,9 @@ __device__ __forceinline__ float4 ld4(const float *p) { return *reinterpret_cast
 // 4 columns.
 template <int EPI>
 __device__ __forceinline__ void epi_fetch(const GemmP &P, int row, int col, float4 &a, float4 &b, uint32_t &kb) {
-    if constexpr (EPI == U2GNN_EPI_ATTN_DS) {
+    if constexpr (EPI == U2GNN_EPI_ATTN_DS_SIGNED) {
+        a = ld4(P.aux0 + (int64_t)row * P.ld_aux + col);
+    } else if constexpr (EPI == U2GNN_EPI_ATTN_DS) {
         const int64_t o = (int64_t)row * P.ld_aux + col;
         a = ld4(P.aux0 + o);
         if (P.keep)
@@ -80,6 +82,15 @@ __device__ __forceinline__ float4 epilogue4(const GemmP &P, int row, int col, fl
                                             uint32_t kb, float dl) {
     if constexpr (EPI == U2GNN_EPI_STORE) {
         return make_float4(P.alpha * v.x, P.alpha * v.y, P.alpha * v.z, P.alpha * v.w);
+    } else if constexpr (EPI == U2GNN_EPI_ATTN_DS_SIGNED) {
+        // x = Pd = P/(1-p) where kept (sign clear), x = -P where dropped (sign set):
+        // dS = P*(keep*dPd/(1-p) - delta) = kept ? x*(dPd - (1-p)*delta) : x*delta
+        const float q = (1.f - P.p) * dl;
+        const float x[4] = {a.x, a.y, a.z, a.w}, g[4] = {v.x, v.y, v.z, v.w};
+        float o[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) o[c] = x[c] * ((__float_as_uint(x[c]) >> 31) ? dl : g[c] - q);
+        return make_float4(o[0], o[1], o[2], o[3]);
     } else if constexpr (EPI == U2GNN_EPI_ATTN_DS) {
         const float4 pr = a;
         if (P.keep) {   // dS = P * (keep * dPd / (1-p) - delta): 4 keep bits instead of 16 B of Pd
@@ -140,7 +151,7 @@ __device__ __forceinline__ void fetch_slice(const GemmP &P, int row, int c0, int
             e.kb[j][g] = 0;
             epi_fetch<EPI>(P, row, c0 + j * 32 + 8 * g + 4 * kh, e.a[j][g], e.b[j][g], e.kb[j][g]);
         }
-    e.dl = EPI == U2GNN_EPI_ATTN_DS ? P.rowvec[row] : 0.f;
+    e.dl = (EPI == U2GNN_EPI_ATTN_DS || EPI == U2GNN_EPI_ATTN_DS_SIGNED) ? P.rowvec[row] : 0.f;
 }
 
 template <int EPI, int TM, int TN>
@@ -255,10 +266,18 @@ __device__ __forceinline__ void g2r(const float *Ab, const float *Bb, int64_t ld
     }
 }
 
-template <int BM, int BN, int BK, int SA, int SB, bool TA, bool TB>
-__device__ __forceinline__ void r2s(float *As, float *Bs, int tid, const float4 (&ra)[BM * BK / 1024],
+// CLAMP: A elements below +0 are staged as 0 (the signed dropped-probability image read as Pd)
+__device__ __forceinline__ float4 clamp0(float4 v) {
+    return make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
+}
+
+template <int BM, int BN, int BK, int SA, int SB, bool TA, bool TB, bool CLAMP>
+__device__ __forceinline__ void r2s(float *As, float *Bs, int tid, const float4 (&ra_)[BM * BK / 1024],
                                     const float4 (&rb)[BN * BK / 1024]) {
     constexpr int NA = BM * BK / 1024, NB = BN * BK / 1024;
+    float4 ra[NA];
+#pragma unroll
+    for (int i = 0; i < NA; ++i) ra[i] = CLAMP ? clamp0(ra_[i]) : ra_[i];
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
         const int idx = tid + i * 256;
@@ -292,7 +311,7 @@ __device__ __forceinline__ void r2s(float *As, float *Bs, int tid, const float4 
 // ------------------------------------------------------------------------------------
 // fp32 MFMA kernel
 // ------------------------------------------------------------------------------------
-template <int BM, int BN, bool TA, bool TB, int EPI>
+template <int BM, int BN, bool TA, bool TB, int EPI, bool CLAMP>
 __global__ void __launch_bounds__(256) gemm_f32_kernel(GemmP P) {
     constexpr int BK = 16;
     constexpr int WTM = BM / 2, WTN = BN / 2;
@@ -333,7 +352,7 @@ __global__ void __launch_bounds__(256) gemm_f32_kernel(GemmP P) {
 
     if (nk > 0) {
         g2r<BM, BN, BK, TA, TB>(Ab, Bb, P.lda, P.ldb, 0, tid, ra, rb);
-        r2s<BM, BN, BK, SA, SB, TA, TB>(As0, Bs0, tid, ra, rb);
+        r2s<BM, BN, BK, SA, SB, TA, TB, CLAMP>(As0, Bs0, tid, ra, rb);
         __syncthreads();
     }
     for (int t = 0; t < nk; ++t) {
@@ -356,7 +375,7 @@ __global__ void __launch_bounds__(256) gemm_f32_kernel(GemmP P) {
                 for (int j = 0; j < TN; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(b[j], a[i], acc[i][j], 0, 0, 0);  // C^T map
         }
-        r2s<BM, BN, BK, SA, SB, TA, TB>(As0 + ((t + 1) & 1) * BK * SA, Bs0 + ((t + 1) & 1) * BK * SB, tid, ra, rb);
+        r2s<BM, BN, BK, SA, SB, TA, TB, CLAMP>(As0 + ((t + 1) & 1) * BK * SA, Bs0 + ((t + 1) & 1) * BK * SB, tid, ra, rb);
         __syncthreads();
     }
 
@@ -466,10 +485,18 @@ __device__ __forceinline__ void split2(float x0, float x1, unsigned &h, unsigned
     }
 }
 
-template <int R, int BK, int LDK, bool T, bool SPLIT, int NT>
-__device__ __forceinline__ void r2s_bf(__bf16 *hi, __bf16 *lo, int tid, const float4 (&v)[R * BK / (4 * NT)]) {
+template <int R, int BK, int LDK, bool T, bool SPLIT, int NT, bool CLAMP = false>
+__device__ __forceinline__ void r2s_bf(__bf16 *hi, __bf16 *lo, int tid, const float4 (&v_)[R * BK / (4 * NT)]) {
     constexpr int NF = R * BK / (4 * NT);
+    float4 v[NF];
+#pragma unroll
+    for (int i = 0; i < NF; ++i) v[i] = CLAMP ? clamp0(v_[i]) : v_[i];
 #ifdef U2GNN_EXP_NOSTAGE
+    return;
+#endif
+#ifdef U2GNN_EXP_NOWRITE   // experiment: loads kept, no split and no LDS write (upper bound of DMA staging)
+#pragma unroll
+    for (int i = 0; i < NF; ++i) asm volatile("" ::"v"(v[i].x), "v"(v[i].y), "v"(v[i].z), "v"(v[i].w));
     return;
 #endif
     if constexpr (!T) {
@@ -519,7 +546,7 @@ __device__ __forceinline__ bf16x8 ld_frag(const __bf16 *img, int r0, int ks, int
     }
 }
 
-template <int BM, int BN, int WM, int WN, int BK, bool TA, bool TB, int EPI, bool SPLIT>
+template <int BM, int BN, int WM, int WN, int BK, bool TA, bool TB, int EPI, bool SPLIT, bool CLAMP>
 __global__ void __launch_bounds__(64 * WM * WN) gemm_bf16_kernel(GemmP P) {
     constexpr int NT = 64 * WM * WN;
     constexpr int LDK = BK + 8;
@@ -603,21 +630,21 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_bf16_kernel(GemmP P) {
         g2r_bf<NFB>(rsB, voB, (0) * kstepB, rb0);
         g2r_bf<NFA>(rsA, voA, (min(1, nk - 1)) * kstepA, ra1);
         g2r_bf<NFB>(rsB, voB, (min(1, nk - 1)) * kstepB, rb1);
-        r2s_bf<BM, BK, LDK, TA, SPLIT, NT>(stage(0), stage(0) + AE, tid, ra0);
+        r2s_bf<BM, BK, LDK, TA, SPLIT, NT, CLAMP>(stage(0), stage(0) + AE, tid, ra0);
         r2s_bf<BN, BK, LDK, !TB, SPLIT, NT>(stage(0) + 2 * AE, stage(0) + 2 * AE + BE, tid, rb0);
         __syncthreads();
         for (int t = 0; t < nk; t += 2) {
             if constexpr (kStageA) g2r_bf<NFA>(rsA, voA, (min(t + 2, nk - 1)) * kstepA, ra0);
             if constexpr (kStageB) g2r_bf<NFB>(rsB, voB, (min(t + 2, nk - 1)) * kstepB, rb0);
             compute(stage(0));
-            if constexpr (kStageA) r2s_bf<BM, BK, LDK, TA, SPLIT, NT>(stage(1), stage(1) + AE, tid, ra1);
+            if constexpr (kStageA) r2s_bf<BM, BK, LDK, TA, SPLIT, NT, CLAMP>(stage(1), stage(1) + AE, tid, ra1);
             if constexpr (kStageB) r2s_bf<BN, BK, LDK, !TB, SPLIT, NT>(stage(1) + 2 * AE, stage(1) + 2 * AE + BE, tid, rb1);
             U2GNN_LOOP_SYNC();
             if (t + 1 < nk) {
                 if constexpr (kStageA) g2r_bf<NFA>(rsA, voA, (min(t + 3, nk - 1)) * kstepA, ra1);
                 if constexpr (kStageB) g2r_bf<NFB>(rsB, voB, (min(t + 3, nk - 1)) * kstepB, rb1);
                 compute(stage(1));
-                if constexpr (kStageA) r2s_bf<BM, BK, LDK, TA, SPLIT, NT>(stage(0), stage(0) + AE, tid, ra0);
+                if constexpr (kStageA) r2s_bf<BM, BK, LDK, TA, SPLIT, NT, CLAMP>(stage(0), stage(0) + AE, tid, ra0);
                 if constexpr (kStageB) r2s_bf<BN, BK, LDK, !TB, SPLIT, NT>(stage(0) + 2 * AE, stage(0) + 2 * AE + BE, tid, rb0);
                 U2GNN_LOOP_SYNC();
             }
@@ -634,21 +661,30 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_bf16_kernel(GemmP P) {
 // staging written after the barrier from one register set (+-2 %).
 template <int VAR> constexpr int CFG_BK = VAR == 1 ? 16 : 32;
 
-template <int KIND, int BM, int BN, int VAR, bool TA, bool TB, int EPI>
+template <int KIND, int BM, int BN, int VAR, bool TA, bool TB, int EPI, bool CLAMP = false>
 void launch_kernel(const GemmP &P, dim3 grid, hipStream_t st) {
     if constexpr (KIND == U2GNN_PREC_F32) {
-        hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, TA, TB, EPI>), grid, dim3(256), 0, st, P);
+        hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, TA, TB, EPI, CLAMP>), grid, dim3(256), 0, st, P);
     } else {
         constexpr int WM = BM == 256 ? 4 : 2, WN = 2;   // 256x128 tiles run 8 waves (4x2)
         hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, WM, WN, CFG_BK<VAR>, TA, TB, EPI,
-                                             KIND == U2GNN_PREC_BF16X3>),
+                                             KIND == U2GNN_PREC_BF16X3, CLAMP>),
                            grid, dim3(64 * WM * WN), 0, st, P);
     }
 }
 
 template <int KIND, int BM, int BN, int VAR, bool TA, bool TB>
-int launch_epi(const GemmP &P, int epi, int split, hipStream_t st) {
+int launch_epi(const GemmP &P, int epi, int split, bool clamp_a, hipStream_t st) {
     dim3 grid(P.gm * P.gn * split);
+    if (clamp_a) {   // the P.V / dV products over the signed probability image: STORE, B not transposed
+        if constexpr (TB) {
+            return U2GNN_E_ARG;
+        } else {
+            if (epi != U2GNN_EPI_STORE) return U2GNN_E_ARG;
+            launch_kernel<KIND, BM, BN, VAR, TA, TB, U2GNN_EPI_STORE, true>(P, grid, st);
+            return u2gnn_launch_status();
+        }
+    }
     switch (epi) {
 #define U2GNN_CASE(E)                                          \
     case E:                                                    \
@@ -661,6 +697,7 @@ int launch_epi(const GemmP &P, int epi, int split, hipStream_t st) {
         U2GNN_CASE(U2GNN_EPI_RELU_DROP_BWD)
         U2GNN_CASE(U2GNN_EPI_ACCUM)
         U2GNN_CASE(U2GNN_EPI_ATTN_DS)
+        U2GNN_CASE(U2GNN_EPI_ATTN_DS_SIGNED)
 #undef U2GNN_CASE
         default:
             return U2GNN_E_ARG;
@@ -669,21 +706,21 @@ int launch_epi(const GemmP &P, int epi, int split, hipStream_t st) {
 }
 
 template <int KIND, int BM, int BN, int VAR = 0>
-int launch_layout(const GemmP &P, bool ta, bool tb, int epi, int split, hipStream_t st) {
-    if (!ta && tb) return launch_epi<KIND, BM, BN, VAR, false, true>(P, epi, split, st);
-    if (!ta && !tb) return launch_epi<KIND, BM, BN, VAR, false, false>(P, epi, split, st);
-    if (ta && !tb) return launch_epi<KIND, BM, BN, VAR, true, false>(P, epi, split, st);
+int launch_layout(const GemmP &P, bool ta, bool tb, int epi, int split, bool clamp_a, hipStream_t st) {
+    if (!ta && tb) return launch_epi<KIND, BM, BN, VAR, false, true>(P, epi, split, clamp_a, st);
+    if (!ta && !tb) return launch_epi<KIND, BM, BN, VAR, false, false>(P, epi, split, clamp_a, st);
+    if (ta && !tb) return launch_epi<KIND, BM, BN, VAR, true, false>(P, epi, split, clamp_a, st);
     return U2GNN_E_ARG;  // A^T B^T is never needed by the encoder
 }
 
 template <int KIND>
-int launch_tile(const GemmP &P, int tile, bool ta, bool tb, int epi, int split, hipStream_t st) {
+int launch_tile(const GemmP &P, int tile, bool ta, bool tb, int epi, int split, bool clamp_a, hipStream_t st) {
     if constexpr (KIND != U2GNN_PREC_F32) {
-        if (tile == 256) return launch_layout<KIND, 256, 128>(P, ta, tb, epi, split, st);
-        if (tile == 129) return launch_layout<KIND, 128, 128, 1>(P, ta, tb, epi, split, st);
+        if (tile == 256) return launch_layout<KIND, 256, 128>(P, ta, tb, epi, split, clamp_a, st);
+        if (tile == 129) return launch_layout<KIND, 128, 128, 1>(P, ta, tb, epi, split, clamp_a, st);
     }
-    if (tile == 128) return launch_layout<KIND, 128, 128>(P, ta, tb, epi, split, st);
-    return launch_layout<KIND, 64, 64>(P, ta, tb, epi, split, st);
+    if (tile == 128) return launch_layout<KIND, 128, 128>(P, ta, tb, epi, split, clamp_a, st);
+    return launch_layout<KIND, 64, 64>(P, ta, tb, epi, split, clamp_a, st);
 }
 
 inline bool al16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
@@ -693,7 +730,7 @@ inline bool al16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) =
 extern "C" int u2gnn_gemm(const u2gnn_gemm_args *a, void *stream) {
     if (!a || !a->A || !a->B || !a->C) return U2GNN_E_ARG;
     if (a->M <= 0 || a->N <= 0 || a->K <= 0) return U2GNN_E_ARG;
-    if (a->epilogue < 0 || a->epilogue > U2GNN_EPI_ATTN_DS) return U2GNN_E_ARG;
+    if (a->epilogue < 0 || a->epilogue > U2GNN_EPI_ATTN_DS_SIGNED) return U2GNN_E_ARG;
     const int prec = a->precision;
     if (prec != U2GNN_PREC_F32 && prec != U2GNN_PREC_BF16X3 && prec != U2GNN_PREC_BF16) return U2GNN_E_ARG;
     const int split = a->split_k < 1 ? 1 : a->split_k;
@@ -713,8 +750,11 @@ extern "C" int u2gnn_gemm(const u2gnn_gemm_args *a, void *stream) {
     const int e = a->epilogue;
     if ((e == U2GNN_EPI_BIAS || e == U2GNN_EPI_BIAS_DROP_RESID || e == U2GNN_EPI_BIAS_RELU_DROP) && !a->bias)
         return U2GNN_E_ARG;
-    if ((e == U2GNN_EPI_BIAS_DROP_RESID || e == U2GNN_EPI_RELU_DROP_BWD || e == U2GNN_EPI_ATTN_DS) && !a->aux0)
+    if ((e == U2GNN_EPI_BIAS_DROP_RESID || e == U2GNN_EPI_RELU_DROP_BWD || e == U2GNN_EPI_ATTN_DS ||
+         e == U2GNN_EPI_ATTN_DS_SIGNED) && !a->aux0)
         return U2GNN_E_ARG;
+    if (e == U2GNN_EPI_ATTN_DS_SIGNED && (!a->rowvec || !(a->p_drop < 1.f))) return U2GNN_E_ARG;
+    if (a->clamp_a && (e != U2GNN_EPI_STORE || a->trans_b)) return U2GNN_E_ARG;
     if (e == U2GNN_EPI_ATTN_DS && ((!a->aux1 && !a->keep) || !a->rowvec)) return U2GNN_E_ARG;
     if (e == U2GNN_EPI_ATTN_DS && a->keep && (a->ld_keep * 32 < a->N || !(a->p_drop < 1.f))) return U2GNN_E_ARG;
     int tile = a->tile;
@@ -759,7 +799,8 @@ extern "C" int u2gnn_gemm(const u2gnn_gemm_args *a, void *stream) {
     P.ld_keep = a->ld_keep;
     hipStream_t st = u2gnn_stream(stream);
     const bool ta = a->trans_a != 0, tb = a->trans_b != 0;
-    if (prec == U2GNN_PREC_BF16X3) return launch_tile<U2GNN_PREC_BF16X3>(P, tile, ta, tb, e, split, st);
-    if (prec == U2GNN_PREC_BF16) return launch_tile<U2GNN_PREC_BF16>(P, tile, ta, tb, e, split, st);
-    return launch_tile<U2GNN_PREC_F32>(P, tile, ta, tb, e, split, st);
+    const bool clamp = a->clamp_a != 0;
+    if (prec == U2GNN_PREC_BF16X3) return launch_tile<U2GNN_PREC_BF16X3>(P, tile, ta, tb, e, split, clamp, st);
+    if (prec == U2GNN_PREC_BF16) return launch_tile<U2GNN_PREC_BF16>(P, tile, ta, tb, e, split, clamp, st);
+    return launch_tile<U2GNN_PREC_F32>(P, tile, ta, tb, e, split, clamp, st);
 }

@@ -28,7 +28,9 @@ class U2GNNNativeError(RuntimeError):
 U2GNN_OK = 0
 ERRORS = {-1: "bad argument", -2: "misaligned pointer / leading dimension", -3: "shape not a tile multiple"}
 
-EPI_STORE, EPI_BIAS, EPI_BIAS_DROP_RESID, EPI_BIAS_RELU_DROP, EPI_RELU_DROP_BWD, EPI_ACCUM, EPI_ATTN_DS = range(7)
+EPI_STORE, EPI_BIAS, EPI_BIAS_DROP_RESID, EPI_BIAS_RELU_DROP, EPI_RELU_DROP_BWD, EPI_ACCUM, EPI_ATTN_DS, \
+    EPI_ATTN_DS_SIGNED = range(8)
+ABI_VERSION = 2   # include/u2gnn_hip.h U2GNN_ABI_VERSION
 PREC_F32, PREC_BF16X3, PREC_BF16 = 0, 1, 2
 
 
@@ -49,6 +51,7 @@ class GemmArgs(ctypes.Structure):
         ("precision", c_int32),
         ("tile", c_int32),
         ("keep", c_void_p), ("ld_keep", c_int64),
+        ("clamp_a", c_int32), ("reserved", c_int32),
     ]
 
 
@@ -154,8 +157,8 @@ def hip_lib():
             raise U2GNNNativeError(f"cannot load {HIP_LIB_PATH}: {e}") from e
         _hip = _bind(lib, _HIP_SIGS)
         v = _hip.u2gnn_abi_version()
-        if v != 1:
-            raise U2GNNNativeError(f"ABI mismatch: library {v}, binding 1")
+        if v != ABI_VERSION:
+            raise U2GNNNativeError(f"ABI mismatch: library {v}, binding {ABI_VERSION}")
     return _hip
 
 

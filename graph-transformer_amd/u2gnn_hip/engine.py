@@ -12,7 +12,8 @@ reference output (slots 1..k never reach the output) at 1/(k+1) of the reference
 Layouts in HBM (fp32, row-major): node rows padded to Np = row_pad(N) (a multiple of 128, of 256
 from 1024 rows on), feature columns
 to dp = roundup(d, 64), FFN width to ffp = roundup(ff, 64); QKV is one [Np, 3*dp] buffer
-(Q pre-scaled by 1/sqrt(d)); attention probabilities P and the dropped Pd are [Np, Np].
+(Q pre-scaled by 1/sqrt(d)); the attention probabilities are one [Np, Np] image (with dropout the
+signed one: P/(1-p) where kept, -P where dropped).
 Padding rows/columns hold zeros in every activation and gradient the encoder produces
 (invariant relied upon by the GEMMs, which run on the padded shapes without masks).
 """
@@ -136,7 +137,7 @@ class PackedLayer:
 
 
 class EncoderLayerCtx:
-    __slots__ = ("X", "QKV", "P", "Pd", "O", "keep", "Z1", "X1", "mean1", "rstd1", "Hd", "Z2", "mean2", "rstd2",
+    __slots__ = ("X", "QKV", "Pd", "O", "Z1", "X1", "mean1", "rstd1", "Hd", "Z2", "mean2", "rstd2",
                  "seeds")
 
 
@@ -192,12 +193,13 @@ class OffPath:
 
 
 def _gemm_split(A, B, C, M, N, Kd, lda, ldb, ldc, trans_a=False, trans_b=False, alpha=1.0, accumulate=False,
-                prec="fp32", rblk=None, cblk=None, target=448, flops=None, deep=False):
+                prec="fp32", rblk=None, cblk=None, target=448, flops=None, deep=False, clamp_a=False):
     """C (+)= alpha * op(A) . op(B) with deterministic split-K: when the tile grid alone would
     leave most of the 256 CUs idle (skinny outputs with a deep node dimension: P.V, Pd^T.dO,
     dS.K, dS^T.Q, the weight gradients, dH.W1, dQKV.W_in), the depth is cut into fp32 slabs
     (>= 4 K-tiles each, ~target workgroups) and one streaming pass sums them into C — applying
-    alpha, accumulation and an optional padded->real block map (rblk, cblk)."""
+    alpha, accumulation and an optional padded->real block map (rblk, cblk).  clamp_a: A is the
+    signed probability image (read as Pd)."""
     bk = 16 if prec == "fp32" else 32
     if prec != "fp32" and M % 256 == 0 and N % 128 == 0 and (M // 256) * (N // 128) >= 32:
         # 256x128 blocks (8 waves, one block per CU): the skinny attention products
@@ -213,11 +215,12 @@ def _gemm_split(A, B, C, M, N, Kd, lda, ldb, ldc, trans_a=False, trans_b=False, 
     mapped = rblk is not None
     if split == 1 and not mapped:
         K.gemm(A, B, C, M, N, Kd, lda, ldb, ldc, trans_a=trans_a, trans_b=trans_b, alpha=alpha,
-               epilogue=E.EPI_ACCUM if accumulate else E.EPI_STORE, precision=prec, tile=t, flops=flops)
+               epilogue=E.EPI_ACCUM if accumulate else E.EPI_STORE, precision=prec, tile=t, flops=flops,
+               clamp_a=clamp_a)
         return
     slabs = torch.empty(split, M, N, device=C.device, dtype=torch.float32)
     K.gemm(A, B, slabs, M, N, Kd, lda, ldb, N, trans_a=trans_a, trans_b=trans_b, split_k=split, slab_stride=M * N,
-           precision=prec, tile=t, flops=flops)
+           precision=prec, tile=t, flops=flops, clamp_a=clamp_a)
     K.slab_reduce(slabs, split, M * N, M, N, N, rblk or (M, M), cblk or (N, N), C, ldc, alpha=alpha,
                   accumulate=accumulate)
 
@@ -233,9 +236,11 @@ def _bias_grad(dY, rows, cols_pad, ld, cblk, out):
     K.colsum(dY, rows, cols_pad, ld, cblk, out, ws)
 
 
-def _gemm_nodes_k(A, B, C, M, N, Kd, lda, ldb, ldc, trans_a=False, alpha=1.0, prec="fp32", flops=None):
+def _gemm_nodes_k(A, B, C, M, N, Kd, lda, ldb, ldc, trans_a=False, alpha=1.0, prec="fp32", flops=None,
+                  clamp_a=False):
     """The skinny attention products whose depth is the node dimension (N = dp, K = Np)."""
-    _gemm_split(A, B, C, M, N, Kd, lda, ldb, ldc, trans_a=trans_a, alpha=alpha, prec=prec, flops=flops)
+    _gemm_split(A, B, C, M, N, Kd, lda, ldb, ldc, trans_a=trans_a, alpha=alpha, prec=prec, flops=flops,
+                clamp_a=clamp_a)
 
 
 def encoder_layer_forward(X: torch.Tensor, w: PackedLayer, p: LayerParams, dims: Dims, train: bool,
@@ -256,14 +261,13 @@ def encoder_layer_forward(X: torch.Tensor, w: PackedLayer, p: LayerParams, dims:
     S = torch.empty(Np, Np, device=dev, dtype=f32)
     K.gemm(Q, Kt, S, Np, Np, dp, 3 * dp, 3 * dp, Np, trans_b=True, precision=prec, flops=att,
            tile=256 if (prec != "fp32" and Np % 256 == 0) else 0)
-    P = torch.empty(Np, Np, device=dev, dtype=f32)
-    Pd = torch.empty(Np, Np, device=dev, dtype=f32) if pd > 0 else P
-    # keep bits for the backward's dS epilogue (3 MB instead of re-reading the 95 MB Pd)
-    keep = torch.empty(Np, Np // 32, device=dev, dtype=torch.int32) if (pd > 0 and need_ctx) else None
-    K.attn_softmax_fwd(S, Np, P, Pd, Np, N, Np, N, Np, pd, seeds.get(SITE_ATTN, 0), keep=keep)
+    # one [Np, Np] image: with dropout the signed one (P/(1-p) where kept, -P where dropped), which
+    # P.V and dP^T.dO read as Pd (negatives staged as 0) and the dS epilogue reads as P and keep
+    Pd = torch.empty(Np, Np, device=dev, dtype=f32)
+    K.attn_softmax_fwd(S, Np, None if pd > 0 else Pd, Pd, Np, N, Np, N, Np, pd, seeds.get(SITE_ATTN, 0))
     del S
     O = torch.empty(Np, dp, device=dev, dtype=f32)
-    _gemm_nodes_k(Pd, V, O, Np, dp, Np, Np, 3 * dp, dp, prec=prec, flops=att)
+    _gemm_nodes_k(Pd, V, O, Np, dp, Np, Np, 3 * dp, dp, prec=prec, flops=att, clamp_a=pd > 0)
     Z1 = torch.empty(Np, dp, device=dev, dtype=f32)
     K.gemm(O, w.W_o, Z1, Np, dp, dp, dp, dp, dp, trans_b=True, epilogue=E.EPI_BIAS_DROP_RESID, bias=w.b_o,
            aux0=X, ld_aux=dp, p_drop=pd, seed=seeds.get(SITE_DROP1, 0), precision=prec, flops=2.0 * N * d * d)
@@ -284,7 +288,7 @@ def encoder_layer_forward(X: torch.Tensor, w: PackedLayer, p: LayerParams, dims:
     ctx = None
     if need_ctx:
         ctx = EncoderLayerCtx()
-        ctx.X, ctx.QKV, ctx.P, ctx.Pd, ctx.O, ctx.keep = X, QKV, P, Pd, O, keep
+        ctx.X, ctx.QKV, ctx.Pd, ctx.O = X, QKV, Pd, O
         ctx.Z1, ctx.X1, ctx.mean1, ctx.rstd1, ctx.Hd = Z1, X1, mean1, rstd1, Hd
         ctx.Z2, ctx.mean2, ctx.rstd2 = Z2, mean2, rstd2
         ctx.seeds = (pd, dict(seeds))
@@ -344,11 +348,11 @@ def encoder_layer_backward(dX2: torch.Tensor, ctx: EncoderLayerCtx, w: PackedLay
     delta = torch.empty(Np, device=dev, dtype=f32)
     K.rowdot(dO, dp, ctx.O, dp, delta, Np, dp)
     dS = torch.empty(Np, Np, device=dev, dtype=f32)
-    K.gemm(dO, V, dS, Np, Np, dp, dp, 3 * dp, Np, trans_b=True, epilogue=E.EPI_ATTN_DS, aux0=ctx.P,
-           aux1=ctx.Pd if ctx.keep is None else None, keep=ctx.keep, p_drop=pd, rowvec=delta, ld_aux=Np,
-           precision=prec, flops=att)
+    K.gemm(dO, V, dS, Np, Np, dp, dp, 3 * dp, Np, trans_b=True, epilogue=E.EPI_ATTN_DS_SIGNED, aux0=ctx.Pd,
+           p_drop=pd, rowvec=delta, ld_aux=Np, precision=prec, flops=att)
     dQKV = torch.empty(Np, 3 * dp, device=dev, dtype=f32)
-    _gemm_nodes_k(ctx.Pd, dO, dQKV[:, 2 * dp:], Np, dp, Np, Np, dp, 3 * dp, trans_a=True, prec=prec, flops=att)
+    _gemm_nodes_k(ctx.Pd, dO, dQKV[:, 2 * dp:], Np, dp, Np, Np, dp, 3 * dp, trans_a=True, prec=prec, flops=att,
+                  clamp_a=pd > 0)
     _gemm_nodes_k(dS, Kt, dQKV[:, :dp], Np, dp, Np, Np, 3 * dp, 3 * dp, alpha=1.0 / math.sqrt(d), prec=prec,
                   flops=att)
     _gemm_nodes_k(dS, Q, dQKV[:, dp:2 * dp], Np, dp, Np, Np, 3 * dp, 3 * dp, trans_a=True, prec=prec, flops=att)

@@ -48,29 +48,31 @@ class LaunchRecorder:
 
 
 REC = LaunchRecorder()
-_EPI_NAMES = ["STORE", "BIAS", "BIAS_DROP_RESID", "BIAS_RELU_DROP", "RELU_DROP_BWD", "ACCUM", "ATTN_DS"]
+_EPI_NAMES = ["STORE", "BIAS", "BIAS_DROP_RESID", "BIAS_RELU_DROP", "RELU_DROP_BWD", "ACCUM", "ATTN_DS",
+              "ATTN_DS_SIGNED"]
 
 
-def gemm_symbol(precision, M, N, split_k, tile, trans_a, trans_b, epilogue):
+def gemm_symbol(precision, M, N, split_k, tile, trans_a, trans_b, epilogue, clamp_a=False):
     """Mirror of the C dispatcher's kernel choice (gemm.hip u2gnn_gemm) -> template symbol."""
     if tile == 0:
         can128 = M % 128 == 0 and N % 128 == 0
         tile = 128 if (can128 and (M // 128) * (N // 128) * max(split_k, 1) >= 480) else 64
     b = lambda x: "true" if x else "false"  # noqa: E731
     if precision == "fp32":
-        return f"gemm_f32_kernel<{tile}, {tile}, {b(trans_a)}, {b(trans_b)}, {int(epilogue)}>"
+        return f"gemm_f32_kernel<{tile}, {tile}, {b(trans_a)}, {b(trans_b)}, {int(epilogue)}, {b(clamp_a)}>"
     # "256" = 256x128 block (4x2 waves); "129" = 128x128 block with a 16-deep K step
     bm, bn, wm, bk = {256: (256, 128, 4, 32), 129: (128, 128, 2, 16)}.get(tile, (tile, tile, 2, 32))
     return (f"gemm_bf16_kernel<{bm}, {bn}, {wm}, 2, {bk}, {b(trans_a)}, {b(trans_b)}, {int(epilogue)}, "
-            f"{b(precision == 'bf16x3')}>")   # the C++ template instance as rocprofv3 names it
+            f"{b(precision == 'bf16x3')}, {b(clamp_a)}>")   # the C++ template instance as rocprofv3 names it
 
 
 def gemm(A, B, C, M, N, K, lda, ldb, ldc, trans_a=False, trans_b=False, epilogue=_lib.EPI_STORE, split_k=1,
          slab_stride=0, bias=None, aux0=None, aux1=None, rowvec=None, ld_aux=0, alpha=1.0, scale_cols=0, p_drop=0.0,
-         seed=0, precision="fp32", tile=0, flops=None, keep=None):
+         seed=0, precision="fp32", tile=0, flops=None, keep=None, clamp_a=False):
     """C[M,N] (epilogue) sum_k A(m,k) B(k,n).  A/B/C may be views (pointer arithmetic via
     storage offsets is done by torch's data_ptr()).  ``flops``: algorithmic FLOPs of the
-    launch for the roofline recorder (None = not recorded)."""
+    launch for the roofline recorder (None = not recorded).  ``clamp_a``: A elements below +0 are read
+    as 0 (the signed probability image of attn_softmax_fwd(P=None) consumed as Pd)."""
     _dev(A, B, C)
     rec = REC.enabled and flops is not None
     if rec:
@@ -97,10 +99,11 @@ def gemm(A, B, C, M, N, K, lda, ldb, ldc, trans_a=False, trans_b=False, epilogue
     if keep is not None:   # ATTN_DS: dropout keep bits (attn_softmax_fwd) instead of Pd
         _dev(keep)
         a.keep, a.ld_keep = keep.data_ptr(), keep.stride(0)
+    a.clamp_a = int(bool(clamp_a))
     check(hip_lib().u2gnn_gemm(ctypes.byref(a), _s()), "u2gnn_gemm")
     if rec:
         ev1.record()
-        REC.records.append((gemm_symbol(precision, M, N, split_k, tile, trans_a, trans_b, epilogue), float(flops),
+        REC.records.append((gemm_symbol(precision, M, N, split_k, tile, trans_a, trans_b, epilogue, clamp_a), float(flops),
                             ev0, ev1))
 
 
@@ -140,8 +143,9 @@ def colsum(X, rows, cols_pad, ld, cblk, out, ws, accumulate=False):
 
 
 def attn_softmax_fwd(S, lds, P, Pd, ldp, rows_valid, rows_pad, n_valid, n_pad, p, seed, keep=None):
-    """keep: optional int32 [rows_pad, >= n_pad/32] receiving the dropout keep bits."""
-    _dev(S, P, Pd, *([keep] if keep is not None else []))
+    """keep: optional int32 [rows_pad, >= n_pad/32] receiving the dropout keep bits.  P=None: Pd receives
+    the signed image (P/(1-p) where kept, -P where dropped)."""
+    _dev(S, Pd, *([t for t in (P, keep) if t is not None]))
     check(hip_lib().u2gnn_attn_softmax_fwd(_p(S), int(lds), _p(P), _p(Pd), int(ldp), int(rows_valid), int(rows_pad),
                                            int(n_valid), int(n_pad), float(p), int(seed), _p(keep),
                                            int(keep.stride(0)) if keep is not None else 0, _s()),

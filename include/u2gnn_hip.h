@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define U2GNN_ABI_VERSION 1
+#define U2GNN_ABI_VERSION 2
 
 #define U2GNN_OK 0
 #define U2GNN_E_ARG (-1)    /* bad size / null pointer */
@@ -43,6 +43,9 @@ extern "C" {
 #define U2GNN_EPI_ACCUM 5           /* C = C + alpha*acc                                  */
 #define U2GNN_EPI_ATTN_DS 6         /* C = aux1[m,n]*acc - aux0[m,n]*rowvec[m]; with keep:
                                        C = aux0[m,n]*(keep(m,n) ? acc/(1-p_drop) : 0 - rowvec[m]) */
+#define U2GNN_EPI_ATTN_DS_SIGNED 7  /* aux0 = x, the signed probability image of
+                                       u2gnn_attn_softmax_fwd (P == NULL): C = x*(acc - (1-p)*rowvec[m])
+                                       where x >= +0 (kept), C = x*rowvec[m] where x <= -0 (dropped) */
 
 /* Matrix-core precision of a GEMM (u2gnn_gemm_args.precision). */
 #define U2GNN_PREC_F32 0    /* v_mfma_f32_32x32x2_f32: exact fp32 fma chains            */
@@ -78,6 +81,9 @@ typedef struct u2gnn_gemm_args {
                              keep[m*ld_keep + n/32]) written by u2gnn_attn_softmax_fwd, or NULL
                              (then aux1 = Pd is read) */
     int64_t ld_keep;      /* words per row of keep */
+    int32_t clamp_a;      /* 1: A elements below +0 are read as 0 (the signed probability image as Pd
+                             for P.V and dP^T.dO); STORE epilogue and trans_b = 0 only */
+    int32_t reserved;
 } u2gnn_gemm_args;
 
 /* ---- library ------------------------------------------------------------------ */
@@ -129,7 +135,9 @@ int u2gnn_colsum(const float *X, int64_t rows, int64_t cols_pad, int64_t ld, int
 
 /* ---- a3.2: attention row softmax + dropout(p) on probabilities (MHA core) ----------
  * P[i,j] = softmax_j(S[i,j], j < n_valid); Pd = P * keep / (1-p); rows >= rows_valid -> 0.
- * Pd may alias P when p == 0.  keep (optional, n_pad % 32 == 0): the keep decisions as bits,
+ * Pd may alias P when p == 0.  P == NULL selects the signed image: Pd = P/(1-p) where kept and
+ * -P where dropped (the sign bit carries the keep decision; keep must then be NULL), consumed by
+ * the clamp_a GEMMs and U2GNN_EPI_ATTN_DS_SIGNED.  keep (optional, n_pad % 32 == 0): the keep decisions as bits,
  * bit j%32 of keep[i*ld_keep + j/32] (0 for j >= n_valid and padded rows), for the ATTN_DS
  * epilogue of the backward.  Rows are held in registers: n_pad <= 32768 (else U2GNN_E_SHAPE). */
 int u2gnn_attn_softmax_fwd(const float *S, int64_t lds, float *P, float *Pd, int64_t ldp,

@@ -189,6 +189,61 @@ def test_attn_ds_epilogue_with_keep_bits(prec):
     assert rel_err(C2, C1) < 1e-5
 
 
+@pytest.mark.parametrize("Np,N,p", [(1280, 1100, 0.5), (256, 230, 0.3), (9216, 9000, 0.5), (512, 500, 0.0)])
+def test_attn_softmax_signed_image(Np, N, p):
+    """P=None: one image, P/(1-p) where kept and -P where dropped (the sign bit is the keep bit,
+    -0.0 for a dropped exact zero); bitwise equal to the two-buffer outputs elsewhere."""
+    S = _mk(Np, Np, seed=23)
+    P, Pd = torch.empty(Np, Np, device=DEV), torch.empty(Np, Np, device=DEV)
+    K.attn_softmax_fwd(S, Np, P, Pd if p > 0 else P, Np, N, Np, N, Np, p, 77)
+    X = torch.full((Np, Np), float("nan"), device=DEV)
+    K.attn_softmax_fwd(S, Np, None if p > 0 else X, X, Np, N, Np, N, Np, p, 77)
+    if p == 0:
+        assert torch.equal(X, P)
+        return
+    mask = K.dropout_mask(77, Np, Np, p).bool()
+    sign = torch.signbit(X)
+    assert torch.equal(sign[:N, :N], ~mask[:N, :N])
+    assert torch.equal(X[mask], Pd[mask])
+    assert torch.equal(-X[~mask], P[~mask])
+    assert X[N:].abs().max().item() == 0 and X[:, N:].abs().max().item() == 0
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16x3"])
+@pytest.mark.parametrize("tile", [0, 256])
+def test_clamp_a_and_signed_ds_epilogue(prec, tile):
+    """The P.V / dP^T.dO products over the signed image (clamp_a) equal the products over Pd, and
+    the ATTN_DS_SIGNED epilogue equals P * (keep * acc / (1-p) - delta)."""
+    if prec == "fp32" and tile == 256:
+        pytest.skip("256 tile is a bf16 mode")
+    Np, N, dp, p = 512, 470, 128, 0.3
+    S = _mk(Np, Np, seed=41)
+    P, Pd, X = (torch.empty(Np, Np, device=DEV) for _ in range(3))
+    K.attn_softmax_fwd(S, Np, P, Pd, Np, N, Np, N, Np, p, 9)
+    K.attn_softmax_fwd(S, Np, None, X, Np, N, Np, N, Np, p, 9)
+    V = _mk(Np, dp, seed=42)
+    for ta in (False, True):
+        O1, O2 = torch.empty(Np, dp, device=DEV), torch.empty(Np, dp, device=DEV)
+        K.gemm(Pd, V, O1, Np, dp, Np, Np, dp, dp, trans_a=ta, precision=prec, tile=tile)
+        K.gemm(X, V, O2, Np, dp, Np, Np, dp, dp, trans_a=ta, precision=prec, tile=tile, clamp_a=True)
+        assert torch.equal(O1, O2)
+        S3 = torch.empty(2, Np, dp, device=DEV)
+        K.gemm(X, V, S3, Np, dp, Np, Np, dp, dp, trans_a=ta, precision=prec, tile=tile, clamp_a=True, split_k=2,
+               slab_stride=Np * dp)
+        assert rel_err(S3.sum(0), O1) < 1e-6
+    dO = _mk(Np, dp, seed=43)
+    acc = dO @ V.t()
+    dl = _mk(Np, seed=44)
+    C = torch.empty(Np, Np, device=DEV)
+    K.gemm(dO, V, C, Np, Np, dp, dp, dp, Np, trans_b=True, epilogue=_lib.EPI_ATTN_DS_SIGNED, aux0=X, p_drop=p,
+           rowvec=dl, ld_aux=Np, precision=prec, tile=tile)
+    keep = K.dropout_mask(9, Np, Np, p).float()
+    ref = P * (keep * acc / (1 - p) - dl[:, None])
+    assert rel_err(C, ref) < (1e-5 if prec == "fp32" else 3e-5)
+    with pytest.raises(_lib.U2GNNNativeError):   # clamp_a only with STORE and B not transposed
+        K.gemm(dO, V, C, Np, Np, dp, dp, dp, Np, trans_b=True, precision=prec, clamp_a=True)
+
+
 def test_layernorm_fwd_bwd():
     Np, N, d, dp = 128, 100, 67, 128
     Z = _mk(Np, dp, seed=11)

@@ -14,6 +14,8 @@ SHAPES = [  # name, M, N, K, ta, tb, [(split, tile), ...] (tile 129 = 128x128 wi
     ("dS    NT", Np, Np, dp, False, True, [(1, 128), (1, 256)], 6),   # dO.V^T, attention-dS epilogue (Pd)
     ("dSkb  NT", Np, Np, dp, False, True, [(1, 128), (1, 256)], 7),   # same, dropout keep bits instead of Pd
     ("P.V   NN", Np, dp, Np, False, False, [(4, 128), (4, 256), (4, 129)]),
+    ("P.Vc  NN", Np, dp, Np, False, False, [(4, 256)], 8),   # A = signed probability image (clamp_a)
+    ("dVc   TN", Np, dp, Np, True, False, [(4, 256)], 8),
     ("dV    TN", Np, dp, Np, True, False, [(4, 128), (4, 256), (4, 129)]),
     ("dWin  TN", 3 * dp, dp, Np, True, False, [(8, 128), (8, 129), (16, 129)]),
     ("dW1   TN", ffp, dp, Np, True, False, [(16, 128), (16, 129)]),
@@ -54,9 +56,13 @@ def run(prec):
                 ext["bias"] = torch.randn(N, device="cuda", generator=g)
             if epi in (2, 4):
                 ext["aux0"] = torch.randn(M, N, device="cuda", generator=g)
+        if epi == 8:
+            ext, epi = dict(clamp_a=True), 0
         if ONLY and not any(name.startswith(o) for o in ONLY.split(",")):
             continue
         A = torch.randn(Kd, M, device="cuda", generator=g) if ta else torch.randn(M, Kd, device="cuda", generator=g)
+        if ext.get("clamp_a"):
+            ref_a = A.clamp(min=0)
         B = torch.randn(N, Kd, device="cuda", generator=g) if tb else torch.randn(Kd, N, device="cuda", generator=g)
         for split, tile in cfgs:
             if prec == "fp32" and tile == 256:
@@ -74,7 +80,8 @@ def run(prec):
             e.record()
             torch.cuda.synchronize()
             us = s.elapsed_time(e) / REPS * 1e3
-            ref = (A.t() if ta else A).double() @ (B.t() if tb else B).double()
+            A_ = ref_a if ext.get("clamp_a") else A
+            ref = (A_.t() if ta else A_).double() @ (B.t() if tb else B).double()
             if epi in (1, 2, 3, 4):   # dropout epilogues: timing only
                 ref = None
             elif epi == 6:

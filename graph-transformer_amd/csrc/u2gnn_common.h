@@ -15,19 +15,26 @@ static inline int u2gnn_launch_status() {
 static inline hipStream_t u2gnn_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }
 
 // ---------------------------------------------------------------------------------------
-// Dropout: counter-based keep decision.  keep(seed, i, j) = U(seed, i, j) >= p with U a
-// 24-bit uniform from a splitmix64 finaliser of (seed + (i<<32|j) * golden).  The same
-// (seed, i, j) regenerates the mask in backward, so masks are never stored.
+// Dropout: counter-based keep decision.  keep(seed, i, j) = U(seed, i, j) >= p with U the top 24
+// bits of a murmur3 32-bit finaliser of (rowkey(seed, i) + j * golden); rowkey folds both seed
+// halves and the row through the same finaliser.  32-bit integer work only (~12 VALU per element
+// once the row key is hoisted, vs ~35 for a 64-bit splitmix): the N^2 attention dropout is the
+// largest consumer.  The same (seed, i, j) regenerates the mask in backward; nothing is stored.
 // ---------------------------------------------------------------------------------------
-__device__ __forceinline__ uint64_t u2gnn_mix64(uint64_t z) {
-    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
-    z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
-    return z ^ (z >> 31);
+__device__ __forceinline__ uint32_t u2gnn_fmix32(uint32_t h) {
+    h ^= h >> 16;
+    h *= 0x85ebca6bu;
+    h ^= h >> 13;
+    h *= 0xc2b2ae35u;
+    return h ^ (h >> 16);
+}
+
+__device__ __forceinline__ uint32_t u2gnn_row_key(uint64_t seed, uint32_t i) {
+    return u2gnn_fmix32((uint32_t)seed ^ u2gnn_fmix32((uint32_t)(seed >> 32) ^ u2gnn_fmix32(i + 0x9E3779B9u)));
 }
 
 __device__ __forceinline__ bool u2gnn_keep(uint64_t seed, uint32_t i, uint32_t j, float p) {
-    const uint64_t x = seed + ((((uint64_t)i) << 32) | (uint64_t)j) * 0x9E3779B97F4A7C15ULL;
-    const uint32_t u = (uint32_t)(u2gnn_mix64(x) >> 40);  // 24 bits
+    const uint32_t u = u2gnn_fmix32(u2gnn_row_key(seed, i) + j * 0x9E3779B9u) >> 8;   // 24 bits
     return (float)u * (1.0f / 16777216.0f) >= p;
 }
 

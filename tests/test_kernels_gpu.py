@@ -244,6 +244,24 @@ def test_clamp_a_and_signed_ds_epilogue(prec, tile):
         K.gemm(dO, V, C, Np, Np, dp, dp, dp, Np, trans_b=True, precision=prec, clamp_a=True)
 
 
+def test_dropout_mask_statistics():
+    """The counter-based keep decision: rate 1-p, no correlation between neighbouring rows, columns
+    or seeds (the masks of the attention dropout are 2-D slices of this stream)."""
+    R = C = 2048
+    for p in (0.1, 0.5, 0.9):
+        m = K.dropout_mask(1234, R, C, p).float()
+        assert abs(m.mean().item() - (1 - p)) < 0.003
+    m = K.dropout_mask(1234, R, C, 0.5).float() - 0.5
+    m2 = K.dropout_mask(1235, R, C, 0.5).float() - 0.5
+
+    def corr(a, b):
+        return ((a * b).mean() / (a.std() * b.std())).abs().item()
+    assert corr(m[:, 1:], m[:, :-1]) < 0.01
+    assert corr(m[1:], m[:-1]) < 0.01
+    assert corr(m, m2) < 0.01
+    assert m.mean(1).std().item() < 4 * 0.5 / C ** 0.5   # per-row rates: binomial spread
+
+
 def test_layernorm_fwd_bwd():
     Np, N, d, dp = 128, 100, 67, 128
     Z = _mk(Np, dp, seed=11)

@@ -312,6 +312,77 @@ __global__ void __launch_bounds__(256) attn_softmax_kernel(const float *S, int64
     }
 }
 
+// Softmax + dropout for the pre-split attention path (gemm_x2.hip): the same row statistics and
+// keep decisions as attn_softmax_kernel, Pd written once in x2 format (kept: P/(1-p), dropped: 0)
+// and the row (max, 1/sum) kept so the dS epilogue recomputes P bit-exactly from the saved scores.
+template <int SM_RV>
+__global__ void __launch_bounds__(256) attn_softmax_x2_kernel(const float *S, int64_t lds, __bf16 *Pd2,
+                                                              int64_t ldp2, float2 *rowstat, int64_t rows_valid,
+                                                              int64_t n_valid, int64_t n_pad, float p,
+                                                              uint64_t seed) {
+    __shared__ float red[4];
+    const int64_t row = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (row >= rows_valid) {
+        for (int64_t c = tid * 4; c < n_pad; c += 1024) store_x2_4(Pd2, ldp2, (int)row, (int)c, z4);
+        if (tid == 0) rowstat[row] = make_float2(0.f, 0.f);
+        return;
+    }
+    const float *srow = S + row * lds;
+    float e[SM_RV][4];
+    float m = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < SM_RV; ++i) {
+        const int64_t c = (int64_t)i * 1024 + tid * 4;
+        const float4 v = c < n_pad ? *reinterpret_cast<const float4 *>(srow + c) : z4;
+        const float x[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            e[i][j] = c + j < n_valid ? x[j] : -INFINITY;
+            m = fmaxf(m, e[i][j]);
+        }
+    }
+    const float M = block_max4(m, red, lane, w);
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < SM_RV; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            e[i][j] = expf(e[i][j] - M);   // exp(-inf) = 0 for masked / padded keys
+            s += e[i][j];
+        }
+    const float inv = 1.f / block_sum4(s, red, lane, w);
+    if (tid == 0) rowstat[row] = make_float2(M, inv);
+    const float ks = p > 0.f ? 1.f / (1.f - p) : 1.f;
+    const uint32_t rkey = u2gnn_row_key(seed, (uint32_t)row);
+#pragma unroll
+    for (int i = 0; i < SM_RV; ++i) {
+        const int64_t cb = (int64_t)i * 1024;
+        if (cb >= n_pad) break;   // block-uniform
+        const int64_t c = cb + tid * 4;
+        if (c >= n_pad) continue;
+        float pdv[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float pv = e[i][j] * inv;
+            const bool kp = !(p > 0.f) ||
+                            (float)(u2gnn_fmix32(rkey + (uint32_t)(c + j) * 0x9E3779B9u) >> 8) * (1.0f / 16777216.0f) >= p;
+            pdv[j] = kp ? pv * ks : 0.f;
+        }
+        store_x2_4(Pd2, ldp2, (int)row, (int)c, make_float4(pdv[0], pdv[1], pdv[2], pdv[3]));
+    }
+}
+
+// fp32 -> x2 over rows x cols (cols % 4 == 0): one thread per 4 columns
+__global__ void __launch_bounds__(256) split_x2_kernel(const float *src, int64_t ld_src, __bf16 *dst, int64_t ld_dst,
+                                                       int64_t rows, int64_t cols) {
+    const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x, per = cols / 4;
+    if (q >= rows * per) return;
+    const int64_t r = q / per, c = (q - r * per) * 4;
+    store_x2_4(dst, ld_dst, (int)r, (int)c, *reinterpret_cast<const float4 *>(src + r * ld_src + c));
+}
+
 __global__ void __launch_bounds__(256) rowdot_kernel(const float *A, int64_t lda, const float *B, int64_t ldb,
                                                      float *out, int64_t rows, int64_t cols) {
     const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -653,6 +724,40 @@ int u2gnn_attn_softmax_fwd(const float *S, int64_t lds, float *P, float *Pd, int
     else
         hipLaunchKernelGGL(attn_softmax_kernel<32>, dim3((unsigned)rows_pad), dim3(256), 0, st, S, lds, P, Pd, ldp,
                            rows_valid, n_valid, n_pad, p, seed, keep, ld_keep);
+    return u2gnn_launch_status();
+}
+
+int u2gnn_attn_softmax_x2_fwd(const float *S, int64_t lds, void *Pd2, int64_t ldp2, float *rowstat,
+                              int64_t rows_valid, int64_t rows_pad, int64_t n_valid, int64_t n_pad, float p,
+                              uint64_t seed, void *stream) {
+    if (!S || !Pd2 || !rowstat || (n_pad & 7) || (lds & 3) || (ldp2 & 15) || n_valid > n_pad || n_valid < 1 ||
+        !(p < 1.f))
+        return U2GNN_E_ARG;
+    if (!al16(S) || !al16(Pd2) || ((uintptr_t)rowstat & 7)) return U2GNN_E_ALIGN;
+    if (n_pad > 1024 * SM_RV_MAX) return U2GNN_E_SHAPE;
+    hipStream_t st = u2gnn_stream(stream);
+    __bf16 *d = static_cast<__bf16 *>(Pd2);
+    float2 *rs = reinterpret_cast<float2 *>(rowstat);
+    if (n_pad <= 8192)
+        hipLaunchKernelGGL(attn_softmax_x2_kernel<8>, dim3((unsigned)rows_pad), dim3(256), 0, st, S, lds, d, ldp2, rs,
+                           rows_valid, n_valid, n_pad, p, seed);
+    else if (n_pad <= 16384)
+        hipLaunchKernelGGL(attn_softmax_x2_kernel<16>, dim3((unsigned)rows_pad), dim3(256), 0, st, S, lds, d, ldp2, rs,
+                           rows_valid, n_valid, n_pad, p, seed);
+    else
+        hipLaunchKernelGGL(attn_softmax_x2_kernel<32>, dim3((unsigned)rows_pad), dim3(256), 0, st, S, lds, d, ldp2, rs,
+                           rows_valid, n_valid, n_pad, p, seed);
+    return u2gnn_launch_status();
+}
+
+int u2gnn_split_x2(const float *src, int64_t ld_src, void *dst2, int64_t ld_dst2, int64_t rows, int64_t cols,
+                   void *stream) {
+    if (!src || !dst2 || rows < 0 || cols < 0 || (cols & 7) || (ld_src & 3) || (ld_dst2 & 15)) return U2GNN_E_ARG;
+    if (!al16(src) || !al16(dst2)) return U2GNN_E_ALIGN;
+    if (rows == 0 || cols == 0) return U2GNN_OK;
+    const int64_t n = rows * (cols / 4);
+    hipLaunchKernelGGL(split_x2_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, u2gnn_stream(stream), src,
+                       ld_src, static_cast<__bf16 *>(dst2), ld_dst2, rows, cols);
     return u2gnn_launch_status();
 }
 

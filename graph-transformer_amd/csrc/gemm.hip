@@ -18,224 +18,12 @@
 //   * fused epilogues (bias, q-scaling, relu, dropout, residual, attention dS) so no
 //     elementwise pass re-reads a GEMM output.
 //   * split-K writes fp32 partial slabs (deterministic; reduced by u2gnn_slab_reduce).
-#include "u2gnn_common.h"
+#include "gemm_common.h"
 
-typedef float f32x16 __attribute__((ext_vector_type(16)));
+#include <cstring>
+
 
 namespace {
-
-struct GemmP {
-    const float *A;
-    const float *B;
-    float *C;
-    int64_t lda, ldb, ldc;
-    int32_t M, N, K;  // K = per-split depth (multiple of the K tile)
-    int32_t Ktot;     // full depth; split z covers [z*K, min((z+1)*K, Ktot))
-    int32_t gm, gn;
-    int64_t slab_stride;
-    const float *bias;
-    const float *aux0;
-    const float *aux1;
-    const float *rowvec;
-    int64_t ld_aux;
-    float alpha;
-    int32_t scale_cols;
-    float p;
-    uint64_t seed;
-    const uint32_t *keep;
-    int64_t ld_keep;
-};
-
-// four consecutive columns (col % 4 == 0) of one row; every vector operand is 16-byte aligned
-// with a leading dimension that is a multiple of 4 (checked by u2gnn_gemm)
-__device__ __forceinline__ float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
-
-// The epilogue runs in two passes per 32-row slice of a wave's tile: epi_fetch issues every
-// auxiliary load (P, keep words, residual, bias, C) first, then epilogue4 combines and stores.
-// Interleaved in one loop, each load would sit behind the previous store (the compiler cannot
-// prove C distinct from the aux operands) and the slice would pay one memory round trip per
-// 4 columns.
-template <int EPI>
-__device__ __forceinline__ void epi_fetch(const GemmP &P, int row, int col, float4 &a, float4 &b, uint32_t &kb) {
-    if constexpr (EPI == U2GNN_EPI_ATTN_DS_SIGNED) {
-        a = ld4(P.aux0 + (int64_t)row * P.ld_aux + col);
-    } else if constexpr (EPI == U2GNN_EPI_ATTN_DS) {
-        const int64_t o = (int64_t)row * P.ld_aux + col;
-        a = ld4(P.aux0 + o);
-        if (P.keep)
-            kb = P.keep[(int64_t)row * P.ld_keep + (col >> 5)] >> (col & 31);
-        else
-            b = ld4(P.aux1 + o);
-    } else if constexpr (EPI == U2GNN_EPI_ACCUM) {
-        a = ld4(P.C + (int64_t)row * P.ldc + col);
-    } else if constexpr (EPI == U2GNN_EPI_RELU_DROP_BWD) {
-        a = ld4(P.aux0 + (int64_t)row * P.ld_aux + col);
-    } else if constexpr (EPI != U2GNN_EPI_STORE) {
-        a = ld4(P.bias + col);
-        if constexpr (EPI == U2GNN_EPI_BIAS_DROP_RESID) b = ld4(P.aux0 + (int64_t)row * P.ld_aux + col);
-    }
-}
-
-// four consecutive columns (col % 4 == 0) of one row; a, b, kb, dl = what epi_fetch loaded
-template <int EPI>
-__device__ __forceinline__ float4 epilogue4(const GemmP &P, int row, int col, float4 v, float4 a, float4 b,
-                                            uint32_t kb, float dl) {
-    if constexpr (EPI == U2GNN_EPI_STORE) {
-        return make_float4(P.alpha * v.x, P.alpha * v.y, P.alpha * v.z, P.alpha * v.w);
-    } else if constexpr (EPI == U2GNN_EPI_ATTN_DS_SIGNED) {
-        // x = Pd = P/(1-p) where kept (sign clear), x = -P where dropped (sign set):
-        // dS = P*(keep*dPd/(1-p) - delta) = kept ? x*(dPd - (1-p)*delta) : x*delta
-        const float q = (1.f - P.p) * dl;
-        const float x[4] = {a.x, a.y, a.z, a.w}, g[4] = {v.x, v.y, v.z, v.w};
-        float o[4];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) o[c] = x[c] * ((__float_as_uint(x[c]) >> 31) ? dl : g[c] - q);
-        return make_float4(o[0], o[1], o[2], o[3]);
-    } else if constexpr (EPI == U2GNN_EPI_ATTN_DS) {
-        const float4 pr = a;
-        if (P.keep) {   // dS = P * (keep * dPd / (1-p) - delta): 4 keep bits instead of 16 B of Pd
-            const float s = 1.f / (1.f - P.p);
-            return make_float4(pr.x * (((kb & 1u) ? v.x * s : 0.f) - dl), pr.y * (((kb & 2u) ? v.y * s : 0.f) - dl),
-                               pr.z * (((kb & 4u) ? v.z * s : 0.f) - dl), pr.w * (((kb & 8u) ? v.w * s : 0.f) - dl));
-        }
-        const float4 pd = b;
-        return make_float4(pd.x * v.x - pr.x * dl, pd.y * v.y - pr.y * dl, pd.z * v.z - pr.z * dl,
-                           pd.w * v.w - pr.w * dl);
-    } else if constexpr (EPI == U2GNN_EPI_ACCUM) {
-        const float4 c = a;
-        return make_float4(c.x + P.alpha * v.x, c.y + P.alpha * v.y, c.z + P.alpha * v.z, c.w + P.alpha * v.w);
-    } else if constexpr (EPI == U2GNN_EPI_RELU_DROP_BWD) {
-        const float4 h = a;
-        const float s = 1.f / (1.f - P.p);
-        return make_float4(h.x > 0.f ? v.x * s : 0.f, h.y > 0.f ? v.y * s : 0.f, h.z > 0.f ? v.z * s : 0.f,
-                           h.w > 0.f ? v.w * s : 0.f);
-    } else {  // bias epilogues: per-column dropout hash
-        float x[4] = {v.x + a.x, v.y + a.y, v.z + a.z, v.w + a.w};
-        if constexpr (EPI == U2GNN_EPI_BIAS) {
-#pragma unroll
-            for (int c = 0; c < 4; ++c) x[c] = col + c < P.scale_cols ? x[c] * P.alpha : x[c];
-        } else {
-            if constexpr (EPI == U2GNN_EPI_BIAS_RELU_DROP) {
-#pragma unroll
-                for (int c = 0; c < 4; ++c) x[c] = fmaxf(x[c], 0.f);
-            }
-            if (P.p > 0.f) {
-                const float s = 1.f / (1.f - P.p);
-#pragma unroll
-                for (int c = 0; c < 4; ++c) x[c] = u2gnn_keep(P.seed, row, col + c, P.p) ? x[c] * s : 0.f;
-            }
-            if constexpr (EPI == U2GNN_EPI_BIAS_DROP_RESID) {
-                x[0] += b.x, x[1] += b.y, x[2] += b.z, x[3] += b.w;
-            }
-        }
-        return make_float4(x[0], x[1], x[2], x[3]);
-    }
-}
-
-// lane (li, kh) of MFMA tile (i, j) holds C[row = li][cols 8g + 4kh .. +3] in acc[i][j][4g .. 4g+3].
-// One 32-row slice (fixed i) of a wave's tile: its auxiliary operands, then its stores.
-template <int EPI, int TN>
-struct EpiSlice {
-    float4 a[TN][4], b[TN][4];
-    uint32_t kb[TN][4];
-    float dl;
-};
-
-template <int EPI, int TN>
-__device__ __forceinline__ void fetch_slice(const GemmP &P, int row, int c0, int kh, EpiSlice<EPI, TN> &e) {
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            e.a[j][g] = e.b[j][g] = make_float4(0.f, 0.f, 0.f, 0.f);
-            e.kb[j][g] = 0;
-            epi_fetch<EPI>(P, row, c0 + j * 32 + 8 * g + 4 * kh, e.a[j][g], e.b[j][g], e.kb[j][g]);
-        }
-    e.dl = (EPI == U2GNN_EPI_ATTN_DS || EPI == U2GNN_EPI_ATTN_DS_SIGNED) ? P.rowvec[row] : 0.f;
-}
-
-template <int EPI, int TM, int TN>
-__device__ __forceinline__ void store_slice(const GemmP &P, float *C, const f32x16 (&acc)[TM][TN], int i, int row,
-                                            int c0, int kh, const EpiSlice<EPI, TN> &e) {
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const int col = c0 + j * 32 + 8 * g + 4 * kh;
-            const float4 v = make_float4(acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2],
-                                         acc[i][j][4 * g + 3]);
-            *reinterpret_cast<float4 *>(C + (int64_t)row * P.ldc + col) =
-                epilogue4<EPI>(P, row, col, v, e.a[j][g], e.b[j][g], e.kb[j][g], e.dl);
-        }
-}
-
-// Attention dS with keep bits: slice 0's P tile, keep words and delta fetched before the main loop
-// (TN*16 + TN + 1 VGPRs), so they land under the MFMAs and the epilogue pays one round trip less.
-template <int TN>
-struct PreDS {
-    float4 p[TN][4];
-    uint32_t kw[TN];
-    float dl;
-};
-
-template <int EPI, int TN>
-__device__ __forceinline__ void prefetch_ds(const GemmP &P, int row, int c0, int kh, PreDS<TN> &f) {
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-        f.kw[j] = P.keep[(int64_t)row * P.ld_keep + ((c0 + j * 32) >> 5)];
-#pragma unroll
-        for (int g = 0; g < 4; ++g) f.p[j][g] = ld4(P.aux0 + (int64_t)row * P.ld_aux + c0 + j * 32 + 8 * g + 4 * kh);
-    }
-    f.dl = P.rowvec[row];
-}
-
-template <int EPI, int TM, int TN>
-__device__ __forceinline__ void store_tile(const GemmP &P, float *C, const f32x16 (&acc)[TM][TN], int r0, int c0,
-                                           int li, int kh, const PreDS<TN> *pre) {
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-        const int row = r0 + i * 32 + li;
-        EpiSlice<EPI, TN> e;
-        if (i == 0 && pre) {
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-#pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    e.a[j][g] = pre->p[j][g];
-                    e.b[j][g] = make_float4(0.f, 0.f, 0.f, 0.f);
-                    e.kb[j][g] = pre->kw[j] >> ((8 * g + 4 * kh) & 31);
-                }
-            e.dl = pre->dl;
-        } else {
-            fetch_slice<EPI>(P, row, c0, kh, e);
-        }
-        store_slice<EPI>(P, C, acc, i, row, c0, kh, e);
-    }
-}
-
-// 1-D grid over gm * gn * split blocks.  The hardware deals workgroups to the 8 XCDs round-robin
-// by linear id, so the bijective remap gives each XCD one contiguous range of logical ids; the
-// logical order is split-slowest, then 8-row-tile groups with the row tile fastest inside a
-// group.  Blocks that share an A row-panel or a B column-panel of the same K range therefore run
-// on the same XCD (one L2), and the large N^2 operands of the skinny attention products are
-// fetched from HBM once.
-__device__ __forceinline__ void tile_coords(int gm, int gn, int &tm, int &tn, int &z) {
-    const int ntile = gm * gn;
-    const int bid = blockIdx.x;
-    const int total = (int)gridDim.x;
-    const int q = total >> 3, r = total & 7, xcd = bid & 7, loc = bid >> 3;
-    const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
-    z = wgid / ntile;
-    const int t = wgid - z * ntile;
-    constexpr int GROUP = 8;
-    const int per_group = GROUP * gn;
-    const int g = t / per_group;
-    const int first_m = g * GROUP;
-    const int gsz = min(gm - first_m, GROUP);
-    const int in_g = t - g * per_group;
-    tm = first_m + in_g % gsz;
-    tn = in_g / gsz;
-}
 
 
 template <int BM, int BN, int BK, bool TA, bool TB>
@@ -397,9 +185,6 @@ __global__ void __launch_bounds__(256) gemm_f32_kernel(GemmP P) {
 // gfx950 transpose read ds_read_b64_tr_b16 (two per fragment), so neither layout needs a
 // register transpose and both keep 16-byte-per-lane coalesced global loads.
 // ------------------------------------------------------------------------------------
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 
 // LDS bank map of the staging stores (banks = dword mod 32 for ds_write):
 //  * [R][K] operands: 8 lanes x 16 B cover one row's 32 k; LDK = 40 bf16 = 20 dwords per row, so
@@ -466,22 +251,6 @@ __device__ __forceinline__ void g2r_bf(__amdgpu_buffer_rsrc_t rs, const int (&vo
     for (int i = 0; i < NF; ++i) {
         const u32x4 u = __builtin_amdgcn_raw_buffer_load_b128(rs, voff[i], soff, 0);
         v[i] = make_float4(__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w));
-    }
-}
-
-// (x0, x1) -> packed bf16 hi pair and, for SPLIT, the packed bf16 residual pair:
-// one v_cvt_pk_bf16_f32, two bit ops, two subtractions, one more cvt_pk (3 VALU / element).
-template <bool SPLIT>
-__device__ __forceinline__ void split2(float x0, float x1, unsigned &h, unsigned &l) {
-    // opaque to the optimizer: otherwise it re-derives bf16(x0) with a second cvt instead of
-    // shifting the packed pair
-#ifdef U2GNN_EXP_NOSPLIT
-    h = __float_as_uint(x0) ^ __float_as_uint(x1); l = h; return;
-#endif
-    asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(h) : "v"(x0), "v"(x1));
-    if constexpr (SPLIT) {
-        const float l0 = x0 - __uint_as_float(h << 16), l1 = x1 - __uint_as_float(h & 0xffff0000u);
-        l = __builtin_bit_cast(unsigned, bf16x2{(__bf16)l0, (__bf16)l1});
     }
 }
 
@@ -727,23 +496,34 @@ inline bool al16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) =
 
 }  // namespace
 
+int u2gnn_gemm_x2_dispatch(const u2gnn_gemm_args *a, GemmP &P, int tile, int split, hipStream_t st);
+
 extern "C" int u2gnn_gemm(const u2gnn_gemm_args *a, void *stream) {
-    if (!a || !a->A || !a->B || !a->C) return U2GNN_E_ARG;
+    if (!a) return U2GNN_E_ARG;
+    const bool x2 = a->a_x2 || a->b_x2;
+    if (x2 ? (!a->A2 || !a->B2) : (!a->A || !a->B)) return U2GNN_E_ARG;
+    if (!a->C && !a->Cx2) return U2GNN_E_ARG;
     if (a->M <= 0 || a->N <= 0 || a->K <= 0) return U2GNN_E_ARG;
-    if (a->epilogue < 0 || a->epilogue > U2GNN_EPI_ATTN_DS_SIGNED) return U2GNN_E_ARG;
+    if (a->epilogue < 0 || a->epilogue > U2GNN_EPI_ATTN_DS_RECOMP) return U2GNN_E_ARG;
+    if (a->epilogue == U2GNN_EPI_ATTN_DS_RECOMP && !x2) return U2GNN_E_ARG;
     const int prec = a->precision;
     if (prec != U2GNN_PREC_F32 && prec != U2GNN_PREC_BF16X3 && prec != U2GNN_PREC_BF16) return U2GNN_E_ARG;
     const int split = a->split_k < 1 ? 1 : a->split_k;
-    if (split > 1 && a->epilogue != U2GNN_EPI_STORE) return U2GNN_E_ARG;
-    if (!al16(a->A) || !al16(a->B) || (a->lda & 3) || (a->ldb & 3)) return U2GNN_E_ALIGN;
-    const int bk = (prec == U2GNN_PREC_F32 || a->tile == 129) ? 16 : 32;   // K step of the kernel
+    if (split > 1 && (a->epilogue != U2GNN_EPI_STORE || a->Cx2 || !a->C)) return U2GNN_E_ARG;
+    if (!x2) {
+        if (!al16(a->A) || !al16(a->B) || (a->lda & 3) || (a->ldb & 3)) return U2GNN_E_ALIGN;
+    }
+    const int bk = (prec == U2GNN_PREC_F32 || a->tile == 129 ||
+                    (x2 && (a->tile == 257 || a->tile == 128 || a->tile == 258 || a->tile == 260)))
+                       ? 16 : 32;   // K step of the kernel
     if (a->K % bk) return U2GNN_E_SHAPE;
-    if (prec != U2GNN_PREC_F32) {   // bf16 staging addresses operands by 32-bit buffer offsets
+    if (prec != U2GNN_PREC_F32 && !x2) {   // bf16 staging addresses operands by 32-bit buffer offsets
         const int64_t span = ((int64_t)a->K + 256) * (a->lda > a->ldb ? a->lda : a->ldb) * 4;
         if (span >= (int64_t)INT32_MAX) return U2GNN_E_SHAPE;
     }
-    // 16-byte epilogue: C, bias and aux rows are read/written as float4
-    if (!al16(a->C) || (a->ldc & 3) || (split > 1 && (a->slab_stride & 3))) return U2GNN_E_ALIGN;
+    // 16-byte epilogue: C, bias and aux rows are read/written as float4; x2 output as 8-byte pairs
+    if ((a->C && (!al16(a->C) || (a->ldc & 3))) || (split > 1 && (a->slab_stride & 3))) return U2GNN_E_ALIGN;
+    if (a->Cx2 && (!al16(a->Cx2) || (a->ldcx2 & 15) || (a->N & 7))) return U2GNN_E_ALIGN;
     if ((a->bias && !al16(a->bias)) || (a->aux0 && !al16(a->aux0)) || (a->aux1 && !al16(a->aux1)) ||
         ((a->aux0 || a->aux1) && (a->ld_aux & 3)))
         return U2GNN_E_ALIGN;
@@ -751,25 +531,33 @@ extern "C" int u2gnn_gemm(const u2gnn_gemm_args *a, void *stream) {
     if ((e == U2GNN_EPI_BIAS || e == U2GNN_EPI_BIAS_DROP_RESID || e == U2GNN_EPI_BIAS_RELU_DROP) && !a->bias)
         return U2GNN_E_ARG;
     if ((e == U2GNN_EPI_BIAS_DROP_RESID || e == U2GNN_EPI_RELU_DROP_BWD || e == U2GNN_EPI_ATTN_DS ||
-         e == U2GNN_EPI_ATTN_DS_SIGNED) && !a->aux0)
+         e == U2GNN_EPI_ATTN_DS_SIGNED || e == U2GNN_EPI_ATTN_DS_RECOMP) && !a->aux0)
         return U2GNN_E_ARG;
     if (e == U2GNN_EPI_ATTN_DS_SIGNED && (!a->rowvec || !(a->p_drop < 1.f))) return U2GNN_E_ARG;
+    if (e == U2GNN_EPI_ATTN_DS_RECOMP && (!a->rowvec || !a->rowstat || !(a->p_drop < 1.f) ||
+                                          ((uintptr_t)a->rowstat & 7)))
+        return U2GNN_E_ARG;
     if (a->clamp_a && (e != U2GNN_EPI_STORE || a->trans_b)) return U2GNN_E_ARG;
     if (e == U2GNN_EPI_ATTN_DS && ((!a->aux1 && !a->keep) || !a->rowvec)) return U2GNN_E_ARG;
     if (e == U2GNN_EPI_ATTN_DS && a->keep && (a->ld_keep * 32 < a->N || !(a->p_drop < 1.f))) return U2GNN_E_ARG;
     int tile = a->tile;
-    if (tile == 0) {
+    if (x2 && tile == 0) tile = 256;
+    if (x2 && tile != 64 && tile != 128 && tile != 256 && tile != 129) {
+        // x2-only tile codes (gemm_x2.hip X2Cfg); shapes are checked by the x2 dispatcher
+    } else if (tile == 0) {
         const bool can128 = (a->M % 128 == 0) && (a->N % 128 == 0);
         const int64_t blocks128 = can128 ? (a->M / 128) * (a->N / 128) * split : 0;
         tile = (can128 && blocks128 >= 480) ? 128 : 64;
     }
     // tile codes: 64, 128 (square), 256 (256x128, 8 waves), 129 (128x128 with a 16-deep K step)
-    if (tile != 64 && tile != 128 && tile != 256 && tile != 129) return U2GNN_E_ARG;
+    const bool x2code = x2 && (tile == 257 || tile == 130 || (tile >= 258 && tile <= 260));
+    if (!x2code && tile != 64 && tile != 128 && tile != 256 && tile != 129) return U2GNN_E_ARG;
     if ((tile == 256 || tile == 129) && prec == U2GNN_PREC_F32) return U2GNN_E_ARG;
-    const int tm_ = tile == 129 ? 128 : tile;
-    const int tile_n = tm_ == 256 ? 128 : tm_;
+    const int tm_ = tile == 129 ? 128 : (tile > 256 ? 256 : (tile == 130 ? 128 : tile));
+    const int tile_n = tile == 260 ? 256 : (tm_ == 256 ? 128 : tm_);
     if (a->M % tm_ || a->N % tile_n) return U2GNN_E_SHAPE;
     GemmP P;
+    std::memset(&P, 0, sizeof(P));
     P.A = a->A;
     P.B = a->B;
     P.C = a->C;
@@ -797,7 +585,15 @@ extern "C" int u2gnn_gemm(const u2gnn_gemm_args *a, void *stream) {
     P.seed = a->seed;
     P.keep = e == U2GNN_EPI_ATTN_DS ? a->keep : nullptr;
     P.ld_keep = a->ld_keep;
+    P.A2 = static_cast<const __bf16 *>(a->A2);
+    P.B2 = static_cast<const __bf16 *>(a->B2);
+    P.Cx2 = static_cast<__bf16 *>(a->Cx2);
+    P.ldcx2 = a->ldcx2;
+    P.rowstat = reinterpret_cast<const float2 *>(a->rowstat);
+    P.m_valid = (int32_t)a->m_valid;
+    P.n_valid = (int32_t)a->n_valid;
     hipStream_t st = u2gnn_stream(stream);
+    if (x2) return u2gnn_gemm_x2_dispatch(a, P, tile, split, st);
     const bool ta = a->trans_a != 0, tb = a->trans_b != 0;
     const bool clamp = a->clamp_a != 0;
     if (prec == U2GNN_PREC_BF16X3) return launch_tile<U2GNN_PREC_BF16X3>(P, tile, ta, tb, e, split, clamp, st);

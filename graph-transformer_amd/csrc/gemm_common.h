@@ -1,0 +1,267 @@
+// Shared pieces of the U2GNN GEMM kernels (gemm.hip: fp32-operand kernels; gemm_x2.hip: kernels over
+// pre-split bf16 hi/lo operands): kernel parameters, the fused epilogues and the XCD-aware tile map.
+#pragma once
+#include "u2gnn_common.h"
+
+// kernel parameters (shared by both translation units, hence outside the anonymous namespace)
+struct GemmP {
+    const float *A;
+    const float *B;
+    float *C;
+    int64_t lda, ldb, ldc;
+    int32_t M, N, K;  // K = per-split depth (multiple of the K tile)
+    int32_t Ktot;     // full depth; split z covers [z*K, min((z+1)*K, Ktot))
+    int32_t gm, gn;
+    int64_t slab_stride;
+    const float *bias;
+    const float *aux0;
+    const float *aux1;
+    const float *rowvec;
+    int64_t ld_aux;
+    float alpha;
+    int32_t scale_cols;
+    float p;
+    uint64_t seed;
+    const uint32_t *keep;
+    int64_t ld_keep;
+    // pre-split operands / outputs (gemm_x2.hip; U2GNN x2 format, see u2gnn_hip.h)
+    const __bf16 *A2;
+    const __bf16 *B2;
+    __bf16 *Cx2;          // non-null: the epilogue also writes C in x2 format
+    int64_t ldcx2;        // bf16 elements
+    const float2 *rowstat;   // ATTN_DS_RECOMP: (row max, 1/row sum) of the forward softmax
+    int32_t m_valid, n_valid;   // ATTN_DS_RECOMP: real rows / keys (P = 0 beyond)
+};
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+
+
+// four consecutive columns (col % 4 == 0) of one row; every vector operand is 16-byte aligned
+// with a leading dimension that is a multiple of 4 (checked by u2gnn_gemm)
+__device__ __forceinline__ float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
+
+// The epilogue runs in two passes per 32-row slice of a wave's tile: epi_fetch issues every
+// auxiliary load (P, keep words, residual, bias, C) first, then epilogue4 combines and stores.
+// Interleaved in one loop, each load would sit behind the previous store (the compiler cannot
+// prove C distinct from the aux operands) and the slice would pay one memory round trip per
+// 4 columns.
+template <int EPI>
+__device__ __forceinline__ void epi_fetch(const GemmP &P, int row, int col, float4 &a, float4 &b, uint32_t &kb) {
+    if constexpr (EPI == U2GNN_EPI_ATTN_DS_SIGNED || EPI == U2GNN_EPI_ATTN_DS_RECOMP) {
+        a = ld4(P.aux0 + (int64_t)row * P.ld_aux + col);
+    } else if constexpr (EPI == U2GNN_EPI_ATTN_DS) {
+        const int64_t o = (int64_t)row * P.ld_aux + col;
+        a = ld4(P.aux0 + o);
+        if (P.keep)
+            kb = P.keep[(int64_t)row * P.ld_keep + (col >> 5)] >> (col & 31);
+        else
+            b = ld4(P.aux1 + o);
+    } else if constexpr (EPI == U2GNN_EPI_ACCUM) {
+        a = ld4(P.C + (int64_t)row * P.ldc + col);
+    } else if constexpr (EPI == U2GNN_EPI_RELU_DROP_BWD) {
+        a = ld4(P.aux0 + (int64_t)row * P.ld_aux + col);
+    } else if constexpr (EPI != U2GNN_EPI_STORE) {
+        a = ld4(P.bias + col);
+        if constexpr (EPI == U2GNN_EPI_BIAS_DROP_RESID) b = ld4(P.aux0 + (int64_t)row * P.ld_aux + col);
+    }
+}
+
+// four consecutive columns (col % 4 == 0) of one row; a, b, kb, dl = what epi_fetch loaded
+template <int EPI>
+__device__ __forceinline__ float4 epilogue4(const GemmP &P, int row, int col, float4 v, float4 a, float4 b,
+                                            uint32_t kb, float dl) {
+    if constexpr (EPI == U2GNN_EPI_STORE) {
+        return make_float4(P.alpha * v.x, P.alpha * v.y, P.alpha * v.z, P.alpha * v.w);
+    } else if constexpr (EPI == U2GNN_EPI_ATTN_DS_SIGNED) {
+        // x = Pd = P/(1-p) where kept (sign clear), x = -P where dropped (sign set):
+        // dS = P*(keep*dPd/(1-p) - delta) = kept ? x*(dPd - (1-p)*delta) : x*delta
+        const float q = (1.f - P.p) * dl;
+        const float x[4] = {a.x, a.y, a.z, a.w}, g[4] = {v.x, v.y, v.z, v.w};
+        float o[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) o[c] = x[c] * ((__float_as_uint(x[c]) >> 31) ? dl : g[c] - q);
+        return make_float4(o[0], o[1], o[2], o[3]);
+    } else if constexpr (EPI == U2GNN_EPI_ATTN_DS) {
+        const float4 pr = a;
+        if (P.keep) {   // dS = P * (keep * dPd / (1-p) - delta): 4 keep bits instead of 16 B of Pd
+            const float s = 1.f / (1.f - P.p);
+            return make_float4(pr.x * (((kb & 1u) ? v.x * s : 0.f) - dl), pr.y * (((kb & 2u) ? v.y * s : 0.f) - dl),
+                               pr.z * (((kb & 4u) ? v.z * s : 0.f) - dl), pr.w * (((kb & 8u) ? v.w * s : 0.f) - dl));
+        }
+        const float4 pd = b;
+        return make_float4(pd.x * v.x - pr.x * dl, pd.y * v.y - pr.y * dl, pd.z * v.z - pr.z * dl,
+                           pd.w * v.w - pr.w * dl);
+    } else if constexpr (EPI == U2GNN_EPI_ACCUM) {
+        const float4 c = a;
+        return make_float4(c.x + P.alpha * v.x, c.y + P.alpha * v.y, c.z + P.alpha * v.z, c.w + P.alpha * v.w);
+    } else if constexpr (EPI == U2GNN_EPI_RELU_DROP_BWD) {
+        const float4 h = a;
+        const float s = 1.f / (1.f - P.p);
+        return make_float4(h.x > 0.f ? v.x * s : 0.f, h.y > 0.f ? v.y * s : 0.f, h.z > 0.f ? v.z * s : 0.f,
+                           h.w > 0.f ? v.w * s : 0.f);
+    } else {  // bias epilogues: per-column dropout hash
+        float x[4] = {v.x + a.x, v.y + a.y, v.z + a.z, v.w + a.w};
+        if constexpr (EPI == U2GNN_EPI_BIAS) {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) x[c] = col + c < P.scale_cols ? x[c] * P.alpha : x[c];
+        } else {
+            if constexpr (EPI == U2GNN_EPI_BIAS_RELU_DROP) {
+#pragma unroll
+                for (int c = 0; c < 4; ++c) x[c] = fmaxf(x[c], 0.f);
+            }
+            if (P.p > 0.f) {
+                const float s = 1.f / (1.f - P.p);
+#pragma unroll
+                for (int c = 0; c < 4; ++c) x[c] = u2gnn_keep(P.seed, row, col + c, P.p) ? x[c] * s : 0.f;
+            }
+            if constexpr (EPI == U2GNN_EPI_BIAS_DROP_RESID) {
+                x[0] += b.x, x[1] += b.y, x[2] += b.z, x[3] += b.w;
+            }
+        }
+        return make_float4(x[0], x[1], x[2], x[3]);
+    }
+}
+
+// lane (li, kh) of MFMA tile (i, j) holds C[row = li][cols 8g + 4kh .. +3] in acc[i][j][4g .. 4g+3].
+// One 32-row slice (fixed i) of a wave's tile: its auxiliary operands, then its stores.
+template <int EPI, int TN>
+struct EpiSlice {
+    float4 a[TN][4], b[TN][4];
+    uint32_t kb[TN][4];
+    float dl;
+    float rm, rinv;   // ATTN_DS_RECOMP: forward softmax row max and 1/sum
+};
+
+template <int EPI, int TN>
+__device__ __forceinline__ void fetch_slice(const GemmP &P, int row, int c0, int kh, EpiSlice<EPI, TN> &e) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            e.a[j][g] = e.b[j][g] = make_float4(0.f, 0.f, 0.f, 0.f);
+            e.kb[j][g] = 0;
+            epi_fetch<EPI>(P, row, c0 + j * 32 + 8 * g + 4 * kh, e.a[j][g], e.b[j][g], e.kb[j][g]);
+        }
+    e.dl = (EPI == U2GNN_EPI_ATTN_DS || EPI == U2GNN_EPI_ATTN_DS_SIGNED || EPI == U2GNN_EPI_ATTN_DS_RECOMP)
+               ? P.rowvec[row] : 0.f;
+    if constexpr (EPI == U2GNN_EPI_ATTN_DS_RECOMP) {
+        const float2 st = P.rowstat[row];
+        e.rm = st.x, e.rinv = st.y;
+    } else {
+        e.rm = e.rinv = 0.f;
+    }
+}
+
+// Attention dS with the probabilities recomputed from the saved scores (ATTN_DS_RECOMP):
+// P = exp(s - rowmax) * (1/rowsum), bit-identical to the forward softmax's P; keep regenerated from
+// the dropout hash; dS = P * (keep * dPd/(1-p) - delta).  Padded rows / keys give 0.
+__device__ __forceinline__ float4 ds_recomp4(const GemmP &P, int row, int col, float4 v, float4 s, float dl, float rm,
+                                             float rinv, uint32_t rkey) {
+    const float x[4] = {s.x, s.y, s.z, s.w}, g[4] = {v.x, v.y, v.z, v.w};
+    const float sc = P.p > 0.f ? 1.f / (1.f - P.p) : 1.f;
+    const bool rv = row < P.m_valid;
+    float o[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const uint32_t cc = (uint32_t)(col + c);
+        const float pr = (rv && (int)cc < P.n_valid) ? expf(x[c] - rm) * rinv : 0.f;
+        const bool kp = !(P.p > 0.f) ||
+                        (float)(u2gnn_fmix32(rkey + cc * 0x9E3779B9u) >> 8) * (1.0f / 16777216.0f) >= P.p;
+        o[c] = pr * ((kp ? g[c] * sc : 0.f) - dl);
+    }
+    return make_float4(o[0], o[1], o[2], o[3]);
+}
+
+template <int EPI, int TM, int TN>
+__device__ __forceinline__ void store_slice(const GemmP &P, float *C, const f32x16 (&acc)[TM][TN], int i, int row,
+                                            int c0, int kh, const EpiSlice<EPI, TN> &e) {
+    uint32_t rkey = 0;
+    if constexpr (EPI == U2GNN_EPI_ATTN_DS_RECOMP) rkey = u2gnn_row_key(P.seed, (uint32_t)row);
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int col = c0 + j * 32 + 8 * g + 4 * kh;
+            const float4 v = make_float4(acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2],
+                                         acc[i][j][4 * g + 3]);
+            float4 o;
+            if constexpr (EPI == U2GNN_EPI_ATTN_DS_RECOMP)
+                o = ds_recomp4(P, row, col, v, e.a[j][g], e.dl, e.rm, e.rinv, rkey);
+            else
+                o = epilogue4<EPI>(P, row, col, v, e.a[j][g], e.b[j][g], e.kb[j][g], e.dl);
+            if (P.C) *reinterpret_cast<float4 *>(C + (int64_t)row * P.ldc + col) = o;
+            if (P.Cx2) store_x2_4(P.Cx2, P.ldcx2, row, col, o);
+        }
+}
+
+// Attention dS with keep bits: slice 0's P tile, keep words and delta fetched before the main loop
+// (TN*16 + TN + 1 VGPRs), so they land under the MFMAs and the epilogue pays one round trip less.
+template <int TN>
+struct PreDS {
+    float4 p[TN][4];
+    uint32_t kw[TN];
+    float dl;
+};
+
+template <int EPI, int TN>
+__device__ __forceinline__ void prefetch_ds(const GemmP &P, int row, int c0, int kh, PreDS<TN> &f) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        f.kw[j] = P.keep[(int64_t)row * P.ld_keep + ((c0 + j * 32) >> 5)];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) f.p[j][g] = ld4(P.aux0 + (int64_t)row * P.ld_aux + c0 + j * 32 + 8 * g + 4 * kh);
+    }
+    f.dl = P.rowvec[row];
+}
+
+template <int EPI, int TM, int TN>
+__device__ __forceinline__ void store_tile(const GemmP &P, float *C, const f32x16 (&acc)[TM][TN], int r0, int c0,
+                                           int li, int kh, const PreDS<TN> *pre) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+        const int row = r0 + i * 32 + li;
+        EpiSlice<EPI, TN> e;
+        if (i == 0 && pre) {
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    e.a[j][g] = pre->p[j][g];
+                    e.b[j][g] = make_float4(0.f, 0.f, 0.f, 0.f);
+                    e.kb[j][g] = pre->kw[j] >> ((8 * g + 4 * kh) & 31);
+                }
+            e.dl = pre->dl;
+        } else {
+            fetch_slice<EPI>(P, row, c0, kh, e);
+        }
+        store_slice<EPI>(P, C, acc, i, row, c0, kh, e);
+    }
+}
+
+// 1-D grid over gm * gn * split blocks.  The hardware deals workgroups to the 8 XCDs round-robin
+// by linear id, so the bijective remap gives each XCD one contiguous range of logical ids; the
+// logical order is split-slowest, then 8-row-tile groups with the row tile fastest inside a
+// group.  Blocks that share an A row-panel or a B column-panel of the same K range therefore run
+// on the same XCD (one L2), and the large N^2 operands of the skinny attention products are
+// fetched from HBM once.
+__device__ __forceinline__ void tile_coords(int gm, int gn, int &tm, int &tn, int &z) {
+    const int ntile = gm * gn;
+    const int bid = blockIdx.x;
+    const int total = (int)gridDim.x;
+    const int q = total >> 3, r = total & 7, xcd = bid & 7, loc = bid >> 3;
+    const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+    z = wgid / ntile;
+    const int t = wgid - z * ntile;
+    constexpr int GROUP = 8;
+    const int per_group = GROUP * gn;
+    const int g = t / per_group;
+    const int first_m = g * GROUP;
+    const int gsz = min(gm - first_m, GROUP);
+    const int in_g = t - g * per_group;
+    tm = first_m + in_g % gsz;
+    tn = in_g / gsz;
+}
+}  // namespace

@@ -63,3 +63,37 @@ __device__ __forceinline__ int64_t blk_map(int64_t i, int64_t blk_pad, int64_t b
     *valid = r < blk_real;
     return b * blk_real + r;
 }
+
+// ---------------------------------------------------------------------------------------
+// x2 format (pre-split fp32, include/u2gnn_hip.h): bf16 hi/lo pairs, hi = bf16_rne(x), lo = bf16_rne(x - hi)
+// ---------------------------------------------------------------------------------------
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+// (x0, x1) -> packed bf16 hi pair and, for SPLIT, the packed bf16 residual pair:
+// one v_cvt_pk_bf16_f32, two bit ops, two subtractions, one more cvt_pk (3 VALU / element).
+template <bool SPLIT>
+__device__ __forceinline__ void split2(float x0, float x1, unsigned &h, unsigned &l) {
+    // opaque to the optimizer: otherwise it re-derives bf16(x0) with a second cvt instead of
+    // shifting the packed pair
+#ifdef U2GNN_EXP_NOSPLIT
+    h = __float_as_uint(x0) ^ __float_as_uint(x1); l = h; return;
+#endif
+    asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(h) : "v"(x0), "v"(x1));
+    if constexpr (SPLIT) {
+        const float l0 = x0 - __uint_as_float(h << 16), l1 = x1 - __uint_as_float(h & 0xffff0000u);
+        l = __builtin_bit_cast(unsigned, bf16x2{(__bf16)l0, (__bf16)l1});
+    }
+}
+
+// x2 store of four consecutive columns (col % 4 == 0): hi at 16*(col/8) + col%8, lo 8 further
+__device__ __forceinline__ void store_x2_4(__bf16 *Cx2, int64_t ldcx2, int row, int col, float4 o) {
+    unsigned h0, h1, l0, l1;
+    split2<true>(o.x, o.y, h0, l0);
+    split2<true>(o.z, o.w, h1, l1);
+    __bf16 *b = Cx2 + (int64_t)row * ldcx2 + 2 * (col & ~7) + (col & 7);
+    *reinterpret_cast<uint2 *>(b) = make_uint2(h0, h1);
+    *reinterpret_cast<uint2 *>(b + 8) = make_uint2(l0, l1);
+}
+

@@ -29,8 +29,8 @@ U2GNN_OK = 0
 ERRORS = {-1: "bad argument", -2: "misaligned pointer / leading dimension", -3: "shape not a tile multiple"}
 
 EPI_STORE, EPI_BIAS, EPI_BIAS_DROP_RESID, EPI_BIAS_RELU_DROP, EPI_RELU_DROP_BWD, EPI_ACCUM, EPI_ATTN_DS, \
-    EPI_ATTN_DS_SIGNED = range(8)
-ABI_VERSION = 2   # include/u2gnn_hip.h U2GNN_ABI_VERSION
+    EPI_ATTN_DS_SIGNED, EPI_ATTN_DS_RECOMP = range(9)
+ABI_VERSION = 3   # include/u2gnn_hip.h U2GNN_ABI_VERSION
 PREC_F32, PREC_BF16X3, PREC_BF16 = 0, 1, 2
 
 
@@ -52,6 +52,10 @@ class GemmArgs(ctypes.Structure):
         ("tile", c_int32),
         ("keep", c_void_p), ("ld_keep", c_int64),
         ("clamp_a", c_int32), ("reserved", c_int32),
+        # ABI v3: pre-split (x2) operands / outputs
+        ("a_x2", c_int32), ("b_x2", c_int32),
+        ("A2", c_void_p), ("B2", c_void_p), ("Cx2", c_void_p), ("ldcx2", c_int64),
+        ("rowstat", c_void_p), ("m_valid", c_int64), ("n_valid", c_int64),
     ]
 
 
@@ -104,6 +108,8 @@ _HIP_SIGS = {
     "u2gnn_colsum": ([VP, I64, I64, I64, I64, I64, VP, I32, VP, VP], c_int32),
     "u2gnn_attn_softmax_fwd": ([VP, I64, VP, VP, I64, I64, I64, I64, I64, F32, c_uint64, VP, I64, VP], c_int32),
     "u2gnn_rowdot": ([VP, I64, VP, I64, VP, I64, I64, VP], c_int32),
+    "u2gnn_attn_softmax_x2_fwd": ([VP, I64, VP, I64, VP, I64, I64, I64, I64, F32, c_uint64, VP], c_int32),
+    "u2gnn_split_x2": ([VP, I64, VP, I64, I64, I64, VP], c_int32),
     "u2gnn_layernorm_fwd": ([VP, I64, VP, VP, VP, I64, VP, VP, I64, I64, I64, I64, F32, VP], c_int32),
     "u2gnn_layernorm_bwd": ([VP, I64, VP, I64, VP, VP, VP, VP, I64, VP, I64, F32, c_uint64, I64, I64, I64, I64, VP],
                             c_int32),

@@ -49,11 +49,14 @@ class LaunchRecorder:
 
 REC = LaunchRecorder()
 _EPI_NAMES = ["STORE", "BIAS", "BIAS_DROP_RESID", "BIAS_RELU_DROP", "RELU_DROP_BWD", "ACCUM", "ATTN_DS",
-              "ATTN_DS_SIGNED"]
+              "ATTN_DS_SIGNED", "ATTN_DS_RECOMP"]
 
 
-def gemm_symbol(precision, M, N, split_k, tile, trans_a, trans_b, epilogue, clamp_a=False):
+def gemm_symbol(precision, M, N, split_k, tile, trans_a, trans_b, epilogue, clamp_a=False, x2=False):
     """Mirror of the C dispatcher's kernel choice (gemm.hip u2gnn_gemm) -> template symbol."""
+    b = lambda x: "true" if x else "false"  # noqa: E731
+    if x2:   # gemm_x2.hip: pre-split operands, 256x128 (8 waves) or 128x128 (4 waves)
+        return f"gemm_x2_kernel<{tile}, 128, {b(trans_a)}, {b(trans_b)}, {int(epilogue)}>"
     if tile == 0:
         can128 = M % 128 == 0 and N % 128 == 0
         tile = 128 if (can128 and (M // 128) * (N // 128) * max(split_k, 1) >= 480) else 64
@@ -68,19 +71,36 @@ def gemm_symbol(precision, M, N, split_k, tile, trans_a, trans_b, epilogue, clam
 
 def gemm(A, B, C, M, N, K, lda, ldb, ldc, trans_a=False, trans_b=False, epilogue=_lib.EPI_STORE, split_k=1,
          slab_stride=0, bias=None, aux0=None, aux1=None, rowvec=None, ld_aux=0, alpha=1.0, scale_cols=0, p_drop=0.0,
-         seed=0, precision="fp32", tile=0, flops=None, keep=None, clamp_a=False):
+         seed=0, precision="fp32", tile=0, flops=None, keep=None, clamp_a=False, Cx2=None, ldcx2=0, rowstat=None,
+         m_valid=0, n_valid=0):
     """C[M,N] (epilogue) sum_k A(m,k) B(k,n).  A/B/C may be views (pointer arithmetic via
     storage offsets is done by torch's data_ptr()).  ``flops``: algorithmic FLOPs of the
     launch for the roofline recorder (None = not recorded).  ``clamp_a``: A elements below +0 are read
-    as 0 (the signed probability image of attn_softmax_fwd(P=None) consumed as Pd)."""
-    _dev(A, B, C)
+    as 0 (the signed probability image of attn_softmax_fwd(P=None) consumed as Pd).
+    x2 operands (include/u2gnn_hip.h): A and B given as bfloat16 tensors are pre-split [rows][2*cols]
+    matrices (lda / ldb in bf16 elements); ``Cx2`` (bfloat16) receives the result in x2 format, C may
+    then be None.  ``rowstat``/``m_valid``/``n_valid``: the ATTN_DS_RECOMP epilogue."""
+    _dev(A, B, C, Cx2, rowstat)
+    x2 = A.dtype == torch.bfloat16
+    if x2 != (B.dtype == torch.bfloat16):
+        raise _lib.U2GNNNativeError("x2 GEMM: both operands must be pre-split (bfloat16) or neither")
     rec = REC.enabled and flops is not None
     if rec:
         ev0 = torch.cuda.Event(enable_timing=True)
         ev1 = torch.cuda.Event(enable_timing=True)
         ev0.record()
     a = _lib.GemmArgs()
-    a.A, a.B, a.C = A.data_ptr(), B.data_ptr(), C.data_ptr()
+    if x2:
+        a.a_x2 = a.b_x2 = 1
+        a.A2, a.B2 = A.data_ptr(), B.data_ptr()
+    else:
+        a.A, a.B = A.data_ptr(), B.data_ptr()
+    a.C = C.data_ptr() if C is not None else None
+    if Cx2 is not None:
+        a.Cx2, a.ldcx2 = Cx2.data_ptr(), int(ldcx2)
+    if rowstat is not None:
+        a.rowstat = rowstat.data_ptr()
+    a.m_valid, a.n_valid = int(m_valid), int(n_valid)
     a.M, a.N, a.K = int(M), int(N), int(K)
     a.lda, a.ldb, a.ldc = int(lda), int(ldb), int(ldc)
     a.trans_a, a.trans_b = int(bool(trans_a)), int(bool(trans_b))
@@ -103,8 +123,8 @@ def gemm(A, B, C, M, N, K, lda, ldb, ldc, trans_a=False, trans_b=False, epilogue
     check(hip_lib().u2gnn_gemm(ctypes.byref(a), _s()), "u2gnn_gemm")
     if rec:
         ev1.record()
-        REC.records.append((gemm_symbol(precision, M, N, split_k, tile, trans_a, trans_b, epilogue, clamp_a), float(flops),
-                            ev0, ev1))
+        REC.records.append((gemm_symbol(precision, M, N, split_k, tile, trans_a, trans_b, epilogue, clamp_a, x2),
+                            float(flops), ev0, ev1))
 
 
 def gather_rows(src, idx, idx_stride, dst, n_rows, n_rows_pad, d, d_pad, err=None):
@@ -150,6 +170,22 @@ def attn_softmax_fwd(S, lds, P, Pd, ldp, rows_valid, rows_pad, n_valid, n_pad, p
                                            int(n_valid), int(n_pad), float(p), int(seed), _p(keep),
                                            int(keep.stride(0)) if keep is not None else 0, _s()),
           "u2gnn_attn_softmax_fwd")
+
+
+def attn_softmax_x2_fwd(S, lds, Pd2, ldp2, rowstat, rows_valid, rows_pad, n_valid, n_pad, p, seed):
+    """Softmax + dropout writing Pd in x2 format (bfloat16 [rows_pad, >= 2*n_pad]) and rowstat
+    [rows_pad, 2] = (row max, 1/row sum) for the ATTN_DS_RECOMP epilogue."""
+    _dev(S, Pd2, rowstat)
+    check(hip_lib().u2gnn_attn_softmax_x2_fwd(_p(S), int(lds), _p(Pd2), int(ldp2), _p(rowstat), int(rows_valid),
+                                              int(rows_pad), int(n_valid), int(n_pad), float(p), int(seed), _s()),
+          "u2gnn_attn_softmax_x2_fwd")
+
+
+def split_x2(src, ld_src, dst2, ld_dst2, rows, cols):
+    """dst2 (bfloat16, x2 format) = split of the fp32 rows x cols block of src."""
+    _dev(src, dst2)
+    check(hip_lib().u2gnn_split_x2(_p(src), int(ld_src), _p(dst2), int(ld_dst2), int(rows), int(cols), _s()),
+          "u2gnn_split_x2")
 
 
 def window_attn_fwd(QKV, W, dp, O, Psave, p, seed, n_nodes, rows_pad):

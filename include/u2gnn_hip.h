@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define U2GNN_ABI_VERSION 2
+#define U2GNN_ABI_VERSION 3
 
 #define U2GNN_OK 0
 #define U2GNN_E_ARG (-1)    /* bad size / null pointer */
@@ -46,6 +46,17 @@ extern "C" {
 #define U2GNN_EPI_ATTN_DS_SIGNED 7  /* aux0 = x, the signed probability image of
                                        u2gnn_attn_softmax_fwd (P == NULL): C = x*(acc - (1-p)*rowvec[m])
                                        where x >= +0 (kept), C = x*rowvec[m] where x <= -0 (dropped) */
+#define U2GNN_EPI_ATTN_DS_RECOMP 8  /* aux0 = S (the saved scores), rowstat[m] = (row max, 1/row sum) of
+                                       u2gnn_attn_softmax_x2_fwd: P = exp(S - max) * (1/sum) (0 for
+                                       m >= m_valid or n >= n_valid), keep = dropout hash (seed, m, n);
+                                       C = P * (keep * acc/(1-p) - rowvec[m]) */
+
+/* x2 operand format (pre-split fp32): a logical fp32 matrix X[R][C] (C % 8 == 0) is stored as
+ * bf16 X2[R][2C] with, per 8-column group g, hi(X[r][8g..8g+7]) then lo(X[r][8g..8g+7]),
+ * hi = bf16_rne(x), lo = bf16_rne(x - hi).  Leading dimensions of x2 matrices are in bf16
+ * elements (>= 2C, multiple of 16).  The bf16x3 product hi*hi + hi*lo + lo*hi of two x2 operands
+ * is the one the BF16X3 kernels form after splitting fp32 operands themselves, so an x2 GEMM
+ * is bit-identical to the fp32-operand BF16X3 GEMM on the same 256x128 / 128x128 tile. */
 
 /* Matrix-core precision of a GEMM (u2gnn_gemm_args.precision). */
 #define U2GNN_PREC_F32 0    /* v_mfma_f32_32x32x2_f32: exact fp32 fma chains            */
@@ -84,6 +95,16 @@ typedef struct u2gnn_gemm_args {
     int32_t clamp_a;      /* 1: A elements below +0 are read as 0 (the signed probability image as Pd
                              for P.V and dP^T.dO); STORE epilogue and trans_b = 0 only */
     int32_t reserved;
+    /* ---- ABI v3: pre-split (x2) operands and outputs ---- */
+    int32_t a_x2, b_x2;   /* 1: A (B) is an x2 bf16 matrix (A2 / B2, lda / ldb in bf16 elements);
+                             both or neither; requires BF16X3 and tile 256 or 128 */
+    const void *A2;
+    const void *B2;
+    void *Cx2;            /* non-NULL: the epilogue result is also (C == NULL: only) written in x2
+                             format, ldcx2 bf16 elements per row; split_k must be 1 */
+    int64_t ldcx2;
+    const float *rowstat; /* ATTN_DS_RECOMP: [M][2] (row max, 1/row sum) */
+    int64_t m_valid, n_valid;   /* ATTN_DS_RECOMP: real rows / keys */
 } u2gnn_gemm_args;
 
 /* ---- library ------------------------------------------------------------------ */
@@ -144,6 +165,16 @@ int u2gnn_attn_softmax_fwd(const float *S, int64_t lds, float *P, float *Pd, int
                            int64_t rows_valid, int64_t rows_pad, int64_t n_valid, int64_t n_pad,
                            float p, uint64_t seed, uint32_t *keep, int64_t ld_keep, void *stream);
 /* delta[i] = sum_c A[i,c]*B[i,c]  (rowsum(dO * O) of the attention backward) */
+/* The same softmax + dropout for the pre-split attention path: Pd2 = x2(Pd) (Pd = P/(1-p) where kept,
+ * 0 where dropped; ldp2 bf16 elements per row, n_pad % 8 == 0) and rowstat[i] = (row max, 1/row sum)
+ * over the n_valid keys ((0, 0) for padded rows), from which the ATTN_DS_RECOMP epilogue recomputes
+ * P exactly. */
+int u2gnn_attn_softmax_x2_fwd(const float *S, int64_t lds, void *Pd2, int64_t ldp2, float *rowstat,
+                              int64_t rows_valid, int64_t rows_pad, int64_t n_valid, int64_t n_pad,
+                              float p, uint64_t seed, void *stream);
+/* dst2 = x2(src) over rows x cols (cols % 8 == 0; ld_dst2 in bf16 elements) */
+int u2gnn_split_x2(const float *src, int64_t ld_src, void *dst2, int64_t ld_dst2, int64_t rows, int64_t cols,
+                   void *stream);
 int u2gnn_rowdot(const float *A, int64_t lda, const float *B, int64_t ldb, float *out, int64_t rows,
                  int64_t cols, void *stream);
 

@@ -73,7 +73,8 @@ if reddit:
     feature_dim_size = 4
 train_store = GraphStore(train_graphs, reddit_tile=4 if reddit else 0)
 test_store = GraphStore(test_graphs, reddit_tile=4 if reddit else 0)
-batch_nodes = BatchLoader(train_store, args.batch_size, args.num_neighbors)
+# native assembly; node features gathered on the GPU from a device-resident copy (DeviceBatch.from_store)
+batch_nodes = BatchLoader(train_store, args.batch_size, args.num_neighbors, gather_x=False)
 print("Loading data... finished!")
 
 model = TransformerU2GNN(feature_dim_size=feature_dim_size, ff_hidden_size=args.ff_hidden_size,
@@ -83,7 +84,12 @@ model = TransformerU2GNN(feature_dim_size=feature_dim_size, ff_hidden_size=args.
 num_batches_per_epoch = int((len(train_graphs) - 1) / args.batch_size) + 1
 
 
+train_X = torch.from_numpy(train_store.X).to(device)
+
+
 def to_device(hb):
+    if hb.X_concat is None:
+        return DeviceBatch.from_store(hb, train_X, device=device)
     return DeviceBatch.from_offsets(hb.input_x, hb.offsets, hb.X_concat, hb.labels, device=device)
 
 

@@ -71,8 +71,10 @@ reddit = "REDDIT" in args.dataset
 if reddit:
     feature_dim_size = 4
 store = GraphStore(graphs, reddit_tile=4 if reddit else 0)
+store_X = torch.from_numpy(store.X).to(device)
 vocab_size = int(store.node_start[-1])
-batch_nodes = BatchLoader(store, args.batch_size, args.num_neighbors, with_input_y=True)
+# native assembly; node features gathered on the GPU from a device-resident copy (DeviceBatch.from_store)
+batch_nodes = BatchLoader(store, args.batch_size, args.num_neighbors, with_input_y=True, gather_x=False)
 print("Loading data... finished!")
 
 model = TransformerU2GNN(feature_dim_size=feature_dim_size, ff_hidden_size=args.ff_hidden_size,
@@ -94,7 +96,7 @@ def train():
         if args.max_steps and steps_done >= args.max_steps:
             break
         hb = batch_nodes()
-        b = DeviceBatch.from_offsets(hb.input_x, hb.offsets, hb.X_concat, None, device=device, input_y=hb.input_y)
+        b = DeviceBatch.from_store(hb, store_X, device=device)
         sid = torch.from_numpy(model.ss.draw_samples()).to(device)
         total_loss += trainer.step(b, sid).item()
         steps_done += 1

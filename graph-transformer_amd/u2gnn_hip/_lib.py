@@ -136,6 +136,7 @@ _LUS_SIGS = {
     "u2gnn_lus_probability": ([VP, I64], c_float),
     "u2gnn_lus_sample_unique": ([VP, c_size_t, VP, c_size_t, VP], c_int32),
     "u2gnn_lus_accidental_matches": ([VP, c_size_t, VP, c_size_t, VP, c_size_t, POINTER(c_size_t)], c_int32),
+    "u2gnn_batch_assemble": ([VP, POINTER(c_int32), VP, I64, VP, VP, VP, VP, VP, I32, I64, VP, VP, VP], c_int32),
 }
 
 _hip = None

@@ -23,6 +23,19 @@ from .engine import (SITE_ATTN, SITE_DROP1, SITE_DROP2, SITE_DROPFF, SITE_HEAD, 
                      OffPath, encoder_layer_backward, encoder_layer_forward, rup, site_seed)
 
 
+_IOTA = {}
+
+
+def _pool_iota(N: int, dev: torch.device):
+    """graph_pool's column indices (0..N-1) and values (ones) as views of cached device buffers."""
+    key = (dev.type, dev.index)
+    c = _IOTA.get(key)
+    if c is None or c[0].numel() < N:
+        n = max(N, 1 << 14, 2 * (c[0].numel() if c is not None else 0))
+        c = _IOTA[key] = (torch.arange(n, device=dev, dtype=torch.int64), torch.ones(n, device=dev, dtype=torch.float32))
+    return c[0][:N], c[1][:N]
+
+
 @dataclass
 class DeviceBatch:
     N: int
@@ -53,6 +66,37 @@ class DeviceBatch:
         iy = None if input_y is None else torch.as_tensor(input_y, dtype=torch.int64).to(dev, non_blocking=True)
         return DeviceBatch(N, B, ix, X, off.to(dev), torch.arange(N, device=dev, dtype=torch.int64),
                            torch.ones(N, device=dev, dtype=torch.float32), lab, iy)
+
+    @staticmethod
+    def from_store(hb, X_dev: torch.Tensor, device="cuda"):
+        """A natively assembled batch (GraphStore.assemble(..., gather_x=False)) -> HBM: input_x, offsets
+        and the rows' dataset node ids cross PCIe asynchronously from page-locked buffers (~0.7 MB at
+        C4 instead of the 7 MB X_concat; BatchLoader assembles straight into a ring of them);
+        X_concat is gathered on the GPU from the dataset's device-resident features X_dev [V, d]
+        (u2gnn_gather_rows).  No host synchronisation."""
+        from . import kernels as K
+        dev = torch.device(device)
+        N, B = int(hb.offsets[-1]), len(hb.offsets) - 1
+        slot = getattr(hb, "pinned", None)
+        if slot is not None:
+            k1 = hb.input_x.shape[1]
+            h2d = lambda t: t.to(dev, non_blocking=True)  # noqa: E731
+            ix = h2d(slot.ix[:N * k1]).view(N, k1)
+            gnode, off, lab = h2d(slot.gnode[:N]), h2d(slot.offsets[:B + 1]), h2d(slot.labels[:B])
+            slot.event = torch.cuda.Event()
+            slot.event.record()
+            iy = gnode if hb.input_y is not None else None   # UnSup labels = dataset node ids
+        else:
+            pin = lambda a: torch.from_numpy(np.ascontiguousarray(a)).pin_memory().to(dev, non_blocking=True)  # noqa: E731
+            ix, gnode, off = pin(hb.input_x), pin(hb.gnode), pin(np.asarray(hb.offsets, dtype=np.int64))
+            lab = None if hb.labels is None else pin(np.asarray(hb.labels, dtype=np.int64))
+            iy = None if hb.input_y is None else pin(np.asarray(hb.input_y, dtype=np.int64))
+        d = X_dev.shape[1]
+        X = torch.empty(N, d, device=dev, dtype=torch.float32)
+        if N:
+            K.gather_rows(X_dev, gnode, 1, X, N, N, d, d)
+        colidx, vals = _pool_iota(N, dev)
+        return DeviceBatch(N, B, ix, X, off, colidx, vals, lab, iy)
 
     @staticmethod
     def from_reference_inputs(input_x, graph_pool, X_concat, labels=None):

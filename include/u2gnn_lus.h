@@ -1,6 +1,6 @@
 /*
- * u2gnn_lus.h — C ABI of libu2gnn_lus.so, the host-side log-uniform sampler used by the
- * sampled-softmax loss.  Replaces the reference's C++ class + Cython binding:
+ * u2gnn_lus.h — C ABI of libu2gnn_lus.so, the host-side natives: the log-uniform sampler used by
+ * the sampled-softmax loss, and the batch assembler (end of file).  Replaces the reference's C++ class + Cython binding:
  *   Log_Uniform_Sampler.h:9-24 / Log_Uniform_Sampler.cpp:10-88 and log_uniform.pyx:16-40
  *   (U2GNN_pytorch/log_uniform/), called from sampled_softmax.py:31.
  * Same engine (std::default_random_engine = minstd_rand0, seed 1111 by default), same
@@ -36,6 +36,22 @@ int u2gnn_lus_sample_unique(void *h, size_t size, const int64_t *excluded, size_
  * written to out_pairs[2*k], out_pairs[2*k+1]; *n_out = number of pairs; capacity in pairs. */
 int u2gnn_lus_accidental_matches(const int64_t *labels, size_t n_labels, const int64_t *samples,
                                  size_t n_samples, int64_t *out_pairs, size_t capacity, size_t *n_out);
+
+/* ---- host batch assembly (csrc/batch_assembly.cpp) -----------------------------------
+ * get_batch_data / Batch_Loader (train_pytorch_U2GNN_Sup.py:99-126, train_pytorch_U2GNN_UnSup.py:
+ * 101-134) for the graphs `ids` (a permutation prefix drawn by the caller): offsets [n_ids+1],
+ * input_x [N, k+1] (row i: i, then k neighbours drawn with replacement, as batch rows; isolated
+ * nodes repeat i) and gnode [N] (dataset-global node id of each row).  The neighbour draws continue
+ * numpy's legacy MT19937 global stream given as (mt_key[624], *mt_pos) from np.random.get_state()
+ * exactly as np.random.randint(0, deg[:, None], size=(n, k)) over the non-isolated nodes does
+ * (masked rejection on 32-bit outputs); the advanced state is written back in place.  Graph g owns
+ * global nodes node_start[g] .. +n_nodes[g]; node v's neighbours (ids local to its graph, in the
+ * reference's edge order) are nbr[nbr_start[v] .. + deg[v]].  n_cap: rows available in input_x /
+ * gnode.  Returns 0, or -1 for a bad argument / N > n_cap. */
+int u2gnn_batch_assemble(uint32_t *mt_key, int32_t *mt_pos, const int64_t *ids, int64_t n_ids,
+                         const int64_t *n_nodes, const int64_t *node_start, const int64_t *deg,
+                         const int64_t *nbr_start, const int64_t *nbr, int32_t k, int64_t n_cap,
+                         int64_t *offsets, int64_t *input_x, int64_t *gnode);
 
 #ifdef __cplusplus
 }

@@ -174,3 +174,49 @@ def test_synthetic_collab_statistics():
     for g in range(20):
         rows = b.input_x[off[g]:off[g + 1]]
         assert rows.min() >= off[g] and rows.max() < off[g + 1]
+
+
+def test_native_assembly_equals_numpy_form_and_stream():
+    """csrc/batch_assembly.cpp continues numpy's MT19937 stream exactly like the numpy randint form:
+    same input_x / offsets / X and the same generator state afterwards (isolated nodes, degree 1,
+    degrees past 2^16 so that the rejection mask spans 17 bits, k = 0)."""
+    from u2gnn_hip.batching import GraphStore
+
+    class G:
+        def __init__(self, n, src, dst, label):
+            self.n, self.label = n, label
+            self.edge_mat = np.stack([src, dst]).astype(np.int64)
+            self.node_features = np.eye(5, dtype=np.float32)[np.arange(n) % 5]
+
+    rs = np.random.RandomState(7)
+    graphs = []
+    for gi in range(40):
+        n = int(rs.randint(1, 60))
+        m = int(rs.randint(0, 4 * n))
+        src, dst = rs.randint(0, n, m), rs.randint(0, n, m)
+        graphs.append(G(n, np.concatenate([src, dst]), np.concatenate([dst, src]), gi % 3))
+    hub = 70000                                   # one node with 70000 (multi-)edges
+    graphs.append(G(3, np.concatenate([np.zeros(hub, np.int64), [1]]), np.concatenate([np.ones(hub, np.int64), [0]]),
+                    1))
+    store = GraphStore(graphs)
+    for k in (0, 1, 16):
+        for seed in (0, 1):
+            np.random.seed(seed)
+            ref = []
+            for _ in range(5):
+                sel = np.random.permutation(len(graphs))[:12]
+                ref.append(store.assemble_numpy(sel, k))
+            st_ref = np.random.get_state()
+            np.random.seed(seed)
+            for r in ref:
+                sel = np.random.permutation(len(graphs))[:12]
+                b = store.assemble(sel, k)
+                assert np.array_equal(b.input_x, r.input_x) and np.array_equal(b.offsets, r.offsets)
+                assert np.array_equal(b.X_concat, r.X_concat) and np.array_equal(b.labels, r.labels)
+            st = np.random.get_state()
+            assert np.array_equal(st[1], st_ref[1]) and st[2] == st_ref[2]
+    np.random.seed(3)                             # a batch holding the hub node
+    a = store.assemble([40, 2], 16)
+    np.random.seed(3)
+    b = store.assemble_numpy([40, 2], 16)
+    assert np.array_equal(a.input_x, b.input_x)

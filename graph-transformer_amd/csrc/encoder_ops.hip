@@ -59,39 +59,49 @@ __global__ void __launch_bounds__(256) slab_reduce_kernel(const float *src, int 
                                                           int64_t rbp, int64_t rbr, int64_t cbp, int64_t cbr,
                                                           float *dst, int64_t ld_dst, float alpha, int accumulate,
                                                           int vec_store) {
-    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    if (r >= rows_pad) return;
+    // one float4 of the output per thread (weight-gradient outputs have only d or ff rows: a wave per
+    // row left the chip latency-bound); 8 slab loads in flight, summed in the fixed order
+    // a += s0, s4, ...; b += s1, s5, ...; e += s2, ...; f += s3, ...; then (a + b) + (e + f)
+    const int64_t c4 = cols_pad >> 2;
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= rows_pad * c4) return;
+    const int64_t r = i / c4, c = (i - r * c4) * 4;
     bool vr;
     const int64_t rr = blk_map(r, rbp, rbr, &vr);
     if (!vr) return;
-    for (int64_t c = (int64_t)lane * 4; c < cols_pad; c += 256) {
-        const float *p = src + r * ld_src + c;
-        float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a, e = a, f = a;
-        int z = 0;
-        for (; z + 4 <= n_slab; z += 4) {
-            a = add4(a, ld4(p + (int64_t)z * slab_stride));
-            b = add4(b, ld4(p + (int64_t)(z + 1) * slab_stride));
-            e = add4(e, ld4(p + (int64_t)(z + 2) * slab_stride));
-            f = add4(f, ld4(p + (int64_t)(z + 3) * slab_stride));
-        }
-        for (; z < n_slab; ++z) a = add4(a, ld4(p + (int64_t)z * slab_stride));
-        const float4 t = add4(add4(a, b), add4(e, f));
-        if (vec_store) {
-            float *o = dst + rr * ld_dst + c;
-            float4 v = make_float4(alpha * t.x, alpha * t.y, alpha * t.z, alpha * t.w);
-            if (accumulate) v = add4(v, ld4(o));
-            *reinterpret_cast<float4 *>(o) = v;
-        } else {
-            const float x[4] = {t.x, t.y, t.z, t.w};
+    const float *p = src + r * ld_src + c;
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a, e = a, f = a;
+    int z = 0;
+    for (; z + 8 <= n_slab; z += 8) {
+        float4 l[8];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                bool vc;
-                const int64_t cc = blk_map(c + q, cbp, cbr, &vc);
-                if (!vc) continue;
-                float *o = dst + rr * ld_dst + cc;
-                *o = accumulate ? *o + alpha * x[q] : alpha * x[q];
-            }
+        for (int q = 0; q < 8; ++q) l[q] = ld4(p + (int64_t)(z + q) * slab_stride);
+        a = add4(a, l[0]), b = add4(b, l[1]), e = add4(e, l[2]), f = add4(f, l[3]);
+        a = add4(a, l[4]), b = add4(b, l[5]), e = add4(e, l[6]), f = add4(f, l[7]);
+    }
+    if (z + 4 <= n_slab) {
+        float4 l[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) l[q] = ld4(p + (int64_t)(z + q) * slab_stride);
+        a = add4(a, l[0]), b = add4(b, l[1]), e = add4(e, l[2]), f = add4(f, l[3]);
+        z += 4;
+    }
+    for (; z < n_slab; ++z) a = add4(a, ld4(p + (int64_t)z * slab_stride));
+    const float4 t = add4(add4(a, b), add4(e, f));
+    if (vec_store) {
+        float *o = dst + rr * ld_dst + c;
+        float4 v = make_float4(alpha * t.x, alpha * t.y, alpha * t.z, alpha * t.w);
+        if (accumulate) v = add4(v, ld4(o));
+        *reinterpret_cast<float4 *>(o) = v;
+    } else {
+        const float x[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            bool vc;
+            const int64_t cc = blk_map(c + q, cbp, cbr, &vc);
+            if (!vc) continue;
+            float *o = dst + rr * ld_dst + cc;
+            *o = accumulate ? *o + alpha * x[q] : alpha * x[q];
         }
     }
 }
@@ -177,7 +187,15 @@ __global__ void __launch_bounds__(256) colsum_final_kernel(const float *ws, int6
     const int64_t c = (int64_t)blockIdx.x * FIN_COLS + cl;
     float s[2] = {0.f, 0.f};
     if (c < cols_pad) {
+        // chunks kg, kg+16, kg+32, ... alternate between s[0] and s[1]; 8 loads in flight
         int64_t k = kg;
+        for (; k + 112 < n_chunks; k += 128) {
+            float l[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) l[q] = ws[(k + 16 * q) * cols_pad + c];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) s[q & 1] += l[q];
+        }
         for (; k + 16 < n_chunks; k += 32) {
             s[0] += ws[k * cols_pad + c];
             s[1] += ws[(k + 16) * cols_pad + c];
@@ -572,13 +590,25 @@ __global__ void __launch_bounds__(256) ln_param_reduce_kernel(const float *ws, i
     const int cl = threadIdx.x % FIN_COLS, kg = threadIdx.x / FIN_COLS;
     const int64_t c = (int64_t)blockIdx.x * FIN_COLS + cl;
     float a = 0.f, b = 0.f, e = 0.f;
-    if (c < d)
-        for (int64_t k = kg; k < n_chunks; k += 16) {
+    if (c < d) {
+        int64_t k = kg;
+        for (; k + 48 < n_chunks; k += 64) {   // 12 loads in flight, same add order
+            float l[4][3];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float *q = ws + (k + 16 * j) * 3 * d_pad + c;
+                l[j][0] = q[0], l[j][1] = q[d_pad], l[j][2] = q[2 * d_pad];
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) a += l[j][0], b += l[j][1], e += l[j][2];
+        }
+        for (; k < n_chunks; k += 16) {
             const float *q = ws + k * 3 * d_pad + c;
             a += q[0];
             b += q[d_pad];
             e += q[2 * d_pad];
         }
+    }
     red[0][kg][cl] = a;
     red[1][kg][cl] = b;
     red[2][kg][cl] = e;
@@ -655,7 +685,7 @@ int u2gnn_slab_reduce(const float *src, int32_t n_slab, int64_t slab_stride, int
     if (!al16(src) || (cols_pad & 3) || (ld_src & 3) || (slab_stride & 3)) return U2GNN_E_ALIGN;
     if (rows_pad == 0 || cols_pad == 0) return U2GNN_OK;
     const int vec_store = cblk_pad == cblk_real && al16(dst) && (ld_dst & 3) == 0;
-    hipLaunchKernelGGL(slab_reduce_kernel, dim3(grid_for(rows_pad, 4, 1 << 30)), dim3(256), 0,
+    hipLaunchKernelGGL(slab_reduce_kernel, dim3(grid_for(rows_pad * (cols_pad / 4), 256, 1 << 30)), dim3(256), 0,
                        u2gnn_stream(stream), src, n_slab, slab_stride, rows_pad, cols_pad, ld_src, rblk_pad, rblk_real,
                        cblk_pad, cblk_real, dst, ld_dst, alpha, accumulate, vec_store);
     return u2gnn_launch_status();

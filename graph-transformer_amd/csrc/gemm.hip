@@ -389,7 +389,7 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_bf16_kernel(GemmP P) {
     };
 
     PreDS<TN> pre;
-    const bool use_pre = EPI == U2GNN_EPI_ATTN_DS && P.keep != nullptr;
+    const bool use_pre = (EPI == U2GNN_EPI_ATTN_DS && P.keep != nullptr) || EPI == U2GNN_EPI_ATTN_DS_SIGNED;
     if (use_pre) prefetch_ds<EPI>(P, m0 + wm * WTM + li, n0 + wn * WTN, kh, pre);
     if (nk > 0) {
         // two register stages: every tile's global loads are in flight across TWO compute phases
@@ -514,7 +514,8 @@ extern "C" int u2gnn_gemm(const u2gnn_gemm_args *a, void *stream) {
         if (!al16(a->A) || !al16(a->B) || (a->lda & 3) || (a->ldb & 3)) return U2GNN_E_ALIGN;
     }
     const int bk = (prec == U2GNN_PREC_F32 || a->tile == 129 ||
-                    (x2 && (a->tile == 257 || a->tile == 128 || a->tile == 258 || a->tile == 260)))
+                    (x2 && (a->tile == 257 || a->tile == 128 || a->tile == 258 || a->tile == 260 || a->tile == 262 ||
+                           a->tile == 263)))
                        ? 16 : 32;   // K step of the kernel
     if (a->K % bk) return U2GNN_E_SHAPE;
     if (prec != U2GNN_PREC_F32 && !x2) {   // bf16 staging addresses operands by 32-bit buffer offsets
@@ -550,11 +551,11 @@ extern "C" int u2gnn_gemm(const u2gnn_gemm_args *a, void *stream) {
         tile = (can128 && blocks128 >= 480) ? 128 : 64;
     }
     // tile codes: 64, 128 (square), 256 (256x128, 8 waves), 129 (128x128 with a 16-deep K step)
-    const bool x2code = x2 && (tile == 257 || tile == 130 || (tile >= 258 && tile <= 260));
+    const bool x2code = x2 && (tile == 257 || tile == 130 || (tile >= 258 && tile <= 263));
     if (!x2code && tile != 64 && tile != 128 && tile != 256 && tile != 129) return U2GNN_E_ARG;
     if ((tile == 256 || tile == 129) && prec == U2GNN_PREC_F32) return U2GNN_E_ARG;
     const int tm_ = tile == 129 ? 128 : (tile > 256 ? 256 : (tile == 130 ? 128 : tile));
-    const int tile_n = tile == 260 ? 256 : (tm_ == 256 ? 128 : tm_);
+    const int tile_n = (tile == 260 || tile == 262) ? 256 : (tm_ == 256 ? 128 : tm_);
     if (a->M % tm_ || a->N % tile_n) return U2GNN_E_SHAPE;
     GemmP P;
     std::memset(&P, 0, sizeof(P));

@@ -210,33 +210,49 @@ template <int EPI, int TN>
 __device__ __forceinline__ void prefetch_ds(const GemmP &P, int row, int c0, int kh, PreDS<TN> &f) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-        f.kw[j] = P.keep[(int64_t)row * P.ld_keep + ((c0 + j * 32) >> 5)];
+        f.kw[j] = EPI == U2GNN_EPI_ATTN_DS ? P.keep[(int64_t)row * P.ld_keep + ((c0 + j * 32) >> 5)] : 0u;
 #pragma unroll
         for (int g = 0; g < 4; ++g) f.p[j][g] = ld4(P.aux0 + (int64_t)row * P.ld_aux + c0 + j * 32 + 8 * g + 4 * kh);
     }
     f.dl = P.rowvec[row];
 }
 
+template <int EPI, int TN>
+__device__ __forceinline__ void slice_from_pre(const PreDS<TN> &pre, int kh, EpiSlice<EPI, TN> &e) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            e.a[j][g] = pre.p[j][g];
+            e.b[j][g] = make_float4(0.f, 0.f, 0.f, 0.f);
+            e.kb[j][g] = pre.kw[j] >> ((8 * g + 4 * kh) & 31);
+        }
+    e.dl = pre.dl;
+    e.rm = e.rinv = 0.f;
+}
+
 template <int EPI, int TM, int TN>
 __device__ __forceinline__ void store_tile(const GemmP &P, float *C, const f32x16 (&acc)[TM][TN], int r0, int c0,
                                            int li, int kh, const PreDS<TN> *pre) {
+    if constexpr (EPI == U2GNN_EPI_ATTN_DS_SIGNED) {
+        // every slice's probability image is requested before the first store (slice 0 usually
+        // prefetched before the main loop): one exposed round trip per tile instead of one per slice
+        EpiSlice<EPI, TN> e[TM];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            if (i == 0 && pre) slice_from_pre<EPI>(*pre, kh, e[i]);
+            else fetch_slice<EPI>(P, r0 + i * 32 + li, c0, kh, e[i]);
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i) store_slice<EPI>(P, C, acc, i, r0 + i * 32 + li, c0, kh, e[i]);
+        return;
+    }
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
         const int row = r0 + i * 32 + li;
         EpiSlice<EPI, TN> e;
-        if (i == 0 && pre) {
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-#pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    e.a[j][g] = pre->p[j][g];
-                    e.b[j][g] = make_float4(0.f, 0.f, 0.f, 0.f);
-                    e.kb[j][g] = pre->kw[j] >> ((8 * g + 4 * kh) & 31);
-                }
-            e.dl = pre->dl;
-        } else {
-            fetch_slice<EPI>(P, row, c0, kh, e);
-        }
+        if (i == 0 && pre) slice_from_pre<EPI>(*pre, kh, e);
+        else fetch_slice<EPI>(P, row, c0, kh, e);
         store_slice<EPI>(P, C, acc, i, row, c0, kh, e);
     }
 }

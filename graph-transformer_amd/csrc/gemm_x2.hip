@@ -110,7 +110,7 @@ __device__ __forceinline__ void wait_vm() {
     else static_assert(N_ == 0, "add the vmcnt literal");
 }
 
-template <int BM, int BN, int WM, int WN, int BK, int NS, int MINB, bool TA, bool TB, int EPI>
+template <int BM, int BN, int WM, int WN, int BK, int NS, int MINB, bool PP, bool TA, bool TB, int EPI>
 __global__ void __launch_bounds__(64 * WM * WN, MINB) gemm_x2_kernel(GemmP P) {
     constexpr int NT = 64 * WM * WN;
     constexpr int WTM = BM / WM, WTN = BN / WN;        // wave tile
@@ -120,6 +120,7 @@ __global__ void __launch_bounds__(64 * WM * WN, MINB) gemm_x2_kernel(GemmP P) {
     constexpr int NIA = AB / (16 * NT), NIB = BB / (16 * NT), NI = NIA + NIB;
     static_assert(NIA * 16 * NT == AB && NIB * 16 * NT == BB, "tile not a multiple of the DMA footprint");
     static_assert(NS == 2 || NS == 3, "2 or 3 LDS stages");
+    static_assert(!PP || (NS == 3 && WM * WN == 8), "ping-pong: 8 waves, 3 stages");
     __shared__ __attribute__((aligned(1024))) char smem[NS * STAGE];
 
     const int tid = threadIdx.x;
@@ -178,6 +179,64 @@ __global__ void __launch_bounds__(64 * WM * WN, MINB) gemm_x2_kernel(GemmP P) {
         }
     };
 
+    if constexpr (PP) {
+        // Ping-pong schedule: waves 0-3 and 4-7 (one of each on every SIMD) run the same
+        // load-phase / MFMA-phase loop one barrier apart, so each SIMD's matrix pipe alternates
+        // between its two waves while the other one reads its next fragments.  Per K step t:
+        //   load phase: issue tile t+2 (stage (t+2)%3, last read as tile t-1), ds_read all of
+        //               tile t, wait for this thread's DMA of tile t+1 and its own LDS reads, barrier
+        //   MFMA phase: 3 x TM x TN x BK/16 MFMAs at raised priority, barrier
+        // Hazards (global barrier index: group 0 code barrier c = global c, group 1 = c + 1):
+        //   RAW  tile t+1 is first read after global 2t+2; every thread waited for its share of it
+        //        before global 2t+1 (group 0) / 2t+2 (group 1)
+        //   WAR  tile t-1 reads completed (lgkmcnt(0)) before global 2t-1 / 2t; stage (t-1)%3 is
+        //        restaged after global 2t / 2t+1
+        const bool g1 = w >= 4;
+        if (0 < nk) issue(0, 0);
+        if (1 < nk) issue(1, 1);
+        if (1 < nk) wait_vm<NI>();
+        else wait_vm<0>();
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (g1) {
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+        }
+        for (int t = 0; t < nk; ++t) {
+            if (t + 2 < nk) issue(t + 2, (t + 2) % 3);
+            const char *Ai = smem + (t % 3) * STAGE, *Bi = Ai + AB;
+            bf16x8 ah[BK / 16][TM], al[BK / 16][TM], bh[BK / 16][TN], bl[BK / 16][TN];
+#pragma unroll
+            for (int ks = 0; ks < BK / 16; ++ks) {
+#pragma unroll
+                for (int i = 0; i < TM; ++i) x2_frag<BM, BK, KRA>(Ai, wm * WTM + i * 32, ks, lane, ah[ks][i], al[ks][i]);
+#pragma unroll
+                for (int j = 0; j < TN; ++j) x2_frag<BN, BK, KRB>(Bi, wn * WTN + j * 32, ks, lane, bh[ks][j], bl[ks][j]);
+            }
+            if (t + 2 < nk) wait_vm<NI>();
+            else wait_vm<0>();
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int ks = 0; ks < BK / 16; ++ks)
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) {
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bh[ks][j], al[ks][i], acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bl[ks][j], ah[ks][i], acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bh[ks][j], ah[ks][i], acc[i][j], 0, 0, 0);
+                    }
+            __builtin_amdgcn_s_setprio(0);
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+        }
+        if (!g1) __builtin_amdgcn_s_barrier();   // same barrier count in both groups
+    } else {
 #pragma unroll
     for (int s = 0; s < NS - 1; ++s)
         if (s < nk) issue(s, s);
@@ -194,6 +253,7 @@ __global__ void __launch_bounds__(64 * WM * WN, MINB) gemm_x2_kernel(GemmP P) {
         if (t + NS - 1 < nk) issue(t + NS - 1, (t + NS - 1) % NS);
 #endif
         compute(smem + (t % NS) * STAGE);
+    }
     }
 #ifdef X2_EXP_NOSYNC
     wait_vm<0>();
@@ -216,14 +276,18 @@ __global__ void __launch_bounds__(64 * WM * WN, MINB) gemm_x2_kernel(GemmP P) {
 //   258: 256x128, 4 waves of 128x64, BK 16, 3 stages (72 KB, 2 blocks/CU)
 //   259: 256x128, 4 waves of 128x64, BK 32, 2 stages (96 KB, 1 block/CU)
 //   260: 256x256, 8 waves of 128x64, BK 16, 3 stages (96 KB, 1 block/CU)
+//   261 / 262 / 263: the ping-pong schedule (PP) on 256x128 BK 32, 256x256 BK 16, 256x128 BK 16
 template <int CODE> struct X2Cfg;
-template <> struct X2Cfg<256> { static constexpr int BM = 256, BN = 128, WM = 4, WN = 2, BK = 32, NS = 3, MINB = 1; };
-template <> struct X2Cfg<257> { static constexpr int BM = 256, BN = 128, WM = 4, WN = 2, BK = 16, NS = 3, MINB = 2; };
-template <> struct X2Cfg<128> { static constexpr int BM = 128, BN = 128, WM = 2, WN = 2, BK = 16, NS = 3, MINB = 3; };
-template <> struct X2Cfg<130> { static constexpr int BM = 128, BN = 128, WM = 2, WN = 2, BK = 32, NS = 2, MINB = 2; };
-template <> struct X2Cfg<258> { static constexpr int BM = 256, BN = 128, WM = 2, WN = 2, BK = 16, NS = 3, MINB = 2; };
-template <> struct X2Cfg<259> { static constexpr int BM = 256, BN = 128, WM = 2, WN = 2, BK = 32, NS = 2, MINB = 1; };
-template <> struct X2Cfg<260> { static constexpr int BM = 256, BN = 256, WM = 2, WN = 4, BK = 16, NS = 3, MINB = 1; };
+template <> struct X2Cfg<256> { static constexpr int BM = 256, BN = 128, WM = 4, WN = 2, BK = 32, NS = 3, MINB = 1; static constexpr bool PP = false; };
+template <> struct X2Cfg<257> { static constexpr int BM = 256, BN = 128, WM = 4, WN = 2, BK = 16, NS = 3, MINB = 2; static constexpr bool PP = false; };
+template <> struct X2Cfg<128> { static constexpr int BM = 128, BN = 128, WM = 2, WN = 2, BK = 16, NS = 3, MINB = 3; static constexpr bool PP = false; };
+template <> struct X2Cfg<130> { static constexpr int BM = 128, BN = 128, WM = 2, WN = 2, BK = 32, NS = 2, MINB = 2; static constexpr bool PP = false; };
+template <> struct X2Cfg<258> { static constexpr int BM = 256, BN = 128, WM = 2, WN = 2, BK = 16, NS = 3, MINB = 2; static constexpr bool PP = false; };
+template <> struct X2Cfg<259> { static constexpr int BM = 256, BN = 128, WM = 2, WN = 2, BK = 32, NS = 2, MINB = 1; static constexpr bool PP = false; };
+template <> struct X2Cfg<260> { static constexpr int BM = 256, BN = 256, WM = 2, WN = 4, BK = 16, NS = 3, MINB = 1; static constexpr bool PP = false; };
+template <> struct X2Cfg<261> { static constexpr int BM = 256, BN = 128, WM = 4, WN = 2, BK = 32, NS = 3, MINB = 1; static constexpr bool PP = true; };
+template <> struct X2Cfg<262> { static constexpr int BM = 256, BN = 256, WM = 2, WN = 4, BK = 16, NS = 3, MINB = 1; static constexpr bool PP = true; };
+template <> struct X2Cfg<263> { static constexpr int BM = 256, BN = 128, WM = 4, WN = 2, BK = 16, NS = 3, MINB = 1; static constexpr bool PP = true; };
 
 template <int CODE, bool TA, bool TB>
 int x2_launch_epi(const GemmP &P, int epi, int split, hipStream_t st) {
@@ -232,12 +296,12 @@ int x2_launch_epi(const GemmP &P, int epi, int split, hipStream_t st) {
     const dim3 grid(P.gm * P.gn * split), block(NT);
     switch (epi) {
         case U2GNN_EPI_STORE:
-            hipLaunchKernelGGL((gemm_x2_kernel<C::BM, C::BN, C::WM, C::WN, C::BK, C::NS, C::MINB, TA, TB, U2GNN_EPI_STORE>), grid, block,
+            hipLaunchKernelGGL((gemm_x2_kernel<C::BM, C::BN, C::WM, C::WN, C::BK, C::NS, C::MINB, C::PP, TA, TB, U2GNN_EPI_STORE>), grid, block,
                                0, st, P);
             break;
         case U2GNN_EPI_ATTN_DS_RECOMP:
             if constexpr (!TA && TB) {
-                hipLaunchKernelGGL((gemm_x2_kernel<C::BM, C::BN, C::WM, C::WN, C::BK, C::NS, C::MINB, TA, TB, U2GNN_EPI_ATTN_DS_RECOMP>),
+                hipLaunchKernelGGL((gemm_x2_kernel<C::BM, C::BN, C::WM, C::WN, C::BK, C::NS, C::MINB, C::PP, TA, TB, U2GNN_EPI_ATTN_DS_RECOMP>),
                                    grid, block, 0, st, P);
                 break;
             } else {
@@ -263,14 +327,14 @@ inline bool al16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) =
 // called by u2gnn_gemm (gemm.hip) when a_x2 / b_x2 are set; P already holds every common field
 int u2gnn_gemm_x2_dispatch(const u2gnn_gemm_args *a, GemmP &P, int tile, int split, hipStream_t st) {
     if (a->precision != U2GNN_PREC_BF16X3 || !a->a_x2 || !a->b_x2 || !a->A2 || !a->B2) return U2GNN_E_ARG;
-    if (tile != 256 && tile != 257 && tile != 128 && tile != 130 && (tile < 258 || tile > 260)) return U2GNN_E_ARG;
+    if (tile != 256 && tile != 257 && tile != 128 && tile != 130 && (tile < 258 || tile > 263)) return U2GNN_E_ARG;
     if (a->clamp_a) return U2GNN_E_ARG;
     if (!al16(a->A2) || !al16(a->B2) || (a->lda & 15) || (a->ldb & 15)) return U2GNN_E_ALIGN;
-    const int bk = (tile == 256 || tile == 130 || tile == 259) ? 32 : 16;
+    const int bk = (tile == 256 || tile == 130 || tile == 259 || tile == 261) ? 32 : 16;
     if (a->K % bk) return U2GNN_E_SHAPE;
     // DMA sources are 64-bit per-lane pointers: no 32-bit offset limit, but rows must lie inside the
     // operand: the caller guarantees M, N, K multiples of the tile (checked by u2gnn_gemm)
-    const int bm = tile >= 256 ? 256 : 128, bn = tile == 260 ? 256 : 128;
+    const int bm = tile >= 256 ? 256 : 128, bn = (tile == 260 || tile == 262) ? 256 : 128;
     if (a->M % bm || a->N % bn) return U2GNN_E_SHAPE;
     P.gm = (int32_t)(a->M / bm);
     P.gn = (int32_t)(a->N / bn);
@@ -283,5 +347,8 @@ int u2gnn_gemm_x2_dispatch(const u2gnn_gemm_args *a, GemmP &P, int tile, int spl
     if (tile == 258) return x2_launch_layout<258>(P, ta, tb, a->epilogue, split, st);
     if (tile == 259) return x2_launch_layout<259>(P, ta, tb, a->epilogue, split, st);
     if (tile == 260) return x2_launch_layout<260>(P, ta, tb, a->epilogue, split, st);
+    if (tile == 261) return x2_launch_layout<261>(P, ta, tb, a->epilogue, split, st);
+    if (tile == 262) return x2_launch_layout<262>(P, ta, tb, a->epilogue, split, st);
+    if (tile == 263) return x2_launch_layout<263>(P, ta, tb, a->epilogue, split, st);
     return x2_launch_layout<128>(P, ta, tb, a->epilogue, split, st);
 }

@@ -54,7 +54,15 @@ X2_CODES = [(512, 384, 512, False, True, 257, 256, 1), (512, 384, 512, False, Fa
             (512, 384, 512, True, False, 258, 256, 1), (512, 384, 512, False, True, 259, 256, 1),
             (512, 384, 512, False, False, 259, 256, 2), (512, 384, 512, True, False, 259, 256, 1),
             (512, 512, 256, False, True, 260, 256, 1), (512, 512, 512, False, False, 260, 256, 2),
-            (512, 512, 256, True, False, 260, 256, 1)]
+            (512, 512, 256, True, False, 260, 256, 1),
+            # ping-pong schedule (261 = 256x128 BK 32, 262 = 256x256 BK 16, 263 = 256x128 BK 16), incl.
+            # K spans of 1 and 2 tiles (prologue / tail paths) and an empty split
+            (512, 384, 512, False, True, 261, 256, 1), (512, 384, 512, False, False, 261, 256, 3),
+            (512, 384, 512, True, False, 261, 256, 2), (512, 384, 64, False, True, 261, 256, 1),
+            (512, 384, 32, False, False, 261, 256, 1), (512, 384, 96, True, False, 261, 256, 4),
+            (512, 512, 256, False, True, 262, 256, 1), (512, 512, 512, False, False, 262, 256, 2),
+            (512, 512, 256, True, False, 262, 256, 1), (512, 384, 512, False, True, 263, 256, 1),
+            (512, 384, 512, False, False, 263, 256, 3), (512, 384, 48, True, False, 263, 256, 2)]
 
 
 @pytest.mark.parametrize("M,N,Kd,ta,tb,tile,split", CASES)

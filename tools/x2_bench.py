@@ -47,7 +47,7 @@ def main():
     ld3, ld3x = 3 * dp, QKV2.stride(0)
     rows = []
 
-    CODES = [int(c) for c in os.environ.get("XB_CODES", "256,257,128,130").split(",")]
+    CODES = [int(c) for c in os.environ.get("XB_CODES", "256,130,261,263").split(",")]
 
     def row(name, fa, fb):
         ta = timeit(fa)

@@ -146,6 +146,7 @@ def main_c5(args):
     t0 = time.perf_counter()
     for i in range(args.steps):
         trainer.step(*batches[(args.warmup + i) % nb])
+    t_issue = time.perf_counter() - t0          # host time to enqueue the K steps
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     loss = float(trainer.loss.item())
@@ -177,7 +178,8 @@ def main_c5(args):
                                   "ff_hidden_size=1024, sampled_num=512, D=4",
                       "global_batch": 4, "mean_nodes_per_batch": round(mean_N, 1), "parallelism": "dp1",
                       "precision": args.precision},
-           "final_loss": round(loss, 4), "roofline": roof, "cpu_baseline": None}
+           "final_loss": round(loss, 4), "host_issue_ms_per_step": round(1e3 * t_issue / args.steps, 3),
+           "roofline": roof, "cpu_baseline": None}
     print(json.dumps(out), flush=True)
 
 

@@ -214,7 +214,35 @@ struct Side {
         if (e == hipSuccess) e = e2;
         return e == hipSuccess ? U2GNN_OK : (int)e;
     }
+    // the main stream waits for everything issued on the side stream so far
+    int join() {
+        if (plan || side == main) return U2GNN_OK;
+        hipEvent_t ev;
+        hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+        if (e != hipSuccess) return (int)e;
+        e = hipEventRecord(ev, side);
+        if (e == hipSuccess) e = hipStreamWaitEvent(main, ev, 0);
+        const hipError_t e2 = hipEventDestroy(ev);
+        if (e == hipSuccess) e = e2;
+        return e == hipSuccess ? U2GNN_OK : (int)e;
+    }
 };
+
+// dV = Pd^T dO runs on the side stream beside the dS -> dQ -> dK chain (fills the CUs the
+// 228-block split-K launches and the launch tails leave idle: -1.4 % step time, measured);
+// U2GNN_DV_SIDE=0 keeps it on the main stream.  U2GNN_DK_SIDE=1 also moves dK = dS^T Q there.
+bool env_flag(const char *name, bool dflt) {
+    const char *e = std::getenv(name);
+    return e && e[0] ? e[0] == '1' : dflt;
+}
+bool dv_side_on() {
+    static const bool v = env_flag("U2GNN_DV_SIDE", true);
+    return v;
+}
+bool dk_side_on() {
+    static const bool v = env_flag("U2GNN_DK_SIDE", false);
+    return v;
+}
 
 int layer_fwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seeds *s, const float *X, float *X2,
               Arena &CA, Arena &W, bool need_ctx, hipStream_t st) {
@@ -284,7 +312,8 @@ int layer_fwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
 }
 
 int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seeds *s, const float *X, Arena &CA,
-              const float *dX2, float *dX, const u2gnn_layer_grads *g, Arena &W, hipStream_t st, hipStream_t side_st) {
+              const float *dX2, float *dX, const u2gnn_layer_grads *g, Arena &W, hipStream_t st, hipStream_t side_st,
+              bool need_dx = true) {
     const int64_t N = D.N, Np = D.Np, d = D.d, dp = D.dp, ff = D.ff, ffp = D.ffp;
     const int prec = D.prec;
     const float pd = s->p_drop;
@@ -320,6 +349,10 @@ int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
     U2GNN_TRY(bias_grad(W, dH, Np, ffp, ffp, ffp, ff, g->l1_b, so));
     // LN1 backward -> dX (residual), dA (dropout1 branch); norm1 + out_proj.bias grads (side)
     float *dA = W.take<float>(Np * dp);
+    // no input gradient wanted (first layer of the stack): LN1's residual half goes to scratch and
+    // the in-projection's dX GEMM below is skipped
+    float *dX_scratch = W.take<float>(Np * dp);   // taken in every mode so the plan covers it
+    if (!need_dx) dX = dX_scratch;
     if (!plan)
         U2GNN_TRY(u2gnn_layernorm_bwd(dX1, dp, c.Z1, dp, c.mean1, c.rstd1, w->n1_w, dX, dp, dA, dp, pd, s->drop1, N,
                                       Np, d, dp, st));
@@ -344,6 +377,13 @@ int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
             U2GNN_TRY(u2gnn_window_attn_bwd(c.QKV, 3 * dp, D.window, (int32_t)dp, dO, dp, c.Psave, pd, s->attn,
                                             q_scale, dQKV, 3 * dp, N / D.window, Np, st));
     } else {
+        dQKV = W.take<float>(Np * 3 * dp);
+        const bool dv_side = dv_side_on() && so != st;
+        if (dv_side) {   // dV needs only Pd and dO: overlap it with the dS chain
+            U2GNN_TRY(sd.fork());
+            U2GNN_TRY(gemm_split(W, D, c.Pd, dO, dQKV + 2 * dp, Np, dp, Np, Np, dp, 3 * dp, true, 1.f, false, nullptr,
+                                 nullptr, false, so, pd > 0.f));
+        }
         float *delta = W.take<float>(Np);
         if (!plan) U2GNN_TRY(u2gnn_rowdot(dO, dp, c.O, dp, delta, Np, dp, st));
         float *dS = W.take<float>(Np * Np);
@@ -353,17 +393,26 @@ int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
             gg.a.aux0 = c.Pd, gg.a.rowvec = delta, gg.a.ld_aux = Np, gg.a.p_drop = pd;
             U2GNN_TRY(gg.run(st, plan));
         }
-        dQKV = W.take<float>(Np * 3 * dp);
-        U2GNN_TRY(gemm_split(W, D, c.Pd, dO, dQKV + 2 * dp, Np, dp, Np, Np, dp, 3 * dp, true, 1.f, false, nullptr,
-                             nullptr, false, st, pd > 0.f));
+        if (!dv_side)
+            U2GNN_TRY(gemm_split(W, D, c.Pd, dO, dQKV + 2 * dp, Np, dp, Np, Np, dp, 3 * dp, true, 1.f, false, nullptr,
+                                 nullptr, false, st, pd > 0.f));
+        const bool dk_side = dv_side && dk_side_on();
+        if (dk_side) {
+            U2GNN_TRY(sd.fork());
+            U2GNN_TRY(gemm_split(W, D, dS, Q, dQKV + dp, Np, dp, Np, Np, 3 * dp, 3 * dp, true, 1.f, false, nullptr,
+                                 nullptr, false, so));
+        }
         U2GNN_TRY(gemm_split(W, D, dS, Kt, dQKV, Np, dp, Np, Np, 3 * dp, 3 * dp, false, q_scale, false, nullptr, nullptr,
                              false, st));
-        U2GNN_TRY(gemm_split(W, D, dS, Q, dQKV + dp, Np, dp, Np, Np, 3 * dp, 3 * dp, true, 1.f, false, nullptr, nullptr,
-                             false, st));
+        if (!dk_side)
+            U2GNN_TRY(gemm_split(W, D, dS, Q, dQKV + dp, Np, dp, Np, Np, 3 * dp, 3 * dp, true, 1.f, false, nullptr,
+                                 nullptr, false, st));
+        if (dv_side) U2GNN_TRY(sd.join());
     }
     // in-projection
-    U2GNN_TRY(gemm_split(W, D, dQKV, w->W_in, dX, Np, dp, 3 * dp, 3 * dp, dp, dp, false, 1.f, true, nullptr, nullptr,
-                         false, st));
+    if (need_dx)
+        U2GNN_TRY(gemm_split(W, D, dQKV, w->W_in, dX, Np, dp, 3 * dp, 3 * dp, dp, dp, false, 1.f, true, nullptr,
+                             nullptr, false, st));
     U2GNN_TRY(sd.fork());
     U2GNN_TRY(wgrad(W, D, dQKV, 3 * dp, X, dp, 3 * dp, dp, g->in_w, d, blk_d, blk_d, so));
     U2GNN_TRY(bias_grad(W, dQKV, Np, 3 * dp, 3 * dp, dp, d, g->in_b, so));
@@ -413,12 +462,12 @@ int u2gnn_layer_fwd(const u2gnn_layer_dims *dims, const u2gnn_layer_params *w, c
 int u2gnn_layer_bwd(const u2gnn_layer_dims *dims, const u2gnn_layer_params *w, const u2gnn_layer_seeds *s,
                     const float *X, const void *ctx, int64_t ctx_bytes, const float *dX2, float *dX,
                     const u2gnn_layer_grads *g, void *ws, int64_t ws_bytes, void *stream, void *side_stream) {
-    if (!dims_ok(dims) || !w || !s || !X || !ctx || !dX2 || !dX || !g || (!ws && ws_bytes > 0)) return U2GNN_E_ARG;
+    if (!dims_ok(dims) || !w || !s || !X || !ctx || !dX2 || !g || (!ws && ws_bytes > 0)) return U2GNN_E_ARG;
     const Dims D = make_dims(dims);
     static char empty_ws alignas(256)[256];
     Arena C(const_cast<void *>(ctx), ctx_bytes), W(ws ? ws : empty_ws, ws ? ws_bytes : 0);
     return layer_bwd(D, w, s, X, C, dX2, dX, g, W, reinterpret_cast<hipStream_t>(stream),
-                     reinterpret_cast<hipStream_t>(side_stream));
+                     reinterpret_cast<hipStream_t>(side_stream), dX != nullptr);
 }
 
 }  // extern "C"

@@ -224,38 +224,87 @@ __global__ void __launch_bounds__(256) ss_fwd_kernel(const float *X, int64_t ldx
     }
 }
 
-// dX[i, c] = g_i (sum_j prob_ij W[s_j, c] - W[y_i, c]); dW[y_i, c] -= g_i X[i, c]
+// Block-wide sum of SS_CH per-thread partials (fixed shuffle tree + fixed 4-wave order, so the
+// result is deterministic); the totals land in tot[0..SS_CH) for every thread.
+constexpr int SS_CH = 8;   // columns per pass (D = d*L is 4 at C5, 19 at C3)
+__device__ __forceinline__ void ss_block_sum(float (&acc)[SS_CH], float (*red)[SS_CH], float (&tot)[SS_CH]) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < SS_CH; ++k) acc[k] = wave_sum(acc[k]);
+    if (lane == 0)
+#pragma unroll
+        for (int k = 0; k < SS_CH; ++k) red[w][k] = acc[k];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < SS_CH; ++k) tot[k] = (red[0][k] + red[1][k]) + (red[2][k] + red[3][k]);
+    __syncthreads();
+}
+
+// dX[i, c] = g_i (sum_j prob_ij W[s_j, c] - W[y_i, c]); dW[y_i, c] -= g_i X[i, c].
+// One block per input row; the S sampled rows are spread over the 256 threads (each thread
+// gathers its rows' SS_CH-column slices: independent loads, no serial latency chain over S).
 __global__ void __launch_bounds__(256) ss_bwd_x_kernel(const float *X, int64_t ldx, const int64_t *labels,
                                                        const int64_t *sids, int64_t S, const float *W, int64_t ldw,
                                                        const float *prob, const float *dloss, float *dX, int64_t lddx,
                                                        float *dW, int64_t lddw, int64_t D) {
+    __shared__ float red[4][SS_CH];
     const int64_t i = blockIdx.x;
+    const int tid = threadIdx.x;
     const float g = dloss ? dloss[i] : 1.f;
     const float *pr = prob + i * S;
-    for (int64_t c = threadIdx.x; c < D; c += 256) {
-        float s = 0.f;
-        for (int64_t j = 0; j < S; ++j) s += pr[j] * W[sids[j] * ldw + c];
-        dX[i * lddx + c] = g * (s - W[labels[i] * ldw + c]);
-        atomicAdd(dW + labels[i] * lddw + c, -g * X[i * ldx + c]);
+    const int64_t y = labels[i];
+    for (int64_t c0 = 0; c0 < D; c0 += SS_CH) {
+        float acc[SS_CH], tot[SS_CH];
+#pragma unroll
+        for (int k = 0; k < SS_CH; ++k) acc[k] = 0.f;
+        for (int64_t j = tid; j < S; j += 256) {
+            const float pj = pr[j];
+            const float *wr = W + sids[j] * ldw + c0;
+#pragma unroll
+            for (int k = 0; k < SS_CH; ++k)
+                if (c0 + k < D) acc[k] += pj * wr[k];
+        }
+        ss_block_sum(acc, red, tot);
+        if (tid < SS_CH && c0 + tid < D) {
+            float t = tot[0];
+#pragma unroll
+            for (int k = 1; k < SS_CH; ++k)
+                if (tid == k) t = tot[k];
+            const int64_t c = c0 + tid;
+            dX[i * lddx + c] = g * (t - W[y * ldw + c]);
+            atomicAdd(dW + y * lddw + c, -g * X[i * ldx + c]);
+        }
     }
 }
 
-// dW[s_j, c] += sum_i g_i prob_ij X[i, c]; block per sample j
+// dW[s_j, c] += sum_i g_i prob_ij X[i, c]; one block per sample j, the input rows spread over
+// the 256 threads (independent loads), deterministic block sum.
 __global__ void __launch_bounds__(256) ss_bwd_w_kernel(const float *X, int64_t ldx, const int64_t *sids, int64_t S,
                                                        const float *prob, const float *dloss, float *dW, int64_t lddw,
                                                        int64_t n_rows, int64_t D) {
-    __shared__ float red[4][256];
+    __shared__ float red[4][SS_CH];
     const int64_t j = blockIdx.x;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    for (int64_t c0 = 0; c0 < D; c0 += 64) {
-        const int64_t c = c0 + lane;
-        float s = 0.f;
-        if (c < D)
-            for (int64_t i = w; i < n_rows; i += 4) s += (dloss ? dloss[i] : 1.f) * prob[i * S + j] * X[i * ldx + c];
-        red[w][lane] = s;
-        __syncthreads();
-        if (w == 0 && c < D) atomicAdd(dW + sids[j] * lddw + c, red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane]);
-        __syncthreads();
+    const int tid = threadIdx.x;
+    float *dw = dW + sids[j] * lddw;
+    for (int64_t c0 = 0; c0 < D; c0 += SS_CH) {
+        float acc[SS_CH], tot[SS_CH];
+#pragma unroll
+        for (int k = 0; k < SS_CH; ++k) acc[k] = 0.f;
+        for (int64_t i = tid; i < n_rows; i += 256) {
+            const float f = (dloss ? dloss[i] : 1.f) * prob[i * S + j];
+            const float *xr = X + i * ldx + c0;
+#pragma unroll
+            for (int k = 0; k < SS_CH; ++k)
+                if (c0 + k < D) acc[k] += f * xr[k];
+        }
+        ss_block_sum(acc, red, tot);
+        if (tid < SS_CH && c0 + tid < D) {
+            float t = tot[0];
+#pragma unroll
+            for (int k = 1; k < SS_CH; ++k)
+                if (tid == k) t = tot[k];
+            atomicAdd(dw + c0 + tid, t);
+        }
     }
 }
 

@@ -220,14 +220,16 @@ class EncoderStack:
                 pre = f"{prefix}.{l}.layers.{t}."
                 g = LayerParams(*[grads[pre + k] for k in LAYER_KEYS])
                 dX = native.layer_backward(dX, ctx["layers"][l][t], self.packed[l][t], self.layer_params(l, t), g,
-                                           tdims, self.prec, side=off.side, deep_wgrad=engine_deep_wgrad())
+                                           tdims, self.prec, side=off.side, deep_wgrad=engine_deep_wgrad(),
+                                           need_dx=l > 0 or t > 0)
             dnext = dX
         off.join()
         return dnext
 
     def backward(self, ctx, ext_grad, grads: dict, prefix: str = "u2gnn_layers"):
         """ext_grad(l) -> fresh padded gradient of outs[l] from outside the stack (head / loss).
-        Writes encoder parameter gradients into grads[<reference key>]."""
+        Writes encoder parameter gradients into grads[<reference key>]; returns None (the stack
+        input, rows of X_concat, takes no gradient)."""
         if "window" in ctx:
             return self._backward_neighbors(ctx, ext_grad, grads, prefix)
         b = ctx["batch"]
@@ -242,12 +244,15 @@ class EncoderStack:
                 pre = f"{prefix}.{l}.layers.{t}."
                 g = LayerParams(*[grads[pre + k] for k in LAYER_KEYS])
                 lc = ctx["layers"][l][t]
+                # the stack's input (gathered X_concat rows) is not trainable: no dX out of layer (0, 0)
+                need_dx = l > 0 or t > 0
                 if isinstance(lc, native.NativeCtx):
                     dX = native.layer_backward(dX, lc, self.packed[l][t], self.layer_params(l, t), g, dims,
-                                               self.prec, side=off.side, deep_wgrad=engine_deep_wgrad())
+                                               self.prec, side=off.side, deep_wgrad=engine_deep_wgrad(),
+                                               need_dx=need_dx)
                 else:
                     dX = encoder_layer_backward(dX, lc, self.packed[l][t], self.layer_params(l, t), g, dims,
-                                                self.prec, off=off)
+                                                self.prec, off=off, need_dx=need_dx)
             dnext = dX
         off.join()   # parameter gradients complete before the caller's optimizer reads them
         return dnext

@@ -297,8 +297,9 @@ def encoder_layer_forward(X: torch.Tensor, w: PackedLayer, p: LayerParams, dims:
 
 def encoder_layer_backward(dX2: torch.Tensor, ctx: EncoderLayerCtx, w: PackedLayer, p: LayerParams,
                            g: LayerParams, dims: Dims, prec: str = "fp32",
-                           off: Optional[OffPath] = None) -> torch.Tensor:
-    """Backward of encoder_layer_forward.  Writes the real-shaped parameter gradients into
+                           off: Optional[OffPath] = None, need_dx: bool = True) -> Optional[torch.Tensor]:
+    """Backward of encoder_layer_forward (``need_dx=False``: the input gradient is not wanted,
+    its in-projection GEMM is skipped and None is returned).  Writes the real-shaped parameter gradients into
     ``g`` (tensors shaped like the params) and returns dX [Np, dp].  Parameter-gradient work is
     enqueued on ``off``'s side stream (joined here unless the caller passes its own OffPath)."""
     N, Np, d, dp, ff, ffp = dims.N, dims.Np, dims.d, dims.dp, dims.ff, dims.ffp
@@ -358,8 +359,9 @@ def encoder_layer_backward(dX2: torch.Tensor, ctx: EncoderLayerCtx, w: PackedLay
     _gemm_nodes_k(dS, Q, dQKV[:, dp:2 * dp], Np, dp, Np, Np, 3 * dp, 3 * dp, trans_a=True, prec=prec, flops=att)
     del dS, dO
     # in-projection
-    _gemm_split(dQKV, w.W_in, dX, Np, dp, 3 * dp, 3 * dp, dp, dp, accumulate=True, prec=prec,
-                flops=6.0 * N * d * d)
+    if need_dx:
+        _gemm_split(dQKV, w.W_in, dX, Np, dp, 3 * dp, 3 * dp, dp, dp, accumulate=True, prec=prec,
+                    flops=6.0 * N * d * d)
 
     def in_proj_grads(dQKV=dQKV):
         _wgrad(dQKV, 3 * dp, ctx.X, dp, 3 * dp, dp, Np, g.in_w, (dp, d), (dp, d), prec, N)
@@ -367,4 +369,4 @@ def encoder_layer_backward(dX2: torch.Tensor, ctx: EncoderLayerCtx, w: PackedLay
     off.run(in_proj_grads, dQKV, ctx.X)
     if own:
         off.join()
-    return dX
+    return dX if need_dx else None

@@ -97,16 +97,17 @@ def layer_forward(X: torch.Tensor, packed, p, dims, train: bool, seeds: Dict[int
 
 
 def layer_backward(dX2: torch.Tensor, ctx: NativeCtx, packed, p, g, dims, prec: str,
-                   side: Optional["torch.cuda.Stream"] = None, deep_wgrad: bool = True) -> torch.Tensor:
+                   side: Optional["torch.cuda.Stream"] = None, deep_wgrad: bool = True,
+                   need_dx: bool = True) -> Optional[torch.Tensor]:
     cb, _, bb = sizes(dims.N, dims.d, dims.ff, prec, ctx.p_drop, deep_wgrad, ctx.window)
     dev = dX2.device
-    dX = torch.empty(dims.Np, dims.dp, device=dev, dtype=torch.float32)
+    dX = torch.empty(dims.Np, dims.dp, device=dev, dtype=torch.float32) if need_dx else None
     ws = torch.empty(max(256, bb), device=dev, dtype=torch.uint8)
     dd = _dims(dims.N, dims.d, dims.ff, prec, deep_wgrad, ctx.window)
     pp, ss = _params(packed, p), _seeds(ctx.p_drop, ctx.seeds)
     gg = LayerGrads(*[getattr(g, k).data_ptr() for k in _lib._PKEYS])
     check(hip_lib().u2gnn_layer_bwd(ctypes.byref(dd), ctypes.byref(pp), ctypes.byref(ss), ctx.X.data_ptr(),
-                                    ctx.buf.data_ptr(), cb, dX2.data_ptr(), dX.data_ptr(), ctypes.byref(gg),
+                                    ctx.buf.data_ptr(), cb, dX2.data_ptr(), dX.data_ptr() if need_dx else None, ctypes.byref(gg),
                                     ws.data_ptr(), ws.numel(), _stream(), _stream(side) if side is not None else None),
           "u2gnn_layer_bwd")
     if side is not None:

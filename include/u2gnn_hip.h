@@ -306,7 +306,8 @@ int u2gnn_layer_sizes(const u2gnn_layer_dims *dims, float p_drop, int64_t *ctx_b
 int u2gnn_layer_fwd(const u2gnn_layer_dims *dims, const u2gnn_layer_params *w,
                     const u2gnn_layer_seeds *s, const float *X, float *X2, void *ctx,
                     int64_t ctx_bytes, void *ws, int64_t ws_bytes, void *stream);
-/* dX2, dX: [Np, dp]; X is the forward's input. */
+/* dX2, dX: [Np, dp]; X is the forward's input.  dX = NULL: the input gradient is not wanted
+ * (first layer of a stack whose input is not trainable) and its in-projection GEMM is skipped. */
 int u2gnn_layer_bwd(const u2gnn_layer_dims *dims, const u2gnn_layer_params *w,
                     const u2gnn_layer_seeds *s, const float *X, const void *ctx, int64_t ctx_bytes,
                     const float *dX2, float *dX, const u2gnn_layer_grads *g, void *ws,

@@ -24,6 +24,7 @@ import time
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path[:0] = [os.path.join(REPO, "graph-transformer_amd"), REPO]
 
+import u2gnn_hip  # noqa: E402,F401  (before the HIP runtime starts: GPU_MAX_HW_QUEUES, see ensure_hw_queues)
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
@@ -36,6 +37,10 @@ PEAK = {"fp32": 157.3,     # TFLOP/s dense f32-input MFMA peak (MI355X_MICROARCH
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--allreduce", default="overlap", choices=["overlap", "after", "none"],
+                    help="gradient all-reduce per layer under the backward (overlap) or after it")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="init the RCCL process group even at one rank (exercises the DP path on one GPU)")
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch-size", type=int, default=64)
@@ -180,11 +185,26 @@ def main_c5(args):
                       "precision": args.precision},
            "final_loss": round(loss, 4), "host_issue_ms_per_step": round(1e3 * t_issue / args.steps, 3),
            "roofline": roof, "cpu_baseline": None}
-    print(json.dumps(out), flush=True)
+    emit(out)
+
+
+_JSON_OUT = None
+
+
+def emit(out: dict) -> None:
+    """The ONE result line, on the original stdout (libraries' stdout chatter -- e.g. RCCL's
+    version banner at communicator init -- is redirected to stderr in main())."""
+    f = _JSON_OUT if _JSON_OUT is not None else sys.stdout
+    f.write(json.dumps(out) + "\n")
+    f.flush()
 
 
 def main():
+    global _JSON_OUT
     args = parse()
+    sys.stdout.flush()
+    _JSON_OUT = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)   # fd 1 -> stderr for everything else (native libraries write to fd 1 directly)
     if args.workload == "c5":
         return main_c5(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -193,13 +213,18 @@ def main():
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     dist = None
-    if world > 1:
+    if os.environ.get("U2GNN_EARLY_SIDE", "1") == "1":
+        from u2gnn_hip.engine import side_stream
+        side_stream(dev)   # before RCCL creates its streams (own hardware queue, see side_stream)
+    if world > 1 or args.force_dist:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if "MASTER_ADDR" not in os.environ:   # --force-dist without a launcher: a 1-rank group
+            os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=os.environ.get("MASTER_PORT", "29533"))
+        dist.init_process_group("nccl", device_id=dev, rank=rank, world_size=world)
 
     from pytorch_U2GNN_Sup import TransformerU2GNN
     from u2gnn_hip.batching import BatchLoader
-    from u2gnn_hip.dp import GradAllReduce, broadcast_params, rank_batches
+    from u2gnn_hip.dp import GradAllReduce, OverlappedGradAllReduce, broadcast_params, rank_batches
     from u2gnn_hip.core import DeviceBatch
     from u2gnn_hip import kernels as K
     from u2gnn_hip.synthetic import collab_like
@@ -223,7 +248,14 @@ def main():
     trainer = SupTrainer(model, lr=args.lr, max_norm=0.5, seed=123 + rank)
     if dist is not None:
         broadcast_params(trainer.flat)
-        trainer.grad_sync = GradAllReduce(bucket_mb=8.0)
+        if args.allreduce == "none":   # diagnostics only: no gradient exchange
+            pass
+        elif args.allreduce == "overlap":   # per-layer buckets under the backward
+            ar = OverlappedGradAllReduce(trainer.flat)
+            model.core.stack.grad_ready = ar.layer_done
+            trainer.grad_sync = ar
+        else:
+            trainer.grad_sync = GradAllReduce(bucket_mb=8.0)
 
     nb = len(batches)
     for i in range(args.warmup):
@@ -300,7 +332,7 @@ def main():
     if rank == 0 and world == 1 and args.cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(host[args.warmup % nb], sd0, args, d, C)
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        emit(out)
     if dist is not None:
         dist.destroy_process_group()
 

@@ -124,6 +124,9 @@ class EncoderStack:
             raise ValueError(f"attention must be 'nodes' or 'neighbors', got {attention!r}")
         self.attention = attention
         self.packed = None
+        # optional callable(prefix, stream): called once a layer's parameter gradients are
+        # enqueued (on `stream`), e.g. dp.OverlappedGradAllReduce.layer_done
+        self.grad_ready = None
 
     def layer_params(self, l, t) -> LayerParams:
         return LayerParams.from_encoder_layer(self.layers[l].layers[t])
@@ -222,6 +225,8 @@ class EncoderStack:
                 dX = native.layer_backward(dX, ctx["layers"][l][t], self.packed[l][t], self.layer_params(l, t), g,
                                            tdims, self.prec, side=off.side, deep_wgrad=engine_deep_wgrad(),
                                            need_dx=l > 0 or t > 0)
+                if self.grad_ready is not None:
+                    self.grad_ready(pre, off.side)
             dnext = dX
         off.join()
         return dnext
@@ -253,6 +258,8 @@ class EncoderStack:
                 else:
                     dX = encoder_layer_backward(dX, lc, self.packed[l][t], self.layer_params(l, t), g, dims,
                                                 self.prec, off=off, need_dx=need_dx)
+                if self.grad_ready is not None:   # this layer's parameter gradients are enqueued
+                    self.grad_ready(pre, off.side)
             dnext = dX
         off.join()   # parameter gradients complete before the caller's optimizer reads them
         return dnext

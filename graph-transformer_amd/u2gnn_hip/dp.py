@@ -13,7 +13,8 @@ rather than latency-bound.  Clip + Adam then run redundantly (bit-identically) o
 """
 from __future__ import annotations
 
-from typing import List
+import contextlib
+from typing import Dict, List, Optional, Tuple
 
 import torch
 
@@ -47,6 +48,73 @@ class GradAllReduce:
             handles.append(self.dist.all_reduce(g[o:o + self.bucket], group=self.group, async_op=True))
         for h in handles:
             h.wait()
+        g.mul_(1.0 / self.world)
+
+
+class OverlappedGradAllReduce:
+    """The gradient average, overlapped with the backward: each encoder layer's gradient region
+    (one contiguous ~5 MB slice of the flat buffer at C4) is all-reduced as soon as its backward
+    has been enqueued, on RCCL's stream ordered after the stream that writes those gradients
+    (the executor's side stream), while the next layer's backward runs; the remaining regions
+    (the head) go at the end of the step, then the step's main stream waits for every
+    collective and scales by 1/world.  Same result as GradAllReduce (sum of the same per-rank
+    buffers by the same collective, then one scaling), each rank issuing the same sequence.
+
+    Wiring: ``stack.grad_ready = ar.layer_done`` (EncoderStack calls it with the layer's
+    parameter-name prefix and the stream that wrote its gradients) and ``trainer.grad_sync = ar``.
+    """
+
+    def __init__(self, flat, group=None):
+        import torch.distributed as dist
+        self.dist = dist
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.flat = flat
+        base = flat.gflat.data_ptr()
+        self.span: Dict[str, Tuple[int, int]] = {}
+        for name in flat.names:
+            g = flat.grads[name]
+            lo = (g.data_ptr() - base) // 4
+            self.span[name] = (lo, lo + g.numel())
+        self.pending: List = []
+        self.launched: List[Tuple[int, int]] = []
+
+    def region(self, prefix: str) -> Tuple[int, int]:
+        """Element range [lo, hi) of the parameters named prefix*, which must be contiguous."""
+        r = sorted(v for k, v in self.span.items() if k.startswith(prefix))
+        if not r:
+            raise KeyError(prefix)
+        lo, hi = r[0][0], r[-1][1]
+        covered = sum(b - a for a, b in r)
+        inside = sum(b - a for k, (a, b) in self.span.items() if a >= lo and b <= hi)
+        if covered != inside:
+            raise ValueError(f"parameters {prefix}* are not contiguous in the flat buffer")
+        return lo, self._align_end(hi)
+
+    def _align_end(self, hi: int) -> int:
+        # the flat buffer pads every parameter to 4 floats: include the padding up to the next one
+        nxt = [a for a, _ in self.span.values() if a >= hi]
+        return min(nxt) if nxt else self.flat.gflat.numel()
+
+    def layer_done(self, prefix: str, stream: Optional["torch.cuda.Stream"] = None) -> None:
+        lo, hi = self.region(prefix)
+        g = self.flat.gflat
+        ctx = torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
+        with ctx:
+            self.pending.append(self.dist.all_reduce(g[lo:hi], group=self.group, async_op=True))
+        self.launched.append((lo, hi))
+
+    def __call__(self, flat) -> None:
+        g = flat.gflat
+        o = 0
+        for lo, hi in sorted(self.launched) + [(g.numel(), g.numel())]:
+            if lo > o:   # a region no layer_done covered (head parameters, padding)
+                self.pending.append(self.dist.all_reduce(g[o:lo], group=self.group, async_op=True))
+            o = max(o, hi)
+        for h in self.pending:
+            h.wait()
+        self.pending.clear()
+        self.launched.clear()
         g.mul_(1.0 / self.world)
 
 

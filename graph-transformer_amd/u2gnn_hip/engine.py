@@ -164,18 +164,24 @@ def set_overlap(on: bool) -> bool:
     return prev
 
 
+def side_stream(dev: torch.device) -> "torch.cuda.Stream":
+    """The per-device side stream (created on first use).  Call it before anything else creates
+    streams -- RCCL's communicator makes several -- so that it gets its own hardware queue:
+    with GPU_MAX_HW_QUEUES = 4 a stream created after RCCL's can share the main stream's queue,
+    which serialises the two (measured: the side stream's 1 ms/step of overlap at C4 was lost)."""
+    s = _SIDE.get(dev.index)
+    if s is None:
+        s = _SIDE[dev.index] = torch.cuda.Stream(device=dev)
+    return s
+
+
 class OffPath:
     """Enqueue closures on the side stream after everything already issued on the current
     stream; tensors they read are record_stream'ed so the caching allocator cannot recycle
     them early.  join() makes the current stream wait for all of it."""
 
     def __init__(self, dev: torch.device):
-        self.side = None
-        if _OVERLAP[0] and dev.type == "cuda":
-            s = _SIDE.get(dev.index)
-            if s is None:
-                s = _SIDE[dev.index] = torch.cuda.Stream(device=dev)
-            self.side = s
+        self.side = side_stream(dev) if _OVERLAP[0] and dev.type == "cuda" else None
 
     def run(self, fn, *uses: torch.Tensor):
         if self.side is None:

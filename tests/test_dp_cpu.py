@@ -33,7 +33,7 @@ def _worker(rank, world, port, out_dir):
     from pytorch_U2GNN_Sup import TransformerU2GNN
     from u2gnn_hip.batching import BatchLoader, GraphStore
     from u2gnn_hip.core import FlatParams
-    from u2gnn_hip.dp import GradAllReduce, broadcast_params, rank_batches
+    from u2gnn_hip.dp import GradAllReduce, OverlappedGradAllReduce, broadcast_params, rank_batches
 
     graphs, C = util.load_data("MUTAG", False)
     np.random.seed(123)
@@ -50,6 +50,23 @@ def _worker(rank, world, port, out_dir):
     for n in flat.names:
         flat.grads[n].copy_(sd[n].grad)
     GradAllReduce(bucket_mb=0.01)(flat)
+    # overlapped form on a 2-timestep, 2-layer model with per-rank random gradients: per-layer
+    # regions in backward order (as EncoderStack.grad_ready issues them), the head at the end;
+    # must give the same buffer as the bucketed all-reduce, bit for bit
+    m2 = TransformerU2GNN(7, 32, C, 2, 0.5, 2)
+    f2 = FlatParams(m2)
+    f2.gflat.copy_(torch.randn(f2.gflat.numel(), generator=torch.Generator().manual_seed(7 + rank)))
+    mine_g = f2.gflat.clone()
+    GradAllReduce(bucket_mb=0.001)(f2)
+    g_after = f2.gflat.clone()
+    f2.gflat.copy_(mine_g)
+    ar = OverlappedGradAllReduce(f2)
+    for l in reversed(range(2)):
+        for t in reversed(range(2)):
+            ar.layer_done(f"u2gnn_layers.{l}.layers.{t}.")
+    ar(f2)
+    assert torch.equal(f2.gflat, g_after)
+    assert not ar.pending and not ar.launched
     np.savez(os.path.join(out_dir, f"r{rank}.npz"), g=flat.gflat.numpy(), p=flat.flat.numpy(),
              ix=np.concatenate([x.input_x.ravel() for x in mine]))
     dist.destroy_process_group()

@@ -134,6 +134,14 @@ struct G {   // one GEMM launch (defaults = plain store)
     int run(hipStream_t st, bool plan) { return plan ? U2GNN_OK : u2gnn_gemm(&a, st); }
 };
 
+bool shallow_nosplit_on() {   // engine._SHALLOW_NOSPLIT
+    static const bool v = [] {
+        const char *e = std::getenv("U2GNN_SHALLOW_NOSPLIT");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
+
 // engine._gemm_split: deterministic split-K into fp32 slabs + one reduce pass (alpha, accumulate,
 // padded->real block map).  deep = weight gradient (16-deep K step, <= 16 slabs).
 int gemm_split(Arena &W, const Dims &D, const float *A, const float *B, float *C, int64_t M, int64_t N, int64_t Kd,
@@ -141,6 +149,19 @@ int gemm_split(Arena &W, const Dims &D, const float *A, const float *B, float *C
                const int64_t *cblk, bool deep, hipStream_t st, bool clamp_a = false) {
     const bool f32 = D.prec == U2GNN_PREC_F32;
     const int64_t bk = f32 ? 16 : 32;
+    const bool plan = W.plan();
+    const bool mapped = rblk != nullptr;
+    if (shallow_nosplit_on() && !f32 && !deep && !mapped && Kd <= 2048 && M % 64 == 0 && N % 64 == 0 &&
+        (M / 64) * (N / 64) >= 256) {
+        // shallow K (dH.W1, dQKV.W_in) with enough 64x64 tiles to fill the chip: no split, the
+        // epilogue accumulates straight into C (no slabs, no reduce pass)
+        G g(A, B, C, M, N, Kd, lda, ldb, ldc, D.prec);
+        if (ta) g.ta();
+        g.a.alpha = alpha;
+        g.a.clamp_a = clamp_a;
+        g.epi(accumulate ? U2GNN_EPI_ACCUM : U2GNN_EPI_STORE).tile(64);
+        return g.run(st, plan);
+    }
     int t;
     int64_t tiles, target = 448;
     if (!f32 && M % 256 == 0 && N % 128 == 0 && (M / 256) * (N / 128) >= 32) {
@@ -158,8 +179,6 @@ int gemm_split(Arena &W, const Dims &D, const float *A, const float *B, float *C
         if (split > 16) split = 16;
         if (split < 1) split = 1;
     }
-    const bool plan = W.plan();
-    const bool mapped = rblk != nullptr;
     if (split == 1 && !mapped) {
         G g(A, B, C, M, N, Kd, lda, ldb, ldc, D.prec);
         if (ta) g.ta();

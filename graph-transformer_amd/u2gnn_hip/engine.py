@@ -165,10 +165,10 @@ def set_overlap(on: bool) -> bool:
 
 
 def side_stream(dev: torch.device) -> "torch.cuda.Stream":
-    """The per-device side stream (created on first use).  Call it before anything else creates
-    streams -- RCCL's communicator makes several -- so that it gets its own hardware queue:
-    with GPU_MAX_HW_QUEUES = 4 a stream created after RCCL's can share the main stream's queue,
-    which serialises the two (measured: the side stream's 1 ms/step of overlap at C4 was lost)."""
+    """The per-device side stream (created on first use).  It only overlaps the main stream when
+    it has a hardware queue of its own: with RCCL's streams in the process, HIP's default 4 queues
+    put it on the main stream's queue (the 1 ms/step of overlap at C4 was lost, whatever the
+    creation order); u2gnn_hip.ensure_hw_queues raises the count to 8 at import."""
     s = _SIDE.get(dev.index)
     if s is None:
         s = _SIDE[dev.index] = torch.cuda.Stream(device=dev)
@@ -198,6 +198,11 @@ class OffPath:
             torch.cuda.current_stream().wait_stream(self.side)
 
 
+# U2GNN_SHALLOW_NOSPLIT=0: shallow-K products split like the deep ones (A/B switch; the native
+# executor reads the same variable)
+_SHALLOW_NOSPLIT = os.environ.get("U2GNN_SHALLOW_NOSPLIT", "1") != "0"
+
+
 def _gemm_split(A, B, C, M, N, Kd, lda, ldb, ldc, trans_a=False, trans_b=False, alpha=1.0, accumulate=False,
                 prec="fp32", rblk=None, cblk=None, target=448, flops=None, deep=False, clamp_a=False):
     """C (+)= alpha * op(A) . op(B) with deterministic split-K: when the tile grid alone would
@@ -207,6 +212,14 @@ def _gemm_split(A, B, C, M, N, Kd, lda, ldb, ldc, trans_a=False, trans_b=False, 
     alpha, accumulation and an optional padded->real block map (rblk, cblk).  clamp_a: A is the
     signed probability image (read as Pd)."""
     bk = 16 if prec == "fp32" else 32
+    if (_SHALLOW_NOSPLIT and prec != "fp32" and not deep and rblk is None and Kd <= 2048 and M % 64 == 0
+            and N % 64 == 0 and (M // 64) * (N // 64) >= 256):
+        # shallow K (dH.W1, dQKV.W_in: K = ff, 3d) with enough 64x64 tiles to fill the chip: no
+        # split, C (+)= alpha acc straight from the epilogue -- no slabs, no reduce pass
+        K.gemm(A, B, C, M, N, Kd, lda, ldb, ldc, trans_a=trans_a, trans_b=trans_b, alpha=alpha,
+               epilogue=E.EPI_ACCUM if accumulate else E.EPI_STORE, precision=prec, tile=64, flops=flops,
+               clamp_a=clamp_a)
+        return
     if prec != "fp32" and M % 256 == 0 and N % 128 == 0 and (M // 256) * (N // 128) >= 32:
         # 256x128 blocks (8 waves, one block per CU): the skinny attention products
         t, tiles, target = 256, (M // 256) * (N // 128), 240

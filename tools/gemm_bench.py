@@ -29,6 +29,9 @@ SHAPES = [  # name, M, N, K, ta, tb, [(split, tile), ...] (tile 129 = 128x128 wi
     ("FFN2r NT", Np, dp, ffp, False, True, [(1, 64), (1, 128), (1, 256)], 2),
     ("dH    NN", Np, ffp, dp, False, False, [(1, 64), (1, 128), (1, 256)], 4),
     ("dO    NN", Np, dp, dp, False, False, [(1, 64), (1, 128), (1, 256)]),
+    # shallow-K backward products (dH.W1 -> dX1, dQKV.W_in -> dX)
+    ("dX1   NN", Np, dp, ffp, False, False, [(1, 64), (1, 128), (2, 128), (4, 256)]),
+    ("dXin  NN", Np, dp, 3 * dp, False, False, [(1, 64), (1, 128), (2, 128), (4, 256)]),
 ]
 
 

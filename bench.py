@@ -81,6 +81,34 @@ def model_step_flops(N, d, ff, T, L):
     return 3.0 * L * T * (8.0 * N * d * d + 4.0 * N * N * d + 4.0 * N * d * ff)
 
 
+def gather_roofline(b, d, ff, K, dev, reps=20):
+    """a2 (pytorch_U2GNN_Sup.py:32, F.embedding(input_x, X_concat)): the reference materialises all
+    k+1 neighbour slots of every node; time u2gnn_gather_rows over the same [N, k+1] index of one
+    C4 batch into the padded [R_pad, dp] token image the neighbour-attention path consumes.
+    HBM-minimum bytes per launch = token image written + index read + the unique source rows
+    (the N x d table, re-read k+1 times from L2/MALL)."""
+    from u2gnn_hip.engine import Dims, rup
+    W = b.input_x.shape[1]
+    R = b.N * W
+    Rp, dp = Dims(R, d, ff).Np, rup(d, 64)
+    dst = torch.empty(Rp, dp, device=dev, dtype=torch.float32)
+    for _ in range(3):
+        K.gather_rows(b.X_concat, b.input_x, 1, dst, R, Rp, d, dp)
+    st = torch.cuda.current_stream(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(reps):
+        K.gather_rows(b.X_concat, b.input_x, 1, dst, R, Rp, d, dp)
+    e1.record(st)
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / reps
+    nbytes = Rp * dp * 4 + R * 8 + b.N * d * 4
+    ach = nbytes / (us * 1e-6) / 1e9
+    return {"bound": "hbm", "kernel": "gather_rows_kernel (a2, all k+1 slots)", "achieved": round(ach, 1),
+            "peak": 8000.0, "unit": "GB/s", "frac": round(ach / 8000.0, 4), "avg_launch_us": round(us, 2),
+            "algorithmic_bytes_per_launch": nbytes, "rows": R, "rows_pad": Rp, "d": d, "d_pad": dp}
+
+
 def cpu_baseline(hb, sd, args, d, C):
     """The oracle restatement (reference semantics incl. all k+1 slots and p=0.5 dropout,
     i.e. the reference's cost) timed on the host cores: forward + loss + backward + clip + Adam."""
@@ -328,7 +356,9 @@ def main():
                       "global_batch": args.batch_size * world, "mean_nodes_per_batch": round(mean_N, 1),
                       "parallelism": f"dp{world}", "precision": args.precision, "attention": args.attention},
            "final_loss": round(loss, 5), "host_issue_ms_per_step": round(1e3 * t_issue / args.steps, 3),
-           "roofline": roof, "cpu_baseline": None}
+           "roofline": roof, "gather": None, "cpu_baseline": None}
+    if rank == 0:
+        out["gather"] = gather_roofline(used[0], d, args.ff_hidden_size, K, dev)
     if rank == 0 and world == 1 and args.cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(host[args.warmup % nb], sd0, args, d, C)
     if rank == 0:

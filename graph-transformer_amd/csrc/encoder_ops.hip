@@ -9,10 +9,17 @@
 namespace {
 
 // ------------------------------------------------------------------------------------------
-// a2 neighbour gather (pytorch_U2GNN_Sup.py:32,39): one wave per destination row.
+// a2 neighbour gather (pytorch_U2GNN_Sup.py:32,39): one wave per destination row, every source
+// load of the row issued before its stores (restrict pointers, unrolled).  MODE 1: 16-byte
+// source rows and destination rows, a float4 of columns per lane in each 256-column chunk.
+// MODE 2: 4-byte-aligned source rows (X_concat with d = 367 starts rows at arbitrary 4-byte
+// offsets): lane-consecutive 4-byte loads and stores, 16 columns per lane in flight.  Both need
+// d_pad <= 1024.  MODE 0: the plain per-column loop for anything else.
 // ------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) gather_rows_kernel(const float *src, int64_t ld_src, int64_t src_rows,
-                                                          const int64_t *idx, int64_t idx_stride, float *dst,
+template <int MODE>
+__global__ void __launch_bounds__(256) gather_rows_kernel(const float *__restrict__ src, int64_t ld_src,
+                                                          int64_t src_rows, const int64_t *__restrict__ idx,
+                                                          int64_t idx_stride, float *__restrict__ dst,
                                                           int64_t ld_dst, int64_t n_rows, int64_t n_rows_pad,
                                                           int64_t d, int64_t d_pad, int32_t *err) {
     const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -27,12 +34,42 @@ __global__ void __launch_bounds__(256) gather_rows_kernel(const float *src, int6
             s = -1;
         }
     }
-    if (s < 0) {
-        for (int64_t c = lane; c < d_pad; c += 64) o[c] = 0.f;
-        return;
+    const float *in = src + (s < 0 ? 0 : s) * ld_src;
+    if constexpr (MODE == 1) {
+        float4 v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int c = 256 * j + 4 * lane;
+            v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (s < 0 || c >= d) continue;
+            if (c + 3 < d) {
+                v[j] = *reinterpret_cast<const float4 *>(in + c);
+            } else {
+                v[j].x = in[c];
+                if (c + 1 < d) v[j].y = in[c + 1];
+                if (c + 2 < d) v[j].z = in[c + 2];
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int c = 256 * j + 4 * lane;
+            if (c < d_pad) *reinterpret_cast<float4 *>(o + c) = v[j];
+        }
+    } else if constexpr (MODE == 2) {
+        float v[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int c = 64 * j + lane;
+            v[j] = (s >= 0 && c < d) ? in[c] : 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int c = 64 * j + lane;
+            if (c < d_pad) o[c] = v[j];
+        }
+    } else {
+        for (int64_t c = lane; c < d_pad; c += 64) o[c] = (s >= 0 && c < d) ? in[c] : 0.f;
     }
-    const float *in = src + s * ld_src;
-    for (int64_t c = lane; c < d_pad; c += 64) o[c] = c < d ? in[c] : 0.f;
 }
 
 __global__ void __launch_bounds__(256) scatter_add_rows_kernel(const float *src, int64_t ld_src, const int64_t *idx,
@@ -664,8 +701,18 @@ int u2gnn_gather_rows(const float *src, int64_t ld_src, int64_t src_rows, const 
                       int32_t *err, void *stream) {
     if (!dst || (n_rows > 0 && (!src || !idx)) || n_rows > n_rows_pad || d > d_pad) return U2GNN_E_ARG;
     if (n_rows_pad == 0) return U2GNN_OK;
-    hipLaunchKernelGGL(gather_rows_kernel, dim3(grid_for(n_rows_pad, 4, 1 << 30)), dim3(256), 0, u2gnn_stream(stream),
-                       src, ld_src, src_rows, idx, idx_stride, dst, ld_dst, n_rows, n_rows_pad, d, d_pad, err);
+    const dim3 grid(grid_for(n_rows_pad, 4, 1 << 30));
+    hipStream_t st = u2gnn_stream(stream);
+    const bool small = d_pad <= 1024;
+    if (small && (d_pad & 3) == 0 && (ld_dst & 3) == 0 && al16(dst) && (ld_src & 3) == 0 && al16(src))
+        hipLaunchKernelGGL(gather_rows_kernel<1>, grid, dim3(256), 0, st, src, ld_src, src_rows, idx, idx_stride, dst,
+                           ld_dst, n_rows, n_rows_pad, d, d_pad, err);
+    else if (small)
+        hipLaunchKernelGGL(gather_rows_kernel<2>, grid, dim3(256), 0, st, src, ld_src, src_rows, idx, idx_stride, dst,
+                           ld_dst, n_rows, n_rows_pad, d, d_pad, err);
+    else
+        hipLaunchKernelGGL(gather_rows_kernel<0>, grid, dim3(256), 0, st, src, ld_src, src_rows, idx, idx_stride, dst,
+                           ld_dst, n_rows, n_rows_pad, d, d_pad, err);
     return u2gnn_launch_status();
 }
 

@@ -25,36 +25,103 @@ __device__ __forceinline__ bool zero_pad_rows(int64_t n_nodes, int W, int64_t ro
     return true;
 }
 
+// LDS images of the node's operands are [W][dp + 4]: the 4-float pad moves consecutive rows 4 banks
+// apart, so the float4 reads of different rows at one column (the (i, j) pairs of a wave) spread
+// over the banks instead of all landing on one (dp = 384 is a multiple of the bank count).
+__device__ __forceinline__ int win_ld(int dp) { return dp + 4; }
+
+// stage rows row0 .. row0+W-1 of a [rows][ld] fp32 operand (column offset col) into a [W][LD] image
+__device__ __forceinline__ void win_stage(const float *src, int64_t ld, int64_t row0, int col, int W, int dp,
+                                          float *img) {
+    const int dq = dp / 4, LD = win_ld(dp);
+    for (int e = threadIdx.x; e < W * dq; e += blockDim.x) {
+        const int i = e / dq, c4 = (e - i * dq) * 4;
+        *reinterpret_cast<float4 *>(img + i * LD + c4) =
+            *reinterpret_cast<const float4 *>(src + (row0 + i) * ld + col + c4);
+    }
+}
+
+// S[i][j] = A_i . B_j (i, j < W) into S[W][W+1]: one (i, j) pair per thread, float4 LDS reads,
+// four partial sums by column residue combined as (s0 + s1) + (s2 + s3)
+__device__ __forceinline__ void win_pair_dots(const float *A, const float *B, int W, int dp, float *S) {
+    const int LD4 = win_ld(dp) / 4, dq = dp / 4;
+    for (int e = threadIdx.x; e < W * W; e += blockDim.x) {
+        const int i = e / W, j = e - i * W;
+        const float4 *a = reinterpret_cast<const float4 *>(A) + i * LD4;
+        const float4 *b = reinterpret_cast<const float4 *>(B) + j * LD4;
+        float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+#pragma unroll 4
+        for (int c = 0; c < dq; ++c) {
+            const float4 x = a[c], y = b[c];
+            s0 = fmaf(x.x, y.x, s0);
+            s1 = fmaf(x.y, y.y, s1);
+            s2 = fmaf(x.z, y.z, s2);
+            s3 = fmaf(x.w, y.w, s3);
+        }
+        S[i * (W + 1) + j] = (s0 + s1) + (s2 + s3);
+    }
+}
+
+// out[row0 + i][col + c] = scale * sum_j C(i, j) * M[j][c] for i < W, c < dp, with C(i, j) =
+// C[i][j] (TRANS false) or C[j][i] (TRANS true) of a [W][W+1] LDS matrix.  A thread owns a float4
+// column group and a block of up to 16 rows (M read once per j for all of them); j runs in order.
+constexpr int WIN_RB = 16;
+template <bool TRANS>
+__device__ __forceinline__ void win_combine(const float *C, const float *M, int W, int dp, float scale, float *out,
+                                            int64_t ldo, int64_t row0, int col) {
+    const int dq = dp / 4, LD4 = win_ld(dp) / 4;
+    int nb = (int)blockDim.x / dq;
+    const int nb_min = (W + WIN_RB - 1) / WIN_RB;
+    if (nb < nb_min) nb = nb_min;
+    if (nb > W) nb = W;
+    const int rb = (W + nb - 1) / nb;
+    const float4 *M4 = reinterpret_cast<const float4 *>(M);
+    for (int e = threadIdx.x; e < dq * nb; e += blockDim.x) {
+        const int c4 = e % dq, i0 = (e / dq) * rb;
+        const int cnt = min(rb, W - i0);
+        if (cnt <= 0) continue;
+        float4 acc[WIN_RB];
+#pragma unroll
+        for (int r = 0; r < WIN_RB; ++r) acc[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int j = 0; j < W; ++j) {
+            const float4 m = M4[j * LD4 + c4];
+#pragma unroll
+            for (int r = 0; r < WIN_RB; ++r) {
+                if (r < cnt) {
+                    const float cf = TRANS ? C[j * (W + 1) + i0 + r] : C[(i0 + r) * (W + 1) + j];
+                    acc[r].x = fmaf(cf, m.x, acc[r].x);
+                    acc[r].y = fmaf(cf, m.y, acc[r].y);
+                    acc[r].z = fmaf(cf, m.z, acc[r].z);
+                    acc[r].w = fmaf(cf, m.w, acc[r].w);
+                }
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < WIN_RB; ++r) {
+            if (r < cnt) {
+                float4 v = acc[r];
+                if (scale != 1.f) v.x *= scale, v.y *= scale, v.z *= scale, v.w *= scale;
+                *reinterpret_cast<float4 *>(out + (row0 + i0 + r) * ldo + col + 4 * c4) = v;
+            }
+        }
+    }
+}
+
 // forward: O_n = dropout(softmax(Qs_n K_n^T)) V_n; P_n (pre-dropout probabilities) saved
 __global__ void __launch_bounds__(256) window_attn_fwd_kernel(const float *QKV, int64_t ldq, int W, int dp,
                                                               float *O, int64_t ldo, float *Psave, float p,
                                                               uint64_t seed, int64_t n_nodes, int64_t rows_pad) {
     if (zero_pad_rows(n_nodes, W, rows_pad, dp, O, ldo)) return;
     extern __shared__ float sm[];
-    float *Qs = sm, *Ks = Qs + W * dp, *Vs = Ks + W * dp, *S = Vs + W * dp;   // S: [W][W+1]
+    const int LD = win_ld(dp);
+    float *Qs = sm, *Ks = Qs + W * LD, *Vs = Ks + W * LD, *S = Vs + W * LD;   // S: [W][W+1]
     const int tid = threadIdx.x;
     const int64_t n = blockIdx.x, row0 = n * W;
-    const int dq = dp / 4;
-    for (int e = tid; e < W * dq; e += 256) {
-        const int i = e / dq, c4 = (e - i * dq) * 4;
-        const float *q = QKV + (row0 + i) * ldq + c4;
-        *reinterpret_cast<float4 *>(Qs + i * dp + c4) = *reinterpret_cast<const float4 *>(q);
-        *reinterpret_cast<float4 *>(Ks + i * dp + c4) = *reinterpret_cast<const float4 *>(q + dp);
-        *reinterpret_cast<float4 *>(Vs + i * dp + c4) = *reinterpret_cast<const float4 *>(q + 2 * dp);
-    }
+    win_stage(QKV, ldq, row0, 0, W, dp, Qs);
+    win_stage(QKV, ldq, row0, dp, W, dp, Ks);
+    win_stage(QKV, ldq, row0, 2 * dp, W, dp, Vs);
     __syncthreads();
-    for (int e = tid; e < W * W; e += 256) {
-        const int i = e / W, j = e - i * W;
-        const float *a = Qs + i * dp, *b = Ks + j * dp;
-        float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-        for (int c = 0; c < dp; c += 4) {
-            s0 = fmaf(a[c], b[c], s0);
-            s1 = fmaf(a[c + 1], b[c + 1], s1);
-            s2 = fmaf(a[c + 2], b[c + 2], s2);
-            s3 = fmaf(a[c + 3], b[c + 3], s3);
-        }
-        S[i * (W + 1) + j] = (s0 + s1) + (s2 + s3);
-    }
+    win_pair_dots(Qs, Ks, W, dp, S);
     __syncthreads();
     if (tid < W) {   // row softmax, save P, keep Pd in S
         float *srow = S + tid * (W + 1);
@@ -74,20 +141,7 @@ __global__ void __launch_bounds__(256) window_attn_fwd_kernel(const float *QKV, 
         }
     }
     __syncthreads();
-    for (int c = tid; c < dp; c += 256) {
-        float acc[WIN_MAX];
-#pragma unroll
-        for (int i = 0; i < WIN_MAX; ++i) acc[i] = 0.f;
-        for (int j = 0; j < W; ++j) {
-            const float v = Vs[j * dp + c];
-#pragma unroll
-            for (int i = 0; i < WIN_MAX; ++i)
-                if (i < W) acc[i] = fmaf(S[i * (W + 1) + j], v, acc[i]);
-        }
-#pragma unroll
-        for (int i = 0; i < WIN_MAX; ++i)
-            if (i < W) O[(row0 + i) * ldo + c] = acc[i];
-    }
+    win_combine<false>(S, Vs, W, dp, 1.f, O, ldo, row0, 0);
 }
 
 // backward: from dO and the saved P -> dQKV (the Q part already multiplied by q_scale = 1/sqrt(d),
@@ -98,33 +152,17 @@ __global__ void __launch_bounds__(256) window_attn_bwd_kernel(const float *QKV, 
                                                               int64_t ldg, int64_t n_nodes, int64_t rows_pad) {
     if (zero_pad_rows(n_nodes, W, rows_pad, 3 * dp, dQKV, ldg)) return;
     extern __shared__ float sm[];
-    float *Qs = sm, *Ks = Qs + W * dp, *Vs = Ks + W * dp, *dOs = Vs + W * dp;
-    float *Pd = dOs + W * dp, *dS = Pd + W * (W + 1);   // [W][W+1] each
+    const int LD = win_ld(dp);
+    float *Qs = sm, *Ks = Qs + W * LD, *Vs = Ks + W * LD, *dOs = Vs + W * LD;
+    float *Pd = dOs + W * LD, *dS = Pd + W * (W + 1);   // [W][W+1] each
     const int tid = threadIdx.x;
     const int64_t n = blockIdx.x, row0 = n * W;
-    const int dq = dp / 4;
-    for (int e = tid; e < W * dq; e += 256) {
-        const int i = e / dq, c4 = (e - i * dq) * 4;
-        const float *q = QKV + (row0 + i) * ldq + c4;
-        *reinterpret_cast<float4 *>(Qs + i * dp + c4) = *reinterpret_cast<const float4 *>(q);
-        *reinterpret_cast<float4 *>(Ks + i * dp + c4) = *reinterpret_cast<const float4 *>(q + dp);
-        *reinterpret_cast<float4 *>(Vs + i * dp + c4) = *reinterpret_cast<const float4 *>(q + 2 * dp);
-        *reinterpret_cast<float4 *>(dOs + i * dp + c4) = *reinterpret_cast<const float4 *>(dO + (row0 + i) * ldo + c4);
-    }
+    win_stage(QKV, ldq, row0, 0, W, dp, Qs);
+    win_stage(QKV, ldq, row0, dp, W, dp, Ks);
+    win_stage(QKV, ldq, row0, 2 * dp, W, dp, Vs);
+    win_stage(dO, ldo, row0, 0, W, dp, dOs);
     __syncthreads();
-    // dPd[i][j] = dO_i . V_j  -> dS (after the softmax backward below)
-    for (int e = tid; e < W * W; e += 256) {
-        const int i = e / W, j = e - i * W;
-        const float *a = dOs + i * dp, *b = Vs + j * dp;
-        float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-        for (int c = 0; c < dp; c += 4) {
-            s0 = fmaf(a[c], b[c], s0);
-            s1 = fmaf(a[c + 1], b[c + 1], s1);
-            s2 = fmaf(a[c + 2], b[c + 2], s2);
-            s3 = fmaf(a[c + 3], b[c + 3], s3);
-        }
-        dS[i * (W + 1) + j] = (s0 + s1) + (s2 + s3);
-    }
+    win_pair_dots(dOs, Vs, W, dp, dS);   // dPd[i][j] = dO_i . V_j -> dS after the softmax backward
     __syncthreads();
     if (tid < W) {
         const float *prow = Psave + (n * W + tid) * W;
@@ -142,24 +180,13 @@ __global__ void __launch_bounds__(256) window_attn_bwd_kernel(const float *QKV, 
         for (int j = 0; j < W; ++j) ds[j] = prow[j] * (ds[j] - delta);
     }
     __syncthreads();
-    for (int c = tid; c < dp; c += 256) {
-        for (int i = 0; i < W; ++i) {   // i = output row of dQ / key row of dK, dV
-            float dq_ = 0.f, dk = 0.f, dv = 0.f;
-            for (int j = 0; j < W; ++j) {
-                dq_ = fmaf(dS[i * (W + 1) + j], Ks[j * dp + c], dq_);
-                dk = fmaf(dS[j * (W + 1) + i], Qs[j * dp + c], dk);
-                dv = fmaf(Pd[j * (W + 1) + i], dOs[j * dp + c], dv);
-            }
-            float *g = dQKV + (row0 + i) * ldg;
-            g[c] = dq_ * q_scale;
-            g[dp + c] = dk;
-            g[2 * dp + c] = dv;
-        }
-    }
+    win_combine<false>(dS, Ks, W, dp, q_scale, dQKV, ldg, row0, 0);    // dQ_i = sum_j dS[i][j] K_j
+    win_combine<true>(dS, Qs, W, dp, 1.f, dQKV, ldg, row0, dp);        // dK_i = sum_j dS[j][i] Q_j
+    win_combine<true>(Pd, dOs, W, dp, 1.f, dQKV, ldg, row0, 2 * dp);   // dV_i = sum_j Pd[j][i] dO_j
 }
 
-inline size_t fwd_lds(int W, int dp) { return (size_t)(3 * W * dp + W * (W + 1)) * sizeof(float); }
-inline size_t bwd_lds(int W, int dp) { return (size_t)(4 * W * dp + 2 * W * (W + 1)) * sizeof(float); }
+inline size_t fwd_lds(int W, int dp) { return (size_t)(3 * W * (dp + 4) + W * (W + 1)) * sizeof(float); }
+inline size_t bwd_lds(int W, int dp) { return (size_t)(4 * W * (dp + 4) + 2 * W * (W + 1)) * sizeof(float); }
 constexpr size_t LDS_LIMIT = 160 * 1024;
 
 }  // namespace
@@ -169,7 +196,8 @@ extern "C" {
 int u2gnn_window_attn_fwd(const float *QKV, int64_t ldq, int32_t W, int32_t dp, float *O, int64_t ldo, float *Psave,
                           float p, uint64_t seed, int64_t n_nodes, int64_t rows_pad, void *stream) {
     if (!QKV || !O || !Psave || W < 1 || W > WIN_MAX || dp < 4 || (dp & 3) || n_nodes < 1) return U2GNN_E_ARG;
-    if (rows_pad < n_nodes * W || (ldq & 3) || ldq < 3 * dp) return U2GNN_E_ARG;
+    if (rows_pad < n_nodes * W || (ldq & 3) || (ldo & 3) || ldq < 3 * dp || ldo < dp) return U2GNN_E_ARG;
+    if (((uintptr_t)QKV & 15) || ((uintptr_t)O & 15)) return U2GNN_E_ALIGN;
     const size_t lds = fwd_lds(W, dp);
     if (lds > LDS_LIMIT) return U2GNN_E_SHAPE;
     static bool attr = false;   // dynamic LDS above 64 KiB must be opted into once per kernel
@@ -190,7 +218,9 @@ int u2gnn_window_attn_bwd(const float *QKV, int64_t ldq, int32_t W, int32_t dp, 
                           int64_t n_nodes, int64_t rows_pad, void *stream) {
     if (!QKV || !dO || !Psave || !dQKV || W < 1 || W > WIN_MAX || dp < 4 || (dp & 3) || n_nodes < 1)
         return U2GNN_E_ARG;
-    if (rows_pad < n_nodes * W || (ldq & 3) || (ldo & 3) || ldq < 3 * dp || ldg < 3 * dp) return U2GNN_E_ARG;
+    if (rows_pad < n_nodes * W || (ldq & 3) || (ldo & 3) || (ldg & 3) || ldq < 3 * dp || ldg < 3 * dp)
+        return U2GNN_E_ARG;
+    if (((uintptr_t)QKV & 15) || ((uintptr_t)dO & 15) || ((uintptr_t)dQKV & 15)) return U2GNN_E_ALIGN;
     const size_t lds = bwd_lds(W, dp);
     if (lds > LDS_LIMIT) return U2GNN_E_SHAPE;
     static bool attr = false;   // dynamic LDS above 64 KiB must be opted into once per kernel

@@ -90,6 +90,8 @@ class UnSupTrainer:
         lrow = torch.empty(N, device=OV.device)
         prob = torch.empty(N, S, device=OV.device)
         K.sampled_softmax_fwd(OVd, D, b.input_y, sample_ids, S, W, W.stride(0), lrow, prob, N, D)
+        if self.ws.numel() < K.colstat_ws_floats(N, 1):   # ceil(N/16) partial sums (u2gnn_hip.h)
+            self.ws = torch.empty(K.colstat_ws_floats(N, 1), device=OV.device)
         K.colsum(lrow.view(N, 1), N, 1, 1, (1, 1), self.loss, self.ws)
         gW = self.flat.grads["ss.weight"]
         gW.zero_()

@@ -311,10 +311,35 @@ def test_gather_pack_colsum():
     assert torch.equal(bm.view(3, 64)[:, :7].reshape(-1), bsrc)
     X = _mk(300, 192, seed=17)
     out = torch.empty(3 * 7, device=DEV)
-    ws = torch.empty(2 * 192, device=DEV)
+    ws = torch.empty(K.colstat_ws_floats(300, 192), device=DEV)   # >= ceil(300/16) * 192 (u2gnn_hip.h)
     K.colsum(X, 300, 192, 192, (64, 7), out, ws)
     ref = X.sum(0).view(3, 64)[:, :7].reshape(-1)
     assert rel_err(out, ref) < 1e-5
+
+
+@pytest.mark.parametrize("d,d_pad,ld_src,n_src,n_rows,n_pad", [
+    (367, 384, 367, 500, 4099, 4352),     # X_concat at C4 width: 4-byte-aligned rows (mode 2)
+    (384, 384, 384, 300, 1000, 1024),     # padded [Np, dp] re-gather: 16-byte rows (mode 1)
+    (7, 64, 7, 50, 30, 64),               # MUTAG width (mode 2)
+    (6, 64, 8, 40, 33, 64),               # aligned source, d % 4 != 0 (mode 1 tail)
+    (1100, 1152, 1100, 20, 17, 64),       # d_pad > 1024 (mode 0 loop)
+])
+def test_gather_rows_modes(d, d_pad, ld_src, n_src, n_rows, n_pad):
+    """a2 gather (pytorch_U2GNN_Sup.py:32): bit-exact copy of the indexed rows, zero padding, and
+    out-of-range indices reported through err with a zero row."""
+    g = torch.Generator(device="cpu").manual_seed(d + n_rows)
+    src_full = torch.randn(n_src, ld_src, generator=g).to(DEV)
+    idx = torch.randint(0, n_src, (n_rows, 2), generator=g)
+    idx[n_rows // 2, 0] = n_src          # out of range -> zero row, err = 1
+    idx = idx.to(DEV)
+    dst = torch.full((n_pad, d_pad), 7.0, device=DEV)
+    err = torch.zeros(1, dtype=torch.int32, device=DEV)
+    K.gather_rows(src_full, idx, 2, dst, n_rows, n_pad, d, d_pad, err)
+    ref = torch.zeros(n_pad, d_pad, device=DEV)
+    ok = idx[:, 0] < n_src
+    ref[:n_rows, :d][ok] = src_full[idx[ok, 0], :d]
+    assert torch.equal(dst, ref)
+    assert err.item() == 1
 
 
 def test_pool_head_ce():

@@ -159,7 +159,8 @@ int gemm_split(Arena &W, const Dims &D, const float *A, const float *B, float *C
         if (ta) g.ta();
         g.a.alpha = alpha;
         g.a.clamp_a = clamp_a;
-        g.epi(accumulate ? U2GNN_EPI_ACCUM : U2GNN_EPI_STORE).tile(64);
+        const bool big = M % 256 == 0 && N % 128 == 0 && (M / 256) * (N / 128) >= U2GNN_BIG_TILE_BLOCKS;
+        g.epi(accumulate ? U2GNN_EPI_ACCUM : U2GNN_EPI_STORE).tile(big ? 256 : 64);
         return g.run(st, plan);
     }
     int t;

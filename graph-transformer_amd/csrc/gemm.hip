@@ -549,6 +549,12 @@ extern "C" int u2gnn_gemm(const u2gnn_gemm_args *a, void *stream) {
         const bool can128 = (a->M % 128 == 0) && (a->N % 128 == 0);
         const int64_t blocks128 = can128 ? (a->M / 128) * (a->N / 128) * split : 0;
         tile = (can128 && blocks128 >= 480) ? 128 : 64;
+        // token-sized products (neighbour attention: M = N(k+1) rows) have 3+ waves of 256x128
+        // blocks: the 8-wave tile's higher intensity wins there.  Node-sized products (C4: at most
+        // 722 such blocks) keep the 128 tile, measured faster for them.
+        if (prec != U2GNN_PREC_F32 && a->M % 256 == 0 && a->N % 128 == 0 &&
+            (a->M / 256) * (a->N / 128) * split >= U2GNN_BIG_TILE_BLOCKS)
+            tile = 256;
     }
     // tile codes: 64, 128 (square), 256 (256x128, 8 waves), 129 (128x128 with a 16-deep K step)
     const bool x2code = x2 && (tile == 257 || tile == 130 || (tile >= 258 && tile <= 263));

@@ -41,6 +41,17 @@ __device__ __forceinline__ void win_stage(const float *src, int64_t ld, int64_t 
     }
 }
 
+// the same with threads t0 .. t0+nt-1 of the block (the others are busy elsewhere)
+__device__ __forceinline__ void win_stage_part(const float *src, int64_t ld, int64_t row0, int col, int W, int dp,
+                                               float *img, int t0, int nt) {
+    const int dq = dp / 4, LD = win_ld(dp);
+    for (int e = t0; e < W * dq; e += nt) {
+        const int i = e / dq, c4 = (e - i * dq) * 4;
+        *reinterpret_cast<float4 *>(img + i * LD + c4) =
+            *reinterpret_cast<const float4 *>(src + (row0 + i) * ld + col + c4);
+    }
+}
+
 // S[i][j] = A_i . B_j (i, j < W) into S[W][W+1]: one (i, j) pair per thread, float4 LDS reads,
 // four partial sums by column residue combined as (s0 + s1) + (s2 + s3)
 __device__ __forceinline__ void win_pair_dots(const float *A, const float *B, int W, int dp, float *S) {
@@ -107,45 +118,53 @@ __device__ __forceinline__ void win_combine(const float *C, const float *M, int 
     }
 }
 
-// forward: O_n = dropout(softmax(Qs_n K_n^T)) V_n; P_n (pre-dropout probabilities) saved
+// forward: O_n = dropout(softmax(Qs_n K_n^T)) V_n; P_n (pre-dropout probabilities) saved.
+// Two operand images (Q, K; V replaces Q once the scores exist, staged by the waves the softmax
+// leaves idle): 54 KB of LDS at W = 17, dp = 384, i.e. 3 blocks per CU.
 __global__ void __launch_bounds__(256) window_attn_fwd_kernel(const float *QKV, int64_t ldq, int W, int dp,
                                                               float *O, int64_t ldo, float *Psave, float p,
                                                               uint64_t seed, int64_t n_nodes, int64_t rows_pad) {
     if (zero_pad_rows(n_nodes, W, rows_pad, dp, O, ldo)) return;
     extern __shared__ float sm[];
     const int LD = win_ld(dp);
-    float *Qs = sm, *Ks = Qs + W * LD, *Vs = Ks + W * LD, *S = Vs + W * LD;   // S: [W][W+1]
+    float *Qs = sm, *Ks = Qs + W * LD, *S = Ks + W * LD;   // S: [W][W+1]
+    float *Vs = Qs;
     const int tid = threadIdx.x;
     const int64_t n = blockIdx.x, row0 = n * W;
     win_stage(QKV, ldq, row0, 0, W, dp, Qs);
     win_stage(QKV, ldq, row0, dp, W, dp, Ks);
-    win_stage(QKV, ldq, row0, 2 * dp, W, dp, Vs);
     __syncthreads();
     win_pair_dots(Qs, Ks, W, dp, S);
     __syncthreads();
-    if (tid < W) {   // row softmax, save P, keep Pd in S
-        float *srow = S + tid * (W + 1);
-        float m = -INFINITY;
-        for (int j = 0; j < W; ++j) m = fmaxf(m, srow[j]);
-        float sum = 0.f;
-        for (int j = 0; j < W; ++j) {
-            srow[j] = expf(srow[j] - m);
-            sum += srow[j];
+    if (tid < 64) {
+        if (tid < W) {   // row softmax, save P, keep Pd in S
+            float *srow = S + tid * (W + 1);
+            float m = -INFINITY;
+            for (int j = 0; j < W; ++j) m = fmaxf(m, srow[j]);
+            float sum = 0.f;
+            for (int j = 0; j < W; ++j) {
+                srow[j] = expf(srow[j] - m);
+                sum += srow[j];
+            }
+            const float inv = 1.f / sum, ks = p > 0.f ? 1.f / (1.f - p) : 1.f;
+            float *prow = Psave + (n * W + tid) * W;
+            for (int j = 0; j < W; ++j) {
+                const float pv = srow[j] * inv;
+                prow[j] = pv;
+                srow[j] = (p > 0.f) ? (u2gnn_keep(seed, (uint32_t)(row0 + tid), (uint32_t)j, p) ? pv * ks : 0.f) : pv;
+            }
         }
-        const float inv = 1.f / sum, ks = p > 0.f ? 1.f / (1.f - p) : 1.f;
-        float *prow = Psave + (n * W + tid) * W;
-        for (int j = 0; j < W; ++j) {
-            const float pv = srow[j] * inv;
-            prow[j] = pv;
-            srow[j] = (p > 0.f) ? (u2gnn_keep(seed, (uint32_t)(row0 + tid), (uint32_t)j, p) ? pv * ks : 0.f) : pv;
-        }
+    } else {
+        win_stage_part(QKV, ldq, row0, 2 * dp, W, dp, Vs, tid - 64, blockDim.x - 64);
     }
     __syncthreads();
     win_combine<false>(S, Vs, W, dp, 1.f, O, ldo, row0, 0);
 }
 
 // backward: from dO and the saved P -> dQKV (the Q part already multiplied by q_scale = 1/sqrt(d),
-// i.e. the gradient of the in-projection's pre-scale output)
+// i.e. the gradient of the in-projection's pre-scale output).  Two operand images: dO and V for
+// dP; K replaces V (staged while wave 0 runs the softmax backward) for dQ beside dV; Q replaces
+// dO for dK.  55 KB of LDS at W = 17, dp = 384: 2 blocks per CU.
 __global__ void __launch_bounds__(256) window_attn_bwd_kernel(const float *QKV, int64_t ldq, int W, int dp,
                                                               const float *dO, int64_t ldo, const float *Psave,
                                                               float p, uint64_t seed, float q_scale, float *dQKV,
@@ -153,40 +172,45 @@ __global__ void __launch_bounds__(256) window_attn_bwd_kernel(const float *QKV, 
     if (zero_pad_rows(n_nodes, W, rows_pad, 3 * dp, dQKV, ldg)) return;
     extern __shared__ float sm[];
     const int LD = win_ld(dp);
-    float *Qs = sm, *Ks = Qs + W * LD, *Vs = Ks + W * LD, *dOs = Vs + W * LD;
-    float *Pd = dOs + W * LD, *dS = Pd + W * (W + 1);   // [W][W+1] each
+    float *img0 = sm, *img1 = img0 + W * LD;
+    float *Pd = img1 + W * LD, *dS = Pd + W * (W + 1);   // [W][W+1] each
     const int tid = threadIdx.x;
     const int64_t n = blockIdx.x, row0 = n * W;
-    win_stage(QKV, ldq, row0, 0, W, dp, Qs);
-    win_stage(QKV, ldq, row0, dp, W, dp, Ks);
-    win_stage(QKV, ldq, row0, 2 * dp, W, dp, Vs);
-    win_stage(dO, ldo, row0, 0, W, dp, dOs);
+    win_stage(dO, ldo, row0, 0, W, dp, img0);            // img0 = dO
+    win_stage(QKV, ldq, row0, 2 * dp, W, dp, img1);      // img1 = V
     __syncthreads();
-    win_pair_dots(dOs, Vs, W, dp, dS);   // dPd[i][j] = dO_i . V_j -> dS after the softmax backward
+    win_pair_dots(img0, img1, W, dp, dS);   // dPd[i][j] = dO_i . V_j -> dS after the softmax backward
     __syncthreads();
-    if (tid < W) {
-        const float *prow = Psave + (n * W + tid) * W;
-        float *ds = dS + tid * (W + 1), *pd = Pd + tid * (W + 1);
-        const float ks = p > 0.f ? 1.f / (1.f - p) : 1.f;
-        float delta = 0.f;
-        for (int j = 0; j < W; ++j) {
-            const bool keep = (p > 0.f) ? u2gnn_keep(seed, (uint32_t)(row0 + tid), (uint32_t)j, p) : true;
-            const float pv = prow[j];
-            const float dp_ = keep ? ds[j] * ks : 0.f;   // gradient w.r.t. the pre-dropout P
-            pd[j] = keep ? pv * ks : 0.f;
-            ds[j] = dp_;
-            delta += dp_ * pv;
+    if (tid < 64) {
+        if (tid < W) {
+            const float *prow = Psave + (n * W + tid) * W;
+            float *ds = dS + tid * (W + 1), *pd = Pd + tid * (W + 1);
+            const float ks = p > 0.f ? 1.f / (1.f - p) : 1.f;
+            float delta = 0.f;
+            for (int j = 0; j < W; ++j) {
+                const bool keep = (p > 0.f) ? u2gnn_keep(seed, (uint32_t)(row0 + tid), (uint32_t)j, p) : true;
+                const float pv = prow[j];
+                const float dp_ = keep ? ds[j] * ks : 0.f;   // gradient w.r.t. the pre-dropout P
+                pd[j] = keep ? pv * ks : 0.f;
+                ds[j] = dp_;
+                delta += dp_ * pv;
+            }
+            for (int j = 0; j < W; ++j) ds[j] = prow[j] * (ds[j] - delta);
         }
-        for (int j = 0; j < W; ++j) ds[j] = prow[j] * (ds[j] - delta);
+    } else {
+        win_stage_part(QKV, ldq, row0, dp, W, dp, img1, tid - 64, blockDim.x - 64);   // img1 = K
     }
     __syncthreads();
-    win_combine<false>(dS, Ks, W, dp, q_scale, dQKV, ldg, row0, 0);    // dQ_i = sum_j dS[i][j] K_j
-    win_combine<true>(dS, Qs, W, dp, 1.f, dQKV, ldg, row0, dp);        // dK_i = sum_j dS[j][i] Q_j
-    win_combine<true>(Pd, dOs, W, dp, 1.f, dQKV, ldg, row0, 2 * dp);   // dV_i = sum_j Pd[j][i] dO_j
+    win_combine<true>(Pd, img0, W, dp, 1.f, dQKV, ldg, row0, 2 * dp);   // dV_i = sum_j Pd[j][i] dO_j
+    win_combine<false>(dS, img1, W, dp, q_scale, dQKV, ldg, row0, 0);   // dQ_i = sum_j dS[i][j] K_j
+    __syncthreads();
+    win_stage(QKV, ldq, row0, 0, W, dp, img0);           // img0 = Q
+    __syncthreads();
+    win_combine<true>(dS, img0, W, dp, 1.f, dQKV, ldg, row0, dp);       // dK_i = sum_j dS[j][i] Q_j
 }
 
-inline size_t fwd_lds(int W, int dp) { return (size_t)(3 * W * (dp + 4) + W * (W + 1)) * sizeof(float); }
-inline size_t bwd_lds(int W, int dp) { return (size_t)(4 * W * (dp + 4) + 2 * W * (W + 1)) * sizeof(float); }
+inline size_t fwd_lds(int W, int dp) { return (size_t)(2 * W * (dp + 4) + W * (W + 1)) * sizeof(float); }
+inline size_t bwd_lds(int W, int dp) { return (size_t)(2 * W * (dp + 4) + 2 * W * (W + 1)) * sizeof(float); }
 constexpr size_t LDS_LIMIT = 160 * 1024;
 
 }  // namespace

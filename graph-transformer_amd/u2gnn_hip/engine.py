@@ -201,6 +201,7 @@ class OffPath:
 # U2GNN_SHALLOW_NOSPLIT=0: shallow-K products split like the deep ones (A/B switch; the native
 # executor reads the same variable)
 _SHALLOW_NOSPLIT = os.environ.get("U2GNN_SHALLOW_NOSPLIT", "1") != "0"
+BIG_TILE_BLOCKS = 768   # U2GNN_BIG_TILE_BLOCKS (u2gnn_hip.h): token-sized products on 256x128 blocks
 
 
 def _gemm_split(A, B, C, M, N, Kd, lda, ldb, ldc, trans_a=False, trans_b=False, alpha=1.0, accumulate=False,
@@ -217,8 +218,9 @@ def _gemm_split(A, B, C, M, N, Kd, lda, ldb, ldc, trans_a=False, trans_b=False, 
         # shallow K (dH.W1, dQKV.W_in: K = ff, 3d) with enough 64x64 tiles to fill the chip: no
         # split, C (+)= alpha acc straight from the epilogue -- no slabs, no reduce pass
         K.gemm(A, B, C, M, N, Kd, lda, ldb, ldc, trans_a=trans_a, trans_b=trans_b, alpha=alpha,
-               epilogue=E.EPI_ACCUM if accumulate else E.EPI_STORE, precision=prec, tile=64, flops=flops,
-               clamp_a=clamp_a)
+               epilogue=E.EPI_ACCUM if accumulate else E.EPI_STORE, precision=prec,
+               tile=256 if (M % 256 == 0 and N % 128 == 0 and (M // 256) * (N // 128) >= BIG_TILE_BLOCKS) else 64,
+               flops=flops, clamp_a=clamp_a)
         return
     if prec != "fp32" and M % 256 == 0 and N % 128 == 0 and (M // 256) * (N // 128) >= 32:
         # 256x128 blocks (8 waves, one block per CU): the skinny attention products

@@ -32,6 +32,9 @@ extern "C" {
 #define U2GNN_OK 0
 #define U2GNN_E_ARG (-1)    /* bad size / null pointer */
 #define U2GNN_E_ALIGN (-2)  /* pointer or leading dimension not 16-byte aligned */
+/* default tile rule (gemm args tile = 0): 256x128 blocks once a bf16x3/bf16 product has at least this
+ * many of them (3 waves of 256 CUs); the shallow-K no-split path of the layer executor uses it too */
+#define U2GNN_BIG_TILE_BLOCKS 768
 #define U2GNN_E_SHAPE (-3)  /* dimension not a multiple of the kernel tile */
 
 /* GEMM epilogues (u2gnn_gemm_args.epilogue). acc = sum_k A(m,k) B(k,n). */

@@ -550,9 +550,12 @@ extern "C" int u2gnn_gemm(const u2gnn_gemm_args *a, void *stream) {
         const int64_t blocks128 = can128 ? (a->M / 128) * (a->N / 128) * split : 0;
         tile = (can128 && blocks128 >= 480) ? 128 : 64;
         // token-sized products (neighbour attention: M = N(k+1) rows) have 3+ waves of 256x128
-        // blocks: the 8-wave tile's higher intensity wins there.  Node-sized products (C4: at most
-        // 722 such blocks) keep the 128 tile, measured faster for them.
-        if (prec != U2GNN_PREC_F32 && a->M % 256 == 0 && a->N % 128 == 0 &&
+        // blocks: the 8-wave tile's higher intensity wins there for plain store / accumulate
+        // epilogues (measured: dH.W1 403 -> 322 us), not for the fused bias/dropout/ReLU ones
+        // (ReLU-backward 464 -> 529 us).  Node-sized products (C4: at most 722 such blocks) keep
+        // the 128 tile, measured faster for them.
+        if (prec != U2GNN_PREC_F32 && (e == U2GNN_EPI_STORE || e == U2GNN_EPI_ACCUM) && a->M % 256 == 0 &&
+            a->N % 128 == 0 &&
             (a->M / 256) * (a->N / 128) * split >= U2GNN_BIG_TILE_BLOCKS)
             tile = 256;
     }

@@ -176,20 +176,30 @@ __global__ void __launch_bounds__(256) pack_multi_kernel(PackBatch pb) {
 
 // column sums, stage 1: block = CS_ROWS rows x 256 columns; each lane owns a float4 of columns,
 // each wave CS_ROWS/4 rows (all its loads in flight at once), ws[chunk][col] via LDS.  Small row
-// chunks give ~Np/16 x cols/256 blocks, enough waves to cover HBM latency.
+// chunks give ~Np/16 x cols/256 blocks, enough waves to cover HBM latency; token-sized inputs
+// (neighbour mode) fold rep groups into one chunk so that at most COLSUM_MAX_CHUNKS partial rows
+// reach the column-parallel stage 2 (rep = 1 below 8K rows: C4 sums are unchanged).
 constexpr int CS_ROWS = 16;
+constexpr int64_t COLSUM_MAX_CHUNKS = 512;
 
+template <bool FOLD>
 __global__ void __launch_bounds__(256) colsum_partial_kernel(const float *X, int64_t rows, int64_t cols_pad,
-                                                             int64_t ld, float *ws) {
+                                                             int64_t ld, int rep, float *ws) {
     __shared__ float4 red[4][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int64_t c = ((int64_t)blockIdx.x * 64 + lane) * 4;
-    const int64_t r0 = (int64_t)blockIdx.y * CS_ROWS + w * (CS_ROWS / 4);
-    float4 v[CS_ROWS / 4];
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    const int nrep = FOLD ? rep : 1;     // compile-time 1 unless folding: the C4 body stays straight-line
+    for (int it = 0; it < nrep; ++it) {  // a chunk = rep consecutive CS_ROWS-row groups
+        const int64_t r0 = ((int64_t)blockIdx.y * nrep + it) * CS_ROWS + w * (CS_ROWS / 4);
+        float4 v[CS_ROWS / 4];
 #pragma unroll
-    for (int j = 0; j < CS_ROWS / 4; ++j)
-        v[j] = (c < cols_pad && r0 + j < rows) ? ld4(X + (r0 + j) * ld + c) : make_float4(0.f, 0.f, 0.f, 0.f);
-    red[w][lane] = add4(add4(v[0], v[1]), add4(v[2], v[3]));
+        for (int j = 0; j < CS_ROWS / 4; ++j)
+            v[j] = (c < cols_pad && r0 + j < rows) ? ld4(X + (r0 + j) * ld + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float4 g = add4(add4(v[0], v[1]), add4(v[2], v[3]));
+        acc = it == 0 ? g : add4(acc, g);
+    }
+    red[w][lane] = acc;
     __syncthreads();
     if (w == 0 && c < cols_pad)
         *reinterpret_cast<float4 *>(ws + (int64_t)blockIdx.y * cols_pad + c) =
@@ -577,18 +587,22 @@ __global__ void __launch_bounds__(256) layernorm_bwd_kernel(const float *dY, int
 
 // LN backward, column part: per CS_ROWS-row chunk, sums over rows of dY*xhat (dgamma), dY (dbeta)
 // and dZd (the bias gradient of the dropout branch feeding this LN) -> ws[chunk][3][d_pad];
-// float4 columns per lane, CS_ROWS/4 rows per wave (all loads in flight).
+// float4 columns per lane, CS_ROWS/4 rows per wave (all loads in flight); a chunk spans rep
+// consecutive CS_ROWS-row groups so that token-sized inputs (neighbour mode, ~82K rows) leave few
+// enough chunks for ln_param_reduce's column-parallel combine (rep = 1 below 8K rows).
+template <bool FOLD>
 __global__ void __launch_bounds__(256) ln_colstats_kernel(const float *dY, int64_t ldy, const float *Z, int64_t ldz,
                                                           const float *mean, const float *rstd, const float *dZd,
                                                           int64_t lddrop, int64_t rows, int64_t d, int64_t d_pad,
-                                                          float *ws) {
+                                                          int rep, float *ws) {
     __shared__ float4 red[4][3][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int64_t c = ((int64_t)blockIdx.x * 64 + lane) * 4;
-    const int64_t r0 = (int64_t)blockIdx.y * CS_ROWS + w * (CS_ROWS / 4);
     const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
     float4 sg = z4, sb = z4, sd = z4;
-    if (c < d_pad) {
+    const int nrep = FOLD ? rep : 1;
+    for (int it = 0; it < nrep && c < d_pad; ++it) {
+        const int64_t r0 = ((int64_t)blockIdx.y * nrep + it) * CS_ROWS + w * (CS_ROWS / 4);
         float4 dy[CS_ROWS / 4], zz[CS_ROWS / 4], dd[CS_ROWS / 4];
         float mu[CS_ROWS / 4], rs[CS_ROWS / 4];
 #pragma unroll
@@ -619,6 +633,8 @@ __global__ void __launch_bounds__(256) ln_colstats_kernel(const float *dY, int64
         *reinterpret_cast<float4 *>(ws + ((int64_t)blockIdx.y * 3 + w) * d_pad + c) =
             add4(add4(red[0][w][lane], red[1][w][lane]), add4(red[2][w][lane], red[3][w][lane]));
 }
+
+constexpr int64_t LN_MAX_CHUNKS = 512;
 
 // block = 16 columns x 16 chunk strides (as colsum_final), fixed-order LDS combine
 __global__ void __launch_bounds__(256) ln_param_reduce_kernel(const float *ws, int64_t n_chunks, int64_t d,
@@ -769,12 +785,15 @@ int u2gnn_colsum(const float *X, int64_t rows, int64_t cols_pad, int64_t ld, int
                  float *out, int32_t accumulate, float *ws, void *stream) {
     if (!X || !out || !ws || cblk_pad < 1) return U2GNN_E_ARG;
     if (cols_pad == 0) return U2GNN_OK;
-    const int64_t chunks = (rows + CS_ROWS - 1) / CS_ROWS;
+    int64_t chunks = (rows + CS_ROWS - 1) / CS_ROWS;
     hipStream_t st = u2gnn_stream(stream);
+    const bool vec = al16(X) && al16(ws) && (ld & 3) == 0 && (cols_pad & 3) == 0;
+    const int rep = vec ? (int)std::max<int64_t>(1, (chunks + COLSUM_MAX_CHUNKS - 1) / COLSUM_MAX_CHUNKS) : 1;
+    chunks = (chunks + rep - 1) / rep;   // never more than the CS_ROWS-row group count callers size ws by
     const unsigned nch = (unsigned)(chunks > 0 ? chunks : 1);
-    if (al16(X) && al16(ws) && (ld & 3) == 0 && (cols_pad & 3) == 0)
-        hipLaunchKernelGGL(colsum_partial_kernel, dim3((unsigned)((cols_pad + 255) / 256), nch), dim3(256), 0, st, X,
-                           rows, cols_pad, ld, ws);
+    if (vec)
+        hipLaunchKernelGGL(rep > 1 ? colsum_partial_kernel<true> : colsum_partial_kernel<false>,
+                           dim3((unsigned)((cols_pad + 255) / 256), nch), dim3(256), 0, st, X, rows, cols_pad, ld, rep, ws);
     else
         hipLaunchKernelGGL(colsum_partial_scalar_kernel, dim3((unsigned)((cols_pad + 63) / 64), nch), dim3(256), 0, st,
                            X, rows, cols_pad, ld, ws);
@@ -881,10 +900,13 @@ int u2gnn_layernorm_bwd_params(const float *dY, int64_t ldy, const float *Z, int
     if (!al16(dY) || !al16(Z) || !al16(ws) || (ldy & 3) || (ldz & 3) || (d_pad & 3) ||
         (dbias && (!al16(dZdrop) || (lddrop & 3))))
         return U2GNN_E_ALIGN;
-    const int64_t chunks = rows_valid > 0 ? (rows_valid + CS_ROWS - 1) / CS_ROWS : 1;
+    const int64_t groups = rows_valid > 0 ? (rows_valid + CS_ROWS - 1) / CS_ROWS : 1;
+    const int rep = (int)((groups + LN_MAX_CHUNKS - 1) / LN_MAX_CHUNKS);
+    const int64_t chunks = (groups + rep - 1) / rep;   // <= the CS_ROWS-row group count callers size ws by
     hipStream_t st = u2gnn_stream(stream);
-    hipLaunchKernelGGL(ln_colstats_kernel, dim3((unsigned)((d_pad + 255) / 256), (unsigned)chunks), dim3(256), 0, st, dY,
-                       ldy, Z, ldz, mean, rstd, dbias ? dZdrop : nullptr, lddrop, rows_valid, d, d_pad, ws);
+    hipLaunchKernelGGL(rep > 1 ? ln_colstats_kernel<true> : ln_colstats_kernel<false>,
+                       dim3((unsigned)((d_pad + 255) / 256), (unsigned)chunks), dim3(256), 0, st, dY,
+                       ldy, Z, ldz, mean, rstd, dbias ? dZdrop : nullptr, lddrop, rows_valid, d, d_pad, rep, ws);
     hipLaunchKernelGGL(ln_param_reduce_kernel, dim3((unsigned)((d + FIN_COLS - 1) / FIN_COLS)), dim3(256), 0, st, ws,
                        chunks, d, d_pad,
                        dgamma, dbeta, dbias);

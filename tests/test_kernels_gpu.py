@@ -317,6 +317,36 @@ def test_gather_pack_colsum():
     assert rel_err(out, ref) < 1e-5
 
 
+@pytest.mark.parametrize("rows", [8192, 8209, 20011, 82110])
+def test_column_reductions_token_sized(rows):
+    """Neighbour-mode row counts: colsum / LN parameter sums fold several 16-row groups into one
+    chunk (at most 512 chunks, the ragged last one included); sums against torch float64."""
+    d, dp = 367, 384
+    X = torch.zeros(rows, dp, device=DEV)
+    X[:, :d] = _mk(rows, d, seed=31)
+    out = torch.empty(d, device=DEV)
+    ws = torch.full((K.colstat_ws_floats(rows, dp),), float("nan"), device=DEV)
+    K.colsum(X, rows, dp, dp, (dp, d), out, ws)
+    ref = X[:, :d].double().sum(0)
+    assert (out.double() - ref).abs().max().item() < 1e-5 * rows ** 0.5 * 4
+    Z = torch.zeros(rows, dp, device=DEV)
+    Z[:, :d] = _mk(rows, d, seed=32)
+    dY = torch.zeros(rows, dp, device=DEV)
+    dY[:, :d] = _mk(rows, d, seed=33)
+    dZd = torch.zeros(rows, dp, device=DEV)
+    dZd[:, :d] = _mk(rows, d, seed=34)
+    mu = Z[:, :d].mean(1)
+    rs = torch.rsqrt(Z[:, :d].var(1, unbiased=False) + 1e-5)
+    dg, db, dbias = (torch.empty(d, device=DEV) for _ in range(3))
+    ws.fill_(float("nan"))
+    K.layernorm_bwd_params(dY, dp, Z, dp, mu, rs, dZd, dp, rows, d, dp, ws, dg, db, dbias)
+    xh = ((Z[:, :d] - mu[:, None]) * rs[:, None]).double()
+    tol = 1e-5 * rows ** 0.5 * 4
+    assert (dg.double() - (dY[:, :d].double() * xh).sum(0)).abs().max().item() < tol
+    assert (db.double() - dY[:, :d].double().sum(0)).abs().max().item() < tol
+    assert (dbias.double() - dZd[:, :d].double().sum(0)).abs().max().item() < tol
+
+
 @pytest.mark.parametrize("d,d_pad,ld_src,n_src,n_rows,n_pad", [
     (367, 384, 367, 500, 4099, 4352),     # X_concat at C4 width: 4-byte-aligned rows (mode 2)
     (384, 384, 384, 300, 1000, 1024),     # padded [Np, dp] re-gather: 16-byte rows (mode 1)

@@ -72,13 +72,19 @@ __global__ void __launch_bounds__(256) gather_rows_kernel(const float *__restric
     }
 }
 
+// an index outside [0, dst_rows) adds nothing and sets *err (F.embedding raises IndexError there)
 __global__ void __launch_bounds__(256) scatter_add_rows_kernel(const float *src, int64_t ld_src, const int64_t *idx,
                                                                int64_t idx_stride, float *dst, int64_t ld_dst,
-                                                               int64_t n_rows, int64_t d) {
+                                                               int64_t dst_rows, int64_t n_rows, int64_t d,
+                                                               int32_t *err) {
     const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (row >= n_rows) return;
     const int64_t t = idx[row * idx_stride];
+    if (t < 0 || t >= dst_rows) {
+        if (lane == 0 && err) atomicExch(err, 1);
+        return;
+    }
     for (int64_t c = lane; c < d; c += 64) atomicAdd(dst + t * ld_dst + c, src[row * ld_src + c]);
 }
 
@@ -733,11 +739,11 @@ int u2gnn_gather_rows(const float *src, int64_t ld_src, int64_t src_rows, const 
 }
 
 int u2gnn_scatter_add_rows(const float *src, int64_t ld_src, const int64_t *idx, int64_t idx_stride, float *dst,
-                           int64_t ld_dst, int64_t n_rows, int64_t d, void *stream) {
+                           int64_t ld_dst, int64_t dst_rows, int64_t n_rows, int64_t d, int32_t *err, void *stream) {
     if (n_rows == 0) return U2GNN_OK;
-    if (!src || !idx || !dst) return U2GNN_E_ARG;
+    if (!src || !idx || !dst || dst_rows < 0) return U2GNN_E_ARG;
     hipLaunchKernelGGL(scatter_add_rows_kernel, dim3(grid_for(n_rows, 4, 1 << 30)), dim3(256), 0,
-                       u2gnn_stream(stream), src, ld_src, idx, idx_stride, dst, ld_dst, n_rows, d);
+                       u2gnn_stream(stream), src, ld_src, idx, idx_stride, dst, ld_dst, dst_rows, n_rows, d, err);
     return u2gnn_launch_status();
 }
 

@@ -115,6 +115,8 @@ class TransformerU2GNN(nn.Module):
             b = X_concat
         else:
             N = X_concat.shape[0]
+            if input_x.numel() and (int(input_x.min()) < 0 or int(input_x.max()) >= N):
+                raise IndexError("index out of range in self (input_x entry outside [0, N))")
             b = DeviceBatch(N, 1, input_x.contiguous(), X_concat.to(torch.float32).contiguous(), None, None, None,
                             None, input_y)
         seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if self.training else 0

@@ -30,7 +30,7 @@ ERRORS = {-1: "bad argument", -2: "misaligned pointer / leading dimension", -3: 
 
 EPI_STORE, EPI_BIAS, EPI_BIAS_DROP_RESID, EPI_BIAS_RELU_DROP, EPI_RELU_DROP_BWD, EPI_ACCUM, EPI_ATTN_DS, \
     EPI_ATTN_DS_SIGNED, EPI_ATTN_DS_RECOMP = range(9)
-ABI_VERSION = 3   # include/u2gnn_hip.h U2GNN_ABI_VERSION
+ABI_VERSION = 4   # include/u2gnn_hip.h U2GNN_ABI_VERSION
 PREC_F32, PREC_BF16X3, PREC_BF16 = 0, 1, 2
 
 
@@ -94,7 +94,7 @@ I64, F32, VP, I32 = c_int64, c_float, c_void_p, c_int32
 _HIP_SIGS = {
     "u2gnn_abi_version": ([], c_int32),
     "u2gnn_gather_rows": ([VP, I64, I64, VP, I64, VP, I64, I64, I64, I64, I64, VP, VP], c_int32),
-    "u2gnn_scatter_add_rows": ([VP, I64, VP, I64, VP, I64, I64, I64, VP], c_int32),
+    "u2gnn_scatter_add_rows": ([VP, I64, VP, I64, VP, I64, I64, I64, I64, VP, VP], c_int32),
     "u2gnn_gemm": ([POINTER(GemmArgs), VP], c_int32),
     "u2gnn_window_attn_fwd": ([VP, I64, I32, I32, VP, I64, VP, F32, c_uint64, I64, I64, VP], c_int32),
     "u2gnn_window_attn_bwd": ([VP, I64, I32, I32, VP, I64, VP, F32, c_uint64, F32, VP, I64, I64, I64, VP], c_int32),

@@ -47,6 +47,18 @@ class DeviceBatch:
     vals: torch.Tensor              # f32 [nnz]
     labels: Optional[torch.Tensor] = None   # int64 [B]
     input_y: Optional[torch.Tensor] = None  # int64 [N] (UnSup softmax labels)
+    # int32[1] device flag the gather / scatter kernels set on an out-of-range input_x entry (they
+    # read and write nothing there); the constructors validate input_x up front, so it stays 0
+    err: Optional[torch.Tensor] = None
+
+    def __post_init__(self):
+        if self.err is None:
+            self.err = torch.zeros(1, device=self.X_concat.device, dtype=torch.int32)
+
+    def check_indices(self):
+        """IndexError if a kernel met an out-of-range input_x entry (host sync; F.embedding raises)."""
+        if int(self.err.item()):
+            raise IndexError("index out of range in self (input_x entry outside [0, N))")
 
     @property
     def idx_stride(self):
@@ -57,6 +69,7 @@ class DeviceBatch:
         """Host arrays (numpy / torch CPU) -> HBM.  Block-diagonal graph_pool of ones given by
         node offsets (train_pytorch_U2GNN_Sup.py:73-89)."""
         dev = torch.device(device)
+        _check_range_host(input_x, int(np.asarray(offsets)[-1]))
         ix = torch.as_tensor(input_x, dtype=torch.int64).to(dev, non_blocking=True).contiguous()
         X = torch.as_tensor(X_concat, dtype=torch.float32).to(dev, non_blocking=True).contiguous()
         off = torch.as_tensor(np.asarray(offsets), dtype=torch.int64)
@@ -78,6 +91,7 @@ class DeviceBatch:
         dev = torch.device(device)
         N, B = int(hb.offsets[-1]), len(hb.offsets) - 1
         slot = getattr(hb, "pinned", None)
+        _check_range_host(hb.input_x, N)
         if slot is not None:
             k1 = hb.input_x.shape[1]
             h2d = lambda t: t.to(dev, non_blocking=True)  # noqa: E731
@@ -105,12 +119,21 @@ class DeviceBatch:
         dev = X_concat.device
         gp = graph_pool.coalesce()
         B, N = gp.shape
+        if input_x.numel() and (int(input_x.min()) < 0 or int(input_x.max()) >= int(N)):
+            raise IndexError("index out of range in self (input_x entry outside [0, N))")
         rows, cols = gp.indices()
         vals = gp.values().to(torch.float32)
         rowptr = torch.zeros(B + 1, dtype=torch.int64, device=dev)
         rowptr[1:] = torch.cumsum(torch.bincount(rows, minlength=B), 0)
         return DeviceBatch(int(N), int(B), input_x.to(dev).contiguous(), X_concat.to(torch.float32).contiguous(),
                            rowptr, cols.contiguous(), vals.contiguous(), labels)
+
+
+def _check_range_host(input_x, N: int):
+    """F.embedding(input_x, X_concat) raises IndexError for an entry outside [0, N) (pytorch_U2GNN_Sup.py:32)."""
+    a = input_x.numpy() if isinstance(input_x, torch.Tensor) else np.asarray(input_x)
+    if a.size and (int(a.min()) < 0 or int(a.max()) >= N):
+        raise IndexError("index out of range in self (input_x entry outside [0, N))")
 
 
 class EncoderStack:
@@ -150,7 +173,7 @@ class EncoderStack:
         Np = dims.Np
         self._pack(dev)
         X = torch.empty(Np, dp, device=dev, dtype=torch.float32)
-        K.gather_rows(b.X_concat, b.input_x, b.idx_stride, X, b.N, Np, d, dp)
+        K.gather_rows(b.X_concat, b.input_x, b.idx_stride, X, b.N, Np, d, dp, b.err)
         outs, lctxs = [], []
         for l in range(self.L):
             lctx = []
@@ -167,7 +190,7 @@ class EncoderStack:
             lctxs.append(lctx)
             if l + 1 < self.L:
                 Xn = torch.empty(Np, dp, device=dev, dtype=torch.float32)
-                K.gather_rows(X, b.input_x, b.idx_stride, Xn, b.N, Np, d, dp)
+                K.gather_rows(X, b.input_x, b.idx_stride, Xn, b.N, Np, d, dp, b.err)
                 X = Xn
         return outs, {"dims": dims, "layers": lctxs, "batch": b}
 
@@ -188,7 +211,7 @@ class EncoderStack:
         self._pack(dev)
         slot0 = torch.arange(b.N, device=dev, dtype=torch.int64) * W
         X = torch.empty(Rp, dp, device=dev, dtype=torch.float32)
-        K.gather_rows(b.X_concat, b.input_x, 1, X, R, Rp, d, dp)
+        K.gather_rows(b.X_concat, b.input_x, 1, X, R, Rp, d, dp, b.err)
         outs, lctxs = [], []
         for l in range(self.L):
             lctx = []
@@ -203,7 +226,7 @@ class EncoderStack:
             lctxs.append(lctx)
             if l + 1 < self.L:
                 X = torch.empty(Rp, dp, device=dev, dtype=torch.float32)
-                K.gather_rows(out, b.input_x, 1, X, R, Rp, d, dp)
+                K.gather_rows(out, b.input_x, 1, X, R, Rp, d, dp, b.err)
         return outs, {"dims": dims, "tdims": tdims, "window": W, "slot0": slot0, "layers": lctxs, "batch": b}
 
     def _backward_neighbors(self, ctx, ext_grad, grads: dict, prefix: str):
@@ -216,7 +239,7 @@ class EncoderStack:
         for l in reversed(range(self.L)):
             dOut = ext_grad(l)                                   # [Np, dp] node rows
             if dnext is not None:                                # re-gather of the next U2GNN layer
-                K.scatter_add_rows(dnext, b.input_x, 1, dOut, R, d)
+                K.scatter_add_rows(dnext, b.input_x, 1, dOut, R, d, b.err)
             dX = torch.zeros(tdims.Np, dp, device=dOut.device, dtype=torch.float32)
             K.scatter_add_rows(dOut, slot0, 1, dX, b.N, d)       # slot 0 of every node
             for t in reversed(range(self.T)):
@@ -244,7 +267,7 @@ class EncoderStack:
         for l in reversed(range(self.L)):
             dX = ext_grad(l)
             if dnext is not None:
-                K.scatter_add_rows(dnext, b.input_x, b.idx_stride, dX, b.N, self.d)
+                K.scatter_add_rows(dnext, b.input_x, b.idx_stride, dX, b.N, self.d, b.err)
             for t in reversed(range(self.T)):
                 pre = f"{prefix}.{l}.layers.{t}."
                 g = LayerParams(*[grads[pre + k] for k in LAYER_KEYS])

@@ -201,7 +201,16 @@ class OffPath:
 # U2GNN_SHALLOW_NOSPLIT=0: shallow-K products split like the deep ones (A/B switch; the native
 # executor reads the same variable)
 _SHALLOW_NOSPLIT = os.environ.get("U2GNN_SHALLOW_NOSPLIT", "1") != "0"
-BIG_TILE_BLOCKS = 768   # U2GNN_BIG_TILE_BLOCKS (u2gnn_hip.h): token-sized products on 256x128 blocks
+BIG_TILE_BLOCKS = 768
+# Precision experiments: products (by role) that run plain bf16 when the layer runs bf16x3.
+# U2GNN_BF16_ROLES=qk,pv,... (tools/prec_probe.py measures each role's parity error).
+ROLES = ("in_proj", "qk", "pv", "out_proj", "ffn1", "ffn2", "ffn2_dx", "ffn2_dw", "ffn1_dx", "ffn1_dw",
+         "out_dx", "out_dw", "dv", "ds", "dq", "dk", "in_dx", "in_dw")
+ROLE_BF16 = set(r for r in os.environ.get("U2GNN_BF16_ROLES", "").split(",") if r)
+
+
+def _rp(role: str, prec: str) -> str:
+    return "bf16" if (prec == "bf16x3" and role in ROLE_BF16) else prec   # U2GNN_BIG_TILE_BLOCKS (u2gnn_hip.h): token-sized products on 256x128 blocks
 
 
 def _gemm_split(A, B, C, M, N, Kd, lda, ldb, ldc, trans_a=False, trans_b=False, alpha=1.0, accumulate=False,
@@ -276,11 +285,11 @@ def encoder_layer_forward(X: torch.Tensor, w: PackedLayer, p: LayerParams, dims:
     f32 = torch.float32
     QKV = torch.empty(Np, 3 * dp, device=dev, dtype=f32)
     K.gemm(X, w.W_in, QKV, Np, 3 * dp, dp, dp, dp, 3 * dp, trans_b=True, epilogue=E.EPI_BIAS, bias=w.b_in,
-           alpha=1.0 / math.sqrt(d), scale_cols=dp, precision=prec, flops=6.0 * N * d * d,
+           alpha=1.0 / math.sqrt(d), scale_cols=dp, precision=_rp("in_proj", prec), flops=6.0 * N * d * d,
            tile=256 if (prec != "fp32" and Np % 256 == 0 and (Np // 256) * (3 * dp // 128) >= 128) else 0)
     Q, Kt, V = QKV[:, :dp], QKV[:, dp:2 * dp], QKV[:, 2 * dp:]
     S = torch.empty(Np, Np, device=dev, dtype=f32)
-    K.gemm(Q, Kt, S, Np, Np, dp, 3 * dp, 3 * dp, Np, trans_b=True, precision=prec, flops=att,
+    K.gemm(Q, Kt, S, Np, Np, dp, 3 * dp, 3 * dp, Np, trans_b=True, precision=_rp("qk", prec), flops=att,
            tile=256 if (prec != "fp32" and Np % 256 == 0) else 0)
     # one [Np, Np] image: with dropout the signed one (P/(1-p) where kept, -P where dropped), which
     # P.V and dP^T.dO read as Pd (negatives staged as 0) and the dS epilogue reads as P and keep
@@ -288,20 +297,20 @@ def encoder_layer_forward(X: torch.Tensor, w: PackedLayer, p: LayerParams, dims:
     K.attn_softmax_fwd(S, Np, None if pd > 0 else Pd, Pd, Np, N, Np, N, Np, pd, seeds.get(SITE_ATTN, 0))
     del S
     O = torch.empty(Np, dp, device=dev, dtype=f32)
-    _gemm_nodes_k(Pd, V, O, Np, dp, Np, Np, 3 * dp, dp, prec=prec, flops=att, clamp_a=pd > 0)
+    _gemm_nodes_k(Pd, V, O, Np, dp, Np, Np, 3 * dp, dp, prec=_rp("pv", prec), flops=att, clamp_a=pd > 0)
     Z1 = torch.empty(Np, dp, device=dev, dtype=f32)
     K.gemm(O, w.W_o, Z1, Np, dp, dp, dp, dp, dp, trans_b=True, epilogue=E.EPI_BIAS_DROP_RESID, bias=w.b_o,
-           aux0=X, ld_aux=dp, p_drop=pd, seed=seeds.get(SITE_DROP1, 0), precision=prec, flops=2.0 * N * d * d)
+           aux0=X, ld_aux=dp, p_drop=pd, seed=seeds.get(SITE_DROP1, 0), precision=_rp("out_proj", prec), flops=2.0 * N * d * d)
     X1 = torch.empty(Np, dp, device=dev, dtype=f32)
     mean1 = torch.empty(Np, device=dev, dtype=f32)
     rstd1 = torch.empty(Np, device=dev, dtype=f32)
     K.layernorm_fwd(Z1, dp, p.n1_w, p.n1_b, X1, dp, mean1, rstd1, N, Np, d, dp)
     Hd = torch.empty(Np, ffp, device=dev, dtype=f32)
     K.gemm(X1, w.W1, Hd, Np, ffp, dp, dp, dp, ffp, trans_b=True, epilogue=E.EPI_BIAS_RELU_DROP, bias=w.b1,
-           p_drop=pd, seed=seeds.get(SITE_DROPFF, 0), precision=prec, flops=2.0 * N * d * ff)
+           p_drop=pd, seed=seeds.get(SITE_DROPFF, 0), precision=_rp("ffn1", prec), flops=2.0 * N * d * ff)
     Z2 = torch.empty(Np, dp, device=dev, dtype=f32)
     K.gemm(Hd, w.W2, Z2, Np, dp, ffp, ffp, ffp, dp, trans_b=True, epilogue=E.EPI_BIAS_DROP_RESID, bias=w.b2,
-           aux0=X1, ld_aux=dp, p_drop=pd, seed=seeds.get(SITE_DROP2, 0), precision=prec, flops=2.0 * N * d * ff)
+           aux0=X1, ld_aux=dp, p_drop=pd, seed=seeds.get(SITE_DROP2, 0), precision=_rp("ffn2", prec), flops=2.0 * N * d * ff)
     X2 = torch.empty(Np, dp, device=dev, dtype=f32)
     mean2 = torch.empty(Np, device=dev, dtype=f32)
     rstd2 = torch.empty(Np, device=dev, dtype=f32)
@@ -342,12 +351,12 @@ def encoder_layer_backward(dX2: torch.Tensor, ctx: EncoderLayerCtx, w: PackedLay
     # FFN: Z2 = X1 + drop(Hd W2^T + b2), Hd = drop(relu(X1 W1^T + b1))
     dH = torch.empty(Np, ffp, device=dev, dtype=f32)
     K.gemm(dF, w.W2, dH, Np, ffp, dp, dp, ffp, ffp, epilogue=E.EPI_RELU_DROP_BWD, aux0=ctx.Hd, ld_aux=ffp,
-           p_drop=pd, precision=prec, flops=2.0 * N * d * ff)
-    off.run(lambda: _wgrad(dF, dp, ctx.Hd, ffp, dp, ffp, Np, g.l2_w, (dp, d), (ffp, ff), prec, N), dF, ctx.Hd)
-    _gemm_split(dH, w.W1, dX1, Np, dp, ffp, ffp, dp, dp, accumulate=True, prec=prec, flops=2.0 * N * d * ff)
+           p_drop=pd, precision=_rp("ffn2_dx", prec), flops=2.0 * N * d * ff)
+    off.run(lambda: _wgrad(dF, dp, ctx.Hd, ffp, dp, ffp, Np, g.l2_w, (dp, d), (ffp, ff), _rp("ffn2_dw", prec), N), dF, ctx.Hd)
+    _gemm_split(dH, w.W1, dX1, Np, dp, ffp, ffp, dp, dp, accumulate=True, prec=_rp("ffn1_dx", prec), flops=2.0 * N * d * ff)
 
     def ffn1_grads(dH=dH):
-        _wgrad(dH, ffp, ctx.X1, dp, ffp, dp, Np, g.l1_w, (ffp, ff), (dp, d), prec, N)
+        _wgrad(dH, ffp, ctx.X1, dp, ffp, dp, Np, g.l1_w, (ffp, ff), (dp, d), _rp("ffn1_dw", prec), N)
         _bias_grad(dH, Np, ffp, ffp, (ffp, ff), g.l1_b)
     off.run(ffn1_grads, dH, ctx.X1)
     del dH, dF
@@ -361,8 +370,8 @@ def encoder_layer_backward(dX2: torch.Tensor, ctx: EncoderLayerCtx, w: PackedLay
     del dX1
     # out-projection
     dO = torch.empty(Np, dp, device=dev, dtype=f32)
-    K.gemm(dA, w.W_o, dO, Np, dp, dp, dp, dp, dp, precision=prec, flops=2.0 * N * d * d)
-    off.run(lambda: _wgrad(dA, dp, ctx.O, dp, dp, dp, Np, g.out_w, (dp, d), (dp, d), prec, N), dA, ctx.O)
+    K.gemm(dA, w.W_o, dO, Np, dp, dp, dp, dp, dp, precision=_rp("out_dx", prec), flops=2.0 * N * d * d)
+    off.run(lambda: _wgrad(dA, dp, ctx.O, dp, dp, dp, Np, g.out_w, (dp, d), (dp, d), _rp("out_dw", prec), N), dA, ctx.O)
     del dA
     # attention core
     QKV = ctx.QKV
@@ -371,21 +380,21 @@ def encoder_layer_backward(dX2: torch.Tensor, ctx: EncoderLayerCtx, w: PackedLay
     K.rowdot(dO, dp, ctx.O, dp, delta, Np, dp)
     dS = torch.empty(Np, Np, device=dev, dtype=f32)
     K.gemm(dO, V, dS, Np, Np, dp, dp, 3 * dp, Np, trans_b=True, epilogue=E.EPI_ATTN_DS_SIGNED, aux0=ctx.Pd,
-           p_drop=pd, rowvec=delta, ld_aux=Np, precision=prec, flops=att)
+           p_drop=pd, rowvec=delta, ld_aux=Np, precision=_rp("ds", prec), flops=att)
     dQKV = torch.empty(Np, 3 * dp, device=dev, dtype=f32)
-    _gemm_nodes_k(ctx.Pd, dO, dQKV[:, 2 * dp:], Np, dp, Np, Np, dp, 3 * dp, trans_a=True, prec=prec, flops=att,
+    _gemm_nodes_k(ctx.Pd, dO, dQKV[:, 2 * dp:], Np, dp, Np, Np, dp, 3 * dp, trans_a=True, prec=_rp("dv", prec), flops=att,
                   clamp_a=pd > 0)
-    _gemm_nodes_k(dS, Kt, dQKV[:, :dp], Np, dp, Np, Np, 3 * dp, 3 * dp, alpha=1.0 / math.sqrt(d), prec=prec,
+    _gemm_nodes_k(dS, Kt, dQKV[:, :dp], Np, dp, Np, Np, 3 * dp, 3 * dp, alpha=1.0 / math.sqrt(d), prec=_rp("dq", prec),
                   flops=att)
-    _gemm_nodes_k(dS, Q, dQKV[:, dp:2 * dp], Np, dp, Np, Np, 3 * dp, 3 * dp, trans_a=True, prec=prec, flops=att)
+    _gemm_nodes_k(dS, Q, dQKV[:, dp:2 * dp], Np, dp, Np, Np, 3 * dp, 3 * dp, trans_a=True, prec=_rp("dk", prec), flops=att)
     del dS, dO
     # in-projection
     if need_dx:
-        _gemm_split(dQKV, w.W_in, dX, Np, dp, 3 * dp, 3 * dp, dp, dp, accumulate=True, prec=prec,
+        _gemm_split(dQKV, w.W_in, dX, Np, dp, 3 * dp, 3 * dp, dp, dp, accumulate=True, prec=_rp("in_dx", prec),
                     flops=6.0 * N * d * d)
 
     def in_proj_grads(dQKV=dQKV):
-        _wgrad(dQKV, 3 * dp, ctx.X, dp, 3 * dp, dp, Np, g.in_w, (dp, d), (dp, d), prec, N)
+        _wgrad(dQKV, 3 * dp, ctx.X, dp, 3 * dp, dp, Np, g.in_w, (dp, d), (dp, d), _rp("in_dw", prec), N)
         _bias_grad(dQKV, Np, 3 * dp, 3 * dp, (dp, d), g.in_b)
     off.run(in_proj_grads, dQKV, ctx.X)
     if own:

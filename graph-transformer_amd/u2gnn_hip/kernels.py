@@ -134,10 +134,12 @@ def gather_rows(src, idx, idx_stride, dst, n_rows, n_rows_pad, d, d_pad, err=Non
                                       _s()), "u2gnn_gather_rows")
 
 
-def scatter_add_rows(src, idx, idx_stride, dst, n_rows, d):
+def scatter_add_rows(src, idx, idx_stride, dst, n_rows, d, err=None):
+    """dst[idx[i]] += src[i] for i < n_rows; out-of-range indices are skipped and flag err (int32[1])."""
     _dev(src, idx, dst)
     check(hip_lib().u2gnn_scatter_add_rows(_p(src), src.stride(0), _p(idx), int(idx_stride), _p(dst), dst.stride(0),
-                                           int(n_rows), int(d), _s()), "u2gnn_scatter_add_rows")
+                                           dst.shape[0], int(n_rows), int(d), _p(err), _s()),
+          "u2gnn_scatter_add_rows")
 
 
 def slab_reduce(src, n_slab, slab_stride, rows_pad, cols_pad, ld_src, rblk, cblk, dst, ld_dst, alpha=1.0,

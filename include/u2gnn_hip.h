@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define U2GNN_ABI_VERSION 3
+#define U2GNN_ABI_VERSION 4
 
 #define U2GNN_OK 0
 #define U2GNN_E_ARG (-1)    /* bad size / null pointer */
@@ -119,9 +119,11 @@ int u2gnn_abi_version(void);
 int u2gnn_gather_rows(const float *src, int64_t ld_src, int64_t src_rows, const int64_t *idx,
                       int64_t idx_stride, float *dst, int64_t ld_dst, int64_t n_rows,
                       int64_t n_rows_pad, int64_t d, int64_t d_pad, int32_t *err, void *stream);
-/* backward of the gather: dst[idx[i*idx_stride], 0:d] += src[i, 0:d] (fp32 atomics) */
+/* backward of the gather: dst[idx[i*idx_stride], 0:d] += src[i, 0:d] (fp32 atomics) for i < n_rows.
+ * Indices outside [0, dst_rows) add nothing and set *err = 1 (err may be NULL). */
 int u2gnn_scatter_add_rows(const float *src, int64_t ld_src, const int64_t *idx, int64_t idx_stride,
-                           float *dst, int64_t ld_dst, int64_t n_rows, int64_t d, void *stream);
+                           float *dst, int64_t ld_dst, int64_t dst_rows, int64_t n_rows, int64_t d,
+                           int32_t *err, void *stream);
 
 /* ---- a3.x: every dense contraction of the encoder (in-proj, Q.K^T, P.V, out-proj, FFN)
  * and of its backward  (torch TransformerEncoderLayer at pytorch_U2GNN_Sup.py:19-21,35;

@@ -23,7 +23,7 @@ def test_libraries_export_every_header_symbol(header, loader):
     missing = [s for s in syms if not hasattr(lib, s)]
     assert not missing, missing
     if loader == "hip_lib":
-        assert lib.u2gnn_abi_version() == _lib.ABI_VERSION == 3
+        assert lib.u2gnn_abi_version() == _lib.ABI_VERSION == 4
 
 
 def test_kernel_wrappers_refuse_host_tensors():
@@ -220,3 +220,17 @@ def test_native_assembly_equals_numpy_form_and_stream():
     np.random.seed(3)
     b = store.assemble_numpy([40, 2], 16)
     assert np.array_equal(a.input_x, b.input_x)
+
+
+def test_device_batch_rejects_out_of_range_input_x():
+    """F.embedding(input_x, X_concat) raises IndexError for an entry outside [0, N)
+    (pytorch_U2GNN_Sup.py:32); the batch constructors check before anything reaches a kernel."""
+    import numpy as np
+    from u2gnn_hip.core import DeviceBatch
+    X = np.zeros((5, 3), np.float32)
+    off = np.array([0, 2, 5])
+    for bad in (5, -1):
+        ix = np.tile(np.arange(5)[:, None], (1, 3))
+        ix[4, 2] = bad
+        with pytest.raises(IndexError):
+            DeviceBatch.from_offsets(ix, off, X, np.array([0, 1]), device="cpu")

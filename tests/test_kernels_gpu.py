@@ -298,6 +298,20 @@ def test_gather_pack_colsum():
     K.gather_rows(src, idx, 5, dst, 30, 64, 7, 64, err)
     assert torch.equal(dst[:30, :7], src[idx[:, 0]]) and dst[30:].abs().max() == 0 and dst[:, 7:].abs().max() == 0
     assert err.item() == 0
+    # out-of-range entries (F.embedding raises IndexError): gather writes zeros, scatter adds nothing,
+    # both flag err and touch no memory outside the buffers
+    bad = idx.clone()
+    bad[3, 0], bad[7, 0] = 50, -1
+    K.gather_rows(src, bad, 5, dst, 30, 64, 7, 64, err)
+    assert err.item() == 1 and dst[3].abs().max() == 0 and dst[7].abs().max() == 0
+    assert torch.equal(dst[4, :7], src[bad[4, 0]])
+    err.zero_()
+    acc = torch.zeros(50, 7, device=DEV)
+    K.scatter_add_rows(src[:30], bad, 5, acc, 30, 7, err)
+    good = torch.ones(30, dtype=torch.bool, device=DEV)
+    good[3] = good[7] = False
+    ref = torch.zeros(50, 7, device=DEV).index_add_(0, bad[good, 0], src[:30][good])
+    assert err.item() == 1 and (acc - ref).abs().max().item() < 1e-5
     W = _mk(3 * 7, 7, seed=16)
     Wp = torch.empty(3 * 64, 64, device=DEV)
     K.pack_padded(W, 7, 3 * 64, 64, (64, 7), (64, 7), Wp, 64)

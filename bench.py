@@ -32,6 +32,17 @@ METRIC = "graphs/sec (fwd+bwd) U2GNN-Sup COLLAB k=16 T=4 at 1/2/4/8 MI355X"
 PEAK = {"fp32": 157.3,     # TFLOP/s dense f32-input MFMA peak (MI355X_MICROARCH.md)
         "bf16x3": 2500.0 / 3,  # 2.5 PF dense bf16 MFMA / 3 MFMAs per fp32-accurate product
         "bf16": 2500.0}
+DTYPE = {"fp32": "fp32", "bf16x3": "bf16x3", "bf16": "bf16",
+         "mixed": "bf16x3 (dS/dQ/dK: bf16)"}
+
+
+def kernel_precision(symbol: str) -> str:
+    """Precision of a GEMM template instance from its name (kernels.gemm_symbol: the 9th template
+    argument is true for the bf16x3 split)."""
+    if symbol.startswith("gemm_f32"):
+        return "fp32"
+    args = symbol[symbol.index("<") + 1:symbol.rindex(">")].split(",")
+    return "bf16x3" if args[8].strip() == "true" else "bf16"
 
 
 def parse():
@@ -48,7 +59,9 @@ def parse():
     ap.add_argument("--num-timesteps", type=int, default=4)
     ap.add_argument("--ff-hidden-size", type=int, default=1024)
     ap.add_argument("--num-hidden-layers", type=int, default=1)
-    ap.add_argument("--precision", default="bf16x3", choices=["fp32", "bf16x3", "bf16"])
+    ap.add_argument("--precision", default="bf16x3", choices=["fp32", "bf16x3", "mixed", "bf16"],
+                    help="mixed = bf16x3 with the attention-backward dS/dQ/dK products on plain bf16 "
+                         "(experiment: +4 %% at C4, outside the 1e-3 bound on the MUTAG L2T2 golden)")
     ap.add_argument("--lr", type=float, default=5e-4)
     ap.add_argument("--distinct-batches", type=int, default=8)
     ap.add_argument("--cpu-baseline", type=int, default=1, help="1 = time the CPU oracle on rank 0 at N=1")
@@ -336,9 +349,10 @@ def main():
         dom = max(summ, key=lambda k: summ[k][2])
         n, fl, ms = summ[dom]
         ach = fl / (ms * 1e-3) / 1e12
-        peak = PEAK[args.precision]
+        peak = PEAK[kernel_precision(dom)]
         fam = sorted(summ.items(), key=lambda kv: -kv[1][2])
         roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
+                "kernel_precision": kernel_precision(dom),
                 "frac": round(ach / peak, 4), "traffic": pmc_traffic(dom),
                 "kernel": dom, "launches": n, "avg_launch_us": round(1e3 * ms / n, 1),
                 "algorithmic_flop_per_launch": round(fl / n),
@@ -348,7 +362,7 @@ def main():
                 "step_tflops_per_gpu": round(step_flops / (elapsed / args.steps) / 1e12, 2)}
     out = {"metric": METRIC, "value": round(value, 2), "unit": "graphs/s", "n_gpus": world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 3), "higher_is_better": True,
-           "scaling": "weak", "vs_baseline": None, "dtype": args.precision,
+           "scaling": "weak", "vs_baseline": None, "dtype": DTYPE[args.precision],
            "data": "synthetic COLLAB-like graphs (5000 graphs, mean 74.49 nodes, degree-tag one-hot d=367, "
                    "3 classes); random-init weights",
            "config": {"workload": "U2GNN-Sup COLLAB (C4): batch_size=64/GPU, num_neighbors=16, num_timesteps=4, "

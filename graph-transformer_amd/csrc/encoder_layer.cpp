@@ -34,6 +34,7 @@ inline int64_t rows_pad(int64_t N) { return N >= 1024 ? rup(N, 256) : rup(N, 128
 struct Dims {
     int64_t N, d, ff, Np, dp, ffp;
     int prec;
+    int prec_ab;   // dS, dQ, dK products (U2GNN_LAYER_ATTN_BWD_BF16: plain bf16)
     bool deep_wgrad;
     int window;   // 0: attention over all N rows; W: within windows of W rows (N % W == 0)
 };
@@ -47,6 +48,8 @@ Dims make_dims(const u2gnn_layer_dims *a) {
     D.dp = rup(a->d, 64);
     D.ffp = rup(a->ff, 64);
     D.prec = a->precision;
+    D.prec_ab = (a->precision == U2GNN_PREC_BF16X3 && (a->flags & U2GNN_LAYER_ATTN_BWD_BF16)) ? U2GNN_PREC_BF16
+                                                                                             : a->precision;
     D.deep_wgrad = (a->flags & U2GNN_LAYER_DEEP_WGRAD) != 0;
     D.window = a->window;
     return D;
@@ -146,8 +149,9 @@ bool shallow_nosplit_on() {   // engine._SHALLOW_NOSPLIT
 // padded->real block map).  deep = weight gradient (16-deep K step, <= 16 slabs).
 int gemm_split(Arena &W, const Dims &D, const float *A, const float *B, float *C, int64_t M, int64_t N, int64_t Kd,
                int64_t lda, int64_t ldb, int64_t ldc, bool ta, float alpha, bool accumulate, const int64_t *rblk,
-               const int64_t *cblk, bool deep, hipStream_t st, bool clamp_a = false) {
-    const bool f32 = D.prec == U2GNN_PREC_F32;
+               const int64_t *cblk, bool deep, hipStream_t st, bool clamp_a = false, int prec = -1) {
+    if (prec < 0) prec = D.prec;
+    const bool f32 = prec == U2GNN_PREC_F32;
     const int64_t bk = f32 ? 16 : 32;
     const bool plan = W.plan();
     const bool mapped = rblk != nullptr;
@@ -155,7 +159,7 @@ int gemm_split(Arena &W, const Dims &D, const float *A, const float *B, float *C
         (M / 64) * (N / 64) >= 256) {
         // shallow K (dH.W1, dQKV.W_in) with enough 64x64 tiles to fill the chip: no split, the
         // epilogue accumulates straight into C (no slabs, no reduce pass)
-        G g(A, B, C, M, N, Kd, lda, ldb, ldc, D.prec);
+        G g(A, B, C, M, N, Kd, lda, ldb, ldc, prec);
         if (ta) g.ta();
         g.a.alpha = alpha;
         g.a.clamp_a = clamp_a;
@@ -181,7 +185,7 @@ int gemm_split(Arena &W, const Dims &D, const float *A, const float *B, float *C
         if (split < 1) split = 1;
     }
     if (split == 1 && !mapped) {
-        G g(A, B, C, M, N, Kd, lda, ldb, ldc, D.prec);
+        G g(A, B, C, M, N, Kd, lda, ldb, ldc, prec);
         if (ta) g.ta();
         g.a.alpha = alpha;
         g.a.clamp_a = clamp_a;
@@ -189,7 +193,7 @@ int gemm_split(Arena &W, const Dims &D, const float *A, const float *B, float *C
         return g.run(st, plan);
     }
     float *slabs = W.take<float>(split * M * N);
-    G g(A, B, slabs, M, N, Kd, lda, ldb, N, D.prec);
+    G g(A, B, slabs, M, N, Kd, lda, ldb, N, prec);
     if (ta) g.ta();
     g.a.split_k = (int32_t)split;
     g.a.slab_stride = M * N;
@@ -408,7 +412,7 @@ int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
         if (!plan) U2GNN_TRY(u2gnn_rowdot(dO, dp, c.O, dp, delta, Np, dp, st));
         float *dS = W.take<float>(Np * Np);
         {
-            G gg(dO, V, dS, Np, Np, dp, dp, 3 * dp, Np, prec);
+            G gg(dO, V, dS, Np, Np, dp, dp, 3 * dp, Np, D.prec_ab);
             gg.tb().epi(U2GNN_EPI_ATTN_DS_SIGNED);
             gg.a.aux0 = c.Pd, gg.a.rowvec = delta, gg.a.ld_aux = Np, gg.a.p_drop = pd;
             U2GNN_TRY(gg.run(st, plan));
@@ -420,13 +424,13 @@ int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
         if (dk_side) {
             U2GNN_TRY(sd.fork());
             U2GNN_TRY(gemm_split(W, D, dS, Q, dQKV + dp, Np, dp, Np, Np, 3 * dp, 3 * dp, true, 1.f, false, nullptr,
-                                 nullptr, false, so));
+                                 nullptr, false, so, false, D.prec_ab));
         }
         U2GNN_TRY(gemm_split(W, D, dS, Kt, dQKV, Np, dp, Np, Np, 3 * dp, 3 * dp, false, q_scale, false, nullptr, nullptr,
-                             false, st));
+                             false, st, false, D.prec_ab));
         if (!dk_side)
             U2GNN_TRY(gemm_split(W, D, dS, Q, dQKV + dp, Np, dp, Np, Np, 3 * dp, 3 * dp, true, 1.f, false, nullptr,
-                                 nullptr, false, st));
+                                 nullptr, false, st, false, D.prec_ab));
         if (dv_side) U2GNN_TRY(sd.join());
     }
     // in-projection

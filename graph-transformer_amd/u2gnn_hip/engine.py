@@ -207,10 +207,20 @@ BIG_TILE_BLOCKS = 768
 ROLES = ("in_proj", "qk", "pv", "out_proj", "ffn1", "ffn2", "ffn2_dx", "ffn2_dw", "ffn1_dx", "ffn1_dw",
          "out_dx", "out_dw", "dv", "ds", "dq", "dk", "in_dx", "in_dw")
 ROLE_BF16 = set(r for r in os.environ.get("U2GNN_BF16_ROLES", "").split(",") if r)
+# precision "mixed" (experiment, not parity-grade): bf16x3 everywhere except the attention-backward
+# products dS, dQ, dK on plain bf16 (u2gnn_hip.h U2GNN_LAYER_ATTN_BWD_BF16).  Joint error on C4
+# batches (tools/prec_probe.py --mixed, profiles/r02/r2b_mixed_probe.log) 2.5e-4..4.0e-4 of the 1e-3
+# bound, but the MUTAG L2T2 golden (d = 7) exceeds it; +4 % C4 step rate.  The forward products and
+# the weight/input-gradient products are far outside the bound in plain bf16 (0.09..0.39: ReLU units
+# flipping), so they stay bf16x3.
+MIXED_BF16_ROLES = ("ds", "dq", "dk")
 
 
 def _rp(role: str, prec: str) -> str:
-    return "bf16" if (prec == "bf16x3" and role in ROLE_BF16) else prec   # U2GNN_BIG_TILE_BLOCKS (u2gnn_hip.h): token-sized products on 256x128 blocks
+    """Matrix-core precision of one product (role) of a layer running at `prec`."""
+    if prec == "mixed":
+        return "bf16" if role in MIXED_BF16_ROLES else "bf16x3"
+    return "bf16" if (prec == "bf16x3" and role in ROLE_BF16) else prec
 
 
 def _gemm_split(A, B, C, M, N, Kd, lda, ldb, ldc, trans_a=False, trans_b=False, alpha=1.0, accumulate=False,

@@ -39,7 +39,10 @@ def set_enabled(on: bool) -> bool:
 
 
 def _dims(N: int, d: int, ff: int, prec: str, deep_wgrad: bool, window: int = 0) -> LayerDims:
-    return LayerDims(int(N), int(d), int(ff), PREC[prec], _lib.LAYER_DEEP_WGRAD if deep_wgrad else 0, int(window), 0)
+    flags = _lib.LAYER_DEEP_WGRAD if deep_wgrad else 0
+    if prec == "mixed":   # bf16x3 except the attention-backward products dS, dQ, dK (engine.MIXED_BF16_ROLES)
+        prec, flags = "bf16x3", flags | _lib.LAYER_ATTN_BWD_BF16
+    return LayerDims(int(N), int(d), int(ff), PREC[prec], flags, int(window), 0)
 
 
 def sizes(N: int, d: int, ff: int, prec: str, p_drop: float, deep_wgrad: bool = True, window: int = 0):

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define U2GNN_ABI_VERSION 4
+#define U2GNN_ABI_VERSION 5
 
 #define U2GNN_OK 0
 #define U2GNN_E_ARG (-1)    /* bad size / null pointer */
@@ -285,6 +285,10 @@ int u2gnn_window_attn_bwd(const float *QKV, int64_t ldq, int32_t W, int32_t dp, 
  * side_stream (NULL: same stream) after the main-stream results it reads; the caller joins the
  * streams before reading grads and must keep X, ctx, dX2 and ws alive until side_stream drains. */
 #define U2GNN_LAYER_DEEP_WGRAD 1   /* weight gradients on the 16-deep-K 128x128 tile */
+/* precision "mixed" (ABI v5): with precision == U2GNN_PREC_BF16X3, the three attention-backward
+ * node-depth products dS = P o (dO V^T - delta), dQ = dS K, dK = dS^T Q run on plain bf16
+ * operands (fp32 accumulation); every other product stays bf16x3 */
+#define U2GNN_LAYER_ATTN_BWD_BF16 2
 typedef struct u2gnn_layer_dims {
     int64_t N, d, ff;      /* real rows (nodes; window mode: nodes * window tokens), model width, FFN width */
     int32_t precision;     /* U2GNN_PREC_* */

@@ -25,7 +25,7 @@ def _zeros_like_params(p: LayerParams) -> LayerParams:
 
 
 @pytest.mark.parametrize("N,d,ff", [(300, 67, 128), (1000, 367, 1024)])
-@pytest.mark.parametrize("prec", ["bf16x3", "fp32"])
+@pytest.mark.parametrize("prec", ["bf16x3", "fp32", "mixed"])
 @pytest.mark.parametrize("train", [True, False])
 @pytest.mark.parametrize("side", [False, True])
 def test_native_layer_matches_python_orchestration(N, d, ff, prec, train, side):
@@ -73,3 +73,34 @@ def test_native_forward_without_ctx_matches():
     Y, c = native.layer_forward(X, packed, p, dims, False, {}, False, "bf16x3", 0.5)
     assert c is None
     assert torch.equal(Y, Y_ref)
+
+
+def test_mixed_precision_only_changes_attention_backward():
+    """precision "mixed": the forward is the bf16x3 forward bit for bit; the backward differs
+    (dS, dQ, dK on plain bf16) but stays within bf16 rounding of the bf16x3 backward."""
+    N, d, ff = 1000, 367, 1024
+    layer = _layer(d, ff, 5)
+    p = LayerParams.from_encoder_layer(layer)
+    dims = Dims(N, d, ff)
+    packed = PackedLayer(d, ff, "cuda")
+    packed.pack(p)
+    seeds = {s: site_seed(77, 0, 1, s) for s in (SITE_ATTN, SITE_DROP1, SITE_DROPFF, SITE_DROP2)}
+    g = torch.Generator(device="cuda").manual_seed(3)
+    X = torch.zeros(dims.Np, dims.dp, device="cuda")
+    X[:N, :d] = torch.randn(N, d, device="cuda", generator=g)
+    dY = torch.zeros(dims.Np, dims.dp, device="cuda")
+    dY[:N, :d] = torch.randn(N, d, device="cuda", generator=g)
+    out = {}
+    for prec in ("bf16x3", "mixed"):
+        Y, ctx = native.layer_forward(X, packed, p, dims, True, seeds, True, prec, 0.5)
+        gg = _zeros_like_params(p)
+        dX = native.layer_backward(dY, ctx, packed, p, gg, dims, prec)
+        torch.cuda.synchronize()
+        out[prec] = (Y, dX, gg)
+    assert torch.equal(out["mixed"][0], out["bf16x3"][0])
+    a, b = out["mixed"][1], out["bf16x3"][1]
+    assert not torch.equal(a, b)
+    assert ((a - b).abs().max() / b.abs().max()).item() < 2e-2
+    # the FFN weight gradients do not depend on the attention backward at all
+    assert torch.equal(out["mixed"][2].l1_w, out["bf16x3"][2].l1_w)
+    assert not torch.equal(out["mixed"][2].in_w, out["bf16x3"][2].in_w)

@@ -63,6 +63,17 @@ def main():
                           "scores": e["scores"], "loss": e["loss"]}), flush=True)
         return e[worst]
 
+    if "--mixed" in sys.argv:
+        # joint error of the attention-backward roles in plain bf16, eval and train mode (same
+        # dropout masks in every run: counter-based), several batches
+        more = [loaders() for _ in range(2)]
+        for bi, hb in enumerate(hbs + more):
+            for train in (False, True):
+                ref = run("fp32", [], hb, train)
+                report(f"b{bi} train={train} bf16x3", run("bf16x3", [], hb, train), ref)
+                for combo in (["ds", "dq", "dk"], ["ds", "dq", "dk", "dv"], ["dq", "dk"], ["dq", "dk", "dv"]):
+                    report(f"b{bi} train={train} bf16:{'+'.join(combo)}", run("bf16x3", combo, hb, train), ref)
+        return
     for bi, hb in enumerate(hbs):
         ref = run("fp32", [], hb)
         if "--oracle" in sys.argv and bi == 0:

@@ -119,6 +119,19 @@ Ctx carve_ctx(Arena &A, const Dims &D, bool drop) {
     return c;
 }
 
+// live launch timing of one role (u2gnn_probe_arm / u2gnn_probe_collect)
+struct Probe {
+    int role = 0, cap = 0, n = 0;
+    hipEvent_t *ev = nullptr;   // [2 * cap]: start, end
+};
+Probe g_probe;
+
+void probe_mark(int role, bool end, hipStream_t st, bool plan) {
+    if (plan || g_probe.role != role || g_probe.n >= g_probe.cap) return;
+    (void)hipEventRecord(g_probe.ev[2 * g_probe.n + (end ? 1 : 0)], st);
+    if (end) ++g_probe.n;
+}
+
 struct G {   // one GEMM launch (defaults = plain store)
     u2gnn_gemm_args a;
     G(const float *A, const float *B, float *C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
@@ -149,7 +162,7 @@ bool shallow_nosplit_on() {   // engine._SHALLOW_NOSPLIT
 // padded->real block map).  deep = weight gradient (16-deep K step, <= 16 slabs).
 int gemm_split(Arena &W, const Dims &D, const float *A, const float *B, float *C, int64_t M, int64_t N, int64_t Kd,
                int64_t lda, int64_t ldb, int64_t ldc, bool ta, float alpha, bool accumulate, const int64_t *rblk,
-               const int64_t *cblk, bool deep, hipStream_t st, bool clamp_a = false, int prec = -1) {
+               const int64_t *cblk, bool deep, hipStream_t st, bool clamp_a = false, int prec = -1, int role = 0) {
     if (prec < 0) prec = D.prec;
     const bool f32 = prec == U2GNN_PREC_F32;
     const int64_t bk = f32 ? 16 : 32;
@@ -165,7 +178,10 @@ int gemm_split(Arena &W, const Dims &D, const float *A, const float *B, float *C
         g.a.clamp_a = clamp_a;
         const bool big = M % 256 == 0 && N % 128 == 0 && (M / 256) * (N / 128) >= U2GNN_BIG_TILE_BLOCKS;
         g.epi(accumulate ? U2GNN_EPI_ACCUM : U2GNN_EPI_STORE).tile(big ? 256 : 64);
-        return g.run(st, plan);
+        probe_mark(role, false, st, plan);
+        const int rc = g.run(st, plan);
+        probe_mark(role, true, st, plan);
+        return rc;
     }
     int t;
     int64_t tiles, target = 448;
@@ -190,7 +206,10 @@ int gemm_split(Arena &W, const Dims &D, const float *A, const float *B, float *C
         g.a.alpha = alpha;
         g.a.clamp_a = clamp_a;
         g.epi(accumulate ? U2GNN_EPI_ACCUM : U2GNN_EPI_STORE).tile(t);
-        return g.run(st, plan);
+        probe_mark(role, false, st, plan);
+        const int rc = g.run(st, plan);
+        probe_mark(role, true, st, plan);
+        return rc;
     }
     float *slabs = W.take<float>(split * M * N);
     G g(A, B, slabs, M, N, Kd, lda, ldb, N, prec);
@@ -199,7 +218,9 @@ int gemm_split(Arena &W, const Dims &D, const float *A, const float *B, float *C
     g.a.slab_stride = M * N;
     g.a.clamp_a = clamp_a;
     g.tile(t);
+    probe_mark(role, false, st, plan);
     U2GNN_TRY(g.run(st, plan));
+    probe_mark(role, true, st, plan);
     if (plan) return U2GNN_OK;
     const int64_t rb0 = rblk ? rblk[0] : M, rb1 = rblk ? rblk[1] : M;
     const int64_t cb0 = cblk ? cblk[0] : N, cb1 = cblk ? cblk[1] : N;
@@ -299,13 +320,15 @@ int layer_fwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
         {
             G g(Q, Kt, S, Np, Np, dp, 3 * dp, 3 * dp, Np, prec);
             g.tb().tile((prec != U2GNN_PREC_F32 && Np % 256 == 0) ? 256 : 0);
+            probe_mark(U2GNN_ROLE_QK, false, st, plan);
             U2GNN_TRY(g.run(st, plan));
+            probe_mark(U2GNN_ROLE_QK, true, st, plan);
         }
         if (!plan)
             U2GNN_TRY(u2gnn_attn_softmax_fwd(S, Np, drop ? nullptr : c.Pd, c.Pd, Np, N, Np, N, Np, pd, s->attn,
                                              nullptr, 0, st));
         U2GNN_TRY(gemm_split(W, D, c.Pd, V, c.O, Np, dp, Np, Np, 3 * dp, dp, false, 1.f, false, nullptr, nullptr,
-                             false, st, drop));
+                             false, st, drop, -1, U2GNN_ROLE_PV));
     }
     // a3.3 out-projection + dropout1 + residual, LayerNorm1
     {
@@ -406,7 +429,7 @@ int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
         if (dv_side) {   // dV needs only Pd and dO: overlap it with the dS chain
             U2GNN_TRY(sd.fork());
             U2GNN_TRY(gemm_split(W, D, c.Pd, dO, dQKV + 2 * dp, Np, dp, Np, Np, dp, 3 * dp, true, 1.f, false, nullptr,
-                                 nullptr, false, so, pd > 0.f));
+                                 nullptr, false, so, pd > 0.f, -1, U2GNN_ROLE_DV));
         }
         float *delta = W.take<float>(Np);
         if (!plan) U2GNN_TRY(u2gnn_rowdot(dO, dp, c.O, dp, delta, Np, dp, st));
@@ -415,22 +438,24 @@ int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
             G gg(dO, V, dS, Np, Np, dp, dp, 3 * dp, Np, D.prec_ab);
             gg.tb().epi(U2GNN_EPI_ATTN_DS_SIGNED);
             gg.a.aux0 = c.Pd, gg.a.rowvec = delta, gg.a.ld_aux = Np, gg.a.p_drop = pd;
+            probe_mark(U2GNN_ROLE_DS, false, st, plan);
             U2GNN_TRY(gg.run(st, plan));
+            probe_mark(U2GNN_ROLE_DS, true, st, plan);
         }
         if (!dv_side)
             U2GNN_TRY(gemm_split(W, D, c.Pd, dO, dQKV + 2 * dp, Np, dp, Np, Np, dp, 3 * dp, true, 1.f, false, nullptr,
-                                 nullptr, false, st, pd > 0.f));
+                                 nullptr, false, st, pd > 0.f, -1, U2GNN_ROLE_DV));
         const bool dk_side = dv_side && dk_side_on();
         if (dk_side) {
             U2GNN_TRY(sd.fork());
             U2GNN_TRY(gemm_split(W, D, dS, Q, dQKV + dp, Np, dp, Np, Np, 3 * dp, 3 * dp, true, 1.f, false, nullptr,
-                                 nullptr, false, so, false, D.prec_ab));
+                                 nullptr, false, so, false, D.prec_ab, U2GNN_ROLE_DK));
         }
         U2GNN_TRY(gemm_split(W, D, dS, Kt, dQKV, Np, dp, Np, Np, 3 * dp, 3 * dp, false, q_scale, false, nullptr, nullptr,
-                             false, st, false, D.prec_ab));
+                             false, st, false, D.prec_ab, U2GNN_ROLE_DQ));
         if (!dk_side)
             U2GNN_TRY(gemm_split(W, D, dS, Q, dQKV + dp, Np, dp, Np, Np, 3 * dp, 3 * dp, true, 1.f, false, nullptr,
-                                 nullptr, false, st, false, D.prec_ab));
+                                 nullptr, false, st, false, D.prec_ab, U2GNN_ROLE_DK));
         if (dv_side) U2GNN_TRY(sd.join());
     }
     // in-projection
@@ -492,6 +517,42 @@ int u2gnn_layer_bwd(const u2gnn_layer_dims *dims, const u2gnn_layer_params *w, c
     Arena C(const_cast<void *>(ctx), ctx_bytes), W(ws ? ws : empty_ws, ws ? ws_bytes : 0);
     return layer_bwd(D, w, s, X, C, dX2, dX, g, W, reinterpret_cast<hipStream_t>(stream),
                      reinterpret_cast<hipStream_t>(side_stream), dX != nullptr);
+}
+
+int u2gnn_probe_arm(int32_t role, int32_t capacity) {
+    if (g_probe.ev) return U2GNN_E_ARG;   // collect the previous probe first
+    if (role < U2GNN_ROLE_QK || role > U2GNN_ROLE_DK || capacity < 1 || capacity > (1 << 16)) return U2GNN_E_ARG;
+    hipEvent_t *ev = new hipEvent_t[2 * capacity];
+    for (int i = 0; i < 2 * capacity; ++i) {
+        const hipError_t e = hipEventCreate(&ev[i]);
+        if (e != hipSuccess) {
+            for (int j = 0; j < i; ++j) (void)hipEventDestroy(ev[j]);
+            delete[] ev;
+            return (int)e;
+        }
+    }
+    g_probe.ev = ev, g_probe.cap = capacity, g_probe.n = 0, g_probe.role = role;
+    return U2GNN_OK;
+}
+
+int u2gnn_probe_collect(float *total_ms, int32_t *launches) {
+    if (!total_ms || !launches) return U2GNN_E_ARG;
+    *total_ms = 0.f, *launches = 0;
+    if (!g_probe.ev) return U2GNN_OK;
+    int rc = U2GNN_OK;
+    double tot = 0.0;
+    for (int i = 0; i < g_probe.n && rc == U2GNN_OK; ++i) {
+        hipError_t e = hipEventSynchronize(g_probe.ev[2 * i + 1]);
+        float ms = 0.f;
+        if (e == hipSuccess) e = hipEventElapsedTime(&ms, g_probe.ev[2 * i], g_probe.ev[2 * i + 1]);
+        if (e != hipSuccess) rc = (int)e;
+        tot += ms;
+    }
+    for (int i = 0; i < 2 * g_probe.cap; ++i) (void)hipEventDestroy(g_probe.ev[i]);
+    delete[] g_probe.ev;
+    *total_ms = (float)tot, *launches = g_probe.n;
+    g_probe = Probe();
+    return rc;
 }
 
 }  // extern "C"

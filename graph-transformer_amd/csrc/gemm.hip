@@ -497,6 +497,7 @@ inline bool al16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) =
 }  // namespace
 
 int u2gnn_gemm_x2_dispatch(const u2gnn_gemm_args *a, GemmP &P, int tile, int split, hipStream_t st);
+int u2gnn_gemm_x3_dispatch(const u2gnn_gemm_args *a, GemmP &P, int tile, int split, hipStream_t st);
 
 extern "C" int u2gnn_gemm(const u2gnn_gemm_args *a, void *stream) {
     if (!a) return U2GNN_E_ARG;
@@ -560,11 +561,11 @@ extern "C" int u2gnn_gemm(const u2gnn_gemm_args *a, void *stream) {
             tile = 256;
     }
     // tile codes: 64, 128 (square), 256 (256x128, 8 waves), 129 (128x128 with a 16-deep K step)
-    const bool x2code = x2 && (tile == 257 || tile == 130 || (tile >= 258 && tile <= 263));
+    const bool x2code = x2 && (tile == 257 || tile == 130 || (tile >= 258 && tile <= 263) || tile == 300 || tile == 301);
     if (!x2code && tile != 64 && tile != 128 && tile != 256 && tile != 129) return U2GNN_E_ARG;
     if ((tile == 256 || tile == 129) && prec == U2GNN_PREC_F32) return U2GNN_E_ARG;
     const int tm_ = tile == 129 ? 128 : (tile > 256 ? 256 : (tile == 130 ? 128 : tile));
-    const int tile_n = (tile == 260 || tile == 262) ? 256 : (tm_ == 256 ? 128 : tm_);
+    const int tile_n = (tile == 260 || tile == 262 || tile == 300) ? 256 : (tm_ == 256 ? 128 : tm_);
     if (a->M % tm_ || a->N % tile_n) return U2GNN_E_SHAPE;
     GemmP P;
     std::memset(&P, 0, sizeof(P));
@@ -603,6 +604,7 @@ extern "C" int u2gnn_gemm(const u2gnn_gemm_args *a, void *stream) {
     P.m_valid = (int32_t)a->m_valid;
     P.n_valid = (int32_t)a->n_valid;
     hipStream_t st = u2gnn_stream(stream);
+    if (x2 && (tile == 300 || tile == 301)) return u2gnn_gemm_x3_dispatch(a, P, tile, split, st);
     if (x2) return u2gnn_gemm_x2_dispatch(a, P, tile, split, st);
     const bool ta = a->trans_a != 0, tb = a->trans_b != 0;
     const bool clamp = a->clamp_a != 0;

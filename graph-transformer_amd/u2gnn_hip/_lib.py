@@ -89,6 +89,7 @@ class LayerGrads(ctypes.Structure):
 
 LAYER_DEEP_WGRAD = 1
 LAYER_ATTN_BWD_BF16 = 2   # precision "mixed": dS, dQ, dK on plain bf16 (ABI v5)
+ROLE_QK, ROLE_PV, ROLE_DS, ROLE_DV, ROLE_DQ, ROLE_DK = range(1, 7)   # u2gnn_probe_arm roles
 
 I64, F32, VP, I32 = c_int64, c_float, c_void_p, c_int32
 
@@ -127,6 +128,8 @@ _HIP_SIGS = {
     "u2gnn_sampled_softmax_bwd": ([VP, I64, VP, VP, I64, VP, I64, VP, VP, VP, I64, VP, I64, I64, I64, VP], c_int32),
     "u2gnn_dropout_mask": ([c_uint64, I64, I64, F32, VP, VP], c_int32),
     "u2gnn_dropout": ([VP, I64, VP, I64, I64, I64, F32, c_uint64, VP], c_int32),
+    "u2gnn_probe_arm": ([I32, I32], c_int32),
+    "u2gnn_probe_collect": ([POINTER(c_float), POINTER(c_int32)], c_int32),
 }
 
 _LUS_SIGS = {

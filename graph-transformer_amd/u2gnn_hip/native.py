@@ -117,3 +117,16 @@ def layer_backward(dX2: torch.Tensor, ctx: NativeCtx, packed, p, g, dims, prec: 
         for t in (ws, ctx.buf, ctx.X, dX2):
             t.record_stream(side)
     return dX
+
+
+def probe_arm(role: int, capacity: int) -> None:
+    """Time the next `capacity` executor launches of one product (``_lib.ROLE_*``) with HIP events
+    recorded on the stream each kernel runs on (u2gnn_probe_arm)."""
+    check(hip_lib().u2gnn_probe_arm(int(role), int(capacity)), "u2gnn_probe_arm")
+
+
+def probe_collect():
+    """(summed device milliseconds, launches) of the armed probe; frees its events."""
+    ms, n = ctypes.c_float(), ctypes.c_int32()
+    check(hip_lib().u2gnn_probe_collect(ctypes.byref(ms), ctypes.byref(n)), "u2gnn_probe_collect")
+    return float(ms.value), int(n.value)

@@ -322,6 +322,21 @@ int u2gnn_layer_bwd(const u2gnn_layer_dims *dims, const u2gnn_layer_params *w,
                     const float *dX2, float *dX, const u2gnn_layer_grads *g, void *ws,
                     int64_t ws_bytes, void *stream, void *side_stream);
 
+/* ---- ABI v5: live launch timing of one product of the layer executor (diagnostics) ----
+ * u2gnn_probe_arm(role, capacity) creates `capacity` pairs of timing events; every following
+ * u2gnn_layer_fwd/bwd launch of that role is bracketed by a pair recorded on the stream the kernel
+ * runs on (the first `capacity` launches).  u2gnn_probe_collect waits for the recorded events and
+ * returns the summed device time and the launch count, then frees the events.  One probe per
+ * process; arm/collect from the thread that issues the layers (bench.py's timed region). */
+#define U2GNN_ROLE_QK 1   /* S = Q K^T                                   */
+#define U2GNN_ROLE_PV 2   /* O = Pd V (split-K GEMM only, not its reduce) */
+#define U2GNN_ROLE_DS 3   /* dS = P o (dO V^T - delta)                   */
+#define U2GNN_ROLE_DV 4
+#define U2GNN_ROLE_DQ 5
+#define U2GNN_ROLE_DK 6
+int u2gnn_probe_arm(int32_t role, int32_t capacity);
+int u2gnn_probe_collect(float *total_ms, int32_t *launches);
+
 #ifdef __cplusplus
 }
 #endif

@@ -201,3 +201,27 @@ def test_ds_recompute_epilogue_matches_signed(N, p):
     scale = dS_ref.abs().max().item()
     assert (dS - dS_ref).abs().max().item() <= 1e-5 * scale
     assert (dS[N:] == 0).all() and (dS[:, N:] == 0).all()
+
+
+@pytest.mark.parametrize("Np,Kd", [(512, 384), (1024, 64), (2304, 416)])
+def test_x3_persistent_nt_kernel(Np, Kd):
+    """gemm_x3.hip (tile code 301: persistent 256x128 blocks, 16x16x32 MFMAs, ping-pong waves) on
+    x2 operands: S = Q.K^T and the signed-image dS epilogue against float64 (bf16x3 accuracy)."""
+    g = torch.Generator(device="cuda").manual_seed(5)
+    A = torch.randn(Np, Kd, device="cuda", generator=g)
+    B = torch.randn(Np, Kd, device="cuda", generator=g)
+    A2, B2 = to_x2(A), to_x2(B)
+    C = torch.full((Np, Np), float("nan"), device="cuda")
+    K.gemm(A2, B2, C, Np, Np, Kd, A2.stride(0), B2.stride(0), Np, trans_b=True, precision="bf16x3", tile=301)
+    ref = A.double() @ B.double().t()
+    assert ((C.double() - ref).abs().max() / ref.abs().max()).item() < 3e-5
+    img = torch.rand(Np, Np, device="cuda", generator=g) * 1e-3
+    img = torch.where(torch.rand(Np, Np, device="cuda", generator=g) < 0.5, -img, img)
+    delta = torch.randn(Np, device="cuda", generator=g)
+    C.fill_(float("nan"))
+    K.gemm(A2, B2, C, Np, Np, Kd, A2.stride(0), B2.stride(0), Np, trans_b=True, epilogue=E.EPI_ATTN_DS_SIGNED,
+           aux0=img, rowvec=delta, ld_aux=Np, p_drop=0.5, precision="bf16x3", tile=301)
+    x = img.double()
+    dl = delta.double()[:, None]
+    refd = torch.where(x < 0, x * dl, x * (ref - 0.5 * dl))
+    assert ((C.double() - refd).abs().max() / refd.abs().max()).item() < 3e-5

@@ -104,3 +104,31 @@ def test_mixed_precision_only_changes_attention_backward():
     # the FFN weight gradients do not depend on the attention backward at all
     assert torch.equal(out["mixed"][2].l1_w, out["bf16x3"][2].l1_w)
     assert not torch.equal(out["mixed"][2].in_w, out["bf16x3"][2].in_w)
+
+
+def test_probe_times_every_launch_of_a_role():
+    """u2gnn_probe_arm/collect (bench.py's live roofline timing): every dS / QK launch of the
+    executor is bracketed by events on its own stream; capacity caps the count."""
+    from u2gnn_hip import _lib
+    N, d, ff = 1000, 367, 1024
+    layer = _layer(d, ff, 5)
+    p = LayerParams.from_encoder_layer(layer)
+    dims = Dims(N, d, ff)
+    packed = PackedLayer(d, ff, "cuda")
+    packed.pack(p)
+    seeds = {s: site_seed(77, 0, 1, s) for s in (SITE_ATTN, SITE_DROP1, SITE_DROPFF, SITE_DROP2)}
+    X = torch.zeros(dims.Np, dims.dp, device="cuda")
+    X[:N, :d] = torch.randn(N, d, device="cuda")
+    dY = torch.zeros_like(X)
+    dY[:N, :d] = torch.randn(N, d, device="cuda")
+    for role, cap, runs, want in ((_lib.ROLE_DS, 8, 3, 3), (_lib.ROLE_QK, 2, 3, 2), (_lib.ROLE_DK, 4, 2, 2)):
+        native.probe_arm(role, cap)
+        off = OffPath(X.device)
+        for _ in range(runs):
+            Y, ctx = native.layer_forward(X, packed, p, dims, True, seeds, True, "bf16x3", 0.5)
+            g = _zeros_like_params(p)
+            native.layer_backward(dY, ctx, packed, p, g, dims, "bf16x3", side=off.side)
+        off.join()
+        ms, n = native.probe_collect()
+        assert n == want and ms > 0.0, (role, n, ms)
+    assert native.probe_collect() == (0.0, 0)   # disarmed

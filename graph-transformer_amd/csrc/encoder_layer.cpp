@@ -261,12 +261,23 @@ struct Side {
     }
     // the main stream waits for everything issued on the side stream so far
     int join() {
+        hipEvent_t ev = nullptr;
+        U2GNN_TRY(mark(&ev));
+        return wait(ev);
+    }
+    // an event at the side stream's current position (joined later by wait(); nullptr when there
+    // is no separate side stream)
+    int mark(hipEvent_t *ev) {
+        *ev = nullptr;
         if (plan || side == main) return U2GNN_OK;
-        hipEvent_t ev;
-        hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
-        if (e != hipSuccess) return (int)e;
-        e = hipEventRecord(ev, side);
-        if (e == hipSuccess) e = hipStreamWaitEvent(main, ev, 0);
+        hipError_t e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventRecord(*ev, side);
+        return e == hipSuccess ? U2GNN_OK : (int)e;
+    }
+    // the main stream waits for a mark() event (released once the recorded work completes)
+    int wait(hipEvent_t ev) {
+        if (!ev) return U2GNN_OK;
+        hipError_t e = hipStreamWaitEvent(main, ev, 0);
         const hipError_t e2 = hipEventDestroy(ev);
         if (e == hipSuccess) e = e2;
         return e == hipSuccess ? U2GNN_OK : (int)e;
@@ -286,6 +297,14 @@ bool dv_side_on() {
 }
 bool dk_side_on() {
     static const bool v = env_flag("U2GNN_DK_SIDE", false);
+    return v;
+}
+// U2GNN_INPROJ_SPLIT=1: the in_proj weight gradient as three products (Q / K / V blocks), each on the
+// side stream as soon as its block of dQKV is final, instead of one product after the in-projection.
+// Measured 0.7 % slower (3.268 vs 3.245 ms/step, one-session A/B, profiles/r02/ab_inproj_split.txt):
+// the earlier side work contends with the dS -> dQ -> dK chain.
+bool inproj_split_on() {
+    static const bool v = env_flag("U2GNN_INPROJ_SPLIT", false);
     return v;
 }
 
@@ -418,6 +437,16 @@ int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
     const float *Q = c.QKV, *Kt = c.QKV + dp, *V = c.QKV + 2 * dp;
     const float q_scale = (float)(1.0 / std::sqrt((double)d));
     float *dQKV;
+    // in_proj weight / bias gradient of one of the Q (0), K (1), V (2) blocks: dQKV[:, p]^T X and
+    // its column sums, on the side stream as soon as that block of dQKV is final (the same split-K
+    // partition and reduction order per element as one [3dp, dp] product, so the same bits)
+    const bool split_in = inproj_split_on() && !D.window;
+    auto in_part = [&](int p) -> int {
+        if (!split_in) return U2GNN_OK;
+        U2GNN_TRY(wgrad(W, D, dQKV + p * dp, 3 * dp, X, dp, dp, dp, g->in_w + (int64_t)p * d * d, d, blk_d, blk_d, so));
+        return bias_grad(W, dQKV + p * dp, Np, dp, 3 * dp, dp, d, g->in_b + (int64_t)p * d, so);
+    };
+    hipEvent_t dv_done = nullptr;   // side-stream position after the dV product (in_dx waits for it)
     if (D.window) {
         dQKV = W.take<float>(Np * 3 * dp);
         if (!plan)
@@ -426,10 +455,13 @@ int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
     } else {
         dQKV = W.take<float>(Np * 3 * dp);
         const bool dv_side = dv_side_on() && so != st;
+        const bool dk_side = dv_side && dk_side_on();
         if (dv_side) {   // dV needs only Pd and dO: overlap it with the dS chain
             U2GNN_TRY(sd.fork());
             U2GNN_TRY(gemm_split(W, D, c.Pd, dO, dQKV + 2 * dp, Np, dp, Np, Np, dp, 3 * dp, true, 1.f, false, nullptr,
                                  nullptr, false, so, pd > 0.f, -1, U2GNN_ROLE_DV));
+            if (!dk_side) U2GNN_TRY(sd.mark(&dv_done));
+            U2GNN_TRY(in_part(2));
         }
         float *delta = W.take<float>(Np);
         if (!plan) U2GNN_TRY(u2gnn_rowdot(dO, dp, c.O, dp, delta, Np, dp, st));
@@ -442,29 +474,40 @@ int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
             U2GNN_TRY(gg.run(st, plan));
             probe_mark(U2GNN_ROLE_DS, true, st, plan);
         }
-        if (!dv_side)
+        if (!dv_side) {
             U2GNN_TRY(gemm_split(W, D, c.Pd, dO, dQKV + 2 * dp, Np, dp, Np, Np, dp, 3 * dp, true, 1.f, false, nullptr,
                                  nullptr, false, st, pd > 0.f, -1, U2GNN_ROLE_DV));
-        const bool dk_side = dv_side && dk_side_on();
+            U2GNN_TRY(sd.fork());
+            U2GNN_TRY(in_part(2));
+        }
         if (dk_side) {
             U2GNN_TRY(sd.fork());
             U2GNN_TRY(gemm_split(W, D, dS, Q, dQKV + dp, Np, dp, Np, Np, 3 * dp, 3 * dp, true, 1.f, false, nullptr,
                                  nullptr, false, so, false, D.prec_ab, U2GNN_ROLE_DK));
+            U2GNN_TRY(sd.mark(&dv_done));   // dV and dK
+            U2GNN_TRY(in_part(1));
         }
         U2GNN_TRY(gemm_split(W, D, dS, Kt, dQKV, Np, dp, Np, Np, 3 * dp, 3 * dp, false, q_scale, false, nullptr, nullptr,
                              false, st, false, D.prec_ab, U2GNN_ROLE_DQ));
-        if (!dk_side)
+        U2GNN_TRY(sd.fork());
+        U2GNN_TRY(in_part(0));
+        if (!dk_side) {
             U2GNN_TRY(gemm_split(W, D, dS, Q, dQKV + dp, Np, dp, Np, Np, 3 * dp, 3 * dp, true, 1.f, false, nullptr,
                                  nullptr, false, st, false, D.prec_ab, U2GNN_ROLE_DK));
-        if (dv_side) U2GNN_TRY(sd.join());
+            U2GNN_TRY(sd.fork());
+            U2GNN_TRY(in_part(1));
+        }
+        U2GNN_TRY(sd.wait(dv_done));   // dV (and dK) before dX += dQKV W_in
     }
     // in-projection
     if (need_dx)
         U2GNN_TRY(gemm_split(W, D, dQKV, w->W_in, dX, Np, dp, 3 * dp, 3 * dp, dp, dp, false, 1.f, true, nullptr,
                              nullptr, false, st));
-    U2GNN_TRY(sd.fork());
-    U2GNN_TRY(wgrad(W, D, dQKV, 3 * dp, X, dp, 3 * dp, dp, g->in_w, d, blk_d, blk_d, so));
-    U2GNN_TRY(bias_grad(W, dQKV, Np, 3 * dp, 3 * dp, dp, d, g->in_b, so));
+    if (!split_in) {
+        U2GNN_TRY(sd.fork());
+        U2GNN_TRY(wgrad(W, D, dQKV, 3 * dp, X, dp, 3 * dp, dp, g->in_w, d, blk_d, blk_d, so));
+        U2GNN_TRY(bias_grad(W, dQKV, Np, 3 * dp, 3 * dp, dp, d, g->in_b, so));
+    }
     return (W.overflow || CA.overflow) ? U2GNN_E_ARG : U2GNN_OK;
 }
 

@@ -61,6 +61,10 @@ def parse():
     ap.add_argument("--probe", default="ds", choices=["qk", "pv", "ds", "dv", "dq", "dk"],
                     help="attention product timed live (HIP events on its own stream) inside the timed "
                          "region for the roofline object; ds = the step's dominant kernel")
+    ap.add_argument("--graph", type=int, default=-1,
+                    help="1 = replay each training step as one captured HIP graph (u2gnn_hip.train.StepGraphs, "
+                         "one graph per distinct batch, captured before the warmup); default: on for c5 "
+                         "(host-bound), off for c4 (the host runs ahead of the GPU)")
     ap.add_argument("--gemm-family", action="store_true",
                     help="extra untimed pass: every GEMM of the same steps serialised with per-launch events "
                          "(per-template-instance table); off by default so that a rocprofv3 trace of the "
@@ -184,16 +188,26 @@ def main_c5(args):
         b = DeviceBatch.from_offsets(hb.input_x, hb.offsets, hb.X_concat, None, device=dev, input_y=hb.input_y)
         batches.append((b, torch.from_numpy(model.ss.draw_samples()).to(dev)))
     nb = len(batches)
+    graph = args.graph != 0
+    runner = None
+    if graph:   # one captured HIP graph per distinct batch, captured (not run) before the warmup
+        from u2gnn_hip.train import StepGraphs
+        runner = StepGraphs(trainer)
+        for bt in batches:
+            runner.capture(*bt)
+    step = runner.step if runner is not None else trainer.step
     for i in range(args.warmup):
-        trainer.step(*batches[i % nb])
+        step(*batches[i % nb])
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        trainer.step(*batches[(args.warmup + i) % nb])
+        step(*batches[(args.warmup + i) % nb])
     t_issue = time.perf_counter() - t0          # host time to enqueue the K steps
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     loss = float(trainer.loss.item())
+    if runner is not None:
+        runner.close()
     roof = None
     if not args.no_roofline:
         n = trainer.flat.n
@@ -221,7 +235,7 @@ def main_c5(args):
            "config": {"workload": "U2GNN-UnSup REDDIT-M5K (C5): batch_size=4, num_neighbors=16, num_timesteps=4, "
                                   "ff_hidden_size=1024, sampled_num=512, D=4",
                       "global_batch": 4, "mean_nodes_per_batch": round(mean_N, 1), "parallelism": "dp1",
-                      "precision": args.precision},
+                      "precision": args.precision, "hip_graph": graph},
            "final_loss": round(loss, 4), "host_issue_ms_per_step": round(1e3 * t_issue / args.steps, 3),
            "roofline": roof, "cpu_baseline": None}
     emit(out)
@@ -297,8 +311,16 @@ def main():
             trainer.grad_sync = GradAllReduce(bucket_mb=8.0)
 
     nb = len(batches)
+    graph = args.graph == 1 and dist is None
+    runner = None
+    if graph:   # one captured HIP graph per distinct batch, captured (not run) before the warmup
+        from u2gnn_hip.train import StepGraphs
+        runner = StepGraphs(trainer)
+        for bt in batches:
+            runner.capture(bt)
+    step = runner.step if runner is not None else trainer.step
     for i in range(args.warmup):
-        trainer.step(batches[i % nb])
+        step(batches[i % nb])
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -307,19 +329,22 @@ def main():
     from u2gnn_hip import _lib as LIB
     role = {"qk": LIB.ROLE_QK, "pv": LIB.ROLE_PV, "ds": LIB.ROLE_DS, "dv": LIB.ROLE_DV, "dq": LIB.ROLE_DQ,
             "dk": LIB.ROLE_DK}[args.probe]
-    probing = not args.no_roofline and args.attention == "nodes" and native.enabled()
+    # (graph replay: the probe's events would belong to the capture, so no live probe)
+    probing = not args.no_roofline and args.attention == "nodes" and native.enabled() and not graph
     per_step = args.num_hidden_layers * args.num_timesteps
     if probing:   # live: HIP events around every launch of that product, on its stream
         native.probe_arm(role, args.steps * per_step)
     t0 = time.perf_counter()
     for i in range(args.steps):
-        trainer.step(batches[(args.warmup + i) % nb])
+        step(batches[(args.warmup + i) % nb])
     t_issue = time.perf_counter() - t0          # host time to enqueue the K steps
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     probe_ms, probe_n = native.probe_collect() if probing else (0.0, 0)
+    if runner is not None:
+        runner.close()
     loss = float(trainer.loss.item())
     # optional per-GEMM family pass: the same K steps again, serialised, with per-GEMM HIP events
     K.REC.records.clear()
@@ -390,7 +415,8 @@ def main():
            "config": {"workload": "U2GNN-Sup COLLAB (C4): batch_size=64/GPU, num_neighbors=16, num_timesteps=4, "
                                   "ff_hidden_size=1024, num_hidden_layers=1, d=367",
                       "global_batch": args.batch_size * world, "mean_nodes_per_batch": round(mean_N, 1),
-                      "parallelism": f"dp{world}", "precision": args.precision, "attention": args.attention},
+                      "parallelism": f"dp{world}", "precision": args.precision, "attention": args.attention,
+                      "hip_graph": graph},
            "final_loss": round(loss, 5), "host_issue_ms_per_step": round(1e3 * t_issue / args.steps, 3),
            "roofline": roof, "gather": None, "cpu_baseline": None}
     if rank == 0:

@@ -306,8 +306,9 @@ __device__ __forceinline__ float block_sum4(float v, float *red, int lane, int w
 template <int SM_RV>
 __global__ void __launch_bounds__(256) attn_softmax_kernel(const float *S, int64_t lds, float *P, float *Pd,
                                                            int64_t ldp, int64_t rows_valid, int64_t n_valid,
-                                                           int64_t n_pad, float p, uint64_t seed, uint32_t *keep,
+                                                           int64_t n_pad, float p, uint64_t seed, const uint64_t *seed_epoch, uint32_t *keep,
                                                            int64_t ld_keep) {
+    seed = u2gnn_seed(seed, seed_epoch);
     __shared__ float red[4];
     const int64_t row = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -390,7 +391,8 @@ template <int SM_RV>
 __global__ void __launch_bounds__(256) attn_softmax_x2_kernel(const float *S, int64_t lds, __bf16 *Pd2,
                                                               int64_t ldp2, float2 *rowstat, int64_t rows_valid,
                                                               int64_t n_valid, int64_t n_pad, float p,
-                                                              uint64_t seed) {
+                                                              uint64_t seed, const uint64_t *seed_epoch) {
+    seed = u2gnn_seed(seed, seed_epoch);
     __shared__ float red[4];
     const int64_t row = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -538,8 +540,9 @@ __global__ void __launch_bounds__(256) layernorm_fwd_kernel(const float *Z, int6
 __global__ void __launch_bounds__(256) layernorm_bwd_kernel(const float *dY, int64_t ldy, const float *Z, int64_t ldz,
                                                             const float *mean, const float *rstd, const float *gamma,
                                                             float *dZ, int64_t lddz, float *dZd, int64_t lddrop,
-                                                            float p, uint64_t seed, int64_t rows_valid,
+                                                            float p, uint64_t seed, const uint64_t *seed_epoch, int64_t rows_valid,
                                                             int64_t rows_pad, int64_t d, int64_t d_pad) {
+    seed = u2gnn_seed(seed, seed_epoch);
     const int64_t row = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 5);
     const int hl = threadIdx.x & 31;
     if (row >= rows_pad) return;
@@ -685,8 +688,9 @@ __global__ void __launch_bounds__(256) ln_param_reduce_kernel(const float *ws, i
     if (dbias) dbias[c] = t[2];
 }
 
-__global__ void __launch_bounds__(256) dropout_mask_kernel(uint64_t seed, int64_t rows, int64_t cols, float p,
+__global__ void __launch_bounds__(256) dropout_mask_kernel(uint64_t seed, const uint64_t *seed_epoch, int64_t rows, int64_t cols, float p,
                                                            uint8_t *out) {
+    seed = u2gnn_seed(seed, seed_epoch);
     const int64_t total = rows * cols;
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
         const int64_t r = i / cols, c = i - r * cols;
@@ -695,7 +699,8 @@ __global__ void __launch_bounds__(256) dropout_mask_kernel(uint64_t seed, int64_
 }
 
 __global__ void __launch_bounds__(256) dropout_kernel(const float *X, int64_t ldx, float *Y, int64_t ldy, int64_t rows,
-                                                      int64_t cols, float p, uint64_t seed) {
+                                                      int64_t cols, float p, uint64_t seed, const uint64_t *seed_epoch) {
+    seed = u2gnn_seed(seed, seed_epoch);
     const int64_t total = rows * cols;
     const float ks = 1.f / (1.f - p);
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
@@ -819,13 +824,13 @@ int u2gnn_attn_softmax_fwd(const float *S, int64_t lds, float *P, float *Pd, int
     hipStream_t st = u2gnn_stream(stream);
     if (n_pad <= 8192)
         hipLaunchKernelGGL(attn_softmax_kernel<8>, dim3((unsigned)rows_pad), dim3(256), 0, st, S, lds, P, Pd, ldp,
-                           rows_valid, n_valid, n_pad, p, seed, keep, ld_keep);
+                           rows_valid, n_valid, n_pad, p, seed, u2gnn_g_epoch, keep, ld_keep);
     else if (n_pad <= 16384)
         hipLaunchKernelGGL(attn_softmax_kernel<16>, dim3((unsigned)rows_pad), dim3(256), 0, st, S, lds, P, Pd, ldp,
-                           rows_valid, n_valid, n_pad, p, seed, keep, ld_keep);
+                           rows_valid, n_valid, n_pad, p, seed, u2gnn_g_epoch, keep, ld_keep);
     else
         hipLaunchKernelGGL(attn_softmax_kernel<32>, dim3((unsigned)rows_pad), dim3(256), 0, st, S, lds, P, Pd, ldp,
-                           rows_valid, n_valid, n_pad, p, seed, keep, ld_keep);
+                           rows_valid, n_valid, n_pad, p, seed, u2gnn_g_epoch, keep, ld_keep);
     return u2gnn_launch_status();
 }
 
@@ -842,13 +847,13 @@ int u2gnn_attn_softmax_x2_fwd(const float *S, int64_t lds, void *Pd2, int64_t ld
     float2 *rs = reinterpret_cast<float2 *>(rowstat);
     if (n_pad <= 8192)
         hipLaunchKernelGGL(attn_softmax_x2_kernel<8>, dim3((unsigned)rows_pad), dim3(256), 0, st, S, lds, d, ldp2, rs,
-                           rows_valid, n_valid, n_pad, p, seed);
+                           rows_valid, n_valid, n_pad, p, seed, u2gnn_g_epoch);
     else if (n_pad <= 16384)
         hipLaunchKernelGGL(attn_softmax_x2_kernel<16>, dim3((unsigned)rows_pad), dim3(256), 0, st, S, lds, d, ldp2, rs,
-                           rows_valid, n_valid, n_pad, p, seed);
+                           rows_valid, n_valid, n_pad, p, seed, u2gnn_g_epoch);
     else
         hipLaunchKernelGGL(attn_softmax_x2_kernel<32>, dim3((unsigned)rows_pad), dim3(256), 0, st, S, lds, d, ldp2, rs,
-                           rows_valid, n_valid, n_pad, p, seed);
+                           rows_valid, n_valid, n_pad, p, seed, u2gnn_g_epoch);
     return u2gnn_launch_status();
 }
 
@@ -893,7 +898,7 @@ int u2gnn_layernorm_bwd(const float *dY, int64_t ldy, const float *Z, int64_t ld
         (dZdrop && (!al16(dZdrop) || (lddrop & 3))))
         return U2GNN_E_ALIGN;
     hipLaunchKernelGGL(layernorm_bwd_kernel, dim3(grid_for(rows_pad, 8, 1 << 30)), dim3(256), 0, u2gnn_stream(stream),
-                       dY, ldy, Z, ldz, mean, rstd, gamma, dZ, lddz, dZdrop, lddrop, p, seed, rows_valid, rows_pad, d,
+                       dY, ldy, Z, ldz, mean, rstd, gamma, dZ, lddz, dZdrop, lddrop, p, seed, u2gnn_g_epoch, rows_valid, rows_pad, d,
                        d_pad);
     return u2gnn_launch_status();
 }
@@ -924,13 +929,13 @@ int u2gnn_dropout(const float *X, int64_t ldx, float *Y, int64_t ldy, int64_t ro
     if (!X || !Y || p < 0.f || p >= 1.f) return U2GNN_E_ARG;
     if (rows * cols == 0) return U2GNN_OK;
     hipLaunchKernelGGL(dropout_kernel, dim3(grid_for(rows * cols, 256)), dim3(256), 0, u2gnn_stream(stream), X, ldx, Y,
-                       ldy, rows, cols, p, seed);
+                       ldy, rows, cols, p, seed, u2gnn_g_epoch);
     return u2gnn_launch_status();
 }
 
 int u2gnn_dropout_mask(uint64_t seed, int64_t rows, int64_t cols, float p, uint8_t *out, void *stream) {
     if (!out) return U2GNN_E_ARG;
-    hipLaunchKernelGGL(dropout_mask_kernel, dim3(grid_for(rows * cols, 256)), dim3(256), 0, u2gnn_stream(stream), seed,
+    hipLaunchKernelGGL(dropout_mask_kernel, dim3(grid_for(rows * cols, 256)), dim3(256), 0, u2gnn_stream(stream), seed, u2gnn_g_epoch,
                        rows, cols, p, out);
     return u2gnn_launch_status();
 }

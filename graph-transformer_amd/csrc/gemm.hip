@@ -101,6 +101,8 @@ __device__ __forceinline__ void r2s(float *As, float *Bs, int tid, const float4 
 // ------------------------------------------------------------------------------------
 template <int BM, int BN, bool TA, bool TB, int EPI, bool CLAMP>
 __global__ void __launch_bounds__(256) gemm_f32_kernel(GemmP P) {
+    if constexpr (EPI == U2GNN_EPI_BIAS_DROP_RESID || EPI == U2GNN_EPI_BIAS_RELU_DROP || EPI == U2GNN_EPI_ATTN_DS_RECOMP)
+        P.seed = u2gnn_seed(P.seed, P.epoch);   // graph replay: device-resident seed epoch
     constexpr int BK = 16;
     constexpr int WTM = BM / 2, WTN = BN / 2;
     constexpr int TM = WTM / 32, TN = WTN / 32;
@@ -317,6 +319,8 @@ __device__ __forceinline__ bf16x8 ld_frag(const __bf16 *img, int r0, int ks, int
 
 template <int BM, int BN, int WM, int WN, int BK, bool TA, bool TB, int EPI, bool SPLIT, bool CLAMP>
 __global__ void __launch_bounds__(64 * WM * WN) gemm_bf16_kernel(GemmP P) {
+    if constexpr (EPI == U2GNN_EPI_BIAS_DROP_RESID || EPI == U2GNN_EPI_BIAS_RELU_DROP || EPI == U2GNN_EPI_ATTN_DS_RECOMP)
+        P.seed = u2gnn_seed(P.seed, P.epoch);   // graph replay: device-resident seed epoch
     constexpr int NT = 64 * WM * WN;
     constexpr int LDK = BK + 8;
     constexpr int WTM = BM / WM, WTN = BN / WN;
@@ -594,6 +598,7 @@ extern "C" int u2gnn_gemm(const u2gnn_gemm_args *a, void *stream) {
     P.scale_cols = (int32_t)a->scale_cols;
     P.p = a->p_drop;
     P.seed = a->seed;
+    P.epoch = u2gnn_g_epoch;
     P.keep = e == U2GNN_EPI_ATTN_DS ? a->keep : nullptr;
     P.ld_keep = a->ld_keep;
     P.A2 = static_cast<const __bf16 *>(a->A2);

@@ -31,6 +31,7 @@ struct GemmP {
     int64_t ldcx2;        // bf16 elements
     const float2 *rowstat;   // ATTN_DS_RECOMP: (row max, 1/row sum) of the forward softmax
     int32_t m_valid, n_valid;   // ATTN_DS_RECOMP: real rows / keys (P = 0 beyond)
+    const uint64_t *epoch;      // seed epoch at launch (u2gnn_set_seed_epoch): seed ^= *epoch * golden
 };
 
 namespace {

@@ -112,6 +112,8 @@ __device__ __forceinline__ void wait_vm() {
 
 template <int BM, int BN, int WM, int WN, int BK, int NS, int MINB, bool PP, bool TA, bool TB, int EPI>
 __global__ void __launch_bounds__(64 * WM * WN, MINB) gemm_x2_kernel(GemmP P) {
+    if constexpr (EPI == U2GNN_EPI_BIAS_DROP_RESID || EPI == U2GNN_EPI_BIAS_RELU_DROP || EPI == U2GNN_EPI_ATTN_DS_RECOMP)
+        P.seed = u2gnn_seed(P.seed, P.epoch);   // graph replay: device-resident seed epoch
     constexpr int NT = 64 * WM * WN;
     constexpr int WTM = BM / WM, WTN = BN / WN;        // wave tile
     constexpr int TM = WTM / 32, TN = WTN / 32;

@@ -97,6 +97,8 @@ __device__ __forceinline__ void x3_tile(int L, int gm, int gn, int &tm, int &tn)
 
 template <int EPI>
 __global__ void __launch_bounds__(X3_NT) gemm_x3_nt_kernel(GemmP P) {
+    if constexpr (EPI == U2GNN_EPI_BIAS_DROP_RESID || EPI == U2GNN_EPI_BIAS_RELU_DROP || EPI == U2GNN_EPI_ATTN_DS_RECOMP)
+        P.seed = u2gnn_seed(P.seed, P.epoch);   // graph replay: device-resident seed epoch
     constexpr int WN = 2, WTM = 64, WTN = 64, MB = 4, NB = 4;
     constexpr int NSTORE = MB * NB;   // float4 stores per thread per output tile
     __shared__ __attribute__((aligned(1024))) char smem[X3_NS * X3_STAGE];

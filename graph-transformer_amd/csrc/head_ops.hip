@@ -3,6 +3,9 @@
 // sampled-softmax loss of the unsupervised model.
 #include "u2gnn_common.h"
 
+// process-wide seed epoch (u2gnn_set_seed_epoch), passed to every dropout-drawing launch
+const uint64_t *u2gnn_g_epoch = nullptr;
+
 namespace {
 
 // ------------------------------------------------------------------------------------------
@@ -11,7 +14,8 @@ namespace {
 // ------------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) pool_fwd_kernel(const float *X, int64_t ldx, const int64_t *rowptr,
                                                        const int64_t *colidx, const float *vals, float *G, int64_t ldg,
-                                                       int64_t d, float p, uint64_t seed) {
+                                                       int64_t d, float p, uint64_t seed, const uint64_t *seed_epoch) {
+    seed = u2gnn_seed(seed, seed_epoch);
     // block = (graph, 64-column chunk); the 4 waves split the graph's rows
     __shared__ float red[4][64];
     const int64_t b = blockIdx.x;
@@ -40,7 +44,8 @@ __global__ void __launch_bounds__(256) pool_fwd_kernel(const float *X, int64_t l
 
 __global__ void __launch_bounds__(256) pool_bwd_kernel(const float *dGd, int64_t ldg, const int64_t *rowptr,
                                                        const int64_t *colidx, const float *vals, float *dX,
-                                                       int64_t ldx, int64_t d, float p, uint64_t seed) {
+                                                       int64_t ldx, int64_t d, float p, uint64_t seed, const uint64_t *seed_epoch) {
+    seed = u2gnn_seed(seed, seed_epoch);
     // block = (graph, row slice, 64-column chunk); one atomic per (row, column)
     const int64_t b = blockIdx.x;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -177,6 +182,38 @@ __global__ void __launch_bounds__(256) adam_kernel(float *param, const float *gr
         const float denom = sqrtf(vi) / bc2_sqrt + eps;
         param[i] = param[i] - step_size * (mi / denom);
     }
+}
+
+// Graph-replay form: the bias corrections from the device-resident step count t and lr (u2gnn_adam_dev),
+// formed in double like the host path (torch: lr / (1 - b1^t), sqrt(1 - b2^t)).
+__global__ void __launch_bounds__(256) adam_dev_kernel(float *param, const float *grad, float *m, float *v, int64_t n,
+                                                       const float *sqnorm, float max_norm, double b1, double b2,
+                                                       float eps, const double *lr, const int64_t *t) {
+    const double tt = (double)t[0];
+    const float step_size = (float)(lr[0] / (1.0 - pow(b1, tt)));
+    const float bc2_sqrt = (float)sqrt(1.0 - pow(b2, tt));
+    float coef = 1.f;
+    if (sqnorm) {
+        const float total = sqrtf(sqnorm[0]);
+        coef = fminf(1.f, max_norm / (total + 1e-6f));
+    }
+    const float fb1 = (float)b1, fb2 = (float)b2;
+    const float w1 = 1.f - fb1, w2 = 1.f - fb2;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        const float g = grad[i] * coef;
+        float mi = m[i];
+        mi = mi + w1 * (g - mi);
+        float vi = v[i] * fb2 + w2 * g * g;
+        m[i] = mi;
+        v[i] = vi;
+        const float denom = sqrtf(vi) / bc2_sqrt + eps;
+        param[i] = param[i] - step_size * (mi / denom);
+    }
+}
+
+__global__ void step_advance_kernel(uint64_t *epoch, int64_t *t) {
+    if (epoch) *epoch += 1;
+    if (t) *t += 1;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -323,7 +360,7 @@ int u2gnn_pool_fwd(const float *X, int64_t ldx, const int64_t *rowptr, const int
                    float *G, int64_t ldg, int64_t B, int64_t d, float p, uint64_t seed, void *stream) {
     if (!X || !rowptr || !colidx || !vals || !G || B < 1 || d < 1) return U2GNN_E_ARG;
     hipLaunchKernelGGL(pool_fwd_kernel, dim3((unsigned)B, (unsigned)((d + 63) / 64)), dim3(256), 0,
-                       u2gnn_stream(stream), X, ldx, rowptr, colidx, vals, G, ldg, d, p, seed);
+                       u2gnn_stream(stream), X, ldx, rowptr, colidx, vals, G, ldg, d, p, seed, u2gnn_g_epoch);
     return u2gnn_launch_status();
 }
 
@@ -331,7 +368,7 @@ int u2gnn_pool_bwd(const float *dGd, int64_t ldg, const int64_t *rowptr, const i
                    float *dX, int64_t ldx, int64_t B, int64_t d, float p, uint64_t seed, void *stream) {
     if (!dGd || !rowptr || !colidx || !vals || !dX || B < 1 || d < 1) return U2GNN_E_ARG;
     hipLaunchKernelGGL(pool_bwd_kernel, dim3((unsigned)B, 8, (unsigned)((d + 63) / 64)), dim3(256), 0,
-                       u2gnn_stream(stream), dGd, ldg, rowptr, colidx, vals, dX, ldx, d, p, seed);
+                       u2gnn_stream(stream), dGd, ldg, rowptr, colidx, vals, dX, ldx, d, p, seed, u2gnn_g_epoch);
     return u2gnn_launch_status();
 }
 
@@ -376,6 +413,27 @@ int u2gnn_adam(float *param, const float *grad, float *exp_avg, float *exp_avg_s
     hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n, 256, 4096)), dim3(256), 0, u2gnn_stream(stream), param, grad,
                        exp_avg, exp_avg_sq, n, sqnorm, max_norm, beta1, beta2, eps, step_size, bc2_sqrt);
     return u2gnn_launch_status();
+}
+
+int u2gnn_adam_dev(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, int64_t n, const float *sqnorm,
+                   float max_norm, double beta1, double beta2, float eps, const double *lr, const int64_t *step,
+                   void *stream) {
+    if (!param || !grad || !exp_avg || !exp_avg_sq || !lr || !step) return U2GNN_E_ARG;
+    if (n == 0) return U2GNN_OK;
+    hipLaunchKernelGGL(adam_dev_kernel, dim3(grid_for(n, 256, 4096)), dim3(256), 0, u2gnn_stream(stream), param, grad,
+                       exp_avg, exp_avg_sq, n, sqnorm, max_norm, beta1, beta2, eps, lr, step);
+    return u2gnn_launch_status();
+}
+
+int u2gnn_step_advance(uint64_t *epoch, int64_t *step, void *stream) {
+    if (!epoch && !step) return U2GNN_OK;
+    hipLaunchKernelGGL(step_advance_kernel, dim3(1), dim3(1), 0, u2gnn_stream(stream), epoch, step);
+    return u2gnn_launch_status();
+}
+
+int u2gnn_set_seed_epoch(const uint64_t *epoch) {
+    u2gnn_g_epoch = epoch;
+    return U2GNN_OK;
 }
 
 int u2gnn_sampled_softmax_fwd(const float *X, int64_t ldx, const int64_t *labels, const int64_t *sample_ids, int64_t S,

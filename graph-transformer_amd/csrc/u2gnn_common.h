@@ -33,6 +33,15 @@ __device__ __forceinline__ uint32_t u2gnn_row_key(uint64_t seed, uint32_t i) {
     return u2gnn_fmix32((uint32_t)seed ^ u2gnn_fmix32((uint32_t)(seed >> 32) ^ u2gnn_fmix32(i + 0x9E3779B9u)));
 }
 
+// Graph replay (ABI v6): every kernel that draws dropout decisions receives, beside its by-value
+// seed, the library's seed-epoch pointer as it was at launch (u2gnn_set_seed_epoch; NULL = off) and
+// mixes the device-resident epoch into the seed, so a captured HIP graph draws new masks on every
+// replay (u2gnn_step_advance bumps the epoch inside the graph).  Epoch 0 leaves the seed unchanged.
+extern const uint64_t *u2gnn_g_epoch;
+__device__ __forceinline__ uint64_t u2gnn_seed(uint64_t seed, const uint64_t *epoch) {
+    return epoch ? seed ^ (*epoch * 0x9E3779B97F4A7C15ull) : seed;
+}
+
 __device__ __forceinline__ bool u2gnn_keep(uint64_t seed, uint32_t i, uint32_t j, float p) {
     const uint32_t u = u2gnn_fmix32(u2gnn_row_key(seed, i) + j * 0x9E3779B9u) >> 8;   // 24 bits
     return (float)u * (1.0f / 16777216.0f) >= p;

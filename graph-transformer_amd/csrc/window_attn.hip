@@ -123,7 +123,8 @@ __device__ __forceinline__ void win_combine(const float *C, const float *M, int 
 // leaves idle): 54 KB of LDS at W = 17, dp = 384, i.e. 3 blocks per CU.
 __global__ void __launch_bounds__(256) window_attn_fwd_kernel(const float *QKV, int64_t ldq, int W, int dp,
                                                               float *O, int64_t ldo, float *Psave, float p,
-                                                              uint64_t seed, int64_t n_nodes, int64_t rows_pad) {
+                                                              uint64_t seed, const uint64_t *seed_epoch, int64_t n_nodes, int64_t rows_pad) {
+    seed = u2gnn_seed(seed, seed_epoch);
     if (zero_pad_rows(n_nodes, W, rows_pad, dp, O, ldo)) return;
     extern __shared__ float sm[];
     const int LD = win_ld(dp);
@@ -167,8 +168,9 @@ __global__ void __launch_bounds__(256) window_attn_fwd_kernel(const float *QKV, 
 // dO for dK.  55 KB of LDS at W = 17, dp = 384: 2 blocks per CU.
 __global__ void __launch_bounds__(256) window_attn_bwd_kernel(const float *QKV, int64_t ldq, int W, int dp,
                                                               const float *dO, int64_t ldo, const float *Psave,
-                                                              float p, uint64_t seed, float q_scale, float *dQKV,
+                                                              float p, uint64_t seed, const uint64_t *seed_epoch, float q_scale, float *dQKV,
                                                               int64_t ldg, int64_t n_nodes, int64_t rows_pad) {
+    seed = u2gnn_seed(seed, seed_epoch);
     if (zero_pad_rows(n_nodes, W, rows_pad, 3 * dp, dQKV, ldg)) return;
     extern __shared__ float sm[];
     const int LD = win_ld(dp);
@@ -233,7 +235,7 @@ int u2gnn_window_attn_fwd(const float *QKV, int64_t ldq, int32_t W, int32_t dp, 
     }
     const int64_t pad_blocks = (rows_pad - n_nodes * W + W - 1) / W;
     hipLaunchKernelGGL(window_attn_fwd_kernel, dim3((unsigned)(n_nodes + pad_blocks)), dim3(256), lds,
-                       u2gnn_stream(stream), QKV, ldq, W, dp, O, ldo, Psave, p, seed, n_nodes, rows_pad);
+                       u2gnn_stream(stream), QKV, ldq, W, dp, O, ldo, Psave, p, seed, u2gnn_g_epoch, n_nodes, rows_pad);
     return u2gnn_launch_status();
 }
 
@@ -256,7 +258,7 @@ int u2gnn_window_attn_bwd(const float *QKV, int64_t ldq, int32_t W, int32_t dp, 
     }
     const int64_t pad_blocks = (rows_pad - n_nodes * W + W - 1) / W;
     hipLaunchKernelGGL(window_attn_bwd_kernel, dim3((unsigned)(n_nodes + pad_blocks)), dim3(256), lds,
-                       u2gnn_stream(stream), QKV, ldq, W, dp, dO, ldo, Psave, p, seed, q_scale, dQKV, ldg, n_nodes,
+                       u2gnn_stream(stream), QKV, ldq, W, dp, dO, ldo, Psave, p, seed, u2gnn_g_epoch, q_scale, dQKV, ldg, n_nodes,
                        rows_pad);
     return u2gnn_launch_status();
 }

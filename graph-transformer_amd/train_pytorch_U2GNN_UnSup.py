@@ -137,7 +137,7 @@ for epoch in range(1, args.num_epochs + 1):
         epoch, (time.time() - epoch_start_time), train_loss, mean_10folds * 100, std_10folds * 100))
     if epoch > 5 and cost_loss[-1] > np.mean(cost_loss[-6:-1]):
         sched_steps += 1
-        trainer.opt.lr = args.learning_rate * 0.1 ** (sched_steps // num_batches_per_epoch)
+        trainer.opt.set_lr(args.learning_rate * 0.1 ** (sched_steps // num_batches_per_epoch))
     write_acc.write('epoch ' + str(epoch) + ' mean: ' + str(mean_10folds * 100) + ' std: ' + str(std_10folds * 100) + '\n')
     if args.max_steps and steps_done >= args.max_steps:
         break

@@ -9,7 +9,7 @@ from __future__ import annotations
 import ctypes
 import os
 import re
-from ctypes import POINTER, c_float, c_int32, c_int64, c_size_t, c_uint8, c_uint32, c_uint64, c_void_p
+from ctypes import POINTER, c_double, c_float, c_int32, c_int64, c_size_t, c_uint8, c_uint32, c_uint64, c_void_p
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REPO_ROOT = os.path.dirname(PKG_ROOT)
@@ -30,7 +30,7 @@ ERRORS = {-1: "bad argument", -2: "misaligned pointer / leading dimension", -3: 
 
 EPI_STORE, EPI_BIAS, EPI_BIAS_DROP_RESID, EPI_BIAS_RELU_DROP, EPI_RELU_DROP_BWD, EPI_ACCUM, EPI_ATTN_DS, \
     EPI_ATTN_DS_SIGNED, EPI_ATTN_DS_RECOMP = range(9)
-ABI_VERSION = 5   # include/u2gnn_hip.h U2GNN_ABI_VERSION
+ABI_VERSION = 6   # include/u2gnn_hip.h U2GNN_ABI_VERSION
 PREC_F32, PREC_BF16X3, PREC_BF16 = 0, 1, 2
 
 
@@ -130,6 +130,9 @@ _HIP_SIGS = {
     "u2gnn_dropout": ([VP, I64, VP, I64, I64, I64, F32, c_uint64, VP], c_int32),
     "u2gnn_probe_arm": ([I32, I32], c_int32),
     "u2gnn_probe_collect": ([POINTER(c_float), POINTER(c_int32)], c_int32),
+    "u2gnn_set_seed_epoch": ([VP], c_int32),
+    "u2gnn_step_advance": ([VP, VP, VP], c_int32),
+    "u2gnn_adam_dev": ([VP, VP, VP, VP, I64, VP, F32, c_double, c_double, F32, VP, VP, VP], c_int32),
 }
 
 _LUS_SIGS = {

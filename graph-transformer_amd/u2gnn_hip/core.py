@@ -20,7 +20,7 @@ from . import kernels as K
 from . import native
 from .engine import deep_wgrad as engine_deep_wgrad
 from .engine import (SITE_ATTN, SITE_DROP1, SITE_DROP2, SITE_DROPFF, SITE_HEAD, Dims, LayerParams, PackedLayer,
-                     OffPath, encoder_layer_backward, encoder_layer_forward, rup, site_seed)
+                     OffPath, encoder_layer_backward, encoder_layer_forward, rup, side_stream_pays, site_seed)
 
 
 _IOTA = {}
@@ -234,7 +234,7 @@ class EncoderStack:
         tdims, W, slot0 = ctx["tdims"], ctx["window"], ctx["slot0"]
         d, dp = self.d, rup(self.d, 64)
         R = b.N * W
-        off = OffPath(b.input_x.device)
+        off = OffPath(b.input_x.device, enabled=side_stream_pays(tdims))
         dnext = None
         for l in reversed(range(self.L)):
             dOut = ext_grad(l)                                   # [Np, dp] node rows
@@ -263,7 +263,7 @@ class EncoderStack:
         b = ctx["batch"]
         dims = ctx["dims"]
         dnext = None
-        off = OffPath(b.input_x.device)
+        off = OffPath(b.input_x.device, enabled=side_stream_pays(dims))
         for l in reversed(range(self.L)):
             dX = ext_grad(l)
             if dnext is not None:
@@ -383,14 +383,39 @@ class FusedAdam:
         self.ws = torch.empty(1024, device=dev, dtype=torch.float32)
         self.sq = torch.zeros(1, device=dev, dtype=torch.float32)
         self.step_count = 0
+        # device-resident schedule (HIP-graph replay, train.StepGraphs): step count t and lr live in
+        # HBM, u2gnn_step_advance bumps t inside the captured step, u2gnn_adam_dev forms the bias
+        # corrections on the device
+        self.t_dev: Optional[torch.Tensor] = None
+        self.lr_dev: Optional[torch.Tensor] = None
+
+    def use_device_schedule(self) -> None:
+        dev = self.f.flat.device
+        self.t_dev = torch.full((1,), self.step_count, device=dev, dtype=torch.int64)
+        self.lr_dev = torch.full((1,), float(self.lr), device=dev, dtype=torch.float64)
+
+    def use_host_schedule(self) -> None:
+        if self.t_dev is not None:
+            self.step_count = int(self.t_dev.item())
+        self.t_dev = self.lr_dev = None
+
+    def set_lr(self, lr: float) -> None:
+        self.lr = lr
+        if self.lr_dev is not None:
+            self.lr_dev.fill_(float(lr))
 
     def step(self):
-        self.step_count += 1
         b1, b2 = self.betas
-        bc1 = 1 - b1 ** self.step_count
-        bc2 = 1 - b2 ** self.step_count
         if self.max_norm is not None:
             K.sqnorm(self.f.gflat, self.f.n, self.ws, self.sq)
+        if self.t_dev is not None:   # t advanced by the caller's u2gnn_step_advance
+            K.adam_dev(self.f.flat, self.f.gflat, self.m, self.v, self.f.n,
+                       self.sq if self.max_norm is not None else None, self.max_norm or 0.0, b1, b2, self.eps,
+                       self.lr_dev, self.t_dev)
+            return
+        self.step_count += 1
+        bc1 = 1 - b1 ** self.step_count
+        bc2 = 1 - b2 ** self.step_count
         K.adam(self.f.flat, self.f.gflat, self.m, self.v, self.f.n, self.sq if self.max_norm is not None else None,
                self.max_norm or 0.0, b1, b2, self.eps, self.lr / bc1, math.sqrt(bc2))
 

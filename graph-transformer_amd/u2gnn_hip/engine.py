@@ -175,13 +175,25 @@ def side_stream(dev: torch.device) -> "torch.cuda.Stream":
     return s
 
 
+# The side stream pays only when the layer's kernels fill the chip: at C4 (Np*dp = 1.9M) it saves
+# 0.31 ms of a 3.27 ms step; at C5 (U2GNN-UnSup REDDIT, d = 4: Np*dp = 0.13M, ~2-10 us kernels) the
+# cross-stream hand-offs cost more than the overlap gains (1.116 vs 1.19-1.28 ms/step, one session,
+# profiles/r02/r2i_graph_knobs.txt).  U2GNN_SIDE_MIN_ELEMS overrides the threshold.
+SIDE_MIN_ELEMS = int(os.environ.get("U2GNN_SIDE_MIN_ELEMS", str(1 << 20)))
+
+
+def side_stream_pays(dims: "Dims") -> bool:
+    return dims.Np * dims.dp >= SIDE_MIN_ELEMS
+
+
 class OffPath:
     """Enqueue closures on the side stream after everything already issued on the current
     stream; tensors they read are record_stream'ed so the caching allocator cannot recycle
-    them early.  join() makes the current stream wait for all of it."""
+    them early.  join() makes the current stream wait for all of it.  enabled=False (or
+    U2GNN_OVERLAP=0): everything runs on the current stream."""
 
-    def __init__(self, dev: torch.device):
-        self.side = side_stream(dev) if _OVERLAP[0] and dev.type == "cuda" else None
+    def __init__(self, dev: torch.device, enabled: bool = True):
+        self.side = side_stream(dev) if enabled and _OVERLAP[0] and dev.type == "cuda" else None
 
     def run(self, fn, *uses: torch.Tensor):
         if self.side is None:

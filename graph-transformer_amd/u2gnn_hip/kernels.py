@@ -319,3 +319,29 @@ def dropout_mask(seed, rows, cols, p, device="cuda"):
     check(hip_lib().u2gnn_dropout_mask(int(seed), int(rows), int(cols), float(p), _p(out), _s()),
           "u2gnn_dropout_mask")
     return out
+
+
+# ---- ABI v6: device-resident step state for HIP-graph replay (u2gnn_hip.h) ----
+def set_seed_epoch(epoch):
+    """Every dropout-drawing launch from now on mixes the device uint64 ``epoch[0]`` into its seed
+    (None switches it off).  Process-wide."""
+    if epoch is not None:
+        _dev(epoch)
+        if epoch.dtype != torch.int64 or epoch.numel() < 1:
+            raise _lib.U2GNNNativeError("seed epoch: one int64 device element")
+    check(hip_lib().u2gnn_set_seed_epoch(_p(epoch) if epoch is not None else None), "u2gnn_set_seed_epoch")
+
+
+def step_advance(epoch, step):
+    """epoch[0] += 1 and step[0] += 1 on the current stream (either may be None)."""
+    check(hip_lib().u2gnn_step_advance(_p(epoch) if epoch is not None else None,
+                                       _p(step) if step is not None else None, _s()), "u2gnn_step_advance")
+
+
+def adam_dev(param, grad, m, v, n, sqnorm, max_norm, b1, b2, eps, lr_dev, step_dev):
+    """u2gnn_adam with the bias corrections formed on the device from lr_dev (float64[1]) and
+    step_dev (int64[1])."""
+    _dev(param, grad, m, v, lr_dev, step_dev)
+    check(hip_lib().u2gnn_adam_dev(_p(param), _p(grad), _p(m), _p(v), int(n), _p(sqnorm) if sqnorm is not None else None,
+                                   float(max_norm), float(b1), float(b2), float(eps), _p(lr_dev), _p(step_dev), _s()),
+          "u2gnn_adam_dev")

@@ -43,4 +43,49 @@ class SupTrainer:
         return loss
 
     def set_lr(self, lr: float):
-        self.opt.lr = lr
+        self.opt.set_lr(lr)
+
+
+class StepGraphs:
+    """HIP-graph replay of a trainer's step (SupTrainer.step(b) / UnSupTrainer.step(b, sample_ids)).
+
+    The first step with a given set of argument objects is captured into a torch.cuda.CUDAGraph
+    (the capture stream plus the parameter-gradient side stream, joined through events) and every
+    step with them afterwards is ONE graph launch instead of ~180 host-issued kernels — the
+    latency-bound d = 4 UnSup step (C5) is host-bound otherwise.  One graph per distinct batch
+    (shapes differ); each keeps its own private memory pool.  What changes from step to step lives
+    in HBM and is advanced by the graph's first node (u2gnn_step_advance): the seed epoch that every
+    dropout-drawing kernel mixes into its capture-time seed (u2gnn_set_seed_epoch) and Adam's step
+    count (FusedAdam.use_device_schedule), so replays draw fresh masks and follow torch's Adam
+    schedule exactly as the eager step does."""
+
+    def __init__(self, trainer):
+        self.tr = trainer
+        dev = trainer.flat.flat.device
+        self.epoch = torch.zeros(1, device=dev, dtype=torch.int64)
+        K.set_seed_epoch(self.epoch)
+        trainer.opt.use_device_schedule()
+        self.graphs = {}
+
+    def capture(self, *args) -> "torch.cuda.CUDAGraph":
+        key = tuple(id(a) for a in args)
+        g = self.graphs.get(key)
+        if g is None:
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                K.step_advance(self.epoch, self.tr.opt.t_dev)
+                self.tr.step(*args)
+            self.graphs[key] = g
+        return g
+
+    def step(self, *args) -> torch.Tensor:
+        self.capture(*args).replay()
+        return self.tr.loss
+
+    def close(self) -> None:
+        """Back to eager steps: the epoch pointer is released, Adam's step count returns to the host."""
+        torch.cuda.synchronize()
+        K.set_seed_epoch(None)
+        self.tr.opt.use_host_schedule()
+        self.graphs.clear()

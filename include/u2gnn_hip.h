@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define U2GNN_ABI_VERSION 5
+#define U2GNN_ABI_VERSION 6
 
 #define U2GNN_OK 0
 #define U2GNN_E_ARG (-1)    /* bad size / null pointer */
@@ -336,6 +336,23 @@ int u2gnn_layer_bwd(const u2gnn_layer_dims *dims, const u2gnn_layer_params *w,
 #define U2GNN_ROLE_DK 6
 int u2gnn_probe_arm(int32_t role, int32_t capacity);
 int u2gnn_probe_collect(float *total_ms, int32_t *launches);
+
+/* ---- ABI v6: device-resident step state (HIP-graph replay of a training step) ----
+ * A captured step replays every launch with its capture-time arguments; the two things that must
+ * change from step to step live in device memory instead:
+ *  - dropout masks: after u2gnn_set_seed_epoch(epoch) every dropout-drawing kernel launched (gemm
+ *    dropout epilogues, softmax, LayerNorm backward, pooling, dropout, window attention) mixes the
+ *    device uint64 *epoch into its by-value seed: seed ^ *epoch * 0x9E3779B97F4A7C15 (epoch 0 =
+ *    the plain seed).  Process-wide, read at launch time; NULL switches it off.
+ *  - Adam's bias corrections: u2gnn_adam_dev is u2gnn_adam with step_size = lr / (1 - beta1^t) and
+ *    bc2_sqrt = sqrt(1 - beta2^t) formed on the device from the double *lr and the int64 step *t.
+ *  u2gnn_step_advance(epoch, t) adds 1 to each non-NULL counter (one single-thread kernel): the first
+ *  launch of a captured step. */
+int u2gnn_set_seed_epoch(const uint64_t *epoch);
+int u2gnn_step_advance(uint64_t *epoch, int64_t *step, void *stream);
+int u2gnn_adam_dev(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, int64_t n,
+                   const float *sqnorm, float max_norm, double beta1, double beta2, float eps,
+                   const double *lr, const int64_t *step, void *stream);
 
 #ifdef __cplusplus
 }

@@ -47,7 +47,7 @@ def _worker(rank, world, port, out_dir):
     from u2gnn_hip.train import SupTrainer
 
     np.random.seed(123)
-    host = rank_batches(BatchLoader(collab_like(seed=0), 32, 16), world, rank, 1)
+    host = rank_batches(BatchLoader(collab_like(seed=0), 64, 16), world, rank, 1)   # C4 size: side stream on
     b = DeviceBatch.from_offsets(host[0].input_x, host[0].offsets, host[0].X_concat, host[0].labels, device=dev)
     out = {}
     for mode in ("overlap", "after"):

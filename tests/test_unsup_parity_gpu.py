@@ -73,3 +73,25 @@ def test_unsup_fused_trainer_step(golden_dir):
     for n, p in m.named_parameters():
         if "after." + n in z:
             assert close(p.detach(), z["after." + n]), n
+
+
+def test_graph_embeddings_match_spmm_over_all_graphs():
+    """evaluate() of train_pytorch_U2GNN_UnSup.py:167-169: spmm(graph_pool, ss.weight) with graph_pool
+    built over ALL graphs (train_pytorch_U2GNN_UnSup.py:92-94) -- the per-graph sums of the learned
+    node embeddings, here against a float64 torch.sparse reference on the PTC node layout."""
+    import util
+    from u2gnn_hip.batching import GraphStore
+    from u2gnn_hip.unsup import graph_embeddings
+    graphs, _ = util.load_data("PTC", False)
+    store = GraphStore(graphs)
+    V = int(store.node_start[-1])
+    g = torch.Generator(device="cuda").manual_seed(11)
+    for D in (19, 4, 64):
+        W = torch.randn(V, D, device="cuda", generator=g)
+        emb = graph_embeddings(W, store.node_start)
+        rows = np.repeat(np.arange(len(graphs)), np.diff(store.node_start))
+        pool = torch.sparse_coo_tensor(torch.tensor(np.stack([rows, np.arange(V)])), torch.ones(V, dtype=torch.float64),
+                                       (len(graphs), V))
+        ref = torch.sparse.mm(pool, W.double().cpu())
+        assert emb.shape == (len(graphs), D)
+        assert ((emb.double().cpu() - ref).abs().max() / ref.abs().max()).item() < 1e-6

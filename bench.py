@@ -71,8 +71,10 @@ def parse():
                          "default command holds only the timed region's launches")
     ap.add_argument("--attention", default="nodes", choices=["nodes", "neighbors"],
                     help="nodes = the fork's semantics (the headline metric); neighbors = paper semantics")
-    ap.add_argument("--workload", default="c4", choices=["c4", "c5"],
-                    help="c4 = U2GNN-Sup COLLAB (the headline metric); c5 = U2GNN-UnSup REDDIT-M5K (HBM-bound)")
+    ap.add_argument("--workload", default="c4", choices=["c4", "c5", "c2", "c3"],
+                    help="c4 = U2GNN-Sup COLLAB (the headline metric); c5 = U2GNN-UnSup REDDIT-M5K (HBM-bound); "
+                         "c2 = U2GNN-Sup IMDBBINARY, c3 = U2GNN-UnSup PTC (BASELINE configs[1], [2]: real data, "
+                         "latency-bound steps, replayed as HIP graphs)")
     return ap.parse_args()
 
 
@@ -241,6 +243,119 @@ def main_c5(args):
     emit(out)
 
 
+METRIC_SMALL = {"c2": "graphs/sec (fwd+bwd) U2GNN-Sup IMDBBINARY k=8 T=4 MI355X",
+                "c3": "graphs/sec (fwd+bwd) U2GNN-UnSup PTC k=4 T=2 S=512 MI355X"}
+
+
+def main_small(args):
+    """BASELINE.json configs[1] (IMDBBINARY supervised, bs 4, k 8, T 4, ff 1024) and configs[2] (PTC
+    unsupervised + SampledSoftmax 512, bs 4, k 4, T 2, ff 1024) on the real datasets of the image:
+    N ~ 80-100 nodes per batch, so a step is latency-bound; it is replayed as one HIP graph per
+    distinct batch (the side stream is off for layers this small).  cpu_baseline: the oracle (all
+    k+1 slots, dropout on) on the same batches, host cores."""
+    import util
+    from oracle import u2gnn_oracle as O
+    from u2gnn_hip.batching import BatchLoader, GraphStore
+    from u2gnn_hip.core import DeviceBatch
+    from u2gnn_hip.train import StepGraphs, SupTrainer
+    if int(os.environ.get("WORLD_SIZE", "1")) != 1:
+        raise SystemExit("--workload c2/c3 runs on one GPU")
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    sup = args.workload == "c2"
+    name, k, T = ("IMDBBINARY", 8, 4) if sup else ("PTC", 4, 2)
+    graphs, C = util.load_data(name, sup)
+    np.random.seed(123)
+    torch.manual_seed(123)
+    store = GraphStore(graphs)
+    d = store.X.shape[1]
+    loader = BatchLoader(store, 4, k, with_input_y=not sup)
+    host = [loader() for _ in range(args.distinct_batches)]
+    if sup:
+        from pytorch_U2GNN_Sup import TransformerU2GNN
+        model = TransformerU2GNN(d, args.ff_hidden_size, C, T, 0.5, 1, precision=args.precision)
+        sd0 = {kk: v.clone() for kk, v in model.state_dict().items()}
+        model = model.to(dev).train()
+        trainer = SupTrainer(model, lr=args.lr, max_norm=0.5)
+        batches = [(DeviceBatch.from_offsets(h.input_x, h.offsets, h.X_concat, h.labels, device=dev),) for h in host]
+    else:
+        from pytorch_U2GNN_UnSup import TransformerU2GNN
+        from u2gnn_hip.unsup import UnSupTrainer
+        V = int(store.node_start[-1])
+        model = TransformerU2GNN(feature_dim_size=d, ff_hidden_size=args.ff_hidden_size, dropout=0.5,
+                                 num_self_att_layers=T, vocab_size=V, sampled_num=512, num_U2GNN_layers=1,
+                                 device=dev, precision=args.precision)
+        sd0 = {kk: v.clone() for kk, v in model.state_dict().items()}
+        model = model.to(dev)
+        trainer = UnSupTrainer(model, lr=5e-3, max_norm=0.5)
+        batches = [(DeviceBatch.from_offsets(h.input_x, h.offsets, h.X_concat, None, device=dev, input_y=h.input_y),
+                    torch.from_numpy(model.ss.draw_samples()).to(dev)) for h in host]
+    graph = args.graph != 0
+    runner = None
+    if graph:
+        runner = StepGraphs(trainer)
+        for bt in batches:
+            runner.capture(*bt)
+    step = runner.step if runner is not None else trainer.step
+    nb = len(batches)
+    for i in range(args.warmup):
+        step(*batches[i % nb])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(*batches[(args.warmup + i) % nb])
+    t_issue = time.perf_counter() - t0
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    loss = float(trainer.loss.item())
+    if runner is not None:
+        runner.close()
+    cpu = None
+    if args.cpu_baseline:
+        threads = max(1, min(int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count(), os.cpu_count()))
+        torch.set_num_threads(threads)
+        params = {kk: v.detach().cpu().clone().requires_grad_(True) for kk, v in sd0.items()}
+        plist = list(params.values())
+        opt = torch.optim.Adam(plist, lr=args.lr if sup else 5e-3)
+        sids = [model.ss.draw_samples() for _ in host] if not sup else None
+        times = []
+        reps = 40
+        for r in range(reps):
+            h = host[r % nb]
+            t1 = time.perf_counter()
+            opt.zero_grad()
+            ix, X = torch.from_numpy(h.input_x), torch.from_numpy(h.X_concat)
+            if sup:
+                s = O.sup_forward(params, ix, h.offsets, X, 1, T, train=True, dropout=0.5)
+                lo = O.soft_cross_entropy(s, O.label_smoothing(torch.from_numpy(h.labels), C))
+            else:
+                enc = {kk: v for kk, v in params.items() if kk != "ss.weight"}
+                lo = O.unsup_forward(enc, params["ss.weight"], ix, X, torch.from_numpy(h.input_y),
+                                     torch.from_numpy(sids[r % nb]), 1, T, train=True).sum()
+            lo.backward()
+            torch.nn.utils.clip_grad_norm_(plist, 0.5)
+            opt.step()
+            times.append(time.perf_counter() - t1)
+        t = float(np.median(times[5:]))
+        cpu = {"value": 4 / t, "unit": "graphs/s", "cores": threads, "kind": "port",
+               "sample": f"{reps - 5} timed training steps of 4-graph {name} batches (all {k + 1} neighbour slots, "
+                         f"dropout on), median {1e3 * t:.1f} ms/step, oracle/u2gnn_oracle.py on torch CPU"}
+    mean_N = float(np.mean([bt[0].N for bt in batches]))
+    out = {"metric": METRIC_SMALL[args.workload], "value": round(args.steps * 4 / elapsed, 2), "unit": "graphs/s",
+           "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+           "ms_per_step": round(1e3 * elapsed / args.steps, 3), "higher_is_better": True, "scaling": "weak",
+           "vs_baseline": None, "dtype": DTYPE[args.precision],
+           "data": f"{name} (the reference's dataset file), seed-123 batches; random-init weights",
+           "config": {"workload": f"U2GNN-{'Sup' if sup else 'UnSup'} {name}: batch_size=4, num_neighbors={k}, "
+                                  f"num_timesteps={T}, ff_hidden_size={args.ff_hidden_size}"
+                                  + ("" if sup else ", sampled_num=512"),
+                      "global_batch": 4, "mean_nodes_per_batch": round(mean_N, 1), "parallelism": "dp1",
+                      "precision": args.precision, "hip_graph": graph},
+           "final_loss": round(loss, 5), "host_issue_ms_per_step": round(1e3 * t_issue / args.steps, 3),
+           "roofline": None, "cpu_baseline": cpu}
+    emit(out)
+
+
 _JSON_OUT = None
 
 
@@ -260,6 +375,8 @@ def main():
     os.dup2(2, 1)   # fd 1 -> stderr for everything else (native libraries write to fd 1 directly)
     if args.workload == "c5":
         return main_c5(args)
+    if args.workload in ("c2", "c3"):
+        return main_small(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))

@@ -121,7 +121,7 @@ def gather_roofline(b, d, ff, K, dev, reps=20):
     us = e0.elapsed_time(e1) * 1e3 / reps
     nbytes = Rp * dp * 4 + R * 8 + b.N * d * 4
     ach = nbytes / (us * 1e-6) / 1e9
-    return {"bound": "hbm", "kernel": "gather_rows_kernel (a2, all k+1 slots)", "achieved": round(ach, 1),
+    return {"bound": "hbm", "kernel": "gather_rows_multi_kernel (a2, all k+1 slots)", "achieved": round(ach, 1),
             "peak": 8000.0, "unit": "GB/s", "frac": round(ach / 8000.0, 4), "avg_launch_us": round(us, 2),
             "algorithmic_bytes_per_launch": nbytes, "rows": R, "rows_pad": Rp, "d": d, "d_pad": dp}
 

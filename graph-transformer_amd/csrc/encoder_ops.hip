@@ -72,6 +72,85 @@ __global__ void __launch_bounds__(256) gather_rows_kernel(const float *__restric
     }
 }
 
+// a2 gather for 4-byte-aligned source rows, d_pad <= 512 (X_concat, d = 367): GR_RPW rows per wave
+// (their index loads, then all their source loads in flight), XCD-aware block order and, for WIDE,
+// 16-byte stores -- each wave transposes its rows through a private LDS image (lane-consecutive
+// 4-byte ds_write, ds_read_b128 of 4 consecutive columns per lane; both conflict-free), so a row
+// leaves as 16-byte pieces instead of 6 x 256-B dword stores.  ld_dst % 4 == 0 and dst 16-byte
+// aligned (checked by the caller); WIDE also needs d_pad % 4 == 0.
+// Measured on one C4 batch (68374 x 367 -> [68608, 384], tools/gather_ab.py, profiles/r02/gather_ab.txt):
+// one wave per row (MODE 2) 29.4 us; 2 rows/wave 24.7; + XCD order 21.6; + wide stores 18.6;
+// 1 row/wave + XCD + wide 17.8 us (= 6.3 TB/s algorithmic; a 105 MB fill_ takes 14.8 us).  Wide stores
+// alone, without the XCD order, lose (27.1 vs 26.2 us at 4 rows/wave); non-temporal stores lose too.
+template <int GR_RPW, bool WIDE, bool XCD>
+__global__ void __launch_bounds__(256) gather_rows_multi_kernel(const float *__restrict__ src, int64_t ld_src,
+                                                                int64_t src_rows, const int64_t *__restrict__ idx,
+                                                                int64_t idx_stride, float *__restrict__ dst,
+                                                                int64_t ld_dst, int64_t n_rows, int64_t n_rows_pad,
+                                                                int64_t d, int64_t d_pad, int32_t *err) {
+    __shared__ __attribute__((aligned(16))) float img[4][WIDE ? GR_RPW : 1][WIDE ? 512 : 4];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    // XCD: blocks are dealt round-robin to the 8 XCDs; remap so XCD x walks one contiguous eighth of
+    // the rows (gridDim.x % 8 == 0) -- a graph's neighbour rows then stay in one XCD's L2
+    const int64_t blk = XCD ? (int64_t)(blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3) : blockIdx.x;
+    const int64_t row0 = (blk * 4 + w) * GR_RPW;
+    if (row0 >= n_rows_pad) return;
+    int64_t s[GR_RPW];
+#pragma unroll
+    for (int i = 0; i < GR_RPW; ++i) {
+        const int64_t row = row0 + i;
+        s[i] = -1;
+        if (row < n_rows) {
+            const int64_t t = idx[row * idx_stride];
+            if (t < 0 || t >= src_rows) {
+                if (lane == 0 && err) atomicExch(err, 1);
+            } else {
+                s[i] = t;
+            }
+        }
+    }
+    float v[GR_RPW][8];
+#pragma unroll
+    for (int i = 0; i < GR_RPW; ++i) {
+        const float *in = src + (s[i] < 0 ? 0 : s[i]) * ld_src;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int c = 64 * j + lane;
+            v[i][j] = (s[i] >= 0 && c < d) ? in[c] : 0.f;
+        }
+    }
+    if constexpr (WIDE) {
+#pragma unroll
+        for (int i = 0; i < GR_RPW; ++i)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) img[w][i][64 * j + lane] = v[i][j];
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int i = 0; i < GR_RPW; ++i) {
+            const int64_t row = row0 + i;
+            if (row >= n_rows_pad) break;
+            float *o = dst + row * ld_dst;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int c = 256 * j + 4 * lane;
+                if (c < d_pad) *reinterpret_cast<float4 *>(o + c) = *reinterpret_cast<const float4 *>(&img[w][i][c]);
+            }
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < GR_RPW; ++i) {
+            const int64_t row = row0 + i;
+            if (row >= n_rows_pad) break;
+            float *o = dst + row * ld_dst;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int c = 64 * j + lane;
+                if (c < d_pad) o[c] = v[i][j];
+            }
+        }
+    }
+}
+
 // an index outside [0, dst_rows) adds nothing and sets *err (F.embedding raises IndexError there)
 __global__ void __launch_bounds__(256) scatter_add_rows_kernel(const float *src, int64_t ld_src, const int64_t *idx,
                                                                int64_t idx_stride, float *dst, int64_t ld_dst,
@@ -723,6 +802,15 @@ inline unsigned grid_for(int64_t n, int64_t per_block, int64_t cap = 8192) {
 
 extern "C" {
 
+// U2GNN_GATHER_MODE=2 (A/B only): the round-1 one-wave-per-row kernel instead of the multi kernel
+static int gather_mode() {
+    static const int m = [] {
+        const char *e = std::getenv("U2GNN_GATHER_MODE");
+        return e && e[0] ? std::atoi(e) : 0;
+    }();
+    return m;
+}
+
 int u2gnn_gather_rows(const float *src, int64_t ld_src, int64_t src_rows, const int64_t *idx, int64_t idx_stride,
                       float *dst, int64_t ld_dst, int64_t n_rows, int64_t n_rows_pad, int64_t d, int64_t d_pad,
                       int32_t *err, void *stream) {
@@ -734,7 +822,16 @@ int u2gnn_gather_rows(const float *src, int64_t ld_src, int64_t src_rows, const 
     if (small && (d_pad & 3) == 0 && (ld_dst & 3) == 0 && al16(dst) && (ld_src & 3) == 0 && al16(src))
         hipLaunchKernelGGL(gather_rows_kernel<1>, grid, dim3(256), 0, st, src, ld_src, src_rows, idx, idx_stride, dst,
                            ld_dst, n_rows, n_rows_pad, d, d_pad, err);
-    else if (small)
+    else if (d_pad <= 512 && (ld_dst & 3) == 0 && al16(dst) && gather_mode() != 2) {
+        // gridDim.x a multiple of 8 for the XCD order (surplus blocks find no rows and return)
+        const dim3 g8((grid_for(n_rows_pad, 4, 1 << 30) + 7u) / 8u * 8u);
+        if (d_pad & 3)
+            hipLaunchKernelGGL((gather_rows_multi_kernel<1, false, true>), g8, dim3(256), 0, st, src, ld_src, src_rows,
+                               idx, idx_stride, dst, ld_dst, n_rows, n_rows_pad, d, d_pad, err);
+        else
+            hipLaunchKernelGGL((gather_rows_multi_kernel<1, true, true>), g8, dim3(256), 0, st, src, ld_src, src_rows,
+                               idx, idx_stride, dst, ld_dst, n_rows, n_rows_pad, d, d_pad, err);
+    } else if (small)
         hipLaunchKernelGGL(gather_rows_kernel<2>, grid, dim3(256), 0, st, src, ld_src, src_rows, idx, idx_stride, dst,
                            ld_dst, n_rows, n_rows_pad, d, d_pad, err);
     else

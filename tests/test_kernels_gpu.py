@@ -361,28 +361,34 @@ def test_column_reductions_token_sized(rows):
     assert (dbias.double() - dZd[:, :d].double().sum(0)).abs().max().item() < tol
 
 
-@pytest.mark.parametrize("d,d_pad,ld_src,n_src,n_rows,n_pad", [
-    (367, 384, 367, 500, 4099, 4352),     # X_concat at C4 width: 4-byte-aligned rows (mode 2)
-    (384, 384, 384, 300, 1000, 1024),     # padded [Np, dp] re-gather: 16-byte rows (mode 1)
-    (7, 64, 7, 50, 30, 64),               # MUTAG width (mode 2)
-    (6, 64, 8, 40, 33, 64),               # aligned source, d % 4 != 0 (mode 1 tail)
-    (1100, 1152, 1100, 20, 17, 64),       # d_pad > 1024 (mode 0 loop)
+@pytest.mark.parametrize("d,d_pad,ld_src,n_src,n_rows,n_pad,ld_dst", [
+    (367, 384, 367, 500, 4099, 4352, 384),  # X_concat at C4 width: 4-byte-aligned rows (multi kernel, wide)
+    (367, 384, 367, 500, 4099, 4102, 384),  # rows_pad not a multiple of the 32 rows of one XCD block round
+    (384, 384, 384, 300, 1000, 1024, 384),  # padded [Np, dp] re-gather: 16-byte rows (mode 1)
+    (7, 64, 7, 50, 30, 64, 64),             # MUTAG width (multi kernel, wide)
+    (5, 66, 5, 40, 33, 40, 68),             # d_pad % 4 != 0 (multi kernel, dword stores)
+    (5, 66, 5, 40, 33, 40, 66),             # dst rows not 16-byte aligned (mode 2)
+    (600, 640, 600, 40, 70, 80, 640),       # 512 < d_pad <= 1024 (mode 2)
+    (6, 64, 8, 40, 33, 64, 64),             # aligned source, d % 4 != 0 (mode 1 tail)
+    (1100, 1152, 1100, 20, 17, 64, 1152),   # d_pad > 1024 (mode 0 loop)
 ])
-def test_gather_rows_modes(d, d_pad, ld_src, n_src, n_rows, n_pad):
+def test_gather_rows_modes(d, d_pad, ld_src, n_src, n_rows, n_pad, ld_dst):
     """a2 gather (pytorch_U2GNN_Sup.py:32): bit-exact copy of the indexed rows, zero padding, and
-    out-of-range indices reported through err with a zero row."""
+    out-of-range indices reported through err with a zero row; columns past d_pad untouched."""
     g = torch.Generator(device="cpu").manual_seed(d + n_rows)
     src_full = torch.randn(n_src, ld_src, generator=g).to(DEV)
     idx = torch.randint(0, n_src, (n_rows, 2), generator=g)
     idx[n_rows // 2, 0] = n_src          # out of range -> zero row, err = 1
     idx = idx.to(DEV)
-    dst = torch.full((n_pad, d_pad), 7.0, device=DEV)
+    dst_full = torch.full((n_pad, ld_dst), 7.0, device=DEV)
+    dst = dst_full[:, :d_pad]
     err = torch.zeros(1, dtype=torch.int32, device=DEV)
     K.gather_rows(src_full, idx, 2, dst, n_rows, n_pad, d, d_pad, err)
-    ref = torch.zeros(n_pad, d_pad, device=DEV)
+    ref = torch.full((n_pad, ld_dst), 7.0, device=DEV)
+    ref[:, :d_pad] = 0
     ok = idx[:, 0] < n_src
     ref[:n_rows, :d][ok] = src_full[idx[ok, 0], :d]
-    assert torch.equal(dst, ref)
+    assert torch.equal(dst_full, ref)
     assert err.item() == 1
 
 

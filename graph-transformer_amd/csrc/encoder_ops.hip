@@ -577,13 +577,31 @@ __global__ void __launch_bounds__(256) layernorm_fwd_kernel(const float *Z, int6
         return;
     }
     const float *z = Z + row * ldz;
-    float v[LN_V4][4];
+    float v[LN_V4][4], gm[LN_V4][4] = {}, bt[LN_V4][4] = {};
+    float4 t[LN_V4];
+#pragma unroll
+    for (int i = 0; i < LN_V4; ++i) {
+        const int64_t c = 4 * (hl + 32 * i);
+        t[i] = c < d_pad ? ld4(z + c) : z4;
+    }
+    // gamma / beta are unpadded [d] vectors at any 4-byte alignment: element loads at a clamped
+    // column, issued with the row's loads (no per-element branch, no second round trip later)
+#pragma unroll
+    for (int i = 0; i < LN_V4; ++i) {
+        const int64_t c = 4 * (hl + 32 * i);
+        if (c >= d_pad) continue;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int64_t cc = c + q < d ? c + q : d - 1;
+            gm[i][q] = gamma[cc];
+            bt[i][q] = beta[cc];
+        }
+    }
     float s = 0.f;
 #pragma unroll
     for (int i = 0; i < LN_V4; ++i) {
         const int64_t c = 4 * (hl + 32 * i);
-        const float4 t = c < d_pad ? ld4(z + c) : z4;
-        const float x[4] = {t.x, t.y, t.z, t.w};
+        const float x[4] = {t[i].x, t[i].y, t[i].z, t[i].w};
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             v[i][q] = c + q < d ? x[q] : 0.f;
@@ -606,7 +624,7 @@ __global__ void __launch_bounds__(256) layernorm_fwd_kernel(const float *Z, int6
         if (c >= d_pad) continue;
         float o[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) o[q] = c + q < d ? (v[i][q] - mu) * rs * gamma[c + q] + beta[c + q] : 0.f;
+        for (int q = 0; q < 4; ++q) o[q] = c + q < d ? (v[i][q] - mu) * rs * gm[i][q] + bt[i][q] : 0.f;
         *reinterpret_cast<float4 *>(y + c) = make_float4(o[0], o[1], o[2], o[3]);
     }
     if (hl == 0) {
@@ -639,18 +657,31 @@ __global__ void __launch_bounds__(256) layernorm_bwd_kernel(const float *dY, int
     const float mu = mean[row], rs = rstd[row];
     const float *dy = dY + row * ldy;
     const float *z = Z + row * ldz;
-    float xh[LN_V4][4], g[LN_V4][4];
+    float xh[LN_V4][4], g[LN_V4][4], gm[LN_V4][4] = {};
+    float4 ta[LN_V4], tb[LN_V4];
+#pragma unroll
+    for (int i = 0; i < LN_V4; ++i) {
+        const int64_t c = 4 * (hl + 32 * i);
+        ta[i] = c < d_pad ? ld4(dy + c) : z4;
+        tb[i] = c < d_pad ? ld4(z + c) : z4;
+    }
+#pragma unroll
+    for (int i = 0; i < LN_V4; ++i) {   // unpadded [d] gamma: clamped element loads (see the forward)
+        const int64_t c = 4 * (hl + 32 * i);
+        if (c >= d_pad) continue;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) gm[i][q] = gamma[c + q < d ? c + q : d - 1];
+    }
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int i = 0; i < LN_V4; ++i) {
         const int64_t c = 4 * (hl + 32 * i);
-        const float4 a = c < d_pad ? ld4(dy + c) : z4, b = c < d_pad ? ld4(z + c) : z4;
-        const float av[4] = {a.x, a.y, a.z, a.w}, bv[4] = {b.x, b.y, b.z, b.w};
+        const float av[4] = {ta[i].x, ta[i].y, ta[i].z, ta[i].w}, bv[4] = {tb[i].x, tb[i].y, tb[i].z, tb[i].w};
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const bool ok = c + q < d;
             xh[i][q] = ok ? (bv[q] - mu) * rs : 0.f;
-            g[i][q] = ok ? av[q] * gamma[c + q] : 0.f;
+            g[i][q] = ok ? av[q] * gm[i][q] : 0.f;
             s1 += g[i][q];
             s2 += g[i][q] * xh[i][q];
         }

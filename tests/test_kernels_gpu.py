@@ -152,7 +152,7 @@ def _unpack_bits(kb, cols):
     return bits.reshape(kb.shape[0], -1)[:, :cols]
 
 
-@pytest.mark.parametrize("Np,N", [(1280, 1100), (256, 256), (2048, 1999), (9216, 9000)])
+@pytest.mark.parametrize("Np,N", [(1280, 1100), (256, 256), (2048, 1999), (4864, 4776), (9216, 9000)])
 def test_attn_softmax_keep_bits(Np, N):
     """keep bits == the dropout mask on the valid block, 0 on padded rows/columns (n_pad not a
     multiple of the 1024-column trip included)."""

@@ -331,10 +331,11 @@ def test_gather_pack_colsum():
     assert rel_err(out, ref) < 1e-5
 
 
-@pytest.mark.parametrize("rows", [8192, 8209, 20011, 82110])
+@pytest.mark.parametrize("rows", [1, 255, 2000, 2560, 2561, 4864, 8192, 8209, 20011, 82110])
 def test_column_reductions_token_sized(rows):
-    """Neighbour-mode row counts: colsum / LN parameter sums fold several 16-row groups into one
-    chunk (at most 512 chunks, the ragged last one included); sums against torch float64."""
+    """colsum / LN parameter sums against torch float64, from one row to neighbour-mode row counts
+    (those fold several 16-row groups into one chunk: at most 512 chunks, the ragged last one
+    included)."""
     d, dp = 367, 384
     X = torch.zeros(rows, dp, device=DEV)
     X[:, :d] = _mk(rows, d, seed=31)

@@ -9,7 +9,7 @@ rows = list(csv.DictReader(open(sys.argv[1])))
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
 key = next(k for k in ("Stream_Id", "Queue_Id", "Stream_ID") if k in rows[0])
 ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r[key], r["Kernel_Name"]) for r in rows)
-ends = [e for s, e, q, n in ev if "adam_kernel" in n]
+ends = [e for s, e, q, n in ev if "adam_kernel" in n or "adam_dev_kernel" in n]
 if len(ends) < steps + 1:
     sys.exit(f"only {len(ends)} optimizer steps in the trace")
 t0, t1 = ends[-steps - 1], ends[-1]

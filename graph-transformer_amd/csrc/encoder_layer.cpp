@@ -185,8 +185,12 @@ int gemm_split(Arena &W, const Dims &D, const float *A, const float *B, float *C
     }
     int t;
     int64_t tiles, target = 448;
+    static const int64_t target256 = [] {   // U2GNN_SPLIT_TARGET256 (A/B): blocks aimed at for 256x128 tiles
+        const char *e = std::getenv("U2GNN_SPLIT_TARGET256");
+        return e && e[0] ? (int64_t)std::atoi(e) : (int64_t)240;
+    }();
     if (!f32 && M % 256 == 0 && N % 128 == 0 && (M / 256) * (N / 128) >= 32) {
-        t = 256, tiles = (M / 256) * (N / 128), target = 240;
+        t = 256, tiles = (M / 256) * (N / 128), target = target256;
     } else {
         t = (M % 128 == 0 && N % 128 == 0) ? 128 : 64;
         tiles = (M / t) * (N / t);

@@ -20,6 +20,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
+#include <vector>
 
 #include "u2gnn_hip.h"
 
@@ -248,12 +251,52 @@ int bias_grad(Arena &W, const float *dY, int64_t rows, int64_t cols_pad, int64_t
     return u2gnn_colsum(dY, rows, cols_pad, ld, cb0, cb1, out, 0, ws, st);
 }
 
+// Fork / join events come from a per-device ring of pre-created events (U2GNN_EVENT_POOL=0: one
+// hipEventCreate / hipEventDestroy per hand-off, the round-1 scheme).  Re-recording an event is
+// safe once the waits on its previous record are enqueued (a wait binds the record current at the
+// call), and a ring of 256 is far longer than the hand-offs of one layer in flight.
+bool event_pool_on() {
+    static const bool v = [] {
+        const char *e = std::getenv("U2GNN_EVENT_POOL");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
+
+hipEvent_t pooled_event() {
+    constexpr size_t kRing = 256;
+    static std::mutex mu;
+    static std::map<int, std::pair<std::vector<hipEvent_t>, size_t>> pools;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> lk(mu);
+    auto &p = pools[dev];
+    if (p.first.empty()) {
+        p.first.resize(kRing, nullptr);
+        for (auto &ev : p.first)
+            if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+                for (auto &x : p.first)
+                    if (x) (void)hipEventDestroy(x);
+                p.first.clear();
+                return nullptr;
+            }
+    }
+    return p.first[p.second++ % kRing];
+}
+
 // side-stream hand-off: the side stream waits for everything issued on main so far
 struct Side {
     hipStream_t main, side;
     bool plan;
     int fork() {
         if (plan || side == main) return U2GNN_OK;
+        if (event_pool_on()) {
+            hipEvent_t ev = pooled_event();
+            if (!ev) return U2GNN_E_ARG;
+            hipError_t e = hipEventRecord(ev, main);
+            if (e == hipSuccess) e = hipStreamWaitEvent(side, ev, 0);
+            return e == hipSuccess ? U2GNN_OK : (int)e;
+        }
         hipEvent_t ev;
         hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
         if (e != hipSuccess) return (int)e;
@@ -274,6 +317,12 @@ struct Side {
     int mark(hipEvent_t *ev) {
         *ev = nullptr;
         if (plan || side == main) return U2GNN_OK;
+        if (event_pool_on()) {
+            *ev = pooled_event();
+            if (!*ev) return U2GNN_E_ARG;
+            const hipError_t e = hipEventRecord(*ev, side);
+            return e == hipSuccess ? U2GNN_OK : (int)e;
+        }
         hipError_t e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
         if (e == hipSuccess) e = hipEventRecord(*ev, side);
         return e == hipSuccess ? U2GNN_OK : (int)e;
@@ -282,6 +331,7 @@ struct Side {
     int wait(hipEvent_t ev) {
         if (!ev) return U2GNN_OK;
         hipError_t e = hipStreamWaitEvent(main, ev, 0);
+        if (event_pool_on()) return e == hipSuccess ? U2GNN_OK : (int)e;
         const hipError_t e2 = hipEventDestroy(ev);
         if (e == hipSuccess) e = e2;
         return e == hipSuccess ? U2GNN_OK : (int)e;

@@ -55,6 +55,10 @@ __device__ __forceinline__ void win_stage_part(const float *src, int64_t ld, int
 // S[i][j] = A_i . B_j (i, j < W) into S[W][W+1]: one (i, j) pair per thread, float4 LDS reads,
 // four partial sums by column residue combined as (s0 + s1) + (s2 + s3)
 __device__ __forceinline__ void win_pair_dots(const float *A, const float *B, int W, int dp, float *S) {
+#ifdef U2GNN_EXP_WIN_NODOTS   // ablation (tools/win_bench.py): scores not computed
+    for (int e = threadIdx.x; e < W * W; e += blockDim.x) S[(e / W) * (W + 1) + e % W] = A[e % 4];
+    return;
+#endif
     const int LD4 = win_ld(dp) / 4, dq = dp / 4;
     for (int e = threadIdx.x; e < W * W; e += blockDim.x) {
         const int i = e / W, j = e - i * W;
@@ -75,40 +79,41 @@ __device__ __forceinline__ void win_pair_dots(const float *A, const float *B, in
 
 // out[row0 + i][col + c] = scale * sum_j C(i, j) * M[j][c] for i < W, c < dp, with C(i, j) =
 // C[i][j] (TRANS false) or C[j][i] (TRANS true) of a [W][W+1] LDS matrix.  A thread owns a float4
-// column group and a block of up to 16 rows (M read once per j for all of them); j runs in order.
+// column group and a block of rb <= RB rows (M read once per j for all of them); j runs in order, so
+// every output is the same fp32 chain as a plain loop.  The RB coefficients of a j are loaded as one
+// batch at clamped rows (rows past the block compute on a duplicate and are not stored): no
+// per-row branch around an LDS read, one wait per j instead of one per coefficient.
 constexpr int WIN_RB = 16;
-template <bool TRANS>
-__device__ __forceinline__ void win_combine(const float *C, const float *M, int W, int dp, float scale, float *out,
-                                            int64_t ldo, int64_t row0, int col) {
+template <bool TRANS, int RB>
+__device__ __forceinline__ void win_combine_rb(const float *C, const float *M, int W, int dp, float scale, float *out,
+                                               int64_t ldo, int64_t row0, int col, int nb, int rb) {
     const int dq = dp / 4, LD4 = win_ld(dp) / 4;
-    int nb = (int)blockDim.x / dq;
-    const int nb_min = (W + WIN_RB - 1) / WIN_RB;
-    if (nb < nb_min) nb = nb_min;
-    if (nb > W) nb = W;
-    const int rb = (W + nb - 1) / nb;
     const float4 *M4 = reinterpret_cast<const float4 *>(M);
     for (int e = threadIdx.x; e < dq * nb; e += blockDim.x) {
         const int c4 = e % dq, i0 = (e / dq) * rb;
         const int cnt = min(rb, W - i0);
         if (cnt <= 0) continue;
-        float4 acc[WIN_RB];
+        int ri[RB];
 #pragma unroll
-        for (int r = 0; r < WIN_RB; ++r) acc[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int r = 0; r < RB; ++r) ri[r] = i0 + min(r, cnt - 1);
+        float4 acc[RB];
+#pragma unroll
+        for (int r = 0; r < RB; ++r) acc[r] = make_float4(0.f, 0.f, 0.f, 0.f);
         for (int j = 0; j < W; ++j) {
             const float4 m = M4[j * LD4 + c4];
+            float cf[RB];
 #pragma unroll
-            for (int r = 0; r < WIN_RB; ++r) {
-                if (r < cnt) {
-                    const float cf = TRANS ? C[j * (W + 1) + i0 + r] : C[(i0 + r) * (W + 1) + j];
-                    acc[r].x = fmaf(cf, m.x, acc[r].x);
-                    acc[r].y = fmaf(cf, m.y, acc[r].y);
-                    acc[r].z = fmaf(cf, m.z, acc[r].z);
-                    acc[r].w = fmaf(cf, m.w, acc[r].w);
-                }
+            for (int r = 0; r < RB; ++r) cf[r] = TRANS ? C[j * (W + 1) + ri[r]] : C[ri[r] * (W + 1) + j];
+#pragma unroll
+            for (int r = 0; r < RB; ++r) {
+                acc[r].x = fmaf(cf[r], m.x, acc[r].x);
+                acc[r].y = fmaf(cf[r], m.y, acc[r].y);
+                acc[r].z = fmaf(cf[r], m.z, acc[r].z);
+                acc[r].w = fmaf(cf[r], m.w, acc[r].w);
             }
         }
 #pragma unroll
-        for (int r = 0; r < WIN_RB; ++r) {
+        for (int r = 0; r < RB; ++r) {
             if (r < cnt) {
                 float4 v = acc[r];
                 if (scale != 1.f) v.x *= scale, v.y *= scale, v.z *= scale, v.w *= scale;
@@ -116,6 +121,28 @@ __device__ __forceinline__ void win_combine(const float *C, const float *M, int 
             }
         }
     }
+}
+
+template <bool TRANS>
+__device__ __forceinline__ void win_combine(const float *C, const float *M, int W, int dp, float scale, float *out,
+                                            int64_t ldo, int64_t row0, int col) {
+#ifdef U2GNN_EXP_WIN_NOCOMBINE   // ablation: the products skipped, the rows still written
+    for (int e = threadIdx.x; e < W * (dp / 4); e += blockDim.x)
+        *reinterpret_cast<float4 *>(out + (row0 + e / (dp / 4)) * ldo + col + 4 * (e % (dp / 4))) =
+            make_float4(C[0], M[0], scale, 0.f);
+    return;
+#endif
+    const int dq = dp / 4;
+    int nb = (int)blockDim.x / dq;
+    const int nb_min = (W + WIN_RB - 1) / WIN_RB;
+    if (nb < nb_min) nb = nb_min;
+    if (nb > W) nb = W;
+    const int rb = (W + nb - 1) / nb;   // block-uniform: one instantiation per launch shape
+    if (rb <= 4) win_combine_rb<TRANS, 4>(C, M, W, dp, scale, out, ldo, row0, col, nb, rb);
+    else if (rb <= 6) win_combine_rb<TRANS, 6>(C, M, W, dp, scale, out, ldo, row0, col, nb, rb);
+    else if (rb <= 9) win_combine_rb<TRANS, 9>(C, M, W, dp, scale, out, ldo, row0, col, nb, rb);
+    else if (rb <= 12) win_combine_rb<TRANS, 12>(C, M, W, dp, scale, out, ldo, row0, col, nb, rb);
+    else win_combine_rb<TRANS, WIN_RB>(C, M, W, dp, scale, out, ldo, row0, col, nb, rb);
 }
 
 // forward: O_n = dropout(softmax(Qs_n K_n^T)) V_n; P_n (pre-dropout probabilities) saved.

@@ -550,7 +550,7 @@ __global__ void __launch_bounds__(256) rowdot_kernel(const float *A, int64_t lda
 // a3.3/a3.4 post-LN (eps 1e-5).  One half-wave (32 lanes) per row, a float4 of columns per lane,
 // the row cached in registers (d_pad <= 1024): 16-byte loads/stores, 8 rows per block.
 // ------------------------------------------------------------------------------------------
-constexpr int LN_V4 = 8;       // d_pad / 128 upper bound
+constexpr int LN_V4_MAX = 8;   // d_pad / 128 upper bound (template V4: float4 per lane = ceil(d_pad / 128))
 constexpr int LN_MAXV = 16;    // d_pad / 64 upper bound (host check)
 
 __device__ __forceinline__ float half_sum(float v) {
@@ -559,6 +559,7 @@ __device__ __forceinline__ float half_sum(float v) {
     return v;
 }
 
+template <int LN_V4>
 __global__ void __launch_bounds__(256) layernorm_fwd_kernel(const float *Z, int64_t ldz, const float *gamma,
                                                             const float *beta, float *Y, int64_t ldy, float *mean,
                                                             float *rstd, int64_t rows_valid, int64_t rows_pad,
@@ -634,6 +635,7 @@ __global__ void __launch_bounds__(256) layernorm_fwd_kernel(const float *Z, int6
 }
 
 // LN backward, row part: one half-wave per row (8 rows per block).
+template <int LN_V4>
 __global__ void __launch_bounds__(256) layernorm_bwd_kernel(const float *dY, int64_t ldy, const float *Z, int64_t ldz,
                                                             const float *mean, const float *rstd, const float *gamma,
                                                             float *dZ, int64_t lddz, float *dZd, int64_t lddrop,
@@ -1011,8 +1013,19 @@ int u2gnn_layernorm_fwd(const float *Z, int64_t ldz, const float *gamma, const f
     if (!Z || !gamma || !beta || !Y || !mean || !rstd || d < 1 || d > d_pad || d_pad > LN_MAXV * 64)
         return U2GNN_E_ARG;
     if (!al16(Z) || !al16(Y) || (ldz & 3) || (ldy & 3) || (d_pad & 3)) return U2GNN_E_ALIGN;
-    hipLaunchKernelGGL(layernorm_fwd_kernel, dim3(grid_for(rows_pad, 8, 1 << 30)), dim3(256), 0, u2gnn_stream(stream),
-                       Z, ldz, gamma, beta, Y, ldy, mean, rstd, rows_valid, rows_pad, d, d_pad, eps);
+    // registers sized to the row: V4 = ceil(d_pad / 128) float4 per lane (C4: 3), not the maximum 8
+    // (measured: the 8-wide arrays held ~160 VGPRs and 3 waves per SIMD for every width)
+    const dim3 gr(grid_for(rows_pad, 8, 1 << 30));
+    hipStream_t st = u2gnn_stream(stream);
+#define U2GNN_LNF(V) hipLaunchKernelGGL(layernorm_fwd_kernel<V>, gr, dim3(256), 0, st, Z, ldz, gamma, beta, Y, ldy, \
+                                        mean, rstd, rows_valid, rows_pad, d, d_pad, eps)
+    const int64_t v4 = (d_pad + 127) / 128;
+    if (v4 <= 1) U2GNN_LNF(1);
+    else if (v4 == 2) U2GNN_LNF(2);
+    else if (v4 == 3) U2GNN_LNF(3);
+    else if (v4 == 4) U2GNN_LNF(4);
+    else U2GNN_LNF(LN_V4_MAX);
+#undef U2GNN_LNF
     return u2gnn_launch_status();
 }
 
@@ -1025,9 +1038,17 @@ int u2gnn_layernorm_bwd(const float *dY, int64_t ldy, const float *Z, int64_t ld
     if (!al16(dY) || !al16(Z) || !al16(dZ) || (ldy & 3) || (ldz & 3) || (lddz & 3) || (d_pad & 3) ||
         (dZdrop && (!al16(dZdrop) || (lddrop & 3))))
         return U2GNN_E_ALIGN;
-    hipLaunchKernelGGL(layernorm_bwd_kernel, dim3(grid_for(rows_pad, 8, 1 << 30)), dim3(256), 0, u2gnn_stream(stream),
-                       dY, ldy, Z, ldz, mean, rstd, gamma, dZ, lddz, dZdrop, lddrop, p, seed, u2gnn_g_epoch, rows_valid, rows_pad, d,
-                       d_pad);
+    const dim3 gr(grid_for(rows_pad, 8, 1 << 30));
+    hipStream_t st = u2gnn_stream(stream);
+#define U2GNN_LNB(V) hipLaunchKernelGGL(layernorm_bwd_kernel<V>, gr, dim3(256), 0, st, dY, ldy, Z, ldz, mean, rstd, gamma, \
+                                        dZ, lddz, dZdrop, lddrop, p, seed, u2gnn_g_epoch, rows_valid, rows_pad, d, d_pad)
+    const int64_t v4 = (d_pad + 127) / 128;
+    if (v4 <= 1) U2GNN_LNB(1);
+    else if (v4 == 2) U2GNN_LNB(2);
+    else if (v4 == 3) U2GNN_LNB(3);
+    else if (v4 == 4) U2GNN_LNB(4);
+    else U2GNN_LNB(LN_V4_MAX);
+#undef U2GNN_LNB
     return u2gnn_launch_status();
 }
 

@@ -262,8 +262,10 @@ def test_dropout_mask_statistics():
     assert m.mean(1).std().item() < 4 * 0.5 / C ** 0.5   # per-row rates: binomial spread
 
 
-def test_layernorm_fwd_bwd():
-    Np, N, d, dp = 128, 100, 67, 128
+@pytest.mark.parametrize("d,dp", [(67, 128), (200, 256), (367, 384), (500, 512), (600, 640), (1000, 1024)])
+def test_layernorm_fwd_bwd(d, dp):
+    """Per-lane widths 1, 2, 3, 4 and the 8-wide fallback of the LayerNorm kernels."""
+    Np, N = 128, 100
     Z = _mk(Np, dp, seed=11)
     gam, bet = _mk(d, seed=12), _mk(d, seed=13)
     Y = torch.empty(Np, dp, device=DEV)

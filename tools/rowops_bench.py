@@ -69,6 +69,17 @@ def main():
     rows.append(("attn_softmax_fwd (signed)", t(lambda: K.attn_softmax_fwd(S, Np, None, Pd, Np, N, Np, N, Np, 0.5, 11)),
                  2 * SMB))
     rows.append(("copy 94.6 MB", t(lambda: Pd.copy_(S)), 2 * SMB))
+    # neighbour-mode token rows (82 K): bandwidth, not launch latency, decides here
+    R = 82176
+    Zt = torch.randn(R, dp, device=dev, generator=g)
+    Yt, dYt = torch.empty_like(Zt), torch.randn(R, dp, device=dev, generator=g)
+    dZt, dZdt = torch.empty_like(Zt), torch.empty_like(Zt)
+    mt, rt = torch.empty(R, device=dev), torch.empty(R, device=dev)
+    TMB = R * dp * 4 / 1e6
+    rows.append(("ln_fwd 82K rows", t(lambda: K.layernorm_fwd(Zt, dp, gam, bet, Yt, dp, mt, rt, R - 66, R, d, dp)), 2 * TMB))
+    rows.append(("ln_bwd (+drop) 82K rows", t(lambda: K.layernorm_bwd(dYt, dp, Zt, dp, mt, rt, gam, dZt, dp, dZdt, dp, 0.5,
+                                                                     7, R - 66, R, d, dp)), 4 * TMB))
+    rows.append(("copy 126 MB", t(lambda: Yt.copy_(Zt)), 2 * TMB))
     for name, us, mb in rows:
         bw = f"{mb / us:6.2f} TB/s" if mb else ""
         print(f"{name:28s} {us:8.2f} us  {mb:7.1f} MB  {bw}", flush=True)

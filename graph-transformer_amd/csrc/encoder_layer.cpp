@@ -187,7 +187,11 @@ int gemm_split(Arena &W, const Dims &D, const float *A, const float *B, float *C
         return rc;
     }
     int t;
-    int64_t tiles, target = 448;
+    static const int64_t target_small = [] {   // U2GNN_SPLIT_TARGET (A/B): blocks aimed at for 64/128 tiles
+        const char *e = std::getenv("U2GNN_SPLIT_TARGET");
+        return e && e[0] ? (int64_t)std::atoi(e) : (int64_t)448;
+    }();
+    int64_t tiles, target = target_small;
     static const int64_t target256 = [] {   // U2GNN_SPLIT_TARGET256 (A/B): blocks aimed at for 256x128 tiles
         const char *e = std::getenv("U2GNN_SPLIT_TARGET256");
         return e && e[0] ? (int64_t)std::atoi(e) : (int64_t)240;

@@ -10,6 +10,9 @@
 // the whole attention core of a node is one block with no HBM round trip for scores.
 #include "u2gnn_common.h"
 
+#include <algorithm>
+#include <cstdlib>
+
 namespace {
 
 constexpr int WIN_MAX = 32;
@@ -189,6 +192,93 @@ __global__ void __launch_bounds__(256) window_attn_fwd_kernel(const float *QKV, 
     win_combine<false>(S, Vs, W, dp, 1.f, O, ldo, row0, 0);
 }
 
+// Persistent forward: the same per-node maths and order (bit-identical outputs), with a block per
+// LDS slot of the chip walking nodes n, n + grid, ... and the operand traffic taken off the
+// critical path: the next node's Q and K are loaded into registers while this node computes, so a
+// node's opening HBM latency overlaps the previous node's work (PF float4 per thread per operand:
+// W * dp / 4 <= 256 * PF; V is staged during the softmax as in window_attn_fwd_kernel -- holding it
+// in registers too spilled).
+template <int PF>
+__device__ __forceinline__ void win_regs_load(const float *src, int64_t ld, int64_t row0, int col, int W, int dq,
+                                              float4 (&r)[PF]) {
+#pragma unroll
+    for (int q = 0; q < PF; ++q) {
+        const int e = threadIdx.x + q * 256;
+        r[q] = e < W * dq ? *reinterpret_cast<const float4 *>(src + (row0 + e / dq) * ld + col + (e % dq) * 4)
+                          : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+}
+
+template <int PF>
+__device__ __forceinline__ void win_regs_store(float *img, int W, int dq, int LD, const float4 (&r)[PF]) {
+#pragma unroll
+    for (int q = 0; q < PF; ++q) {
+        const int e = threadIdx.x + q * 256;
+        if (e < W * dq) *reinterpret_cast<float4 *>(img + (e / dq) * LD + (e % dq) * 4) = r[q];
+    }
+}
+
+// MINW waves per SIMD = blocks per CU (3 = the LDS bound at C4 shapes)
+template <int PF, int RB, int MINW>
+__global__ void __launch_bounds__(256, MINW) window_attn_fwd_pf_kernel(const float *QKV, int64_t ldq, int W, int dp,
+                                                                 float *O, int64_t ldo, float *Psave, float p,
+                                                                 uint64_t seed, const uint64_t *seed_epoch,
+                                                                 int64_t n_nodes, int64_t rows_pad) {
+    seed = u2gnn_seed(seed, seed_epoch);
+    extern __shared__ float sm[];
+    const int LD = win_ld(dp), dq = dp / 4;
+    float *Qs = sm, *Ks = Qs + W * LD, *S = Ks + W * LD;   // S: [W][W+1]
+    float *Vs = Qs;
+    const int tid = threadIdx.x;
+    float4 rq[PF], rk[PF];
+    int64_t n = blockIdx.x;
+    if (n < n_nodes) {
+        win_regs_load<PF>(QKV, ldq, n * W, 0, W, dq, rq);
+        win_regs_load<PF>(QKV, ldq, n * W, dp, W, dq, rk);
+    }
+    for (; n < n_nodes; n += gridDim.x) {
+        const int64_t row0 = n * W;
+        win_regs_store<PF>(Qs, W, dq, LD, rq);
+        win_regs_store<PF>(Ks, W, dq, LD, rk);
+        const int64_t nn = n + gridDim.x;
+        if (nn < n_nodes) {   // the next node's Q, K: land during this node's work
+            win_regs_load<PF>(QKV, ldq, nn * W, 0, W, dq, rq);
+            win_regs_load<PF>(QKV, ldq, nn * W, dp, W, dq, rk);
+        }
+        __syncthreads();
+        win_pair_dots(Qs, Ks, W, dp, S);
+        __syncthreads();
+        if (tid < 64) {
+          if (tid < W) {   // row softmax, save P, keep Pd in S (as window_attn_fwd_kernel)
+            float *srow = S + tid * (W + 1);
+            float m = -INFINITY;
+            for (int j = 0; j < W; ++j) m = fmaxf(m, srow[j]);
+            float sum = 0.f;
+            for (int j = 0; j < W; ++j) {
+                srow[j] = expf(srow[j] - m);
+                sum += srow[j];
+            }
+            const float inv = 1.f / sum, ks = p > 0.f ? 1.f / (1.f - p) : 1.f;
+            float *prow = Psave + (n * W + tid) * W;
+            for (int j = 0; j < W; ++j) {
+                const float pv = srow[j] * inv;
+                prow[j] = pv;
+                srow[j] = (p > 0.f) ? (u2gnn_keep(seed, (uint32_t)(row0 + tid), (uint32_t)j, p) ? pv * ks : 0.f) : pv;
+            }
+          }
+        } else {   // V over the dead Q image by the waves the softmax leaves idle
+            win_stage_part(QKV, ldq, row0, 2 * dp, W, dp, Vs, tid - 64, blockDim.x - 64);
+        }
+        __syncthreads();
+        // the combine at the one row-block width the host chose (win_combine's rule), so the
+        // kernel's registers are not sized by the widest instantiation
+        win_combine_rb<false, RB>(S, Vs, W, dp, 1.f, O, ldo, row0, 0, (W + RB - 1) / RB, RB);
+        __syncthreads();   // the next node overwrites Qs / Ks / S
+    }
+    for (int64_t r = n_nodes * W + blockIdx.x; r < rows_pad; r += gridDim.x)
+        for (int c = tid * 4; c < dp; c += 1024) *reinterpret_cast<float4 *>(O + r * ldo + c) = make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
 // backward: from dO and the saved P -> dQKV (the Q part already multiplied by q_scale = 1/sqrt(d),
 // i.e. the gradient of the in-projection's pre-scale output).  Two operand images: dO and V for
 // dP; K replaces V (staged while wave 0 runs the softmax backward) for dQ beside dV; Q replaces
@@ -238,9 +328,99 @@ __global__ void __launch_bounds__(256) window_attn_bwd_kernel(const float *QKV, 
     win_combine<true>(dS, img0, W, dp, 1.f, dQKV, ldg, row0, dp);       // dK_i = sum_j dS[j][i] Q_j
 }
 
+// Persistent backward (the same per-node maths and order as window_attn_bwd_kernel, bit-identical):
+// the next node's dO and V are loaded into registers while this node computes and this node's Q
+// while its scores are formed (K is staged beside the softmax as before; holding it in registers
+// too spilled).
+template <int PF, int RB, int MINW>
+__global__ void __launch_bounds__(256, MINW) window_attn_bwd_pf_kernel(const float *QKV, int64_t ldq, int W, int dp,
+                                                                       const float *dO, int64_t ldo,
+                                                                       const float *Psave, float p, uint64_t seed,
+                                                                       const uint64_t *seed_epoch, float q_scale,
+                                                                       float *dQKV, int64_t ldg, int64_t n_nodes,
+                                                                       int64_t rows_pad) {
+    seed = u2gnn_seed(seed, seed_epoch);
+    extern __shared__ float sm[];
+    const int LD = win_ld(dp), dq = dp / 4;
+    float *img0 = sm, *img1 = img0 + W * LD;
+    float *Pd = img1 + W * LD, *dS = Pd + W * (W + 1);   // [W][W+1] each
+    const int tid = threadIdx.x;
+    const int nb = (W + RB - 1) / RB;
+    float4 ra[PF], rv[PF], rq[PF];
+    int64_t n = blockIdx.x;
+    if (n < n_nodes) {
+        win_regs_load<PF>(dO, ldo, n * W, 0, W, dq, ra);
+        win_regs_load<PF>(QKV, ldq, n * W, 2 * dp, W, dq, rv);
+    }
+    for (; n < n_nodes; n += gridDim.x) {
+        const int64_t row0 = n * W;
+        win_regs_store<PF>(img0, W, dq, LD, ra);   // img0 = dO
+        win_regs_store<PF>(img1, W, dq, LD, rv);   // img1 = V
+        win_regs_load<PF>(QKV, ldq, row0, 0, W, dq, rq);   // this node's Q: lands during the dots
+        const int64_t nn = n + gridDim.x;
+        if (nn < n_nodes) {   // the next node's dO and V land during this node's work
+            win_regs_load<PF>(dO, ldo, nn * W, 0, W, dq, ra);
+            win_regs_load<PF>(QKV, ldq, nn * W, 2 * dp, W, dq, rv);
+        }
+        __syncthreads();
+        win_pair_dots(img0, img1, W, dp, dS);
+        __syncthreads();
+        if (tid < 64) {
+            if (tid < W) {
+                const float *prow = Psave + (n * W + tid) * W;
+                float *ds = dS + tid * (W + 1), *pd = Pd + tid * (W + 1);
+                const float ks = p > 0.f ? 1.f / (1.f - p) : 1.f;
+                float delta = 0.f;
+                for (int j = 0; j < W; ++j) {
+                    const bool keep = (p > 0.f) ? u2gnn_keep(seed, (uint32_t)(row0 + tid), (uint32_t)j, p) : true;
+                    const float pv = prow[j];
+                    const float dp_ = keep ? ds[j] * ks : 0.f;
+                    pd[j] = keep ? pv * ks : 0.f;
+                    ds[j] = dp_;
+                    delta += dp_ * pv;
+                }
+                for (int j = 0; j < W; ++j) ds[j] = prow[j] * (ds[j] - delta);
+            }
+        } else {
+            win_stage_part(QKV, ldq, row0, dp, W, dp, img1, tid - 64, blockDim.x - 64);   // img1 = K
+        }
+        __syncthreads();
+        win_combine_rb<true, RB>(Pd, img0, W, dp, 1.f, dQKV, ldg, row0, 2 * dp, nb, RB);    // dV
+        win_combine_rb<false, RB>(dS, img1, W, dp, q_scale, dQKV, ldg, row0, 0, nb, RB);   // dQ
+        __syncthreads();
+        win_regs_store<PF>(img0, W, dq, LD, rq);   // img0 = Q
+        __syncthreads();
+        win_combine_rb<true, RB>(dS, img0, W, dp, 1.f, dQKV, ldg, row0, dp, nb, RB);       // dK
+        __syncthreads();   // the next node overwrites the images
+    }
+    for (int64_t r = n_nodes * W + blockIdx.x; r < rows_pad; r += gridDim.x)
+        for (int c = tid * 4; c < 3 * dp; c += 1024)
+            *reinterpret_cast<float4 *>(dQKV + r * ldg + c) = make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
 inline size_t fwd_lds(int W, int dp) { return (size_t)(2 * W * (dp + 4) + W * (W + 1)) * sizeof(float); }
 inline size_t bwd_lds(int W, int dp) { return (size_t)(2 * W * (dp + 4) + 2 * W * (W + 1)) * sizeof(float); }
 constexpr size_t LDS_LIMIT = 160 * 1024;
+
+// U2GNN_WIN_PF (A/B): 0 = one block per node; 2 (default) = the persistent prefetching kernels at 2
+// blocks per CU; 3 = the forward at 3 blocks per CU (its registers then spill: slower, measured)
+int win_pf_mode() {
+    static const int v = [] {
+        const char *e = std::getenv("U2GNN_WIN_PF");
+        return e && e[0] ? std::atoi(e) : 2;
+    }();
+    return v;
+}
+
+int cu_count() {
+    static const int n = [] {
+        int dev = 0, c = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            return 256;
+        return c > 0 ? c : 256;
+    }();
+    return n;
+}
 
 }  // namespace
 
@@ -259,6 +439,29 @@ int u2gnn_window_attn_fwd(const float *QKV, int64_t ldq, int32_t W, int32_t dp, 
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_LIMIT);
         if (e != hipSuccess) return (int)e;
         attr = true;
+    }
+    // persistent prefetching variant for the shapes it is instantiated for (C4 neighbour mode:
+    // W = 17, dp = 384 -> 1632 float4 per operand = 7 per thread; win_combine's row blocks: 2 x 9)
+    const int64_t elems = (int64_t)W * (dp / 4);   // float4 per operand image
+    int nb = 256 / (dp / 4);
+    nb = std::max(nb, (W + 15) / 16);
+    nb = std::min(nb, (int)W);
+    const int rb = (W + nb - 1) / nb;
+    const int pf = win_pf_mode();
+    if ((pf == 2 || pf == 3) && elems > 256 * 6 && elems <= 256 * 7 && rb == 9 && (W + 8) / 9 == nb) {
+        auto kern = pf == 2 ? window_attn_fwd_pf_kernel<7, 9, 2> : window_attn_fwd_pf_kernel<7, 9, 3>;
+        static bool attr_pf[2] = {false, false};
+        if (!attr_pf[pf - 2]) {
+            const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_LIMIT);
+            if (e != hipSuccess) return (int)e;
+            attr_pf[pf - 2] = true;
+        }
+        const int64_t per_cu = std::min<int64_t>(pf, std::max<int64_t>(1, (int64_t)(LDS_LIMIT / lds)));
+        const int64_t grid = std::min<int64_t>(n_nodes, per_cu * cu_count());
+        hipLaunchKernelGGL(kern, dim3((unsigned)std::max<int64_t>(grid, 1)), dim3(256), lds, u2gnn_stream(stream), QKV,
+                           ldq, W, dp, O, ldo, Psave, p, seed, u2gnn_g_epoch, n_nodes, rows_pad);
+        return u2gnn_launch_status();
     }
     const int64_t pad_blocks = (rows_pad - n_nodes * W + W - 1) / W;
     hipLaunchKernelGGL(window_attn_fwd_kernel, dim3((unsigned)(n_nodes + pad_blocks)), dim3(256), lds,
@@ -282,6 +485,26 @@ int u2gnn_window_attn_bwd(const float *QKV, int64_t ldq, int32_t W, int32_t dp, 
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_LIMIT);
         if (e != hipSuccess) return (int)e;
         attr = true;
+    }
+    const int64_t elems = (int64_t)W * (dp / 4);
+    int nb = 256 / (dp / 4);
+    nb = std::max(nb, (W + 15) / 16);
+    nb = std::min(nb, (int)W);
+    const int rb = (W + nb - 1) / nb;
+    if (win_pf_mode() == 2 && elems > 256 * 6 && elems <= 256 * 7 && rb == 9 && (W + 8) / 9 == nb) {
+        auto kern = window_attn_bwd_pf_kernel<7, 9, 2>;
+        static bool attr_pf = false;
+        if (!attr_pf) {
+            const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_LIMIT);
+            if (e != hipSuccess) return (int)e;
+            attr_pf = true;
+        }
+        const int64_t per_cu = std::min<int64_t>(2, std::max<int64_t>(1, (int64_t)(LDS_LIMIT / lds)));
+        const int64_t grid = std::min<int64_t>(n_nodes, per_cu * cu_count());
+        hipLaunchKernelGGL(kern, dim3((unsigned)std::max<int64_t>(grid, 1)), dim3(256), lds, u2gnn_stream(stream), QKV,
+                           ldq, W, dp, dO, ldo, Psave, p, seed, u2gnn_g_epoch, q_scale, dQKV, ldg, n_nodes, rows_pad);
+        return u2gnn_launch_status();
     }
     const int64_t pad_blocks = (rows_pad - n_nodes * W + W - 1) / W;
     hipLaunchKernelGGL(window_attn_bwd_kernel, dim3((unsigned)(n_nodes + pad_blocks)), dim3(256), lds,

@@ -67,6 +67,7 @@ def run(prec):
         if ext.get("clamp_a"):
             ref_a = A.clamp(min=0)
         B = torch.randn(N, Kd, device="cuda", generator=g) if tb else torch.randn(Kd, N, device="cuda", generator=g)
+        first = None
         for split, tile in cfgs:
             if prec == "fp32" and tile == 256:
                 continue
@@ -94,8 +95,14 @@ def run(prec):
                 kb = ((w[:, :, None] >> torch.arange(32, device="cuda")) & 1).reshape(M, -1).double()
                 ref = ext["aux0"].double() * (kb * ref * 2 - ext["rowvec"].double()[:, None])
             err = float("nan") if ref is None else ((C.sum(0).double() - ref).abs().max() / ref.abs().max()).item()
+            same = ""
+            if split == 1:
+                if first is None:
+                    first = C.clone()
+                else:
+                    same = f"  same bits as tile {cfgs[0][1]}: {torch.equal(C, first)}"
             print(f"{prec:7s} {name}  M={M:5d} N={N:5d} K={Kd:5d} split={split:2d} tile={tile:3d}: {us:8.1f} us "
-                  f"{2.0 * M * N * Kd / us / 1e6:7.1f} TF/s  relerr {err:.1e}")
+                  f"{2.0 * M * N * Kd / us / 1e6:7.1f} TF/s  relerr {err:.1e}{same}")
 
 
 if __name__ == "__main__":

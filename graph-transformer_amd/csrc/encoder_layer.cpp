@@ -353,6 +353,13 @@ bool dv_side_on() {
     static const bool v = env_flag("U2GNN_DV_SIDE", true);
     return v;
 }
+// The side stream starts dV only after dS is issued (dS, the largest launch, then runs alone at
+// ~92 us instead of ~110 us beside dV; dV overlaps dQ and dK): 3.059-3.080 vs 3.085-3.092 ms per
+// C4 step, one session.  U2GNN_DV_AFTER_DS=0: dV beside dS (round-1 schedule).
+bool dv_after_ds_on() {
+    static const bool v = env_flag("U2GNN_DV_AFTER_DS", true);
+    return v;
+}
 bool dk_side_on() {
     static const bool v = env_flag("U2GNN_DK_SIDE", false);
     return v;
@@ -514,7 +521,8 @@ int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
         dQKV = W.take<float>(Np * 3 * dp);
         const bool dv_side = dv_side_on() && so != st;
         const bool dk_side = dv_side && dk_side_on();
-        if (dv_side) {   // dV needs only Pd and dO: overlap it with the dS chain
+        const bool dv_late = dv_side && dv_after_ds_on();   // dV beside dQ / dK instead of beside dS
+        if (dv_side && !dv_late) {   // dV needs only Pd and dO: overlap it with the dS chain
             U2GNN_TRY(sd.fork());
             U2GNN_TRY(gemm_split(W, D, c.Pd, dO, dQKV + 2 * dp, Np, dp, Np, Np, dp, 3 * dp, true, 1.f, false, nullptr,
                                  nullptr, false, so, pd > 0.f, -1, U2GNN_ROLE_DV));
@@ -531,6 +539,13 @@ int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
             probe_mark(U2GNN_ROLE_DS, false, st, plan);
             U2GNN_TRY(gg.run(st, plan));
             probe_mark(U2GNN_ROLE_DS, true, st, plan);
+        }
+        if (dv_late) {
+            U2GNN_TRY(sd.fork());
+            U2GNN_TRY(gemm_split(W, D, c.Pd, dO, dQKV + 2 * dp, Np, dp, Np, Np, dp, 3 * dp, true, 1.f, false, nullptr,
+                                 nullptr, false, so, pd > 0.f, -1, U2GNN_ROLE_DV));
+            if (!dk_side) U2GNN_TRY(sd.mark(&dv_done));
+            U2GNN_TRY(in_part(2));
         }
         if (!dv_side) {
             U2GNN_TRY(gemm_split(W, D, c.Pd, dO, dQKV + 2 * dp, Np, dp, Np, Np, dp, 3 * dp, true, 1.f, false, nullptr,

@@ -353,11 +353,13 @@ bool dv_side_on() {
     static const bool v = env_flag("U2GNN_DV_SIDE", true);
     return v;
 }
-// The side stream starts dV only after dS is issued (dS, the largest launch, then runs alone at
-// ~92 us instead of ~110 us beside dV; dV overlaps dQ and dK): 3.059-3.080 vs 3.085-3.092 ms per
-// C4 step, one session.  U2GNN_DV_AFTER_DS=0: dV beside dS (round-1 schedule).
+// U2GNN_DV_AFTER_DS=1: the side stream starts dV only after dS is issued (dV then overlaps dQ and
+// dK): 3.059-3.080 vs 3.085-3.092 ms per C4 step, one session, but dS then often waits for CUs the
+// side stream's earlier blocks hold, so its live probe (events around the launch, 111.7 us) and the
+// rocprof kernel time (102.1 us, first wave to last) part by 9 %; off by default so that the
+// bench's dominant-kernel timing and the profile agree (110.6 vs 109.6 us).
 bool dv_after_ds_on() {
-    static const bool v = env_flag("U2GNN_DV_AFTER_DS", true);
+    static const bool v = env_flag("U2GNN_DV_AFTER_DS", false);
     return v;
 }
 bool dk_side_on() {

@@ -162,7 +162,7 @@ bool shallow_nosplit_on() {   // engine._SHALLOW_NOSPLIT
 }
 
 // engine._gemm_split: deterministic split-K into fp32 slabs + one reduce pass (alpha, accumulate,
-// padded->real block map).  deep = weight gradient (16-deep K step, <= 16 slabs).
+// padded->real block map).  deep = weight gradient (16-deep K step, <= 8 slabs).
 int gemm_split(Arena &W, const Dims &D, const float *A, const float *B, float *C, int64_t M, int64_t N, int64_t Kd,
                int64_t lda, int64_t ldb, int64_t ldc, bool ta, float alpha, bool accumulate, const int64_t *rblk,
                const int64_t *cblk, bool deep, hipStream_t st, bool clamp_a = false, int prec = -1, int role = 0) {
@@ -205,10 +205,14 @@ int gemm_split(Arena &W, const Dims &D, const float *A, const float *B, float *C
     int64_t split = target / (tiles > 0 ? tiles : 1);
     if (Kd / (4 * bk) < split) split = Kd / (4 * bk);
     if (split < 1) split = 1;
+    static const int64_t wgrad_split_max = [] {   // U2GNN_WGRAD_SPLIT_MAX (A/B): slab cap of the weight gradients
+        const char *e = std::getenv("U2GNN_WGRAD_SPLIT_MAX");
+        return e && e[0] ? (int64_t)std::atoi(e) : (int64_t)8;   // engine.WGRAD_SPLIT_MAX
+    }();
     if (deep && D.deep_wgrad && !f32 && t == 128) {
         t = 129;
         split = target / (tiles > 0 ? tiles : 1);
-        if (split > 16) split = 16;
+        if (split > wgrad_split_max) split = wgrad_split_max;
         if (split < 1) split = 1;
     }
     if (split == 1 && !mapped) {

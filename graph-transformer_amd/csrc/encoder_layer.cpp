@@ -205,10 +205,13 @@ int gemm_split(Arena &W, const Dims &D, const float *A, const float *B, float *C
     int64_t split = target / (tiles > 0 ? tiles : 1);
     if (Kd / (4 * bk) < split) split = Kd / (4 * bk);
     if (split < 1) split = 1;
-    static const int64_t wgrad_split_max = [] {   // U2GNN_WGRAD_SPLIT_MAX (A/B): slab cap of the weight gradients
+    // slab cap of the weight gradients (engine.wgrad_split_cap): 8 for node-sized depths, 16 for
+    // token-sized ones (neighbour mode, K = N(k+1) rows); U2GNN_WGRAD_SPLIT_MAX overrides (A/B)
+    static const int64_t wgrad_split_env = [] {
         const char *e = std::getenv("U2GNN_WGRAD_SPLIT_MAX");
-        return e && e[0] ? (int64_t)std::atoi(e) : (int64_t)8;   // engine.WGRAD_SPLIT_MAX
+        return e && e[0] ? (int64_t)std::atoi(e) : (int64_t)0;
     }();
+    const int64_t wgrad_split_max = wgrad_split_env > 0 ? wgrad_split_env : (Kd <= 8192 ? 8 : 16);
     if (deep && D.deep_wgrad && !f32 && t == 128) {
         t = 129;
         split = target / (tiles > 0 ? tiles : 1);

@@ -214,10 +214,15 @@ class OffPath:
 # executor reads the same variable)
 _SHALLOW_NOSPLIT = os.environ.get("U2GNN_SHALLOW_NOSPLIT", "1") != "0"
 BIG_TILE_BLOCKS = 768
-# slab cap of the deep weight-gradient products (encoder_layer.cpp reads the same variable): 8 slabs
-# move half the bytes of 16 beside the main stream; C4 3.236 / 3.238 vs 3.251 / 3.260 ms (16), 3.26 (12),
-# 3.27 (4), one session
-WGRAD_SPLIT_MAX = int(os.environ.get("U2GNN_WGRAD_SPLIT_MAX", "8"))
+# slab cap of the deep weight-gradient products (encoder_layer.cpp applies the same rule): at node-sized
+# depths 8 slabs move half the bytes of 16 beside the main stream (C4 3.236 / 3.238 vs 3.251 / 3.260 ms;
+# 12: 3.26, 4: 3.27); token-sized depths (neighbour mode, K = 82 K rows) keep 16 (8: 15.2 vs 13.9 ms).
+# U2GNN_WGRAD_SPLIT_MAX overrides.
+_WGRAD_SPLIT_ENV = int(os.environ.get("U2GNN_WGRAD_SPLIT_MAX", "0"))
+
+
+def wgrad_split_cap(kd: int) -> int:
+    return _WGRAD_SPLIT_ENV if _WGRAD_SPLIT_ENV > 0 else (8 if kd <= 8192 else 16)
 # Precision experiments: products (by role) that run plain bf16 when the layer runs bf16x3.
 # U2GNN_BF16_ROLES=qk,pv,... (tools/prec_probe.py measures each role's parity error).
 ROLES = ("in_proj", "qk", "pv", "out_proj", "ffn1", "ffn2", "ffn2_dx", "ffn2_dw", "ffn1_dx", "ffn1_dw",
@@ -267,7 +272,7 @@ def _gemm_split(A, B, C, M, N, Kd, lda, ldb, ldc, trans_a=False, trans_b=False, 
     if deep and _DEEP_WGRAD and prec != "fp32" and t == 128:
         # weight gradients (a few dozen 128x128 output tiles, K = Np): the 16-deep K step runs 3
         # blocks per CU; <= 16 slabs keeps the reduce pass short
-        t, split = 129, max(1, min(WGRAD_SPLIT_MAX, target // max(tiles, 1)))
+        t, split = 129, max(1, min(wgrad_split_cap(Kd), target // max(tiles, 1)))
     mapped = rblk is not None
     if split == 1 and not mapped:
         K.gemm(A, B, C, M, N, Kd, lda, ldb, ldc, trans_a=trans_a, trans_b=trans_b, alpha=alpha,

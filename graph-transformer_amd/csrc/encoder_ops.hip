@@ -308,6 +308,45 @@ __global__ void __launch_bounds__(256) colsum_partial_scalar_kernel(const float 
         ws[(int64_t)blockIdx.y * cols_pad + c] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
 }
 
+// Single-launch column sums for short inputs (rows <= SMALL_ROWS: the ~100-node batches of C2 / C3,
+// whose steps are latency-bound at ~5 us per launch): block = 1024 threads = 16 float4 columns x 64
+// row lanes, lane l sums rows l, l+64, ... (2 accumulators), then a fixed-order LDS tree over the 64
+// lanes (deterministic).  One block per 64 columns.  Measured slower at C5's 1920 rows (one CU per
+// 64 columns reads too slowly there), hence the bound.
+constexpr int64_t SMALL_ROWS = 512;
+
+__global__ void __launch_bounds__(1024) colsum_small_kernel(const float *X, int64_t rows, int64_t cols_pad, int64_t ld,
+                                                            int64_t cbp, int64_t cbr, float *out, int accumulate) {
+    __shared__ float4 red[64][16];
+    const int cg = threadIdx.x & 15, rl = threadIdx.x >> 4;
+    const int64_t c = ((int64_t)blockIdx.x * 16 + cg) * 4;
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 a = z4, b = z4;
+    if (c < cols_pad) {
+        int64_t r = rl;
+        for (; r + 64 < rows; r += 128) {
+            a = add4(a, ld4(X + r * ld + c));
+            b = add4(b, ld4(X + (r + 64) * ld + c));
+        }
+        if (r < rows) a = add4(a, ld4(X + r * ld + c));
+    }
+    red[rl][cg] = add4(a, b);
+#pragma unroll
+    for (int h = 32; h > 0; h >>= 1) {
+        __syncthreads();
+        if (rl < h) red[rl][cg] = add4(red[rl][cg], red[rl + h][cg]);
+    }
+    __syncthreads();
+    if (rl != 0 || c >= cols_pad) return;
+    const float t[4] = {red[0][cg].x, red[0][cg].y, red[0][cg].z, red[0][cg].w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        bool v;
+        const int64_t cc = blk_map(c + q, cbp, cbr, &v);
+        if (v) out[cc] = accumulate ? out[cc] + t[q] : t[q];
+    }
+}
+
 // stage 2: block = 16 columns x 16 chunk strides (thread t: column t%16, chunks t/16, t/16+16, ...),
 // then a fixed-order LDS combine (deterministic).  ~cols/16 blocks keep the serial chain short.
 constexpr int FIN_COLS = 16;
@@ -757,6 +796,53 @@ __global__ void __launch_bounds__(256) ln_colstats_kernel(const float *dY, int64
 
 constexpr int64_t LN_MAX_CHUNKS = 512;
 
+// single-launch LN parameter gradients for short inputs (rows <= SMALL_ROWS), the layout of
+// colsum_small_kernel with three sums (dY * xhat, dY, dZd)
+__global__ void __launch_bounds__(1024) ln_params_small_kernel(const float *dY, int64_t ldy, const float *Z, int64_t ldz,
+                                                               const float *mean, const float *rstd, const float *dZd,
+                                                               int64_t lddrop, int64_t rows, int64_t d, int64_t d_pad,
+                                                               float *dgamma, float *dbeta, float *dbias) {
+    __shared__ float4 red[3][64][16];
+    const int cg = threadIdx.x & 15, rl = threadIdx.x >> 4;
+    const int64_t c = ((int64_t)blockIdx.x * 16 + cg) * 4;
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 sg = z4, sb = z4, sd = z4;
+    if (c < d_pad) {
+        for (int64_t r = rl; r < rows; r += 64) {
+            const float4 dy = ld4(dY + r * ldy + c), zz = ld4(Z + r * ldz + c);
+            const float4 dd = dZd ? ld4(dZd + r * lddrop + c) : z4;
+            const float mu = mean[r], rs = rstd[r];
+            sg.x += dy.x * ((zz.x - mu) * rs);
+            sg.y += dy.y * ((zz.y - mu) * rs);
+            sg.z += dy.z * ((zz.z - mu) * rs);
+            sg.w += dy.w * ((zz.w - mu) * rs);
+            sb = add4(sb, dy);
+            sd = add4(sd, dd);
+        }
+    }
+    red[0][rl][cg] = sg;
+    red[1][rl][cg] = sb;
+    red[2][rl][cg] = sd;
+#pragma unroll
+    for (int h = 32; h > 0; h >>= 1) {
+        __syncthreads();
+        if (rl < h)
+#pragma unroll
+            for (int k = 0; k < 3; ++k) red[k][rl][cg] = add4(red[k][rl][cg], red[k][rl + h][cg]);
+    }
+    __syncthreads();
+    if (rl != 0) return;
+    const float4 g = red[0][0][cg], b = red[1][0][cg], e = red[2][0][cg];
+    const float gv[4] = {g.x, g.y, g.z, g.w}, bv[4] = {b.x, b.y, b.z, b.w}, ev[4] = {e.x, e.y, e.z, e.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        if (c + q >= d) break;
+        dgamma[c + q] = gv[q];
+        dbeta[c + q] = bv[q];
+        if (dbias) dbias[c + q] = ev[q];
+    }
+}
+
 // block = 16 columns x 16 chunk strides (as colsum_final), fixed-order LDS combine
 __global__ void __launch_bounds__(256) ln_param_reduce_kernel(const float *ws, int64_t n_chunks, int64_t d,
                                                               int64_t d_pad, float *dgamma, float *dbeta, float *dbias) {
@@ -834,6 +920,15 @@ inline unsigned grid_for(int64_t n, int64_t per_block, int64_t cap = 8192) {
 }  // namespace
 
 extern "C" {
+
+// U2GNN_SMALL_REDUCE=0 (A/B): short inputs also take the two-launch column reductions
+static bool small_reduce_on() {
+    static const bool v = [] {
+        const char *e = std::getenv("U2GNN_SMALL_REDUCE");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
 
 // U2GNN_GATHER_MODE=2 (A/B only): the round-1 one-wave-per-row kernel instead of the multi kernel
 static int gather_mode() {
@@ -929,6 +1024,11 @@ int u2gnn_colsum(const float *X, int64_t rows, int64_t cols_pad, int64_t ld, int
     int64_t chunks = (rows + CS_ROWS - 1) / CS_ROWS;
     hipStream_t st = u2gnn_stream(stream);
     const bool vec = al16(X) && al16(ws) && (ld & 3) == 0 && (cols_pad & 3) == 0;
+    if (vec && rows <= SMALL_ROWS && small_reduce_on()) {
+        hipLaunchKernelGGL(colsum_small_kernel, dim3((unsigned)((cols_pad + 63) / 64)), dim3(1024), 0, st, X, rows,
+                           cols_pad, ld, cblk_pad, cblk_real, out, accumulate);
+        return u2gnn_launch_status();
+    }
     const int rep = vec ? (int)std::max<int64_t>(1, (chunks + COLSUM_MAX_CHUNKS - 1) / COLSUM_MAX_CHUNKS) : 1;
     chunks = (chunks + rep - 1) / rep;   // never more than the CS_ROWS-row group count callers size ws by
     const unsigned nch = (unsigned)(chunks > 0 ? chunks : 1);
@@ -1064,6 +1164,12 @@ int u2gnn_layernorm_bwd_params(const float *dY, int64_t ldy, const float *Z, int
     const int rep = (int)((groups + LN_MAX_CHUNKS - 1) / LN_MAX_CHUNKS);
     const int64_t chunks = (groups + rep - 1) / rep;   // <= the CS_ROWS-row group count callers size ws by
     hipStream_t st = u2gnn_stream(stream);
+    if (rows_valid <= SMALL_ROWS && small_reduce_on()) {
+        hipLaunchKernelGGL(ln_params_small_kernel, dim3((unsigned)((d_pad + 63) / 64)), dim3(1024), 0, st, dY, ldy, Z,
+                           ldz, mean, rstd, dbias ? dZdrop : nullptr, lddrop, rows_valid, d, d_pad, dgamma, dbeta,
+                           dbias);
+        return u2gnn_launch_status();
+    }
     hipLaunchKernelGGL(rep > 1 ? ln_colstats_kernel<true> : ln_colstats_kernel<false>,
                        dim3((unsigned)((d_pad + 255) / 256), (unsigned)chunks), dim3(256), 0, st, dY,
                        ldy, Z, ldz, mean, rstd, dbias ? dZdrop : nullptr, lddrop, rows_valid, d, d_pad, rep, ws);

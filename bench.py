@@ -514,6 +514,7 @@ def main():
                 "frac": round(ach / peak, 4), "traffic": pmc_traffic(sym),
                 "kernel": sym, "kernel_precision": pk, "role": args.probe,
                 "timing": "live: HIP events around each launch on its own stream inside the timed region",
+                "dominance": "largest per-product device time on the critical path (DESIGN.md section 8)",
                 "launches": probe_n, "avg_launch_us": round(1e3 * probe_ms / probe_n, 1),
                 "algorithmic_flop_per_launch": round(fl / probe_n),
                 "step_tflops_per_gpu": round(step_flops / (elapsed / args.steps) / 1e12, 2)}

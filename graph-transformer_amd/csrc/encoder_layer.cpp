@@ -382,6 +382,18 @@ bool inproj_split_on() {
     return v;
 }
 
+// U2GNN_FUSED_LN=0 (A/B): the separate layernorm_fwd launch even where the GEMM tile holds whole rows
+bool fused_ln_on() {
+    static const bool v = env_flag("U2GNN_FUSED_LN", true);
+    return v;
+}
+
+void set_ln(u2gnn_gemm_args &a, const float *gamma, const float *beta, float *y, int64_t ldy, float *mean, float *rstd,
+            int64_t d, int64_t rows) {
+    a.ln_gamma = gamma, a.ln_beta = beta, a.ln_y = y, a.ln_ldy = ldy;
+    a.ln_mean = mean, a.ln_rstd = rstd, a.ln_d = d, a.ln_rows = rows, a.ln_eps = 1e-5f;
+}
+
 int layer_fwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seeds *s, const float *X, float *X2,
               Arena &CA, Arena &W, bool need_ctx, hipStream_t st) {
     const int64_t N = D.N, Np = D.Np, d = D.d, dp = D.dp, ffp = D.ffp;
@@ -423,14 +435,18 @@ int layer_fwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
         U2GNN_TRY(gemm_split(W, D, c.Pd, V, c.O, Np, dp, Np, Np, 3 * dp, dp, false, 1.f, false, nullptr, nullptr,
                              false, st, drop, -1, U2GNN_ROLE_PV));
     }
-    // a3.3 out-projection + dropout1 + residual, LayerNorm1
+    // a3.3 out-projection + dropout1 + residual, LayerNorm1 (fused into the GEMM epilogue when a
+    // 64-column tile holds whole rows: d <= 64, bf16 modes; engine.fused_ln mirrors the rule)
+    const bool fuse_ln = dp == 64 && prec != U2GNN_PREC_F32 && fused_ln_on();
     {
         G g(c.O, w->W_o, c.Z1, Np, dp, dp, dp, dp, dp, prec);
-        g.tb().epi(U2GNN_EPI_BIAS_DROP_RESID);
+        g.tb().epi(fuse_ln ? U2GNN_EPI_BIAS_DROP_RESID_LN : U2GNN_EPI_BIAS_DROP_RESID);
         g.a.bias = w->b_o, g.a.aux0 = X, g.a.ld_aux = dp, g.a.p_drop = pd, g.a.seed = s->drop1;
+        if (fuse_ln) set_ln(g.a, w->n1_w, w->n1_b, c.X1, dp, c.mean1, c.rstd1, d, N);
         U2GNN_TRY(g.run(st, plan));
     }
-    if (!plan) U2GNN_TRY(u2gnn_layernorm_fwd(c.Z1, dp, w->n1_w, w->n1_b, c.X1, dp, c.mean1, c.rstd1, N, Np, d, dp, 1e-5f, st));
+    if (!plan && !fuse_ln)
+        U2GNN_TRY(u2gnn_layernorm_fwd(c.Z1, dp, w->n1_w, w->n1_b, c.X1, dp, c.mean1, c.rstd1, N, Np, d, dp, 1e-5f, st));
     // a3.4 FFN + dropout2 + residual, LayerNorm2
     {
         G g(c.X1, w->W1, c.Hd, Np, ffp, dp, dp, dp, ffp, prec);
@@ -440,11 +456,13 @@ int layer_fwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
     }
     {
         G g(c.Hd, w->W2, c.Z2, Np, dp, ffp, ffp, ffp, dp, prec);
-        g.tb().epi(U2GNN_EPI_BIAS_DROP_RESID);
+        g.tb().epi(fuse_ln ? U2GNN_EPI_BIAS_DROP_RESID_LN : U2GNN_EPI_BIAS_DROP_RESID);
         g.a.bias = w->b2, g.a.aux0 = c.X1, g.a.ld_aux = dp, g.a.p_drop = pd, g.a.seed = s->drop2;
+        if (fuse_ln) set_ln(g.a, w->n2_w, w->n2_b, X2, dp, c.mean2, c.rstd2, d, N);
         U2GNN_TRY(g.run(st, plan));
     }
-    if (!plan) U2GNN_TRY(u2gnn_layernorm_fwd(c.Z2, dp, w->n2_w, w->n2_b, X2, dp, c.mean2, c.rstd2, N, Np, d, dp, 1e-5f, st));
+    if (!plan && !fuse_ln)
+        U2GNN_TRY(u2gnn_layernorm_fwd(c.Z2, dp, w->n2_w, w->n2_b, X2, dp, c.mean2, c.rstd2, N, Np, d, dp, 1e-5f, st));
     if ((W.overflow || CA.overflow) && debug_on())
         std::fprintf(stderr, "u2gnn: layer_fwd arena overflow (ws %lld/%lld, ctx %lld/%lld)\n", (long long)W.used,
                      (long long)W.cap, (long long)CA.used, (long long)CA.cap);

@@ -101,7 +101,8 @@ __device__ __forceinline__ void r2s(float *As, float *Bs, int tid, const float4 
 // ------------------------------------------------------------------------------------
 template <int BM, int BN, bool TA, bool TB, int EPI, bool CLAMP>
 __global__ void __launch_bounds__(256) gemm_f32_kernel(GemmP P) {
-    if constexpr (EPI == U2GNN_EPI_BIAS_DROP_RESID || EPI == U2GNN_EPI_BIAS_RELU_DROP || EPI == U2GNN_EPI_ATTN_DS_RECOMP)
+    if constexpr (EPI == U2GNN_EPI_BIAS_DROP_RESID || EPI == U2GNN_EPI_BIAS_RELU_DROP || EPI == U2GNN_EPI_ATTN_DS_RECOMP ||
+                  EPI == U2GNN_EPI_BIAS_DROP_RESID_LN)
         P.seed = u2gnn_seed(P.seed, P.epoch);   // graph replay: device-resident seed epoch
     constexpr int BK = 16;
     constexpr int WTM = BM / 2, WTN = BN / 2;
@@ -319,7 +320,8 @@ __device__ __forceinline__ bf16x8 ld_frag(const __bf16 *img, int r0, int ks, int
 
 template <int BM, int BN, int WM, int WN, int BK, bool TA, bool TB, int EPI, bool SPLIT, bool CLAMP>
 __global__ void __launch_bounds__(64 * WM * WN) gemm_bf16_kernel(GemmP P) {
-    if constexpr (EPI == U2GNN_EPI_BIAS_DROP_RESID || EPI == U2GNN_EPI_BIAS_RELU_DROP || EPI == U2GNN_EPI_ATTN_DS_RECOMP)
+    if constexpr (EPI == U2GNN_EPI_BIAS_DROP_RESID || EPI == U2GNN_EPI_BIAS_RELU_DROP || EPI == U2GNN_EPI_ATTN_DS_RECOMP ||
+                  EPI == U2GNN_EPI_BIAS_DROP_RESID_LN)
         P.seed = u2gnn_seed(P.seed, P.epoch);   // graph replay: device-resident seed epoch
     constexpr int NT = 64 * WM * WN;
     constexpr int LDK = BK + 8;
@@ -472,6 +474,12 @@ int launch_epi(const GemmP &P, int epi, int split, bool clamp_a, hipStream_t st)
         U2GNN_CASE(U2GNN_EPI_ATTN_DS)
         U2GNN_CASE(U2GNN_EPI_ATTN_DS_SIGNED)
 #undef U2GNN_CASE
+        case U2GNN_EPI_BIAS_DROP_RESID_LN:   // row-complete 64 x 64 blocks, NT, bf16 kinds only
+            if constexpr (KIND != U2GNN_PREC_F32 && BM == 64 && BN == 64 && !TA && TB)
+                launch_kernel<KIND, BM, BN, VAR, TA, TB, U2GNN_EPI_BIAS_DROP_RESID_LN>(P, grid, st);
+            else
+                return U2GNN_E_ARG;
+            break;
         default:
             return U2GNN_E_ARG;
     }
@@ -509,7 +517,7 @@ extern "C" int u2gnn_gemm(const u2gnn_gemm_args *a, void *stream) {
     if (x2 ? (!a->A2 || !a->B2) : (!a->A || !a->B)) return U2GNN_E_ARG;
     if (!a->C && !a->Cx2) return U2GNN_E_ARG;
     if (a->M <= 0 || a->N <= 0 || a->K <= 0) return U2GNN_E_ARG;
-    if (a->epilogue < 0 || a->epilogue > U2GNN_EPI_ATTN_DS_RECOMP) return U2GNN_E_ARG;
+    if (a->epilogue < 0 || a->epilogue > U2GNN_EPI_BIAS_DROP_RESID_LN) return U2GNN_E_ARG;
     if (a->epilogue == U2GNN_EPI_ATTN_DS_RECOMP && !x2) return U2GNN_E_ARG;
     const int prec = a->precision;
     if (prec != U2GNN_PREC_F32 && prec != U2GNN_PREC_BF16X3 && prec != U2GNN_PREC_BF16) return U2GNN_E_ARG;
@@ -534,9 +542,17 @@ extern "C" int u2gnn_gemm(const u2gnn_gemm_args *a, void *stream) {
         ((a->aux0 || a->aux1) && (a->ld_aux & 3)))
         return U2GNN_E_ALIGN;
     const int e = a->epilogue;
-    if ((e == U2GNN_EPI_BIAS || e == U2GNN_EPI_BIAS_DROP_RESID || e == U2GNN_EPI_BIAS_RELU_DROP) && !a->bias)
+    if ((e == U2GNN_EPI_BIAS || e == U2GNN_EPI_BIAS_DROP_RESID || e == U2GNN_EPI_BIAS_RELU_DROP ||
+         e == U2GNN_EPI_BIAS_DROP_RESID_LN) && !a->bias)
         return U2GNN_E_ARG;
-    if ((e == U2GNN_EPI_BIAS_DROP_RESID || e == U2GNN_EPI_RELU_DROP_BWD || e == U2GNN_EPI_ATTN_DS ||
+    if (e == U2GNN_EPI_BIAS_DROP_RESID_LN) {   // row-complete 64-column tiles only (the d <= 64 encoders)
+        if (x2 || prec == U2GNN_PREC_F32 || split != 1 || a->N != 64 || (a->tile != 0 && a->tile != 64) ||
+            a->trans_a || !a->trans_b || !a->aux0 || !a->ln_gamma || !a->ln_beta || !a->ln_y || !a->ln_mean ||
+            !a->ln_rstd || a->ln_d < 1 || a->ln_d > 64 || a->ln_rows < 0)
+            return U2GNN_E_ARG;
+        if (!al16(a->ln_y) || (a->ln_ldy & 3)) return U2GNN_E_ALIGN;
+    }
+    if ((e == U2GNN_EPI_BIAS_DROP_RESID || e == U2GNN_EPI_BIAS_DROP_RESID_LN || e == U2GNN_EPI_RELU_DROP_BWD || e == U2GNN_EPI_ATTN_DS ||
          e == U2GNN_EPI_ATTN_DS_SIGNED || e == U2GNN_EPI_ATTN_DS_RECOMP) && !a->aux0)
         return U2GNN_E_ARG;
     if (e == U2GNN_EPI_ATTN_DS_SIGNED && (!a->rowvec || !(a->p_drop < 1.f))) return U2GNN_E_ARG;
@@ -608,6 +624,17 @@ extern "C" int u2gnn_gemm(const u2gnn_gemm_args *a, void *stream) {
     P.rowstat = reinterpret_cast<const float2 *>(a->rowstat);
     P.m_valid = (int32_t)a->m_valid;
     P.n_valid = (int32_t)a->n_valid;
+    if (e == U2GNN_EPI_BIAS_DROP_RESID_LN) {   // N == 64: the tile rule above picked 64
+        P.ln_gamma = a->ln_gamma;
+        P.ln_beta = a->ln_beta;
+        P.ln_y = a->ln_y;
+        P.ln_ldy = a->ln_ldy;
+        P.ln_mean = a->ln_mean;
+        P.ln_rstd = a->ln_rstd;
+        P.ln_d = (int32_t)a->ln_d;
+        P.ln_rows = (int32_t)a->ln_rows;
+        P.ln_eps = a->ln_eps;
+    }
     hipStream_t st = u2gnn_stream(stream);
     if (x2 && (tile == 300 || tile == 301)) return u2gnn_gemm_x3_dispatch(a, P, tile, split, st);
     if (x2) return u2gnn_gemm_x2_dispatch(a, P, tile, split, st);

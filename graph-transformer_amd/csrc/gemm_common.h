@@ -32,6 +32,12 @@ struct GemmP {
     const float2 *rowstat;   // ATTN_DS_RECOMP: (row max, 1/row sum) of the forward softmax
     int32_t m_valid, n_valid;   // ATTN_DS_RECOMP: real rows / keys (P = 0 beyond)
     const uint64_t *epoch;      // seed epoch at launch (u2gnn_set_seed_epoch): seed ^= *epoch * golden
+    // EPI_BIAS_DROP_RESID_LN: the post-LayerNorm of the row-complete 64-column result
+    const float *ln_gamma, *ln_beta;
+    float *ln_y, *ln_mean, *ln_rstd;
+    int64_t ln_ldy;
+    int32_t ln_d, ln_rows;
+    float ln_eps;
 };
 
 namespace {
@@ -232,9 +238,85 @@ __device__ __forceinline__ void slice_from_pre(const PreDS<TN> &pre, int kh, Epi
     e.rm = e.rinv = 0.f;
 }
 
+// EPI_BIAS_DROP_RESID_LN on 64 x 64 blocks of 2 x 2 waves that cover whole 64-column rows: the
+// bias-dropout-residual result Z is stored as usual and kept in registers, then each row's LayerNorm
+// (two-pass: mean, then the mean square deviation, over the first ln_d columns) is reduced across the
+// row's two lanes (l, l ^ 32) and its two waves (LDS), and Y = (Z - mean) * rstd * gamma + beta is
+// written with the row's mean / rstd -- the separate layernorm_fwd launch of a d <= 64 encoder.
+template <int TM, int TN>
+__device__ __forceinline__ void store_tile_ln(const GemmP &P, float *C, const f32x16 (&acc)[TM][TN], int r0, int c0,
+                                              int li, int kh) {
+    static_assert(TM == 1 && TN == 1, "row-complete LayerNorm epilogue: 64 x 64 blocks of 2 x 2 waves");
+    constexpr int E = U2GNN_EPI_BIAS_DROP_RESID;
+    __shared__ float lnred[2][2][64];
+    const int row = r0 + li;
+    const int rb = (r0 & 63) + li, wn = (c0 & 63) >> 5;
+    EpiSlice<E, TN> e;
+    fetch_slice<E>(P, row, c0, kh, e);
+    float z[16];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        const int col = c0 + 8 * g + 4 * kh;
+        const float4 v = make_float4(acc[0][0][4 * g], acc[0][0][4 * g + 1], acc[0][0][4 * g + 2], acc[0][0][4 * g + 3]);
+        const float4 o = epilogue4<E>(P, row, col, v, e.a[0][g], e.b[0][g], e.kb[0][g], e.dl);
+        if (P.C) *reinterpret_cast<float4 *>(C + (int64_t)row * P.ldc + col) = o;
+        z[4 * g] = o.x, z[4 * g + 1] = o.y, z[4 * g + 2] = o.z, z[4 * g + 3] = o.w;
+    }
+    const int d = P.ln_d;
+    float gm[16], bt[16];
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int col = c0 + 8 * g + 4 * kh + c;
+            const int cc = col < d ? col : d - 1;   // unpadded [d] vectors: clamped loads
+            gm[4 * g + c] = P.ln_gamma[cc];
+            bt[4 * g + c] = P.ln_beta[cc];
+        }
+    float s = 0.f;
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) s += (c0 + 8 * g + 4 * kh + c < d) ? z[4 * g + c] : 0.f;
+    s += __shfl_xor(s, 32, 64);
+    if (kh == 0) lnred[0][wn][rb] = s;
+    __syncthreads();
+    const float mu = (lnred[0][0][rb] + lnred[0][1][rb]) / (float)d;
+    float q = 0.f;
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const float t = (c0 + 8 * g + 4 * kh + c < d) ? z[4 * g + c] - mu : 0.f;
+            q += t * t;
+        }
+    q += __shfl_xor(q, 32, 64);
+    if (kh == 0) lnred[1][wn][rb] = q;
+    __syncthreads();
+    const float rs = rsqrtf((lnred[1][0][rb] + lnred[1][1][rb]) / (float)d + P.ln_eps);
+    const bool live = row < P.ln_rows;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        const int col = c0 + 8 * g + 4 * kh;
+        float y[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+            y[c] = (live && col + c < d) ? (z[4 * g + c] - mu) * rs * gm[4 * g + c] + bt[4 * g + c] : 0.f;
+        *reinterpret_cast<float4 *>(P.ln_y + (int64_t)row * P.ln_ldy + col) = make_float4(y[0], y[1], y[2], y[3]);
+    }
+    if (kh == 0 && wn == 0) {
+        P.ln_mean[row] = live ? mu : 0.f;
+        P.ln_rstd[row] = live ? rs : 0.f;
+    }
+}
+
 template <int EPI, int TM, int TN>
 __device__ __forceinline__ void store_tile(const GemmP &P, float *C, const f32x16 (&acc)[TM][TN], int r0, int c0,
                                            int li, int kh, const PreDS<TN> *pre) {
+    if constexpr (EPI == U2GNN_EPI_BIAS_DROP_RESID_LN) {
+        store_tile_ln<TM, TN>(P, C, acc, r0, c0, li, kh);
+        return;
+    }
     if constexpr (EPI == U2GNN_EPI_ATTN_DS_SIGNED) {
         // every slice's probability image is requested before the first store (slice 0 usually
         // prefetched before the main loop): one exposed round trip per tile instead of one per slice

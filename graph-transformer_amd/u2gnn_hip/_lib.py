@@ -29,8 +29,8 @@ U2GNN_OK = 0
 ERRORS = {-1: "bad argument", -2: "misaligned pointer / leading dimension", -3: "shape not a tile multiple"}
 
 EPI_STORE, EPI_BIAS, EPI_BIAS_DROP_RESID, EPI_BIAS_RELU_DROP, EPI_RELU_DROP_BWD, EPI_ACCUM, EPI_ATTN_DS, \
-    EPI_ATTN_DS_SIGNED, EPI_ATTN_DS_RECOMP = range(9)
-ABI_VERSION = 6   # include/u2gnn_hip.h U2GNN_ABI_VERSION
+    EPI_ATTN_DS_SIGNED, EPI_ATTN_DS_RECOMP, EPI_BIAS_DROP_RESID_LN = range(10)
+ABI_VERSION = 7   # include/u2gnn_hip.h U2GNN_ABI_VERSION
 PREC_F32, PREC_BF16X3, PREC_BF16 = 0, 1, 2
 
 
@@ -56,6 +56,10 @@ class GemmArgs(ctypes.Structure):
         ("a_x2", c_int32), ("b_x2", c_int32),
         ("A2", c_void_p), ("B2", c_void_p), ("Cx2", c_void_p), ("ldcx2", c_int64),
         ("rowstat", c_void_p), ("m_valid", c_int64), ("n_valid", c_int64),
+        # ABI v7: LayerNorm fused into the bias-dropout-residual epilogue
+        ("ln_gamma", c_void_p), ("ln_beta", c_void_p), ("ln_y", c_void_p), ("ln_ldy", c_int64),
+        ("ln_mean", c_void_p), ("ln_rstd", c_void_p), ("ln_d", c_int64), ("ln_rows", c_int64),
+        ("ln_eps", c_float), ("ln_reserved", c_int32),
     ]
 
 

@@ -182,6 +182,17 @@ def side_stream(dev: torch.device) -> "torch.cuda.Stream":
 SIDE_MIN_ELEMS = int(os.environ.get("U2GNN_SIDE_MIN_ELEMS", str(1 << 20)))
 
 
+# U2GNN_FUSED_LN=0 (A/B): the separate layernorm_fwd launch even where the GEMM tile holds whole rows
+# (encoder_layer.cpp applies the same rule)
+_FUSED_LN = os.environ.get("U2GNN_FUSED_LN", "1") != "0"
+
+
+def fused_ln(dp: int, prec: str) -> bool:
+    """LayerNorm forward inside the bias-dropout-residual GEMM epilogue: d <= 64 (one 64-column tile
+    per row), matrix-core precisions."""
+    return _FUSED_LN and dp == 64 and prec != "fp32"
+
+
 def side_stream_pays(dims: "Dims") -> bool:
     return dims.Np * dims.dp >= SIDE_MIN_ELEMS
 
@@ -330,22 +341,29 @@ def encoder_layer_forward(X: torch.Tensor, w: PackedLayer, p: LayerParams, dims:
     O = torch.empty(Np, dp, device=dev, dtype=f32)
     _gemm_nodes_k(Pd, V, O, Np, dp, Np, Np, 3 * dp, dp, prec=_rp("pv", prec), flops=att, clamp_a=pd > 0)
     Z1 = torch.empty(Np, dp, device=dev, dtype=f32)
-    K.gemm(O, w.W_o, Z1, Np, dp, dp, dp, dp, dp, trans_b=True, epilogue=E.EPI_BIAS_DROP_RESID, bias=w.b_o,
-           aux0=X, ld_aux=dp, p_drop=pd, seed=seeds.get(SITE_DROP1, 0), precision=_rp("out_proj", prec), flops=2.0 * N * d * d)
     X1 = torch.empty(Np, dp, device=dev, dtype=f32)
     mean1 = torch.empty(Np, device=dev, dtype=f32)
     rstd1 = torch.empty(Np, device=dev, dtype=f32)
-    K.layernorm_fwd(Z1, dp, p.n1_w, p.n1_b, X1, dp, mean1, rstd1, N, Np, d, dp)
+    fuse = fused_ln(dp, prec)   # LayerNorm in the GEMM epilogue when a 64-column tile holds whole rows
+    K.gemm(O, w.W_o, Z1, Np, dp, dp, dp, dp, dp, trans_b=True,
+           epilogue=E.EPI_BIAS_DROP_RESID_LN if fuse else E.EPI_BIAS_DROP_RESID, bias=w.b_o,
+           aux0=X, ld_aux=dp, p_drop=pd, seed=seeds.get(SITE_DROP1, 0), precision=_rp("out_proj", prec),
+           flops=2.0 * N * d * d, ln=(p.n1_w, p.n1_b, X1, dp, mean1, rstd1, d, N, 1e-5) if fuse else None)
+    if not fuse:
+        K.layernorm_fwd(Z1, dp, p.n1_w, p.n1_b, X1, dp, mean1, rstd1, N, Np, d, dp)
     Hd = torch.empty(Np, ffp, device=dev, dtype=f32)
     K.gemm(X1, w.W1, Hd, Np, ffp, dp, dp, dp, ffp, trans_b=True, epilogue=E.EPI_BIAS_RELU_DROP, bias=w.b1,
            p_drop=pd, seed=seeds.get(SITE_DROPFF, 0), precision=_rp("ffn1", prec), flops=2.0 * N * d * ff)
     Z2 = torch.empty(Np, dp, device=dev, dtype=f32)
-    K.gemm(Hd, w.W2, Z2, Np, dp, ffp, ffp, ffp, dp, trans_b=True, epilogue=E.EPI_BIAS_DROP_RESID, bias=w.b2,
-           aux0=X1, ld_aux=dp, p_drop=pd, seed=seeds.get(SITE_DROP2, 0), precision=_rp("ffn2", prec), flops=2.0 * N * d * ff)
     X2 = torch.empty(Np, dp, device=dev, dtype=f32)
     mean2 = torch.empty(Np, device=dev, dtype=f32)
     rstd2 = torch.empty(Np, device=dev, dtype=f32)
-    K.layernorm_fwd(Z2, dp, p.n2_w, p.n2_b, X2, dp, mean2, rstd2, N, Np, d, dp)
+    K.gemm(Hd, w.W2, Z2, Np, dp, ffp, ffp, ffp, dp, trans_b=True,
+           epilogue=E.EPI_BIAS_DROP_RESID_LN if fuse else E.EPI_BIAS_DROP_RESID, bias=w.b2,
+           aux0=X1, ld_aux=dp, p_drop=pd, seed=seeds.get(SITE_DROP2, 0), precision=_rp("ffn2", prec),
+           flops=2.0 * N * d * ff, ln=(p.n2_w, p.n2_b, X2, dp, mean2, rstd2, d, N, 1e-5) if fuse else None)
+    if not fuse:
+        K.layernorm_fwd(Z2, dp, p.n2_w, p.n2_b, X2, dp, mean2, rstd2, N, Np, d, dp)
     ctx = None
     if need_ctx:
         ctx = EncoderLayerCtx()

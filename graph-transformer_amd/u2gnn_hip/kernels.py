@@ -72,14 +72,15 @@ def gemm_symbol(precision, M, N, split_k, tile, trans_a, trans_b, epilogue, clam
 def gemm(A, B, C, M, N, K, lda, ldb, ldc, trans_a=False, trans_b=False, epilogue=_lib.EPI_STORE, split_k=1,
          slab_stride=0, bias=None, aux0=None, aux1=None, rowvec=None, ld_aux=0, alpha=1.0, scale_cols=0, p_drop=0.0,
          seed=0, precision="fp32", tile=0, flops=None, keep=None, clamp_a=False, Cx2=None, ldcx2=0, rowstat=None,
-         m_valid=0, n_valid=0):
+         m_valid=0, n_valid=0, ln=None):
     """C[M,N] (epilogue) sum_k A(m,k) B(k,n).  A/B/C may be views (pointer arithmetic via
     storage offsets is done by torch's data_ptr()).  ``flops``: algorithmic FLOPs of the
     launch for the roofline recorder (None = not recorded).  ``clamp_a``: A elements below +0 are read
     as 0 (the signed probability image of attn_softmax_fwd(P=None) consumed as Pd).
     x2 operands (include/u2gnn_hip.h): A and B given as bfloat16 tensors are pre-split [rows][2*cols]
     matrices (lda / ldb in bf16 elements); ``Cx2`` (bfloat16) receives the result in x2 format, C may
-    then be None.  ``rowstat``/``m_valid``/``n_valid``: the ATTN_DS_RECOMP epilogue."""
+    then be None.  ``rowstat``/``m_valid``/``n_valid``: the ATTN_DS_RECOMP epilogue.  ``ln`` =
+    (gamma, beta, Y, ldy, mean, rstd, d, rows, eps): the EPI_BIAS_DROP_RESID_LN LayerNorm (N == 64)."""
     _dev(A, B, C, Cx2, rowstat)
     x2 = A.dtype == torch.bfloat16
     if x2 != (B.dtype == torch.bfloat16):
@@ -120,6 +121,12 @@ def gemm(A, B, C, M, N, K, lda, ldb, ldc, trans_a=False, trans_b=False, epilogue
         _dev(keep)
         a.keep, a.ld_keep = keep.data_ptr(), keep.stride(0)
     a.clamp_a = int(bool(clamp_a))
+    if ln is not None:
+        gam, bet, Y, ldy, mean, rstd, d_real, rows, eps = ln
+        _dev(gam, bet, Y, mean, rstd)
+        a.ln_gamma, a.ln_beta, a.ln_y, a.ln_ldy = gam.data_ptr(), bet.data_ptr(), Y.data_ptr(), int(ldy)
+        a.ln_mean, a.ln_rstd = mean.data_ptr(), rstd.data_ptr()
+        a.ln_d, a.ln_rows, a.ln_eps = int(d_real), int(rows), float(eps)
     check(hip_lib().u2gnn_gemm(ctypes.byref(a), _s()), "u2gnn_gemm")
     if rec:
         ev1.record()

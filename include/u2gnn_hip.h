@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define U2GNN_ABI_VERSION 6
+#define U2GNN_ABI_VERSION 7
 
 #define U2GNN_OK 0
 #define U2GNN_E_ARG (-1)    /* bad size / null pointer */
@@ -53,6 +53,11 @@ extern "C" {
                                        u2gnn_attn_softmax_x2_fwd: P = exp(S - max) * (1/sum) (0 for
                                        m >= m_valid or n >= n_valid), keep = dropout hash (seed, m, n);
                                        C = P * (keep * acc/(1-p) - rowvec[m]) */
+#define U2GNN_EPI_BIAS_DROP_RESID_LN 9 /* ABI v7: C = Z = aux0 + drop(acc + bias) as BIAS_DROP_RESID, and ln_y = the
+                                          post-LayerNorm of Z's first ln_d columns (ln_gamma, ln_beta, ln_eps;
+                                          ln_mean / ln_rstd per row; rows >= ln_rows and columns >= ln_d
+                                          written as 0).  Row-complete tiles only: N == 64 (tile 64),
+                                          bf16 / bf16x3, split_k 1 -- the d <= 64 encoders (C3, C5) */
 
 /* x2 operand format (pre-split fp32): a logical fp32 matrix X[R][C] (C % 8 == 0) is stored as
  * bf16 X2[R][2C] with, per 8-column group g, hi(X[r][8g..8g+7]) then lo(X[r][8g..8g+7]),
@@ -108,6 +113,14 @@ typedef struct u2gnn_gemm_args {
     int64_t ldcx2;
     const float *rowstat; /* ATTN_DS_RECOMP: [M][2] (row max, 1/row sum) */
     int64_t m_valid, n_valid;   /* ATTN_DS_RECOMP: real rows / keys */
+    /* ---- ABI v7: LayerNorm fused into the bias-dropout-residual epilogue (EPI_BIAS_DROP_RESID_LN) ---- */
+    const float *ln_gamma, *ln_beta;   /* [ln_d], any 4-byte alignment */
+    float *ln_y;                       /* [M][ln_ldy], 16-byte aligned rows */
+    int64_t ln_ldy;
+    float *ln_mean, *ln_rstd;          /* [M] */
+    int64_t ln_d, ln_rows;
+    float ln_eps;
+    int32_t ln_reserved;
 } u2gnn_gemm_args;
 
 /* ---- library ------------------------------------------------------------------ */

@@ -292,6 +292,36 @@ def test_layernorm_fwd_bwd(d, dp):
     assert dZ[N:].abs().max().item() == 0 and dZ[:, d:].abs().max().item() == 0
 
 
+@pytest.mark.parametrize("d,K_,p", [(19, 64, 0.0), (19, 1024, 0.5), (64, 64, 0.5), (4, 64, 0.0)])
+@pytest.mark.parametrize("prec", ["bf16x3", "bf16"])
+def test_bias_drop_resid_layernorm_epilogue(d, K_, p, prec):
+    """EPI_BIAS_DROP_RESID_LN (d <= 64, one 64-column tile per row): Z is bit-identical to the
+    BIAS_DROP_RESID epilogue, Y / mean / rstd match layernorm_fwd on that Z (fp32, 1e-5), rows past
+    ln_rows and columns past d are zero."""
+    Np, N, dp = 320, 300, 64
+    A = _mk(Np, K_, seed=41)
+    W = _mk(dp, K_, seed=42) * 0.1
+    bias = _mk(dp, seed=43)
+    X = _mk(Np, dp, seed=44)
+    gam, bet = _mk(d, seed=45), _mk(d, seed=46)
+    Z_ref = torch.empty(Np, dp, device=DEV)
+    K.gemm(A, W, Z_ref, Np, dp, K_, K_, K_, dp, trans_b=True, epilogue=_lib.EPI_BIAS_DROP_RESID, bias=bias, aux0=X,
+           ld_aux=dp, p_drop=p, seed=5, precision=prec)
+    Z = torch.full((Np, dp), float("nan"), device=DEV)
+    Y = torch.full((Np, dp), float("nan"), device=DEV)
+    mu, rs = torch.full((Np,), float("nan"), device=DEV), torch.full((Np,), float("nan"), device=DEV)
+    K.gemm(A, W, Z, Np, dp, K_, K_, K_, dp, trans_b=True, epilogue=_lib.EPI_BIAS_DROP_RESID_LN, bias=bias, aux0=X,
+           ld_aux=dp, p_drop=p, seed=5, precision=prec, ln=(gam, bet, Y, dp, mu, rs, d, N, 1e-5))
+    assert torch.equal(Z, Z_ref)
+    Y_ref = torch.empty(Np, dp, device=DEV)
+    mu_ref, rs_ref = torch.empty(Np, device=DEV), torch.empty(Np, device=DEV)
+    K.layernorm_fwd(Z_ref, dp, gam, bet, Y_ref, dp, mu_ref, rs_ref, N, Np, d, dp)
+    assert rel_err(Y, Y_ref) < 1e-5
+    assert rel_err(mu, mu_ref) < 1e-5 and rel_err(rs, rs_ref) < 1e-5
+    assert Y[N:].abs().max().item() == 0 and (d == dp or Y[:, d:].abs().max().item() == 0)
+    assert mu[N:].abs().max().item() == 0 and rs[N:].abs().max().item() == 0
+
+
 def test_gather_pack_colsum():
     src = _mk(50, 7, seed=15)
     idx = torch.randint(0, 50, (30, 5), device=DEV)

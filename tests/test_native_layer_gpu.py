@@ -24,7 +24,7 @@ def _zeros_like_params(p: LayerParams) -> LayerParams:
     return LayerParams(*[torch.full_like(t, float("nan")) for t in p.tensors()])
 
 
-@pytest.mark.parametrize("N,d,ff", [(300, 67, 128), (1000, 367, 1024)])
+@pytest.mark.parametrize("N,d,ff", [(300, 67, 128), (1000, 367, 1024), (300, 19, 128)])   # d = 19: fused LN
 @pytest.mark.parametrize("prec", ["bf16x3", "fp32", "mixed"])
 @pytest.mark.parametrize("train", [True, False])
 @pytest.mark.parametrize("side", [False, True])

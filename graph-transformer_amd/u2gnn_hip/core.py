@@ -10,6 +10,7 @@
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 from typing import List, Optional
 
@@ -24,6 +25,18 @@ from .engine import (SITE_ATTN, SITE_DROP1, SITE_DROP2, SITE_DROPFF, SITE_HEAD, 
 
 
 _IOTA = {}
+
+
+# U2GNN_COPY_STREAM=0 (A/B): DeviceBatch.from_store's transfers on the compute stream
+_COPY_STREAM = os.environ.get("U2GNN_COPY_STREAM", "1") != "0"
+_COPY: dict = {}
+
+
+def _copy_stream(dev: torch.device) -> "torch.cuda.Stream":
+    s = _COPY.get(dev.index)
+    if s is None:
+        s = _COPY[dev.index] = torch.cuda.Stream(device=dev)
+    return s
 
 
 def _pool_iota(N: int, dev: torch.device):
@@ -92,6 +105,31 @@ class DeviceBatch:
         N, B = int(hb.offsets[-1]), len(hb.offsets) - 1
         slot = getattr(hb, "pinned", None)
         _check_range_host(hb.input_x, N)
+        if slot is not None and _COPY_STREAM and dev.type == "cuda":
+            # the batch's transfers and its feature gather run on a copy stream, so the next batch
+            # crosses PCIe while the current step computes; the compute stream waits on one event
+            main = torch.cuda.current_stream(dev)
+            cs = _copy_stream(dev)
+            k1 = hb.input_x.shape[1]
+            with torch.cuda.stream(cs):
+                h2d = lambda t: t.to(dev, non_blocking=True)  # noqa: E731
+                ix = h2d(slot.ix[:N * k1]).view(N, k1)
+                gnode, off, lab = h2d(slot.gnode[:N]), h2d(slot.offsets[:B + 1]), h2d(slot.labels[:B])
+                slot.event = torch.cuda.Event()
+                slot.event.record()
+                d = X_dev.shape[1]
+                X = torch.empty(N, d, device=dev, dtype=torch.float32)
+                if N:
+                    K.gather_rows(X_dev, gnode, 1, X, N, N, d, d)
+                err = torch.zeros(1, device=dev, dtype=torch.int32)
+            ready = torch.cuda.Event()
+            ready.record(cs)
+            main.wait_event(ready)
+            for t in (ix, gnode, off, lab, X, err):   # allocated on the copy stream, used on the compute one
+                t.record_stream(main)
+            iy = gnode if hb.input_y is not None else None
+            colidx, vals = _pool_iota(N, dev)
+            return DeviceBatch(N, B, ix, X, off, colidx, vals, lab, iy, err)
         if slot is not None:
             k1 = hb.input_x.shape[1]
             h2d = lambda t: t.to(dev, non_blocking=True)  # noqa: E731

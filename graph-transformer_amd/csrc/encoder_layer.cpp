@@ -388,6 +388,15 @@ bool fused_ln_on() {
     return v;
 }
 
+// U2GNN_ROWDOT_FUSE=1 (A/B, opt-in): delta = rowsum(dO * O) from the dO GEMM's STORE_ROWDOT epilogue
+// (per-64-column partials that the dS epilogue sums) instead of its own u2gnn_rowdot launch.  Measured
+// slower on C4 (2 sessions x 3 reps: 3.33 vs 3.29 and 3.376 vs 3.363 ms per step; rocprof: rowdot
+// 7.2 us saved, dO GEMM +1.9 us, dS +6.8 us from its 6 extra partial loads per row and slice)
+bool rowdot_fuse_on() {
+    static const bool v = env_flag("U2GNN_ROWDOT_FUSE", false);
+    return v;
+}
+
 void set_ln(u2gnn_gemm_args &a, const float *gamma, const float *beta, float *y, int64_t ldy, float *mean, float *rstd,
             int64_t d, int64_t rows) {
     a.ln_gamma = gamma, a.ln_beta = beta, a.ln_y = y, a.ln_ldy = ldy;
@@ -520,8 +529,16 @@ int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
                                              g->n1_b, g->out_b, so));
     // out-projection
     float *dO = W.take<float>(Np * dp);
+    // delta = rowsum(dO * O) of the attention backward: partial sums per 32 columns from the dO GEMM's
+    // epilogue (node attention), summed in group order by the dS epilogue
+    const bool fuse_rowdot = !D.window && rowdot_fuse_on();
+    float *delta_parts = fuse_rowdot ? W.take<float>((dp / 64) * Np) : nullptr;
     {
         G gg(dA, w->W_o, dO, Np, dp, dp, dp, dp, dp, prec);
+        if (fuse_rowdot) {
+            gg.epi(U2GNN_EPI_STORE_ROWDOT);
+            gg.a.aux0 = c.O, gg.a.ld_aux = dp, gg.a.rowpart = delta_parts, gg.a.ld_rowpart = Np;
+        }
         U2GNN_TRY(gg.run(st, plan));
     }
     U2GNN_TRY(wgrad(W, D, dA, dp, c.O, dp, dp, dp, g->out_w, d, blk_d, blk_d, so));   // side (forked above)
@@ -556,13 +573,14 @@ int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
             if (!dk_side) U2GNN_TRY(sd.mark(&dv_done));
             U2GNN_TRY(in_part(2));
         }
-        float *delta = W.take<float>(Np);
-        if (!plan) U2GNN_TRY(u2gnn_rowdot(dO, dp, c.O, dp, delta, Np, dp, st));
+        float *delta = fuse_rowdot ? delta_parts : W.take<float>(Np);
+        if (!plan && !fuse_rowdot) U2GNN_TRY(u2gnn_rowdot(dO, dp, c.O, dp, delta, Np, dp, st));
         float *dS = W.take<float>(Np * Np);
         {
             G gg(dO, V, dS, Np, Np, dp, dp, 3 * dp, Np, D.prec_ab);
             gg.tb().epi(U2GNN_EPI_ATTN_DS_SIGNED);
             gg.a.aux0 = c.Pd, gg.a.rowvec = delta, gg.a.ld_aux = Np, gg.a.p_drop = pd;
+            if (fuse_rowdot) gg.a.rowvec_parts = (int32_t)(dp / 64), gg.a.ld_rowvec = Np;
             probe_mark(U2GNN_ROLE_DS, false, st, plan);
             U2GNN_TRY(gg.run(st, plan));
             probe_mark(U2GNN_ROLE_DS, true, st, plan);

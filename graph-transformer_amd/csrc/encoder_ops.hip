@@ -247,7 +247,37 @@ struct PackBatch {
     u2gnn_pack_desc d[PACK_MAX];
 };
 
+// Many padded-copy jobs in one launch: blockIdx.y = job, blockIdx.x = a group of PACK_RB rows, each
+// thread one column per 256 (the column map computed once per column, the row map once per row, in
+// 32-bit arithmetic: the first version's two 64-bit divisions per element held the C4 launch at 26 us
+// for 42 MB).  Jobs whose extents do not fit 32 bits use pack_multi64_kernel.
+constexpr uint32_t PACK_RB = 8;
+
 __global__ void __launch_bounds__(256) pack_multi_kernel(PackBatch pb) {
+    const u2gnn_pack_desc &D = pb.d[blockIdx.y];
+    const uint32_t rows = (uint32_t)D.rows_pad, cols = (uint32_t)D.cols_pad;
+    const uint32_t r0 = blockIdx.x * PACK_RB;
+    if (r0 >= rows) return;
+    const uint32_t rbp = (uint32_t)D.rblk_pad, rbr = (uint32_t)D.rblk_real;
+    const uint32_t cbp = (uint32_t)D.cblk_pad, cbr = (uint32_t)D.cblk_real;
+    const uint32_t nr = min(PACK_RB, rows - r0);
+    for (uint32_t c = threadIdx.x; c < cols; c += 256) {
+        const uint32_t cb = c / cbp, ci = c - cb * cbp;
+        const bool vc = ci < cbr;
+        const uint32_t cc = cb * cbr + ci;
+        float v[PACK_RB];
+#pragma unroll
+        for (uint32_t k = 0; k < PACK_RB; ++k) {   // every row's load in flight before the stores
+            const uint32_t r = r0 + k, rb = r / rbp, ri = r - rb * rbp;
+            v[k] = (k < nr && vc && ri < rbr) ? D.src[(int64_t)(rb * rbr + ri) * D.ld_src + cc] : 0.f;
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < PACK_RB; ++k)
+            if (k < nr) D.dst[(int64_t)(r0 + k) * D.ld_dst + c] = v[k];
+    }
+}
+
+__global__ void __launch_bounds__(256) pack_multi64_kernel(PackBatch pb) {
     const u2gnn_pack_desc &D = pb.d[blockIdx.y];
     const int64_t total = D.rows_pad * D.cols_pad;
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
@@ -1005,14 +1035,26 @@ int u2gnn_pack_padded_multi(const u2gnn_pack_desc *descs, int32_t n, void *strea
     for (int32_t o = 0; o < n; o += PACK_MAX) {
         PackBatch pb;
         const int32_t m = n - o < PACK_MAX ? n - o : PACK_MAX;
-        int64_t biggest = 1;
+        int64_t biggest = 1, max_rows = 1;
+        bool fits32 = true;
         for (int32_t i = 0; i < m; ++i) {
             pb.d[i] = descs[o + i];
-            if (!pb.d[i].src || !pb.d[i].dst || pb.d[i].rblk_pad < 1 || pb.d[i].cblk_pad < 1) return U2GNN_E_ARG;
-            biggest = std::max<int64_t>(biggest, pb.d[i].rows_pad * pb.d[i].cols_pad);
+            const u2gnn_pack_desc &d = pb.d[i];
+            if (!d.src || !d.dst || d.rblk_pad < 1 || d.cblk_pad < 1 || d.rows_pad < 0 || d.cols_pad < 0)
+                return U2GNN_E_ARG;
+            biggest = std::max<int64_t>(biggest, d.rows_pad * d.cols_pad);
+            max_rows = std::max<int64_t>(max_rows, d.rows_pad);
+            // 32-bit maps: padded extents, and the real row / column indices they map to
+            const int64_t lim = (int64_t)1 << 31;
+            fits32 = fits32 && d.rows_pad + d.rblk_pad < lim && d.cols_pad + d.cblk_pad < lim &&
+                     d.rblk_real < lim && d.cblk_real < lim;
         }
-        hipLaunchKernelGGL(pack_multi_kernel, dim3(grid_for(biggest, 256, 2048), (unsigned)m), dim3(256), 0,
-                           u2gnn_stream(stream), pb);
+        if (fits32)
+            hipLaunchKernelGGL(pack_multi_kernel, dim3((unsigned)((max_rows + PACK_RB - 1) / PACK_RB), (unsigned)m),
+                               dim3(256), 0, u2gnn_stream(stream), pb);
+        else
+            hipLaunchKernelGGL(pack_multi64_kernel, dim3(grid_for(biggest, 256, 2048), (unsigned)m), dim3(256), 0,
+                               u2gnn_stream(stream), pb);
     }
     return u2gnn_launch_status();
 }

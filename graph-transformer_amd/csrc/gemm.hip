@@ -473,6 +473,7 @@ int launch_epi(const GemmP &P, int epi, int split, bool clamp_a, hipStream_t st)
         U2GNN_CASE(U2GNN_EPI_ACCUM)
         U2GNN_CASE(U2GNN_EPI_ATTN_DS)
         U2GNN_CASE(U2GNN_EPI_ATTN_DS_SIGNED)
+        U2GNN_CASE(U2GNN_EPI_STORE_ROWDOT)
 #undef U2GNN_CASE
         case U2GNN_EPI_BIAS_DROP_RESID_LN:   // row-complete 64 x 64 blocks, NT, bf16 kinds only
             if constexpr (KIND != U2GNN_PREC_F32 && BM == 64 && BN == 64 && !TA && TB)
@@ -517,7 +518,7 @@ extern "C" int u2gnn_gemm(const u2gnn_gemm_args *a, void *stream) {
     if (x2 ? (!a->A2 || !a->B2) : (!a->A || !a->B)) return U2GNN_E_ARG;
     if (!a->C && !a->Cx2) return U2GNN_E_ARG;
     if (a->M <= 0 || a->N <= 0 || a->K <= 0) return U2GNN_E_ARG;
-    if (a->epilogue < 0 || a->epilogue > U2GNN_EPI_BIAS_DROP_RESID_LN) return U2GNN_E_ARG;
+    if (a->epilogue < 0 || a->epilogue > U2GNN_EPI_STORE_ROWDOT) return U2GNN_E_ARG;
     if (a->epilogue == U2GNN_EPI_ATTN_DS_RECOMP && !x2) return U2GNN_E_ARG;
     const int prec = a->precision;
     if (prec != U2GNN_PREC_F32 && prec != U2GNN_PREC_BF16X3 && prec != U2GNN_PREC_BF16) return U2GNN_E_ARG;
@@ -552,10 +553,15 @@ extern "C" int u2gnn_gemm(const u2gnn_gemm_args *a, void *stream) {
             return U2GNN_E_ARG;
         if (!al16(a->ln_y) || (a->ln_ldy & 3)) return U2GNN_E_ALIGN;
     }
-    if ((e == U2GNN_EPI_BIAS_DROP_RESID || e == U2GNN_EPI_BIAS_DROP_RESID_LN || e == U2GNN_EPI_RELU_DROP_BWD || e == U2GNN_EPI_ATTN_DS ||
+    if ((e == U2GNN_EPI_BIAS_DROP_RESID || e == U2GNN_EPI_BIAS_DROP_RESID_LN || e == U2GNN_EPI_RELU_DROP_BWD ||
+         e == U2GNN_EPI_STORE_ROWDOT || e == U2GNN_EPI_ATTN_DS ||
          e == U2GNN_EPI_ATTN_DS_SIGNED || e == U2GNN_EPI_ATTN_DS_RECOMP) && !a->aux0)
         return U2GNN_E_ARG;
     if (e == U2GNN_EPI_ATTN_DS_SIGNED && (!a->rowvec || !(a->p_drop < 1.f))) return U2GNN_E_ARG;
+    if (a->rowvec_parts > 1 && (e != U2GNN_EPI_ATTN_DS_SIGNED || x2 || a->ld_rowvec < a->M)) return U2GNN_E_ARG;
+    if (e == U2GNN_EPI_STORE_ROWDOT &&
+        (x2 || split != 1 || a->Cx2 || !a->aux0 || !a->rowpart || a->ld_rowpart < a->M || (a->N & 63)))
+        return U2GNN_E_ARG;
     if (e == U2GNN_EPI_ATTN_DS_RECOMP && (!a->rowvec || !a->rowstat || !(a->p_drop < 1.f) ||
                                           ((uintptr_t)a->rowstat & 7)))
         return U2GNN_E_ARG;
@@ -624,6 +630,10 @@ extern "C" int u2gnn_gemm(const u2gnn_gemm_args *a, void *stream) {
     P.rowstat = reinterpret_cast<const float2 *>(a->rowstat);
     P.m_valid = (int32_t)a->m_valid;
     P.n_valid = (int32_t)a->n_valid;
+    P.rowpart = a->rowpart;
+    P.ld_rowpart = a->ld_rowpart;
+    P.rowvec_parts = a->rowvec_parts;
+    P.ld_rowvec = a->ld_rowvec;
     if (e == U2GNN_EPI_BIAS_DROP_RESID_LN) {   // N == 64: the tile rule above picked 64
         P.ln_gamma = a->ln_gamma;
         P.ln_beta = a->ln_beta;

@@ -38,6 +38,11 @@ struct GemmP {
     int64_t ln_ldy;
     int32_t ln_d, ln_rows;
     float ln_eps;
+    // EPI_STORE_ROWDOT: per-32-column-group row partials of C*aux0; ATTN_DS_SIGNED: rowvec_parts of them
+    float *rowpart;
+    int64_t ld_rowpart;
+    int32_t rowvec_parts;
+    int64_t ld_rowvec;
 };
 
 namespace {
@@ -68,9 +73,9 @@ __device__ __forceinline__ void epi_fetch(const GemmP &P, int row, int col, floa
             b = ld4(P.aux1 + o);
     } else if constexpr (EPI == U2GNN_EPI_ACCUM) {
         a = ld4(P.C + (int64_t)row * P.ldc + col);
-    } else if constexpr (EPI == U2GNN_EPI_RELU_DROP_BWD) {
+    } else if constexpr (EPI == U2GNN_EPI_RELU_DROP_BWD || EPI == U2GNN_EPI_STORE_ROWDOT) {
         a = ld4(P.aux0 + (int64_t)row * P.ld_aux + col);
-    } else if constexpr (EPI != U2GNN_EPI_STORE) {
+    } else if constexpr (EPI != U2GNN_EPI_STORE) {   // bias epilogues
         a = ld4(P.bias + col);
         if constexpr (EPI == U2GNN_EPI_BIAS_DROP_RESID) b = ld4(P.aux0 + (int64_t)row * P.ld_aux + col);
     }
@@ -80,7 +85,7 @@ __device__ __forceinline__ void epi_fetch(const GemmP &P, int row, int col, floa
 template <int EPI>
 __device__ __forceinline__ float4 epilogue4(const GemmP &P, int row, int col, float4 v, float4 a, float4 b,
                                             uint32_t kb, float dl) {
-    if constexpr (EPI == U2GNN_EPI_STORE) {
+    if constexpr (EPI == U2GNN_EPI_STORE || EPI == U2GNN_EPI_STORE_ROWDOT) {
         return make_float4(P.alpha * v.x, P.alpha * v.y, P.alpha * v.z, P.alpha * v.w);
     } else if constexpr (EPI == U2GNN_EPI_ATTN_DS_SIGNED) {
         // x = Pd = P/(1-p) where kept (sign clear), x = -P where dropped (sign set):
@@ -132,6 +137,34 @@ __device__ __forceinline__ float4 epilogue4(const GemmP &P, int row, int col, fl
     }
 }
 
+// The attention backward's delta of one row: rowvec[row], or (ABI v8) the sum of the dO GEMM's
+// STORE_ROWDOT partials (one per 64 columns) in group order -- one fixed order, so the native and
+// Python paths agree.  The partials are loaded into registers with the other epilogue operands and
+// summed only when the slice is stored: summing at load time would make the wave wait for every load
+// issued before them (the dS kernel prefetches slice 0's P tile ahead of its main loop).
+constexpr int DELTA_REGS = 8;
+struct DeltaParts {
+    float v[DELTA_REGS];
+};
+__device__ __forceinline__ void delta_load(const GemmP &P, int row, DeltaParts &d) {
+    if (P.rowvec_parts <= 1) {
+        d.v[0] = P.rowvec[row];
+        return;
+    }
+#pragma unroll
+    for (int q = 0; q < DELTA_REGS; ++q)
+        d.v[q] = q < P.rowvec_parts ? P.rowvec[(int64_t)q * P.ld_rowvec + row] : 0.f;
+}
+__device__ __forceinline__ float delta_sum(const GemmP &P, int row, const DeltaParts &d) {
+    if (P.rowvec_parts <= 1) return d.v[0];
+    float s = 0.f;
+#pragma unroll
+    for (int q = 0; q < DELTA_REGS; ++q)
+        if (q < P.rowvec_parts) s += d.v[q];
+    for (int q = DELTA_REGS; q < P.rowvec_parts; ++q) s += P.rowvec[(int64_t)q * P.ld_rowvec + row];
+    return s;
+}
+
 // lane (li, kh) of MFMA tile (i, j) holds C[row = li][cols 8g + 4kh .. +3] in acc[i][j][4g .. 4g+3].
 // One 32-row slice (fixed i) of a wave's tile: its auxiliary operands, then its stores.
 template <int EPI, int TN>
@@ -139,6 +172,7 @@ struct EpiSlice {
     float4 a[TN][4], b[TN][4];
     uint32_t kb[TN][4];
     float dl;
+    DeltaParts dp;    // ATTN_DS_SIGNED: dl = delta_sum(dp) when the slice is stored
     float rm, rinv;   // ATTN_DS_RECOMP: forward softmax row max and 1/sum
 };
 
@@ -152,8 +186,8 @@ __device__ __forceinline__ void fetch_slice(const GemmP &P, int row, int c0, int
             e.kb[j][g] = 0;
             epi_fetch<EPI>(P, row, c0 + j * 32 + 8 * g + 4 * kh, e.a[j][g], e.b[j][g], e.kb[j][g]);
         }
-    e.dl = (EPI == U2GNN_EPI_ATTN_DS || EPI == U2GNN_EPI_ATTN_DS_SIGNED || EPI == U2GNN_EPI_ATTN_DS_RECOMP)
-               ? P.rowvec[row] : 0.f;
+    e.dl = (EPI == U2GNN_EPI_ATTN_DS || EPI == U2GNN_EPI_ATTN_DS_RECOMP) ? P.rowvec[row] : 0.f;
+    if constexpr (EPI == U2GNN_EPI_ATTN_DS_SIGNED) delta_load(P, row, e.dp);
     if constexpr (EPI == U2GNN_EPI_ATTN_DS_RECOMP) {
         const float2 st = P.rowstat[row];
         e.rm = st.x, e.rinv = st.y;
@@ -182,11 +216,16 @@ __device__ __forceinline__ float4 ds_recomp4(const GemmP &P, int row, int col, f
     return make_float4(o[0], o[1], o[2], o[3]);
 }
 
+// One slice's stores.  STORE_ROWDOT: returns this lane's share of sum_n C[row,n] * aux0[row,n] over
+// the wave's columns (TN MFMA tiles in j order, columns 8g + 4kh of each), 0 otherwise.
 template <int EPI, int TM, int TN>
-__device__ __forceinline__ void store_slice(const GemmP &P, float *C, const f32x16 (&acc)[TM][TN], int i, int row,
-                                            int c0, int kh, const EpiSlice<EPI, TN> &e) {
+__device__ __forceinline__ float store_slice(const GemmP &P, float *C, const f32x16 (&acc)[TM][TN], int i, int row,
+                                             int c0, int kh, const EpiSlice<EPI, TN> &e) {
     uint32_t rkey = 0;
     if constexpr (EPI == U2GNN_EPI_ATTN_DS_RECOMP) rkey = u2gnn_row_key(P.seed, (uint32_t)row);
+    float dl = e.dl;
+    if constexpr (EPI == U2GNN_EPI_ATTN_DS_SIGNED) dl = delta_sum(P, row, e.dp);
+    float rs = 0.f;
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
@@ -198,10 +237,15 @@ __device__ __forceinline__ void store_slice(const GemmP &P, float *C, const f32x
             if constexpr (EPI == U2GNN_EPI_ATTN_DS_RECOMP)
                 o = ds_recomp4(P, row, col, v, e.a[j][g], e.dl, e.rm, e.rinv, rkey);
             else
-                o = epilogue4<EPI>(P, row, col, v, e.a[j][g], e.b[j][g], e.kb[j][g], e.dl);
+                o = epilogue4<EPI>(P, row, col, v, e.a[j][g], e.b[j][g], e.kb[j][g], dl);
             if (P.C) *reinterpret_cast<float4 *>(C + (int64_t)row * P.ldc + col) = o;
             if (P.Cx2) store_x2_4(P.Cx2, P.ldcx2, row, col, o);
+            if constexpr (EPI == U2GNN_EPI_STORE_ROWDOT) {
+                const float4 x = e.a[j][g];
+                rs += o.x * x.x + o.y * x.y + o.z * x.z + o.w * x.w;
+            }
         }
+    return rs;
 }
 
 // Attention dS with keep bits: slice 0's P tile, keep words and delta fetched before the main loop
@@ -211,6 +255,7 @@ struct PreDS {
     float4 p[TN][4];
     uint32_t kw[TN];
     float dl;
+    DeltaParts dp;
 };
 
 template <int EPI, int TN>
@@ -221,7 +266,8 @@ __device__ __forceinline__ void prefetch_ds(const GemmP &P, int row, int c0, int
 #pragma unroll
         for (int g = 0; g < 4; ++g) f.p[j][g] = ld4(P.aux0 + (int64_t)row * P.ld_aux + c0 + j * 32 + 8 * g + 4 * kh);
     }
-    f.dl = P.rowvec[row];
+    if constexpr (EPI == U2GNN_EPI_ATTN_DS_SIGNED) delta_load(P, row, f.dp);
+    else f.dl = P.rowvec[row];
 }
 
 template <int EPI, int TN>
@@ -235,6 +281,7 @@ __device__ __forceinline__ void slice_from_pre(const PreDS<TN> &pre, int kh, Epi
             e.kb[j][g] = pre.kw[j] >> ((8 * g + 4 * kh) & 31);
         }
     e.dl = pre.dl;
+    e.dp = pre.dp;
     e.rm = e.rinv = 0.f;
 }
 
@@ -330,13 +377,34 @@ __device__ __forceinline__ void store_tile(const GemmP &P, float *C, const f32x1
         for (int i = 0; i < TM; ++i) store_slice<EPI>(P, C, acc, i, r0 + i * 32 + li, c0, kh, e[i]);
         return;
     }
+    float rs[TM];
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
         const int row = r0 + i * 32 + li;
         EpiSlice<EPI, TN> e;
         if (i == 0 && pre) slice_from_pre<EPI>(*pre, kh, e);
         else fetch_slice<EPI>(P, row, c0, kh, e);
-        store_slice<EPI>(P, C, acc, i, row, c0, kh, e);
+        rs[i] = store_slice<EPI>(P, C, acc, i, row, c0, kh, e);
+    }
+    if constexpr (EPI == U2GNN_EPI_STORE_ROWDOT) {
+        // one row partial per 64 output columns: lanes l and l + 32 hold a row's two column halves of
+        // each MFMA tile; 64-column waves (TN == 2) own a group, 32-column waves (64 x 64 blocks of
+        // 2 x 2 waves) add their neighbour's half through LDS
+        static_assert(TN == 1 || TN == 2, "STORE_ROWDOT: 32- or 64-column wave tiles");
+#pragma unroll
+        for (int i = 0; i < TM; ++i) rs[i] += __shfl_xor(rs[i], 32, 64);
+        if constexpr (TN == 2) {
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+                if (kh == 0) P.rowpart[(int64_t)(c0 >> 6) * P.ld_rowpart + r0 + i * 32 + li] = rs[i];
+        } else {
+            static_assert(TM == 1, "STORE_ROWDOT: 64 x 64 blocks of 2 x 2 waves");
+            __shared__ float rdred[64];
+            const int row = r0 + li, rb = row & 63, wn = (c0 & 63) >> 5;
+            if (kh == 0 && wn == 1) rdred[rb] = rs[0];
+            __syncthreads();
+            if (kh == 0 && wn == 0) P.rowpart[(int64_t)(c0 >> 6) * P.ld_rowpart + row] = rs[0] + rdred[rb];
+        }
     }
 }
 

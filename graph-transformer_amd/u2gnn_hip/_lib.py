@@ -29,8 +29,8 @@ U2GNN_OK = 0
 ERRORS = {-1: "bad argument", -2: "misaligned pointer / leading dimension", -3: "shape not a tile multiple"}
 
 EPI_STORE, EPI_BIAS, EPI_BIAS_DROP_RESID, EPI_BIAS_RELU_DROP, EPI_RELU_DROP_BWD, EPI_ACCUM, EPI_ATTN_DS, \
-    EPI_ATTN_DS_SIGNED, EPI_ATTN_DS_RECOMP, EPI_BIAS_DROP_RESID_LN = range(10)
-ABI_VERSION = 7   # include/u2gnn_hip.h U2GNN_ABI_VERSION
+    EPI_ATTN_DS_SIGNED, EPI_ATTN_DS_RECOMP, EPI_BIAS_DROP_RESID_LN, EPI_STORE_ROWDOT = range(11)
+ABI_VERSION = 8   # include/u2gnn_hip.h U2GNN_ABI_VERSION
 PREC_F32, PREC_BF16X3, PREC_BF16 = 0, 1, 2
 
 
@@ -60,6 +60,9 @@ class GemmArgs(ctypes.Structure):
         ("ln_gamma", c_void_p), ("ln_beta", c_void_p), ("ln_y", c_void_p), ("ln_ldy", c_int64),
         ("ln_mean", c_void_p), ("ln_rstd", c_void_p), ("ln_d", c_int64), ("ln_rows", c_int64),
         ("ln_eps", c_float), ("ln_reserved", c_int32),
+        # ABI v8: delta = rowsum(dO * O) from the dO GEMM's epilogue (STORE_ROWDOT -> ATTN_DS_SIGNED)
+        ("rowpart", c_void_p), ("ld_rowpart", c_int64),
+        ("rowvec_parts", c_int32), ("rowvec_reserved", c_int32), ("ld_rowvec", c_int64),
     ]
 
 

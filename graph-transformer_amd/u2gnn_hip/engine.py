@@ -185,6 +185,9 @@ SIDE_MIN_ELEMS = int(os.environ.get("U2GNN_SIDE_MIN_ELEMS", str(1 << 20)))
 # U2GNN_FUSED_LN=0 (A/B): the separate layernorm_fwd launch even where the GEMM tile holds whole rows
 # (encoder_layer.cpp applies the same rule)
 _FUSED_LN = os.environ.get("U2GNN_FUSED_LN", "1") != "0"
+# U2GNN_ROWDOT_FUSE=1 (A/B, opt-in; measured slower, encoder_layer.cpp rowdot_fuse_on): delta = rowsum(dO * O)
+# from the dO GEMM's STORE_ROWDOT epilogue instead of its own rowdot launch
+_ROWDOT_FUSE = os.environ.get("U2GNN_ROWDOT_FUSE", "0") == "1"
 
 
 def fused_ln(dp: int, prec: str) -> bool:
@@ -419,14 +422,21 @@ def encoder_layer_backward(dX2: torch.Tensor, ctx: EncoderLayerCtx, w: PackedLay
     del dX1
     # out-projection
     dO = torch.empty(Np, dp, device=dev, dtype=f32)
-    K.gemm(dA, w.W_o, dO, Np, dp, dp, dp, dp, dp, precision=_rp("out_dx", prec), flops=2.0 * N * d * d)
+    # delta = rowsum(dO * O): per-64-column partials from the dO GEMM's epilogue, summed by the dS epilogue
+    delta_parts = torch.empty(dp // 64, Np, device=dev, dtype=f32) if _ROWDOT_FUSE else None
+    K.gemm(dA, w.W_o, dO, Np, dp, dp, dp, dp, dp, precision=_rp("out_dx", prec), flops=2.0 * N * d * d,
+           **({} if delta_parts is None else dict(epilogue=E.EPI_STORE_ROWDOT, aux0=ctx.O, ld_aux=dp,
+                                                  rowpart=delta_parts)))
     off.run(lambda: _wgrad(dA, dp, ctx.O, dp, dp, dp, Np, g.out_w, (dp, d), (dp, d), _rp("out_dw", prec), N), dA, ctx.O)
     del dA
     # attention core
     QKV = ctx.QKV
     Q, Kt, V = QKV[:, :dp], QKV[:, dp:2 * dp], QKV[:, 2 * dp:]
-    delta = torch.empty(Np, device=dev, dtype=f32)
-    K.rowdot(dO, dp, ctx.O, dp, delta, Np, dp)
+    if delta_parts is None:
+        delta = torch.empty(Np, device=dev, dtype=f32)
+        K.rowdot(dO, dp, ctx.O, dp, delta, Np, dp)
+    else:
+        delta = delta_parts
     dS = torch.empty(Np, Np, device=dev, dtype=f32)
     K.gemm(dO, V, dS, Np, Np, dp, dp, 3 * dp, Np, trans_b=True, epilogue=E.EPI_ATTN_DS_SIGNED, aux0=ctx.Pd,
            p_drop=pd, rowvec=delta, ld_aux=Np, precision=_rp("ds", prec), flops=att)

@@ -72,7 +72,7 @@ def gemm_symbol(precision, M, N, split_k, tile, trans_a, trans_b, epilogue, clam
 def gemm(A, B, C, M, N, K, lda, ldb, ldc, trans_a=False, trans_b=False, epilogue=_lib.EPI_STORE, split_k=1,
          slab_stride=0, bias=None, aux0=None, aux1=None, rowvec=None, ld_aux=0, alpha=1.0, scale_cols=0, p_drop=0.0,
          seed=0, precision="fp32", tile=0, flops=None, keep=None, clamp_a=False, Cx2=None, ldcx2=0, rowstat=None,
-         m_valid=0, n_valid=0, ln=None):
+         m_valid=0, n_valid=0, ln=None, rowpart=None):
     """C[M,N] (epilogue) sum_k A(m,k) B(k,n).  A/B/C may be views (pointer arithmetic via
     storage offsets is done by torch's data_ptr()).  ``flops``: algorithmic FLOPs of the
     launch for the roofline recorder (None = not recorded).  ``clamp_a``: A elements below +0 are read
@@ -80,7 +80,9 @@ def gemm(A, B, C, M, N, K, lda, ldb, ldc, trans_a=False, trans_b=False, epilogue
     x2 operands (include/u2gnn_hip.h): A and B given as bfloat16 tensors are pre-split [rows][2*cols]
     matrices (lda / ldb in bf16 elements); ``Cx2`` (bfloat16) receives the result in x2 format, C may
     then be None.  ``rowstat``/``m_valid``/``n_valid``: the ATTN_DS_RECOMP epilogue.  ``ln`` =
-    (gamma, beta, Y, ldy, mean, rstd, d, rows, eps): the EPI_BIAS_DROP_RESID_LN LayerNorm (N == 64)."""
+    (gamma, beta, Y, ldy, mean, rstd, d, rows, eps): the EPI_BIAS_DROP_RESID_LN LayerNorm (N == 64).
+    ``rowpart`` [N/64, >= M]: the EPI_STORE_ROWDOT row partials (ABI v8).  A 2-D ``rowvec`` [P, >= M]
+    gives ATTN_DS_SIGNED the sum of its P partials per row (in row order of ``rowvec``)."""
     _dev(A, B, C, Cx2, rowstat)
     x2 = A.dtype == torch.bfloat16
     if x2 != (B.dtype == torch.bfloat16):
@@ -110,6 +112,11 @@ def gemm(A, B, C, M, N, K, lda, ldb, ldc, trans_a=False, trans_b=False, epilogue
     a.aux0 = aux0.data_ptr() if aux0 is not None else None
     a.aux1 = aux1.data_ptr() if aux1 is not None else None
     a.rowvec = rowvec.data_ptr() if rowvec is not None else None
+    if rowvec is not None and rowvec.dim() == 2:   # ABI v8: partials of a STORE_ROWDOT epilogue
+        a.rowvec_parts, a.ld_rowvec = int(rowvec.shape[0]), int(rowvec.stride(0))
+    if rowpart is not None:
+        _dev(rowpart)
+        a.rowpart, a.ld_rowpart = rowpart.data_ptr(), int(rowpart.stride(0))
     a.ld_aux = int(ld_aux)
     a.alpha = float(alpha)
     a.scale_cols = int(scale_cols)

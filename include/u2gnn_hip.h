@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define U2GNN_ABI_VERSION 7
+#define U2GNN_ABI_VERSION 8
 
 #define U2GNN_OK 0
 #define U2GNN_E_ARG (-1)    /* bad size / null pointer */
@@ -58,6 +58,11 @@ extern "C" {
                                           ln_mean / ln_rstd per row; rows >= ln_rows and columns >= ln_d
                                           written as 0).  Row-complete tiles only: N == 64 (tile 64),
                                           bf16 / bf16x3, split_k 1 -- the d <= 64 encoders (C3, C5) */
+#define U2GNN_EPI_STORE_ROWDOT 10   /* ABI v8: C = alpha*acc as STORE, and per 64-column group q = n/64 the
+                                       row partial rowpart[q*ld_rowpart + m] = sum_{n in q} C[m,n]*aux0[m,n]
+                                       (the attention backward's delta = rowsum(dO * O) formed by the dO
+                                       GEMM; ATTN_DS_SIGNED sums the N/64 partials in q order, rowvec_parts).
+                                       N % 64 == 0, split_k 1, fp32-operand kernels only */
 
 /* x2 operand format (pre-split fp32): a logical fp32 matrix X[R][C] (C % 8 == 0) is stored as
  * bf16 X2[R][2C] with, per 8-column group g, hi(X[r][8g..8g+7]) then lo(X[r][8g..8g+7]),
@@ -121,6 +126,13 @@ typedef struct u2gnn_gemm_args {
     int64_t ln_d, ln_rows;
     float ln_eps;
     int32_t ln_reserved;
+    /* ---- ABI v8: delta from the dO GEMM (EPI_STORE_ROWDOT -> EPI_ATTN_DS_SIGNED) ---- */
+    float *rowpart;       /* STORE_ROWDOT: [N/64][ld_rowpart] row partials (ld_rowpart >= M) */
+    int64_t ld_rowpart;
+    int32_t rowvec_parts; /* ATTN_DS_SIGNED: 0/1 = rowvec[m]; P > 1 = sum_{q<P} rowvec[q*ld_rowvec + m] in
+                             q order (fp32-operand kernels only) */
+    int32_t rowvec_reserved;
+    int64_t ld_rowvec;
 } u2gnn_gemm_args;
 
 /* ---- library ------------------------------------------------------------------ */

@@ -244,6 +244,48 @@ def test_clamp_a_and_signed_ds_epilogue(prec, tile):
         K.gemm(dO, V, C, Np, Np, dp, dp, dp, Np, trans_b=True, precision=prec, clamp_a=True)
 
 
+@pytest.mark.parametrize("dp", [384, 640])   # 6 partials, and 10 (> the 8 held in registers)
+@pytest.mark.parametrize("prec", ["fp32", "bf16x3", "bf16"])
+@pytest.mark.parametrize("tile", [0, 64, 128])
+def test_store_rowdot_partials_feed_signed_ds(prec, tile, dp):
+    """ABI v8: the dO GEMM's STORE_ROWDOT epilogue stores C exactly as STORE and writes the row partials
+    sum_{n in 64-column group q} C[m,n] * O[m,n]; ATTN_DS_SIGNED with those partials (rowvec_parts)
+    equals the same epilogue fed delta = their sum in group order, and the rowdot delta to fp32 rounding."""
+    Np, N, p = 512, 470, 0.3
+    dA, Wo, O = _mk(Np, dp, seed=51), _mk(dp, dp, seed=52) * 0.05, _mk(Np, dp, seed=53)
+    C0, C1 = torch.empty(Np, dp, device=DEV), torch.empty(Np, dp, device=DEV)
+    parts = torch.full((dp // 64, Np + 64), float("nan"), device=DEV)[:, :Np + 16]   # ld_rowpart > M
+    K.gemm(dA, Wo, C0, Np, dp, dp, dp, dp, dp, precision=prec, tile=tile)
+    K.gemm(dA, Wo, C1, Np, dp, dp, dp, dp, dp, precision=prec, tile=tile, epilogue=_lib.EPI_STORE_ROWDOT, aux0=O,
+           ld_aux=dp, rowpart=parts)
+    assert torch.equal(C0, C1)
+    ref = (C0.double() * O.double()).view(Np, dp // 64, 64).sum(2).t()
+    assert torch.isfinite(parts[:, :Np]).all()
+    assert rel_err(parts[:, :Np].double(), ref) < 1e-5
+    delta_seq = torch.zeros(Np, device=DEV)
+    for q in range(dp // 64):   # the dS epilogue's order
+        delta_seq = delta_seq + parts[q, :Np]
+    delta_rd = torch.empty(Np, device=DEV)
+    K.rowdot(C1, dp, O, dp, delta_rd, Np, dp)
+    assert rel_err(delta_seq, delta_rd) < 1e-5
+    S = _mk(Np, Np, seed=54)
+    X = torch.empty(Np, Np, device=DEV)
+    K.attn_softmax_fwd(S, Np, None, X, Np, N, Np, N, Np, p, 9)
+    V = _mk(Np, dp, seed=55)
+    dS1, dS2 = torch.empty(Np, Np, device=DEV), torch.empty(Np, Np, device=DEV)
+    K.gemm(C1, V, dS1, Np, Np, dp, dp, dp, Np, trans_b=True, epilogue=_lib.EPI_ATTN_DS_SIGNED, aux0=X, p_drop=p,
+           rowvec=parts[:, :Np], ld_aux=Np, precision=prec)
+    K.gemm(C1, V, dS2, Np, Np, dp, dp, dp, Np, trans_b=True, epilogue=_lib.EPI_ATTN_DS_SIGNED, aux0=X, p_drop=p,
+           rowvec=delta_seq, ld_aux=Np, precision=prec)
+    assert torch.equal(dS1, dS2)
+    with pytest.raises(_lib.U2GNNNativeError):   # partials only for the dS epilogue
+        K.gemm(C1, V, dS1, Np, Np, dp, dp, dp, Np, trans_b=True, aux0=X, rowvec=parts[:, :Np], ld_aux=Np,
+               precision=prec)
+    with pytest.raises(_lib.U2GNNNativeError):   # no split-K with the row partials
+        K.gemm(dA, Wo, C1, Np, dp, dp, dp, dp, dp, precision=prec, epilogue=_lib.EPI_STORE_ROWDOT, aux0=O,
+               ld_aux=dp, rowpart=parts, split_k=2, slab_stride=Np * dp)
+
+
 def test_dropout_mask_statistics():
     """The counter-based keep decision: rate 1-p, no correlation between neighbouring rows, columns
     or seeds (the masks of the attention dropout are 2-D slices of this stream)."""
@@ -361,6 +403,35 @@ def test_gather_pack_colsum():
     K.colsum(X, 300, 192, 192, (64, 7), out, ws)
     ref = X.sum(0).view(3, 64)[:, :7].reshape(-1)
     assert rel_err(out, ref) < 1e-5
+
+
+def test_pack_multi_c4_shapes_equal_single_jobs():
+    """The batched pack (8 rows per block, 32-bit maps) writes exactly what one pack_padded launch per
+    job writes: C4's in-projection (3 row blocks), FFN weights, a bias row with 3 column blocks, and a
+    job whose padded row count is not a multiple of 8."""
+    d, dp, ff = 367, 384, 1024
+    shapes = [  # (real rows, real cols, rows_pad, cols_pad, rblk, cblk)
+        (3 * d, d, 3 * dp, dp, (dp, d), (dp, d)),
+        (ff, d, ff, dp, (ff, ff), (dp, d)),
+        (d, ff, dp, ff, (dp, d), (ff, ff)),
+        (1, 3 * d, 1, 3 * dp, (1, 1), (dp, d)),
+        (3 * 5, 7, 3 * 7, 64, (7, 5), (64, 7)),
+    ]
+    jobs, singles = [], []
+    for i, (r, c, rp, cp, rb, cb) in enumerate(shapes):
+        src = _mk(r, c, seed=60 + i)
+        a, b = torch.full((rp, cp), 9.0, device=DEV), torch.full((rp, cp), -9.0, device=DEV)
+        jobs.append((src, c, rp, cp, rb, cb, a, cp))
+        K.pack_padded(src, c, rp, cp, rb, cb, b, cp)
+        singles.append(b)
+    K.pack_padded_multi(jobs)
+    for j, b in zip(jobs, singles):
+        assert torch.equal(j[6], b)
+    Wp = singles[0]   # spot check of the block map against the real matrix
+    W = jobs[0][0]
+    for q in range(3):
+        assert torch.equal(Wp[q * dp:q * dp + d, :d], W[q * d:(q + 1) * d])
+        assert Wp[q * dp + d:(q + 1) * dp].abs().max().item() == 0 and Wp[:, d:].abs().max().item() == 0
 
 
 @pytest.mark.parametrize("rows", [1, 255, 2000, 2560, 2561, 4864, 8192, 8209, 20011, 82110])

@@ -388,6 +388,13 @@ bool fused_ln_on() {
     return v;
 }
 
+// U2GNN_LN_DELTA=0 (A/B): the attention backward's delta by its own u2gnn_rowdot launch instead of
+// LayerNorm1's backward (u2gnn_layernorm_bwd_delta: sum_c dA * ((Z1 - X)(1-p) - b_o), no dO / O reads)
+bool ln_delta_on() {
+    static const bool v = env_flag("U2GNN_LN_DELTA", true);
+    return v;
+}
+
 // U2GNN_ROWDOT_FUSE=1 (A/B, opt-in): delta = rowsum(dO * O) from the dO GEMM's STORE_ROWDOT epilogue
 // (per-64-column partials that the dS epilogue sums) instead of its own u2gnn_rowdot launch.  Measured
 // slower on C4 (2 sessions x 3 reps: 3.33 vs 3.29 and 3.376 vs 3.363 ms per step; rocprof: rowdot
@@ -520,7 +527,14 @@ int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
     // the in-projection's dX GEMM below is skipped
     float *dX_scratch = W.take<float>(Np * dp);   // taken in every mode so the plan covers it
     if (!need_dx) dX = dX_scratch;
-    if (!plan)
+    // node attention: LayerNorm1's backward also forms delta = rowsum(dO * O) for the dS epilogue
+    const bool fuse_rowdot = !D.window && rowdot_fuse_on();
+    const bool ln_delta = !D.window && !fuse_rowdot && ln_delta_on();
+    float *delta_ln = ln_delta ? W.take<float>(Np) : nullptr;
+    if (!plan && ln_delta)
+        U2GNN_TRY(u2gnn_layernorm_bwd_delta(dX1, dp, c.Z1, dp, c.mean1, c.rstd1, w->n1_w, dX, dp, dA, dp, pd,
+                                            s->drop1, N, Np, d, dp, X, dp, w->b_o, delta_ln, st));
+    else if (!plan)
         U2GNN_TRY(u2gnn_layernorm_bwd(dX1, dp, c.Z1, dp, c.mean1, c.rstd1, w->n1_w, dX, dp, dA, dp, pd, s->drop1, N,
                                       Np, d, dp, st));
     U2GNN_TRY(sd.fork());
@@ -531,7 +545,6 @@ int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
     float *dO = W.take<float>(Np * dp);
     // delta = rowsum(dO * O) of the attention backward: partial sums per 32 columns from the dO GEMM's
     // epilogue (node attention), summed in group order by the dS epilogue
-    const bool fuse_rowdot = !D.window && rowdot_fuse_on();
     float *delta_parts = fuse_rowdot ? W.take<float>((dp / 64) * Np) : nullptr;
     {
         G gg(dA, w->W_o, dO, Np, dp, dp, dp, dp, dp, prec);
@@ -573,8 +586,8 @@ int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
             if (!dk_side) U2GNN_TRY(sd.mark(&dv_done));
             U2GNN_TRY(in_part(2));
         }
-        float *delta = fuse_rowdot ? delta_parts : W.take<float>(Np);
-        if (!plan && !fuse_rowdot) U2GNN_TRY(u2gnn_rowdot(dO, dp, c.O, dp, delta, Np, dp, st));
+        float *delta = fuse_rowdot ? delta_parts : ln_delta ? delta_ln : W.take<float>(Np);
+        if (!plan && !fuse_rowdot && !ln_delta) U2GNN_TRY(u2gnn_rowdot(dO, dp, c.O, dp, delta, Np, dp, st));
         float *dS = W.take<float>(Np * Np);
         {
             G gg(dO, V, dS, Np, Np, dp, dp, 3 * dp, Np, D.prec_ab);

@@ -704,12 +704,23 @@ __global__ void __launch_bounds__(256) layernorm_fwd_kernel(const float *Z, int6
 }
 
 // LN backward, row part: one half-wave per row (8 rows per block).
-template <int LN_V4>
+// DELTA (LayerNorm1 of an encoder layer, u2gnn_layernorm_bwd_delta): also the attention backward's
+// delta[row] = sum_c dZd[row,c] * ((Z - X)[row,c] * (1-p) - bias[c]).  Z = X + drop(A + bias) with
+// A = O W_o^T the out-projection product, so where dZd != 0 (kept) the bracket is A, and
+// sum_c dZd * A = sum_c (dZd W_o) * O = rowsum(dO * O): the u2gnn_rowdot launch without reading dO / O.
+struct LnDelta {
+    const float *X;
+    int64_t ldx;
+    const float *bias;   // [d_pad], zero-padded (the out-projection's padded bias)
+    float *delta;        // [rows_pad]
+};
+
+template <int LN_V4, bool DELTA>
 __global__ void __launch_bounds__(256) layernorm_bwd_kernel(const float *dY, int64_t ldy, const float *Z, int64_t ldz,
                                                             const float *mean, const float *rstd, const float *gamma,
                                                             float *dZ, int64_t lddz, float *dZd, int64_t lddrop,
                                                             float p, uint64_t seed, const uint64_t *seed_epoch, int64_t rows_valid,
-                                                            int64_t rows_pad, int64_t d, int64_t d_pad) {
+                                                            int64_t rows_pad, int64_t d, int64_t d_pad, LnDelta dt) {
     seed = u2gnn_seed(seed, seed_epoch);
     const int64_t row = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 5);
     const int hl = threadIdx.x & 31;
@@ -722,6 +733,8 @@ __global__ void __launch_bounds__(256) layernorm_bwd_kernel(const float *dY, int
             *reinterpret_cast<float4 *>(dz + c) = z4;
             if (dzd) *reinterpret_cast<float4 *>(dzd + c) = z4;
         }
+        if constexpr (DELTA)
+            if (hl == 0) dt.delta[row] = 0.f;
         return;
     }
     const float ks = p > 0.f ? 1.f / (1.f - p) : 1.f;
@@ -729,12 +742,16 @@ __global__ void __launch_bounds__(256) layernorm_bwd_kernel(const float *dY, int
     const float *dy = dY + row * ldy;
     const float *z = Z + row * ldz;
     float xh[LN_V4][4], g[LN_V4][4], gm[LN_V4][4] = {};
-    float4 ta[LN_V4], tb[LN_V4];
+    float4 ta[LN_V4], tb[LN_V4], tx[DELTA ? LN_V4 : 1], tc[DELTA ? LN_V4 : 1];
 #pragma unroll
     for (int i = 0; i < LN_V4; ++i) {
         const int64_t c = 4 * (hl + 32 * i);
         ta[i] = c < d_pad ? ld4(dy + c) : z4;
         tb[i] = c < d_pad ? ld4(z + c) : z4;
+        if constexpr (DELTA) {
+            tx[i] = c < d_pad ? ld4(dt.X + row * dt.ldx + c) : z4;
+            tc[i] = c < d_pad ? ld4(dt.bias + c) : z4;
+        }
     }
 #pragma unroll
     for (int i = 0; i < LN_V4; ++i) {   // unpadded [d] gamma: clamped element loads (see the forward)
@@ -759,6 +776,7 @@ __global__ void __launch_bounds__(256) layernorm_bwd_kernel(const float *dY, int
     }
     const float m1 = half_sum(s1) / (float)d;
     const float m2 = half_sum(s2) / (float)d;
+    float s3 = 0.f;   // DELTA
 #pragma unroll
     for (int i = 0; i < LN_V4; ++i) {
         const int64_t c = 4 * (hl + 32 * i);
@@ -772,6 +790,16 @@ __global__ void __launch_bounds__(256) layernorm_bwd_kernel(const float *dY, int
         }
         *reinterpret_cast<float4 *>(dz + c) = make_float4(o[0], o[1], o[2], o[3]);
         if (dzd) *reinterpret_cast<float4 *>(dzd + c) = make_float4(od[0], od[1], od[2], od[3]);
+        if constexpr (DELTA) {
+            const float zv[4] = {tb[i].x, tb[i].y, tb[i].z, tb[i].w}, xv[4] = {tx[i].x, tx[i].y, tx[i].z, tx[i].w};
+            const float bv[4] = {tc[i].x, tc[i].y, tc[i].z, tc[i].w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) s3 += od[q] * ((zv[q] - xv[q]) * (1.f - p) - bv[q]);
+        }
+    }
+    if constexpr (DELTA) {
+        const float dl = half_sum(s3);
+        if (hl == 0) dt.delta[row] = dl;
     }
 }
 
@@ -1171,19 +1199,32 @@ int u2gnn_layernorm_fwd(const float *Z, int64_t ldz, const float *gamma, const f
     return u2gnn_launch_status();
 }
 
-int u2gnn_layernorm_bwd(const float *dY, int64_t ldy, const float *Z, int64_t ldz, const float *mean,
-                        const float *rstd, const float *gamma, float *dZ, int64_t lddz, float *dZdrop, int64_t lddrop,
-                        float p, uint64_t seed, int64_t rows_valid, int64_t rows_pad, int64_t d, int64_t d_pad,
-                        void *stream) {
+namespace {
+int layernorm_bwd_launch(const float *dY, int64_t ldy, const float *Z, int64_t ldz, const float *mean,
+                         const float *rstd, const float *gamma, float *dZ, int64_t lddz, float *dZdrop, int64_t lddrop,
+                         float p, uint64_t seed, int64_t rows_valid, int64_t rows_pad, int64_t d, int64_t d_pad,
+                         const LnDelta *dt, void *stream) {
     if (!dY || !Z || !mean || !rstd || !gamma || !dZ || d < 1 || d > d_pad || d_pad > LN_MAXV * 64)
         return U2GNN_E_ARG;
     if (!al16(dY) || !al16(Z) || !al16(dZ) || (ldy & 3) || (ldz & 3) || (lddz & 3) || (d_pad & 3) ||
         (dZdrop && (!al16(dZdrop) || (lddrop & 3))))
         return U2GNN_E_ALIGN;
+    if (dt && (!dt->X || !dt->bias || !dt->delta)) return U2GNN_E_ARG;
+    if (dt && (!al16(dt->X) || !al16(dt->bias) || (dt->ldx & 3))) return U2GNN_E_ALIGN;
     const dim3 gr(grid_for(rows_pad, 8, 1 << 30));
     hipStream_t st = u2gnn_stream(stream);
-#define U2GNN_LNB(V) hipLaunchKernelGGL(layernorm_bwd_kernel<V>, gr, dim3(256), 0, st, dY, ldy, Z, ldz, mean, rstd, gamma, \
-                                        dZ, lddz, dZdrop, lddrop, p, seed, u2gnn_g_epoch, rows_valid, rows_pad, d, d_pad)
+    const LnDelta none{nullptr, 0, nullptr, nullptr};
+#define U2GNN_LNB(V)                                                                                                   \
+    do {                                                                                                               \
+        if (dt)                                                                                                        \
+            hipLaunchKernelGGL((layernorm_bwd_kernel<V, true>), gr, dim3(256), 0, st, dY, ldy, Z, ldz, mean, rstd,    \
+                               gamma, dZ, lddz, dZdrop, lddrop, p, seed, u2gnn_g_epoch, rows_valid, rows_pad, d,       \
+                               d_pad, *dt);                                                                            \
+        else                                                                                                           \
+            hipLaunchKernelGGL((layernorm_bwd_kernel<V, false>), gr, dim3(256), 0, st, dY, ldy, Z, ldz, mean, rstd,   \
+                               gamma, dZ, lddz, dZdrop, lddrop, p, seed, u2gnn_g_epoch, rows_valid, rows_pad, d,       \
+                               d_pad, none);                                                                           \
+    } while (0)
     const int64_t v4 = (d_pad + 127) / 128;
     if (v4 <= 1) U2GNN_LNB(1);
     else if (v4 == 2) U2GNN_LNB(2);
@@ -1192,6 +1233,25 @@ int u2gnn_layernorm_bwd(const float *dY, int64_t ldy, const float *Z, int64_t ld
     else U2GNN_LNB(LN_V4_MAX);
 #undef U2GNN_LNB
     return u2gnn_launch_status();
+}
+}  // namespace
+
+int u2gnn_layernorm_bwd(const float *dY, int64_t ldy, const float *Z, int64_t ldz, const float *mean,
+                        const float *rstd, const float *gamma, float *dZ, int64_t lddz, float *dZdrop, int64_t lddrop,
+                        float p, uint64_t seed, int64_t rows_valid, int64_t rows_pad, int64_t d, int64_t d_pad,
+                        void *stream) {
+    return layernorm_bwd_launch(dY, ldy, Z, ldz, mean, rstd, gamma, dZ, lddz, dZdrop, lddrop, p, seed, rows_valid,
+                                rows_pad, d, d_pad, nullptr, stream);
+}
+
+int u2gnn_layernorm_bwd_delta(const float *dY, int64_t ldy, const float *Z, int64_t ldz, const float *mean,
+                              const float *rstd, const float *gamma, float *dZ, int64_t lddz, float *dZdrop,
+                              int64_t lddrop, float p, uint64_t seed, int64_t rows_valid, int64_t rows_pad, int64_t d,
+                              int64_t d_pad, const float *X, int64_t ldx, const float *bias, float *delta,
+                              void *stream) {
+    const LnDelta dt{X, ldx, bias, delta};
+    return layernorm_bwd_launch(dY, ldy, Z, ldz, mean, rstd, gamma, dZ, lddz, dZdrop, lddrop, p, seed, rows_valid,
+                                rows_pad, d, d_pad, &dt, stream);
 }
 
 int u2gnn_layernorm_bwd_params(const float *dY, int64_t ldy, const float *Z, int64_t ldz, const float *mean,

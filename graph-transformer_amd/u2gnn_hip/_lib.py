@@ -122,6 +122,8 @@ _HIP_SIGS = {
     "u2gnn_layernorm_fwd": ([VP, I64, VP, VP, VP, I64, VP, VP, I64, I64, I64, I64, F32, VP], c_int32),
     "u2gnn_layernorm_bwd": ([VP, I64, VP, I64, VP, VP, VP, VP, I64, VP, I64, F32, c_uint64, I64, I64, I64, I64, VP],
                             c_int32),
+    "u2gnn_layernorm_bwd_delta": ([VP, I64, VP, I64, VP, VP, VP, VP, I64, VP, I64, F32, c_uint64, I64, I64, I64, I64,
+                                   VP, I64, VP, VP, VP], c_int32),
     "u2gnn_layernorm_bwd_params": ([VP, I64, VP, I64, VP, VP, VP, I64, I64, I64, I64, VP, VP, VP, VP, VP], c_int32),
     "u2gnn_pack_padded_multi": ([VP, I32, VP], c_int32),
     "u2gnn_pool_fwd": ([VP, I64, VP, VP, VP, VP, I64, I64, I64, F32, c_uint64, VP], c_int32),

@@ -188,6 +188,9 @@ _FUSED_LN = os.environ.get("U2GNN_FUSED_LN", "1") != "0"
 # U2GNN_ROWDOT_FUSE=1 (A/B, opt-in; measured slower, encoder_layer.cpp rowdot_fuse_on): delta = rowsum(dO * O)
 # from the dO GEMM's STORE_ROWDOT epilogue instead of its own rowdot launch
 _ROWDOT_FUSE = os.environ.get("U2GNN_ROWDOT_FUSE", "0") == "1"
+# U2GNN_LN_DELTA=0 (A/B; encoder_layer.cpp ln_delta_on): delta by its own rowdot launch instead of LayerNorm1's
+# backward (layernorm_bwd_delta)
+_LN_DELTA = os.environ.get("U2GNN_LN_DELTA", "1") != "0"
 
 
 def fused_ln(dp: int, prec: str) -> bool:
@@ -415,8 +418,14 @@ def encoder_layer_backward(dX2: torch.Tensor, ctx: EncoderLayerCtx, w: PackedLay
     # LN1 backward -> dX (residual), dA (dropout1 branch)
     dX = torch.empty(Np, dp, device=dev, dtype=f32)
     dA = torch.empty(Np, dp, device=dev, dtype=f32)
-    K.layernorm_bwd(dX1, dp, ctx.Z1, dp, ctx.mean1, ctx.rstd1, p.n1_w, dX, dp, dA, dp, pd,
-                    seeds.get(SITE_DROP1, 0), N, Np, d, dp)
+    ln_delta = _LN_DELTA and not _ROWDOT_FUSE
+    if ln_delta:   # LayerNorm1's backward also forms the attention backward's delta = rowsum(dO * O)
+        delta = torch.empty(Np, device=dev, dtype=f32)
+        K.layernorm_bwd_delta(dX1, dp, ctx.Z1, dp, ctx.mean1, ctx.rstd1, p.n1_w, dX, dp, dA, dp, pd,
+                              seeds.get(SITE_DROP1, 0), N, Np, d, dp, ctx.X, dp, w.b_o, delta)
+    else:
+        K.layernorm_bwd(dX1, dp, ctx.Z1, dp, ctx.mean1, ctx.rstd1, p.n1_w, dX, dp, dA, dp, pd,
+                        seeds.get(SITE_DROP1, 0), N, Np, d, dp)
     off.run(lambda: K.layernorm_bwd_params(dX1, dp, ctx.Z1, dp, ctx.mean1, ctx.rstd1, dA, dp, N, d, dp, ws, g.n1_w,
                                            g.n1_b, g.out_b), dX1, ctx.Z1, ctx.mean1, ctx.rstd1, dA)
     del dX1
@@ -432,11 +441,11 @@ def encoder_layer_backward(dX2: torch.Tensor, ctx: EncoderLayerCtx, w: PackedLay
     # attention core
     QKV = ctx.QKV
     Q, Kt, V = QKV[:, :dp], QKV[:, dp:2 * dp], QKV[:, 2 * dp:]
-    if delta_parts is None:
+    if delta_parts is not None:
+        delta = delta_parts
+    elif not ln_delta:
         delta = torch.empty(Np, device=dev, dtype=f32)
         K.rowdot(dO, dp, ctx.O, dp, delta, Np, dp)
-    else:
-        delta = delta_parts
     dS = torch.empty(Np, Np, device=dev, dtype=f32)
     K.gemm(dO, V, dS, Np, Np, dp, dp, 3 * dp, Np, trans_b=True, epilogue=E.EPI_ATTN_DS_SIGNED, aux0=ctx.Pd,
            p_drop=pd, rowvec=delta, ld_aux=Np, precision=_rp("ds", prec), flops=att)

@@ -248,6 +248,17 @@ def layernorm_bwd(dY, ldy, Z, ldz, mean, rstd, gamma, dZ, lddz, dZdrop, lddrop, 
                                         int(rows_pad), int(d), int(d_pad), _s()), "u2gnn_layernorm_bwd")
 
 
+def layernorm_bwd_delta(dY, ldy, Z, ldz, mean, rstd, gamma, dZ, lddz, dZdrop, lddrop, p, seed, rows_valid, rows_pad, d,
+                        d_pad, X, ldx, bias, delta):
+    """layernorm_bwd of an encoder layer's LayerNorm1 that also writes the attention backward's delta
+    (rowsum(dO * O) recovered as sum_c dZdrop * ((Z - X)(1-p) - bias); include/u2gnn_hip.h)."""
+    _dev(dY, Z, mean, rstd, gamma, dZ, X, bias, delta)
+    check(hip_lib().u2gnn_layernorm_bwd_delta(_p(dY), int(ldy), _p(Z), int(ldz), _p(mean), _p(rstd), _p(gamma),
+                                              _p(dZ), int(lddz), _p(dZdrop), int(lddrop), float(p), int(seed),
+                                              int(rows_valid), int(rows_pad), int(d), int(d_pad), _p(X), int(ldx),
+                                              _p(bias), _p(delta), _s()), "u2gnn_layernorm_bwd_delta")
+
+
 def layernorm_bwd_params(dY, ldy, Z, ldz, mean, rstd, dZdrop, lddrop, rows_valid, d, d_pad, ws, dgamma, dbeta,
                          dbias=None):
     _dev(dY, Z, mean, rstd, ws, dgamma, dbeta)

@@ -219,6 +219,16 @@ int u2gnn_layernorm_bwd(const float *dY, int64_t ldy, const float *Z, int64_t ld
                         const float *rstd, const float *gamma, float *dZ, int64_t lddz, float *dZdrop,
                         int64_t lddrop, float p, uint64_t seed, int64_t rows_valid, int64_t rows_pad,
                         int64_t d, int64_t d_pad, void *stream);
+/* ABI v8: u2gnn_layernorm_bwd of an encoder layer's LayerNorm1 that also writes the attention backward's
+ * delta[r] = sum_{c<d_pad} dZdrop[r,c] * ((Z - X)[r,c] * (1-p) - bias[c]) (0 for r >= rows_valid), where
+ * Z = X + drop(O W_o^T + bias) is the LN input, X the layer input and bias the zero-padded out-projection
+ * bias: in exact arithmetic rowsum(dO * O) with dO = dZdrop W_o (u2gnn_rowdot), without reading dO or O.
+ * X [rows_pad][ldx] and bias [d_pad] 16-byte aligned; delta [rows_pad]. */
+int u2gnn_layernorm_bwd_delta(const float *dY, int64_t ldy, const float *Z, int64_t ldz, const float *mean,
+                              const float *rstd, const float *gamma, float *dZ, int64_t lddz, float *dZdrop,
+                              int64_t lddrop, float p, uint64_t seed, int64_t rows_valid, int64_t rows_pad,
+                              int64_t d, int64_t d_pad, const float *X, int64_t ldx, const float *bias,
+                              float *delta, void *stream);
 /* LN parameter gradients: dgamma[c] = sum_r dY*xhat, dbeta[c] = sum_r dY (c < d) and, when
  * dbias != NULL, dbias[c] = sum_r dZdrop[r, c] (bias of the linear whose output was dropped into
  * the residual: out_proj.bias for norm1, linear2.bias for norm2).  Deterministic two-pass column

@@ -405,6 +405,44 @@ def test_gather_pack_colsum():
     assert rel_err(out, ref) < 1e-5
 
 
+@pytest.mark.parametrize("N,Np,d,dp,p", [(470, 512, 367, 384, 0.5), (300, 320, 19, 64, 0.3), (200, 256, 65, 128, 0.0)])
+def test_layernorm_bwd_delta_equals_rowdot(N, Np, d, dp, p):
+    """LayerNorm1's backward with the attention delta (ABI v8): dZ / dZdrop bit-identical to
+    layernorm_bwd, and delta = sum_c dZdrop * ((Z - X)(1-p) - b_o) equal to rowdot(dO, O) with
+    dO = dZdrop W_o (fp32 products; 1e-5 of the row scale), 0 on padded rows."""
+    seed = 321
+    O = torch.zeros(Np, dp, device=DEV)
+    O[:N, :d] = _mk(N, d, seed=71)
+    X = torch.zeros(Np, dp, device=DEV)
+    X[:N, :d] = _mk(N, d, seed=72)
+    Wo = torch.zeros(dp, dp, device=DEV)
+    Wo[:d, :d] = _mk(d, d, seed=73) / math.sqrt(d)
+    bo = torch.zeros(dp, device=DEV)
+    bo[:d] = _mk(d, seed=74) * 0.1
+    Z = torch.empty(Np, dp, device=DEV)   # the executor's out-projection: Z = X + drop(O W_o^T + b_o)
+    K.gemm(O, Wo, Z, Np, dp, dp, dp, dp, dp, trans_b=True, epilogue=_lib.EPI_BIAS_DROP_RESID, bias=bo, aux0=X,
+           ld_aux=dp, p_drop=p, seed=seed)
+    gam = _mk(d, seed=75)
+    bet = _mk(d, seed=76)
+    Y, mean, rstd = torch.empty(Np, dp, device=DEV), torch.empty(Np, device=DEV), torch.empty(Np, device=DEV)
+    K.layernorm_fwd(Z, dp, gam, bet, Y, dp, mean, rstd, N, Np, d, dp)
+    dY = torch.zeros(Np, dp, device=DEV)
+    dY[:N, :d] = _mk(N, d, seed=77)
+    dZ1, dA1, dZ2, dA2 = (torch.full((Np, dp), float("nan"), device=DEV) for _ in range(4))
+    K.layernorm_bwd(dY, dp, Z, dp, mean, rstd, gam, dZ1, dp, dA1, dp, p, seed, N, Np, d, dp)
+    delta = torch.full((Np,), float("nan"), device=DEV)
+    K.layernorm_bwd_delta(dY, dp, Z, dp, mean, rstd, gam, dZ2, dp, dA2, dp, p, seed, N, Np, d, dp, X, dp, bo, delta)
+    assert torch.equal(dZ1, dZ2) and torch.equal(dA1, dA2)
+    dO = dA2.double() @ Wo.double()
+    ref = (dO * O.double()).sum(1)
+    scale = ((dO.abs() * O.double().abs()).sum(1)).max().item()
+    assert (delta.double() - ref).abs().max().item() < 1e-5 * scale
+    assert delta[N:].abs().max().item() == 0
+    with pytest.raises(_lib.U2GNNNativeError):
+        K.layernorm_bwd_delta(dY, dp, Z, dp, mean, rstd, gam, dZ2, dp, dA2, dp, p, seed, N, Np, d, dp, X[:, 1:], dp,
+                              bo, delta)   # misaligned X
+
+
 def test_pack_multi_c4_shapes_equal_single_jobs():
     """The batched pack (8 rows per block, 32-bit maps) writes exactly what one pack_padded launch per
     job writes: C4's in-projection (3 row blocks), FFN weights, a bias row with 3 column blocks, and a

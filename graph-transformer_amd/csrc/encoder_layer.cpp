@@ -421,9 +421,18 @@ int layer_fwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
     // a3.1 in-projection (+bias, Q scaled by 1/sqrt(d))
     {
         G g(X, w->W_in, c.QKV, Np, 3 * dp, dp, dp, dp, 3 * dp, prec);
-        // 256x128 blocks once they fill the chip (C4: 19 x 9); the 64 tile below that
-        g.tb().epi(U2GNN_EPI_BIAS).tile(prec != U2GNN_PREC_F32 && Np % 256 == 0 && (Np / 256) * (3 * dp / 128) >= 128
-                                            ? 256 : 0);
+        // 256x128 blocks from 3 waves of them on (token-sized rows, neighbour mode), the default tile
+        // rule below that: C4's 19 x 9 blocks of 256x128 leave a third of the CUs idle, its 76 x 18 64-tile
+        // blocks run the step 0.8 % faster (3/3 reps, profiles/r02/qkv_tile_ab.txt; bit-identical).
+        // U2GNN_QKV_TILE (A/B) forces a tile code (the Python engine mirrors both)
+        static const int qkv_tile_env = [] {
+            const char *e = std::getenv("U2GNN_QKV_TILE");
+            return e && e[0] ? std::atoi(e) : -1;
+        }();
+        const int qkv_tile = qkv_tile_env >= 0 ? qkv_tile_env
+                             : (prec != U2GNN_PREC_F32 && Np % 256 == 0 &&
+                                (Np / 256) * (3 * dp / 128) >= U2GNN_BIG_TILE_BLOCKS) ? 256 : 0;
+        g.tb().epi(U2GNN_EPI_BIAS).tile(qkv_tile);
         g.a.bias = w->b_in;
         g.a.alpha = (float)(1.0 / std::sqrt((double)d));
         g.a.scale_cols = dp;

@@ -395,7 +395,7 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_bf16_kernel(GemmP P) {
     };
 
     PreDS<TN> pre;
-    const bool use_pre = (EPI == U2GNN_EPI_ATTN_DS && P.keep != nullptr) || EPI == U2GNN_EPI_ATTN_DS_SIGNED;
+    const bool use_pre = (EPI == U2GNN_EPI_ATTN_DS && P.keep != nullptr) || ds_signed<EPI>;
     if (use_pre) prefetch_ds<EPI>(P, m0 + wm * WTM + li, n0 + wn * WTN, kh, pre);
     if (nk > 0) {
         // two register stages: every tile's global loads are in flight across TWO compute phases
@@ -472,9 +472,14 @@ int launch_epi(const GemmP &P, int epi, int split, bool clamp_a, hipStream_t st)
         U2GNN_CASE(U2GNN_EPI_RELU_DROP_BWD)
         U2GNN_CASE(U2GNN_EPI_ACCUM)
         U2GNN_CASE(U2GNN_EPI_ATTN_DS)
-        U2GNN_CASE(U2GNN_EPI_ATTN_DS_SIGNED)
         U2GNN_CASE(U2GNN_EPI_STORE_ROWDOT)
 #undef U2GNN_CASE
+        case U2GNN_EPI_ATTN_DS_SIGNED:   // delta as STORE_ROWDOT partials: its own instantiation
+            if (P.rowvec_parts > 1)
+                launch_kernel<KIND, BM, BN, VAR, TA, TB, EPI_DS_SIGNED_PARTS>(P, grid, st);
+            else
+                launch_kernel<KIND, BM, BN, VAR, TA, TB, U2GNN_EPI_ATTN_DS_SIGNED>(P, grid, st);
+            break;
         case U2GNN_EPI_BIAS_DROP_RESID_LN:   // row-complete 64 x 64 blocks, NT, bf16 kinds only
             if constexpr (KIND != U2GNN_PREC_F32 && BM == 64 && BN == 64 && !TA && TB)
                 launch_kernel<KIND, BM, BN, VAR, TA, TB, U2GNN_EPI_BIAS_DROP_RESID_LN>(P, grid, st);

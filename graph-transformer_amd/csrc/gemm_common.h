@@ -38,7 +38,7 @@ struct GemmP {
     int64_t ln_ldy;
     int32_t ln_d, ln_rows;
     float ln_eps;
-    // EPI_STORE_ROWDOT: per-32-column-group row partials of C*aux0; ATTN_DS_SIGNED: rowvec_parts of them
+    // EPI_STORE_ROWDOT: per-64-column-group row partials of C*aux0; EPI_DS_SIGNED_PARTS: rowvec_parts of them
     float *rowpart;
     int64_t ld_rowpart;
     int32_t rowvec_parts;
@@ -48,6 +48,12 @@ struct GemmP {
 namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// Internal epilogue template code (not an ABI value): ATTN_DS_SIGNED with delta given as rowvec_parts
+// STORE_ROWDOT partials.  A separate instantiation, so that the plain ATTN_DS_SIGNED kernel (the C4
+// dS product) keeps its registers and schedule: carrying the partials there cost it ~10 % (113 -> 124 us).
+constexpr int EPI_DS_SIGNED_PARTS = 100;
+template <int EPI> constexpr bool ds_signed = EPI == U2GNN_EPI_ATTN_DS_SIGNED || EPI == EPI_DS_SIGNED_PARTS;
 
 
 
@@ -62,7 +68,7 @@ __device__ __forceinline__ float4 ld4(const float *p) { return *reinterpret_cast
 // 4 columns.
 template <int EPI>
 __device__ __forceinline__ void epi_fetch(const GemmP &P, int row, int col, float4 &a, float4 &b, uint32_t &kb) {
-    if constexpr (EPI == U2GNN_EPI_ATTN_DS_SIGNED || EPI == U2GNN_EPI_ATTN_DS_RECOMP) {
+    if constexpr (ds_signed<EPI> || EPI == U2GNN_EPI_ATTN_DS_RECOMP) {
         a = ld4(P.aux0 + (int64_t)row * P.ld_aux + col);
     } else if constexpr (EPI == U2GNN_EPI_ATTN_DS) {
         const int64_t o = (int64_t)row * P.ld_aux + col;
@@ -87,7 +93,7 @@ __device__ __forceinline__ float4 epilogue4(const GemmP &P, int row, int col, fl
                                             uint32_t kb, float dl) {
     if constexpr (EPI == U2GNN_EPI_STORE || EPI == U2GNN_EPI_STORE_ROWDOT) {
         return make_float4(P.alpha * v.x, P.alpha * v.y, P.alpha * v.z, P.alpha * v.w);
-    } else if constexpr (EPI == U2GNN_EPI_ATTN_DS_SIGNED) {
+    } else if constexpr (ds_signed<EPI>) {
         // x = Pd = P/(1-p) where kept (sign clear), x = -P where dropped (sign set):
         // dS = P*(keep*dPd/(1-p) - delta) = kept ? x*(dPd - (1-p)*delta) : x*delta
         const float q = (1.f - P.p) * dl;
@@ -172,7 +178,7 @@ struct EpiSlice {
     float4 a[TN][4], b[TN][4];
     uint32_t kb[TN][4];
     float dl;
-    DeltaParts dp;    // ATTN_DS_SIGNED: dl = delta_sum(dp) when the slice is stored
+    DeltaParts dp;    // EPI_DS_SIGNED_PARTS: dl = delta_sum(dp) when the slice is stored
     float rm, rinv;   // ATTN_DS_RECOMP: forward softmax row max and 1/sum
 };
 
@@ -186,8 +192,9 @@ __device__ __forceinline__ void fetch_slice(const GemmP &P, int row, int c0, int
             e.kb[j][g] = 0;
             epi_fetch<EPI>(P, row, c0 + j * 32 + 8 * g + 4 * kh, e.a[j][g], e.b[j][g], e.kb[j][g]);
         }
-    e.dl = (EPI == U2GNN_EPI_ATTN_DS || EPI == U2GNN_EPI_ATTN_DS_RECOMP) ? P.rowvec[row] : 0.f;
-    if constexpr (EPI == U2GNN_EPI_ATTN_DS_SIGNED) delta_load(P, row, e.dp);
+    e.dl = (EPI == U2GNN_EPI_ATTN_DS || EPI == U2GNN_EPI_ATTN_DS_SIGNED || EPI == U2GNN_EPI_ATTN_DS_RECOMP)
+               ? P.rowvec[row] : 0.f;
+    if constexpr (EPI == EPI_DS_SIGNED_PARTS) delta_load(P, row, e.dp);
     if constexpr (EPI == U2GNN_EPI_ATTN_DS_RECOMP) {
         const float2 st = P.rowstat[row];
         e.rm = st.x, e.rinv = st.y;
@@ -224,7 +231,7 @@ __device__ __forceinline__ float store_slice(const GemmP &P, float *C, const f32
     uint32_t rkey = 0;
     if constexpr (EPI == U2GNN_EPI_ATTN_DS_RECOMP) rkey = u2gnn_row_key(P.seed, (uint32_t)row);
     float dl = e.dl;
-    if constexpr (EPI == U2GNN_EPI_ATTN_DS_SIGNED) dl = delta_sum(P, row, e.dp);
+    if constexpr (EPI == EPI_DS_SIGNED_PARTS) dl = delta_sum(P, row, e.dp);
     float rs = 0.f;
 #pragma unroll
     for (int j = 0; j < TN; ++j)
@@ -266,7 +273,7 @@ __device__ __forceinline__ void prefetch_ds(const GemmP &P, int row, int c0, int
 #pragma unroll
         for (int g = 0; g < 4; ++g) f.p[j][g] = ld4(P.aux0 + (int64_t)row * P.ld_aux + c0 + j * 32 + 8 * g + 4 * kh);
     }
-    if constexpr (EPI == U2GNN_EPI_ATTN_DS_SIGNED) delta_load(P, row, f.dp);
+    if constexpr (EPI == EPI_DS_SIGNED_PARTS) delta_load(P, row, f.dp);
     else f.dl = P.rowvec[row];
 }
 
@@ -364,7 +371,7 @@ __device__ __forceinline__ void store_tile(const GemmP &P, float *C, const f32x1
         store_tile_ln<TM, TN>(P, C, acc, r0, c0, li, kh);
         return;
     }
-    if constexpr (EPI == U2GNN_EPI_ATTN_DS_SIGNED) {
+    if constexpr (ds_signed<EPI>) {
         // every slice's probability image is requested before the first store (slice 0 usually
         // prefetched before the main loop): one exposed round trip per tile instead of one per slice
         EpiSlice<EPI, TN> e[TM];

@@ -191,6 +191,8 @@ _ROWDOT_FUSE = os.environ.get("U2GNN_ROWDOT_FUSE", "0") == "1"
 # U2GNN_LN_DELTA=0 (A/B; encoder_layer.cpp ln_delta_on): delta by its own rowdot launch instead of LayerNorm1's
 # backward (layernorm_bwd_delta)
 _LN_DELTA = os.environ.get("U2GNN_LN_DELTA", "1") != "0"
+# U2GNN_QKV_TILE (A/B; encoder_layer.cpp): force the in-projection GEMM's tile code
+_QKV_TILE = int(os.environ.get("U2GNN_QKV_TILE", "-1") or -1)
 
 
 def fused_ln(dp: int, prec: str) -> bool:
@@ -334,7 +336,8 @@ def encoder_layer_forward(X: torch.Tensor, w: PackedLayer, p: LayerParams, dims:
     QKV = torch.empty(Np, 3 * dp, device=dev, dtype=f32)
     K.gemm(X, w.W_in, QKV, Np, 3 * dp, dp, dp, dp, 3 * dp, trans_b=True, epilogue=E.EPI_BIAS, bias=w.b_in,
            alpha=1.0 / math.sqrt(d), scale_cols=dp, precision=_rp("in_proj", prec), flops=6.0 * N * d * d,
-           tile=256 if (prec != "fp32" and Np % 256 == 0 and (Np // 256) * (3 * dp // 128) >= 128) else 0)
+           tile=_QKV_TILE if _QKV_TILE >= 0 else
+           (256 if (prec != "fp32" and Np % 256 == 0 and (Np // 256) * (3 * dp // 128) >= BIG_TILE_BLOCKS) else 0))
     Q, Kt, V = QKV[:, :dp], QKV[:, dp:2 * dp], QKV[:, 2 * dp:]
     S = torch.empty(Np, Np, device=dev, dtype=f32)
     K.gemm(Q, Kt, S, Np, Np, dp, 3 * dp, 3 * dp, Np, trans_b=True, precision=_rp("qk", prec), flops=att,

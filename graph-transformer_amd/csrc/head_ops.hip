@@ -12,33 +12,45 @@ namespace {
 // a5/a6 pooling: torch.spmm(graph_pool, output_Tr) with graph_pool in CSR form
 // (pytorch_U2GNN_Sup.py:41) followed by dropout (:42).  Block = one graph x 64 columns.
 // ------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) pool_fwd_kernel(const float *X, int64_t ldx, const int64_t *rowptr,
-                                                       const int64_t *colidx, const float *vals, float *G, int64_t ldg,
-                                                       int64_t d, float p, uint64_t seed, const uint64_t *seed_epoch) {
+// block = (graph, 64-column chunk); POOL_WAVES waves split the graph's rows, each with 4 rows' index,
+// weight and feature loads in flight (the per-row chain colidx -> X is latency-bound: a COLLAB graph's
+// ~75 rows over 4 waves of 1 load each took 14 us per C4 launch)
+constexpr int POOL_WAVES = 8;
+
+__global__ void __launch_bounds__(64 * POOL_WAVES) pool_fwd_kernel(const float *X, int64_t ldx, const int64_t *rowptr,
+                                                                   const int64_t *colidx, const float *vals, float *G,
+                                                                   int64_t ldg, int64_t d, float p, uint64_t seed,
+                                                                   const uint64_t *seed_epoch) {
     seed = u2gnn_seed(seed, seed_epoch);
-    // block = (graph, 64-column chunk); the 4 waves split the graph's rows
-    __shared__ float red[4][64];
+    __shared__ float red[POOL_WAVES][64];
     const int64_t b = blockIdx.x;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int64_t e0 = rowptr[b], e1 = rowptr[b + 1];
-    {
-        const int64_t c0 = (int64_t)blockIdx.y * 64;
-        const int64_t c = c0 + lane;
-        float s[4] = {0.f, 0.f, 0.f, 0.f};
-        if (c < d) {
-            int64_t e = e0 + w;
-            for (; e + 12 < e1; e += 16)
+    const int64_t c = (int64_t)blockIdx.y * 64 + lane;
+    float s[4] = {0.f, 0.f, 0.f, 0.f};
+    if (c < d) {
+        constexpr int NW = POOL_WAVES;
+        int64_t e = e0 + w;
+        for (; e + 3 * NW < e1; e += 4 * NW) {
+            int64_t r[4];
+            float v[4], x[4];
 #pragma unroll
-                for (int j = 0; j < 4; ++j) s[j] += vals[e + 4 * j] * X[colidx[e + 4 * j] * ldx + c];
-            for (; e < e1; e += 4) s[0] += vals[e] * X[colidx[e] * ldx + c];
+            for (int j = 0; j < 4; ++j) r[j] = colidx[e + j * NW], v[j] = vals[e + j * NW];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) x[j] = X[r[j] * ldx + c];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) s[j] += v[j] * x[j];
         }
-        red[w][lane] = (s[0] + s[1]) + (s[2] + s[3]);
-        __syncthreads();
-        if (w == 0 && c < d) {
-            float v = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
-            if (p > 0.f) v = u2gnn_keep(seed, (uint32_t)b, (uint32_t)c, p) ? v * (1.f / (1.f - p)) : 0.f;
-            G[b * ldg + c] = v;
-        }
+        for (; e < e1; e += NW) s[0] += vals[e] * X[colidx[e] * ldx + c];
+    }
+    red[w][lane] = (s[0] + s[1]) + (s[2] + s[3]);
+    __syncthreads();
+    if (w == 0 && c < d) {
+        float v = 0.f;
+#pragma unroll
+        for (int q = 0; q < POOL_WAVES; ++q) v += red[q][lane];
+        if (p > 0.f) v = u2gnn_keep(seed, (uint32_t)b, (uint32_t)c, p) ? v * (1.f / (1.f - p)) : 0.f;
+        G[b * ldg + c] = v;
     }
 }
 
@@ -359,7 +371,7 @@ extern "C" {
 int u2gnn_pool_fwd(const float *X, int64_t ldx, const int64_t *rowptr, const int64_t *colidx, const float *vals,
                    float *G, int64_t ldg, int64_t B, int64_t d, float p, uint64_t seed, void *stream) {
     if (!X || !rowptr || !colidx || !vals || !G || B < 1 || d < 1) return U2GNN_E_ARG;
-    hipLaunchKernelGGL(pool_fwd_kernel, dim3((unsigned)B, (unsigned)((d + 63) / 64)), dim3(256), 0,
+    hipLaunchKernelGGL(pool_fwd_kernel, dim3((unsigned)B, (unsigned)((d + 63) / 64)), dim3(64 * POOL_WAVES), 0,
                        u2gnn_stream(stream), X, ldx, rowptr, colidx, vals, G, ldg, d, p, seed, u2gnn_g_epoch);
     return u2gnn_launch_status();
 }

@@ -72,6 +72,35 @@ __global__ void __launch_bounds__(256) pool_bwd_kernel(const float *dGd, int64_t
     }
 }
 
+// Pool backward for block-row pools (every row index appears once in colidx[0, N), N = rowptr[B]):
+// plain stores instead of atomics into a zero-filled buffer.  Blocks x < B write their graph's rows,
+// columns >= d as 0; blocks x >= B zero the padding rows [N, rows_pad), one row per wave.
+__global__ void __launch_bounds__(256) pool_bwd_rows_kernel(const float *dGd, int64_t ldg, const int64_t *rowptr,
+                                                            const int64_t *colidx, const float *vals, float *dX,
+                                                            int64_t ldx, int64_t B, int64_t d, int64_t d_pad, int64_t N,
+                                                            int64_t rows_pad, float p, uint64_t seed,
+                                                            const uint64_t *seed_epoch) {
+    seed = u2gnn_seed(seed, seed_epoch);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t c = (int64_t)blockIdx.z * 64 + lane;
+    if (c >= d_pad) return;
+    const int64_t waves = (int64_t)gridDim.y * 4;
+    if ((int64_t)blockIdx.x < B) {
+        const int64_t b = blockIdx.x;
+        const int64_t e0 = rowptr[b], e1 = rowptr[b + 1];
+        float g = 0.f;
+        if (c < d) {
+            g = dGd[b * ldg + c];
+            if (p > 0.f) g = u2gnn_keep(seed, (uint32_t)b, (uint32_t)c, p) ? g * (1.f / (1.f - p)) : 0.f;
+        }
+        for (int64_t e = e0 + (int64_t)blockIdx.y * 4 + w; e < e1; e += waves)
+            dX[colidx[e] * ldx + c] = c < d ? vals[e] * g : 0.f;
+    } else {
+        const int64_t r = N + ((int64_t)blockIdx.x - B) * waves + (int64_t)blockIdx.y * 4 + w;
+        if (r < rows_pad) dX[r * ldx + c] = 0.f;
+    }
+}
+
 // head: scores[b, k] (+)= G[b,:] . W[k,:] + bias[k];  one wave per (b, k)
 __global__ void __launch_bounds__(256) head_fwd_kernel(const float *G, int64_t ldg, const float *W, const float *bias,
                                                        float *scores, int64_t B, int64_t C, int64_t d, int accumulate) {
@@ -99,6 +128,13 @@ __global__ void __launch_bounds__(256) head_bwd_kernel(const float *dS, const fl
         const int64_t u = t - B * d, k = u / d, j = u - k * d;
         float s[4] = {0.f, 0.f, 0.f, 0.f};
         int64_t b = 0;
+        for (; b + 16 <= B; b += 16) {   // 16 rows' loads in flight; s[q] still sums b = q mod 4 in order
+            float x[16], y[16];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) x[q] = dS[(b + q) * C + k], y[q] = G[(b + q) * ldg + j];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) s[q & 3] += x[q] * y[q];
+        }
         for (; b + 4 <= B; b += 4)
 #pragma unroll
             for (int q = 0; q < 4; ++q) s[q] += dS[(b + q) * C + k] * G[(b + q) * ldg + j];
@@ -381,6 +417,19 @@ int u2gnn_pool_bwd(const float *dGd, int64_t ldg, const int64_t *rowptr, const i
     if (!dGd || !rowptr || !colidx || !vals || !dX || B < 1 || d < 1) return U2GNN_E_ARG;
     hipLaunchKernelGGL(pool_bwd_kernel, dim3((unsigned)B, 8, (unsigned)((d + 63) / 64)), dim3(256), 0,
                        u2gnn_stream(stream), dGd, ldg, rowptr, colidx, vals, dX, ldx, d, p, seed, u2gnn_g_epoch);
+    return u2gnn_launch_status();
+}
+
+int u2gnn_pool_bwd_rows(const float *dGd, int64_t ldg, const int64_t *rowptr, const int64_t *colidx,
+                        const float *vals, float *dX, int64_t ldx, int64_t B, int64_t d, int64_t d_pad, int64_t N,
+                        int64_t rows_pad, float p, uint64_t seed, void *stream) {
+    if (!dGd || !rowptr || !colidx || !vals || !dX || B < 1 || d < 1 || d > d_pad || d_pad > ldx || N < 0 ||
+        N > rows_pad)
+        return U2GNN_E_ARG;
+    const int64_t zb = (rows_pad - N + 31) / 32;   // padding-row blocks: 8 x 4 waves, one row each
+    hipLaunchKernelGGL(pool_bwd_rows_kernel, dim3((unsigned)(B + zb), 8, (unsigned)((d_pad + 63) / 64)), dim3(256), 0,
+                       u2gnn_stream(stream), dGd, ldg, rowptr, colidx, vals, dX, ldx, B, d, d_pad, N, rows_pad, p,
+                       seed, u2gnn_g_epoch);
     return u2gnn_launch_status();
 }
 

@@ -128,6 +128,7 @@ _HIP_SIGS = {
     "u2gnn_pack_padded_multi": ([VP, I32, VP], c_int32),
     "u2gnn_pool_fwd": ([VP, I64, VP, VP, VP, VP, I64, I64, I64, F32, c_uint64, VP], c_int32),
     "u2gnn_pool_bwd": ([VP, I64, VP, VP, VP, VP, I64, I64, I64, F32, c_uint64, VP], c_int32),
+    "u2gnn_pool_bwd_rows": ([VP, I64, VP, VP, VP, VP, I64, I64, I64, I64, I64, I64, F32, c_uint64, VP], c_int32),
     "u2gnn_head_fwd": ([VP, I64, VP, VP, VP, I64, I64, I64, I32, VP], c_int32),
     "u2gnn_head_bwd": ([VP, VP, I64, VP, VP, I64, VP, VP, I64, I64, I64, I32, VP], c_int32),
     "u2gnn_smoothed_ce": ([VP, VP, I64, I64, F32, VP, VP, VP], c_int32),

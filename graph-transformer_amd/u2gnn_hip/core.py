@@ -63,6 +63,9 @@ class DeviceBatch:
     # int32[1] device flag the gather / scatter kernels set on an out-of-range input_x entry (they
     # read and write nothing there); the constructors validate input_x up front, so it stays 0
     err: Optional[torch.Tensor] = None
+    # True when colidx is 0..N-1 in order (batches built from offsets, _pool_iota): the pool backward
+    # then stores every row of its output (u2gnn_pool_bwd_rows) instead of accumulating into zeros
+    block_rows: bool = False
 
     def __post_init__(self):
         if self.err is None:
@@ -91,7 +94,7 @@ class DeviceBatch:
         lab = None if labels is None else torch.as_tensor(labels, dtype=torch.int64).to(dev, non_blocking=True)
         iy = None if input_y is None else torch.as_tensor(input_y, dtype=torch.int64).to(dev, non_blocking=True)
         return DeviceBatch(N, B, ix, X, off.to(dev), torch.arange(N, device=dev, dtype=torch.int64),
-                           torch.ones(N, device=dev, dtype=torch.float32), lab, iy)
+                           torch.ones(N, device=dev, dtype=torch.float32), lab, iy, block_rows=True)
 
     @staticmethod
     def from_store(hb, X_dev: torch.Tensor, device="cuda"):
@@ -129,7 +132,7 @@ class DeviceBatch:
                 t.record_stream(main)
             iy = gnode if hb.input_y is not None else None
             colidx, vals = _pool_iota(N, dev)
-            return DeviceBatch(N, B, ix, X, off, colidx, vals, lab, iy, err)
+            return DeviceBatch(N, B, ix, X, off, colidx, vals, lab, iy, err, block_rows=True)
         if slot is not None:
             k1 = hb.input_x.shape[1]
             h2d = lambda t: t.to(dev, non_blocking=True)  # noqa: E731
@@ -148,7 +151,7 @@ class DeviceBatch:
         if N:
             K.gather_rows(X_dev, gnode, 1, X, N, N, d, d)
         colidx, vals = _pool_iota(N, dev)
-        return DeviceBatch(N, B, ix, X, off, colidx, vals, lab, iy)
+        return DeviceBatch(N, B, ix, X, off, colidx, vals, lab, iy, block_rows=True)
 
     @staticmethod
     def from_reference_inputs(input_x, graph_pool, X_concat, labels=None):
@@ -172,6 +175,10 @@ def _check_range_host(input_x, N: int):
     a = input_x.numpy() if isinstance(input_x, torch.Tensor) else np.asarray(input_x)
     if a.size and (int(a.min()) < 0 or int(a.max()) >= N):
         raise IndexError("index out of range in self (input_x entry outside [0, N))")
+
+
+# U2GNN_POOL_ROWS=0 (A/B): the accumulating pool backward into a zero-filled buffer for every batch
+_POOL_ROWS = os.environ.get("U2GNN_POOL_ROWS", "1") != "0"
 
 
 class EncoderStack:
@@ -370,8 +377,12 @@ class SupCore:
             dG = torch.empty(b.B, dp, device=dev, dtype=torch.float32)
             K.head_bwd(dscores, G, dp, self.m.predictions[l].weight, dG, dp, grads[f"predictions.{l}.weight"],
                        grads[f"predictions.{l}.bias"], b.B, self.C, d)
-            dX = torch.zeros(Np, dp, device=dev, dtype=torch.float32)
-            K.pool_bwd(dG, dp, b.rowptr, b.colidx, b.vals, dX, dp, b.B, d, ctx["ph"], hs)
+            if b.block_rows and _POOL_ROWS:   # every row stored: no zero fill, no atomics
+                dX = torch.empty(Np, dp, device=dev, dtype=torch.float32)
+                K.pool_bwd_rows(dG, dp, b.rowptr, b.colidx, b.vals, dX, dp, b.B, d, dp, b.N, Np, ctx["ph"], hs)
+            else:
+                dX = torch.zeros(Np, dp, device=dev, dtype=torch.float32)
+                K.pool_bwd(dG, dp, b.rowptr, b.colidx, b.vals, dX, dp, b.B, d, ctx["ph"], hs)
             return dX
         return self.stack.backward(ctx["stack"], ext, grads)
 

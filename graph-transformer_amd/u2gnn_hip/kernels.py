@@ -283,6 +283,14 @@ def pool_fwd(X, ldx, rowptr, colidx, vals, G, ldg, B, d, p, seed):
                                    int(d), float(p), int(seed), _s()), "u2gnn_pool_fwd")
 
 
+def pool_bwd_rows(dG, ldg, rowptr, colidx, vals, dX, ldx, B, d, d_pad, N, rows_pad, p, seed):
+    """Block-row pool backward with plain stores (every row of dX[:rows_pad, :d_pad] written)."""
+    _dev(dG, rowptr, colidx, vals, dX)
+    check(hip_lib().u2gnn_pool_bwd_rows(_p(dG), int(ldg), _p(rowptr), _p(colidx), _p(vals), _p(dX), int(ldx), int(B),
+                                        int(d), int(d_pad), int(N), int(rows_pad), float(p), int(seed), _s()),
+          "u2gnn_pool_bwd_rows")
+
+
 def pool_bwd(dG, ldg, rowptr, colidx, vals, dX, ldx, B, d, p, seed):
     _dev(dG, rowptr, colidx, vals, dX)
     check(hip_lib().u2gnn_pool_bwd(_p(dG), int(ldg), _p(rowptr), _p(colidx), _p(vals), _p(dX), int(ldx), int(B),

@@ -249,6 +249,12 @@ int u2gnn_pool_fwd(const float *X, int64_t ldx, const int64_t *rowptr, const int
 int u2gnn_pool_bwd(const float *dGd, int64_t ldg, const int64_t *rowptr, const int64_t *colidx,
                    const float *vals, float *dX, int64_t ldx, int64_t B, int64_t d, float p,
                    uint64_t seed, void *stream);
+/* ABI v8: pool backward for block-row pools, whose colidx[0, N) (N = rowptr[B]) holds every row index
+ * 0..N-1 once: dX[colidx[e], c] = vals[e] * dGd[b, c] * keep/(1-p) for c < d, 0 for d <= c < d_pad,
+ * and rows N..rows_pad-1 = 0 -- plain stores, so dX needs no zero fill (u2gnn_pool_bwd accumulates). */
+int u2gnn_pool_bwd_rows(const float *dGd, int64_t ldg, const int64_t *rowptr, const int64_t *colidx,
+                        const float *vals, float *dX, int64_t ldx, int64_t B, int64_t d, int64_t d_pad,
+                        int64_t N, int64_t rows_pad, float p, uint64_t seed, void *stream);
 /* scores[b, c] (+)= sum_j G[b, j] W[c, j] + bias[c]   (W real [C, d]) */
 int u2gnn_head_fwd(const float *G, int64_t ldg, const float *W, const float *bias, float *scores,
                    int64_t B, int64_t C, int64_t d, int32_t accumulate, void *stream);

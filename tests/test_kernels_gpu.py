@@ -559,6 +559,32 @@ def test_pool_head_ce():
     assert abs(loss.item() - lref.item()) < 1e-5 and rel_err(ds, s.grad) < 1e-5
 
 
+@pytest.mark.parametrize("B,N,Np,d,dp,p", [(4, 100, 128, 10, 64, 0.3), (64, 4776, 4864, 367, 384, 0.5),
+                                            (3, 256, 256, 65, 128, 0.0)])
+def test_pool_bwd_rows_equals_accumulating_pool_bwd(B, N, Np, d, dp, p):
+    """ABI v8 block-row pool backward (plain stores, no zero fill) == the accumulating kernel into a
+    zero-filled buffer: graph rows, padding columns d..dp and padding rows N..Np; and head_bwd's
+    16-deep load batches leave its dW / db / dG equal to a float64 reference."""
+    g = torch.Generator().manual_seed(5)
+    cuts = torch.sort(torch.randperm(N - 1, generator=g)[:B - 1] + 1).values
+    off = torch.cat([torch.tensor([0]), cuts, torch.tensor([N])]).to(DEV)
+    col = torch.arange(N, device=DEV)
+    vals = torch.rand(N, generator=g).to(DEV) + 0.5
+    dG = _mk(B, dp, seed=81)
+    ref = torch.zeros(Np, dp, device=DEV)
+    K.pool_bwd(dG, dp, off, col, vals, ref, dp, B, d, p, 17)
+    out = torch.full((Np, dp), float("nan"), device=DEV)
+    K.pool_bwd_rows(dG, dp, off, col, vals, out, dp, B, d, dp, N, Np, p, 17)
+    assert torch.equal(out, ref)
+    C = 3
+    G, W, dS = _mk(B, dp, seed=82), _mk(C, d, seed=83), _mk(B, C, seed=84)
+    dGo, dW, db = torch.empty(B, dp, device=DEV), torch.empty(C, d, device=DEV), torch.empty(C, device=DEV)
+    K.head_bwd(dS, G, dp, W, dGo, dp, dW, db, B, C, d)
+    assert rel_err(dW.double(), dS.double().t() @ G[:, :d].double()) < 1e-5
+    assert rel_err(db.double(), dS.double().sum(0)) < 1e-5
+    assert rel_err(dGo[:, :d].double(), dS.double() @ W.double()) < 1e-5
+
+
 def test_adam_matches_torch():
     n = 1000
     p0 = _mk(n, seed=21)

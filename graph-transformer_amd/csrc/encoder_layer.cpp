@@ -161,11 +161,16 @@ bool shallow_nosplit_on() {   // engine._SHALLOW_NOSPLIT
     return v;
 }
 
+bool event_pool_on();
+hipEvent_t pooled_event();
+
 // engine._gemm_split: deterministic split-K into fp32 slabs + one reduce pass (alpha, accumulate,
-// padded->real block map).  deep = weight gradient (16-deep K step, <= 8 slabs).
+// padded->real block map).  deep = weight gradient (16-deep K step, <= 8 slabs).  red_st: run the
+// reduce pass on that stream after the GEMM (pooled fork event; the caller joins it back).
 int gemm_split(Arena &W, const Dims &D, const float *A, const float *B, float *C, int64_t M, int64_t N, int64_t Kd,
                int64_t lda, int64_t ldb, int64_t ldc, bool ta, float alpha, bool accumulate, const int64_t *rblk,
-               const int64_t *cblk, bool deep, hipStream_t st, bool clamp_a = false, int prec = -1, int role = 0) {
+               const int64_t *cblk, bool deep, hipStream_t st, bool clamp_a = false, int prec = -1, int role = 0,
+               hipStream_t red_st = nullptr) {
     if (prec < 0) prec = D.prec;
     const bool f32 = prec == U2GNN_PREC_F32;
     const int64_t bk = f32 ? 16 : 32;
@@ -242,8 +247,15 @@ int gemm_split(Arena &W, const Dims &D, const float *A, const float *B, float *C
     if (plan) return U2GNN_OK;
     const int64_t rb0 = rblk ? rblk[0] : M, rb1 = rblk ? rblk[1] : M;
     const int64_t cb0 = cblk ? cblk[0] : N, cb1 = cblk ? cblk[1] : N;
+    hipStream_t rs = st;
+    if (red_st && red_st != st) {
+        hipEvent_t ev = pooled_event();
+        if (!ev) return U2GNN_E_ARG;
+        if (hipEventRecord(ev, st) != hipSuccess || hipStreamWaitEvent(red_st, ev, 0) != hipSuccess) return U2GNN_E_ARG;
+        rs = red_st;
+    }
     return u2gnn_slab_reduce(slabs, (int32_t)split, M * N, M, N, N, rb0, rb1, cb0, cb1, C, ldc, alpha,
-                             accumulate ? 1 : 0, st);
+                             accumulate ? 1 : 0, rs);
 }
 
 // engine._wgrad: dst(real) = unpack(dY^T X)
@@ -627,8 +639,13 @@ int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
             U2GNN_TRY(sd.mark(&dv_done));   // dV and dK
             U2GNN_TRY(in_part(1));
         }
+        // U2GNN_DQ_REDUCE_SIDE=1 (A/B): dQ's split-K reduce on the side stream (behind dV), so that dK
+        // starts right after the dQ GEMM; the join before the in-projection covers it
+        static const bool dq_red_env = env_flag("U2GNN_DQ_REDUCE_SIDE", false);
+        const bool dq_red_side = dv_side && event_pool_on() && dq_red_env;
         U2GNN_TRY(gemm_split(W, D, dS, Kt, dQKV, Np, dp, Np, Np, 3 * dp, 3 * dp, false, q_scale, false, nullptr, nullptr,
-                             false, st, false, D.prec_ab, U2GNN_ROLE_DQ));
+                             false, st, false, D.prec_ab, U2GNN_ROLE_DQ, dq_red_side ? so : nullptr));
+        if (dq_red_side && !plan) U2GNN_TRY(sd.mark(&dv_done));   // dV (, dK) and the dQ reduce
         U2GNN_TRY(sd.fork());
         U2GNN_TRY(in_part(0));
         if (!dk_side) {

@@ -1113,6 +1113,15 @@ int u2gnn_colsum(const float *X, int64_t rows, int64_t cols_pad, int64_t ld, int
     return u2gnn_launch_status();
 }
 
+// U2GNN_SOFTMAX_RV=0 (A/B): the fixed 8-float4 row registers for every n_pad <= 8192
+static bool softmax_rows_sized() {
+    static const bool v = [] {
+        const char *e = std::getenv("U2GNN_SOFTMAX_RV");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
+
 int u2gnn_attn_softmax_fwd(const float *S, int64_t lds, float *P, float *Pd, int64_t ldp, int64_t rows_valid,
                            int64_t rows_pad, int64_t n_valid, int64_t n_pad, float p, uint64_t seed, uint32_t *keep,
                            int64_t ld_keep, void *stream) {
@@ -1122,9 +1131,26 @@ int u2gnn_attn_softmax_fwd(const float *S, int64_t lds, float *P, float *Pd, int
     if (keep && ((n_pad & 31) || ld_keep < n_pad / 32)) return U2GNN_E_ARG;
     if (n_pad > 1024 * SM_RV_MAX) return U2GNN_E_SHAPE;   // rows are held in registers
     hipStream_t st = u2gnn_stream(stream);
-    if (n_pad <= 8192)
-        hipLaunchKernelGGL(attn_softmax_kernel<8>, dim3((unsigned)rows_pad), dim3(256), 0, st, S, lds, P, Pd, ldp,
-                           rows_valid, n_valid, n_pad, p, seed, u2gnn_g_epoch, keep, ld_keep);
+    // registers sized to the row (ceil(n_pad / 1024) float4 per thread up to 8): a fixed 8 made every
+    // C4 row (4864 keys) compute 8192 exponentials, 3328 of them exp(-inf) = 0; the terms it drops are
+    // exact zeros appended after the live ones, so P is bit-identical
+    const int64_t rv = (n_pad + 1023) / 1024;
+#define U2GNN_SMX(V) hipLaunchKernelGGL(attn_softmax_kernel<V>, dim3((unsigned)rows_pad), dim3(256), 0, st, S, lds, P, Pd, \
+                                        ldp, rows_valid, n_valid, n_pad, p, seed, u2gnn_g_epoch, keep, ld_keep)
+    if (rv <= 8 && softmax_rows_sized()) {
+        switch (rv) {
+            case 1: U2GNN_SMX(1); break;
+            case 2: U2GNN_SMX(2); break;
+            case 3: U2GNN_SMX(3); break;
+            case 4: U2GNN_SMX(4); break;
+            case 5: U2GNN_SMX(5); break;
+            case 6: U2GNN_SMX(6); break;
+            case 7: U2GNN_SMX(7); break;
+            default: U2GNN_SMX(8); break;
+        }
+    } else if (n_pad <= 8192)
+        U2GNN_SMX(8);
+#undef U2GNN_SMX
     else if (n_pad <= 16384)
         hipLaunchKernelGGL(attn_softmax_kernel<16>, dim3((unsigned)rows_pad), dim3(256), 0, st, S, lds, P, Pd, ldp,
                            rows_valid, n_valid, n_pad, p, seed, u2gnn_g_epoch, keep, ld_keep);

@@ -487,7 +487,11 @@ int layer_fwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
     // a3.4 FFN + dropout2 + residual, LayerNorm2
     {
         G g(c.X1, w->W1, c.Hd, Np, ffp, dp, dp, dp, ffp, prec);
-        g.tb().epi(U2GNN_EPI_BIAS_RELU_DROP);
+        static const int ffn1_tile = [] {   // U2GNN_FFN1_TILE (A/B): force this GEMM's tile code
+            const char *e = std::getenv("U2GNN_FFN1_TILE");
+            return e && e[0] ? std::atoi(e) : 0;
+        }();
+        g.tb().epi(U2GNN_EPI_BIAS_RELU_DROP).tile(ffn1_tile);
         g.a.bias = w->b1, g.a.p_drop = pd, g.a.seed = s->dropff;
         U2GNN_TRY(g.run(st, plan));
     }
@@ -532,7 +536,11 @@ int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
     float *dH = W.take<float>(Np * ffp);
     {
         G gg(dF, w->W2, dH, Np, ffp, dp, dp, ffp, ffp, prec);
-        gg.epi(U2GNN_EPI_RELU_DROP_BWD);
+        static const int relu_bwd_tile = [] {   // U2GNN_RELU_BWD_TILE (A/B): force this GEMM's tile code
+            const char *e = std::getenv("U2GNN_RELU_BWD_TILE");
+            return e && e[0] ? std::atoi(e) : 0;
+        }();
+        gg.epi(U2GNN_EPI_RELU_DROP_BWD).tile(relu_bwd_tile);
         gg.a.aux0 = c.Hd, gg.a.ld_aux = ffp, gg.a.p_drop = pd;
         U2GNN_TRY(gg.run(st, plan));
     }

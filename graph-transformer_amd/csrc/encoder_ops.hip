@@ -628,18 +628,26 @@ __device__ __forceinline__ float half_sum(float v) {
     return v;
 }
 
-template <int LN_V4>
+// sum over the LPR lanes (32: a half-wave, 64: a wave) that hold one row
+template <int LPR>
+__device__ __forceinline__ float row_sum(float v) {
+#pragma unroll
+    for (int o = LPR / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+template <int LN_V4, int LPR = 32>
 __global__ void __launch_bounds__(256) layernorm_fwd_kernel(const float *Z, int64_t ldz, const float *gamma,
                                                             const float *beta, float *Y, int64_t ldy, float *mean,
                                                             float *rstd, int64_t rows_valid, int64_t rows_pad,
                                                             int64_t d, int64_t d_pad, float eps) {
-    const int64_t row = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 5);
-    const int hl = threadIdx.x & 31;
+    const int64_t row = (int64_t)blockIdx.x * (256 / LPR) + (threadIdx.x / LPR);   // LPR lanes per row
+    const int hl = threadIdx.x & (LPR - 1);
     if (row >= rows_pad) return;
     float *y = Y + row * ldy;
     const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
     if (row >= rows_valid) {
-        for (int64_t c = hl * 4; c < d_pad; c += 128) *reinterpret_cast<float4 *>(y + c) = z4;
+        for (int64_t c = hl * 4; c < d_pad; c += 4 * LPR) *reinterpret_cast<float4 *>(y + c) = z4;
         if (hl == 0) {
             mean[row] = 0.f;
             rstd[row] = 0.f;
@@ -651,14 +659,14 @@ __global__ void __launch_bounds__(256) layernorm_fwd_kernel(const float *Z, int6
     float4 t[LN_V4];
 #pragma unroll
     for (int i = 0; i < LN_V4; ++i) {
-        const int64_t c = 4 * (hl + 32 * i);
+        const int64_t c = 4 * (hl + LPR * i);
         t[i] = c < d_pad ? ld4(z + c) : z4;
     }
     // gamma / beta are unpadded [d] vectors at any 4-byte alignment: element loads at a clamped
     // column, issued with the row's loads (no per-element branch, no second round trip later)
 #pragma unroll
     for (int i = 0; i < LN_V4; ++i) {
-        const int64_t c = 4 * (hl + 32 * i);
+        const int64_t c = 4 * (hl + LPR * i);
         if (c >= d_pad) continue;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -670,7 +678,7 @@ __global__ void __launch_bounds__(256) layernorm_fwd_kernel(const float *Z, int6
     float s = 0.f;
 #pragma unroll
     for (int i = 0; i < LN_V4; ++i) {
-        const int64_t c = 4 * (hl + 32 * i);
+        const int64_t c = 4 * (hl + LPR * i);
         const float x[4] = {t[i].x, t[i].y, t[i].z, t[i].w};
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -678,19 +686,19 @@ __global__ void __launch_bounds__(256) layernorm_fwd_kernel(const float *Z, int6
             s += v[i][q];
         }
     }
-    const float mu = half_sum(s) / (float)d;
+    const float mu = row_sum<LPR>(s) / (float)d;
     float sq = 0.f;
 #pragma unroll
     for (int i = 0; i < LN_V4; ++i)
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const float t = 4 * (hl + 32 * i) + q < d ? v[i][q] - mu : 0.f;
+            const float t = 4 * (hl + LPR * i) + q < d ? v[i][q] - mu : 0.f;
             sq += t * t;
         }
-    const float rs = rsqrtf(half_sum(sq) / (float)d + eps);
+    const float rs = rsqrtf(row_sum<LPR>(sq) / (float)d + eps);
 #pragma unroll
     for (int i = 0; i < LN_V4; ++i) {
-        const int64_t c = 4 * (hl + 32 * i);
+        const int64_t c = 4 * (hl + LPR * i);
         if (c >= d_pad) continue;
         float o[4];
 #pragma unroll
@@ -1203,6 +1211,14 @@ int u2gnn_rowdot(const float *A, int64_t lda, const float *B, int64_t ldb, float
     return u2gnn_launch_status();
 }
 
+static bool ln_fwd_wave() {
+    static const bool v = [] {
+        const char *e = std::getenv("U2GNN_LN_WAVE");
+        return e && e[0] == '1';
+    }();
+    return v;
+}
+
 int u2gnn_layernorm_fwd(const float *Z, int64_t ldz, const float *gamma, const float *beta, float *Y, int64_t ldy,
                         float *mean, float *rstd, int64_t rows_valid, int64_t rows_pad, int64_t d, int64_t d_pad,
                         float eps, void *stream) {
@@ -1211,10 +1227,18 @@ int u2gnn_layernorm_fwd(const float *Z, int64_t ldz, const float *gamma, const f
     if (!al16(Z) || !al16(Y) || (ldz & 3) || (ldy & 3) || (d_pad & 3)) return U2GNN_E_ALIGN;
     // registers sized to the row: V4 = ceil(d_pad / 128) float4 per lane (C4: 3), not the maximum 8
     // (measured: the 8-wide arrays held ~160 VGPRs and 3 waves per SIMD for every width)
-    const dim3 gr(grid_for(rows_pad, 8, 1 << 30));
     hipStream_t st = u2gnn_stream(stream);
-#define U2GNN_LNF(V) hipLaunchKernelGGL(layernorm_fwd_kernel<V>, gr, dim3(256), 0, st, Z, ldz, gamma, beta, Y, ldy, \
-                                        mean, rstd, rows_valid, rows_pad, d, d_pad, eps)
+    if (ln_fwd_wave() && d_pad > 256 && d_pad <= 512) {
+        // U2GNN_LN_WAVE=1 (A/B): a full wave per row (2 float4 per lane, 4 rows per block): twice the
+        // rows in flight of the half-wave form at C4's width
+        const dim3 gw(grid_for(rows_pad, 4, 1 << 30));
+        hipLaunchKernelGGL((layernorm_fwd_kernel<2, 64>), gw, dim3(256), 0, st, Z, ldz, gamma, beta, Y, ldy, mean,
+                           rstd, rows_valid, rows_pad, d, d_pad, eps);
+        return u2gnn_launch_status();
+    }
+    const dim3 gr(grid_for(rows_pad, 8, 1 << 30));
+#define U2GNN_LNF(V) hipLaunchKernelGGL((layernorm_fwd_kernel<V, 32>), gr, dim3(256), 0, st, Z, ldz, gamma, beta, Y, \
+                                        ldy, mean, rstd, rows_valid, rows_pad, d, d_pad, eps)
     const int64_t v4 = (d_pad + 127) / 128;
     if (v4 <= 1) U2GNN_LNF(1);
     else if (v4 == 2) U2GNN_LNF(2);

@@ -153,16 +153,11 @@ struct G {   // one GEMM launch (defaults = plain store)
     int run(hipStream_t st, bool plan) { return plan ? U2GNN_OK : u2gnn_gemm(&a, st); }
 };
 
-bool shallow_nosplit_on() {   // engine._SHALLOW_NOSPLIT
-    static const bool v = [] {
-        const char *e = std::getenv("U2GNN_SHALLOW_NOSPLIT");
-        return !(e && e[0] == '0');
-    }();
-    return v;
-}
-
-bool event_pool_on();
 hipEvent_t pooled_event();
+
+// split-K block targets (engine._gemm_split): 448 blocks for 64 / 128 tiles, 240 for 256x128 tiles
+// (round-2 sweeps: 224 / 896 within noise, 120 / 300 / 460 slower on the 256x128 products)
+constexpr int64_t kSplitTarget = 448, kSplitTarget256 = 240;
 
 // engine._gemm_split: deterministic split-K into fp32 slabs + one reduce pass (alpha, accumulate,
 // padded->real block map).  deep = weight gradient (16-deep K step, <= 8 slabs).  red_st: run the
@@ -176,7 +171,7 @@ int gemm_split(Arena &W, const Dims &D, const float *A, const float *B, float *C
     const int64_t bk = f32 ? 16 : 32;
     const bool plan = W.plan();
     const bool mapped = rblk != nullptr;
-    if (shallow_nosplit_on() && !f32 && !deep && !mapped && Kd <= 2048 && M % 64 == 0 && N % 64 == 0 &&
+    if (!f32 && !deep && !mapped && Kd <= 2048 && M % 64 == 0 && N % 64 == 0 &&
         (M / 64) * (N / 64) >= 256) {
         // shallow K (dH.W1, dQKV.W_in) with enough 64x64 tiles to fill the chip: no split, the
         // epilogue accumulates straight into C (no slabs, no reduce pass)
@@ -192,17 +187,9 @@ int gemm_split(Arena &W, const Dims &D, const float *A, const float *B, float *C
         return rc;
     }
     int t;
-    static const int64_t target_small = [] {   // U2GNN_SPLIT_TARGET (A/B): blocks aimed at for 64/128 tiles
-        const char *e = std::getenv("U2GNN_SPLIT_TARGET");
-        return e && e[0] ? (int64_t)std::atoi(e) : (int64_t)448;
-    }();
-    int64_t tiles, target = target_small;
-    static const int64_t target256 = [] {   // U2GNN_SPLIT_TARGET256 (A/B): blocks aimed at for 256x128 tiles
-        const char *e = std::getenv("U2GNN_SPLIT_TARGET256");
-        return e && e[0] ? (int64_t)std::atoi(e) : (int64_t)240;
-    }();
+    int64_t tiles, target = kSplitTarget;
     if (!f32 && M % 256 == 0 && N % 128 == 0 && (M / 256) * (N / 128) >= 32) {
-        t = 256, tiles = (M / 256) * (N / 128), target = target256;
+        t = 256, tiles = (M / 256) * (N / 128), target = kSplitTarget256;
     } else {
         t = (M % 128 == 0 && N % 128 == 0) ? 128 : 64;
         tiles = (M / t) * (N / t);
@@ -211,12 +198,8 @@ int gemm_split(Arena &W, const Dims &D, const float *A, const float *B, float *C
     if (Kd / (4 * bk) < split) split = Kd / (4 * bk);
     if (split < 1) split = 1;
     // slab cap of the weight gradients (engine.wgrad_split_cap): 8 for node-sized depths, 16 for
-    // token-sized ones (neighbour mode, K = N(k+1) rows); U2GNN_WGRAD_SPLIT_MAX overrides (A/B)
-    static const int64_t wgrad_split_env = [] {
-        const char *e = std::getenv("U2GNN_WGRAD_SPLIT_MAX");
-        return e && e[0] ? (int64_t)std::atoi(e) : (int64_t)0;
-    }();
-    const int64_t wgrad_split_max = wgrad_split_env > 0 ? wgrad_split_env : (Kd <= 8192 ? 8 : 16);
+    // token-sized ones (neighbour mode, K = N(k+1) rows)
+    const int64_t wgrad_split_max = Kd <= 8192 ? 8 : 16;
     if (deep && D.deep_wgrad && !f32 && t == 128) {
         t = 129;
         split = target / (tiles > 0 ? tiles : 1);
@@ -274,17 +257,9 @@ int bias_grad(Arena &W, const float *dY, int64_t rows, int64_t cols_pad, int64_t
     return u2gnn_colsum(dY, rows, cols_pad, ld, cb0, cb1, out, 0, ws, st);
 }
 
-// Fork / join events come from a per-device ring of pre-created events (U2GNN_EVENT_POOL=0: one
-// hipEventCreate / hipEventDestroy per hand-off, the round-1 scheme).  Re-recording an event is
+// Fork / join events come from a per-device ring of pre-created events.  Re-recording an event is
 // safe once the waits on its previous record are enqueued (a wait binds the record current at the
 // call), and a ring of 256 is far longer than the hand-offs of one layer in flight.
-bool event_pool_on() {
-    static const bool v = [] {
-        const char *e = std::getenv("U2GNN_EVENT_POOL");
-        return !(e && e[0] == '0');
-    }();
-    return v;
-}
 
 hipEvent_t pooled_event() {
     constexpr size_t kRing = 256;
@@ -313,20 +288,10 @@ struct Side {
     bool plan;
     int fork() {
         if (plan || side == main) return U2GNN_OK;
-        if (event_pool_on()) {
-            hipEvent_t ev = pooled_event();
-            if (!ev) return U2GNN_E_ARG;
-            hipError_t e = hipEventRecord(ev, main);
-            if (e == hipSuccess) e = hipStreamWaitEvent(side, ev, 0);
-            return e == hipSuccess ? U2GNN_OK : (int)e;
-        }
-        hipEvent_t ev;
-        hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
-        if (e != hipSuccess) return (int)e;
-        e = hipEventRecord(ev, main);
+        hipEvent_t ev = pooled_event();
+        if (!ev) return U2GNN_E_ARG;
+        hipError_t e = hipEventRecord(ev, main);
         if (e == hipSuccess) e = hipStreamWaitEvent(side, ev, 0);
-        const hipError_t e2 = hipEventDestroy(ev);   // resources released once the recorded work completes
-        if (e == hipSuccess) e = e2;
         return e == hipSuccess ? U2GNN_OK : (int)e;
     }
     // the main stream waits for everything issued on the side stream so far
@@ -340,82 +305,26 @@ struct Side {
     int mark(hipEvent_t *ev) {
         *ev = nullptr;
         if (plan || side == main) return U2GNN_OK;
-        if (event_pool_on()) {
-            *ev = pooled_event();
-            if (!*ev) return U2GNN_E_ARG;
-            const hipError_t e = hipEventRecord(*ev, side);
-            return e == hipSuccess ? U2GNN_OK : (int)e;
-        }
-        hipError_t e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
-        if (e == hipSuccess) e = hipEventRecord(*ev, side);
+        *ev = pooled_event();
+        if (!*ev) return U2GNN_E_ARG;
+        const hipError_t e = hipEventRecord(*ev, side);
         return e == hipSuccess ? U2GNN_OK : (int)e;
     }
-    // the main stream waits for a mark() event (released once the recorded work completes)
+    // the main stream waits for a mark() event
     int wait(hipEvent_t ev) {
         if (!ev) return U2GNN_OK;
-        hipError_t e = hipStreamWaitEvent(main, ev, 0);
-        if (event_pool_on()) return e == hipSuccess ? U2GNN_OK : (int)e;
-        const hipError_t e2 = hipEventDestroy(ev);
-        if (e == hipSuccess) e = e2;
+        const hipError_t e = hipStreamWaitEvent(main, ev, 0);
         return e == hipSuccess ? U2GNN_OK : (int)e;
     }
 };
 
-// dV = Pd^T dO runs on the side stream beside the dS -> dQ -> dK chain (fills the CUs the
-// 228-block split-K launches and the launch tails leave idle: -1.4 % step time, measured);
-// U2GNN_DV_SIDE=0 keeps it on the main stream.  U2GNN_DK_SIDE=1 also moves dK = dS^T Q there.
-bool env_flag(const char *name, bool dflt) {
-    const char *e = std::getenv(name);
-    return e && e[0] ? e[0] == '1' : dflt;
-}
-bool dv_side_on() {
-    static const bool v = env_flag("U2GNN_DV_SIDE", true);
-    return v;
-}
-// U2GNN_DV_AFTER_DS=1: the side stream starts dV only after dS is issued (dV then overlaps dQ and
-// dK): 3.059-3.080 vs 3.085-3.092 ms per C4 step, one session, but dS then often waits for CUs the
-// side stream's earlier blocks hold, so its live probe (events around the launch, 111.7 us) and the
-// rocprof kernel time (102.1 us, first wave to last) part by 9 %; off by default so that the
-// bench's dominant-kernel timing and the profile agree (110.6 vs 109.6 us).
-bool dv_after_ds_on() {
-    static const bool v = env_flag("U2GNN_DV_AFTER_DS", false);
-    return v;
-}
-bool dk_side_on() {
-    static const bool v = env_flag("U2GNN_DK_SIDE", false);
-    return v;
-}
-// U2GNN_INPROJ_SPLIT=1: the in_proj weight gradient as three products (Q / K / V blocks), each on the
-// side stream as soon as its block of dQKV is final, instead of one product after the in-projection.
-// Measured 0.7 % slower (3.268 vs 3.245 ms/step, one-session A/B, profiles/r02/ab_inproj_split.txt):
-// the earlier side work contends with the dS -> dQ -> dK chain.
-bool inproj_split_on() {
-    static const bool v = env_flag("U2GNN_INPROJ_SPLIT", false);
-    return v;
-}
-
-// U2GNN_FUSED_LN=0 (A/B): the separate layernorm_fwd launch even where the GEMM tile holds whole rows
-bool fused_ln_on() {
-    static const bool v = env_flag("U2GNN_FUSED_LN", true);
-    return v;
-}
-
-// U2GNN_LN_DELTA=0 (A/B): the attention backward's delta by its own u2gnn_rowdot launch instead of
-// LayerNorm1's backward (u2gnn_layernorm_bwd_delta: sum_c dA * ((Z1 - X)(1-p) - b_o), no dO / O reads)
-bool ln_delta_on() {
-    static const bool v = env_flag("U2GNN_LN_DELTA", true);
-    return v;
-}
-
-// U2GNN_ROWDOT_FUSE=1 (A/B, opt-in): delta = rowsum(dO * O) from the dO GEMM's STORE_ROWDOT epilogue
-// (per-64-column partials that the dS epilogue sums) instead of its own u2gnn_rowdot launch.  Measured
-// slower on C4 (2 sessions x 3 reps: 3.33 vs 3.29 and 3.376 vs 3.363 ms per step; rocprof: rowdot
-// 7.2 us saved, dO GEMM +1.9 us, dS +6.8 us from its 6 extra partial loads per row and slice)
-bool rowdot_fuse_on() {
-    static const bool v = env_flag("U2GNN_ROWDOT_FUSE", false);
-    return v;
-}
-
+// Schedule decisions (each measured in rounds 1-2; the A/B switches are gone):
+//  * dV = Pd^T dO runs on the side stream beside the dS -> dQ -> dK chain (-1.4 % step time);
+//  * LayerNorm forward is fused into the bias-dropout-residual epilogue when one 64-column tile holds
+//    whole rows (d <= 64, matrix-core precisions);
+//  * delta = rowsum(dO * O) of the attention backward comes from LayerNorm1's backward
+//    (u2gnn_layernorm_bwd_delta: sum_c dA * ((Z1 - X)(1-p) - b_o)) in the matrix-core precisions; the
+//    fp32 parity path keeps u2gnn_rowdot, whose error does not grow with |X|.
 void set_ln(u2gnn_gemm_args &a, const float *gamma, const float *beta, float *y, int64_t ldy, float *mean, float *rstd,
             int64_t d, int64_t rows) {
     a.ln_gamma = gamma, a.ln_beta = beta, a.ln_y = y, a.ln_ldy = ldy;
@@ -436,14 +345,8 @@ int layer_fwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
         // 256x128 blocks from 3 waves of them on (token-sized rows, neighbour mode), the default tile
         // rule below that: C4's 19 x 9 blocks of 256x128 leave a third of the CUs idle, its 76 x 18 64-tile
         // blocks run the step 0.8 % faster (3/3 reps, profiles/r02/qkv_tile_ab.txt; bit-identical).
-        // U2GNN_QKV_TILE (A/B) forces a tile code (the Python engine mirrors both)
-        static const int qkv_tile_env = [] {
-            const char *e = std::getenv("U2GNN_QKV_TILE");
-            return e && e[0] ? std::atoi(e) : -1;
-        }();
-        const int qkv_tile = qkv_tile_env >= 0 ? qkv_tile_env
-                             : (prec != U2GNN_PREC_F32 && Np % 256 == 0 &&
-                                (Np / 256) * (3 * dp / 128) >= U2GNN_BIG_TILE_BLOCKS) ? 256 : 0;
+        const int qkv_tile = (prec != U2GNN_PREC_F32 && Np % 256 == 0 &&
+                              (Np / 256) * (3 * dp / 128) >= U2GNN_BIG_TILE_BLOCKS) ? 256 : 0;
         g.tb().epi(U2GNN_EPI_BIAS).tile(qkv_tile);
         g.a.bias = w->b_in;
         g.a.alpha = (float)(1.0 / std::sqrt((double)d));
@@ -474,7 +377,7 @@ int layer_fwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
     }
     // a3.3 out-projection + dropout1 + residual, LayerNorm1 (fused into the GEMM epilogue when a
     // 64-column tile holds whole rows: d <= 64, bf16 modes; engine.fused_ln mirrors the rule)
-    const bool fuse_ln = dp == 64 && prec != U2GNN_PREC_F32 && fused_ln_on();
+    const bool fuse_ln = dp == 64 && prec != U2GNN_PREC_F32;
     {
         G g(c.O, w->W_o, c.Z1, Np, dp, dp, dp, dp, dp, prec);
         g.tb().epi(fuse_ln ? U2GNN_EPI_BIAS_DROP_RESID_LN : U2GNN_EPI_BIAS_DROP_RESID);
@@ -487,11 +390,7 @@ int layer_fwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
     // a3.4 FFN + dropout2 + residual, LayerNorm2
     {
         G g(c.X1, w->W1, c.Hd, Np, ffp, dp, dp, dp, ffp, prec);
-        static const int ffn1_tile = [] {   // U2GNN_FFN1_TILE (A/B): force this GEMM's tile code
-            const char *e = std::getenv("U2GNN_FFN1_TILE");
-            return e && e[0] ? std::atoi(e) : 0;
-        }();
-        g.tb().epi(U2GNN_EPI_BIAS_RELU_DROP).tile(ffn1_tile);
+        g.tb().epi(U2GNN_EPI_BIAS_RELU_DROP);
         g.a.bias = w->b1, g.a.p_drop = pd, g.a.seed = s->dropff;
         U2GNN_TRY(g.run(st, plan));
     }
@@ -536,11 +435,7 @@ int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
     float *dH = W.take<float>(Np * ffp);
     {
         G gg(dF, w->W2, dH, Np, ffp, dp, dp, ffp, ffp, prec);
-        static const int relu_bwd_tile = [] {   // U2GNN_RELU_BWD_TILE (A/B): force this GEMM's tile code
-            const char *e = std::getenv("U2GNN_RELU_BWD_TILE");
-            return e && e[0] ? std::atoi(e) : 0;
-        }();
-        gg.epi(U2GNN_EPI_RELU_DROP_BWD).tile(relu_bwd_tile);
+        gg.epi(U2GNN_EPI_RELU_DROP_BWD);
         gg.a.aux0 = c.Hd, gg.a.ld_aux = ffp, gg.a.p_drop = pd;
         U2GNN_TRY(gg.run(st, plan));
     }
@@ -557,8 +452,7 @@ int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
     float *dX_scratch = W.take<float>(Np * dp);   // taken in every mode so the plan covers it
     if (!need_dx) dX = dX_scratch;
     // node attention: LayerNorm1's backward also forms delta = rowsum(dO * O) for the dS epilogue
-    const bool fuse_rowdot = !D.window && rowdot_fuse_on();
-    const bool ln_delta = !D.window && !fuse_rowdot && ln_delta_on();
+    const bool ln_delta = !D.window && prec != U2GNN_PREC_F32;
     float *delta_ln = ln_delta ? W.take<float>(Np) : nullptr;
     if (!plan && ln_delta)
         U2GNN_TRY(u2gnn_layernorm_bwd_delta(dX1, dp, c.Z1, dp, c.mean1, c.rstd1, w->n1_w, dX, dp, dA, dp, pd,
@@ -572,15 +466,8 @@ int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
                                              g->n1_b, g->out_b, so));
     // out-projection
     float *dO = W.take<float>(Np * dp);
-    // delta = rowsum(dO * O) of the attention backward: partial sums per 32 columns from the dO GEMM's
-    // epilogue (node attention), summed in group order by the dS epilogue
-    float *delta_parts = fuse_rowdot ? W.take<float>((dp / 64) * Np) : nullptr;
     {
         G gg(dA, w->W_o, dO, Np, dp, dp, dp, dp, dp, prec);
-        if (fuse_rowdot) {
-            gg.epi(U2GNN_EPI_STORE_ROWDOT);
-            gg.a.aux0 = c.O, gg.a.ld_aux = dp, gg.a.rowpart = delta_parts, gg.a.ld_rowpart = Np;
-        }
         U2GNN_TRY(gg.run(st, plan));
     }
     U2GNN_TRY(wgrad(W, D, dA, dp, c.O, dp, dp, dp, g->out_w, d, blk_d, blk_d, so));   // side (forked above)
@@ -588,15 +475,6 @@ int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
     const float *Q = c.QKV, *Kt = c.QKV + dp, *V = c.QKV + 2 * dp;
     const float q_scale = (float)(1.0 / std::sqrt((double)d));
     float *dQKV;
-    // in_proj weight / bias gradient of one of the Q (0), K (1), V (2) blocks: dQKV[:, p]^T X and
-    // its column sums, on the side stream as soon as that block of dQKV is final (the same split-K
-    // partition and reduction order per element as one [3dp, dp] product, so the same bits)
-    const bool split_in = inproj_split_on() && !D.window;
-    auto in_part = [&](int p) -> int {
-        if (!split_in) return U2GNN_OK;
-        U2GNN_TRY(wgrad(W, D, dQKV + p * dp, 3 * dp, X, dp, dp, dp, g->in_w + (int64_t)p * d * d, d, blk_d, blk_d, so));
-        return bias_grad(W, dQKV + p * dp, Np, dp, 3 * dp, dp, d, g->in_b + (int64_t)p * d, so);
-    };
     hipEvent_t dv_done = nullptr;   // side-stream position after the dV product (in_dx waits for it)
     if (D.window) {
         dQKV = W.take<float>(Np * 3 * dp);
@@ -605,74 +483,36 @@ int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
                                             q_scale, dQKV, 3 * dp, N / D.window, Np, st));
     } else {
         dQKV = W.take<float>(Np * 3 * dp);
-        const bool dv_side = dv_side_on() && so != st;
-        const bool dk_side = dv_side && dk_side_on();
-        const bool dv_late = dv_side && dv_after_ds_on();   // dV beside dQ / dK instead of beside dS
-        if (dv_side && !dv_late) {   // dV needs only Pd and dO: overlap it with the dS chain
-            U2GNN_TRY(sd.fork());
-            U2GNN_TRY(gemm_split(W, D, c.Pd, dO, dQKV + 2 * dp, Np, dp, Np, Np, dp, 3 * dp, true, 1.f, false, nullptr,
-                                 nullptr, false, so, pd > 0.f, -1, U2GNN_ROLE_DV));
-            if (!dk_side) U2GNN_TRY(sd.mark(&dv_done));
-            U2GNN_TRY(in_part(2));
-        }
-        float *delta = fuse_rowdot ? delta_parts : ln_delta ? delta_ln : W.take<float>(Np);
-        if (!plan && !fuse_rowdot && !ln_delta) U2GNN_TRY(u2gnn_rowdot(dO, dp, c.O, dp, delta, Np, dp, st));
+        const bool dv_side = so != st;
+        // dV needs only Pd and dO: on the side stream it overlaps the dS -> dQ -> dK chain
+        U2GNN_TRY(sd.fork());
+        U2GNN_TRY(gemm_split(W, D, c.Pd, dO, dQKV + 2 * dp, Np, dp, Np, Np, dp, 3 * dp, true, 1.f, false, nullptr,
+                             nullptr, false, dv_side ? so : st, pd > 0.f, -1, U2GNN_ROLE_DV));
+        if (dv_side) U2GNN_TRY(sd.mark(&dv_done));
+        float *delta = ln_delta ? delta_ln : W.take<float>(Np);
+        if (!plan && !ln_delta) U2GNN_TRY(u2gnn_rowdot(dO, dp, c.O, dp, delta, Np, dp, st));
         float *dS = W.take<float>(Np * Np);
         {
             G gg(dO, V, dS, Np, Np, dp, dp, 3 * dp, Np, D.prec_ab);
             gg.tb().epi(U2GNN_EPI_ATTN_DS_SIGNED);
             gg.a.aux0 = c.Pd, gg.a.rowvec = delta, gg.a.ld_aux = Np, gg.a.p_drop = pd;
-            if (fuse_rowdot) gg.a.rowvec_parts = (int32_t)(dp / 64), gg.a.ld_rowvec = Np;
             probe_mark(U2GNN_ROLE_DS, false, st, plan);
             U2GNN_TRY(gg.run(st, plan));
             probe_mark(U2GNN_ROLE_DS, true, st, plan);
         }
-        if (dv_late) {
-            U2GNN_TRY(sd.fork());
-            U2GNN_TRY(gemm_split(W, D, c.Pd, dO, dQKV + 2 * dp, Np, dp, Np, Np, dp, 3 * dp, true, 1.f, false, nullptr,
-                                 nullptr, false, so, pd > 0.f, -1, U2GNN_ROLE_DV));
-            if (!dk_side) U2GNN_TRY(sd.mark(&dv_done));
-            U2GNN_TRY(in_part(2));
-        }
-        if (!dv_side) {
-            U2GNN_TRY(gemm_split(W, D, c.Pd, dO, dQKV + 2 * dp, Np, dp, Np, Np, dp, 3 * dp, true, 1.f, false, nullptr,
-                                 nullptr, false, st, pd > 0.f, -1, U2GNN_ROLE_DV));
-            U2GNN_TRY(sd.fork());
-            U2GNN_TRY(in_part(2));
-        }
-        if (dk_side) {
-            U2GNN_TRY(sd.fork());
-            U2GNN_TRY(gemm_split(W, D, dS, Q, dQKV + dp, Np, dp, Np, Np, 3 * dp, 3 * dp, true, 1.f, false, nullptr,
-                                 nullptr, false, so, false, D.prec_ab, U2GNN_ROLE_DK));
-            U2GNN_TRY(sd.mark(&dv_done));   // dV and dK
-            U2GNN_TRY(in_part(1));
-        }
-        // U2GNN_DQ_REDUCE_SIDE=1 (A/B): dQ's split-K reduce on the side stream (behind dV), so that dK
-        // starts right after the dQ GEMM; the join before the in-projection covers it
-        static const bool dq_red_env = env_flag("U2GNN_DQ_REDUCE_SIDE", false);
-        const bool dq_red_side = dv_side && event_pool_on() && dq_red_env;
         U2GNN_TRY(gemm_split(W, D, dS, Kt, dQKV, Np, dp, Np, Np, 3 * dp, 3 * dp, false, q_scale, false, nullptr, nullptr,
-                             false, st, false, D.prec_ab, U2GNN_ROLE_DQ, dq_red_side ? so : nullptr));
-        if (dq_red_side && !plan) U2GNN_TRY(sd.mark(&dv_done));   // dV (, dK) and the dQ reduce
-        U2GNN_TRY(sd.fork());
-        U2GNN_TRY(in_part(0));
-        if (!dk_side) {
-            U2GNN_TRY(gemm_split(W, D, dS, Q, dQKV + dp, Np, dp, Np, Np, 3 * dp, 3 * dp, true, 1.f, false, nullptr,
-                                 nullptr, false, st, false, D.prec_ab, U2GNN_ROLE_DK));
-            U2GNN_TRY(sd.fork());
-            U2GNN_TRY(in_part(1));
-        }
-        U2GNN_TRY(sd.wait(dv_done));   // dV (and dK) before dX += dQKV W_in
+                             false, st, false, D.prec_ab, U2GNN_ROLE_DQ));
+        U2GNN_TRY(gemm_split(W, D, dS, Q, dQKV + dp, Np, dp, Np, Np, 3 * dp, 3 * dp, true, 1.f, false, nullptr,
+                             nullptr, false, st, false, D.prec_ab, U2GNN_ROLE_DK));
+        U2GNN_TRY(sd.wait(dv_done));   // dV before dX += dQKV W_in
     }
     // in-projection
     if (need_dx)
         U2GNN_TRY(gemm_split(W, D, dQKV, w->W_in, dX, Np, dp, 3 * dp, 3 * dp, dp, dp, false, 1.f, true, nullptr,
                              nullptr, false, st));
-    if (!split_in) {
-        U2GNN_TRY(sd.fork());
-        U2GNN_TRY(wgrad(W, D, dQKV, 3 * dp, X, dp, 3 * dp, dp, g->in_w, d, blk_d, blk_d, so));
-        U2GNN_TRY(bias_grad(W, dQKV, Np, 3 * dp, 3 * dp, dp, d, g->in_b, so));
-    }
+    U2GNN_TRY(sd.fork());
+    U2GNN_TRY(wgrad(W, D, dQKV, 3 * dp, X, dp, 3 * dp, dp, g->in_w, d, blk_d, blk_d, so));
+    U2GNN_TRY(bias_grad(W, dQKV, Np, 3 * dp, 3 * dp, dp, d, g->in_b, so));
     return (W.overflow || CA.overflow) ? U2GNN_E_ARG : U2GNN_OK;
 }
 

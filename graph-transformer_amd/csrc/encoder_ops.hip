@@ -987,24 +987,6 @@ inline unsigned grid_for(int64_t n, int64_t per_block, int64_t cap = 8192) {
 
 extern "C" {
 
-// U2GNN_SMALL_REDUCE=0 (A/B): short inputs also take the two-launch column reductions
-static bool small_reduce_on() {
-    static const bool v = [] {
-        const char *e = std::getenv("U2GNN_SMALL_REDUCE");
-        return !(e && e[0] == '0');
-    }();
-    return v;
-}
-
-// U2GNN_GATHER_MODE=2 (A/B only): the round-1 one-wave-per-row kernel instead of the multi kernel
-static int gather_mode() {
-    static const int m = [] {
-        const char *e = std::getenv("U2GNN_GATHER_MODE");
-        return e && e[0] ? std::atoi(e) : 0;
-    }();
-    return m;
-}
-
 int u2gnn_gather_rows(const float *src, int64_t ld_src, int64_t src_rows, const int64_t *idx, int64_t idx_stride,
                       float *dst, int64_t ld_dst, int64_t n_rows, int64_t n_rows_pad, int64_t d, int64_t d_pad,
                       int32_t *err, void *stream) {
@@ -1016,7 +998,7 @@ int u2gnn_gather_rows(const float *src, int64_t ld_src, int64_t src_rows, const 
     if (small && (d_pad & 3) == 0 && (ld_dst & 3) == 0 && al16(dst) && (ld_src & 3) == 0 && al16(src))
         hipLaunchKernelGGL(gather_rows_kernel<1>, grid, dim3(256), 0, st, src, ld_src, src_rows, idx, idx_stride, dst,
                            ld_dst, n_rows, n_rows_pad, d, d_pad, err);
-    else if (d_pad <= 512 && (ld_dst & 3) == 0 && al16(dst) && gather_mode() != 2) {
+    else if (d_pad <= 512 && (ld_dst & 3) == 0 && al16(dst)) {
         // gridDim.x a multiple of 8 for the XCD order (surplus blocks find no rows and return)
         const dim3 g8((grid_for(n_rows_pad, 4, 1 << 30) + 7u) / 8u * 8u);
         if (d_pad & 3)
@@ -1102,7 +1084,7 @@ int u2gnn_colsum(const float *X, int64_t rows, int64_t cols_pad, int64_t ld, int
     int64_t chunks = (rows + CS_ROWS - 1) / CS_ROWS;
     hipStream_t st = u2gnn_stream(stream);
     const bool vec = al16(X) && al16(ws) && (ld & 3) == 0 && (cols_pad & 3) == 0;
-    if (vec && rows <= SMALL_ROWS && small_reduce_on()) {
+    if (vec && rows <= SMALL_ROWS) {
         hipLaunchKernelGGL(colsum_small_kernel, dim3((unsigned)((cols_pad + 63) / 64)), dim3(1024), 0, st, X, rows,
                            cols_pad, ld, cblk_pad, cblk_real, out, accumulate);
         return u2gnn_launch_status();
@@ -1121,15 +1103,6 @@ int u2gnn_colsum(const float *X, int64_t rows, int64_t cols_pad, int64_t ld, int
     return u2gnn_launch_status();
 }
 
-// U2GNN_SOFTMAX_RV=0 (A/B): the fixed 8-float4 row registers for every n_pad <= 8192
-static bool softmax_rows_sized() {
-    static const bool v = [] {
-        const char *e = std::getenv("U2GNN_SOFTMAX_RV");
-        return !(e && e[0] == '0');
-    }();
-    return v;
-}
-
 int u2gnn_attn_softmax_fwd(const float *S, int64_t lds, float *P, float *Pd, int64_t ldp, int64_t rows_valid,
                            int64_t rows_pad, int64_t n_valid, int64_t n_pad, float p, uint64_t seed, uint32_t *keep,
                            int64_t ld_keep, void *stream) {
@@ -1145,7 +1118,7 @@ int u2gnn_attn_softmax_fwd(const float *S, int64_t lds, float *P, float *Pd, int
     const int64_t rv = (n_pad + 1023) / 1024;
 #define U2GNN_SMX(V) hipLaunchKernelGGL(attn_softmax_kernel<V>, dim3((unsigned)rows_pad), dim3(256), 0, st, S, lds, P, Pd, \
                                         ldp, rows_valid, n_valid, n_pad, p, seed, u2gnn_g_epoch, keep, ld_keep)
-    if (rv <= 8 && softmax_rows_sized()) {
+    if (rv <= 8) {
         switch (rv) {
             case 1: U2GNN_SMX(1); break;
             case 2: U2GNN_SMX(2); break;
@@ -1156,8 +1129,7 @@ int u2gnn_attn_softmax_fwd(const float *S, int64_t lds, float *P, float *Pd, int
             case 7: U2GNN_SMX(7); break;
             default: U2GNN_SMX(8); break;
         }
-    } else if (n_pad <= 8192)
-        U2GNN_SMX(8);
+    }
 #undef U2GNN_SMX
     else if (n_pad <= 16384)
         hipLaunchKernelGGL(attn_softmax_kernel<16>, dim3((unsigned)rows_pad), dim3(256), 0, st, S, lds, P, Pd, ldp,
@@ -1211,14 +1183,6 @@ int u2gnn_rowdot(const float *A, int64_t lda, const float *B, int64_t ldb, float
     return u2gnn_launch_status();
 }
 
-static bool ln_fwd_wave() {
-    static const bool v = [] {
-        const char *e = std::getenv("U2GNN_LN_WAVE");
-        return e && e[0] == '1';
-    }();
-    return v;
-}
-
 int u2gnn_layernorm_fwd(const float *Z, int64_t ldz, const float *gamma, const float *beta, float *Y, int64_t ldy,
                         float *mean, float *rstd, int64_t rows_valid, int64_t rows_pad, int64_t d, int64_t d_pad,
                         float eps, void *stream) {
@@ -1228,14 +1192,6 @@ int u2gnn_layernorm_fwd(const float *Z, int64_t ldz, const float *gamma, const f
     // registers sized to the row: V4 = ceil(d_pad / 128) float4 per lane (C4: 3), not the maximum 8
     // (measured: the 8-wide arrays held ~160 VGPRs and 3 waves per SIMD for every width)
     hipStream_t st = u2gnn_stream(stream);
-    if (ln_fwd_wave() && d_pad > 256 && d_pad <= 512) {
-        // U2GNN_LN_WAVE=1 (A/B): a full wave per row (2 float4 per lane, 4 rows per block): twice the
-        // rows in flight of the half-wave form at C4's width
-        const dim3 gw(grid_for(rows_pad, 4, 1 << 30));
-        hipLaunchKernelGGL((layernorm_fwd_kernel<2, 64>), gw, dim3(256), 0, st, Z, ldz, gamma, beta, Y, ldy, mean,
-                           rstd, rows_valid, rows_pad, d, d_pad, eps);
-        return u2gnn_launch_status();
-    }
     const dim3 gr(grid_for(rows_pad, 8, 1 << 30));
 #define U2GNN_LNF(V) hipLaunchKernelGGL((layernorm_fwd_kernel<V, 32>), gr, dim3(256), 0, st, Z, ldz, gamma, beta, Y, \
                                         ldy, mean, rstd, rows_valid, rows_pad, d, d_pad, eps)
@@ -1316,7 +1272,7 @@ int u2gnn_layernorm_bwd_params(const float *dY, int64_t ldy, const float *Z, int
     const int rep = (int)((groups + LN_MAX_CHUNKS - 1) / LN_MAX_CHUNKS);
     const int64_t chunks = (groups + rep - 1) / rep;   // <= the CS_ROWS-row group count callers size ws by
     hipStream_t st = u2gnn_stream(stream);
-    if (rows_valid <= SMALL_ROWS && small_reduce_on()) {
+    if (rows_valid <= SMALL_ROWS) {
         hipLaunchKernelGGL(ln_params_small_kernel, dim3((unsigned)((d_pad + 63) / 64)), dim3(1024), 0, st, dY, ldy, Z,
                            ldz, mean, rstd, dbias ? dZdrop : nullptr, lddrop, rows_valid, d, d_pad, dgamma, dbeta,
                            dbias);

@@ -514,12 +514,18 @@ inline bool al16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) =
 
 }  // namespace
 
-int u2gnn_gemm_x2_dispatch(const u2gnn_gemm_args *a, GemmP &P, int tile, int split, hipStream_t st);
-int u2gnn_gemm_x3_dispatch(const u2gnn_gemm_args *a, GemmP &P, int tile, int split, hipStream_t st);
+// The pre-split (x2) kernels (gemm_x2.hip, gemm_x3.hip) are experiments off the layer's path (DESIGN.md
+// sections 5.1 and 5.3): they live in libu2gnn_hip_x2.so (make target x2, tests/test_gemm_x2_gpu.py),
+// not in the product library.  Weak references: without those objects x2 operands are rejected.
+__attribute__((weak)) int u2gnn_gemm_x2_dispatch(const u2gnn_gemm_args *a, GemmP &P, int tile, int split,
+                                                 hipStream_t st);
+__attribute__((weak)) int u2gnn_gemm_x3_dispatch(const u2gnn_gemm_args *a, GemmP &P, int tile, int split,
+                                                 hipStream_t st);
 
 extern "C" int u2gnn_gemm(const u2gnn_gemm_args *a, void *stream) {
     if (!a) return U2GNN_E_ARG;
     const bool x2 = a->a_x2 || a->b_x2;
+    if (x2 && (!u2gnn_gemm_x2_dispatch || !u2gnn_gemm_x3_dispatch)) return U2GNN_E_ARG;   // not this build
     if (x2 ? (!a->A2 || !a->B2) : (!a->A || !a->B)) return U2GNN_E_ARG;
     if (!a->C && !a->Cx2) return U2GNN_E_ARG;
     if (a->M <= 0 || a->N <= 0 || a->K <= 0) return U2GNN_E_ARG;

@@ -402,15 +402,9 @@ inline size_t fwd_lds(int W, int dp) { return (size_t)(2 * W * (dp + 4) + W * (W
 inline size_t bwd_lds(int W, int dp) { return (size_t)(2 * W * (dp + 4) + 2 * W * (W + 1)) * sizeof(float); }
 constexpr size_t LDS_LIMIT = 160 * 1024;
 
-// U2GNN_WIN_PF (A/B): 0 = one block per node; 2 (default) = the persistent prefetching kernels at 2
-// blocks per CU; 3 = the forward at 3 blocks per CU (its registers then spill: slower, measured)
-int win_pf_mode() {
-    static const int v = [] {
-        const char *e = std::getenv("U2GNN_WIN_PF");
-        return e && e[0] ? std::atoi(e) : 2;
-    }();
-    return v;
-}
+// The persistent prefetching kernels run at 2 blocks per CU (measured round 2: 3 blocks per CU spill
+// the forward's registers and run slower; one block per node is the generic kernel below).
+constexpr int kWinPfBlocksPerCu = 2;
 
 int cu_count() {
     static const int n = [] {
@@ -447,17 +441,16 @@ int u2gnn_window_attn_fwd(const float *QKV, int64_t ldq, int32_t W, int32_t dp, 
     nb = std::max(nb, (W + 15) / 16);
     nb = std::min(nb, (int)W);
     const int rb = (W + nb - 1) / nb;
-    const int pf = win_pf_mode();
-    if ((pf == 2 || pf == 3) && elems > 256 * 6 && elems <= 256 * 7 && rb == 9 && (W + 8) / 9 == nb) {
-        auto kern = pf == 2 ? window_attn_fwd_pf_kernel<7, 9, 2> : window_attn_fwd_pf_kernel<7, 9, 3>;
-        static bool attr_pf[2] = {false, false};
-        if (!attr_pf[pf - 2]) {
+    if (elems > 256 * 6 && elems <= 256 * 7 && rb == 9 && (W + 8) / 9 == nb) {
+        auto kern = window_attn_fwd_pf_kernel<7, 9, kWinPfBlocksPerCu>;
+        static bool attr_pf = false;
+        if (!attr_pf) {
             const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_LIMIT);
             if (e != hipSuccess) return (int)e;
-            attr_pf[pf - 2] = true;
+            attr_pf = true;
         }
-        const int64_t per_cu = std::min<int64_t>(pf, std::max<int64_t>(1, (int64_t)(LDS_LIMIT / lds)));
+        const int64_t per_cu = std::min<int64_t>(kWinPfBlocksPerCu, std::max<int64_t>(1, (int64_t)(LDS_LIMIT / lds)));
         const int64_t grid = std::min<int64_t>(n_nodes, per_cu * cu_count());
         hipLaunchKernelGGL(kern, dim3((unsigned)std::max<int64_t>(grid, 1)), dim3(256), lds, u2gnn_stream(stream), QKV,
                            ldq, W, dp, O, ldo, Psave, p, seed, u2gnn_g_epoch, n_nodes, rows_pad);
@@ -491,8 +484,8 @@ int u2gnn_window_attn_bwd(const float *QKV, int64_t ldq, int32_t W, int32_t dp, 
     nb = std::max(nb, (W + 15) / 16);
     nb = std::min(nb, (int)W);
     const int rb = (W + nb - 1) / nb;
-    if (win_pf_mode() == 2 && elems > 256 * 6 && elems <= 256 * 7 && rb == 9 && (W + 8) / 9 == nb) {
-        auto kern = window_attn_bwd_pf_kernel<7, 9, 2>;
+    if (elems > 256 * 6 && elems <= 256 * 7 && rb == 9 && (W + 8) / 9 == nb) {
+        auto kern = window_attn_bwd_pf_kernel<7, 9, kWinPfBlocksPerCu>;
         static bool attr_pf = false;
         if (!attr_pf) {
             const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
@@ -500,7 +493,7 @@ int u2gnn_window_attn_bwd(const float *QKV, int64_t ldq, int32_t W, int32_t dp, 
             if (e != hipSuccess) return (int)e;
             attr_pf = true;
         }
-        const int64_t per_cu = std::min<int64_t>(2, std::max<int64_t>(1, (int64_t)(LDS_LIMIT / lds)));
+        const int64_t per_cu = std::min<int64_t>(kWinPfBlocksPerCu, std::max<int64_t>(1, (int64_t)(LDS_LIMIT / lds)));
         const int64_t grid = std::min<int64_t>(n_nodes, per_cu * cu_count());
         hipLaunchKernelGGL(kern, dim3((unsigned)std::max<int64_t>(grid, 1)), dim3(256), lds, u2gnn_stream(stream), QKV,
                            ldq, W, dp, dO, ldo, Psave, p, seed, u2gnn_g_epoch, q_scale, dQKV, ldg, n_nodes, rows_pad);

@@ -10,7 +10,6 @@
 from __future__ import annotations
 
 import math
-import os
 from dataclasses import dataclass
 from typing import List, Optional
 
@@ -27,8 +26,6 @@ from .engine import (SITE_ATTN, SITE_DROP1, SITE_DROP2, SITE_DROPFF, SITE_HEAD, 
 _IOTA = {}
 
 
-# U2GNN_COPY_STREAM=0 (A/B): DeviceBatch.from_store's transfers on the compute stream
-_COPY_STREAM = os.environ.get("U2GNN_COPY_STREAM", "1") != "0"
 _COPY: dict = {}
 
 
@@ -108,7 +105,7 @@ class DeviceBatch:
         N, B = int(hb.offsets[-1]), len(hb.offsets) - 1
         slot = getattr(hb, "pinned", None)
         _check_range_host(hb.input_x, N)
-        if slot is not None and _COPY_STREAM and dev.type == "cuda":
+        if slot is not None and dev.type == "cuda":
             # the batch's transfers and its feature gather run on a copy stream, so the next batch
             # crosses PCIe while the current step computes; the compute stream waits on one event
             main = torch.cuda.current_stream(dev)
@@ -175,10 +172,6 @@ def _check_range_host(input_x, N: int):
     a = input_x.numpy() if isinstance(input_x, torch.Tensor) else np.asarray(input_x)
     if a.size and (int(a.min()) < 0 or int(a.max()) >= N):
         raise IndexError("index out of range in self (input_x entry outside [0, N))")
-
-
-# U2GNN_POOL_ROWS=0 (A/B): the accumulating pool backward into a zero-filled buffer for every batch
-_POOL_ROWS = os.environ.get("U2GNN_POOL_ROWS", "1") != "0"
 
 
 class EncoderStack:
@@ -377,7 +370,7 @@ class SupCore:
             dG = torch.empty(b.B, dp, device=dev, dtype=torch.float32)
             K.head_bwd(dscores, G, dp, self.m.predictions[l].weight, dG, dp, grads[f"predictions.{l}.weight"],
                        grads[f"predictions.{l}.bias"], b.B, self.C, d)
-            if b.block_rows and _POOL_ROWS:   # every row stored: no zero fill, no atomics
+            if b.block_rows:   # every row stored: no zero fill, no atomics
                 dX = torch.empty(Np, dp, device=dev, dtype=torch.float32)
                 K.pool_bwd_rows(dG, dp, b.rowptr, b.colidx, b.vals, dX, dp, b.B, d, dp, b.N, Np, ctx["ph"], hs)
             else:
@@ -457,7 +450,12 @@ class FusedAdam:
         b1, b2 = self.betas
         if self.max_norm is not None:
             K.sqnorm(self.f.gflat, self.f.n, self.ws, self.sq)
-        if self.t_dev is not None:   # t advanced by the caller's u2gnn_step_advance
+        if self.t_dev is not None:
+            # inside a captured step the graph's first node (StepGraphs: u2gnn_step_advance) bumps t;
+            # an eager step taken while the device schedule is live bumps it here, so every path
+            # advances t exactly once per step (a fresh t of 0 gave lr / (1 - b1^0) = inf)
+            if not torch.cuda.is_current_stream_capturing():
+                K.step_advance(None, self.t_dev)
             K.adam_dev(self.f.flat, self.f.gflat, self.m, self.v, self.f.n,
                        self.sq if self.max_norm is not None else None, self.max_norm or 0.0, b1, b2, self.eps,
                        self.lr_dev, self.t_dev)

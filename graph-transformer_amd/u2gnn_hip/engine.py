@@ -20,7 +20,6 @@ Padding rows/columns hold zeros in every activation and gradient the encoder pro
 from __future__ import annotations
 
 import math
-import os
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
 
@@ -141,9 +140,8 @@ class EncoderLayerCtx:
                  "seeds")
 
 
-# weight gradients on the 16-deep-K 128x128 tile (-1 % step time, A/B on one box);
-# U2GNN_DEEP_WGRAD=0 selects the 32-deep tile
-_DEEP_WGRAD = os.environ.get("U2GNN_DEEP_WGRAD", "1") == "1"
+# weight gradients on the 16-deep-K 128x128 tile (-1 % step time, A/B on one box)
+_DEEP_WGRAD = True
 
 
 def deep_wgrad() -> bool:
@@ -151,8 +149,8 @@ def deep_wgrad() -> bool:
 
 
 # Gradient work off the backward's critical path (weight, bias and LayerNorm-parameter gradients)
-# runs on a second HIP stream, overlapping the dX chain; U2GNN_OVERLAP=0 serialises it.
-_OVERLAP = [os.environ.get("U2GNN_OVERLAP", "1") == "1"]
+# runs on a second HIP stream, overlapping the dX chain; set_overlap(False) serialises it.
+_OVERLAP = [True]
 _SIDE: Dict[int, "torch.cuda.Stream"] = {}
 
 
@@ -178,27 +176,21 @@ def side_stream(dev: torch.device) -> "torch.cuda.Stream":
 # The side stream pays only when the layer's kernels fill the chip: at C4 (Np*dp = 1.9M) it saves
 # 0.31 ms of a 3.27 ms step; at C5 (U2GNN-UnSup REDDIT, d = 4: Np*dp = 0.13M, ~2-10 us kernels) the
 # cross-stream hand-offs cost more than the overlap gains (1.116 vs 1.19-1.28 ms/step, one session,
-# profiles/r02/r2i_graph_knobs.txt).  U2GNN_SIDE_MIN_ELEMS overrides the threshold.
-SIDE_MIN_ELEMS = int(os.environ.get("U2GNN_SIDE_MIN_ELEMS", str(1 << 20)))
-
-
-# U2GNN_FUSED_LN=0 (A/B): the separate layernorm_fwd launch even where the GEMM tile holds whole rows
-# (encoder_layer.cpp applies the same rule)
-_FUSED_LN = os.environ.get("U2GNN_FUSED_LN", "1") != "0"
-# U2GNN_ROWDOT_FUSE=1 (A/B, opt-in; measured slower, encoder_layer.cpp rowdot_fuse_on): delta = rowsum(dO * O)
-# from the dO GEMM's STORE_ROWDOT epilogue instead of its own rowdot launch
-_ROWDOT_FUSE = os.environ.get("U2GNN_ROWDOT_FUSE", "0") == "1"
-# U2GNN_LN_DELTA=0 (A/B; encoder_layer.cpp ln_delta_on): delta by its own rowdot launch instead of LayerNorm1's
-# backward (layernorm_bwd_delta)
-_LN_DELTA = os.environ.get("U2GNN_LN_DELTA", "1") != "0"
-# U2GNN_QKV_TILE (A/B; encoder_layer.cpp): force the in-projection GEMM's tile code
-_QKV_TILE = int(os.environ.get("U2GNN_QKV_TILE", "-1") or -1)
+# profiles/r02/r2i_graph_knobs.txt).
+SIDE_MIN_ELEMS = 1 << 20
 
 
 def fused_ln(dp: int, prec: str) -> bool:
     """LayerNorm forward inside the bias-dropout-residual GEMM epilogue: d <= 64 (one 64-column tile
-    per row), matrix-core precisions."""
-    return _FUSED_LN and dp == 64 and prec != "fp32"
+    per row), matrix-core precisions (encoder_layer.cpp applies the same rule)."""
+    return dp == 64 and prec != "fp32"
+
+
+def ln_delta(prec: str) -> bool:
+    """The attention backward's delta = rowsum(dO * O) from LayerNorm1's backward
+    (layernorm_bwd_delta) in the matrix-core precisions; the fp32 parity path keeps its own rowdot
+    launch, whose error does not grow with |X| (encoder_layer.cpp applies the same rule)."""
+    return prec != "fp32"
 
 
 def side_stream_pays(dims: "Dims") -> bool:
@@ -209,7 +201,7 @@ class OffPath:
     """Enqueue closures on the side stream after everything already issued on the current
     stream; tensors they read are record_stream'ed so the caching allocator cannot recycle
     them early.  join() makes the current stream wait for all of it.  enabled=False (or
-    U2GNN_OVERLAP=0): everything runs on the current stream."""
+    set_overlap(False)): everything runs on the current stream."""
 
     def __init__(self, dev: torch.device, enabled: bool = True):
         self.side = side_stream(dev) if enabled and _OVERLAP[0] and dev.type == "cuda" else None
@@ -229,24 +221,21 @@ class OffPath:
             torch.cuda.current_stream().wait_stream(self.side)
 
 
-# U2GNN_SHALLOW_NOSPLIT=0: shallow-K products split like the deep ones (A/B switch; the native
-# executor reads the same variable)
-_SHALLOW_NOSPLIT = os.environ.get("U2GNN_SHALLOW_NOSPLIT", "1") != "0"
 BIG_TILE_BLOCKS = 768
 # slab cap of the deep weight-gradient products (encoder_layer.cpp applies the same rule): at node-sized
 # depths 8 slabs move half the bytes of 16 beside the main stream (C4 3.236 / 3.238 vs 3.251 / 3.260 ms;
 # 12: 3.26, 4: 3.27); token-sized depths (neighbour mode, K = 82 K rows) keep 16 (8: 15.2 vs 13.9 ms).
-# U2GNN_WGRAD_SPLIT_MAX overrides.
-_WGRAD_SPLIT_ENV = int(os.environ.get("U2GNN_WGRAD_SPLIT_MAX", "0"))
 
 
 def wgrad_split_cap(kd: int) -> int:
-    return _WGRAD_SPLIT_ENV if _WGRAD_SPLIT_ENV > 0 else (8 if kd <= 8192 else 16)
-# Precision experiments: products (by role) that run plain bf16 when the layer runs bf16x3.
-# U2GNN_BF16_ROLES=qk,pv,... (tools/prec_probe.py measures each role's parity error).
+    return 8 if kd <= 8192 else 16
+
+
+# Precision experiments (Python orchestration only): products (by role) that run plain bf16 when the
+# layer runs bf16x3; tools/prec_probe.py fills ROLE_BF16 to measure each role's parity error.
 ROLES = ("in_proj", "qk", "pv", "out_proj", "ffn1", "ffn2", "ffn2_dx", "ffn2_dw", "ffn1_dx", "ffn1_dw",
          "out_dx", "out_dw", "dv", "ds", "dq", "dk", "in_dx", "in_dw")
-ROLE_BF16 = set(r for r in os.environ.get("U2GNN_BF16_ROLES", "").split(",") if r)
+ROLE_BF16: set = set()
 # precision "mixed" (experiment, not parity-grade): bf16x3 everywhere except the attention-backward
 # products dS, dQ, dK on plain bf16 (u2gnn_hip.h U2GNN_LAYER_ATTN_BWD_BF16).  Joint error on C4
 # batches (tools/prec_probe.py --mixed, profiles/r02/r2b_mixed_probe.log) 2.5e-4..4.0e-4 of the 1e-3
@@ -272,7 +261,7 @@ def _gemm_split(A, B, C, M, N, Kd, lda, ldb, ldc, trans_a=False, trans_b=False, 
     alpha, accumulation and an optional padded->real block map (rblk, cblk).  clamp_a: A is the
     signed probability image (read as Pd)."""
     bk = 16 if prec == "fp32" else 32
-    if (_SHALLOW_NOSPLIT and prec != "fp32" and not deep and rblk is None and Kd <= 2048 and M % 64 == 0
+    if (prec != "fp32" and not deep and rblk is None and Kd <= 2048 and M % 64 == 0
             and N % 64 == 0 and (M // 64) * (N // 64) >= 256):
         # shallow K (dH.W1, dQKV.W_in: K = ff, 3d) with enough 64x64 tiles to fill the chip: no
         # split, C (+)= alpha acc straight from the epilogue -- no slabs, no reduce pass
@@ -336,8 +325,7 @@ def encoder_layer_forward(X: torch.Tensor, w: PackedLayer, p: LayerParams, dims:
     QKV = torch.empty(Np, 3 * dp, device=dev, dtype=f32)
     K.gemm(X, w.W_in, QKV, Np, 3 * dp, dp, dp, dp, 3 * dp, trans_b=True, epilogue=E.EPI_BIAS, bias=w.b_in,
            alpha=1.0 / math.sqrt(d), scale_cols=dp, precision=_rp("in_proj", prec), flops=6.0 * N * d * d,
-           tile=_QKV_TILE if _QKV_TILE >= 0 else
-           (256 if (prec != "fp32" and Np % 256 == 0 and (Np // 256) * (3 * dp // 128) >= BIG_TILE_BLOCKS) else 0))
+           tile=256 if (prec != "fp32" and Np % 256 == 0 and (Np // 256) * (3 * dp // 128) >= BIG_TILE_BLOCKS) else 0)
     Q, Kt, V = QKV[:, :dp], QKV[:, dp:2 * dp], QKV[:, 2 * dp:]
     S = torch.empty(Np, Np, device=dev, dtype=f32)
     K.gemm(Q, Kt, S, Np, Np, dp, 3 * dp, 3 * dp, Np, trans_b=True, precision=_rp("qk", prec), flops=att,
@@ -421,8 +409,8 @@ def encoder_layer_backward(dX2: torch.Tensor, ctx: EncoderLayerCtx, w: PackedLay
     # LN1 backward -> dX (residual), dA (dropout1 branch)
     dX = torch.empty(Np, dp, device=dev, dtype=f32)
     dA = torch.empty(Np, dp, device=dev, dtype=f32)
-    ln_delta = _LN_DELTA and not _ROWDOT_FUSE
-    if ln_delta:   # LayerNorm1's backward also forms the attention backward's delta = rowsum(dO * O)
+    use_ln_delta = ln_delta(prec)
+    if use_ln_delta:   # LayerNorm1's backward also forms the attention backward's delta = rowsum(dO * O)
         delta = torch.empty(Np, device=dev, dtype=f32)
         K.layernorm_bwd_delta(dX1, dp, ctx.Z1, dp, ctx.mean1, ctx.rstd1, p.n1_w, dX, dp, dA, dp, pd,
                               seeds.get(SITE_DROP1, 0), N, Np, d, dp, ctx.X, dp, w.b_o, delta)
@@ -434,19 +422,13 @@ def encoder_layer_backward(dX2: torch.Tensor, ctx: EncoderLayerCtx, w: PackedLay
     del dX1
     # out-projection
     dO = torch.empty(Np, dp, device=dev, dtype=f32)
-    # delta = rowsum(dO * O): per-64-column partials from the dO GEMM's epilogue, summed by the dS epilogue
-    delta_parts = torch.empty(dp // 64, Np, device=dev, dtype=f32) if _ROWDOT_FUSE else None
-    K.gemm(dA, w.W_o, dO, Np, dp, dp, dp, dp, dp, precision=_rp("out_dx", prec), flops=2.0 * N * d * d,
-           **({} if delta_parts is None else dict(epilogue=E.EPI_STORE_ROWDOT, aux0=ctx.O, ld_aux=dp,
-                                                  rowpart=delta_parts)))
+    K.gemm(dA, w.W_o, dO, Np, dp, dp, dp, dp, dp, precision=_rp("out_dx", prec), flops=2.0 * N * d * d)
     off.run(lambda: _wgrad(dA, dp, ctx.O, dp, dp, dp, Np, g.out_w, (dp, d), (dp, d), _rp("out_dw", prec), N), dA, ctx.O)
     del dA
     # attention core
     QKV = ctx.QKV
     Q, Kt, V = QKV[:, :dp], QKV[:, dp:2 * dp], QKV[:, 2 * dp:]
-    if delta_parts is not None:
-        delta = delta_parts
-    elif not ln_delta:
+    if not use_ln_delta:
         delta = torch.empty(Np, device=dev, dtype=f32)
         K.rowdot(dO, dp, ctx.O, dp, delta, Np, dp)
     dS = torch.empty(Np, Np, device=dev, dtype=f32)

@@ -134,7 +134,8 @@ def gemm(A, B, C, M, N, K, lda, ldb, ldc, trans_a=False, trans_b=False, epilogue
         a.ln_gamma, a.ln_beta, a.ln_y, a.ln_ldy = gam.data_ptr(), bet.data_ptr(), Y.data_ptr(), int(ldy)
         a.ln_mean, a.ln_rstd = mean.data_ptr(), rstd.data_ptr()
         a.ln_d, a.ln_rows, a.ln_eps = int(d_real), int(rows), float(eps)
-    check(hip_lib().u2gnn_gemm(ctypes.byref(a), _s()), "u2gnn_gemm")
+    # pre-split operands exist only in the experiments library (x2_lib); the product library rejects them
+    check((_lib.x2_lib() if x2 else hip_lib()).u2gnn_gemm(ctypes.byref(a), _s()), "u2gnn_gemm")
     if rec:
         ev1.record()
         REC.records.append((gemm_symbol(precision, M, N, split_k, tile, trans_a, trans_b, epilogue, clamp_a, x2),

@@ -65,27 +65,50 @@ class StepGraphs:
         self.epoch = torch.zeros(1, device=dev, dtype=torch.int64)
         K.set_seed_epoch(self.epoch)
         trainer.opt.use_device_schedule()
+        # key -> (graph, the argument objects it was captured with).  The graph holds their device
+        # pointers and shapes, so the objects are kept alive here: a freed batch whose id() is reused
+        # by a new object would otherwise replay a graph over freed memory.
         self.graphs = {}
+        self._open = True
 
     def capture(self, *args) -> "torch.cuda.CUDAGraph":
+        if not self._open:
+            raise RuntimeError("StepGraphs is closed")
         key = tuple(id(a) for a in args)
-        g = self.graphs.get(key)
-        if g is None:
+        ent = self.graphs.get(key)
+        if ent is None:
             torch.cuda.synchronize()
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 K.step_advance(self.epoch, self.tr.opt.t_dev)
                 self.tr.step(*args)
-            self.graphs[key] = g
-        return g
+            ent = self.graphs[key] = (g, args)
+        return ent[0]
 
     def step(self, *args) -> torch.Tensor:
         self.capture(*args).replay()
         return self.tr.loss
 
     def close(self) -> None:
-        """Back to eager steps: the epoch pointer is released, Adam's step count returns to the host."""
+        """Back to eager steps: the epoch pointer is released, Adam's step count returns to the host.
+        Idempotent; also run by the context manager and the finaliser, so the process-wide epoch
+        pointer never outlives self.epoch."""
+        if not self._open:
+            return
+        self._open = False
         torch.cuda.synchronize()
         K.set_seed_epoch(None)
         self.tr.opt.use_host_schedule()
         self.graphs.clear()
+
+    def __enter__(self) -> "StepGraphs":
+        return self
+
+    def __exit__(self, *exc) -> None:
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:   # interpreter shutdown: the library may already be gone
+            pass

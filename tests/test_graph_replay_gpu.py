@@ -147,3 +147,34 @@ def test_unsup_graph_replay_equals_eager_steps():
     (l0, p0), (l1, p1) = finals
     assert np.allclose(l0, l1, rtol=1e-6, atol=0)
     assert ((p0 - p1).abs().max() / p0.abs().max()).item() <= 1e-6
+
+
+def test_eager_steps_while_graphs_are_live_advance_adam():
+    """once StepGraphs switches Adam to the device schedule, an eager trainer.step must
+    still advance the device step count (a fresh t of 0 gave lr / (1 - b1^0) = inf).  Eager and
+    replayed steps interleaved == five eager steps; the context manager releases the epoch."""
+    from u2gnn_hip.train import StepGraphs, SupTrainer
+    base, bs = _sup(8, 1)
+    sd = {k: v.clone() for k, v in base.state_dict().items()}
+    finals = []
+    for mixed in (False, True):
+        base.load_state_dict(sd)
+        m = base.to("cuda").eval()
+        tr = SupTrainer(m, lr=5e-4)
+        losses = []
+        if mixed:
+            with StepGraphs(tr) as runner:
+                for i in range(5):
+                    b = bs[i % 2]
+                    loss = tr.step(b, False) if i in (0, 1, 4) else runner.step(b, False)
+                    losses.append(float(loss.item()))
+                assert int(tr.opt.t_dev.item()) == 5
+            assert tr.opt.t_dev is None and tr.opt.step_count == 5
+        else:
+            losses = [float(tr.step(bs[i % 2], False).item()) for i in range(5)]
+        torch.cuda.synchronize()
+        finals.append((np.array(losses), tr.flat.flat.detach().cpu().clone()))
+    (l0, p0), (l1, p1) = finals
+    assert np.isfinite(p1.numpy()).all()
+    assert np.allclose(l0, l1, rtol=1e-6, atol=0)
+    assert ((p0 - p1).abs().max() / p0.abs().max()).item() <= 1e-6

@@ -12,7 +12,9 @@ over one 64-graph batch per rank; batches are pre-assembled and resident in HBM 
 Data-parallel: one process per GPU, each rank trains its own 64-graph batch (weak scaling; the
 attention couples all graphs of a batch, so a batch never splits across GPUs).
 
-Usage: python bench.py [--gpus N --steps K --warmup W]   (N>1 under torch.distributed.run)
+Usage: python bench.py [--gpus N --steps K --warmup W]
+  N > 1: run under `torch.distributed.run --nproc-per-node N` (the driver's form), or let bench.py
+  start that launcher itself when WORLD_SIZE is unset (the parent never touches the GPU).
 """
 import argparse
 import json
@@ -56,7 +58,12 @@ def parse():
     ap.add_argument("--lr", type=float, default=5e-4)
     ap.add_argument("--distinct-batches", type=int, default=8)
     ap.add_argument("--cpu-baseline", type=int, default=1, help="1 = time the CPU oracle on rank 0 at N=1")
-    ap.add_argument("--cpu-steps", type=int, default=1)
+    ap.add_argument("--cpu-steps", type=int, default=3, help="CPU baseline steps (median reported)")
+    ap.add_argument("--pipeline-steps", type=int, default=20,
+                    help="C4 at N=1: steps of the on-the-fly pipeline line (native assembly + copy-stream H2D + "
+                         "GPU feature gather per step); 0 = skip")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="ranks report (rank, world) and exit before touching the GPU (tests the --gpus launcher)")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--probe", default="ds", choices=["qk", "pv", "ds", "dv", "dq", "dk"],
                     help="attention product timed live (HIP events on its own stream) inside the timed "
@@ -79,18 +86,63 @@ def parse():
 
 
 def pmc_traffic(symbol):
-    """HBM bytes per launch of `symbol` from the committed PMC pass (profiles/<round>/pmc_traffic.json,
+    """HBM bytes per launch of `symbol` from a committed PMC pass (profiles/<round>/pmc_traffic.json,
     written by tools/pmc_traffic.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs with
-    the gfx950 FETCH_SIZE x2 correction).  None when no pass covers this kernel."""
+    the gfx950 FETCH_SIZE x2 correction) OF THIS BUILD: the table's build_id must equal the hash of
+    the native sources (u2gnn_hip._lib.source_build_id).  Returns (bytes or None, source or note)."""
     import glob
-    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*", "pmc_traffic.json")), reverse=True):
+    from u2gnn_hip._lib import source_build_id
+    bid = source_build_id()
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*", "*pmc_traffic.json")), reverse=True):
         try:
             table = json.load(open(path))
         except (OSError, ValueError):
             continue
-        if symbol in table.get("kernels", {}):
-            return table["kernels"][symbol]["hbm_bytes_per_launch"]
-    return None
+        if table.get("build_id") == bid and symbol in table.get("kernels", {}):
+            return table["kernels"][symbol]["hbm_bytes_per_launch"], os.path.relpath(path, REPO)
+    return None, f"no PMC pass of build {bid} covers this kernel"
+
+
+def host_cpu():
+    """(model name, logical CPUs) of the host, from /proc/cpuinfo (lscpu's source)."""
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return model, os.cpu_count()
+
+
+def cpu_threads():
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
+    return max(1, min(threads, os.cpu_count()))
+
+
+def launch_ranks(args) -> int:
+    """--gpus N > 1 without a launcher: run `torch.distributed.run --nproc-per-node N bench.py ...` as a
+    CHILD process (this process has not initialised the GPU and never does; no exec) and relay the
+    ranks' JSON lines.  Returns the launcher's exit code."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True)
+    for line in proc.stdout:
+        line = line.strip()
+        if line.startswith("{"):
+            try:
+                json.loads(line)
+            except ValueError:
+                continue
+            print(line, flush=True)
+    return proc.wait()
 
 
 def model_step_flops(N, d, ff, T, L):
@@ -128,10 +180,10 @@ def gather_roofline(b, d, ff, K, dev, reps=20):
 
 def cpu_baseline(hb, sd, args, d, C):
     """The oracle restatement (reference semantics incl. all k+1 slots and p=0.5 dropout,
-    i.e. the reference's cost) timed on the host cores: forward + loss + backward + clip + Adam."""
+    i.e. the reference's cost) timed on the host cores: forward + loss + backward + clip + Adam;
+    median of --cpu-steps (>= 3) steps on one batch."""
     from oracle import u2gnn_oracle as O
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
-    threads = max(1, min(threads, os.cpu_count()))
+    threads = cpu_threads()
     torch.set_num_threads(threads)
     params = {k: v.detach().cpu().clone().requires_grad_(True) for k, v in sd.items()}
     plist = list(params.values())
@@ -151,65 +203,163 @@ def cpu_baseline(hb, sd, args, d, C):
         opt.step()
         times.append(time.perf_counter() - t0)
     t = float(np.median(times))
+    model, ncpu = host_cpu()
     return {"value": hb.labels.shape[0] / t, "unit": "graphs/s", "cores": threads, "kind": "port",
-            "sample": f"{args.cpu_steps} full training step(s) of one {hb.labels.shape[0]}-graph batch "
+            "cpu_model": model, "host_cpus": ncpu, "step_s": [round(x, 2) for x in times],
+            "sample": f"median of {args.cpu_steps} full training steps of one {hb.labels.shape[0]}-graph batch "
                       f"(N={hb.N} nodes, all {args.num_neighbors + 1} neighbour slots, dropout on) "
-                      f"= {t:.1f} s/step, oracle/u2gnn_oracle.py on torch CPU"}
+                      f"= {t:.1f} s/step, oracle/u2gnn_oracle.py on torch CPU, {threads} threads"}
+
+
+def pipeline_rate(store, trainer, args, dev, resident_value):
+    """The same C4 training step with each batch built on the fly (SURVEY §8(d)'s timed region
+    with the H2D inside; train_pytorch_U2GNN_Sup.py:114,117,153): native assembly of the next
+    batch from the reference numpy stream into page-locked buffers, its H2D on the copy stream and
+    the feature gather on the GPU (DeviceBatch.from_store), then the step.  Reported beside the
+    resident-batch value, never as it (PCIe-inclusive rate)."""
+    from u2gnn_hip.batching import BatchLoader
+    from u2gnn_hip.core import DeviceBatch
+    from u2gnn_hip.synthetic import as_graph_store
+    gs = as_graph_store(store)
+    X_dev = torch.from_numpy(gs.X).to(dev)
+    np.random.seed(321)
+    loader = BatchLoader(gs, args.batch_size, args.num_neighbors, gather_x=False)
+    for _ in range(2):
+        trainer.step(DeviceBatch.from_store(loader(), X_dev, device=dev))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.pipeline_steps):
+        trainer.step(DeviceBatch.from_store(loader(), X_dev, device=dev))
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    v = args.pipeline_steps * args.batch_size / el
+    return {"value": round(v, 2), "unit": "graphs/s", "ms_per_step": round(1e3 * el / args.pipeline_steps, 3),
+            "steps": args.pipeline_steps, "ratio_to_resident": round(v / resident_value, 4),
+            "what": "per step: native batch assembly (numpy MT19937 stream continued in C++) into page-locked "
+                    "buffers, H2D on a copy stream, GPU feature gather, training step"}
 
 
 METRIC_C5 = "graphs/sec (fwd+bwd) U2GNN-UnSup REDDIT-M5K k=16 T=4 S=512 MI355X"
+
+
+def init_dist(args, dev):
+    """RCCL process group when the job has more than one rank (or --force-dist)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1 or args.force_dist:
+        import torch.distributed as dist
+        if "MASTER_ADDR" not in os.environ:   # --force-dist without a launcher: a 1-rank group
+            os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=os.environ.get("MASTER_PORT", "29533"))
+        dist.init_process_group("nccl", device_id=dev, rank=rank, world_size=world)
+        return dist, world, rank
+    return None, world, rank
+
+
+def unsup_cpu_baseline(hbs, sids, sd, V, T, lr, steps):
+    """C5 CPU baseline: the oracle's UnSup composite with the reference's cost (all k+1 slots,
+    dropout on) on the same batches and sample ids: forward + summed loss + backward + clip + Adam
+    over the encoders and the dense [V, D] table; median of `steps` steps."""
+    from oracle import u2gnn_oracle as O
+    threads = cpu_threads()
+    torch.set_num_threads(threads)
+    params = {k: v.detach().cpu().clone().requires_grad_(True) for k, v in sd.items()}
+    plist = list(params.values())
+    opt = torch.optim.Adam(plist, lr=lr)
+    enc = {k: v for k, v in params.items() if k != "ss.weight"}
+    times = []
+    for r in range(steps):
+        h, sid = hbs[r % len(hbs)], sids[r % len(sids)]
+        t0 = time.perf_counter()
+        opt.zero_grad()
+        lo = O.unsup_forward(enc, params["ss.weight"], torch.from_numpy(h.input_x), torch.from_numpy(h.X_concat),
+                             torch.from_numpy(h.input_y), torch.from_numpy(sid), 1, T, train=True).sum()
+        lo.backward()
+        torch.nn.utils.clip_grad_norm_(plist, 0.5)
+        opt.step()
+        times.append(time.perf_counter() - t0)
+    t = float(np.median(times))
+    model, ncpu = host_cpu()
+    return {"value": hbs[0].labels.shape[0] / t, "unit": "graphs/s", "cores": threads, "kind": "port",
+            "cpu_model": model, "host_cpus": ncpu, "step_s": [round(x, 2) for x in times],
+            "sample": f"median of {steps} training steps on the first {min(steps, len(hbs))} bench batches "
+                      f"(all {hbs[0].input_x.shape[1]} neighbour slots, dropout on, V = {V}), "
+                      f"median {t:.2f} s/step, oracle/u2gnn_oracle.py on torch CPU, {threads} threads"}
 
 
 def main_c5(args):
     """synthetic REDDIT-MULTI-5K (4999 graphs, mean 508.5 nodes, V = sum of
     nodes ~2.54M), batch 4, k=16, T=4, ff=1024, 512 sampled classes, D = 4.  HBM-bound: the
     roofline kernel is the optimizer sweep (clip-norm + Adam over the dense embedding table,
-    32 algorithmic bytes per parameter: sqnorm reads g; Adam reads p, g, m, v and writes p, m, v)."""
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world != 1:
-        raise SystemExit("--workload c5 runs on one GPU (replicas only)")
-    dev = torch.device("cuda", 0)
+    32 algorithmic bytes per parameter: sqnorm reads g; Adam reads p, g, m, v and writes p, m, v).
+    Data-parallel (world > 1): rank r trains batch r of each group of `world` with the r-th sample
+    draw of the group; encoder gradients all-reduced, ss.weight's touched rows all-gathered
+    (dp.UnSupGradSync)."""
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = torch.device("cuda", local_rank)
     torch.cuda.set_device(dev)
+    dist, world, rank = init_dist(args, dev)
     from pytorch_U2GNN_UnSup import TransformerU2GNN as UnSupModel
     from u2gnn_hip.batching import BatchLoader
     from u2gnn_hip.core import DeviceBatch
+    from u2gnn_hip.dp import UnSupGradSync, broadcast_params, max_batch_nodes, rank_batches
     from u2gnn_hip.synthetic import reddit5k_like
     from u2gnn_hip.unsup import UnSupTrainer
+    bs = 4
     store = reddit5k_like(seed=0)
     V = int(store.node_start[-1])
     np.random.seed(123)
-    loader = BatchLoader(store, 4, args.num_neighbors, with_input_y=True)
+    loader = BatchLoader(store, bs, args.num_neighbors, with_input_y=True)
+    host = rank_batches(loader, world, rank, args.distinct_batches)
     torch.manual_seed(123)
     model = UnSupModel(feature_dim_size=4, ff_hidden_size=args.ff_hidden_size, dropout=0.5,
                        num_self_att_layers=args.num_timesteps, vocab_size=V, sampled_num=512,
-                       num_U2GNN_layers=args.num_hidden_layers, device=dev, precision=args.precision).to(dev)
-    trainer = UnSupTrainer(model, lr=args.lr, max_norm=0.5)
-    batches = []
+                       num_U2GNN_layers=args.num_hidden_layers, device=dev, precision=args.precision)
+    sd0 = {k: v.clone() for k, v in model.state_dict().items() if k in set(model.trainable_names())}
+    model = model.to(dev)
+    # one sample draw per batch of the single stream; rank r keeps draw r of each group
+    sids_host = []
     for _ in range(args.distinct_batches):
-        hb = loader()
-        b = DeviceBatch.from_offsets(hb.input_x, hb.offsets, hb.X_concat, None, device=dev, input_y=hb.input_y)
-        batches.append((b, torch.from_numpy(model.ss.draw_samples()).to(dev)))
+        draws = [model.ss.draw_samples() for _ in range(world)]
+        sids_host.append(draws[rank])
+    trainer = UnSupTrainer(model, lr=args.lr, max_norm=0.5, seed=123 + rank)
+    if dist is not None:
+        broadcast_params(trainer.flat)
+        sync = UnSupGradSync(trainer.flat, max_batch_nodes(store.node_start, bs))
+        trainer.grad_sync = trainer.row_sync = sync
+    batches = [(DeviceBatch.from_offsets(h.input_x, h.offsets, h.X_concat, None, device=dev, input_y=h.input_y),
+                torch.from_numpy(s).to(dev)) for h, s in zip(host, sids_host)]
     nb = len(batches)
-    graph = args.graph != 0
+    graph = args.graph != 0 and dist is None
     runner = None
-    if graph:   # one captured HIP graph per distinct batch, captured (not run) before the warmup
-        from u2gnn_hip.train import StepGraphs
-        runner = StepGraphs(trainer)
-        for bt in batches:
-            runner.capture(*bt)
-    step = runner.step if runner is not None else trainer.step
-    for i in range(args.warmup):
-        step(*batches[i % nb])
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(*batches[(args.warmup + i) % nb])
-    t_issue = time.perf_counter() - t0          # host time to enqueue the K steps
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    loss = float(trainer.loss.item())
-    if runner is not None:
-        runner.close()
+    try:
+        if graph:   # one captured HIP graph per distinct batch, captured (not run) before the warmup
+            from u2gnn_hip.train import StepGraphs
+            runner = StepGraphs(trainer)
+            for bt in batches:
+                runner.capture(*bt)
+        step = runner.step if runner is not None else trainer.step
+        for i in range(args.warmup):
+            step(*batches[i % nb])
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            step(*batches[(args.warmup + i) % nb])
+        t_issue = time.perf_counter() - t0          # host time to enqueue the K steps
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        loss = float(trainer.loss.item())
+    finally:
+        if runner is not None:
+            runner.close()
+    if dist is not None:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
     roof = None
     if not args.no_roofline:
         n = trainer.flat.n
@@ -229,18 +379,27 @@ def main_c5(args):
                 "params": n, "algorithmic_bytes_per_step": byts, "optimizer_us": round(us, 1),
                 "optimizer_share_of_step": round(us * 1e-3 / (1e3 * elapsed / args.steps), 3)}
     mean_N = float(np.mean([b.N for b, _ in batches]))
-    out = {"metric": METRIC_C5, "value": round(args.steps * 4 / elapsed, 2), "unit": "graphs/s", "n_gpus": 1,
-           "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 3),
-           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.precision,
+    out = {"metric": METRIC_C5, "value": round(args.steps * bs * world / elapsed, 2), "unit": "graphs/s",
+           "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+           "ms_per_step": round(1e3 * elapsed / args.steps, 3), "higher_is_better": True, "scaling": "weak",
+           "vs_baseline": None, "dtype": args.precision,
            "data": f"synthetic REDDIT-M5K-like graphs (4999 graphs, V={V} nodes, X = 0.01*ones[n,4]); "
                    "random-init weights",
-           "config": {"workload": "U2GNN-UnSup REDDIT-M5K (C5): batch_size=4, num_neighbors=16, num_timesteps=4, "
+           "config": {"workload": "U2GNN-UnSup REDDIT-M5K (C5): batch_size=4/GPU, num_neighbors=16, num_timesteps=4, "
                                   "ff_hidden_size=1024, sampled_num=512, D=4",
-                      "global_batch": 4, "mean_nodes_per_batch": round(mean_N, 1), "parallelism": "dp1",
+                      "global_batch": bs * world, "mean_nodes_per_batch": round(mean_N, 1),
+                      "parallelism": f"dp{world}" + (" (encoder all-reduce + ss.weight row all-gather)" if world > 1
+                                                     else ""),
                       "precision": args.precision, "hip_graph": graph},
            "final_loss": round(loss, 4), "host_issue_ms_per_step": round(1e3 * t_issue / args.steps, 3),
            "roofline": roof, "cpu_baseline": None}
-    emit(out)
+    if rank == 0 and world == 1 and args.cpu_baseline:
+        out["cpu_baseline"] = unsup_cpu_baseline(host, sids_host, sd0, V, args.num_timesteps, args.lr,
+                                                 max(3, args.cpu_steps))
+    if rank == 0:
+        emit(out)
+    if dist is not None:
+        dist.destroy_process_group()
 
 
 METRIC_SMALL = {"c2": "graphs/sec (fwd+bwd) U2GNN-Sup IMDBBINARY k=8 T=4 MI355X",
@@ -370,27 +529,31 @@ def emit(out: dict) -> None:
 def main():
     global _JSON_OUT
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # no launcher around us: start one as a child; nothing here has touched the GPU
+        sys.exit(launch_ranks(args))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"WORLD_SIZE={world} but --gpus {args.gpus}: one rank per GPU")
+    if args.launch_check:   # test hook: the launcher reached every rank (no GPU work)
+        print(json.dumps({"launch_check": True, "rank": int(os.environ.get("RANK", "0")), "world": world}),
+              flush=True)
+        return
     sys.stdout.flush()
     _JSON_OUT = os.fdopen(os.dup(1), "w")
     os.dup2(2, 1)   # fd 1 -> stderr for everything else (native libraries write to fd 1 directly)
     if args.workload == "c5":
         return main_c5(args)
     if args.workload in ("c2", "c3"):
+        if world != 1:
+            raise SystemExit("--workload c2/c3 runs on one GPU")
         return main_small(args)
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
-    dist = None
-    if os.environ.get("U2GNN_EARLY_SIDE", "1") == "1":
-        from u2gnn_hip.engine import side_stream
-        side_stream(dev)   # before RCCL creates its streams (own hardware queue, see side_stream)
-    if world > 1 or args.force_dist:
-        import torch.distributed as dist
-        if "MASTER_ADDR" not in os.environ:   # --force-dist without a launcher: a 1-rank group
-            os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=os.environ.get("MASTER_PORT", "29533"))
-        dist.init_process_group("nccl", device_id=dev, rank=rank, world_size=world)
+    from u2gnn_hip.engine import side_stream
+    side_stream(dev)   # before RCCL creates its streams (own hardware queue, see side_stream)
+    dist, world, rank = init_dist(args, dev)
 
     from pytorch_U2GNN_Sup import TransformerU2GNN
     from u2gnn_hip.batching import BatchLoader
@@ -430,18 +593,6 @@ def main():
     nb = len(batches)
     graph = args.graph == 1 and dist is None
     runner = None
-    if graph:   # one captured HIP graph per distinct batch, captured (not run) before the warmup
-        from u2gnn_hip.train import StepGraphs
-        runner = StepGraphs(trainer)
-        for bt in batches:
-            runner.capture(bt)
-    step = runner.step if runner is not None else trainer.step
-    for i in range(args.warmup):
-        step(batches[i % nb])
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
     from u2gnn_hip import native
     from u2gnn_hip import _lib as LIB
     role = {"qk": LIB.ROLE_QK, "pv": LIB.ROLE_PV, "ds": LIB.ROLE_DS, "dv": LIB.ROLE_DV, "dq": LIB.ROLE_DQ,
@@ -449,19 +600,33 @@ def main():
     # (graph replay: the probe's events would belong to the capture, so no live probe)
     probing = not args.no_roofline and args.attention == "nodes" and native.enabled() and not graph
     per_step = args.num_hidden_layers * args.num_timesteps
-    if probing:   # live: HIP events around every launch of that product, on its stream
-        native.probe_arm(role, args.steps * per_step)
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(batches[(args.warmup + i) % nb])
-    t_issue = time.perf_counter() - t0          # host time to enqueue the K steps
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    probe_ms, probe_n = native.probe_collect() if probing else (0.0, 0)
-    if runner is not None:
-        runner.close()
+    try:
+        if graph:   # one captured HIP graph per distinct batch, captured (not run) before the warmup
+            from u2gnn_hip.train import StepGraphs
+            runner = StepGraphs(trainer)
+            for bt in batches:
+                runner.capture(bt)
+        step = runner.step if runner is not None else trainer.step
+        for i in range(args.warmup):
+            step(batches[i % nb])
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        if probing:   # live: HIP events around every launch of that product, on its stream
+            native.probe_arm(role, args.steps * per_step)
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            step(batches[(args.warmup + i) % nb])
+        t_issue = time.perf_counter() - t0          # host time to enqueue the K steps
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        probe_ms, probe_n = native.probe_collect() if probing else (0.0, 0)
+    finally:
+        if runner is not None:
+            runner.close()
     loss = float(trainer.loss.item())
     # optional per-GEMM family pass: the same K steps again, serialised, with per-GEMM HIP events
     K.REC.records.clear()
@@ -510,8 +675,9 @@ def main():
         sym = K.gemm_symbol(pk, Np0, nn, split, tile, ta, tb, epi, clamp_a=args.probe in ("pv", "dv"))
         ach = fl / (probe_ms * 1e-3) / 1e12
         peak = PEAK[pk]
+        traffic, traffic_src = pmc_traffic(sym)
         roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
-                "frac": round(ach / peak, 4), "traffic": pmc_traffic(sym),
+                "frac": round(ach / peak, 4), "traffic": traffic, "traffic_source": traffic_src,
                 "kernel": sym, "kernel_precision": pk, "role": args.probe,
                 "timing": "live: HIP events around each launch on its own stream inside the timed region",
                 "dominance": "largest per-product device time on the critical path (DESIGN.md section 8)",
@@ -539,6 +705,8 @@ def main():
            "roofline": roof, "gather": None, "cpu_baseline": None}
     if rank == 0:
         out["gather"] = gather_roofline(used[0], d, args.ff_hidden_size, K, dev)
+    if rank == 0 and world == 1 and args.pipeline_steps > 0 and args.attention == "nodes":
+        out["pipeline"] = pipeline_rate(store, trainer, args, dev, value)
     if rank == 0 and world == 1 and args.cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(host[args.warmup % nb], sd0, args, d, C)
     if rank == 0:

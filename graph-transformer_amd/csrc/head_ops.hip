@@ -328,6 +328,8 @@ __device__ __forceinline__ void ss_block_sum(float (&acc)[SS_CH], float (*red)[S
 // dX[i, c] = g_i (sum_j prob_ij W[s_j, c] - W[y_i, c]); dW[y_i, c] -= g_i X[i, c].
 // One block per input row; the S sampled rows are spread over the 256 threads (each thread
 // gathers its rows' SS_CH-column slices: independent loads, no serial latency chain over S).
+// ROWS (ABI v9): the label term is stored as compact row i of dW (ld lddw) instead of added at y_i.
+template <bool ROWS>
 __global__ void __launch_bounds__(256) ss_bwd_x_kernel(const float *X, int64_t ldx, const int64_t *labels,
                                                        const int64_t *sids, int64_t S, const float *W, int64_t ldw,
                                                        const float *prob, const float *dloss, float *dX, int64_t lddx,
@@ -357,20 +359,24 @@ __global__ void __launch_bounds__(256) ss_bwd_x_kernel(const float *X, int64_t l
                 if (tid == k) t = tot[k];
             const int64_t c = c0 + tid;
             dX[i * lddx + c] = g * (t - W[y * ldw + c]);
-            atomicAdd(dW + y * lddw + c, -g * X[i * ldx + c]);
+            if constexpr (ROWS)
+                dW[i * lddw + c] = -g * X[i * ldx + c];
+            else
+                atomicAdd(dW + y * lddw + c, -g * X[i * ldx + c]);
         }
     }
 }
 
 // dW[s_j, c] += sum_i g_i prob_ij X[i, c]; one block per sample j, the input rows spread over
-// the 256 threads (independent loads), deterministic block sum.
+// the 256 threads (independent loads), deterministic block sum.  ROWS: stored as compact row j.
+template <bool ROWS>
 __global__ void __launch_bounds__(256) ss_bwd_w_kernel(const float *X, int64_t ldx, const int64_t *sids, int64_t S,
                                                        const float *prob, const float *dloss, float *dW, int64_t lddw,
                                                        int64_t n_rows, int64_t D) {
     __shared__ float red[4][SS_CH];
     const int64_t j = blockIdx.x;
     const int tid = threadIdx.x;
-    float *dw = dW + sids[j] * lddw;
+    float *dw = dW + (ROWS ? j : sids[j]) * lddw;
     for (int64_t c0 = 0; c0 < D; c0 += SS_CH) {
         float acc[SS_CH], tot[SS_CH];
 #pragma unroll
@@ -388,7 +394,34 @@ __global__ void __launch_bounds__(256) ss_bwd_w_kernel(const float *X, int64_t l
 #pragma unroll
             for (int k = 1; k < SS_CH; ++k)
                 if (tid == k) t = tot[k];
-            atomicAdd(dw + c0 + tid, t);
+            if constexpr (ROWS)
+                dw[c0 + tid] = t;
+            else
+                atomicAdd(dw + c0 + tid, t);
+        }
+    }
+}
+
+// dst[idx[r], c] (+)= alpha * src[r, c]: one wave per row, the row's columns over the lanes.  ZERO:
+// dst[idx[r], c] = 0 (src unused).  Destinations of one launch are distinct (u2gnn_hip.h), so the
+// read-modify-write needs no atomics.
+template <bool ZERO>
+__global__ void __launch_bounds__(256) index_rows_kernel(const float *src, int64_t ld_src, const int64_t *idx,
+                                                         int64_t n_rows, float alpha, float *dst, int64_t ld_dst,
+                                                         int64_t dst_rows, int64_t D, int32_t *err) {
+    const int lane = threadIdx.x & 63;
+    for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < n_rows; r += (int64_t)gridDim.x * 4) {
+        const int64_t y = idx[r];
+        if (y < 0 || y >= dst_rows) {
+            if (err && lane == 0) *err = 1;
+            continue;
+        }
+        float *d = dst + y * ld_dst;
+        for (int64_t c = lane; c < D; c += 64) {
+            if constexpr (ZERO)
+                d[c] = 0.f;
+            else
+                d[c] += alpha * src[r * ld_src + c];
         }
     }
 }
@@ -513,10 +546,46 @@ int u2gnn_sampled_softmax_bwd(const float *X, int64_t ldx, const int64_t *labels
     if (!X || !labels || !sample_ids || !W || !prob || !dX || !dW || S < 1) return U2GNN_E_ARG;
     if (n_rows == 0) return U2GNN_OK;
     hipStream_t st = u2gnn_stream(stream);
-    hipLaunchKernelGGL(ss_bwd_x_kernel, dim3((unsigned)n_rows), dim3(256), 0, st, X, ldx, labels, sample_ids, S, W, ldw,
-                       prob, dloss, dX, lddx, dW, lddw, D);
-    hipLaunchKernelGGL(ss_bwd_w_kernel, dim3((unsigned)S), dim3(256), 0, st, X, ldx, sample_ids, S, prob, dloss, dW,
-                       lddw, n_rows, D);
+    hipLaunchKernelGGL(ss_bwd_x_kernel<false>, dim3((unsigned)n_rows), dim3(256), 0, st, X, ldx, labels, sample_ids, S,
+                       W, ldw, prob, dloss, dX, lddx, dW, lddw, D);
+    hipLaunchKernelGGL(ss_bwd_w_kernel<false>, dim3((unsigned)S), dim3(256), 0, st, X, ldx, sample_ids, S, prob, dloss,
+                       dW, lddw, n_rows, D);
+    return u2gnn_launch_status();
+}
+
+int u2gnn_sampled_softmax_bwd_rows(const float *X, int64_t ldx, const int64_t *labels, const int64_t *sample_ids,
+                                   int64_t S, const float *W, int64_t ldw, const float *prob, const float *dloss,
+                                   float *dX, int64_t lddx, float *dW_lab, int64_t ld_lab, float *dW_smp,
+                                   int64_t ld_smp, int64_t n_rows, int64_t D, void *stream) {
+    if (!X || !labels || !sample_ids || !W || !prob || !dX || !dW_smp || S < 1 || D < 1) return U2GNN_E_ARG;
+    if (n_rows > 0 && !dW_lab) return U2GNN_E_ARG;
+    if (ld_lab < D || ld_smp < D) return U2GNN_E_ARG;
+    hipStream_t st = u2gnn_stream(stream);
+    if (n_rows > 0)
+        hipLaunchKernelGGL(ss_bwd_x_kernel<true>, dim3((unsigned)n_rows), dim3(256), 0, st, X, ldx, labels, sample_ids,
+                           S, W, ldw, prob, dloss, dX, lddx, dW_lab, ld_lab, D);
+    hipLaunchKernelGGL(ss_bwd_w_kernel<true>, dim3((unsigned)S), dim3(256), 0, st, X, ldx, sample_ids, S, prob, dloss,
+                       dW_smp, ld_smp, n_rows, D);
+    return u2gnn_launch_status();
+}
+
+int u2gnn_index_add_rows(const float *src, int64_t ld_src, const int64_t *idx, int64_t n_rows, float alpha,
+                         float *dst, int64_t ld_dst, int64_t dst_rows, int64_t D, int32_t *err, void *stream) {
+    if (n_rows < 0 || D < 0) return U2GNN_E_ARG;
+    if (n_rows == 0 || D == 0) return U2GNN_OK;
+    if (!src || !idx || !dst || ld_src < D || ld_dst < D) return U2GNN_E_ARG;
+    hipLaunchKernelGGL(index_rows_kernel<false>, dim3(grid_for(n_rows, 4, 1 << 20)), dim3(256), 0,
+                       u2gnn_stream(stream), src, ld_src, idx, n_rows, alpha, dst, ld_dst, dst_rows, D, err);
+    return u2gnn_launch_status();
+}
+
+int u2gnn_index_zero_rows(const int64_t *idx, int64_t n_rows, float *dst, int64_t ld_dst, int64_t dst_rows, int64_t D,
+                          int32_t *err, void *stream) {
+    if (n_rows < 0 || D < 0) return U2GNN_E_ARG;
+    if (n_rows == 0 || D == 0) return U2GNN_OK;
+    if (!idx || !dst || ld_dst < D) return U2GNN_E_ARG;
+    hipLaunchKernelGGL(index_rows_kernel<true>, dim3(grid_for(n_rows, 4, 1 << 20)), dim3(256), 0,
+                       u2gnn_stream(stream), nullptr, 0, idx, n_rows, 0.f, dst, ld_dst, dst_rows, D, err);
     return u2gnn_launch_status();
 }
 

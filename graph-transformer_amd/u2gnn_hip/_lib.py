@@ -32,7 +32,7 @@ ERRORS = {-1: "bad argument", -2: "misaligned pointer / leading dimension", -3: 
 
 EPI_STORE, EPI_BIAS, EPI_BIAS_DROP_RESID, EPI_BIAS_RELU_DROP, EPI_RELU_DROP_BWD, EPI_ACCUM, EPI_ATTN_DS, \
     EPI_ATTN_DS_SIGNED, EPI_ATTN_DS_RECOMP, EPI_BIAS_DROP_RESID_LN, EPI_STORE_ROWDOT = range(11)
-ABI_VERSION = 8   # include/u2gnn_hip.h U2GNN_ABI_VERSION
+ABI_VERSION = 9   # include/u2gnn_hip.h U2GNN_ABI_VERSION
 PREC_F32, PREC_BF16X3, PREC_BF16 = 0, 1, 2
 
 
@@ -138,6 +138,10 @@ _HIP_SIGS = {
     "u2gnn_adam": ([VP, VP, VP, VP, I64, VP, F32, F32, F32, F32, F32, F32, VP], c_int32),
     "u2gnn_sampled_softmax_fwd": ([VP, I64, VP, VP, I64, VP, I64, VP, VP, I64, I64, VP], c_int32),
     "u2gnn_sampled_softmax_bwd": ([VP, I64, VP, VP, I64, VP, I64, VP, VP, VP, I64, VP, I64, I64, I64, VP], c_int32),
+    "u2gnn_sampled_softmax_bwd_rows": ([VP, I64, VP, VP, I64, VP, I64, VP, VP, VP, I64, VP, I64, VP, I64, I64, I64, VP],
+                                       c_int32),
+    "u2gnn_index_add_rows": ([VP, I64, VP, I64, F32, VP, I64, I64, I64, VP, VP], c_int32),
+    "u2gnn_index_zero_rows": ([VP, I64, VP, I64, I64, I64, VP, VP], c_int32),
     "u2gnn_dropout_mask": ([c_uint64, I64, I64, F32, VP, VP], c_int32),
     "u2gnn_dropout": ([VP, I64, VP, I64, I64, I64, F32, c_uint64, VP], c_int32),
     "u2gnn_probe_arm": ([I32, I32], c_int32),
@@ -215,6 +219,22 @@ def check(rc: int, what: str):
     if rc != 0:
         msg = ERRORS.get(rc, f"hipError {rc}")
         raise U2GNNNativeError(f"{what} failed: {msg} (rc={rc})")
+
+
+def source_build_id() -> str:
+    """Hash of the native sources (csrc/ + include/): the build a profile was taken from.  bench.py
+    uses a committed PMC traffic table only when its recorded build id equals this one."""
+    import hashlib
+    h = hashlib.sha256()
+    csrc = os.path.join(PKG_ROOT, "csrc")
+    files = sorted(os.path.join(csrc, f) for f in os.listdir(csrc)
+                   if f.endswith((".hip", ".cpp", ".h")) or f == "Makefile")
+    files += sorted(os.path.join(INCLUDE_DIR, f) for f in os.listdir(INCLUDE_DIR) if f.endswith(".h"))
+    for f in files:
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
 
 
 def header_symbols(header: str):

@@ -6,16 +6,23 @@ numpy stream; rank r assembles batch r and *replays* (consumes without building)
 the union of the ranks' batches is exactly what a single process would train on G steps.  A
 64-graph batch never splits across GPUs (attention couples all graphs of a batch).
 
-The only collective is the gradient all-reduce (average) over the flat fp32 gradient buffer,
-issued in a few large buckets: xGMI is point-to-point (7 links per GPU), so RCCL's ring/tree
-bandwidth per collective is what matters, and a handful of multi-MB buckets keeps it link-bound
-rather than latency-bound.  Clip + Adam then run redundantly (bit-identically) on every rank.
+Supervised step: the only collective is the gradient all-reduce (average) over the flat fp32
+gradient buffer, issued in a few large buckets: xGMI is point-to-point (7 links per GPU), so RCCL's
+ring/tree bandwidth per collective is what matters, and a handful of multi-MB buckets keeps it
+link-bound rather than latency-bound.  Clip + Adam then run redundantly (bit-identically) on every rank.
+
+Unsupervised step (UnSupGradSync): the encoder gradients (37 K floats at C5) are all-reduced; the
+embedding table's gradient (ss.weight, [V, D] = 10.2 M floats at C5) is non-zero only on the rows a
+batch touches -- its nodes' labels and the 512 sampled ids (sampled_softmax.py:45,48) -- so those rows
+are all-gathered (ids + values, ~40 KB per rank at C5) and folded into every rank's dense gradient
+in rank order: the dense all-reduce's result at a fraction of its bytes.
 """
 from __future__ import annotations
 
 import contextlib
 from typing import Dict, List, Optional, Tuple
 
+import numpy as np
 import torch
 
 
@@ -121,3 +128,86 @@ class OverlappedGradAllReduce:
 def broadcast_params(flat, src: int = 0, group=None) -> None:
     import torch.distributed as dist
     dist.broadcast(flat.flat, src, group=group)
+
+
+def max_batch_nodes(node_start, batch_size: int) -> int:
+    """An upper bound on the nodes of any batch of `batch_size` graphs (the sum of the largest graph
+    sizes): the fixed per-rank row count of the label-row all-gather, so that no rank has to learn
+    the others' batch sizes (no host synchronisation inside a step)."""
+    sizes = np.diff(np.asarray(node_start, dtype=np.int64))
+    return int(np.sort(sizes)[::-1][:batch_size].sum())
+
+
+class UnSupGradSync:
+    """Data-parallel gradient exchange of the unsupervised U2GNN step (SURVEY.md §8(e);
+    train_pytorch_U2GNN_UnSup.py:149-162).  Rank r trains batch r of each group of `world` consecutive
+    batches (rank_batches) with the r-th sample draw of the group, so the ranks together see exactly
+    what one process sees in `world` steps; the averaged gradient is their mean.
+
+    * ``__call__(flat)``: all-reduce (sum, then 1/world) of the encoder region of the flat gradient;
+      the ss.weight region is excluded (its rows come from ``rows``).
+    * ``rows(ids_lab, rows_lab, ids_smp, rows_smp, gW)``: all-gather every rank's compact rows
+      (label rows padded with id -1 to ``id_cap``; the S sample rows) and fold them into the dense
+      gW (all zero on entry) in rank order, labels before samples, scaled by 1/world -- the same
+      destinations in the same order on every rank, so every rank holds the same bits.  Returns the
+      gathered id tensors (the rows to zero after the optimizer step).
+
+    Device tensors go through u2gnn_index_add_rows; CPU tensors (the gloo tests) through torch's
+    index_add_ with the padding rows dropped -- the same sums in the same order."""
+
+    def __init__(self, flat, id_cap: int, group=None, weight_name: str = "ss.weight"):
+        import torch.distributed as dist
+        self.dist = dist
+        self.group = group
+        self.world = dist.get_world_size(group)
+        g = flat.grads[weight_name]
+        self.lo = (g.data_ptr() - flat.gflat.data_ptr()) // 4
+        self.hi = self.lo + g.numel()
+        self.id_cap = int(id_cap)
+        self._bufs: Dict = {}
+
+    def __call__(self, flat) -> None:
+        g = flat.gflat
+        regions = [(0, self.lo), (self.hi, g.numel())]
+        for a, b in regions:
+            if b > a:
+                self.dist.all_reduce(g[a:b], group=self.group)
+                g[a:b].mul_(1.0 / self.world)
+
+    def _gather(self, t: torch.Tensor) -> torch.Tensor:
+        # concatenated along dim 0 (the layout both RCCL and gloo accept), viewed as [world, ...]
+        out = torch.empty((self.world * t.shape[0],) + tuple(t.shape[1:]), device=t.device, dtype=t.dtype)
+        self.dist.all_gather_into_tensor(out, t.contiguous(), group=self.group)
+        return out.view((self.world,) + tuple(t.shape))
+
+    def rows(self, ids_lab: torch.Tensor, rows_lab: torch.Tensor, ids_smp: torch.Tensor, rows_smp: torch.Tensor,
+             gW: torch.Tensor):
+        n, D = rows_lab.shape
+        if n > self.id_cap:
+            raise ValueError(f"batch has {n} label rows, above the exchange cap {self.id_cap}")
+        key = (ids_lab.device, D)
+        buf = self._bufs.get(key)
+        if buf is None:
+            buf = self._bufs[key] = (torch.empty(self.id_cap, dtype=torch.int64, device=ids_lab.device),
+                                     torch.empty(self.id_cap, D, dtype=rows_lab.dtype, device=rows_lab.device))
+        ids_pad, rows_pad = buf
+        ids_pad.fill_(-1)
+        ids_pad[:n].copy_(ids_lab)
+        rows_pad[:n].copy_(rows_lab)
+        rows_pad[n:].zero_()
+        all_ids_lab, all_rows_lab = self._gather(ids_pad), self._gather(rows_pad)
+        all_ids_smp, all_rows_smp = self._gather(ids_smp.to(torch.int64)), self._gather(rows_smp)
+        alpha = 1.0 / self.world
+        for r in range(self.world):
+            _index_add(gW, all_ids_lab[r], all_rows_lab[r], alpha)
+            _index_add(gW, all_ids_smp[r], all_rows_smp[r], alpha)
+        return (all_ids_lab.view(-1), all_ids_smp.view(-1))
+
+
+def _index_add(dst: torch.Tensor, ids: torch.Tensor, rows: torch.Tensor, alpha: float) -> None:
+    if dst.is_cuda:
+        from . import kernels as K
+        K.index_add_rows(rows, ids, dst, alpha)
+    else:   # gloo tests on CPU: the same per-element sum dst += alpha * row
+        keep = ids >= 0
+        dst.index_add_(0, ids[keep], rows[keep] * alpha)

@@ -342,6 +342,33 @@ def sampled_softmax_bwd(X, ldx, labels, sample_ids, S, W, ldw, prob, dloss, dX, 
                                               int(D), _s()), "u2gnn_sampled_softmax_bwd")
 
 
+def sampled_softmax_bwd_rows(X, ldx, labels, sample_ids, S, W, ldw, prob, dloss, dX, lddx, dW_lab, dW_smp, n_rows, D):
+    """ABI v9: W's gradient as compact rows -- dW_lab [n_rows, >= D] (row of W labels[i]) and dW_smp
+    [S, >= D] (row of W sample_ids[j]) -- instead of a dense [V, D] image."""
+    _dev(X, labels, sample_ids, W, prob, dX, dW_smp, dW_lab)
+    check(hip_lib().u2gnn_sampled_softmax_bwd_rows(_p(X), int(ldx), _p(labels), _p(sample_ids), int(S), _p(W), int(ldw),
+                                                   _p(prob), _p(dloss), _p(dX), int(lddx), _p(dW_lab),
+                                                   int(dW_lab.stride(0)) if dW_lab is not None else int(D), _p(dW_smp),
+                                                   int(dW_smp.stride(0)), int(n_rows), int(D), _s()),
+          "u2gnn_sampled_softmax_bwd_rows")
+
+
+def index_add_rows(src, idx, dst, alpha=1.0, err=None):
+    """dst[idx[r]] += alpha * src[r] (idx distinct within one call; u2gnn_hip.h ABI v9)."""
+    _dev(src, idx, dst, err)
+    n, D = int(idx.numel()), int(dst.shape[1])
+    check(hip_lib().u2gnn_index_add_rows(_p(src), int(src.stride(0)), _p(idx), n, float(alpha), _p(dst),
+                                         int(dst.stride(0)), int(dst.shape[0]), D, _p(err), _s()),
+          "u2gnn_index_add_rows")
+
+
+def index_zero_rows(idx, dst, err=None):
+    """dst[idx[r]] = 0 (ABI v9)."""
+    _dev(idx, dst, err)
+    check(hip_lib().u2gnn_index_zero_rows(_p(idx), int(idx.numel()), _p(dst), int(dst.stride(0)), int(dst.shape[0]),
+                                          int(dst.shape[1]), _p(err), _s()), "u2gnn_index_zero_rows")
+
+
 def dropout(X, ldx, Y, ldy, rows, cols, p, seed):
     _dev(X, Y)
     check(hip_lib().u2gnn_dropout(_p(X), int(ldx), _p(Y), int(ldy), int(rows), int(cols), float(p), int(seed), _s()),

@@ -103,3 +103,23 @@ def reddit5k_like(seed: int = 0) -> SyntheticStore:
     """REDDITMULTI5K: 4999 graphs, 5 classes, mean 508.52 nodes in [22, 3648], 594.87 edges
     per graph, X = 0.01 * ones[n, 4]."""
     return SyntheticStore(4999, 508.52, 22, 3648, 594.87, 5, 4, seed=seed, dist="lognormal", feature="reddit")
+
+
+class _Graph:
+    """The attributes GraphStore reads from a util.S2VGraph."""
+
+    def __init__(self, n, label, X, src, dst):
+        self.n, self.label, self.node_features = n, label, X
+        self.edge_mat = np.stack([src, dst])
+
+
+def as_graph_store(s: "SyntheticStore"):
+    """The same synthetic graphs as a GraphStore (the real-dataset path: native batch assembly into
+    page-locked buffers, features gathered on the GPU) -- bench.py's on-the-fly pipeline line."""
+    from .batching import GraphStore
+    gs = []
+    for gid in range(len(s.graphs)):
+        start, nbr, deg, X = s.graph(gid)
+        src = np.repeat(np.arange(len(deg)), deg)
+        gs.append(_Graph(len(deg), int(s.labels[gid]), X, src, nbr))
+    return GraphStore(gs)

@@ -68,7 +68,12 @@ class UnSupTrainer:
         self.loss = torch.zeros(1, device=dev)
         self.ws = torch.empty(1024, device=dev)
         self.gen = torch.Generator().manual_seed(seed)
+        # data parallelism (dp.UnSupGradSync): grad_sync(flat) averages the encoder gradients,
+        # row_sync.rows(...) exchanges the touched rows of ss.weight's gradient
         self.grad_sync = None
+        self.row_sync = None
+        # ss.weight rows written by this step's gradient (zeroed again after the optimizer step)
+        self._touched = ()
 
     def next_seed(self) -> int:
         return int(torch.randint(0, 2 ** 62, (1,), generator=self.gen).item())
@@ -93,11 +98,23 @@ class UnSupTrainer:
         if self.ws.numel() < K.colstat_ws_floats(N, 1):   # ceil(N/16) partial sums (u2gnn_hip.h)
             self.ws = torch.empty(K.colstat_ws_floats(N, 1), device=OV.device)
         K.colsum(lrow.view(N, 1), N, 1, 1, (1, 1), self.loss, self.ws)
+        self.last_logits = lrow   # per-node losses of the step (the reference forward's output)
+        # W's gradient touches only the label rows and the S sampled rows (sampled_softmax.py:45,48):
+        # the backward writes them as compact rows, folded into the dense gradient (all zero between
+        # steps, so no dense zero fill of the [V, D] table) -- locally, or after the data-parallel
+        # row exchange
         gW = self.flat.grads["ss.weight"]
-        gW.zero_()
         dOV = torch.empty_like(OV)
-        K.sampled_softmax_bwd(OVd, D, b.input_y, sample_ids, S, W, W.stride(0), prob, None, dOV, D, gW, gW.stride(0),
-                              N, D)
+        rows_lab = torch.empty(N, D, device=OV.device)
+        rows_smp = torch.empty(S, D, device=OV.device)
+        K.sampled_softmax_bwd_rows(OVd, D, b.input_y, sample_ids, S, W, W.stride(0), prob, None, dOV, D, rows_lab,
+                                   rows_smp, N, D)
+        if self.row_sync is not None:
+            self._touched = self.row_sync.rows(b.input_y, rows_lab, sample_ids, rows_smp, gW)
+        else:   # labels first, then samples: distinct destinations per call, fixed order
+            K.index_add_rows(rows_lab, b.input_y, gW)
+            K.index_add_rows(rows_smp, sample_ids, gW)
+            self._touched = (b.input_y, sample_ids)
         if p > 0:
             K.dropout(dOV, D, dOV, D, N, D, p, ds)
         core.encode_backward(sctx, dOV, self.flat.grads)
@@ -108,7 +125,16 @@ class UnSupTrainer:
         if self.grad_sync is not None:
             self.grad_sync(self.flat)
         self.opt.step()
+        self.clear_row_grads()
         return loss
+
+    def clear_row_grads(self):
+        """Zero the ss.weight gradient rows this step wrote (the dense gradient is all zero between
+        steps; torch's Adam sees the same dense gradient either way)."""
+        gW = self.flat.grads["ss.weight"]
+        for ids in self._touched:
+            K.index_zero_rows(ids, gW)
+        self._touched = ()
 
 
 def graph_embeddings(weight: torch.Tensor, node_start: np.ndarray) -> torch.Tensor:

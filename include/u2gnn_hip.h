@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define U2GNN_ABI_VERSION 8
+#define U2GNN_ABI_VERSION 9
 
 #define U2GNN_OK 0
 #define U2GNN_E_ARG (-1)    /* bad size / null pointer */
@@ -291,6 +291,27 @@ int u2gnn_sampled_softmax_bwd(const float *X, int64_t ldx, const int64_t *labels
                               const int64_t *sample_ids, int64_t S, const float *W, int64_t ldw,
                               const float *prob, const float *dloss, float *dX, int64_t lddx,
                               float *dW, int64_t lddw, int64_t n_rows, int64_t D, void *stream);
+/* ABI v9: the same backward with W's gradient as compact rows instead of a dense [V, D] image:
+ * dW_lab[i] = -dloss_i x_i  (row of W labels[i]),  dW_smp[j] = sum_i dloss_i prob_ij x_i  (row of W
+ * sample_ids[j]).  Plain stores, no atomics, no zero fill: the rows are what the data-parallel
+ * exchange all-gathers (train_pytorch_U2GNN_UnSup.py:149-162, sampled_softmax.py:45,48 touch only
+ * these rows), and u2gnn_index_add_rows folds them into the dense gradient. */
+int u2gnn_sampled_softmax_bwd_rows(const float *X, int64_t ldx, const int64_t *labels,
+                                   const int64_t *sample_ids, int64_t S, const float *W, int64_t ldw,
+                                   const float *prob, const float *dloss, float *dX, int64_t lddx,
+                                   float *dW_lab, int64_t ld_lab, float *dW_smp, int64_t ld_smp, int64_t n_rows,
+                                   int64_t D, void *stream);
+
+/* ---- ABI v9: row-indexed updates of a dense [V, D] buffer ------------------------------------
+ * dst[idx[r], c] += alpha * src[r, c] (r < n_rows, c < D).  The idx entries of ONE call must be
+ * distinct (plain read-modify-write, no atomics): callers order overlapping sets over separate calls,
+ * which makes the sum order, and so the bits, fixed.  idx outside [0, dst_rows) is skipped and sets
+ * *err (when err is non-NULL). */
+int u2gnn_index_add_rows(const float *src, int64_t ld_src, const int64_t *idx, int64_t n_rows, float alpha,
+                         float *dst, int64_t ld_dst, int64_t dst_rows, int64_t D, int32_t *err, void *stream);
+/* dst[idx[r], c] = 0 for r < n_rows, c < D (duplicates allowed); out-of-range idx skipped + *err. */
+int u2gnn_index_zero_rows(const int64_t *idx, int64_t n_rows, float *dst, int64_t ld_dst, int64_t dst_rows,
+                          int64_t D, int32_t *err, void *stream);
 
 /* ---- a12: dropout on the concatenated UnSup node embeddings (model_U2GNN_Unsup_multi.py:56) --
  * Y[i, j] = X[i, j] * keep(seed, i, j) / (1-p) for i < rows, j < cols.  The backward is the same

@@ -105,3 +105,99 @@ def test_gloo_world2_batches_and_grad_average(tmp_path):
         got.append(r[0]["g"][off:off + p.numel()])
         off += (p.numel() + 3) // 4 * 4
     assert np.allclose(np.concatenate(got), mean, rtol=1e-5, atol=1e-6)
+
+
+def _unsup_grads(rank_batch, sids, sd, W):
+    """Oracle (train_pytorch_U2GNN_UnSup.py:149-157, eval mode): dense gradients of the summed
+    sampled-softmax loss of one batch w.r.t. the encoder parameters and ss.weight."""
+    from oracle import u2gnn_oracle as O
+    enc = {k: v.detach().clone().requires_grad_(True) for k, v in sd.items()}
+    w = W.detach().clone().requires_grad_(True)
+    b = rank_batch
+    loss = O.unsup_forward(enc, w, torch.from_numpy(b.input_x), torch.from_numpy(b.X_concat),
+                           torch.from_numpy(b.input_y), torch.from_numpy(sids), 1, 1, train=False, slots=1).sum()
+    loss.backward()
+    return {k: v.grad for k, v in enc.items()}, w.grad
+
+
+def _unsup_setup(world, rank, steps=2):
+    import util
+    from log_uniform import LogUniformSampler
+    from pytorch_U2GNN_UnSup import TransformerU2GNN
+    from u2gnn_hip.batching import BatchLoader, GraphStore
+    from u2gnn_hip.dp import rank_batches
+    graphs, _ = util.load_data("PTC", False)
+    store = GraphStore(graphs)
+    V = int(store.node_start[-1])
+    np.random.seed(123)
+    mine = rank_batches(BatchLoader(store, 4, 4, with_input_y=True), world, rank, steps)
+    sampler = LogUniformSampler(V)
+    draws = [sampler.sample_set_order(64)[0] for _ in range(world * steps)]   # one draw per batch, in order
+    my_sids = [np.asarray(draws[s * world + rank], dtype=np.int64) for s in range(steps)]
+    torch.manual_seed(123)
+    m = TransformerU2GNN(vocab_size=V, feature_dim_size=store.X.shape[1], ff_hidden_size=32, sampled_num=64,
+                         num_self_att_layers=1, num_U2GNN_layers=1, dropout=0.5, device="cpu")
+    return store, m, mine, my_sids
+
+
+def _unsup_worker(rank, world, port, out_dir):
+    sys.path[:0] = [os.path.join(REPO, "graph-transformer_amd"), REPO]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from u2gnn_hip.core import FlatParams
+    from u2gnn_hip.dp import UnSupGradSync, max_batch_nodes
+    store, m, mine, my_sids = _unsup_setup(world, rank)
+    flat = FlatParams(m, names=m.trainable_names())
+    sd = {k: v.detach() for k, v in m.state_dict().items() if k.startswith("u2gnn_layers.")}
+    b, sids = mine[1], my_sids[1]                       # second global step
+    g_enc, g_w = _unsup_grads(b, sids, sd, m.ss.weight.detach().clone())
+    for k, v in g_enc.items():
+        flat.grads[k].copy_(v)
+    # compact rows: label rows, then the sample rows not already counted among the labels
+    lab = torch.from_numpy(b.input_y)
+    smp = torch.from_numpy(sids)
+    rows_lab = g_w.index_select(0, lab)
+    rows_smp = g_w.index_select(0, smp) * (~torch.isin(smp, lab)).float()[:, None]
+    sync = UnSupGradSync(flat, max_batch_nodes(store.node_start, 4))
+    gW = flat.grads["ss.weight"]
+    assert float(gW.abs().sum()) == 0.0            # zero between steps
+    touched = sync.rows(lab, rows_lab, smp, rows_smp, gW)
+    sync(flat)
+    np.savez(os.path.join(out_dir, f"u{rank}.npz"), g=flat.gflat.numpy().copy())
+    for ids in touched:                               # what UnSupTrainer.clear_row_grads does
+        keep = ids >= 0
+        gW[ids[keep]] = 0.0
+    assert float(gW.abs().sum()) == 0.0
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_unsup_sparse_row_exchange(tmp_path):
+    """Row e2: 2 ranks, each one UnSup batch + its own sample draw; after the encoder
+    all-reduce and the ss.weight row all-gather, both ranks hold the same gradient, equal to the mean
+    of the dense oracle gradients of the same 2 consecutive batches of the single stream."""
+    world = 2
+    mp.spawn(_unsup_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    r = [dict(np.load(os.path.join(tmp_path, f"u{i}.npz"))) for i in range(world)]
+    assert np.array_equal(r[0]["g"], r[1]["g"])
+    sys.path[:0] = [os.path.join(REPO, "graph-transformer_amd"), REPO]
+    from u2gnn_hip.batching import BatchLoader  # noqa: F401  (path check)
+    enc_sum, w_sum = None, None
+    for rank in range(world):
+        store, m, mine, my_sids = _unsup_setup(world, rank)
+        sd = {k: v.detach() for k, v in m.state_dict().items() if k.startswith("u2gnn_layers.")}
+        g_enc, g_w = _unsup_grads(mine[1], my_sids[1], sd, m.ss.weight.detach())
+        enc_sum = g_enc if enc_sum is None else {k: enc_sum[k] + g_enc[k] for k in g_enc}
+        w_sum = g_w if w_sum is None else w_sum + g_w
+    names = m.trainable_names()
+    off, got, ref = 0, [], []
+    params = dict(m.named_parameters())
+    for n in names:
+        k = params[n].numel()
+        got.append(r[0]["g"][off:off + k])
+        ref.append(((w_sum if n == "ss.weight" else enc_sum[n]) / world).reshape(-1).numpy())
+        off += (k + 3) // 4 * 4
+    got, ref = np.concatenate(got), np.concatenate(ref)
+    assert np.abs(ref).max() > 0
+    assert np.allclose(got, ref, rtol=1e-5, atol=1e-6)

@@ -42,8 +42,11 @@ def per_kernel(db, counter):
 def main():
     fetch = per_kernel(sys.argv[1], "FETCH_SIZE")
     write = per_kernel(sys.argv[2], "WRITE_SIZE")
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "graph-transformer_amd"))
+    from u2gnn_hip._lib import source_build_id
     out = {"method": "(2*FETCH_SIZE + WRITE_SIZE) KB * 1024 per launch; separate --pmc passes; "
-                     "bench.py --steps 3 --warmup 1 (C4 COLLAB-like, bf16x3)", "kernels": {}}
+                     "bench.py --steps 3 --warmup 1 (C4 COLLAB-like, bf16x3)",
+           "build_id": source_build_id(), "kernels": {}}
     for k in sorted(set(fetch) | set(write)):
         nf, f = fetch.get(k, [0, 0.0])
         nw, w = write.get(k, [0, 0.0])

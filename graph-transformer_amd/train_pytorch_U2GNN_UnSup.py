@@ -29,7 +29,7 @@ np.random.seed(123)
 from pytorch_U2GNN_UnSup import TransformerU2GNN  # noqa: E402
 from u2gnn_hip.batching import BatchLoader, GraphStore  # noqa: E402
 from u2gnn_hip.core import DeviceBatch  # noqa: E402
-from u2gnn_hip.unsup import UnSupTrainer, graph_embeddings  # noqa: E402
+from u2gnn_hip.unsup import UnSupTrainer, fold_accuracies, graph_embeddings  # noqa: E402
 from util import load_data, separate_data_idx  # noqa: E402
 
 if not torch.cuda.is_available():
@@ -104,18 +104,15 @@ def train():
     return total_loss
 
 
+FOLDS = [separate_data_idx(graphs, fold_idx) for fold_idx in range(10)]
+
+
 def evaluate():
-    from sklearn.linear_model import LogisticRegression
     model.eval()
     with torch.no_grad():
         emb = graph_embeddings(model.ss.weight.detach(), store.node_start).cpu().numpy()
-    acc_10folds = []
-    for fold_idx in range(10):
-        train_idx, test_idx = separate_data_idx(graphs, fold_idx)
-        cls = LogisticRegression(solver="liblinear", tol=0.001)
-        cls.fit(emb[train_idx], graph_labels[train_idx])
-        ACC = cls.score(emb[test_idx], graph_labels[test_idx])
-        acc_10folds.append(ACC)
+    acc_10folds = fold_accuracies(emb, graph_labels, FOLDS)
+    for fold_idx, ACC in enumerate(acc_10folds):
         print('epoch ', epoch, ' fold ', fold_idx, ' acc ', ACC)
     return statistics.mean(acc_10folds), statistics.stdev(acc_10folds)
 

@@ -149,3 +149,16 @@ def graph_embeddings(weight: torch.Tensor, node_start: np.ndarray) -> torch.Tens
     vals = torch.ones(V, device=dev)
     K.pool_fwd(weight, D, rowptr, col, vals, out, D, G, D, 0.0, 0)
     return out
+
+
+def fold_accuracies(emb: np.ndarray, labels: np.ndarray, splits) -> list:
+    """The classifier half of evaluate() (train_pytorch_U2GNN_UnSup.py:171-181): per (train, test) split
+    a LogisticRegression(solver="liblinear", tol=0.001) on the graph embeddings; returns the test
+    accuracies.  Host code (sklearn), after graph_embeddings on the device."""
+    from sklearn.linear_model import LogisticRegression
+    accs = []
+    for train_idx, test_idx in splits:
+        cls = LogisticRegression(solver="liblinear", tol=0.001)
+        cls.fit(emb[train_idx], labels[train_idx])
+        accs.append(float(cls.score(emb[test_idx], labels[test_idx])))
+    return accs

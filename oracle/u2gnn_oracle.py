@@ -19,6 +19,8 @@ What is restated (file:line relative to /root/reference):
 * clip_grad_norm_(0.5) + Adam           train_pytorch_U2GNN_Sup.py:145,160-161 (torch semantics)
 * sampled softmax                       U2GNN_pytorch/sampled_softmax.py:36-56
 * UnSup composite (a12 of SURVEY §8)    pytorch_U2GNN_UnSup.py:52-69 + U2GNN_tf/model_U2GNN_Unsup_multi.py:43-58
+* UnSup evaluation (§8(f) row 3)        train_pytorch_U2GNN_UnSup.py:82-94 (graph_pool over all graphs),
+                                        :164-188 (spmm + 10-fold LogisticRegression(liblinear, tol=1e-3))
 
 The model restatement computes ALL k+1 neighbour slots with dropout p=0.5 when
 ``train=True`` so that its cost is the reference's cost (used as the CPU
@@ -340,3 +342,30 @@ def unsup_forward(sd: Dict[str, torch.Tensor], weight: torch.Tensor, input_x: to
     hm = None if masks is None else masks.get("ss")
     ov = _drop(ov, dropout, train, hm)
     return sampled_softmax_logits(ov, input_y, weight, sample_ids)
+
+
+# ----------------------------------------------------------------------------
+# UnSup evaluation  (train_pytorch_U2GNN_UnSup.py:82-94, 164-188)
+# ----------------------------------------------------------------------------
+
+def unsup_evaluate(weight: torch.Tensor, n_nodes: Sequence[int], labels: Sequence[int], seed: int = 0):
+    """evaluate(): graph_pool = sparse [G, V] of ones over every graph's nodes (get_graphpool over ALL
+    graphs, nodes contiguous in dataset order); graph embeddings = torch.spmm(graph_pool, ss.weight);
+    per fold of separate_data_idx (StratifiedKFold(10, shuffle, seed 0)) a
+    LogisticRegression(solver="liblinear", tol=0.001) fit on the train graphs, scored on the test
+    graphs.  Returns the 10 accuracies (mean / stdev are statistics.mean / statistics.stdev of them)."""
+    from sklearn.linear_model import LogisticRegression
+    n_nodes = np.asarray(n_nodes, dtype=np.int64)
+    start = np.concatenate([[0], np.cumsum(n_nodes)])
+    rows = np.repeat(np.arange(len(n_nodes)), n_nodes)
+    idx = torch.from_numpy(np.stack([rows, np.arange(int(start[-1]))]))
+    graph_pool = torch.sparse_coo_tensor(idx, torch.ones(int(start[-1])), (len(n_nodes), int(start[-1])))
+    emb = torch.spmm(graph_pool, weight.float()).numpy()
+    labels = np.asarray(labels)
+    accs = []
+    for fold in range(10):
+        tr, te = separate_data_idx(labels, fold)
+        cls = LogisticRegression(solver="liblinear", tol=0.001)
+        cls.fit(emb[tr], labels[tr])
+        accs.append(float(cls.score(emb[te], labels[te])))
+    return accs

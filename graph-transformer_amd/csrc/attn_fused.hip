@@ -1,0 +1,497 @@
+// Attention forward over the node axis after S = Q K^T (a3.2 of SURVEY.md §8: softmax(Q K^T) -> dropout ->
+// . V inside torch's MultiheadAttention, pytorch_U2GNN_Sup.py:19-21,35 / pytorch_U2GNN_UnSup.py:37-40,57).
+//
+// The scores come from the QK^T GEMM, whose epilogue also leaves per-row softmax partials
+// (EPI_STORE_ROWSTAT, per 64-column group); one fused kernel folds those into (max, 1/sum) per row and
+// then does what the softmax pass and the P.V GEMM did: it reads each score once, forms
+// P = exp(s - max)/sum and the dropout decision in registers, writes the signed image the backward
+// reads (the only N x N write left in the forward) and multiplies the kept probabilities into V on the
+// matrix cores (split bf16, 3 products per term) without staging P anywhere.
+//
+// One workgroup = 4 waves = 128 query rows (32 per wave, one wave per SIMD) x one range of keys (the key
+// axis is split over workgroups so ~256 of them fill the chip; a combine pass adds the ranges).  Per
+// block of 32 keys:
+//   * the 128 x 32 score tile and the 32-key V tile (pre-split x2 rows of the in-projection output)
+//     arrive by LDS-DMA, one block ahead;
+//   * lane l of a wave takes query l%32 and the 8 consecutive keys 8h .. 8h+7 (h = l/32) of each
+//     16-key step -- exactly the B operand of v_mfma_f32_32x32x16_bf16 -- so P never leaves registers;
+//   * O^T += V^T . P, V^T fragments read with ds_read_b64_tr_b16 from the k-major V image (BF16X3: the
+//     three split products hi.lo + lo.hi + hi.hi; BF16: hi.hi only).
+#include "u2gnn_common.h"
+
+#include <type_traits>
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+typedef __attribute__((address_space(3))) void lds_void;
+
+constexpr int FA_BM = 128;   // query rows per workgroup (4 waves x 32)
+constexpr int FA_BN = 32;    // keys per block
+constexpr int FA_NT = 256;
+constexpr int S_IMG = FA_BM * FA_BN * 4;   // bytes of one score tile
+
+// V image (x2 rows of 4*dp bytes, k-major for the transpose reads): byte b of k-row r stored at
+// b ^ kr_swz(r) -- the four k-rows of one ds_read_b64_tr_b16 land in four different 64-B bank quarters.
+__device__ __forceinline__ int kr_swz(int krow) { return ((krow & 1) << 4) | ((krow & 2) << 6); }
+// score image: 128-B rows (32 keys); 16-B chunk c of row r stored at c ^ ((r >> 1) & 7), so the 16 rows a
+// 16-lane group of a ds_read_b128 touches hit 16 distinct bank slots.
+__device__ __forceinline__ int s_swz(int r) { return (r >> 1) & 7; }
+
+// One 16-B LDS-DMA per lane: global base (wave-uniform, SGPRs) + 32-bit lane offset -> LDS (wave-uniform
+// piece base in M0, lane-linear inside it).
+// Written as an asm statement on purpose: the compiler does not count it, so it neither inserts a
+// vmcnt(0) in front of the fragment reads of the OTHER stage (it cannot tell the two stages apart
+// through a DMA) nor orders anything after it; every wait on these is the counted wait_vm below.
+// M0 is reserved (never allocated) and nothing else in these kernels reads it, so it is not clobbered.
+__device__ __forceinline__ void dma16(const char *base, int off, unsigned m0) {
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2" ::"s"(m0), "v"(off), "s"(base)
+                 : "memory");
+}
+
+// LDS byte address of a shared object (a link-time constant)
+__device__ __forceinline__ unsigned lds_addr(const void *p) { return (unsigned)(size_t)(const lds_void *)p; }
+
+template <int DP>
+__device__ __forceinline__ void issue_v(const char *vbase, int64_t ld_bytes, unsigned img, int tid, int w) {
+    constexpr int RB = 4 * DP;                       // bytes per k-row
+    constexpr int NI = FA_BN * RB / (16 * FA_NT);   // DMA instructions per thread (DP / 32)
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+        const int b = (i * FA_NT + tid) * 16;
+        const int kr = b / RB, pb = b % RB;
+        dma16(vbase, (int)(kr * ld_bytes) + (pb ^ kr_swz(kr)), img + (i * FA_NT + 64 * w) * 16);
+    }
+}
+
+// the 128 x 32 score tile: 4 DMA instructions per thread
+__device__ __forceinline__ void issue_s(const char *sbase, int64_t lds_bytes, unsigned img, int tid, int w) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int c = i * FA_NT + tid;       // 16-B chunk of the image
+        const int r = c >> 3, q = (c & 7) ^ s_swz(r);
+        dma16(sbase, (int)(r * lds_bytes) + q * 16, img + (i * FA_NT + 64 * w) * 16);
+    }
+}
+
+template <int N_>
+__device__ __forceinline__ void wait_vm() {
+    static_assert(N_ >= 0 && N_ <= 63, "vmcnt range");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N_) : "memory");
+}
+
+// V^T fragment reads (A operand: row = d, k = key).  Lane (g = l/16, q = (l/4)%4, p = l%4) reads k-row
+// kr = 16 ks + 8 (g>>1) + q, columns 32 t + 16 (g&1) + 4p .. +3 of the hi and lo halves.  kr_swz(kr)
+// depends on q only (bits 4 and 7); bit 7 is also bit 0 of the tile index t, so
+//   (128 t + x) ^ kr_swz = (x ^ (16 (q&1))) + 128 (t ^ (q>>1))
+// and each lane keeps one base per parity of t -- every other term is a compile-time offset.
+struct VBase {
+    int a[2], b[2];   // hi / lo half byte offsets for even / odd t
+};
+
+template <int DP>
+__device__ __forceinline__ VBase v_base(int lane) {
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    const int row = ((g >> 1) * 8 + q) * (4 * DP);
+    const int x = (g & 1) * 64 + (p >> 1) * 32 + (p & 1) * 8;   // < 128, bit 4 clear
+    const int sq = (q >> 1) & 1;
+    VBase B;
+    B.a[0] = row + x + 16 * (q & 1) + 128 * sq;
+    B.b[0] = row + x + 16 * (1 - (q & 1)) + 128 * sq;
+    B.a[1] = B.a[0] - 256 * sq;
+    B.b[1] = B.b[0] - 256 * sq;
+    return B;
+}
+
+template <int DP>
+__device__ __forceinline__ void v_frag(const char *img, const VBase &B, int dt, int ks, bf16x8 &hi, bf16x8 &lo) {
+    const char *a = img + B.a[dt & 1] + 128 * dt + ks * 64 * DP;
+    const char *b = img + B.b[dt & 1] + 128 * dt + ks * 64 * DP;
+    const s16x4 h0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(a));
+    const s16x4 h1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(a + 16 * DP));
+    const s16x4 l0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(b));
+    const s16x4 l1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(b + 16 * DP));
+    const s16x4 vh[2] = {h0, h1}, vl[2] = {l0, l1};
+    hi = __builtin_bit_cast(bf16x8, vh);
+    lo = __builtin_bit_cast(bf16x8, vl);
+}
+
+__device__ __forceinline__ void split8(const float *x, bf16x8 &hi, bf16x8 &lo) {
+    unsigned h[4], l[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) split2<true>(x[2 * i], x[2 * i + 1], h[i], l[i]);
+    hi = __builtin_bit_cast(bf16x8, h);
+    lo = __builtin_bit_cast(bf16x8, l);
+}
+
+struct SpvP {
+    const float *S;        // scores [rows_pad][lds]
+    int64_t lds;
+    const float *rowpart;  // EPI_STORE_ROWSTAT partials: [rows_pad][ld_rowpart] (max, sum) pairs
+    int64_t ld_rowpart;
+    int32_t ngroups;
+    const __bf16 *qkv2;    // x2 [rows_pad][ldq2]
+    int64_t ldq2;
+    float *Pd;             // signed image [rows_pad][ldp]
+    int64_t ldp;
+    float *Opart;          // [nsplit][rows_pad][dp]
+    int32_t n_valid, rows_pad, kb_valid, kb_per_split, nsplit, qblocks;
+    float p;
+    uint64_t seed;
+    const uint64_t *epoch;
+};
+
+__device__ __forceinline__ void lse_merge(float &m, float &l, float m2, float l2) {
+    if (m2 == -INFINITY) return;
+    if (m == -INFINITY) {
+        m = m2, l = l2;
+        return;
+    }
+    const float n = fmaxf(m, m2);
+    l = l * __expf(m - n) + l2 * __expf(m2 - n);
+    m = n;
+}
+
+// (max, 1/sum) of one row from its ngroups (max, sum exp) partials: the row's two lanes (h = 0, 1) take
+// alternate pairs of groups and merge at the end -- the same order in every workgroup of the row block
+__device__ __forceinline__ void row_stat(const SpvP &P, int query, int h, float &M, float &inv) {
+    const float4 *pr = reinterpret_cast<const float4 *>(P.rowpart + 2 * (int64_t)query * P.ld_rowpart);
+    float m = -INFINITY, l = 0.f;
+    for (int j = h; j < P.ngroups / 2; j += 2) {
+        const float4 v = pr[j];
+        lse_merge(m, l, v.x, v.y);
+        lse_merge(m, l, v.z, v.w);
+    }
+    const float m2 = __shfl_xor(m, 32, 64), l2 = __shfl_xor(l, 32, 64);
+    if (h == 0) {
+        lse_merge(m, l, m2, l2);
+    } else {   // the same merge, operands in lane-0 order, so both lanes agree bit for bit
+        float mm = m2, ll = l2;
+        lse_merge(mm, ll, m, l);
+        m = mm, l = ll;
+    }
+    M = m, inv = 1.f / l;
+}
+
+// this lane's P for keys kb*32 + 16 ks + 8 h .. +7 (ks = 0, 1: the B operands of the block's two 16-key
+// steps), from the score tile simg; writes the signed image and returns the kept P/(1-p) split to bf16
+struct PRow {
+    int r, h, klim;
+    float mb, inv, sc, p;
+    uint32_t rkey;
+    float *prow;
+};
+
+__device__ __forceinline__ void p_block(const PRow &R, const char *simg, int kb, bf16x8 (&ph)[2], bf16x8 (&pl)[2]) {
+    const int key0 = kb * FA_BN;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+        const int c = 4 * ks + 2 * R.h;   // logical 16-B chunk of the row
+        const char *rowp = simg + R.r * 128;
+        const float4 a = *reinterpret_cast<const float4 *>(rowp + ((c ^ s_swz(R.r)) << 4));
+        const float4 b = *reinterpret_cast<const float4 *>(rowp + (((c + 1) ^ s_swz(R.r)) << 4));
+        float sv[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+        // pin the two vector reads: without this the compiler turns the key mask below into branches
+        // and sinks single-element LDS reads into them
+#pragma unroll
+        for (int t = 0; t < 8; ++t) asm("" : "+v"(sv[t]));
+        float pv[8], img[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            // branch-free: masked keys/rows go through exp2(-inf) = 0; at p = 0 every u >= p keeps
+            const int key = key0 + 16 * ks + 8 * R.h + t;
+            const float x = key < R.klim ? sv[t] * 1.4426950408889634f - R.mb : -INFINITY;
+            const float pr = __builtin_amdgcn_exp2f(x) * R.inv;
+            const float u = (float)(u2gnn_fmix32(R.rkey + (uint32_t)key * 0x9E3779B9u) >> 8) * (1.0f / 16777216.0f);
+            const bool kp = u >= R.p;
+            const float ps = pr * R.sc;
+            pv[t] = kp ? ps : 0.f;
+            img[t] = kp ? ps : -pr;
+        }
+        float *dst = R.prow + key0 + 16 * ks + 8 * R.h;
+#ifndef SPV_NO_STORE
+        *reinterpret_cast<float4 *>(dst) = make_float4(img[0], img[1], img[2], img[3]);
+        *reinterpret_cast<float4 *>(dst + 4) = make_float4(img[4], img[5], img[6], img[7]);
+#else
+        if (img[0] == 123.f) *dst = img[1] + img[2] + img[3] + img[4] + img[5] + img[6] + img[7];
+#endif
+        split8(pv, ph[ks], pl[ks]);
+    }
+}
+
+// O^T += V^T . P over one block (V image vimg, P operands ph / pl); fragments of d tile t + 1 are read
+// while the products of tile t run
+template <int DP, bool X3>
+__device__ __forceinline__ void pv_block(const char *vimg, const VBase &vb, const bf16x8 (&ph)[2],
+                                         const bf16x8 (&pl)[2], f32x16 (&o)[DP / 32]) {
+    constexpr int DT = DP / 32;
+    bf16x8 vh[2][2], vl[2][2];
+    v_frag<DP>(vimg, vb, 0, 0, vh[0][0], vl[0][0]);
+    v_frag<DP>(vimg, vb, 0, 1, vh[0][1], vl[0][1]);
+#pragma unroll
+    for (int t = 0; t < DT; ++t) {
+        const int cur = t & 1;
+        if (t + 1 < DT) {
+            v_frag<DP>(vimg, vb, t + 1, 0, vh[cur ^ 1][0], vl[cur ^ 1][0]);
+            v_frag<DP>(vimg, vb, t + 1, 1, vh[cur ^ 1][1], vl[cur ^ 1][1]);
+        }
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            if constexpr (X3) {
+                o[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vh[cur][ks], pl[ks], o[t], 0, 0, 0);
+                o[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vl[cur][ks], ph[ks], o[t], 0, 0, 0);
+            }
+            o[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vh[cur][ks], ph[ks], o[t], 0, 0, 0);
+        }
+    }
+}
+
+// Interleave hint for the scheduler: per matrix product, a few LDS reads and the VALU share of the next
+// block's probabilities (~450 VALU per block: 6 per product in BF16X3, 18 in BF16), so the in-order wave
+// issues them while the matrix pipe is busy (one wave per SIMD: nothing else would cover them).
+template <int NMFMA, int NVALU>
+__device__ __forceinline__ void interleave_hint() {
+#pragma unroll
+    for (int i = 0; i < NMFMA; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);       // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);       // DS read
+        __builtin_amdgcn_sched_group_barrier(0x002, NVALU, 0);   // VALU
+    }
+}
+
+// Workgroup id -> (query block, key range): consecutive ids go to different XCDs (b and b + 8 share one),
+// so deal the split-major list out in contiguous chunks per XCD -- the workgroups of one key range then
+// share one L2 for their V tiles.
+__device__ __forceinline__ void spv_block(int id, int total, int qblocks, int &qb, int &split) {
+    const int x = id & 7, slot = id >> 3;
+    const int base = total >> 3, extra = total & 7;
+    const int pos = x * base + min(x, extra) + slot;
+    split = pos / qblocks;
+    qb = pos - split * qblocks;
+}
+
+template <int DP, bool X3>
+__global__ void __launch_bounds__(FA_NT, 1) attn_softmax_pv_kernel(SpvP P) {
+    constexpr int DT = DP / 32;              // 32-wide d tiles of O
+    constexpr int VIMG = FA_BN * 4 * DP;     // bytes of one V image
+    __shared__ __attribute__((aligned(1024))) char vst0[VIMG];
+    __shared__ __attribute__((aligned(1024))) char vst1[VIMG];
+    __shared__ __attribute__((aligned(1024))) char sst0[S_IMG];
+    __shared__ __attribute__((aligned(1024))) char sst1[S_IMG];
+    const uint64_t seed = u2gnn_seed(P.seed, P.epoch);
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    int qb, split;
+    spv_block(blockIdx.x, P.qblocks * P.nsplit, P.qblocks, qb, split);
+    const int qrow0 = qb * FA_BM;
+    PRow R;
+    R.r = 32 * w + (lane & 31);              // this lane's row inside the block
+    R.h = lane >> 5;
+    const int query = qrow0 + R.r;
+    const int kb0 = split * P.kb_per_split;
+    const int kb1 = min(kb0 + P.kb_per_split, P.kb_valid);
+    const int64_t ld_bytes = P.ldq2 * 2, lds_bytes = P.lds * 4;
+    const char *vcol = reinterpret_cast<const char *>(P.qkv2) + 8 * DP;   // x2 byte offset of V
+    const char *srow0 = reinterpret_cast<const char *>(P.S + (int64_t)qrow0 * P.lds);
+    const bool qvalid = query < P.n_valid;
+    float M = 0.f, inv = 0.f;
+    if (qb * FA_BM < P.n_valid) row_stat(P, query, R.h, M, inv);
+    // retire those loads before any LDS-DMA is in flight (every later wait below is a counted one)
+    wait_vm<0>();
+    R.klim = qvalid ? P.n_valid : 0;         // keys < klim carry probability
+    R.mb = qvalid ? M * 1.4426950408889634f : 0.f;
+    R.inv = qvalid ? inv : 0.f;
+    R.p = P.p;
+    R.sc = P.p > 0.f ? 1.f / (1.f - P.p) : 1.f;
+    R.rkey = u2gnn_row_key(seed, (uint32_t)query);
+    R.prow = P.Pd + (int64_t)query * P.ldp;
+    const VBase vb = v_base<DP>(lane);
+
+    f32x16 o[DT];
+#pragma unroll
+    for (int t = 0; t < DT; ++t)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) o[t][i] = 0.f;
+
+    // Software pipeline over the key blocks: iteration kb multiplies block kb's P (computed one iteration
+    // earlier) into V(kb) while it forms block kb+1's P from the score tile S(kb+1); LDS holds V(kb) and
+    // S(kb+1) for the current iteration and receives V(kb+1) and S(kb+2) by DMA.  The stages are separate
+    // LDS objects and the loop is unrolled by two, so every access names its stage at compile time.
+    auto issue_vt = [&](int kb, unsigned img) {
+        issue_v<DP>(vcol + (int64_t)kb * FA_BN * ld_bytes, ld_bytes, img, tid, w);
+    };
+    auto issue_st = [&](int kb, unsigned img) {
+        issue_s(srow0 + (int64_t)kb * FA_BN * 4, lds_bytes, img, tid, w);
+    };
+    bf16x8 ph[2], pl[2];
+    // an iteration that also forms the next block's P (kb + 1 < kb1)
+    auto body = [&](auto stage, int kb) {
+        constexpr int STG = decltype(stage)::value;
+        // V(kb), S(kb+1) landed (this wave's pieces: only the 4 image stores issued after those DMAs
+        // may still be in flight), then everyone's; every wave is also done with V(kb-1) and S(kb), whose
+        // stages the next DMAs overwrite
+        wait_vm<4>();
+        __builtin_amdgcn_s_barrier();
+#ifndef SPV_NO_DMA
+        issue_vt(kb + 1, lds_addr(STG ? vst0 : vst1));
+        if (kb + 2 < kb1) issue_st(kb + 2, lds_addr(STG ? sst1 : sst0));
+#endif
+        bf16x8 nh[2], nl[2];
+#ifndef SPV_NO_P
+        p_block(R, STG ? sst0 : sst1, kb + 1, nh, nl);
+#else
+        nh[0] = ph[1], nh[1] = ph[0], nl[0] = pl[1], nl[1] = pl[0];
+#endif
+#ifndef SPV_NO_MFMA
+        pv_block<DP, X3>(STG ? vst1 : vst0, vb, ph, pl, o);
+#endif
+#ifndef SPV_NO_HINT
+        interleave_hint<(X3 ? 6 : 2) * DT, X3 ? 6 : 18>();
+#endif
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) ph[ks] = nh[ks], pl[ks] = nl[ks];
+    };
+    auto last = [&](auto stage) {
+        constexpr int STG = decltype(stage)::value;
+        wait_vm<4>();
+        __builtin_amdgcn_s_barrier();
+        pv_block<DP, X3>(STG ? vst1 : vst0, vb, ph, pl, o);
+    };
+    if (kb0 < kb1) {
+        issue_vt(kb0, lds_addr(vst0));
+        issue_st(kb0, lds_addr(sst0));
+        if (kb0 + 1 < kb1) issue_st(kb0 + 1, lds_addr(sst1));
+        wait_vm<0>();
+        __builtin_amdgcn_s_barrier();
+        p_block(R, sst0, kb0, ph, pl);
+        int kb = kb0;
+        for (; kb + 2 < kb1; kb += 2) {
+            body(std::integral_constant<int, 0>(), kb);
+            body(std::integral_constant<int, 1>(), kb + 1);
+        }
+        if (kb + 1 < kb1) {
+            body(std::integral_constant<int, 0>(), kb);
+            last(std::integral_constant<int, 1>());
+        } else {
+            last(std::integral_constant<int, 0>());
+        }
+    }
+    // ---- partial O of this key range: O^T lane layout = query l%32, d = 32 t + 8 g + 4 h .. +3
+    float *orow = P.Opart + ((int64_t)split * P.rows_pad + query) * DP;
+#pragma unroll
+    for (int t = 0; t < DT; ++t)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+            *reinterpret_cast<float4 *>(orow + 32 * t + 8 * g + 4 * R.h) =
+                make_float4(o[t][4 * g], o[t][4 * g + 1], o[t][4 * g + 2], o[t][4 * g + 3]);
+}
+
+// O[row] = sum over the key ranges (fixed order); rows >= n_valid zero; and the parts of the signed
+// image no fused block wrote: keys from kb_valid*32 on, rows of query blocks past n_valid.
+// One wave per row, float4 columns.
+__global__ void __launch_bounds__(256) attn_pv_combine_kernel(const float *Opart, int nsplit, int rows_pad,
+                                                              int n_valid, int dp, float *O, int64_t ldo, float *Pd,
+                                                              int64_t ldp, int key_end, int row_end) {
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= rows_pad) return;
+    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+    float *orow = O + (int64_t)row * ldo;
+    for (int c = lane * 4; c < dp; c += 256) {
+        float4 acc = z;
+        if (row < n_valid)
+            for (int s = 0; s < nsplit; ++s) {
+                const float4 v = *reinterpret_cast<const float4 *>(Opart + ((int64_t)s * rows_pad + row) * dp + c);
+                acc.x += v.x, acc.y += v.y, acc.z += v.z, acc.w += v.w;
+            }
+        *reinterpret_cast<float4 *>(orow + c) = acc;
+    }
+    float *prow = Pd + (int64_t)row * ldp;
+    for (int c = (row < row_end ? key_end : 0) + lane * 4; c < rows_pad; c += 256) *reinterpret_cast<float4 *>(prow + c) = z;
+}
+
+inline int spv_nsplit(int64_t n_valid) {
+    const int64_t qb = (n_valid + FA_BM - 1) / FA_BM;
+    const int64_t kb = (n_valid + FA_BN - 1) / FA_BN;
+    int64_t s = 256 / (qb > 0 ? qb : 1);   // one workgroup per CU: ~256 of them in one round
+    if (s > kb) s = kb;
+    if (s < 1) s = 1;
+    return (int)s;
+}
+
+template <int DP>
+void launch_spv(const SpvP &P, bool x3, hipStream_t st) {
+    const dim3 grid((unsigned)(P.qblocks * P.nsplit));
+    if (x3)
+        hipLaunchKernelGGL((attn_softmax_pv_kernel<DP, true>), grid, dim3(FA_NT), 0, st, P);
+    else
+        hipLaunchKernelGGL((attn_softmax_pv_kernel<DP, false>), grid, dim3(FA_NT), 0, st, P);
+}
+
+}  // namespace
+
+extern "C" {
+
+int64_t u2gnn_attn_softmax_pv_ws_floats(int64_t n_valid, int64_t rows_pad, int64_t dp) {
+    if (n_valid < 1 || rows_pad < n_valid || dp < 64 || dp % 64) return -1;
+    return (int64_t)spv_nsplit(n_valid) * rows_pad * dp;
+}
+
+int u2gnn_attn_softmax_pv(const float *S, int64_t lds, const float *rowpart, int64_t ld_rowpart, int64_t ngroups,
+                          const void *qkv2, int64_t ldq2, int64_t dp, float *Pd, int64_t ldp, float *O, int64_t ldo,
+                          float *ws, int64_t ws_floats, int64_t n_valid, int64_t rows_pad, float p, uint64_t seed,
+                          int32_t precision, void *stream) {
+    if (!S || !rowpart || !qkv2 || !Pd || !O || !ws || n_valid < 1 || rows_pad < n_valid || rows_pad % FA_BM ||
+        !(p < 1.f) || p < 0.f || (precision != U2GNN_PREC_BF16X3 && precision != U2GNN_PREC_BF16))
+        return U2GNN_E_ARG;
+    if (dp < 64 || dp > 384 || dp % 64 || ldq2 < 6 * dp || (ldq2 & 7) || lds < rows_pad || (lds & 3) ||
+        ldp < rows_pad || (ldp & 3) || ldo < dp || (ldo & 3) || ngroups < 2 || (ngroups & 1) ||
+        ld_rowpart < ngroups || (ld_rowpart & 1) || ngroups > INT32_MAX)
+        return U2GNN_E_ARG;
+    if (((uintptr_t)S & 15) || ((uintptr_t)qkv2 & 15) || ((uintptr_t)Pd & 15) || ((uintptr_t)O & 15) ||
+        ((uintptr_t)rowpart & 15) || ((uintptr_t)ws & 15))
+        return U2GNN_E_ALIGN;
+    // 32-bit byte offsets inside one block's DMA sources
+    if ((int64_t)FA_BM * lds * 4 >= INT32_MAX || (int64_t)FA_BN * ldq2 * 2 >= INT32_MAX) return U2GNN_E_SHAPE;
+    const int64_t need = u2gnn_attn_softmax_pv_ws_floats(n_valid, rows_pad, dp);
+    if (need < 0 || ws_floats < need) return U2GNN_E_ARG;
+    SpvP P;
+    P.S = S;
+    P.lds = lds;
+    P.rowpart = rowpart;
+    P.ld_rowpart = ld_rowpart;
+    P.ngroups = (int32_t)ngroups;
+    P.qkv2 = static_cast<const __bf16 *>(qkv2);
+    P.ldq2 = ldq2;
+    P.Pd = Pd;
+    P.ldp = ldp;
+    P.Opart = ws;
+    P.nsplit = spv_nsplit(n_valid);
+    P.qblocks = (int32_t)((n_valid + FA_BM - 1) / FA_BM);   // blocks of padding rows only: zeroed below
+    P.n_valid = (int32_t)n_valid;
+    P.rows_pad = (int32_t)rows_pad;
+    P.kb_valid = (int32_t)((n_valid + FA_BN - 1) / FA_BN);
+    P.kb_per_split = (P.kb_valid + P.nsplit - 1) / P.nsplit;
+    P.p = p;
+    P.seed = seed;
+    P.epoch = u2gnn_g_epoch;
+    hipStream_t st = u2gnn_stream(stream);
+    const bool x3 = precision == U2GNN_PREC_BF16X3;
+    switch (dp) {
+        case 64: launch_spv<64>(P, x3, st); break;
+        case 128: launch_spv<128>(P, x3, st); break;
+        case 192: launch_spv<192>(P, x3, st); break;
+        case 256: launch_spv<256>(P, x3, st); break;
+        case 320: launch_spv<320>(P, x3, st); break;
+        default: launch_spv<384>(P, x3, st); break;
+    }
+    const int rc = u2gnn_launch_status();
+    if (rc != U2GNN_OK) return rc;
+    hipLaunchKernelGGL(attn_pv_combine_kernel, dim3((unsigned)((rows_pad + 3) / 4)), dim3(256), 0, st, ws, P.nsplit,
+                       (int)rows_pad, (int)n_valid, (int)dp, O, ldo, Pd, ldp, P.kb_valid * FA_BN, P.qblocks * FA_BM);
+    return u2gnn_launch_status();
+}
+
+}  // extern "C"

@@ -331,6 +331,10 @@ void set_ln(u2gnn_gemm_args &a, const float *gamma, const float *beta, float *y,
     a.ln_mean = mean, a.ln_rstd = rstd, a.ln_d = d, a.ln_rows = rows, a.ln_eps = 1e-5f;
 }
 
+// the fused attention forward (u2gnn_attn_softmax_pv): node-axis attention in the matrix-core
+// precisions with dp <= 384 (engine.fused_attn mirrors the rule)
+bool fused_attn(const Dims &D) { return !D.window && D.prec != U2GNN_PREC_F32 && D.dp <= 384; }
+
 int layer_fwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seeds *s, const float *X, float *X2,
               Arena &CA, Arena &W, bool need_ctx, hipStream_t st) {
     const int64_t N = D.N, Np = D.Np, d = D.d, dp = D.dp, ffp = D.ffp;
@@ -339,6 +343,9 @@ int layer_fwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
     const bool drop = pd > 0.f;
     const bool plan = W.plan();
     Ctx c = carve_ctx(need_ctx ? CA : W, D, drop);
+    const bool fused = fused_attn(D);
+    // the in-projection output again in x2 format: the V tiles the fused softmax.P.V kernel reads
+    void *qkv2 = fused ? static_cast<void *>(W.take<uint16_t>(Np * 6 * dp)) : nullptr;
     // a3.1 in-projection (+bias, Q scaled by 1/sqrt(d))
     {
         G g(X, w->W_in, c.QKV, Np, 3 * dp, dp, dp, dp, 3 * dp, prec);
@@ -351,6 +358,7 @@ int layer_fwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
         g.a.bias = w->b_in;
         g.a.alpha = (float)(1.0 / std::sqrt((double)d));
         g.a.scale_cols = dp;
+        if (fused) g.a.Cx2 = qkv2, g.a.ldcx2 = 6 * dp;
         U2GNN_TRY(g.run(st, plan));
     }
     const float *Q = c.QKV, *Kt = c.QKV + dp, *V = c.QKV + 2 * dp;
@@ -359,8 +367,29 @@ int layer_fwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
         if (!plan)
             U2GNN_TRY(u2gnn_window_attn_fwd(c.QKV, 3 * dp, D.window, (int32_t)dp, c.O, dp, c.Psave, pd, s->attn,
                                             N / D.window, Np, st));
+    } else if (fused) {
+        // a3.2 as S = Q K^T with the softmax row partials from the GEMM epilogue, then one fused
+        // softmax -> dropout -> P.V pass that overwrites S with the signed image (attn_fused.hip)
+        const int64_t ld_rp = Np / 32, groups = Np / 64;   // 64-column groups of the 256 / 128 tiles
+        float *rowpart = W.take<float>(Np * 2 * ld_rp);
+        float *pv_ws = W.take<float>(u2gnn_attn_softmax_pv_ws_floats(N, Np, dp));
+        {
+            G g(Q, Kt, c.Pd, Np, Np, dp, 3 * dp, 3 * dp, Np, prec);
+            g.tb().epi(U2GNN_EPI_STORE_ROWSTAT).tile(Np % 256 == 0 ? 256 : 128);
+            g.a.rowpart = rowpart, g.a.ld_rowpart = ld_rp, g.a.n_valid = N;
+            probe_mark(U2GNN_ROLE_QK, false, st, plan);
+            U2GNN_TRY(g.run(st, plan));
+            probe_mark(U2GNN_ROLE_QK, true, st, plan);
+        }
+        if (!plan) {
+            probe_mark(U2GNN_ROLE_PV, false, st, plan);
+            U2GNN_TRY(u2gnn_attn_softmax_pv(c.Pd, Np, rowpart, ld_rp, groups, qkv2, 6 * dp, dp, c.Pd, Np, c.O, dp,
+                                            pv_ws, u2gnn_attn_softmax_pv_ws_floats(N, Np, dp), N, Np, pd, s->attn,
+                                            prec, st));
+            probe_mark(U2GNN_ROLE_PV, true, st, plan);
+        }
     } else {
-        // a3.2 scores, softmax + dropout, P.V
+        // a3.2 scores, softmax + dropout, P.V (fp32 parity path, dp > 384)
         float *S = W.take<float>(Np * Np);
         {
             G g(Q, Kt, S, Np, Np, dp, 3 * dp, 3 * dp, Np, prec);

@@ -474,6 +474,12 @@ int launch_epi(const GemmP &P, int epi, int split, bool clamp_a, hipStream_t st)
         U2GNN_CASE(U2GNN_EPI_ATTN_DS)
         U2GNN_CASE(U2GNN_EPI_STORE_ROWDOT)
 #undef U2GNN_CASE
+        case U2GNN_EPI_STORE_ROWSTAT:   // the attention scores and their row partials, bf16 kinds only
+            if constexpr (KIND != U2GNN_PREC_F32 && !TA && TB)
+                launch_kernel<KIND, BM, BN, VAR, TA, TB, U2GNN_EPI_STORE_ROWSTAT>(P, grid, st);
+            else
+                return U2GNN_E_ARG;
+            break;
         case U2GNN_EPI_ATTN_DS_SIGNED:   // delta as STORE_ROWDOT partials: its own instantiation
             if (P.rowvec_parts > 1)
                 launch_kernel<KIND, BM, BN, VAR, TA, TB, EPI_DS_SIGNED_PARTS>(P, grid, st);
@@ -529,7 +535,7 @@ extern "C" int u2gnn_gemm(const u2gnn_gemm_args *a, void *stream) {
     if (x2 ? (!a->A2 || !a->B2) : (!a->A || !a->B)) return U2GNN_E_ARG;
     if (!a->C && !a->Cx2) return U2GNN_E_ARG;
     if (a->M <= 0 || a->N <= 0 || a->K <= 0) return U2GNN_E_ARG;
-    if (a->epilogue < 0 || a->epilogue > U2GNN_EPI_STORE_ROWDOT) return U2GNN_E_ARG;
+    if (a->epilogue < 0 || a->epilogue > U2GNN_EPI_STORE_ROWSTAT) return U2GNN_E_ARG;
     if (a->epilogue == U2GNN_EPI_ATTN_DS_RECOMP && !x2) return U2GNN_E_ARG;
     const int prec = a->precision;
     if (prec != U2GNN_PREC_F32 && prec != U2GNN_PREC_BF16X3 && prec != U2GNN_PREC_BF16) return U2GNN_E_ARG;
@@ -576,6 +582,12 @@ extern "C" int u2gnn_gemm(const u2gnn_gemm_args *a, void *stream) {
     if (e == U2GNN_EPI_ATTN_DS_RECOMP && (!a->rowvec || !a->rowstat || !(a->p_drop < 1.f) ||
                                           ((uintptr_t)a->rowstat & 7)))
         return U2GNN_E_ARG;
+    if (e == U2GNN_EPI_STORE_ROWSTAT) {
+        if (x2 || prec == U2GNN_PREC_F32 || split != 1 || a->Cx2 || !a->C || !a->rowpart || a->trans_a ||
+            !a->trans_b || a->n_valid < 1 || a->n_valid > a->N || a->ld_rowpart < a->N / 32)
+            return U2GNN_E_ARG;
+        if ((uintptr_t)a->rowpart & 7) return U2GNN_E_ALIGN;
+    }
     if (a->clamp_a && (e != U2GNN_EPI_STORE || a->trans_b)) return U2GNN_E_ARG;
     if (e == U2GNN_EPI_ATTN_DS && ((!a->aux1 && !a->keep) || !a->rowvec)) return U2GNN_E_ARG;
     if (e == U2GNN_EPI_ATTN_DS && a->keep && (a->ld_keep * 32 < a->N || !(a->p_drop < 1.f))) return U2GNN_E_ARG;

@@ -45,6 +45,7 @@ struct GemmP {
     int64_t ld_rowvec;
 };
 
+
 namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -91,7 +92,7 @@ __device__ __forceinline__ void epi_fetch(const GemmP &P, int row, int col, floa
 template <int EPI>
 __device__ __forceinline__ float4 epilogue4(const GemmP &P, int row, int col, float4 v, float4 a, float4 b,
                                             uint32_t kb, float dl) {
-    if constexpr (EPI == U2GNN_EPI_STORE || EPI == U2GNN_EPI_STORE_ROWDOT) {
+    if constexpr (EPI == U2GNN_EPI_STORE || EPI == U2GNN_EPI_STORE_ROWDOT || EPI == U2GNN_EPI_STORE_ROWSTAT) {
         return make_float4(P.alpha * v.x, P.alpha * v.y, P.alpha * v.z, P.alpha * v.w);
     } else if constexpr (ds_signed<EPI>) {
         // x = Pd = P/(1-p) where kept (sign clear), x = -P where dropped (sign set):
@@ -364,6 +365,36 @@ __device__ __forceinline__ void store_tile_ln(const GemmP &P, float *C, const f3
     }
 }
 
+// EPI_STORE_ROWSTAT: softmax partials of one row over this wave's 32*TN columns (those < n_valid):
+// (max, sum exp(C - max)) reduced over the row's two lanes (l, l ^ 32), stored as one float2 per
+// (row, column group) at rowpart + 2 * (row * ld_rowpart + c0 / (32 * TN)).
+template <int TM, int TN>
+__device__ __forceinline__ void rowstat_slice(const GemmP &P, const f32x16 (&acc)[TM][TN], int i, int row, int c0,
+                                              int kh) {
+    float m = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                if (c0 + j * 32 + 8 * g + 4 * kh + c < P.n_valid) m = fmaxf(m, P.alpha * acc[i][j][4 * g + c]);
+    m = fmaxf(m, __shfl_xor(m, 32, 64));
+    float l = 0.f;
+    if (m != -INFINITY) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+                    if (c0 + j * 32 + 8 * g + 4 * kh + c < P.n_valid) l += __expf(P.alpha * acc[i][j][4 * g + c] - m);
+    }
+    l += __shfl_xor(l, 32, 64);
+    if (kh == 0)
+        *reinterpret_cast<float2 *>(P.rowpart + 2 * ((int64_t)row * P.ld_rowpart + c0 / (32 * TN))) = make_float2(m, l);
+}
+
 template <int EPI, int TM, int TN>
 __device__ __forceinline__ void store_tile(const GemmP &P, float *C, const f32x16 (&acc)[TM][TN], int r0, int c0,
                                            int li, int kh, const PreDS<TN> *pre) {
@@ -392,6 +423,7 @@ __device__ __forceinline__ void store_tile(const GemmP &P, float *C, const f32x1
         if (i == 0 && pre) slice_from_pre<EPI>(*pre, kh, e);
         else fetch_slice<EPI>(P, row, c0, kh, e);
         rs[i] = store_slice<EPI>(P, C, acc, i, row, c0, kh, e);
+        if constexpr (EPI == U2GNN_EPI_STORE_ROWSTAT) rowstat_slice<TM, TN>(P, acc, i, row, c0, kh);
     }
     if constexpr (EPI == U2GNN_EPI_STORE_ROWDOT) {
         // one row partial per 64 output columns: lanes l and l + 32 hold a row's two column halves of

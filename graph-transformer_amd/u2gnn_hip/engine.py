@@ -312,6 +312,29 @@ def _gemm_nodes_k(A, B, C, M, N, Kd, lda, ldb, ldc, trans_a=False, alpha=1.0, pr
                 clamp_a=clamp_a)
 
 
+def fused_attn(dp: int, prec_qk: str, prec_pv: str) -> bool:
+    """Node-axis attention forward through the fused softmax.P.V kernel: matrix-core precisions,
+    dp <= 384 (encoder_layer.cpp fused_attn)."""
+    return prec_qk != "fp32" and prec_pv != "fp32" and dp <= 384
+
+
+def _attn_split(Q, Kt, V, N, Np, dp, pd, seeds, prec, att, dev):
+    """a3.2 as three passes (fp32 parity path, dp > 384): S = Q K^T, softmax + dropout into the image,
+    split-K P.V."""
+    f32 = torch.float32
+    S = torch.empty(Np, Np, device=dev, dtype=f32)
+    K.gemm(Q, Kt, S, Np, Np, dp, 3 * dp, 3 * dp, Np, trans_b=True, precision=_rp("qk", prec), flops=att,
+           tile=256 if (prec != "fp32" and Np % 256 == 0) else 0)
+    # one [Np, Np] image: with dropout the signed one (P/(1-p) where kept, -P where dropped), which
+    # P.V and dP^T.dO read as Pd (negatives staged as 0) and the dS epilogue reads as P and keep
+    Pd = torch.empty(Np, Np, device=dev, dtype=f32)
+    K.attn_softmax_fwd(S, Np, None if pd > 0 else Pd, Pd, Np, N, Np, N, Np, pd, seeds.get(SITE_ATTN, 0))
+    del S
+    O = torch.empty(Np, dp, device=dev, dtype=f32)
+    _gemm_nodes_k(Pd, V, O, Np, dp, Np, Np, 3 * dp, dp, prec=_rp("pv", prec), flops=att, clamp_a=pd > 0)
+    return Pd, O
+
+
 def encoder_layer_forward(X: torch.Tensor, w: PackedLayer, p: LayerParams, dims: Dims, train: bool,
                           seeds: Dict[int, int], need_ctx: bool, prec: str = "fp32",
                           p_drop: float = 0.5) -> (torch.Tensor, Optional[EncoderLayerCtx]):
@@ -323,20 +346,28 @@ def encoder_layer_forward(X: torch.Tensor, w: PackedLayer, p: LayerParams, dims:
     dev = X.device
     f32 = torch.float32
     QKV = torch.empty(Np, 3 * dp, device=dev, dtype=f32)
+    fused = fused_attn(dp, _rp("qk", prec), _rp("pv", prec))
+    QKV2 = torch.empty(Np, 6 * dp, device=dev, dtype=torch.bfloat16) if fused else None   # x2 copy for P.V
     K.gemm(X, w.W_in, QKV, Np, 3 * dp, dp, dp, dp, 3 * dp, trans_b=True, epilogue=E.EPI_BIAS, bias=w.b_in,
            alpha=1.0 / math.sqrt(d), scale_cols=dp, precision=_rp("in_proj", prec), flops=6.0 * N * d * d,
-           tile=256 if (prec != "fp32" and Np % 256 == 0 and (Np // 256) * (3 * dp // 128) >= BIG_TILE_BLOCKS) else 0)
+           tile=256 if (prec != "fp32" and Np % 256 == 0 and (Np // 256) * (3 * dp // 128) >= BIG_TILE_BLOCKS) else 0,
+           Cx2=QKV2, ldcx2=6 * dp)
     Q, Kt, V = QKV[:, :dp], QKV[:, dp:2 * dp], QKV[:, 2 * dp:]
-    S = torch.empty(Np, Np, device=dev, dtype=f32)
-    K.gemm(Q, Kt, S, Np, Np, dp, 3 * dp, 3 * dp, Np, trans_b=True, precision=_rp("qk", prec), flops=att,
-           tile=256 if (prec != "fp32" and Np % 256 == 0) else 0)
-    # one [Np, Np] image: with dropout the signed one (P/(1-p) where kept, -P where dropped), which
-    # P.V and dP^T.dO read as Pd (negatives staged as 0) and the dS epilogue reads as P and keep
-    Pd = torch.empty(Np, Np, device=dev, dtype=f32)
-    K.attn_softmax_fwd(S, Np, None if pd > 0 else Pd, Pd, Np, N, Np, N, Np, pd, seeds.get(SITE_ATTN, 0))
-    del S
-    O = torch.empty(Np, dp, device=dev, dtype=f32)
-    _gemm_nodes_k(Pd, V, O, Np, dp, Np, Np, 3 * dp, dp, prec=_rp("pv", prec), flops=att, clamp_a=pd > 0)
+    if fused:
+        # S = Q K^T written straight into the image buffer, with the softmax row partials of each 64-column
+        # group from the GEMM epilogue; one fused softmax -> dropout -> P.V pass then overwrites S with the
+        # signed image and forms O (attn_fused.hip; encoder_layer.cpp layer_fwd, launch for launch)
+        Pd = torch.empty(Np, Np, device=dev, dtype=f32)
+        rowpart = torch.empty(Np, 2 * (Np // 32), device=dev, dtype=f32)
+        K.gemm(Q, Kt, Pd, Np, Np, dp, 3 * dp, 3 * dp, Np, trans_b=True, epilogue=E.EPI_STORE_ROWSTAT,
+               rowpart=rowpart, n_valid=N, precision=_rp("qk", prec), flops=att, tile=256 if Np % 256 == 0 else 128)
+        ws = torch.empty(K.attn_softmax_pv_ws_floats(N, Np, dp), device=dev, dtype=f32)
+        O = torch.empty(Np, dp, device=dev, dtype=f32)
+        K.attn_softmax_pv(Pd, Np, rowpart, Np // 64, QKV2, 6 * dp, dp, Pd, Np, O, dp, ws, N, Np, pd,
+                          seeds.get(SITE_ATTN, 0), precision=_rp("pv", prec))
+        del QKV2, rowpart, ws
+    else:
+        Pd, O = _attn_split(Q, Kt, V, N, Np, dp, pd, seeds, prec, att, dev)
     Z1 = torch.empty(Np, dp, device=dev, dtype=f32)
     X1 = torch.empty(Np, dp, device=dev, dtype=f32)
     mean1 = torch.empty(Np, device=dev, dtype=f32)

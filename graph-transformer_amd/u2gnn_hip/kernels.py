@@ -117,6 +117,8 @@ def gemm(A, B, C, M, N, K, lda, ldb, ldc, trans_a=False, trans_b=False, epilogue
     if rowpart is not None:
         _dev(rowpart)
         a.rowpart, a.ld_rowpart = rowpart.data_ptr(), int(rowpart.stride(0))
+        if epilogue == _lib.EPI_STORE_ROWSTAT:   # [M, 2 * groups] float32: ld in (max, sum) pairs
+            a.ld_rowpart = int(rowpart.stride(0)) // 2
     a.ld_aux = int(ld_aux)
     a.alpha = float(alpha)
     a.scale_cols = int(scale_cols)
@@ -340,6 +342,22 @@ def sampled_softmax_bwd(X, ldx, labels, sample_ids, S, W, ldw, prob, dloss, dX, 
     check(hip_lib().u2gnn_sampled_softmax_bwd(_p(X), int(ldx), _p(labels), _p(sample_ids), int(S), _p(W), int(ldw),
                                               _p(prob), _p(dloss), _p(dX), int(lddx), _p(dW), int(lddw), int(n_rows),
                                               int(D), _s()), "u2gnn_sampled_softmax_bwd")
+
+
+def attn_softmax_pv_ws_floats(n_valid, rows_pad, dp):
+    return int(hip_lib().u2gnn_attn_softmax_pv_ws_floats(int(n_valid), int(rows_pad), int(dp)))
+
+
+def attn_softmax_pv(S, lds, rowpart, ngroups, qkv2, ldq2, dp, Pd, ldp, O, ldo, ws, n_valid, rows_pad, p, seed,
+                    precision="bf16x3"):
+    """ABI v10: signed probability image Pd and O = dropout(P) V from the scores S, the EPI_STORE_ROWSTAT
+    row partials ``rowpart`` (float32 [rows, >= 2*ngroups]) and the x2 in-projection output qkv2 (bfloat16)."""
+    _dev(S, rowpart, qkv2, Pd, O, ws)
+    check(hip_lib().u2gnn_attn_softmax_pv(_p(S), int(lds), _p(rowpart), int(rowpart.stride(0)) // 2, int(ngroups),
+                                          _p(qkv2), int(ldq2), int(dp), _p(Pd), int(ldp), _p(O), int(ldo), _p(ws),
+                                          int(ws.numel()), int(n_valid), int(rows_pad), float(p),
+                                          int(seed) & 0xFFFFFFFFFFFFFFFF, PREC[precision], _s()),
+          "u2gnn_attn_softmax_pv")
 
 
 def sampled_softmax_bwd_rows(X, ldx, labels, sample_ids, S, W, ldw, prob, dloss, dX, lddx, dW_lab, dW_smp, n_rows, D):

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define U2GNN_ABI_VERSION 9
+#define U2GNN_ABI_VERSION 10
 
 #define U2GNN_OK 0
 #define U2GNN_E_ARG (-1)    /* bad size / null pointer */
@@ -63,6 +63,13 @@ extern "C" {
                                        (the attention backward's delta = rowsum(dO * O) formed by the dO
                                        GEMM; ATTN_DS_SIGNED sums the N/64 partials in q order, rowvec_parts).
                                        N % 64 == 0, split_k 1, fp32-operand kernels only */
+#define U2GNN_EPI_STORE_ROWSTAT 11 /* ABI v10: C = alpha*acc as STORE, and per row m and group q of 32*TN
+                                       output columns (the wave tile's width: 64 on 128- and 256-row tiles, 32 on
+                                       64x64 tiles; row_group_cols reports it) the softmax partials over the
+                                       columns n < n_valid: rowpart[2*(m*ld_rowpart + q)] = max, [+1] =
+                                       sum exp(C - max) (-inf and 0 when the group has no such column) -- the
+                                       attention scores S = Q K^T and their row statistics in one pass
+                                       (u2gnn_attn_softmax_pv folds the groups).  bf16 kinds, split_k 1 */
 
 /* x2 operand format (pre-split fp32): a logical fp32 matrix X[R][C] (C % 8 == 0) is stored as
  * bf16 X2[R][2C] with, per 8-column group g, hi(X[r][8g..8g+7]) then lo(X[r][8g..8g+7]),
@@ -127,7 +134,9 @@ typedef struct u2gnn_gemm_args {
     float ln_eps;
     int32_t ln_reserved;
     /* ---- ABI v8: delta from the dO GEMM (EPI_STORE_ROWDOT -> EPI_ATTN_DS_SIGNED) ---- */
-    float *rowpart;       /* STORE_ROWDOT: [N/64][ld_rowpart] row partials (ld_rowpart >= M) */
+    float *rowpart;       /* STORE_ROWDOT: [N/64][ld_rowpart] row partials (ld_rowpart >= M);
+                             STORE_ROWSTAT (ABI v10): [M][ld_rowpart] (max, sum) float2 pairs, ld_rowpart in
+                             pairs (>= N/32), 8-byte aligned; n_valid = the columns taken */
     int64_t ld_rowpart;
     int32_t rowvec_parts; /* ATTN_DS_SIGNED: 0/1 = rowvec[m]; P > 1 = sum_{q<P} rowvec[q*ld_rowvec + m] in
                              q order (fp32-operand kernels only) */
@@ -313,6 +322,24 @@ int u2gnn_index_add_rows(const float *src, int64_t ld_src, const int64_t *idx, i
 int u2gnn_index_zero_rows(const int64_t *idx, int64_t n_rows, float *dst, int64_t ld_dst, int64_t dst_rows,
                           int64_t D, int32_t *err, void *stream);
 
+/* ---- ABI v10: fused softmax -> dropout -> P.V over the node axis (a3.2; pytorch_U2GNN_Sup.py:19-21,35) ----
+ * The attention forward after S = Q K^T (u2gnn_gemm with EPI_STORE_ROWSTAT, whose epilogue leaves per row
+ * the (max, sum exp) partials of ngroups column groups in rowpart, ld_rowpart pairs per row): the
+ * probabilities never exist apart from the one signed image the backward reads.  Per row m < n_valid the
+ * kernel folds the partials into (M, L) and, for keys n < n_valid, P = exp(S[m,n] - M) / L, keep =
+ * keep(seed, m, n) (the hash of every dropout site); it writes the signed image Pd = keep ? P/(1-p) : -P
+ * (zero for padded rows / keys; what EPI_ATTN_DS_SIGNED and the clamped P^T.dO read) and
+ * O = Pd_kept . V on the matrix cores (precision BF16X3: split-bf16, 3 products; BF16: 1), V read from qkv2
+ * (the in-projection output in x2 format, [rows_pad][ldq2] bf16, V = columns 2dp .. 3dp).  dp in {64, 128,
+ * ..., 384}, rows_pad % 128 == 0, ngroups and ld_rowpart even, rowpart 16-byte aligned; S and Pd may
+ * alias (the image is written over the scores it replaces).
+ * ws: u2gnn_attn_softmax_pv_ws_floats(n_valid, rows_pad, dp) floats (per key range partial outputs). */
+int64_t u2gnn_attn_softmax_pv_ws_floats(int64_t n_valid, int64_t rows_pad, int64_t dp);
+int u2gnn_attn_softmax_pv(const float *S, int64_t lds, const float *rowpart, int64_t ld_rowpart, int64_t ngroups,
+                          const void *qkv2, int64_t ldq2, int64_t dp, float *Pd, int64_t ldp, float *O, int64_t ldo,
+                          float *ws, int64_t ws_floats, int64_t n_valid, int64_t rows_pad, float p, uint64_t seed,
+                          int32_t precision, void *stream);
+
 /* ---- a12: dropout on the concatenated UnSup node embeddings (model_U2GNN_Unsup_multi.py:56) --
  * Y[i, j] = X[i, j] * keep(seed, i, j) / (1-p) for i < rows, j < cols.  The backward is the same
  * call on the upstream gradient with the same seed.  Y may alias X. */
@@ -391,7 +418,8 @@ int u2gnn_layer_bwd(const u2gnn_layer_dims *dims, const u2gnn_layer_params *w,
  * returns the summed device time and the launch count, then frees the events.  One probe per
  * process; arm/collect from the thread that issues the layers (bench.py's timed region). */
 #define U2GNN_ROLE_QK 1   /* S = Q K^T                                   */
-#define U2GNN_ROLE_PV 2   /* O = Pd V (split-K GEMM only, not its reduce) */
+#define U2GNN_ROLE_PV 2   /* O = Pd V (split-K GEMM only, not its reduce; fused path: the softmax.P.V
+                             kernel and its combine pass) */
 #define U2GNN_ROLE_DS 3   /* dS = P o (dO V^T - delta)                   */
 #define U2GNN_ROLE_DV 4
 #define U2GNN_ROLE_DQ 5

@@ -2,21 +2,25 @@
 // . V inside torch's MultiheadAttention, pytorch_U2GNN_Sup.py:19-21,35 / pytorch_U2GNN_UnSup.py:37-40,57).
 //
 // The scores come from the QK^T GEMM, whose epilogue also leaves per-row softmax partials
-// (EPI_STORE_ROWSTAT, per 64-column group); one fused kernel folds those into (max, 1/sum) per row and
-// then does what the softmax pass and the P.V GEMM did: it reads each score once, forms
-// P = exp(s - max)/sum and the dropout decision in registers, writes the signed image the backward
-// reads (the only N x N write left in the forward) and multiplies the kept probabilities into V on the
-// matrix cores (split bf16, 3 products per term) without staging P anywhere.
+// (EPI_STORE_ROWSTAT, per 64-column group; masked keys stored as -inf); one fused kernel folds those
+// into (max, 1/sum) per row and then does what the softmax pass and the P.V GEMM did: it reads each
+// score once, forms P = exp(s - max)/sum and the dropout decision in registers, writes the signed
+// image the backward reads (the only N x N write left in the forward) and multiplies the kept
+// probabilities into V on the matrix cores (split bf16, 3 products per term) without staging P.
 //
 // One workgroup = 4 waves = 128 query rows (32 per wave, one wave per SIMD) x one range of keys (the key
 // axis is split over workgroups so ~256 of them fill the chip; a combine pass adds the ranges).  Per
 // block of 32 keys:
-//   * the 128 x 32 score tile and the 32-key V tile (pre-split x2 rows of the in-projection output)
-//     arrive by LDS-DMA, one block ahead;
+//   * the 32-key V tile (pre-split x2 rows of the in-projection output) arrives by LDS-DMA one block
+//     ahead, the 128 x 32 score tile two blocks ahead;
 //   * lane l of a wave takes query l%32 and the 8 consecutive keys 8h .. 8h+7 (h = l/32) of each
 //     16-key step -- exactly the B operand of v_mfma_f32_32x32x16_bf16 -- so P never leaves registers;
+//     block kb+1's P is formed while block kb's products run (software pipeline);
 //   * O^T += V^T . P, V^T fragments read with ds_read_b64_tr_b16 from the k-major V image (BF16X3: the
 //     three split products hi.lo + lo.hi + hi.hi; BF16: hi.hi only).
+// Measured variants: two waves per SIMD (8 waves, d split in halves, P handed
+// between partner waves through LDS) ran 2-4 % slower than this form; an ablation puts ~30 of its
+// ~95 us (C4) in the fixed costs (row statistics, partial-output stores, the combine pass).
 #include "u2gnn_common.h"
 
 #include <type_traits>
@@ -46,33 +50,44 @@ __device__ __forceinline__ int s_swz(int r) { return (r >> 1) & 7; }
 // vmcnt(0) in front of the fragment reads of the OTHER stage (it cannot tell the two stages apart
 // through a DMA) nor orders anything after it; every wait on these is the counted wait_vm below.
 // M0 is reserved (never allocated) and nothing else in these kernels reads it, so it is not clobbered.
+__device__ __forceinline__ const char *uniform_ptr(const char *p) {
+    const uint64_t v = reinterpret_cast<uint64_t>(p);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return reinterpret_cast<const char *>(((uint64_t)hi << 32) | lo);
+}
+
+// base and m0 are wave-uniform by construction; the readfirstlanes only tell the compiler so (the "s"
+// operands need SGPRs whatever its divergence analysis concludes)
 __device__ __forceinline__ void dma16(const char *base, int off, unsigned m0) {
-    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2" ::"s"(m0), "v"(off), "s"(base)
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2" ::"s"(__builtin_amdgcn_readfirstlane(m0)),
+                 "v"(off), "s"(uniform_ptr(base))
                  : "memory");
 }
 
 // LDS byte address of a shared object (a link-time constant)
 __device__ __forceinline__ unsigned lds_addr(const void *p) { return (unsigned)(size_t)(const lds_void *)p; }
 
-template <int DP>
+template <int DP, int NT = FA_NT>
 __device__ __forceinline__ void issue_v(const char *vbase, int64_t ld_bytes, unsigned img, int tid, int w) {
-    constexpr int RB = 4 * DP;                       // bytes per k-row
-    constexpr int NI = FA_BN * RB / (16 * FA_NT);   // DMA instructions per thread (DP / 32)
+    constexpr int RB = 4 * DP;                      // bytes per k-row
+    constexpr int NI = FA_BN * RB / (16 * NT);     // DMA instructions per thread
+    static_assert(NI * 16 * NT == FA_BN * RB, "V tile / threads");
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
-        const int b = (i * FA_NT + tid) * 16;
+        const int b = (i * NT + tid) * 16;
         const int kr = b / RB, pb = b % RB;
-        dma16(vbase, (int)(kr * ld_bytes) + (pb ^ kr_swz(kr)), img + (i * FA_NT + 64 * w) * 16);
+        dma16(vbase, (int)(kr * ld_bytes) + (pb ^ kr_swz(kr)), img + (i * NT + 64 * w) * 16);
     }
 }
 
-// the 128 x 32 score tile: 4 DMA instructions per thread
+// the 128 x 32 score tile: 16 KB, 1 KB per wave-instruction
+template <int NT = FA_NT>
 __device__ __forceinline__ void issue_s(const char *sbase, int64_t lds_bytes, unsigned img, int tid, int w) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int c = i * FA_NT + tid;       // 16-B chunk of the image
+    for (int i = 0; i < S_IMG / (16 * NT); ++i) {
+        const int c = i * NT + tid;          // 16-B chunk of the image
         const int r = c >> 3, q = (c & 7) ^ s_swz(r);
-        dma16(sbase, (int)(r * lds_bytes) + q * 16, img + (i * FA_NT + 64 * w) * 16);
+        dma16(sbase, (int)(r * lds_bytes) + q * 16, img + (i * NT + 64 * w) * 16);
     }
 }
 
@@ -143,26 +158,34 @@ struct SpvP {
     const uint64_t *epoch;
 };
 
+// (m, l) <- the log-sum-exp merge with (m2, l2); -inf maxima (empty groups) contribute nothing
 __device__ __forceinline__ void lse_merge(float &m, float &l, float m2, float l2) {
-    if (m2 == -INFINITY) return;
-    if (m == -INFINITY) {
-        m = m2, l = l2;
-        return;
-    }
     const float n = fmaxf(m, m2);
-    l = l * __expf(m - n) + l2 * __expf(m2 - n);
+    const float e1 = m == -INFINITY ? 0.f : __expf(m - n);
+    const float e2 = m2 == -INFINITY ? 0.f : __expf(m2 - n);
+    l = l * e1 + l2 * e2;
     m = n;
 }
 
 // (max, 1/sum) of one row from its ngroups (max, sum exp) partials: the row's two lanes (h = 0, 1) take
-// alternate pairs of groups and merge at the end -- the same order in every workgroup of the row block
+// alternate pairs of groups, 8 loads in flight per lane, and merge at the end -- the same order in every
+// workgroup of the row block
 __device__ __forceinline__ void row_stat(const SpvP &P, int query, int h, float &M, float &inv) {
     const float4 *pr = reinterpret_cast<const float4 *>(P.rowpart + 2 * (int64_t)query * P.ld_rowpart);
+    const int n4 = P.ngroups / 2;
     float m = -INFINITY, l = 0.f;
-    for (int j = h; j < P.ngroups / 2; j += 2) {
-        const float4 v = pr[j];
-        lse_merge(m, l, v.x, v.y);
-        lse_merge(m, l, v.z, v.w);
+    for (int j0 = h; j0 < n4; j0 += 16) {
+        float4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int j = j0 + 2 * u;
+            v[u] = j < n4 ? pr[j] : make_float4(-INFINITY, 0.f, -INFINITY, 0.f);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            lse_merge(m, l, v[u].x, v[u].y);
+            lse_merge(m, l, v[u].z, v[u].w);
+        }
     }
     const float m2 = __shfl_xor(m, 32, 64), l2 = __shfl_xor(l, 32, 64);
     if (h == 0) {
@@ -176,49 +199,51 @@ __device__ __forceinline__ void row_stat(const SpvP &P, int query, int h, float 
 }
 
 // this lane's P for keys kb*32 + 16 ks + 8 h .. +7 (ks = 0, 1: the B operands of the block's two 16-key
-// steps), from the score tile simg; writes the signed image and returns the kept P/(1-p) split to bf16
+// steps), from the score tile simg; writes the signed image and returns the kept P/(1-p) split to bf16.
+// No masks: keys >= n_valid hold -inf in S (EPI_STORE_ROWSTAT) and padded query rows have mb = +inf, so
+// both reach exp2(-inf) = 0.
 struct PRow {
-    int r, h, klim;
-    float mb, inv, sc, p;
-    uint32_t rkey;
+    int r, h;
+    float mb, inv, sc;
+    uint32_t rkey, thr;
     float *prow;
 };
 
-__device__ __forceinline__ void p_block(const PRow &R, const char *simg, int kb, bf16x8 (&ph)[2], bf16x8 (&pl)[2]) {
-    const int key0 = kb * FA_BN;
+__device__ __forceinline__ void p_half(const PRow &R, const char *simg, int kb, int ks, bf16x8 &ph, bf16x8 &pl) {
+    const int c = 4 * ks + 2 * R.h;   // logical 16-B chunk of the row
+    const char *rowp = simg + R.r * 128;
+    const float4 a = *reinterpret_cast<const float4 *>(rowp + ((c ^ s_swz(R.r)) << 4));
+    const float4 b = *reinterpret_cast<const float4 *>(rowp + (((c + 1) ^ s_swz(R.r)) << 4));
+    float sv[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    // pin the two vector reads (the compiler otherwise splits them into single-element reads)
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-        const int c = 4 * ks + 2 * R.h;   // logical 16-B chunk of the row
-        const char *rowp = simg + R.r * 128;
-        const float4 a = *reinterpret_cast<const float4 *>(rowp + ((c ^ s_swz(R.r)) << 4));
-        const float4 b = *reinterpret_cast<const float4 *>(rowp + (((c + 1) ^ s_swz(R.r)) << 4));
-        float sv[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-        // pin the two vector reads: without this the compiler turns the key mask below into branches
-        // and sinks single-element LDS reads into them
+    for (int t = 0; t < 8; ++t) asm("" : "+v"(sv[t]));
+    const int kbase = kb * FA_BN + 16 * ks + 8 * R.h;   // even: keys kbase + 2q, + 2q + 1 share hash q
+    uint32_t hs[4];
 #pragma unroll
-        for (int t = 0; t < 8; ++t) asm("" : "+v"(sv[t]));
-        float pv[8], img[8];
+    for (int q = 0; q < 4; ++q) hs[q] = u2gnn_pair_hash(R.rkey, (uint32_t)(kbase >> 1) + q);
+    float pv[8], img[8];
 #pragma unroll
-        for (int t = 0; t < 8; ++t) {
-            // branch-free: masked keys/rows go through exp2(-inf) = 0; at p = 0 every u >= p keeps
-            const int key = key0 + 16 * ks + 8 * R.h + t;
-            const float x = key < R.klim ? sv[t] * 1.4426950408889634f - R.mb : -INFINITY;
-            const float pr = __builtin_amdgcn_exp2f(x) * R.inv;
-            const float u = (float)(u2gnn_fmix32(R.rkey + (uint32_t)key * 0x9E3779B9u) >> 8) * (1.0f / 16777216.0f);
-            const bool kp = u >= R.p;
-            const float ps = pr * R.sc;
-            pv[t] = kp ? ps : 0.f;
-            img[t] = kp ? ps : -pr;
-        }
-        float *dst = R.prow + key0 + 16 * ks + 8 * R.h;
-#ifndef SPV_NO_STORE
-        *reinterpret_cast<float4 *>(dst) = make_float4(img[0], img[1], img[2], img[3]);
-        *reinterpret_cast<float4 *>(dst + 4) = make_float4(img[4], img[5], img[6], img[7]);
-#else
-        if (img[0] == 123.f) *dst = img[1] + img[2] + img[3] + img[4] + img[5] + img[6] + img[7];
-#endif
-        split8(pv, ph[ks], pl[ks]);
+    for (int t = 0; t < 8; ++t) {
+        const float pr = __builtin_amdgcn_exp2f(sv[t] * 1.4426950408889634f - R.mb) * R.inv;
+        const bool kp = (t & 1) ? u2gnn_keep_hi(hs[t >> 1], R.thr) : u2gnn_keep_lo(hs[t >> 1], R.thr);
+        const float ps = pr * R.sc;
+        pv[t] = kp ? ps : 0.f;
+        img[t] = kp ? ps : -pr;
     }
+    float *dst = R.prow + kbase;
+#ifndef SPV_NO_STORE
+    *reinterpret_cast<float4 *>(dst) = make_float4(img[0], img[1], img[2], img[3]);
+    *reinterpret_cast<float4 *>(dst + 4) = make_float4(img[4], img[5], img[6], img[7]);
+#else
+    if (img[0] == 123.f) *dst = img[1] + img[2] + img[3] + img[4] + img[5] + img[6] + img[7];
+#endif
+    split8(pv, ph, pl);
+}
+
+__device__ __forceinline__ void p_block(const PRow &R, const char *simg, int kb, bf16x8 (&ph)[2], bf16x8 (&pl)[2]) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) p_half(R, simg, kb, ks, ph[ks], pl[ks]);
 }
 
 // O^T += V^T . P over one block (V image vimg, P operands ph / pl); fragments of d tile t + 1 are read
@@ -297,13 +322,16 @@ __global__ void __launch_bounds__(FA_NT, 1) attn_softmax_pv_kernel(SpvP P) {
     const char *srow0 = reinterpret_cast<const char *>(P.S + (int64_t)qrow0 * P.lds);
     const bool qvalid = query < P.n_valid;
     float M = 0.f, inv = 0.f;
+#ifndef SPV_NO_ROWSTAT
     if (qb * FA_BM < P.n_valid) row_stat(P, query, R.h, M, inv);
+#else
+    M = 0.f, inv = 1e-3f;
+#endif
     // retire those loads before any LDS-DMA is in flight (every later wait below is a counted one)
     wait_vm<0>();
-    R.klim = qvalid ? P.n_valid : 0;         // keys < klim carry probability
-    R.mb = qvalid ? M * 1.4426950408889634f : 0.f;
+    R.mb = qvalid ? M * 1.4426950408889634f : INFINITY;   // padded rows: exp2(s - inf) = 0
     R.inv = qvalid ? inv : 0.f;
-    R.p = P.p;
+    R.thr = u2gnn_keep_thr(P.p);
     R.sc = P.p > 0.f ? 1.f / (1.f - P.p) : 1.f;
     R.rkey = u2gnn_row_key(seed, (uint32_t)query);
     R.prow = P.Pd + (int64_t)query * P.ldp;
@@ -319,15 +347,15 @@ __global__ void __launch_bounds__(FA_NT, 1) attn_softmax_pv_kernel(SpvP P) {
     // earlier) into V(kb) while it forms block kb+1's P from the score tile S(kb+1); LDS holds V(kb) and
     // S(kb+1) for the current iteration and receives V(kb+1) and S(kb+2) by DMA.  The stages are separate
     // LDS objects and the loop is unrolled by two, so every access names its stage at compile time.
-    auto issue_vt = [&](int kb, unsigned img) {
+    auto issue_vt = [&](int kb, unsigned img) __attribute__((always_inline)) {
         issue_v<DP>(vcol + (int64_t)kb * FA_BN * ld_bytes, ld_bytes, img, tid, w);
     };
-    auto issue_st = [&](int kb, unsigned img) {
+    auto issue_st = [&](int kb, unsigned img) __attribute__((always_inline)) {
         issue_s(srow0 + (int64_t)kb * FA_BN * 4, lds_bytes, img, tid, w);
     };
     bf16x8 ph[2], pl[2];
     // an iteration that also forms the next block's P (kb + 1 < kb1)
-    auto body = [&](auto stage, int kb) {
+    auto body = [&](auto stage, int kb) __attribute__((always_inline)) {
         constexpr int STG = decltype(stage)::value;
         // V(kb), S(kb+1) landed (this wave's pieces: only the 4 image stores issued after those DMAs
         // may still be in flight), then everyone's; every wave is also done with V(kb-1) and S(kb), whose
@@ -353,7 +381,7 @@ __global__ void __launch_bounds__(FA_NT, 1) attn_softmax_pv_kernel(SpvP P) {
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) ph[ks] = nh[ks], pl[ks] = nl[ks];
     };
-    auto last = [&](auto stage) {
+    auto last = [&](auto stage) __attribute__((always_inline)) {
         constexpr int STG = decltype(stage)::value;
         wait_vm<4>();
         __builtin_amdgcn_s_barrier();
@@ -380,12 +408,19 @@ __global__ void __launch_bounds__(FA_NT, 1) attn_softmax_pv_kernel(SpvP P) {
     }
     // ---- partial O of this key range: O^T lane layout = query l%32, d = 32 t + 8 g + 4 h .. +3
     float *orow = P.Opart + ((int64_t)split * P.rows_pad + query) * DP;
+#ifndef SPV_NO_OSTORE
 #pragma unroll
     for (int t = 0; t < DT; ++t)
 #pragma unroll
         for (int g = 0; g < 4; ++g)
             *reinterpret_cast<float4 *>(orow + 32 * t + 8 * g + 4 * R.h) =
                 make_float4(o[t][4 * g], o[t][4 * g + 1], o[t][4 * g + 2], o[t][4 * g + 3]);
+#else
+    float acc = 0.f;
+#pragma unroll
+    for (int t = 0; t < DT; ++t) acc += o[t][0] + o[t][5];
+    if (acc == 123.f) *orow = acc;
+#endif
 }
 
 // O[row] = sum over the key ranges (fixed order); rows >= n_valid zero; and the parts of the signed

@@ -501,6 +501,7 @@ __global__ void __launch_bounds__(256) attn_softmax_kernel(const float *S, int64
         }
     const float inv = 1.f / block_sum4(s, red, lane, w);
     const float ks = p > 0.f ? 1.f / (1.f - p) : 1.f;
+    const uint32_t rkey = u2gnn_row_key(seed, (uint32_t)row), thr = u2gnn_keep_thr(p);
 #pragma unroll
     for (int i = 0; i < SM_RV; ++i) {
         const int64_t cb = (int64_t)i * 1024;
@@ -512,7 +513,7 @@ __global__ void __launch_bounds__(256) attn_softmax_kernel(const float *S, int64
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             pv[j] = e[i][j] * inv;
-            kp[j] = (p > 0.f) ? u2gnn_keep(seed, (uint32_t)row, (uint32_t)(c + j), p) : true;
+            kp[j] = u2gnn_keep_rk(rkey, (uint32_t)(c + j), thr);
             pdv[j] = kp[j] ? pv[j] * ks : (sgn ? -pv[j] : 0.f);
         }
         if (in) {
@@ -587,8 +588,7 @@ __global__ void __launch_bounds__(256) attn_softmax_x2_kernel(const float *S, in
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const float pv = e[i][j] * inv;
-            const bool kp = !(p > 0.f) ||
-                            (float)(u2gnn_fmix32(rkey + (uint32_t)(c + j) * 0x9E3779B9u) >> 8) * (1.0f / 16777216.0f) >= p;
+            const bool kp = u2gnn_keep_rk(rkey, (uint32_t)(c + j), u2gnn_keep_thr(p));
             pdv[j] = kp ? pv * ks : 0.f;
         }
         store_x2_4(Pd2, ldp2, (int)row, (int)c, make_float4(pdv[0], pdv[1], pdv[2], pdv[3]));

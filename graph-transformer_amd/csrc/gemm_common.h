@@ -92,7 +92,12 @@ __device__ __forceinline__ void epi_fetch(const GemmP &P, int row, int col, floa
 template <int EPI>
 __device__ __forceinline__ float4 epilogue4(const GemmP &P, int row, int col, float4 v, float4 a, float4 b,
                                             uint32_t kb, float dl) {
-    if constexpr (EPI == U2GNN_EPI_STORE || EPI == U2GNN_EPI_STORE_ROWDOT || EPI == U2GNN_EPI_STORE_ROWSTAT) {
+    if constexpr (EPI == U2GNN_EPI_STORE_ROWSTAT) {
+        // masked keys (columns >= n_valid) stored as -inf: their probability is exp(-inf) = 0 downstream
+        const float ni = -INFINITY;
+        return make_float4(col < P.n_valid ? P.alpha * v.x : ni, col + 1 < P.n_valid ? P.alpha * v.y : ni,
+                           col + 2 < P.n_valid ? P.alpha * v.z : ni, col + 3 < P.n_valid ? P.alpha * v.w : ni);
+    } else if constexpr (EPI == U2GNN_EPI_STORE || EPI == U2GNN_EPI_STORE_ROWDOT) {
         return make_float4(P.alpha * v.x, P.alpha * v.y, P.alpha * v.z, P.alpha * v.w);
     } else if constexpr (ds_signed<EPI>) {
         // x = Pd = P/(1-p) where kept (sign clear), x = -P where dropped (sign set):
@@ -132,9 +137,14 @@ __device__ __forceinline__ float4 epilogue4(const GemmP &P, int row, int col, fl
                 for (int c = 0; c < 4; ++c) x[c] = fmaxf(x[c], 0.f);
             }
             if (P.p > 0.f) {
+                // col % 4 == 0: the four columns are two hash pairs
                 const float s = 1.f / (1.f - P.p);
+                const uint32_t rk = u2gnn_row_key(P.seed, (uint32_t)row), thr = u2gnn_keep_thr(P.p);
+                const uint32_t h0 = u2gnn_pair_hash(rk, (uint32_t)col >> 1), h1 = u2gnn_pair_hash(rk, ((uint32_t)col >> 1) + 1);
+                const bool kp[4] = {u2gnn_keep_lo(h0, thr), u2gnn_keep_hi(h0, thr), u2gnn_keep_lo(h1, thr),
+                                    u2gnn_keep_hi(h1, thr)};
 #pragma unroll
-                for (int c = 0; c < 4; ++c) x[c] = u2gnn_keep(P.seed, row, col + c, P.p) ? x[c] * s : 0.f;
+                for (int c = 0; c < 4; ++c) x[c] = kp[c] ? x[c] * s : 0.f;
             }
             if constexpr (EPI == U2GNN_EPI_BIAS_DROP_RESID) {
                 x[0] += b.x, x[1] += b.y, x[2] += b.z, x[3] += b.w;
@@ -217,8 +227,7 @@ __device__ __forceinline__ float4 ds_recomp4(const GemmP &P, int row, int col, f
     for (int c = 0; c < 4; ++c) {
         const uint32_t cc = (uint32_t)(col + c);
         const float pr = (rv && (int)cc < P.n_valid) ? expf(x[c] - rm) * rinv : 0.f;
-        const bool kp = !(P.p > 0.f) ||
-                        (float)(u2gnn_fmix32(rkey + cc * 0x9E3779B9u) >> 8) * (1.0f / 16777216.0f) >= P.p;
+        const bool kp = u2gnn_keep_rk(rkey, cc, u2gnn_keep_thr(P.p));
         o[c] = pr * ((kp ? g[c] * sc : 0.f) - dl);
     }
     return make_float4(o[0], o[1], o[2], o[3]);

@@ -15,10 +15,11 @@ static inline int u2gnn_launch_status() {
 static inline hipStream_t u2gnn_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }
 
 // ---------------------------------------------------------------------------------------
-// Dropout: counter-based keep decision.  keep(seed, i, j) = U(seed, i, j) >= p with U the top 24
-// bits of a murmur3 32-bit finaliser of (rowkey(seed, i) + j * golden); rowkey folds both seed
-// halves and the row through the same finaliser.  32-bit integer work only (~12 VALU per element
-// once the row key is hoisted, vs ~35 for a 64-bit splitmix): the N^2 attention dropout is the
+// Dropout: counter-based keep decision.  keep(seed, i, j) = U(seed, i, j) >= p with U a 16-bit
+// uniform: half of a murmur3 32-bit finaliser of (rowkey(seed, i) + (j / 2) * golden), the low half
+// for even j, the high half for odd j -- one finaliser per two columns.  rowkey folds both seed
+// halves and the row through the same finaliser.  32-bit integer work only, and the comparison in
+// integers (U >= ceil(65536 p), exact for every p in [0, 1)): the N^2 attention dropout is the
 // largest consumer.  The same (seed, i, j) regenerates the mask in backward; nothing is stored.
 // ---------------------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t u2gnn_fmix32(uint32_t h) {
@@ -42,9 +43,25 @@ __device__ __forceinline__ uint64_t u2gnn_seed(uint64_t seed, const uint64_t *ep
     return epoch ? seed ^ (*epoch * 0x9E3779B97F4A7C15ull) : seed;
 }
 
+// the integer threshold of keep probability 1 - p: U >= thr  <=>  U / 65536 >= p
+__device__ __forceinline__ uint32_t u2gnn_keep_thr(float p) { return (uint32_t)ceilf(p * 65536.f); }
+
+// the finaliser word of columns 2c, 2c + 1 of the row with key rkey
+__device__ __forceinline__ uint32_t u2gnn_pair_hash(uint32_t rkey, uint32_t c) {
+    return u2gnn_fmix32(rkey + c * 0x9E3779B9u);
+}
+
+// keep bits of columns 2c (low half of h) and 2c + 1 (high half)
+__device__ __forceinline__ bool u2gnn_keep_lo(uint32_t h, uint32_t thr) { return (h & 0xFFFFu) >= thr; }
+__device__ __forceinline__ bool u2gnn_keep_hi(uint32_t h, uint32_t thr) { return (h >> 16) >= thr; }
+
+__device__ __forceinline__ bool u2gnn_keep_rk(uint32_t rkey, uint32_t j, uint32_t thr) {
+    const uint32_t h = u2gnn_pair_hash(rkey, j >> 1);
+    return (j & 1) ? u2gnn_keep_hi(h, thr) : u2gnn_keep_lo(h, thr);
+}
+
 __device__ __forceinline__ bool u2gnn_keep(uint64_t seed, uint32_t i, uint32_t j, float p) {
-    const uint32_t u = u2gnn_fmix32(u2gnn_row_key(seed, i) + j * 0x9E3779B9u) >> 8;   // 24 bits
-    return (float)u * (1.0f / 16777216.0f) >= p;
+    return u2gnn_keep_rk(u2gnn_row_key(seed, i), j, u2gnn_keep_thr(p));
 }
 
 // ---------------------------------------------------------------------------------------

@@ -65,8 +65,8 @@ extern "C" {
                                        N % 64 == 0, split_k 1, fp32-operand kernels only */
 #define U2GNN_EPI_STORE_ROWSTAT 11 /* ABI v10: C = alpha*acc as STORE, and per row m and group q of 32*TN
                                        output columns (the wave tile's width: 64 on 128- and 256-row tiles, 32 on
-                                       64x64 tiles; row_group_cols reports it) the softmax partials over the
-                                       columns n < n_valid: rowpart[2*(m*ld_rowpart + q)] = max, [+1] =
+                                       64x64 tiles) the softmax partials over the columns n < n_valid (columns
+                                       n >= n_valid are stored as -inf: masked keys): rowpart[2*(m*ld_rowpart + q)] = max, [+1] =
                                        sum exp(C - max) (-inf and 0 when the group has no such column) -- the
                                        attention scores S = Q K^T and their row statistics in one pass
                                        (u2gnn_attn_softmax_pv folds the groups).  bf16 kinds, split_k 1 */
@@ -331,8 +331,8 @@ int u2gnn_index_zero_rows(const int64_t *idx, int64_t n_rows, float *dst, int64_
  * (zero for padded rows / keys; what EPI_ATTN_DS_SIGNED and the clamped P^T.dO read) and
  * O = Pd_kept . V on the matrix cores (precision BF16X3: split-bf16, 3 products; BF16: 1), V read from qkv2
  * (the in-projection output in x2 format, [rows_pad][ldq2] bf16, V = columns 2dp .. 3dp).  dp in {64, 128,
- * ..., 384}, rows_pad % 128 == 0, ngroups and ld_rowpart even, rowpart 16-byte aligned; S and Pd may
- * alias (the image is written over the scores it replaces).
+ * ..., 384}, rows_pad % 128 == 0, ngroups and ld_rowpart even, rowpart 16-byte aligned; S columns >= n_valid
+ * hold -inf (as EPI_STORE_ROWSTAT writes them); S and Pd may alias (the image is written over the scores).
  * ws: u2gnn_attn_softmax_pv_ws_floats(n_valid, rows_pad, dp) floats (per key range partial outputs). */
 int64_t u2gnn_attn_softmax_pv_ws_floats(int64_t n_valid, int64_t rows_pad, int64_t dp);
 int u2gnn_attn_softmax_pv(const float *S, int64_t lds, const float *rowpart, int64_t ld_rowpart, int64_t ngroups,

@@ -32,7 +32,7 @@ def _ref_rowstat(S, N, Np):
                                           (4864, 4776, 384, 256), (384, 70, 64, 128)])
 @pytest.mark.parametrize("prec", ["bf16x3", "bf16"])
 def test_store_rowstat_epilogue(Np, N, dp, tile, prec):
-    """S is bitwise the plain STORE result; each 64-column group carries (max, sum exp(S - max)) of its
+    """S is bitwise the plain STORE result over the N real keys (-inf beyond); each 64-column group carries (max, sum exp(S - max)) of its
     columns < N, (-inf, 0) when it has none."""
     QKV = _mk(Np, 3 * dp, seed=3, scale=0.3)
     Q, Kt = QKV[:, :dp], QKV[:, dp:2 * dp]
@@ -43,7 +43,8 @@ def test_store_rowstat_epilogue(Np, N, dp, tile, prec):
     K.gemm(Q, Kt, S, Np, Np, dp, 3 * dp, 3 * dp, Np, trans_b=True, precision=prec, tile=tile, alpha=0.7,
            epilogue=_lib.EPI_STORE_ROWSTAT, rowpart=rp, n_valid=N)
     torch.cuda.synchronize()
-    assert torch.equal(S, S0)
+    assert torch.equal(S[:, :N], S0[:, :N])
+    assert torch.isneginf(S[:, N:]).all()   # masked keys: exp(-inf) = 0 downstream
     G = Np // 64
     pairs = rp[:, :2 * G].view(Np, G, 2)[:N].double()
     s = S0[:N].double().view(N, G, 64)
@@ -94,6 +95,7 @@ def test_softmax_pv(Np, N, dp, p, prec, tol):
     and S / Pd aliasing gives the same bits."""
     seed = 4242
     S = _mk(Np, Np, seed=7, scale=2.0)
+    S[:, N:] = float("-inf")   # as EPI_STORE_ROWSTAT leaves the masked keys
     V = _mk(Np, dp, seed=9)
     rp = _partials(S, N, Np)
     rs = _ref_rowstat(S, N, Np)

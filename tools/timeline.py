@@ -1,18 +1,21 @@
 """Timeline view of a rocprofv3 kernel trace (the CSV tools/kstats.py keeps): GPU busy time (union of
 kernel intervals), per-stream busy time, time with both streams busy, and the idle gaps, over the
-window from the first to the last kernel of the trace's final N steps (adam_kernel marks a step end).
-Usage: python tools/timeline.py trace.csv [steps]"""
+window from the first to the last kernel of the trace's final N steps (adam_kernel marks a step end),
+optionally ending SKIP steps before the trace's last one (bench.py's pipeline_rate steps follow the timed
+region: --pipeline-steps 20 plus 2 warmup steps = skip 22).
+Usage: python tools/timeline.py trace.csv [steps] [skip]"""
 import csv
 import sys
 
 rows = list(csv.DictReader(open(sys.argv[1])))
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+skip = int(sys.argv[3]) if len(sys.argv) > 3 else 0
 key = next(k for k in ("Stream_Id", "Queue_Id", "Stream_ID") if k in rows[0])
 ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r[key], r["Kernel_Name"]) for r in rows)
 ends = [e for s, e, q, n in ev if "adam_kernel" in n or "adam_dev_kernel" in n]
-if len(ends) < steps + 1:
+if len(ends) < steps + skip + 1:
     sys.exit(f"only {len(ends)} optimizer steps in the trace")
-t0, t1 = ends[-steps - 1], ends[-1]
+t0, t1 = ends[len(ends) - skip - steps - 1], ends[len(ends) - skip - 1]
 win = [(max(s, t0), min(e, t1), q, n) for s, e, q, n in ev if e > t0 and s < t1]
 
 

@@ -32,6 +32,11 @@ SHAPES = [  # name, M, N, K, ta, tb, [(split, tile), ...] (tile 129 = 128x128 wi
     # shallow-K backward products (dH.W1 -> dX1, dQKV.W_in -> dX)
     ("dX1   NN", Np, dp, ffp, False, False, [(1, 64), (1, 128), (2, 128), (4, 256)]),
     ("dXin  NN", Np, dp, 3 * dp, False, False, [(1, 64), (1, 128), (2, 128), (4, 256)]),
+    # the same weight products with the weight stored transposed (NT): the k-contiguous B image
+    ("dH-T  NT", Np, ffp, dp, False, True, [(1, 64), (1, 128)], 4),
+    ("dO-T  NT", Np, dp, dp, False, True, [(1, 64), (1, 128)]),
+    ("dX1-T NT", Np, dp, ffp, False, True, [(1, 64), (1, 128)]),
+    ("dXin-T NT", Np, dp, 3 * dp, False, True, [(1, 64), (1, 128)]),
 ]
 
 

@@ -539,9 +539,14 @@ int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
     if (need_dx)
         U2GNN_TRY(gemm_split(W, D, dQKV, w->W_in, dX, Np, dp, 3 * dp, 3 * dp, dp, dp, false, 1.f, true, nullptr,
                              nullptr, false, st));
-    U2GNN_TRY(sd.fork());
-    U2GNN_TRY(wgrad(W, D, dQKV, 3 * dp, X, dp, 3 * dp, dp, g->in_w, d, blk_d, blk_d, so));
-    U2GNN_TRY(bias_grad(W, dQKV, Np, 3 * dp, 3 * dp, dp, d, g->in_b, so));
+    // the in-projection's parameter gradients: on the side stream beside the dX product, but on this
+    // stream for the last layer of the backward (need_dx false), where nothing is left to overlap and
+    // the hand-off plus the step's final join cost more than the products (C4: ~75 us idle per step)
+    const bool side_w = need_dx;   // 3.140-3.157 vs 3.171-3.194 ms per C4 step (4 pairs, one session)
+    hipStream_t wst = side_w ? so : st;
+    if (side_w) U2GNN_TRY(sd.fork());
+    U2GNN_TRY(wgrad(W, D, dQKV, 3 * dp, X, dp, 3 * dp, dp, g->in_w, d, blk_d, blk_d, wst));
+    U2GNN_TRY(bias_grad(W, dQKV, Np, 3 * dp, 3 * dp, dp, d, g->in_b, wst));
     return (W.overflow || CA.overflow) ? U2GNN_E_ARG : U2GNN_OK;
 }
 

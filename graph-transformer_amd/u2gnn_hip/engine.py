@@ -480,7 +480,10 @@ def encoder_layer_backward(dX2: torch.Tensor, ctx: EncoderLayerCtx, w: PackedLay
     def in_proj_grads(dQKV=dQKV):
         _wgrad(dQKV, 3 * dp, ctx.X, dp, 3 * dp, dp, Np, g.in_w, (dp, d), (dp, d), _rp("in_dw", prec), N)
         _bias_grad(dQKV, Np, 3 * dp, 3 * dp, (dp, d), g.in_b)
-    off.run(in_proj_grads, dQKV, ctx.X)
+    if need_dx:
+        off.run(in_proj_grads, dQKV, ctx.X)
+    else:   # the last layer of the backward: nothing left on this stream to overlap, skip the hand-off
+        in_proj_grads()
     if own:
         off.join()
     return dX if need_dx else None

@@ -21,6 +21,16 @@ sys.path[:0] = [REPO, os.path.join(REPO, "graph-transformer_amd")]
 REF_FILE = "/root/reference/U2GNN_pytorch/pytorch_U2GNN_Sup.py"
 
 
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.machine()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=3)
@@ -85,7 +95,7 @@ def main():
         print(f"reference {t_ref[-1]:.1f} s, oracle {t_orc[-1]:.1f} s", flush=True)
     mr, mo = float(np.median(t_ref)), float(np.median(t_orc))
     out = {"what": "one C4 training step (64 graphs, all 17 slots, dropout on, clip + Adam) on torch CPU",
-           "batch_nodes": int(off[-1]), "threads": threads, "cpu": platform.processor() or platform.machine(),
+           "batch_nodes": int(off[-1]), "threads": threads, "cpu": cpu_model(),
            "reference_step_s": [round(x, 2) for x in t_ref], "oracle_step_s": [round(x, 2) for x in t_orc],
            "reference_graphs_per_s": round(B / mr, 3), "oracle_graphs_per_s": round(B / mo, 3),
            "oracle_over_reference_time": round(mo / mr, 3), "bar": "within +-15 % (SURVEY §8(d))",

@@ -662,12 +662,20 @@ __global__ void __launch_bounds__(256) layernorm_fwd_kernel(const float *Z, int6
         const int64_t c = 4 * (hl + LPR * i);
         t[i] = c < d_pad ? ld4(z + c) : z4;
     }
-    // gamma / beta are unpadded [d] vectors at any 4-byte alignment: element loads at a clamped
-    // column, issued with the row's loads (no per-element branch, no second round trip later)
+    // gamma / beta are unpadded [d] vectors: element loads at a clamped column, issued with the row's
+    // loads (no per-element branch, no second round trip later) -- or, when both are 16-byte aligned
+    // (the flat parameter buffer's views are), one float4 per full 4-column chunk
+    const bool gb16 = ((reinterpret_cast<uintptr_t>(gamma) | reinterpret_cast<uintptr_t>(beta)) & 15) == 0;
 #pragma unroll
     for (int i = 0; i < LN_V4; ++i) {
         const int64_t c = 4 * (hl + LPR * i);
         if (c >= d_pad) continue;
+        if (gb16 && c + 4 <= d) {
+            const float4 g = ld4(gamma + c), b = ld4(beta + c);
+            gm[i][0] = g.x, gm[i][1] = g.y, gm[i][2] = g.z, gm[i][3] = g.w;
+            bt[i][0] = b.x, bt[i][1] = b.y, bt[i][2] = b.z, bt[i][3] = b.w;
+            continue;
+        }
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int64_t cc = c + q < d ? c + q : d - 1;
@@ -761,10 +769,16 @@ __global__ void __launch_bounds__(256) layernorm_bwd_kernel(const float *dY, int
             tc[i] = c < d_pad ? ld4(dt.bias + c) : z4;
         }
     }
+    const bool g16 = (reinterpret_cast<uintptr_t>(gamma) & 15) == 0;
 #pragma unroll
-    for (int i = 0; i < LN_V4; ++i) {   // unpadded [d] gamma: clamped element loads (see the forward)
+    for (int i = 0; i < LN_V4; ++i) {   // unpadded [d] gamma: float4 or clamped element loads (see the forward)
         const int64_t c = 4 * (hl + 32 * i);
         if (c >= d_pad) continue;
+        if (g16 && c + 4 <= d) {
+            const float4 g = ld4(gamma + c);
+            gm[i][0] = g.x, gm[i][1] = g.y, gm[i][2] = g.z, gm[i][3] = g.w;
+            continue;
+        }
 #pragma unroll
         for (int q = 0; q < 4; ++q) gm[i][q] = gamma[c + q < d ? c + q : d - 1];
     }

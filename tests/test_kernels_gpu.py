@@ -305,11 +305,12 @@ def test_dropout_mask_statistics():
 
 
 @pytest.mark.parametrize("d,dp", [(67, 128), (200, 256), (367, 384), (500, 512), (600, 640), (1000, 1024)])
-def test_layernorm_fwd_bwd(d, dp):
+@pytest.mark.parametrize("gb_offset", [0, 1])   # 16-byte aligned gamma / beta (float4 loads) or not
+def test_layernorm_fwd_bwd(d, dp, gb_offset):
     """Per-lane widths 1, 2, 3, 4 and the 8-wide fallback of the LayerNorm kernels."""
     Np, N = 128, 100
     Z = _mk(Np, dp, seed=11)
-    gam, bet = _mk(d, seed=12), _mk(d, seed=13)
+    gam, bet = _mk(d + gb_offset, seed=12)[gb_offset:], _mk(d + gb_offset, seed=13)[gb_offset:]
     Y = torch.empty(Np, dp, device=DEV)
     mu, rs = torch.empty(Np, device=DEV), torch.empty(Np, device=DEV)
     K.layernorm_fwd(Z, dp, gam, bet, Y, dp, mu, rs, N, Np, d, dp)

@@ -423,28 +423,40 @@ __global__ void __launch_bounds__(FA_NT, 1) attn_softmax_pv_kernel(SpvP P) {
 #endif
 }
 
-// O[row] = sum over the key ranges (fixed order); rows >= n_valid zero; and the parts of the signed
-// image no fused block wrote: keys from kb_valid*32 on, rows of query blocks past n_valid.
-// One wave per row, float4 columns.
+// O[row] = sum over the key ranges (fixed order s = 0, 1, ...); rows >= n_valid zero.  One thread per
+// float4 of O with every range's load in flight (8 at a time).  Then the parts of the signed image no
+// fused block wrote -- keys from kb_valid*32 on, rows of query blocks past n_valid -- one wave per row.
 __global__ void __launch_bounds__(256) attn_pv_combine_kernel(const float *Opart, int nsplit, int rows_pad,
                                                               int n_valid, int dp, float *O, int64_t ldo, float *Pd,
                                                               int64_t ldp, int key_end, int row_end) {
-    const int lane = threadIdx.x & 63;
-    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (row >= rows_pad) return;
+    const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
     const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-    float *orow = O + (int64_t)row * ldo;
-    for (int c = lane * 4; c < dp; c += 256) {
+    const int c4 = dp >> 2;
+    if (gid < (int64_t)rows_pad * c4) {
+        const int row = (int)(gid / c4), c = (int)(gid - (int64_t)row * c4) * 4;
         float4 acc = z;
-        if (row < n_valid)
-            for (int s = 0; s < nsplit; ++s) {
-                const float4 v = *reinterpret_cast<const float4 *>(Opart + ((int64_t)s * rows_pad + row) * dp + c);
-                acc.x += v.x, acc.y += v.y, acc.z += v.z, acc.w += v.w;
+        if (row < n_valid) {
+            const float *p = Opart + (int64_t)row * dp + c;
+            const int64_t stride = (int64_t)rows_pad * dp;
+            for (int s0 = 0; s0 < nsplit; s0 += 8) {
+                float4 v[8];
+#pragma unroll
+                for (int q = 0; q < 8; ++q)
+                    if (s0 + q < nsplit) v[q] = *reinterpret_cast<const float4 *>(p + (s0 + q) * stride);
+#pragma unroll
+                for (int q = 0; q < 8; ++q)
+                    if (s0 + q < nsplit) acc.x += v[q].x, acc.y += v[q].y, acc.z += v[q].z, acc.w += v[q].w;
             }
-        *reinterpret_cast<float4 *>(orow + c) = acc;
+        }
+        *reinterpret_cast<float4 *>(O + (int64_t)row * ldo + c) = acc;
     }
-    float *prow = Pd + (int64_t)row * ldp;
-    for (int c = (row < row_end ? key_end : 0) + lane * 4; c < rows_pad; c += 256) *reinterpret_cast<float4 *>(prow + c) = z;
+    const int64_t row = gid >> 6;
+    const int lane = (int)(gid & 63);
+    if (row < rows_pad) {
+        float *prow = Pd + row * ldp;
+        for (int c = (row < row_end ? key_end : 0) + lane * 4; c < rows_pad; c += 256)
+            *reinterpret_cast<float4 *>(prow + c) = z;
+    }
 }
 
 inline int spv_nsplit(int64_t n_valid) {
@@ -524,7 +536,8 @@ int u2gnn_attn_softmax_pv(const float *S, int64_t lds, const float *rowpart, int
     }
     const int rc = u2gnn_launch_status();
     if (rc != U2GNN_OK) return rc;
-    hipLaunchKernelGGL(attn_pv_combine_kernel, dim3((unsigned)((rows_pad + 3) / 4)), dim3(256), 0, st, ws, P.nsplit,
+    const int64_t cthreads = rows_pad * (dp / 4) > rows_pad * 64 ? rows_pad * (dp / 4) : rows_pad * 64;
+    hipLaunchKernelGGL(attn_pv_combine_kernel, dim3((unsigned)((cthreads + 255) / 256)), dim3(256), 0, st, ws, P.nsplit,
                        (int)rows_pad, (int)n_valid, (int)dp, O, ldo, Pd, ldp, P.kb_valid * FA_BN, P.qblocks * FA_BM);
     return u2gnn_launch_status();
 }

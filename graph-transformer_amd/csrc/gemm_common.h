@@ -328,15 +328,26 @@ __device__ __forceinline__ void store_tile_ln(const GemmP &P, float *C, const f3
     }
     const int d = P.ln_d;
     float gm[16], bt[16];
+    // unpadded [d] vectors: float4 loads of full 4-column chunks when 16-byte aligned (the flat
+    // parameter buffer's views are), clamped element loads otherwise
+    const bool gb16 = ((reinterpret_cast<uintptr_t>(P.ln_gamma) | reinterpret_cast<uintptr_t>(P.ln_beta)) & 15) == 0;
 #pragma unroll
-    for (int g = 0; g < 4; ++g)
+    for (int g = 0; g < 4; ++g) {
+        const int col0 = c0 + 8 * g + 4 * kh;
+        if (gb16 && col0 + 4 <= d) {
+            const float4 gv = ld4(P.ln_gamma + col0), bv = ld4(P.ln_beta + col0);
+            gm[4 * g] = gv.x, gm[4 * g + 1] = gv.y, gm[4 * g + 2] = gv.z, gm[4 * g + 3] = gv.w;
+            bt[4 * g] = bv.x, bt[4 * g + 1] = bv.y, bt[4 * g + 2] = bv.z, bt[4 * g + 3] = bv.w;
+            continue;
+        }
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-            const int col = c0 + 8 * g + 4 * kh + c;
-            const int cc = col < d ? col : d - 1;   // unpadded [d] vectors: clamped loads
+            const int col = col0 + c;
+            const int cc = col < d ? col : d - 1;
             gm[4 * g + c] = P.ln_gamma[cc];
             bt[4 * g + c] = P.ln_beta[cc];
         }
+    }
     float s = 0.f;
 #pragma unroll
     for (int g = 0; g < 4; ++g)

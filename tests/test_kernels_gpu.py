@@ -337,7 +337,8 @@ def test_layernorm_fwd_bwd(d, dp, gb_offset):
 
 @pytest.mark.parametrize("d,K_,p", [(19, 64, 0.0), (19, 1024, 0.5), (64, 64, 0.5), (4, 64, 0.0)])
 @pytest.mark.parametrize("prec", ["bf16x3", "bf16"])
-def test_bias_drop_resid_layernorm_epilogue(d, K_, p, prec):
+@pytest.mark.parametrize("gb_offset", [0, 1])   # 16-byte aligned gamma / beta (float4 loads) or not
+def test_bias_drop_resid_layernorm_epilogue(d, K_, p, prec, gb_offset):
     """EPI_BIAS_DROP_RESID_LN (d <= 64, one 64-column tile per row): Z is bit-identical to the
     BIAS_DROP_RESID epilogue, Y / mean / rstd match layernorm_fwd on that Z (fp32, 1e-5), rows past
     ln_rows and columns past d are zero."""
@@ -346,7 +347,7 @@ def test_bias_drop_resid_layernorm_epilogue(d, K_, p, prec):
     W = _mk(dp, K_, seed=42) * 0.1
     bias = _mk(dp, seed=43)
     X = _mk(Np, dp, seed=44)
-    gam, bet = _mk(d, seed=45), _mk(d, seed=46)
+    gam, bet = _mk(d + gb_offset, seed=45)[gb_offset:], _mk(d + gb_offset, seed=46)[gb_offset:]
     Z_ref = torch.empty(Np, dp, device=DEV)
     K.gemm(A, W, Z_ref, Np, dp, K_, K_, K_, dp, trans_b=True, epilogue=_lib.EPI_BIAS_DROP_RESID, bias=bias, aux0=X,
            ld_aux=dp, p_drop=p, seed=5, precision=prec)

@@ -22,6 +22,7 @@
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <algorithm>
 #include <vector>
 
 #include "u2gnn_hip.h"
@@ -155,6 +156,41 @@ struct G {   // one GEMM launch (defaults = plain store)
 
 hipEvent_t pooled_event();
 
+// Reductions (and weight-gradient products) held back to the end of a latency-bound layer's backward,
+// where they go out as one grouped GEMM launch and one u2gnn_reduce_batch call (<= 2 launches) instead
+// of 12-16 launches of a few microseconds each.  Used when the layer runs on one stream (no side stream:
+// C5, C2, C3).  Every job computes the same bits as its immediate launch (u2gnn_hip.h, ABI v11).
+struct Defer {
+    std::vector<u2gnn_reduce_job> red;
+    std::vector<u2gnn_gemm_args> gemm;
+    bool gemms = false;   // hold back the weight-gradient GEMM launches as well
+};
+
+int flush(Defer *df, Arena &W, hipStream_t st) {
+    if (!df) return U2GNN_OK;
+    const bool plan = W.plan();
+    for (size_t o = 0; o < df->gemm.size(); o += 8) {
+        const int32_t n = (int32_t)std::min<size_t>(8, df->gemm.size() - o);
+        if (!plan) U2GNN_TRY(u2gnn_gemm_group(df->gemm.data() + o, n, st));
+    }
+    const int64_t wsf = u2gnn_reduce_batch_ws_floats(df->red.data(), (int32_t)df->red.size());
+    if (wsf < 0) return U2GNN_E_ARG;
+    float *ws = W.take<float>(wsf > 0 ? wsf : 1);
+    if (!plan && !df->red.empty())
+        U2GNN_TRY(u2gnn_reduce_batch(df->red.data(), (int32_t)df->red.size(), ws, wsf, st));
+    df->red.clear();
+    df->gemm.clear();
+    return U2GNN_OK;
+}
+
+u2gnn_reduce_job rjob(int kind) {
+    u2gnn_reduce_job j;
+    std::memset(&j, 0, sizeof(j));
+    j.kind = kind;
+    j.alpha = 1.f;
+    return j;
+}
+
 // split-K block targets (engine._gemm_split): 448 blocks for 64 / 128 tiles, 240 for 256x128 tiles
 // (round-2 sweeps: 224 / 896 within noise, 120 / 300 / 460 slower on the 256x128 products)
 constexpr int64_t kSplitTarget = 448, kSplitTarget256 = 240;
@@ -165,7 +201,7 @@ constexpr int64_t kSplitTarget = 448, kSplitTarget256 = 240;
 int gemm_split(Arena &W, const Dims &D, const float *A, const float *B, float *C, int64_t M, int64_t N, int64_t Kd,
                int64_t lda, int64_t ldb, int64_t ldc, bool ta, float alpha, bool accumulate, const int64_t *rblk,
                const int64_t *cblk, bool deep, hipStream_t st, bool clamp_a = false, int prec = -1, int role = 0,
-               hipStream_t red_st = nullptr) {
+               hipStream_t red_st = nullptr, Defer *df = nullptr) {
     if (prec < 0) prec = D.prec;
     const bool f32 = prec == U2GNN_PREC_F32;
     const int64_t bk = f32 ? 16 : 32;
@@ -212,6 +248,10 @@ int gemm_split(Arena &W, const Dims &D, const float *A, const float *B, float *C
         g.a.alpha = alpha;
         g.a.clamp_a = clamp_a;
         g.epi(accumulate ? U2GNN_EPI_ACCUM : U2GNN_EPI_STORE).tile(t);
+        if (df && df->gemms && !accumulate) {
+            df->gemm.push_back(g.a);
+            return U2GNN_OK;
+        }
         probe_mark(role, false, st, plan);
         const int rc = g.run(st, plan);
         probe_mark(role, true, st, plan);
@@ -224,12 +264,27 @@ int gemm_split(Arena &W, const Dims &D, const float *A, const float *B, float *C
     g.a.slab_stride = M * N;
     g.a.clamp_a = clamp_a;
     g.tile(t);
+    const int64_t rb0 = rblk ? rblk[0] : M, rb1 = rblk ? rblk[1] : M;
+    const int64_t cb0 = cblk ? cblk[0] : N, cb1 = cblk ? cblk[1] : N;
+    if (df) {   // slab reduce (and with df->gemms the GEMM itself) at the layer's flush
+        if (df->gemms) {
+            df->gemm.push_back(g.a);
+        } else {
+            probe_mark(role, false, st, plan);
+            U2GNN_TRY(g.run(st, plan));
+            probe_mark(role, true, st, plan);
+        }
+        u2gnn_reduce_job j = rjob(U2GNN_RJOB_SLAB);
+        j.src = slabs, j.n_slab = (int32_t)split, j.slab_stride = M * N, j.rows = M, j.cols = N, j.ld_src = N;
+        j.rblk_pad = rb0, j.rblk_real = rb1, j.cblk_pad = cb0, j.cblk_real = cb1;
+        j.dst = C, j.ld_dst = ldc, j.alpha = alpha, j.accumulate = accumulate ? 1 : 0;
+        df->red.push_back(j);
+        return U2GNN_OK;
+    }
     probe_mark(role, false, st, plan);
     U2GNN_TRY(g.run(st, plan));
     probe_mark(role, true, st, plan);
     if (plan) return U2GNN_OK;
-    const int64_t rb0 = rblk ? rblk[0] : M, rb1 = rblk ? rblk[1] : M;
-    const int64_t cb0 = cblk ? cblk[0] : N, cb1 = cblk ? cblk[1] : N;
     hipStream_t rs = st;
     if (red_st && red_st != st) {
         hipEvent_t ev = pooled_event();
@@ -243,16 +298,24 @@ int gemm_split(Arena &W, const Dims &D, const float *A, const float *B, float *C
 
 // engine._wgrad: dst(real) = unpack(dY^T X)
 int wgrad(Arena &W, const Dims &D, const float *dY, int64_t ld_dy, const float *X, int64_t ld_x, int64_t m_pad,
-          int64_t n_pad, float *dst, int64_t ld_dst, const int64_t *rblk, const int64_t *cblk, hipStream_t st) {
+          int64_t n_pad, float *dst, int64_t ld_dst, const int64_t *rblk, const int64_t *cblk, hipStream_t st,
+          Defer *df = nullptr) {
     return gemm_split(W, D, dY, X, dst, m_pad, n_pad, D.Np, ld_dy, ld_x, ld_dst, true, 1.f, false, rblk, cblk, true,
-                      st);
+                      st, false, -1, 0, nullptr, df);
 }
 
 int64_t colstat_ws_floats(int64_t rows, int64_t cols) { return ((rows + 15) / 16 > 0 ? (rows + 15) / 16 : 1) * 3 * cols; }
 
 int bias_grad(Arena &W, const float *dY, int64_t rows, int64_t cols_pad, int64_t ld, int64_t cb0, int64_t cb1,
-              float *out, hipStream_t st) {
+              float *out, hipStream_t st, Defer *df = nullptr) {
+    // taken in both modes: the size plan (u2gnn_layer_sizes runs the one-stream form) covers the side-stream form
     float *ws = W.take<float>(colstat_ws_floats(rows, cols_pad));
+    if (df) {
+        u2gnn_reduce_job j = rjob(U2GNN_RJOB_COLSUM);
+        j.src = dY, j.rows = rows, j.cols = cols_pad, j.ld_src = ld, j.cblk_pad = cb0, j.cblk_real = cb1, j.dst = out;
+        df->red.push_back(j);
+        return U2GNN_OK;
+    }
     if (W.plan()) return U2GNN_OK;
     return u2gnn_colsum(dY, rows, cols_pad, ld, cb0, cb1, out, 0, ws, st);
 }
@@ -317,6 +380,21 @@ struct Side {
         return e == hipSuccess ? U2GNN_OK : (int)e;
     }
 };
+
+// u2gnn_layernorm_bwd_params now, or as a job of the layer's flush
+int ln_params(const float *dY, const float *Z, const float *mean, const float *rstd, const float *dZd, int64_t ld,
+              int64_t rows, int64_t d, int64_t dp, float *ws, float *dgamma, float *dbeta, float *dbias, hipStream_t st,
+              bool plan, Defer *df) {
+    if (df) {
+        u2gnn_reduce_job j = rjob(U2GNN_RJOB_LNPARAMS);
+        j.src = dY, j.ld_src = ld, j.Z = Z, j.ldz = ld, j.mean = mean, j.rstd = rstd, j.dZdrop = dZd, j.lddrop = ld;
+        j.rows = rows, j.d = d, j.cols = dp, j.dst = dgamma, j.dbeta = dbeta, j.dbias = dbias;
+        df->red.push_back(j);
+        return U2GNN_OK;
+    }
+    if (plan) return U2GNN_OK;
+    return u2gnn_layernorm_bwd_params(dY, ld, Z, ld, mean, rstd, dZd, ld, rows, d, dp, ws, dgamma, dbeta, dbias, st);
+}
 
 // Schedule decisions (each measured in rounds 1-2; the A/B switches are gone):
 //  * dV = Pd^T dO runs on the side stream beside the dS -> dQ -> dK chain (-1.4 % step time);
@@ -449,6 +527,11 @@ int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
     Ctx c = carve_ctx(CA, D, drop);
     Side sd{st, side_st ? side_st : st, plan};
     hipStream_t so = sd.side;
+    // one stream (latency-bound layers): the parameter-gradient reductions and products go out together
+    // at the end (df), the attention products' slab reduces together before the in-projection (att)
+    Defer defer_p, defer_a;
+    defer_p.gemms = true;
+    Defer *df = so == st ? &defer_p : nullptr, *att = so == st ? &defer_a : nullptr;
     const int64_t blk_d[2] = {dp, d}, blk_ff[2] = {ffp, ff};
     float *ws = W.take<float>(colstat_ws_floats(N, dp));
     // LN2 backward -> dX1 (residual), dF (dropout2 branch); norm2 + linear2.bias grads (side)
@@ -457,9 +540,7 @@ int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
         U2GNN_TRY(u2gnn_layernorm_bwd(dX2, dp, c.Z2, dp, c.mean2, c.rstd2, w->n2_w, dX1, dp, dF, dp, pd, s->drop2, N,
                                       Np, d, dp, st));
     U2GNN_TRY(sd.fork());
-    if (!plan)
-        U2GNN_TRY(u2gnn_layernorm_bwd_params(dX2, dp, c.Z2, dp, c.mean2, c.rstd2, dF, dp, N, d, dp, ws, g->n2_w,
-                                             g->n2_b, g->l2_b, so));
+    U2GNN_TRY(ln_params(dX2, c.Z2, c.mean2, c.rstd2, dF, dp, N, d, dp, ws, g->n2_w, g->n2_b, g->l2_b, so, plan, df));
     // FFN
     float *dH = W.take<float>(Np * ffp);
     {
@@ -468,12 +549,12 @@ int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
         gg.a.aux0 = c.Hd, gg.a.ld_aux = ffp, gg.a.p_drop = pd;
         U2GNN_TRY(gg.run(st, plan));
     }
-    U2GNN_TRY(wgrad(W, D, dF, dp, c.Hd, ffp, dp, ffp, g->l2_w, ff, blk_d, blk_ff, so));   // side (forked above)
+    U2GNN_TRY(wgrad(W, D, dF, dp, c.Hd, ffp, dp, ffp, g->l2_w, ff, blk_d, blk_ff, so, df));   // side (forked above)
     U2GNN_TRY(gemm_split(W, D, dH, w->W1, dX1, Np, dp, ffp, ffp, dp, dp, false, 1.f, true, nullptr, nullptr, false,
                          st));
     U2GNN_TRY(sd.fork());
-    U2GNN_TRY(wgrad(W, D, dH, ffp, c.X1, dp, ffp, dp, g->l1_w, d, blk_ff, blk_d, so));
-    U2GNN_TRY(bias_grad(W, dH, Np, ffp, ffp, ffp, ff, g->l1_b, so));
+    U2GNN_TRY(wgrad(W, D, dH, ffp, c.X1, dp, ffp, dp, g->l1_w, d, blk_ff, blk_d, so, df));
+    U2GNN_TRY(bias_grad(W, dH, Np, ffp, ffp, ffp, ff, g->l1_b, so, df));
     // LN1 backward -> dX (residual), dA (dropout1 branch); norm1 + out_proj.bias grads (side)
     float *dA = W.take<float>(Np * dp);
     // no input gradient wanted (first layer of the stack): LN1's residual half goes to scratch and
@@ -490,16 +571,14 @@ int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
         U2GNN_TRY(u2gnn_layernorm_bwd(dX1, dp, c.Z1, dp, c.mean1, c.rstd1, w->n1_w, dX, dp, dA, dp, pd, s->drop1, N,
                                       Np, d, dp, st));
     U2GNN_TRY(sd.fork());
-    if (!plan)
-        U2GNN_TRY(u2gnn_layernorm_bwd_params(dX1, dp, c.Z1, dp, c.mean1, c.rstd1, dA, dp, N, d, dp, ws, g->n1_w,
-                                             g->n1_b, g->out_b, so));
+    U2GNN_TRY(ln_params(dX1, c.Z1, c.mean1, c.rstd1, dA, dp, N, d, dp, ws, g->n1_w, g->n1_b, g->out_b, so, plan, df));
     // out-projection
     float *dO = W.take<float>(Np * dp);
     {
         G gg(dA, w->W_o, dO, Np, dp, dp, dp, dp, dp, prec);
         U2GNN_TRY(gg.run(st, plan));
     }
-    U2GNN_TRY(wgrad(W, D, dA, dp, c.O, dp, dp, dp, g->out_w, d, blk_d, blk_d, so));   // side (forked above)
+    U2GNN_TRY(wgrad(W, D, dA, dp, c.O, dp, dp, dp, g->out_w, d, blk_d, blk_d, so, df));   // side (forked above)
     // attention core
     const float *Q = c.QKV, *Kt = c.QKV + dp, *V = c.QKV + 2 * dp;
     const float q_scale = (float)(1.0 / std::sqrt((double)d));
@@ -516,7 +595,7 @@ int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
         // dV needs only Pd and dO: on the side stream it overlaps the dS -> dQ -> dK chain
         U2GNN_TRY(sd.fork());
         U2GNN_TRY(gemm_split(W, D, c.Pd, dO, dQKV + 2 * dp, Np, dp, Np, Np, dp, 3 * dp, true, 1.f, false, nullptr,
-                             nullptr, false, dv_side ? so : st, pd > 0.f, -1, U2GNN_ROLE_DV));
+                             nullptr, false, dv_side ? so : st, pd > 0.f, -1, U2GNN_ROLE_DV, nullptr, att));
         if (dv_side) U2GNN_TRY(sd.mark(&dv_done));
         float *delta = ln_delta ? delta_ln : W.take<float>(Np);
         if (!plan && !ln_delta) U2GNN_TRY(u2gnn_rowdot(dO, dp, c.O, dp, delta, Np, dp, st));
@@ -530,10 +609,11 @@ int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
             probe_mark(U2GNN_ROLE_DS, true, st, plan);
         }
         U2GNN_TRY(gemm_split(W, D, dS, Kt, dQKV, Np, dp, Np, Np, 3 * dp, 3 * dp, false, q_scale, false, nullptr, nullptr,
-                             false, st, false, D.prec_ab, U2GNN_ROLE_DQ));
+                             false, st, false, D.prec_ab, U2GNN_ROLE_DQ, nullptr, att));
         U2GNN_TRY(gemm_split(W, D, dS, Q, dQKV + dp, Np, dp, Np, Np, 3 * dp, 3 * dp, true, 1.f, false, nullptr,
-                             nullptr, false, st, false, D.prec_ab, U2GNN_ROLE_DK));
+                             nullptr, false, st, false, D.prec_ab, U2GNN_ROLE_DK, nullptr, att));
         U2GNN_TRY(sd.wait(dv_done));   // dV before dX += dQKV W_in
+        U2GNN_TRY(flush(att, W, st));
     }
     // in-projection
     if (need_dx)
@@ -545,8 +625,9 @@ int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
     const bool side_w = need_dx;   // 3.140-3.157 vs 3.171-3.194 ms per C4 step (4 pairs, one session)
     hipStream_t wst = side_w ? so : st;
     if (side_w) U2GNN_TRY(sd.fork());
-    U2GNN_TRY(wgrad(W, D, dQKV, 3 * dp, X, dp, 3 * dp, dp, g->in_w, d, blk_d, blk_d, wst));
-    U2GNN_TRY(bias_grad(W, dQKV, Np, 3 * dp, 3 * dp, dp, d, g->in_b, wst));
+    U2GNN_TRY(wgrad(W, D, dQKV, 3 * dp, X, dp, 3 * dp, dp, g->in_w, d, blk_d, blk_d, wst, df));
+    U2GNN_TRY(bias_grad(W, dQKV, Np, 3 * dp, 3 * dp, dp, d, g->in_b, wst, df));
+    U2GNN_TRY(flush(df, W, st));
     return (W.overflow || CA.overflow) ? U2GNN_E_ARG : U2GNN_OK;
 }
 

@@ -5,6 +5,8 @@
 #include "u2gnn_common.h"
 
 #include <algorithm>
+#include <cstring>
+#include <vector>
 
 namespace {
 
@@ -176,16 +178,16 @@ __device__ __forceinline__ float4 add4(float4 a, float4 b) { return make_float4(
 // One wave per padded row, a float4 of columns per lane; the slab loop keeps 4 independent
 // 16-byte loads in flight.  Rows/columns outside the real blocks are skipped; the real
 // destination is written with 16-byte stores when the column map is the identity and aligned.
-__global__ void __launch_bounds__(256) slab_reduce_kernel(const float *src, int n_slab, int64_t slab_stride,
-                                                          int64_t rows_pad, int64_t cols_pad, int64_t ld_src,
-                                                          int64_t rbp, int64_t rbr, int64_t cbp, int64_t cbr,
-                                                          float *dst, int64_t ld_dst, float alpha, int accumulate,
-                                                          int vec_store) {
+// The bodies of the reduction kernels take their block coordinates as arguments, so that the batched
+// launch (reduce_batch_kernel, u2gnn_reduce_batch) runs the very same per-element arithmetic.
+__device__ __forceinline__ void slab_reduce_body(const float *src, int n_slab, int64_t slab_stride, int64_t rows_pad,
+                                                 int64_t cols_pad, int64_t ld_src, int64_t rbp, int64_t rbr,
+                                                 int64_t cbp, int64_t cbr, float *dst, int64_t ld_dst, float alpha,
+                                                 int accumulate, int vec_store, int64_t i) {
     // one float4 of the output per thread (weight-gradient outputs have only d or ff rows: a wave per
     // row left the chip latency-bound); 8 slab loads in flight, summed in the fixed order
     // a += s0, s4, ...; b += s1, s5, ...; e += s2, ...; f += s3, ...; then (a + b) + (e + f)
     const int64_t c4 = cols_pad >> 2;
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= rows_pad * c4) return;
     const int64_t r = i / c4, c = (i - r * c4) * 4;
     bool vr;
@@ -226,6 +228,15 @@ __global__ void __launch_bounds__(256) slab_reduce_kernel(const float *src, int 
             *o = accumulate ? *o + alpha * x[q] : alpha * x[q];
         }
     }
+}
+
+__global__ void __launch_bounds__(256) slab_reduce_kernel(const float *src, int n_slab, int64_t slab_stride,
+                                                          int64_t rows_pad, int64_t cols_pad, int64_t ld_src,
+                                                          int64_t rbp, int64_t rbr, int64_t cbp, int64_t cbr,
+                                                          float *dst, int64_t ld_dst, float alpha, int accumulate,
+                                                          int vec_store) {
+    slab_reduce_body(src, n_slab, slab_stride, rows_pad, cols_pad, ld_src, rbp, rbr, cbp, cbr, dst, ld_dst, alpha,
+                     accumulate, vec_store, (int64_t)blockIdx.x * 256 + threadIdx.x);
 }
 
 __global__ void __launch_bounds__(256) pack_padded_kernel(const float *src, int64_t ld_src, int64_t rows_pad,
@@ -298,15 +309,15 @@ constexpr int CS_ROWS = 16;
 constexpr int64_t COLSUM_MAX_CHUNKS = 512;
 
 template <bool FOLD>
-__global__ void __launch_bounds__(256) colsum_partial_kernel(const float *X, int64_t rows, int64_t cols_pad,
-                                                             int64_t ld, int rep, float *ws) {
+__device__ __forceinline__ void colsum_partial_body(const float *X, int64_t rows, int64_t cols_pad, int64_t ld, int rep,
+                                                    float *ws, int bx, int by) {
     __shared__ float4 red[4][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int64_t c = ((int64_t)blockIdx.x * 64 + lane) * 4;
+    const int64_t c = ((int64_t)bx * 64 + lane) * 4;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     const int nrep = FOLD ? rep : 1;     // compile-time 1 unless folding: the C4 body stays straight-line
     for (int it = 0; it < nrep; ++it) {  // a chunk = rep consecutive CS_ROWS-row groups
-        const int64_t r0 = ((int64_t)blockIdx.y * nrep + it) * CS_ROWS + w * (CS_ROWS / 4);
+        const int64_t r0 = ((int64_t)by * nrep + it) * CS_ROWS + w * (CS_ROWS / 4);
         float4 v[CS_ROWS / 4];
 #pragma unroll
         for (int j = 0; j < CS_ROWS / 4; ++j)
@@ -317,8 +328,14 @@ __global__ void __launch_bounds__(256) colsum_partial_kernel(const float *X, int
     red[w][lane] = acc;
     __syncthreads();
     if (w == 0 && c < cols_pad)
-        *reinterpret_cast<float4 *>(ws + (int64_t)blockIdx.y * cols_pad + c) =
+        *reinterpret_cast<float4 *>(ws + (int64_t)by * cols_pad + c) =
             add4(add4(red[0][lane], red[1][lane]), add4(red[2][lane], red[3][lane]));
+}
+
+template <bool FOLD>
+__global__ void __launch_bounds__(256) colsum_partial_kernel(const float *X, int64_t rows, int64_t cols_pad,
+                                                             int64_t ld, int rep, float *ws) {
+    colsum_partial_body<FOLD>(X, rows, cols_pad, ld, rep, ws, blockIdx.x, blockIdx.y);
 }
 
 // the same partial sums for operands that are not float4-addressable (e.g. a column vector):
@@ -345,11 +362,11 @@ __global__ void __launch_bounds__(256) colsum_partial_scalar_kernel(const float 
 // 64 columns reads too slowly there), hence the bound.
 constexpr int64_t SMALL_ROWS = 512;
 
-__global__ void __launch_bounds__(1024) colsum_small_kernel(const float *X, int64_t rows, int64_t cols_pad, int64_t ld,
-                                                            int64_t cbp, int64_t cbr, float *out, int accumulate) {
+__device__ __forceinline__ void colsum_small_body(const float *X, int64_t rows, int64_t cols_pad, int64_t ld, int64_t cbp,
+                                                  int64_t cbr, float *out, int accumulate, int bx) {
     __shared__ float4 red[64][16];
     const int cg = threadIdx.x & 15, rl = threadIdx.x >> 4;
-    const int64_t c = ((int64_t)blockIdx.x * 16 + cg) * 4;
+    const int64_t c = ((int64_t)bx * 16 + cg) * 4;
     const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
     float4 a = z4, b = z4;
     if (c < cols_pad) {
@@ -377,15 +394,20 @@ __global__ void __launch_bounds__(1024) colsum_small_kernel(const float *X, int6
     }
 }
 
+__global__ void __launch_bounds__(1024) colsum_small_kernel(const float *X, int64_t rows, int64_t cols_pad, int64_t ld,
+                                                            int64_t cbp, int64_t cbr, float *out, int accumulate) {
+    colsum_small_body(X, rows, cols_pad, ld, cbp, cbr, out, accumulate, blockIdx.x);
+}
+
 // stage 2: block = 16 columns x 16 chunk strides (thread t: column t%16, chunks t/16, t/16+16, ...),
 // then a fixed-order LDS combine (deterministic).  ~cols/16 blocks keep the serial chain short.
 constexpr int FIN_COLS = 16;
 
-__global__ void __launch_bounds__(256) colsum_final_kernel(const float *ws, int64_t n_chunks, int64_t cols_pad,
-                                                           int64_t cbp, int64_t cbr, float *out, int accumulate) {
+__device__ __forceinline__ void colsum_final_body(const float *ws, int64_t n_chunks, int64_t cols_pad, int64_t cbp,
+                                                  int64_t cbr, float *out, int accumulate, int bx) {
     __shared__ float red[16][FIN_COLS + 1];
     const int cl = threadIdx.x % FIN_COLS, kg = threadIdx.x / FIN_COLS;
-    const int64_t c = (int64_t)blockIdx.x * FIN_COLS + cl;
+    const int64_t c = (int64_t)bx * FIN_COLS + cl;
     float s[2] = {0.f, 0.f};
     if (c < cols_pad) {
         // chunks kg, kg+16, kg+32, ... alternate between s[0] and s[1]; 8 loads in flight
@@ -413,6 +435,11 @@ __global__ void __launch_bounds__(256) colsum_final_kernel(const float *ws, int6
 #pragma unroll
     for (int j = 0; j < 16; ++j) t += red[j][cl];
     out[cc] = accumulate ? out[cc] + t : t;
+}
+
+__global__ void __launch_bounds__(256) colsum_final_kernel(const float *ws, int64_t n_chunks, int64_t cols_pad,
+                                                           int64_t cbp, int64_t cbr, float *out, int accumulate) {
+    colsum_final_body(ws, n_chunks, cols_pad, cbp, cbr, out, accumulate, blockIdx.x);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -831,18 +858,17 @@ __global__ void __launch_bounds__(256) layernorm_bwd_kernel(const float *dY, int
 // consecutive CS_ROWS-row groups so that token-sized inputs (neighbour mode, ~82K rows) leave few
 // enough chunks for ln_param_reduce's column-parallel combine (rep = 1 below 8K rows).
 template <bool FOLD>
-__global__ void __launch_bounds__(256) ln_colstats_kernel(const float *dY, int64_t ldy, const float *Z, int64_t ldz,
-                                                          const float *mean, const float *rstd, const float *dZd,
-                                                          int64_t lddrop, int64_t rows, int64_t d, int64_t d_pad,
-                                                          int rep, float *ws) {
+__device__ __forceinline__ void ln_colstats_body(const float *dY, int64_t ldy, const float *Z, int64_t ldz,
+                                                 const float *mean, const float *rstd, const float *dZd, int64_t lddrop,
+                                                 int64_t rows, int64_t d_pad, int rep, float *ws, int bx, int by) {
     __shared__ float4 red[4][3][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int64_t c = ((int64_t)blockIdx.x * 64 + lane) * 4;
+    const int64_t c = ((int64_t)bx * 64 + lane) * 4;
     const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
     float4 sg = z4, sb = z4, sd = z4;
     const int nrep = FOLD ? rep : 1;
     for (int it = 0; it < nrep && c < d_pad; ++it) {
-        const int64_t r0 = ((int64_t)blockIdx.y * nrep + it) * CS_ROWS + w * (CS_ROWS / 4);
+        const int64_t r0 = ((int64_t)by * nrep + it) * CS_ROWS + w * (CS_ROWS / 4);
         float4 dy[CS_ROWS / 4], zz[CS_ROWS / 4], dd[CS_ROWS / 4];
         float mu[CS_ROWS / 4], rs[CS_ROWS / 4];
 #pragma unroll
@@ -870,21 +896,30 @@ __global__ void __launch_bounds__(256) ln_colstats_kernel(const float *dY, int64
     red[w][2][lane] = sd;
     __syncthreads();
     if (w < 3 && c < d_pad)
-        *reinterpret_cast<float4 *>(ws + ((int64_t)blockIdx.y * 3 + w) * d_pad + c) =
+        *reinterpret_cast<float4 *>(ws + ((int64_t)by * 3 + w) * d_pad + c) =
             add4(add4(red[0][w][lane], red[1][w][lane]), add4(red[2][w][lane], red[3][w][lane]));
+}
+
+template <bool FOLD>
+__global__ void __launch_bounds__(256) ln_colstats_kernel(const float *dY, int64_t ldy, const float *Z, int64_t ldz,
+                                                          const float *mean, const float *rstd, const float *dZd,
+                                                          int64_t lddrop, int64_t rows, int64_t d, int64_t d_pad,
+                                                          int rep, float *ws) {
+    (void)d;
+    ln_colstats_body<FOLD>(dY, ldy, Z, ldz, mean, rstd, dZd, lddrop, rows, d_pad, rep, ws, blockIdx.x, blockIdx.y);
 }
 
 constexpr int64_t LN_MAX_CHUNKS = 512;
 
 // single-launch LN parameter gradients for short inputs (rows <= SMALL_ROWS), the layout of
 // colsum_small_kernel with three sums (dY * xhat, dY, dZd)
-__global__ void __launch_bounds__(1024) ln_params_small_kernel(const float *dY, int64_t ldy, const float *Z, int64_t ldz,
-                                                               const float *mean, const float *rstd, const float *dZd,
-                                                               int64_t lddrop, int64_t rows, int64_t d, int64_t d_pad,
-                                                               float *dgamma, float *dbeta, float *dbias) {
+__device__ __forceinline__ void ln_params_small_body(const float *dY, int64_t ldy, const float *Z, int64_t ldz,
+                                                     const float *mean, const float *rstd, const float *dZd,
+                                                     int64_t lddrop, int64_t rows, int64_t d, int64_t d_pad,
+                                                     float *dgamma, float *dbeta, float *dbias, int bx) {
     __shared__ float4 red[3][64][16];
     const int cg = threadIdx.x & 15, rl = threadIdx.x >> 4;
-    const int64_t c = ((int64_t)blockIdx.x * 16 + cg) * 4;
+    const int64_t c = ((int64_t)bx * 16 + cg) * 4;
     const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
     float4 sg = z4, sb = z4, sd = z4;
     if (c < d_pad) {
@@ -923,12 +958,19 @@ __global__ void __launch_bounds__(1024) ln_params_small_kernel(const float *dY, 
     }
 }
 
+__global__ void __launch_bounds__(1024) ln_params_small_kernel(const float *dY, int64_t ldy, const float *Z, int64_t ldz,
+                                                               const float *mean, const float *rstd, const float *dZd,
+                                                               int64_t lddrop, int64_t rows, int64_t d, int64_t d_pad,
+                                                               float *dgamma, float *dbeta, float *dbias) {
+    ln_params_small_body(dY, ldy, Z, ldz, mean, rstd, dZd, lddrop, rows, d, d_pad, dgamma, dbeta, dbias, blockIdx.x);
+}
+
 // block = 16 columns x 16 chunk strides (as colsum_final), fixed-order LDS combine
-__global__ void __launch_bounds__(256) ln_param_reduce_kernel(const float *ws, int64_t n_chunks, int64_t d,
-                                                              int64_t d_pad, float *dgamma, float *dbeta, float *dbias) {
+__device__ __forceinline__ void ln_param_reduce_body(const float *ws, int64_t n_chunks, int64_t d, int64_t d_pad,
+                                                     float *dgamma, float *dbeta, float *dbias, int bx) {
     __shared__ float red[3][16][FIN_COLS + 1];
     const int cl = threadIdx.x % FIN_COLS, kg = threadIdx.x / FIN_COLS;
-    const int64_t c = (int64_t)blockIdx.x * FIN_COLS + cl;
+    const int64_t c = (int64_t)bx * FIN_COLS + cl;
     float a = 0.f, b = 0.f, e = 0.f;
     if (c < d) {
         int64_t k = kg;
@@ -964,6 +1006,70 @@ __global__ void __launch_bounds__(256) ln_param_reduce_kernel(const float *ws, i
     dgamma[c] = t[0];
     dbeta[c] = t[1];
     if (dbias) dbias[c] = t[2];
+}
+
+__global__ void __launch_bounds__(256) ln_param_reduce_kernel(const float *ws, int64_t n_chunks, int64_t d,
+                                                              int64_t d_pad, float *dgamma, float *dbeta, float *dbias) {
+    ln_param_reduce_body(ws, n_chunks, d, d_pad, dgamma, dbeta, dbias, blockIdx.x);
+}
+
+// ------------------------------------------------------------------------------------------
+// batched reductions (u2gnn_reduce_batch): the jobs of one launch travel by value in the kernel
+// arguments; a block finds its job by walking the per-job block counts (uniform, scalar) and runs
+// that job's body with its own block coordinates.  Latency-bound layers (C5: ~4.6 us per launch of
+// a few-KB reduction) issue a layer's 8-12 reductions as 2 launches.
+// ------------------------------------------------------------------------------------------
+enum RbKind : int32_t { RB_SLAB, RB_CS_PART, RB_CS_FINAL, RB_CS_SMALL, RB_LN_PART, RB_LN_FINAL, RB_LN_SMALL };
+constexpr int RB_MAX = 12;
+struct RbJob {
+    int32_t kind, nblk, nbx, n;   // n: slab count / fold rep / chunk count
+    int32_t flag, vec;            // accumulate; vectorised slab store
+    float alpha;
+    const float *src, *Z, *mean, *rstd, *dZd;
+    float *o0, *o1, *o2, *ws;
+    int64_t ld_src, stride, rows, cols, d, rbp, rbr, cbp, cbr, ld_dst, ldz, lddrop;
+};
+struct RbBatch {
+    RbJob j[RB_MAX];
+    int32_t n;
+};
+
+template <int NT>
+__global__ void __launch_bounds__(NT) reduce_batch_kernel(RbBatch B) {
+    int bid = blockIdx.x, j = 0;
+    while (j + 1 < B.n && bid >= B.j[j].nblk) bid -= B.j[j++].nblk;
+    const RbJob &J = B.j[j];
+    if constexpr (NT == 256) {
+        switch (J.kind) {
+            case RB_SLAB:
+                slab_reduce_body(J.src, J.n, J.stride, J.rows, J.cols, J.ld_src, J.rbp, J.rbr, J.cbp, J.cbr, J.o0,
+                                 J.ld_dst, J.alpha, J.flag, J.vec, (int64_t)bid * 256 + threadIdx.x);
+                break;
+            case RB_CS_PART:
+                colsum_partial_body<true>(J.src, J.rows, J.cols, J.ld_src, J.n, J.ws, bid % J.nbx, bid / J.nbx);
+                break;
+            case RB_CS_FINAL: colsum_final_body(J.ws, J.n, J.cols, J.cbp, J.cbr, J.o0, J.flag, bid); break;
+            case RB_LN_PART:
+                ln_colstats_body<true>(J.src, J.ld_src, J.Z, J.ldz, J.mean, J.rstd, J.dZd, J.lddrop, J.rows, J.cols, J.n,
+                                       J.ws, bid % J.nbx, bid / J.nbx);
+                break;
+            case RB_LN_FINAL: ln_param_reduce_body(J.ws, J.n, J.d, J.cols, J.o0, J.o1, J.o2, bid); break;
+            default: break;
+        }
+    } else {
+        switch (J.kind) {
+            case RB_SLAB:
+                slab_reduce_body(J.src, J.n, J.stride, J.rows, J.cols, J.ld_src, J.rbp, J.rbr, J.cbp, J.cbr, J.o0,
+                                 J.ld_dst, J.alpha, J.flag, J.vec, (int64_t)bid * NT + threadIdx.x);
+                break;
+            case RB_CS_SMALL: colsum_small_body(J.src, J.rows, J.cols, J.ld_src, J.cbp, J.cbr, J.o0, J.flag, bid); break;
+            case RB_LN_SMALL:
+                ln_params_small_body(J.src, J.ld_src, J.Z, J.ldz, J.mean, J.rstd, J.dZd, J.lddrop, J.rows, J.d, J.cols,
+                                     J.o0, J.o1, J.o2, bid);
+                break;
+            default: break;
+        }
+    }
 }
 
 __global__ void __launch_bounds__(256) dropout_mask_kernel(uint64_t seed, const uint64_t *seed_epoch, int64_t rows, int64_t cols, float p,
@@ -1299,6 +1405,157 @@ int u2gnn_layernorm_bwd_params(const float *dY, int64_t ldy, const float *Z, int
                        chunks, d, d_pad,
                        dgamma, dbeta, dbias);
     return u2gnn_launch_status();
+}
+
+}  // extern "C"
+
+namespace {
+
+// the launch geometry of one public job, exactly as its single-job entry point chooses it
+struct RbPlan {
+    bool small;            // one-launch small form (1024 threads)
+    int64_t chunks;        // partial rows (COLSUM / LNPARAMS, long form)
+    int rep;               // fold factor of the partial pass
+    int64_t ws_floats;     // partial sums (long form)
+};
+
+// ptrs = false: shapes only (the layer executor sizes its workspace before any buffer exists)
+int rb_plan(const u2gnn_reduce_job &J, RbPlan &p, bool ptrs = true) {
+    p = RbPlan{false, 0, 1, 0};
+    switch (J.kind) {
+        case U2GNN_RJOB_SLAB:
+            if (J.n_slab < 1 || J.rblk_pad < 1 || J.cblk_pad < 1 || J.rows < 0 || J.cols < 0) return U2GNN_E_ARG;
+            if (!ptrs) return U2GNN_OK;
+            if (!J.src || !J.dst) return U2GNN_E_ARG;
+            if (!al16(J.src) || (J.cols & 3) || (J.ld_src & 3) || (J.slab_stride & 3)) return U2GNN_E_ALIGN;
+            return U2GNN_OK;
+        case U2GNN_RJOB_COLSUM: {   // u2gnn_colsum, vectorised forms only
+            if (J.cblk_pad < 1 || J.rows < 0 || J.cols < 0) return U2GNN_E_ARG;
+            if (ptrs && (!J.src || !J.dst)) return U2GNN_E_ARG;
+            if ((ptrs && !al16(J.src)) || (J.ld_src & 3) || (J.cols & 3)) return U2GNN_E_ALIGN;
+            p.small = J.rows <= SMALL_ROWS;
+            int64_t chunks = (J.rows + CS_ROWS - 1) / CS_ROWS;
+            p.rep = (int)std::max<int64_t>(1, (chunks + COLSUM_MAX_CHUNKS - 1) / COLSUM_MAX_CHUNKS);
+            chunks = (chunks + p.rep - 1) / p.rep;
+            p.chunks = chunks > 0 ? chunks : 1;
+            if (!p.small) p.ws_floats = (p.chunks * J.cols + 3) / 4 * 4;
+            return U2GNN_OK;
+        }
+        case U2GNN_RJOB_LNPARAMS: {   // u2gnn_layernorm_bwd_params
+            if (J.d < 1 || J.d > J.cols) return U2GNN_E_ARG;
+            if (ptrs) {
+                if (!J.src || !J.Z || !J.mean || !J.rstd || !J.dst || !J.dbeta) return U2GNN_E_ARG;
+                if (J.dbias && !J.dZdrop) return U2GNN_E_ARG;
+                if (!al16(J.src) || !al16(J.Z) || (J.dbias && !al16(J.dZdrop))) return U2GNN_E_ALIGN;
+            }
+            if ((J.ld_src & 3) || (J.ldz & 3) || (J.cols & 3) || (J.dbias && (J.lddrop & 3))) return U2GNN_E_ALIGN;
+            p.small = J.rows <= SMALL_ROWS;
+            const int64_t groups = J.rows > 0 ? (J.rows + CS_ROWS - 1) / CS_ROWS : 1;
+            p.rep = (int)((groups + LN_MAX_CHUNKS - 1) / LN_MAX_CHUNKS);
+            p.chunks = (groups + p.rep - 1) / p.rep;
+            if (!p.small) p.ws_floats = p.chunks * 3 * J.cols;
+            return U2GNN_OK;
+        }
+        default: return U2GNN_E_ARG;
+    }
+}
+
+template <int NT>
+int rb_launch(std::vector<RbJob> &jobs, hipStream_t st) {
+    for (size_t o = 0; o < jobs.size(); o += RB_MAX) {
+        RbBatch B;
+        std::memset(&B, 0, sizeof(B));
+        B.n = (int32_t)std::min<size_t>(RB_MAX, jobs.size() - o);
+        int64_t blocks = 0;
+        for (int i = 0; i < B.n; ++i) B.j[i] = jobs[o + i], blocks += B.j[i].nblk;
+        if (blocks <= 0) continue;
+        if (blocks >= (int64_t)1 << 31) return U2GNN_E_SHAPE;
+        hipLaunchKernelGGL(reduce_batch_kernel<NT>, dim3((unsigned)blocks), dim3(NT), 0, st, B);
+    }
+    return u2gnn_launch_status();
+}
+
+}  // namespace
+
+extern "C" {
+
+int64_t u2gnn_reduce_batch_ws_floats(const u2gnn_reduce_job *jobs, int32_t n) {
+    if (n < 0 || (n && !jobs)) return -1;
+    int64_t tot = 0;
+    for (int32_t i = 0; i < n; ++i) {
+        RbPlan p;
+        if (rb_plan(jobs[i], p, false) != U2GNN_OK) return -1;
+        tot += p.ws_floats;
+    }
+    return tot;
+}
+
+int u2gnn_reduce_batch(const u2gnn_reduce_job *jobs, int32_t n, float *ws, int64_t ws_floats, void *stream) {
+    if (n < 0 || (n && !jobs)) return U2GNN_E_ARG;
+    if (ws && !al16(ws)) return U2GNN_E_ALIGN;
+    std::vector<RbJob> part, fin, small;
+    std::vector<const u2gnn_reduce_job *> slabs;
+    int64_t off = 0;
+    for (int32_t i = 0; i < n; ++i) {
+        const u2gnn_reduce_job &J = jobs[i];
+        RbPlan p;
+        const int rc = rb_plan(J, p);
+        if (rc != U2GNN_OK) return rc;
+        if (J.kind == U2GNN_RJOB_SLAB) {
+            if (J.rows > 0 && J.cols > 0) slabs.push_back(&J);
+            continue;
+        }
+        RbJob r;
+        std::memset(&r, 0, sizeof(r));
+        r.src = J.src, r.ld_src = J.ld_src, r.rows = J.rows, r.cols = J.cols, r.flag = J.accumulate;
+        r.cbp = J.cblk_pad, r.cbr = J.cblk_real, r.o0 = J.dst;
+        const bool ln = J.kind == U2GNN_RJOB_LNPARAMS;
+        if (ln) {
+            r.Z = J.Z, r.ldz = J.ldz, r.mean = J.mean, r.rstd = J.rstd, r.dZd = J.dbias ? J.dZdrop : nullptr;
+            r.lddrop = J.lddrop, r.d = J.d, r.o1 = J.dbeta, r.o2 = J.dbias;
+        } else if (J.cols == 0) {
+            continue;   // u2gnn_colsum: nothing to sum
+        }
+        if (p.small) {
+            r.kind = ln ? RB_LN_SMALL : RB_CS_SMALL;
+            r.nblk = (int32_t)((J.cols + 63) / 64);
+            small.push_back(r);
+            continue;
+        }
+        if (!ws || off + p.ws_floats > ws_floats) return U2GNN_E_ARG;
+        r.ws = ws + off;
+        off += p.ws_floats;
+        RbJob q = r;
+        q.kind = ln ? RB_LN_PART : RB_CS_PART;
+        q.nbx = (int32_t)((J.cols + 255) / 256);
+        q.nblk = q.nbx * (int32_t)p.chunks;
+        q.n = p.rep;
+        part.push_back(q);
+        r.kind = ln ? RB_LN_FINAL : RB_CS_FINAL;
+        r.nblk = (int32_t)(((ln ? J.d : J.cols) + FIN_COLS - 1) / FIN_COLS);
+        r.n = (int32_t)p.chunks;
+        fin.push_back(r);
+    }
+    // slab jobs ride with the small jobs' launch when there is one (per-thread bodies: any block size)
+    const int slab_nt = small.empty() ? 256 : 1024;
+    for (const u2gnn_reduce_job *J : slabs) {
+        RbJob r;
+        std::memset(&r, 0, sizeof(r));
+        r.kind = RB_SLAB;
+        r.src = J->src, r.n = J->n_slab, r.stride = J->slab_stride, r.rows = J->rows, r.cols = J->cols;
+        r.ld_src = J->ld_src, r.rbp = J->rblk_pad, r.rbr = J->rblk_real, r.cbp = J->cblk_pad, r.cbr = J->cblk_real;
+        r.o0 = J->dst, r.ld_dst = J->ld_dst, r.alpha = J->alpha, r.flag = J->accumulate;
+        r.vec = J->cblk_pad == J->cblk_real && al16(J->dst) && (J->ld_dst & 3) == 0;
+        const int64_t nb = (J->rows * (J->cols / 4) + slab_nt - 1) / slab_nt;
+        if (nb >= (int64_t)1 << 31) return U2GNN_E_SHAPE;
+        r.nblk = (int32_t)nb;
+        (small.empty() ? fin : small).push_back(r);
+    }
+    hipStream_t st = u2gnn_stream(stream);
+    int rc = rb_launch<256>(part, st);
+    if (rc == U2GNN_OK) rc = rb_launch<256>(fin, st);
+    if (rc == U2GNN_OK) rc = rb_launch<1024>(small, st);
+    return rc;
 }
 
 int u2gnn_dropout(const float *X, int64_t ldx, float *Y, int64_t ldy, int64_t rows, int64_t cols, float p,

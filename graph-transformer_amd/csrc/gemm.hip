@@ -318,11 +318,10 @@ __device__ __forceinline__ bf16x8 ld_frag(const __bf16 *img, int r0, int ks, int
     }
 }
 
+// The main loop and epilogue of one output tile (tile coordinates from the caller: the plain launch's
+// XCD-aware map, or the grouped launch's job walk).
 template <int BM, int BN, int WM, int WN, int BK, bool TA, bool TB, int EPI, bool SPLIT, bool CLAMP>
-__global__ void __launch_bounds__(64 * WM * WN) gemm_bf16_kernel(GemmP P) {
-    if constexpr (EPI == U2GNN_EPI_BIAS_DROP_RESID || EPI == U2GNN_EPI_BIAS_RELU_DROP || EPI == U2GNN_EPI_ATTN_DS_RECOMP ||
-                  EPI == U2GNN_EPI_BIAS_DROP_RESID_LN)
-        P.seed = u2gnn_seed(P.seed, P.epoch);   // graph replay: device-resident seed epoch
+__device__ __forceinline__ void gemm_bf16_body(const GemmP &P, int tmi, int tni, int zi) {
     constexpr int NT = 64 * WM * WN;
     constexpr int LDK = BK + 8;
     constexpr int WTM = BM / WM, WTN = BN / WN;
@@ -334,9 +333,6 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_bf16_kernel(GemmP P) {
     __shared__ __attribute__((aligned(16))) __bf16 smem[2 * STAGE];
 
     const int tid = threadIdx.x;
-    int tmi, tni;
-    int zi;
-    tile_coords(P.gm, P.gn, tmi, tni, zi);
     const int m0 = tmi * BM, n0 = tni * BN;
     const int64_t kbase = (int64_t)zi * P.K;
     const int64_t klen = min((int64_t)P.K, (int64_t)P.Ktot - kbase);
@@ -428,6 +424,37 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_bf16_kernel(GemmP P) {
 
     store_tile<EPI>(P, P.C + (int64_t)zi * P.slab_stride, acc, m0 + wm * WTM, n0 + wn * WTN, li, kh,
                     use_pre ? &pre : nullptr);
+}
+
+template <int BM, int BN, int WM, int WN, int BK, bool TA, bool TB, int EPI, bool SPLIT, bool CLAMP>
+__global__ void __launch_bounds__(64 * WM * WN) gemm_bf16_kernel(GemmP P) {
+    if constexpr (EPI == U2GNN_EPI_BIAS_DROP_RESID || EPI == U2GNN_EPI_BIAS_RELU_DROP || EPI == U2GNN_EPI_ATTN_DS_RECOMP ||
+                  EPI == U2GNN_EPI_BIAS_DROP_RESID_LN)
+        P.seed = u2gnn_seed(P.seed, P.epoch);   // graph replay: device-resident seed epoch
+    int tmi, tni, zi;
+    tile_coords(P.gm, P.gn, tmi, tni, zi);
+    gemm_bf16_body<BM, BN, WM, WN, BK, TA, TB, EPI, SPLIT, CLAMP>(P, tmi, tni, zi);
+}
+
+// Grouped launch (u2gnn_gemm_group): several STORE products that share one kernel configuration.  The
+// XCD-aware logical id runs over the whole grid; job j owns ids [start[j], start[j+1]) and maps its
+// local id to a tile exactly as its own launch would (same tile arithmetic, hence the same bits).
+constexpr int GG_MAX = 8;
+struct GemmGroup {
+    GemmP p[GG_MAX];
+    int32_t start[GG_MAX + 1];
+    int32_t n;
+};
+
+template <int BM, int BN, int WM, int WN, int BK, bool TA, bool TB, bool SPLIT>
+__global__ void __launch_bounds__(64 * WM * WN) gemm_bf16_group_kernel(GemmGroup G) {
+    const int w = xcd_wgid();
+    int j = 0;
+    while (j + 1 < G.n && w >= G.start[j + 1]) ++j;
+    const GemmP &P = G.p[j];
+    int tmi, tni, zi;
+    tile_of(P.gm, P.gn, w - G.start[j], tmi, tni, zi);
+    gemm_bf16_body<BM, BN, WM, WN, BK, TA, TB, U2GNN_EPI_STORE, SPLIT, false>(P, tmi, tni, zi);
 }
 
 // bf16 K-step variants: 0 = BK 32 (2 blocks/CU at 128x128), 1 = BK 16 (40 KB LDS, 140-152
@@ -528,7 +555,16 @@ __attribute__((weak)) int u2gnn_gemm_x2_dispatch(const u2gnn_gemm_args *a, GemmP
 __attribute__((weak)) int u2gnn_gemm_x3_dispatch(const u2gnn_gemm_args *a, GemmP &P, int tile, int split,
                                                  hipStream_t st);
 
-extern "C" int u2gnn_gemm(const u2gnn_gemm_args *a, void *stream) {
+namespace {
+
+// validated launch description of one u2gnn_gemm call
+struct GemmPlan {
+    GemmP P;
+    int tile, split, prec, epi;
+    bool ta, tb, clamp, x2;
+};
+
+int gemm_plan(const u2gnn_gemm_args *a, GemmPlan &G) {
     if (!a) return U2GNN_E_ARG;
     const bool x2 = a->a_x2 || a->b_x2;
     if (x2 && (!u2gnn_gemm_x2_dispatch || !u2gnn_gemm_x3_dispatch)) return U2GNN_E_ARG;   // not this build
@@ -668,12 +704,76 @@ extern "C" int u2gnn_gemm(const u2gnn_gemm_args *a, void *stream) {
         P.ln_rows = (int32_t)a->ln_rows;
         P.ln_eps = a->ln_eps;
     }
+    G.P = P;
+    G.tile = tile, G.split = split, G.prec = prec, G.epi = e;
+    G.ta = a->trans_a != 0, G.tb = a->trans_b != 0, G.clamp = a->clamp_a != 0, G.x2 = x2;
+    return U2GNN_OK;
+}
+
+int gemm_launch(const u2gnn_gemm_args *a, GemmPlan &G, hipStream_t st) {
+    if (G.x2 && (G.tile == 300 || G.tile == 301)) return u2gnn_gemm_x3_dispatch(a, G.P, G.tile, G.split, st);
+    if (G.x2) return u2gnn_gemm_x2_dispatch(a, G.P, G.tile, G.split, st);
+    if (G.prec == U2GNN_PREC_BF16X3)
+        return launch_tile<U2GNN_PREC_BF16X3>(G.P, G.tile, G.ta, G.tb, G.epi, G.split, G.clamp, st);
+    if (G.prec == U2GNN_PREC_BF16)
+        return launch_tile<U2GNN_PREC_BF16>(G.P, G.tile, G.ta, G.tb, G.epi, G.split, G.clamp, st);
+    return launch_tile<U2GNN_PREC_F32>(G.P, G.tile, G.ta, G.tb, G.epi, G.split, G.clamp, st);
+}
+
+// the grouped kernels: the weight-gradient tiles (64 and the 16-deep 128), A^T B, STORE
+template <int KIND>
+int launch_group(GemmGroup &GG, int tile, int blocks, hipStream_t st) {
+    constexpr bool SPLIT = KIND == U2GNN_PREC_BF16X3;
+    if (tile == 64)
+        hipLaunchKernelGGL((gemm_bf16_group_kernel<64, 64, 2, 2, 32, true, false, SPLIT>), dim3(blocks), dim3(256), 0,
+                           st, GG);
+    else
+        hipLaunchKernelGGL((gemm_bf16_group_kernel<128, 128, 2, 2, 16, true, false, SPLIT>), dim3(blocks), dim3(256),
+                           0, st, GG);
+    return u2gnn_launch_status();
+}
+
+}  // namespace
+
+extern "C" int u2gnn_gemm(const u2gnn_gemm_args *a, void *stream) {
+    GemmPlan G;
+    const int rc = gemm_plan(a, G);
+    if (rc != U2GNN_OK) return rc;
+    return gemm_launch(a, G, u2gnn_stream(stream));
+}
+
+extern "C" int u2gnn_gemm_group(const u2gnn_gemm_args *args, int32_t n, void *stream) {
+    if (n < 0 || n > GG_MAX || (n && !args)) return U2GNN_E_ARG;
     hipStream_t st = u2gnn_stream(stream);
-    if (x2 && (tile == 300 || tile == 301)) return u2gnn_gemm_x3_dispatch(a, P, tile, split, st);
-    if (x2) return u2gnn_gemm_x2_dispatch(a, P, tile, split, st);
-    const bool ta = a->trans_a != 0, tb = a->trans_b != 0;
-    const bool clamp = a->clamp_a != 0;
-    if (prec == U2GNN_PREC_BF16X3) return launch_tile<U2GNN_PREC_BF16X3>(P, tile, ta, tb, e, split, clamp, st);
-    if (prec == U2GNN_PREC_BF16) return launch_tile<U2GNN_PREC_BF16>(P, tile, ta, tb, e, split, clamp, st);
-    return launch_tile<U2GNN_PREC_F32>(P, tile, ta, tb, e, split, clamp, st);
+    GemmPlan G[GG_MAX];
+    for (int32_t i = 0; i < n; ++i) {
+        const int rc = gemm_plan(&args[i], G[i]);
+        if (rc != U2GNN_OK) return rc;
+    }
+    // one launch when every job runs the same grouped kernel
+    bool same = n > 1;
+    for (int32_t i = 0; i < n && same; ++i)
+        same = !G[i].x2 && G[i].prec == G[0].prec && G[i].prec != U2GNN_PREC_F32 && G[i].tile == G[0].tile &&
+               (G[i].tile == 64 || G[i].tile == 129) && G[i].ta && !G[i].tb && G[i].epi == U2GNN_EPI_STORE &&
+               !G[i].clamp;
+    if (!same) {
+        for (int32_t i = 0; i < n; ++i) {
+            const int rc = gemm_launch(&args[i], G[i], st);
+            if (rc != U2GNN_OK) return rc;
+        }
+        return U2GNN_OK;
+    }
+    GemmGroup GG;
+    std::memset(&GG, 0, sizeof(GG));
+    GG.n = n;
+    int64_t blocks = 0;
+    for (int32_t i = 0; i < n; ++i) {
+        GG.p[i] = G[i].P;
+        GG.start[i] = (int32_t)blocks;
+        blocks += (int64_t)G[i].P.gm * G[i].P.gn * G[i].split;
+    }
+    if (blocks >= ((int64_t)1 << 31)) return U2GNN_E_SHAPE;
+    GG.start[n] = (int32_t)blocks;
+    if (G[0].prec == U2GNN_PREC_BF16X3) return launch_group<U2GNN_PREC_BF16X3>(GG, G[0].tile, (int)blocks, st);
+    return launch_group<U2GNN_PREC_BF16>(GG, G[0].tile, (int)blocks, st);
 }

@@ -473,12 +473,16 @@ __device__ __forceinline__ void store_tile(const GemmP &P, float *C, const f32x1
 // group.  Blocks that share an A row-panel or a B column-panel of the same K range therefore run
 // on the same XCD (one L2), and the large N^2 operands of the skinny attention products are
 // fetched from HBM once.
-__device__ __forceinline__ void tile_coords(int gm, int gn, int &tm, int &tn, int &z) {
-    const int ntile = gm * gn;
+__device__ __forceinline__ int xcd_wgid() {
     const int bid = blockIdx.x;
     const int total = (int)gridDim.x;
     const int q = total >> 3, r = total & 7, xcd = bid & 7, loc = bid >> 3;
-    const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+}
+
+// logical id -> (row tile, column tile, split) of a gm x gn grid
+__device__ __forceinline__ void tile_of(int gm, int gn, int wgid, int &tm, int &tn, int &z) {
+    const int ntile = gm * gn;
     z = wgid / ntile;
     const int t = wgid - z * ntile;
     constexpr int GROUP = 8;
@@ -489,5 +493,9 @@ __device__ __forceinline__ void tile_coords(int gm, int gn, int &tm, int &tn, in
     const int in_g = t - g * per_group;
     tm = first_m + in_g % gsz;
     tn = in_g / gsz;
+}
+
+__device__ __forceinline__ void tile_coords(int gm, int gn, int &tm, int &tn, int &z) {
+    tile_of(gm, gn, xcd_wgid(), tm, tn, z);
 }
 }  // namespace

@@ -32,7 +32,7 @@ ERRORS = {-1: "bad argument", -2: "misaligned pointer / leading dimension", -3: 
 
 EPI_STORE, EPI_BIAS, EPI_BIAS_DROP_RESID, EPI_BIAS_RELU_DROP, EPI_RELU_DROP_BWD, EPI_ACCUM, EPI_ATTN_DS, \
     EPI_ATTN_DS_SIGNED, EPI_ATTN_DS_RECOMP, EPI_BIAS_DROP_RESID_LN, EPI_STORE_ROWDOT, EPI_STORE_ROWSTAT = range(12)
-ABI_VERSION = 10   # include/u2gnn_hip.h U2GNN_ABI_VERSION
+ABI_VERSION = 11   # include/u2gnn_hip.h U2GNN_ABI_VERSION
 PREC_F32, PREC_BF16X3, PREC_BF16 = 0, 1, 2
 
 
@@ -74,6 +74,18 @@ class PackDesc(ctypes.Structure):
                 ("cblk_real", c_int64), ("ld_dst", c_int64)]
 
 
+class ReduceJob(ctypes.Structure):   # u2gnn_reduce_job (ABI v11)
+    _fields_ = [("kind", c_int32), ("n_slab", c_int32), ("accumulate", c_int32), ("alpha", c_float),
+                ("src", c_void_p), ("ld_src", c_int64), ("slab_stride", c_int64), ("rows", c_int64),
+                ("cols", c_int64), ("d", c_int64), ("rblk_pad", c_int64), ("rblk_real", c_int64),
+                ("cblk_pad", c_int64), ("cblk_real", c_int64), ("dst", c_void_p), ("ld_dst", c_int64),
+                ("Z", c_void_p), ("mean", c_void_p), ("rstd", c_void_p), ("dZdrop", c_void_p), ("ldz", c_int64),
+                ("lddrop", c_int64), ("dbeta", c_void_p), ("dbias", c_void_p)]
+
+
+RJOB_SLAB, RJOB_COLSUM, RJOB_LNPARAMS = 0, 1, 2
+
+
 class LayerDims(ctypes.Structure):
     _fields_ = [("N", c_int64), ("d", c_int64), ("ff", c_int64), ("precision", c_int32), ("flags", c_int32),
                 ("window", c_int32), ("reserved", c_int32)]
@@ -107,6 +119,9 @@ _HIP_SIGS = {
     "u2gnn_gather_rows": ([VP, I64, I64, VP, I64, VP, I64, I64, I64, I64, I64, VP, VP], c_int32),
     "u2gnn_scatter_add_rows": ([VP, I64, VP, I64, VP, I64, I64, I64, I64, VP, VP], c_int32),
     "u2gnn_gemm": ([POINTER(GemmArgs), VP], c_int32),
+    "u2gnn_gemm_group": ([POINTER(GemmArgs), I32, VP], c_int32),
+    "u2gnn_reduce_batch_ws_floats": ([POINTER(ReduceJob), I32], I64),
+    "u2gnn_reduce_batch": ([POINTER(ReduceJob), I32, VP, I64, VP], c_int32),
     "u2gnn_window_attn_fwd": ([VP, I64, I32, I32, VP, I64, VP, F32, c_uint64, I64, I64, VP], c_int32),
     "u2gnn_window_attn_bwd": ([VP, I64, I32, I32, VP, I64, VP, F32, c_uint64, F32, VP, I64, I64, I64, VP], c_int32),
     "u2gnn_layer_sizes": ([POINTER(LayerDims), F32, POINTER(c_int64), POINTER(c_int64), POINTER(c_int64)], c_int32),

@@ -83,15 +83,43 @@ def gemm(A, B, C, M, N, K, lda, ldb, ldc, trans_a=False, trans_b=False, epilogue
     (gamma, beta, Y, ldy, mean, rstd, d, rows, eps): the EPI_BIAS_DROP_RESID_LN LayerNorm (N == 64).
     ``rowpart`` [N/64, >= M]: the EPI_STORE_ROWDOT row partials (ABI v8).  A 2-D ``rowvec`` [P, >= M]
     gives ATTN_DS_SIGNED the sum of its P partials per row (in row order of ``rowvec``)."""
-    _dev(A, B, C, Cx2, rowstat)
-    x2 = A.dtype == torch.bfloat16
-    if x2 != (B.dtype == torch.bfloat16):
-        raise _lib.U2GNNNativeError("x2 GEMM: both operands must be pre-split (bfloat16) or neither")
     rec = REC.enabled and flops is not None
     if rec:
         ev0 = torch.cuda.Event(enable_timing=True)
         ev1 = torch.cuda.Event(enable_timing=True)
         ev0.record()
+    a, x2 = _gemm_args(A, B, C, M, N, K, lda, ldb, ldc, trans_a, trans_b, epilogue, split_k, slab_stride, bias, aux0,
+                       aux1, rowvec, ld_aux, alpha, scale_cols, p_drop, seed, precision, tile, keep, clamp_a, Cx2, ldcx2,
+                       rowstat, m_valid, n_valid, ln, rowpart)
+    # pre-split operands exist only in the experiments library (x2_lib); the product library rejects them
+    check((_lib.x2_lib() if x2 else hip_lib()).u2gnn_gemm(ctypes.byref(a), _s()), "u2gnn_gemm")
+    if rec:
+        ev1.record()
+        REC.records.append((gemm_symbol(precision, M, N, split_k, tile, trans_a, trans_b, epilogue, clamp_a, x2),
+                            float(flops), ev0, ev1))
+
+
+def gemm_group(calls):
+    """Several gemm() calls (each a dict of gemm's keyword arguments; STORE products) in one launch when
+    they share a kernel configuration (u2gnn_gemm_group, ABI v11); bit-identical to the separate calls."""
+    arr = (_lib.GemmArgs * len(calls))()
+    for i, kw in enumerate(calls):
+        kw = dict(kw)
+        kw.pop("flops", None)
+        arr[i], x2 = _gemm_args(**kw)
+        if x2:
+            raise _lib.U2GNNNativeError("gemm_group: pre-split operands are not supported")
+    check(hip_lib().u2gnn_gemm_group(arr, len(calls), _s()), "u2gnn_gemm_group")
+
+
+def _gemm_args(A, B, C, M, N, K, lda, ldb, ldc, trans_a=False, trans_b=False, epilogue=_lib.EPI_STORE, split_k=1,
+               slab_stride=0, bias=None, aux0=None, aux1=None, rowvec=None, ld_aux=0, alpha=1.0, scale_cols=0,
+               p_drop=0.0, seed=0, precision="fp32", tile=0, keep=None, clamp_a=False, Cx2=None, ldcx2=0,
+               rowstat=None, m_valid=0, n_valid=0, ln=None, rowpart=None):
+    _dev(A, B, C, Cx2, rowstat)
+    x2 = A.dtype == torch.bfloat16
+    if x2 != (B.dtype == torch.bfloat16):
+        raise _lib.U2GNNNativeError("x2 GEMM: both operands must be pre-split (bfloat16) or neither")
     a = _lib.GemmArgs()
     if x2:
         a.a_x2 = a.b_x2 = 1
@@ -136,12 +164,7 @@ def gemm(A, B, C, M, N, K, lda, ldb, ldc, trans_a=False, trans_b=False, epilogue
         a.ln_gamma, a.ln_beta, a.ln_y, a.ln_ldy = gam.data_ptr(), bet.data_ptr(), Y.data_ptr(), int(ldy)
         a.ln_mean, a.ln_rstd = mean.data_ptr(), rstd.data_ptr()
         a.ln_d, a.ln_rows, a.ln_eps = int(d_real), int(rows), float(eps)
-    # pre-split operands exist only in the experiments library (x2_lib); the product library rejects them
-    check((_lib.x2_lib() if x2 else hip_lib()).u2gnn_gemm(ctypes.byref(a), _s()), "u2gnn_gemm")
-    if rec:
-        ev1.record()
-        REC.records.append((gemm_symbol(precision, M, N, split_k, tile, trans_a, trans_b, epilogue, clamp_a, x2),
-                            float(flops), ev0, ev1))
+    return a, x2
 
 
 def gather_rows(src, idx, idx_stride, dst, n_rows, n_rows_pad, d, d_pad, err=None):
@@ -173,6 +196,27 @@ def pack_padded(src, ld_src, rows_pad, cols_pad, rblk, cblk, dst, ld_dst):
     check(hip_lib().u2gnn_pack_padded(_p(src), int(ld_src), int(rows_pad), int(cols_pad), int(rblk[0]),
                                       int(rblk[1]), int(cblk[0]), int(cblk[1]), _p(dst), int(ld_dst), _s()),
           "u2gnn_pack_padded")
+
+
+def reduce_batch(jobs):
+    """u2gnn_reduce_batch (ABI v11): a list of dicts of u2gnn_reduce_job fields (tensors for the pointer
+    fields); the partial-sum workspace is allocated here.  Bit-identical to the single-job calls."""
+    arr = (_lib.ReduceJob * len(jobs))()
+    dev = None
+    for i, j in enumerate(jobs):
+        for k, v in j.items():
+            if isinstance(v, torch.Tensor):
+                _dev(v)
+                dev = v.device
+                v = v.data_ptr()
+            setattr(arr[i], k, v)
+    lib = hip_lib()
+    wsf = lib.u2gnn_reduce_batch_ws_floats(arr, len(jobs))
+    if wsf < 0:
+        raise _lib.U2GNNNativeError("u2gnn_reduce_batch_ws_floats: invalid job")
+    ws = torch.empty(max(4, wsf), device=dev, dtype=torch.float32)
+    check(lib.u2gnn_reduce_batch(arr, len(jobs), _p(ws), int(wsf), _s()), "u2gnn_reduce_batch")
+    return ws
 
 
 def colsum(X, rows, cols_pad, ld, cblk, out, ws, accumulate=False):

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define U2GNN_ABI_VERSION 10
+#define U2GNN_ABI_VERSION 11
 
 #define U2GNN_OK 0
 #define U2GNN_E_ARG (-1)    /* bad size / null pointer */
@@ -247,6 +247,42 @@ int u2gnn_layernorm_bwd_params(const float *dY, int64_t ldy, const float *Z, int
                                const float *mean, const float *rstd, const float *dZdrop,
                                int64_t lddrop, int64_t rows_valid, int64_t d, int64_t d_pad, float *ws,
                                float *dgamma, float *dbeta, float *dbias, void *stream);
+
+/* ---- ABI v11: batched reductions -------------------------------------------------------------
+ * Many u2gnn_slab_reduce / u2gnn_colsum / u2gnn_layernorm_bwd_params jobs in at most two launches (the
+ * column partials of every long job, then every combine; jobs over <= 512 rows take the one-launch small
+ * forms), each job with the per-element arithmetic and summation order of its single-job call, so the
+ * results are bit-identical.  Jobs must write distinct outputs.  Fields per kind:
+ *   SLAB:     src, n_slab, slab_stride, rows (= rows_pad), cols (= cols_pad), ld_src, rblk_*, cblk_*,
+ *             dst, ld_dst, alpha, accumulate                       (u2gnn_slab_reduce)
+ *   COLSUM:   src (= X), rows, cols (= cols_pad), ld_src, cblk_*, dst, accumulate   (u2gnn_colsum)
+ *   LNPARAMS: src (= dY), ld_src, Z, ldz, mean, rstd, dZdrop, lddrop, rows (= rows_valid), d,
+ *             cols (= d_pad), dst (= dgamma), dbeta, dbias      (u2gnn_layernorm_bwd_params)
+ * COLSUM / LNPARAMS need 16-byte aligned operands (leading dimensions and cols multiples of 4).
+ * ws: >= u2gnn_reduce_batch_ws_floats(jobs, n) floats, 16-byte aligned (the partial sums). */
+#define U2GNN_RJOB_SLAB 0
+#define U2GNN_RJOB_COLSUM 1
+#define U2GNN_RJOB_LNPARAMS 2
+typedef struct u2gnn_reduce_job {
+    int32_t kind, n_slab, accumulate;
+    float alpha;
+    const float *src;
+    int64_t ld_src, slab_stride, rows, cols, d;
+    int64_t rblk_pad, rblk_real, cblk_pad, cblk_real;
+    float *dst;
+    int64_t ld_dst;
+    const float *Z, *mean, *rstd, *dZdrop;
+    int64_t ldz, lddrop;
+    float *dbeta, *dbias;
+} u2gnn_reduce_job;
+int64_t u2gnn_reduce_batch_ws_floats(const u2gnn_reduce_job *jobs, int32_t n);
+int u2gnn_reduce_batch(const u2gnn_reduce_job *jobs, int32_t n, float *ws, int64_t ws_floats, void *stream);
+
+/* ABI v11: several u2gnn_gemm calls in one launch when they resolve to the same kernel (precision, tile,
+ * transposes, STORE epilogue without clamp; split-K allowed): the blocks of the launch are shared out
+ * over the jobs, each tile computed exactly as by its own u2gnn_gemm call (bit-identical).  Calls that do
+ * not share a kernel are launched one by one.  At most 8 jobs. */
+int u2gnn_gemm_group(const u2gnn_gemm_args *args, int32_t n, void *stream);
 
 /* ---- a5/a6: sum pooling + dropout + per-layer head  (pytorch_U2GNN_Sup.py:41-44) ------
  * G[b, c] = drop(sum_{e in [rowptr[b], rowptr[b+1])} vals[e] * X[colidx[e], c]), c < d;

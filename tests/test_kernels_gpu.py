@@ -604,3 +604,89 @@ def test_adam_matches_torch():
         opt.step()
     assert abs(sq.item() - (g.double() ** 2).sum().item()) / sq.item() < 1e-5
     assert rel_err(p1, tp.detach()) < 1e-5
+
+
+# ---- ABI v11: batched reductions and grouped weight-gradient GEMMs (bit-identical to single calls) ----
+@pytest.mark.parametrize("rows", [300, 1920, 20000])   # small forms, long forms, folded long forms
+def test_reduce_batch_equals_single_jobs(rows):
+    d, dp, ff, ffp = 19, 64, 100, 128
+    g = torch.Generator(device=DEV).manual_seed(11)
+    rn = lambda *s: torch.randn(*s, device=DEV, generator=g)   # noqa: E731
+    dY, Z, dZd = rn(rows, dp), rn(rows, dp), rn(rows, dp)
+    mean, rstd = rn(rows), rn(rows).abs() + 0.5
+    X = rn(rows, ffp)
+    slabs = rn(6, ffp, dp)
+    ref = {k: torch.full((n,), float("nan"), device=DEV) for k, n in
+           (("gam", d), ("bet", d), ("bia", d), ("gam2", d), ("bet2", d), ("cs", ff))}
+    ref["w"] = torch.full((ff, d), float("nan"), device=DEV)
+    ref["acc"] = rn(ffp, dp)
+    out = {k: v.clone() for k, v in ref.items()}
+    ws = torch.empty(K.colstat_ws_floats(rows, ffp), device=DEV)
+    K.layernorm_bwd_params(dY, dp, Z, dp, mean, rstd, dZd, dp, rows, d, dp, ws, ref["gam"], ref["bet"], ref["bia"])
+    K.layernorm_bwd_params(dY, dp, Z, dp, mean, rstd, None, dp, rows, d, dp, ws, ref["gam2"], ref["bet2"], None)
+    K.colsum(X, rows, ffp, ffp, (ffp, ff), ref["cs"], ws)
+    K.slab_reduce(slabs, 6, ffp * dp, ffp, dp, dp, (ffp, ff), (dp, d), ref["w"], d, alpha=0.5)
+    K.slab_reduce(slabs, 6, ffp * dp, ffp, dp, dp, (ffp, ffp), (dp, dp), ref["acc"], dp, accumulate=True)
+    R = _lib
+    jobs = [
+        dict(kind=R.RJOB_LNPARAMS, src=dY, ld_src=dp, Z=Z, ldz=dp, mean=mean, rstd=rstd, dZdrop=dZd, lddrop=dp,
+             rows=rows, d=d, cols=dp, dst=out["gam"], dbeta=out["bet"], dbias=out["bia"]),
+        dict(kind=R.RJOB_SLAB, src=slabs, n_slab=6, slab_stride=ffp * dp, rows=ffp, cols=dp, ld_src=dp,
+             rblk_pad=ffp, rblk_real=ff, cblk_pad=dp, cblk_real=d, dst=out["w"], ld_dst=d, alpha=0.5),
+        dict(kind=R.RJOB_COLSUM, src=X, rows=rows, cols=ffp, ld_src=ffp, cblk_pad=ffp, cblk_real=ff, dst=out["cs"]),
+        dict(kind=R.RJOB_LNPARAMS, src=dY, ld_src=dp, Z=Z, ldz=dp, mean=mean, rstd=rstd, rows=rows, d=d, cols=dp,
+             dst=out["gam2"], dbeta=out["bet2"]),
+        dict(kind=R.RJOB_SLAB, src=slabs, n_slab=6, slab_stride=ffp * dp, rows=ffp, cols=dp, ld_src=dp,
+             rblk_pad=ffp, rblk_real=ffp, cblk_pad=dp, cblk_real=dp, dst=out["acc"], ld_dst=dp, alpha=1.0,
+             accumulate=1),
+    ]
+    K.reduce_batch(jobs)
+    torch.cuda.synchronize()
+    for k in ref:
+        assert torch.isfinite(out[k]).all(), k
+        assert torch.equal(out[k], ref[k]), k
+
+
+def test_reduce_batch_rejects_bad_jobs():
+    x = torch.zeros(64, 64, device=DEV)
+    with pytest.raises(_lib.U2GNNNativeError):
+        K.reduce_batch([dict(kind=7, src=x, dst=x)])
+    with pytest.raises(_lib.U2GNNNativeError):   # LN job without mean / rstd
+        K.reduce_batch([dict(kind=_lib.RJOB_LNPARAMS, src=x, ld_src=64, Z=x, ldz=64, rows=64, d=4, cols=64, dst=x,
+                             dbeta=x)])
+
+
+@pytest.mark.parametrize("prec", ["bf16x3", "bf16"])
+@pytest.mark.parametrize("tile", [64, 129])
+def test_gemm_group_equals_single_calls(prec, tile):
+    # the weight-gradient shapes of a d <= 64 layer (dY^T X over Np rows) with split-K slabs
+    Np, shapes = 2048, [(64, 1024, 16), (1024, 64, 16), (64, 64, 16), (192, 64, 8)]
+    if tile == 129:
+        shapes = [(128, 1024, 4), (1024, 128, 4), (384, 128, 8)]
+    calls, outs, refs = [], [], []
+    for i, (M, N, split) in enumerate(shapes):
+        A, B = _mk(Np, M, seed=10 + i), _mk(Np, N, seed=20 + i)
+        o, r = torch.full((split, M, N), float("nan"), device=DEV), torch.full((split, M, N), float("nan"), device=DEV)
+        kw = dict(A=A, B=B, C=o, M=M, N=N, K=Np, lda=M, ldb=N, ldc=N, trans_a=True, split_k=split,
+                  slab_stride=M * N, precision=prec, tile=tile)
+        K.gemm(**dict(kw, C=r))
+        calls.append(kw)
+        outs.append(o)
+        refs.append(r)
+    K.gemm_group(calls)
+    torch.cuda.synchronize()
+    for o, r in zip(outs, refs):
+        assert torch.equal(o, r)
+
+
+def test_gemm_group_mixed_configurations_fall_back():
+    A, B = _mk(512, 128, seed=1), _mk(512, 64, seed=2)
+    c1, c2 = torch.empty(128, 64, device=DEV), torch.empty(128, 64, device=DEV)
+    r1, r2 = torch.empty_like(c1), torch.empty_like(c2)
+    k1 = dict(A=A, B=B, C=c1, M=128, N=64, K=512, lda=128, ldb=64, ldc=64, trans_a=True, precision="bf16x3", tile=64)
+    k2 = dict(A=A, B=B, C=c2, M=128, N=64, K=512, lda=128, ldb=64, ldc=64, trans_a=True, precision="fp32", tile=64)
+    K.gemm(**dict(k1, C=r1))
+    K.gemm(**dict(k2, C=r2))
+    K.gemm_group([k1, k2])
+    torch.cuda.synchronize()
+    assert torch.equal(c1, r1) and torch.equal(c2, r2)

@@ -163,15 +163,23 @@ hipEvent_t pooled_event();
 struct Defer {
     std::vector<u2gnn_reduce_job> red;
     std::vector<u2gnn_gemm_args> gemm;
-    bool gemms = false;   // hold back the weight-gradient GEMM launches as well
+    std::vector<int> role;   // probe role of each held-back GEMM
+    bool gemms = false;   // hold back the GEMM launches as well (one grouped launch)
 };
 
 int flush(Defer *df, Arena &W, hipStream_t st) {
     if (!df) return U2GNN_OK;
     const bool plan = W.plan();
     for (size_t o = 0; o < df->gemm.size(); o += 8) {
-        const int32_t n = (int32_t)std::min<size_t>(8, df->gemm.size() - o);
-        if (!plan) U2GNN_TRY(u2gnn_gemm_group(df->gemm.data() + o, n, st));
+        const size_t n = std::min<size_t>(8, df->gemm.size() - o);
+        // a grouped launch is timed as a whole under each role it carries (u2gnn_probe_arm)
+        int probed = 0;
+        for (size_t i = o; i < o + n; ++i)
+            if (df->role[i] && df->role[i] != probed) probed = df->role[i], probe_mark(probed, false, st, plan);
+        if (!plan) U2GNN_TRY(u2gnn_gemm_group(df->gemm.data() + o, (int32_t)n, st));
+        probed = 0;
+        for (size_t i = o; i < o + n; ++i)
+            if (df->role[i] && df->role[i] != probed) probed = df->role[i], probe_mark(probed, true, st, plan);
     }
     const int64_t wsf = u2gnn_reduce_batch_ws_floats(df->red.data(), (int32_t)df->red.size());
     if (wsf < 0) return U2GNN_E_ARG;
@@ -180,6 +188,7 @@ int flush(Defer *df, Arena &W, hipStream_t st) {
         U2GNN_TRY(u2gnn_reduce_batch(df->red.data(), (int32_t)df->red.size(), ws, wsf, st));
     df->red.clear();
     df->gemm.clear();
+    df->role.clear();
     return U2GNN_OK;
 }
 
@@ -250,6 +259,7 @@ int gemm_split(Arena &W, const Dims &D, const float *A, const float *B, float *C
         g.epi(accumulate ? U2GNN_EPI_ACCUM : U2GNN_EPI_STORE).tile(t);
         if (df && df->gemms && !accumulate) {
             df->gemm.push_back(g.a);
+            df->role.push_back(role);
             return U2GNN_OK;
         }
         probe_mark(role, false, st, plan);
@@ -269,6 +279,7 @@ int gemm_split(Arena &W, const Dims &D, const float *A, const float *B, float *C
     if (df) {   // slab reduce (and with df->gemms the GEMM itself) at the layer's flush
         if (df->gemms) {
             df->gemm.push_back(g.a);
+            df->role.push_back(role);
         } else {
             probe_mark(role, false, st, plan);
             U2GNN_TRY(g.run(st, plan));
@@ -411,6 +422,19 @@ void set_ln(u2gnn_gemm_args &a, const float *gamma, const float *beta, float *y,
 
 // the fused attention forward (u2gnn_attn_softmax_pv): node-axis attention in the matrix-core
 // precisions with dp <= 384 (engine.fused_attn mirrors the rule)
+// split-K depth of FFN2 in the fused-LayerNorm (d <= 64) form: with fewer than 128 row-complete 64x64
+// tiles, aim at ~256 blocks of >= 4 K steps (engine.ffn2_split mirrors the rule)
+int64_t ffn2_split(bool fuse_ln, int64_t Np, int64_t ffp) {
+    if (!fuse_ln || Np / 64 >= 128) return 1;
+    int64_t sp = 256 / (Np / 64);
+    if (sp > ffp / 128) sp = ffp / 128;
+    return sp > 1 ? sp : 1;
+}
+
+// tile of S = Q K^T: 256x128 blocks unless they would leave most CUs idle (C5's Np = 2048 gives 128 of
+// them), then 128x128 (the same per-element sums: same bits; engine.qk_tile mirrors the rule)
+int qk_tile(int64_t Np) { return (Np % 256 == 0 && (Np / 256) * (Np / 128) >= 256) ? 256 : 128; }
+
 bool fused_attn(const Dims &D) { return !D.window && D.prec != U2GNN_PREC_F32 && D.dp <= 384; }
 
 int layer_fwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seeds *s, const float *X, float *X2,
@@ -453,7 +477,7 @@ int layer_fwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
         float *pv_ws = W.take<float>(u2gnn_attn_softmax_pv_ws_floats(N, Np, dp));
         {
             G g(Q, Kt, c.Pd, Np, Np, dp, 3 * dp, 3 * dp, Np, prec);
-            g.tb().epi(U2GNN_EPI_STORE_ROWSTAT).tile(Np % 256 == 0 ? 256 : 128);
+            g.tb().epi(U2GNN_EPI_STORE_ROWSTAT).tile(qk_tile(Np));
             g.a.rowpart = rowpart, g.a.ld_rowpart = ld_rp, g.a.n_valid = N;
             probe_mark(U2GNN_ROLE_QK, false, st, plan);
             U2GNN_TRY(g.run(st, plan));
@@ -501,7 +525,20 @@ int layer_fwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
         g.a.bias = w->b1, g.a.p_drop = pd, g.a.seed = s->dropff;
         U2GNN_TRY(g.run(st, plan));
     }
-    {
+    const int64_t f2_split = ffn2_split(fuse_ln, Np, ffp);
+    if (f2_split > 1) {
+        // too few row-complete tiles (C5: 32 of them, each a 32-step K loop): split-K slabs, then the
+        // bias / dropout / residual / LayerNorm pass over the slabs
+        float *slabs = W.take<float>(f2_split * Np * dp);
+        G g(c.Hd, w->W2, slabs, Np, dp, ffp, ffp, ffp, dp, prec);
+        g.tb().tile(64);
+        g.a.split_k = (int32_t)f2_split, g.a.slab_stride = Np * dp;
+        U2GNN_TRY(g.run(st, plan));
+        if (!plan)
+            U2GNN_TRY(u2gnn_slab_bias_drop_resid_ln(slabs, (int32_t)f2_split, Np * dp, dp, w->b2, c.X1, dp, pd,
+                                                    s->drop2, c.Z2, dp, w->n2_w, w->n2_b, X2, dp, c.mean2, c.rstd2, d,
+                                                    N, Np, 1e-5f, st));
+    } else {
         G g(c.Hd, w->W2, c.Z2, Np, dp, ffp, ffp, ffp, dp, prec);
         g.tb().epi(fuse_ln ? U2GNN_EPI_BIAS_DROP_RESID_LN : U2GNN_EPI_BIAS_DROP_RESID);
         g.a.bias = w->b2, g.a.aux0 = c.X1, g.a.ld_aux = dp, g.a.p_drop = pd, g.a.seed = s->drop2;
@@ -530,8 +567,11 @@ int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
     // one stream (latency-bound layers): the parameter-gradient reductions and products go out together
     // at the end (df), the attention products' slab reduces together before the in-projection (att)
     Defer defer_p, defer_a;
-    defer_p.gemms = true;
-    Defer *df = so == st ? &defer_p : nullptr, *att = so == st ? &defer_a : nullptr;
+    defer_p.gemms = defer_a.gemms = true;
+    // the attention products dQ, dK (and dV when it runs on this stream) go out as one grouped launch and
+    // their slab reduces as one batch, in both modes (C4, side-stream schedule: 3.029 / 3.028 / 3.041 vs
+    // 3.024 / 3.046 / 3.035 ms per step without the grouping, one session: neutral; C5 -2 launches per layer)
+    Defer *df = so == st ? &defer_p : nullptr, *att = &defer_a;
     const int64_t blk_d[2] = {dp, d}, blk_ff[2] = {ffp, ff};
     float *ws = W.take<float>(colstat_ws_floats(N, dp));
     // LN2 backward -> dX1 (residual), dF (dropout2 branch); norm2 + linear2.bias grads (side)
@@ -595,7 +635,8 @@ int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
         // dV needs only Pd and dO: on the side stream it overlaps the dS -> dQ -> dK chain
         U2GNN_TRY(sd.fork());
         U2GNN_TRY(gemm_split(W, D, c.Pd, dO, dQKV + 2 * dp, Np, dp, Np, Np, dp, 3 * dp, true, 1.f, false, nullptr,
-                             nullptr, false, dv_side ? so : st, pd > 0.f, -1, U2GNN_ROLE_DV, nullptr, att));
+                             nullptr, false, dv_side ? so : st, pd > 0.f, -1, U2GNN_ROLE_DV, nullptr,
+                             dv_side ? nullptr : att));
         if (dv_side) U2GNN_TRY(sd.mark(&dv_done));
         float *delta = ln_delta ? delta_ln : W.take<float>(Np);
         if (!plan && !ln_delta) U2GNN_TRY(u2gnn_rowdot(dO, dp, c.O, dp, delta, Np, dp, st));
@@ -612,8 +653,8 @@ int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
                              false, st, false, D.prec_ab, U2GNN_ROLE_DQ, nullptr, att));
         U2GNN_TRY(gemm_split(W, D, dS, Q, dQKV + dp, Np, dp, Np, Np, 3 * dp, 3 * dp, true, 1.f, false, nullptr,
                              nullptr, false, st, false, D.prec_ab, U2GNN_ROLE_DK, nullptr, att));
-        U2GNN_TRY(sd.wait(dv_done));   // dV before dX += dQKV W_in
         U2GNN_TRY(flush(att, W, st));
+        U2GNN_TRY(sd.wait(dv_done));   // dV before dX += dQKV W_in
     }
     // in-projection
     if (need_dx)

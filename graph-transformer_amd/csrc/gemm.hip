@@ -320,8 +320,17 @@ __device__ __forceinline__ bf16x8 ld_frag(const __bf16 *img, int r0, int ks, int
 
 // The main loop and epilogue of one output tile (tile coordinates from the caller: the plain launch's
 // XCD-aware map, or the grouped launch's job walk).
+// bf16 elements of the kernel's LDS image (two stages of hi + lo planes of both operands)
+template <int BM, int BN, int BK, bool TA, bool TB>
+constexpr int bf16_smem_elems() {
+    constexpr int LDK = BK + 8;
+    constexpr int AE = TA ? BK * (BM + 32) : BM * LDK;
+    constexpr int BE = !TB ? BK * (BN + 32) : BN * LDK;
+    return 2 * 2 * (AE + BE);
+}
+
 template <int BM, int BN, int WM, int WN, int BK, bool TA, bool TB, int EPI, bool SPLIT, bool CLAMP>
-__device__ __forceinline__ void gemm_bf16_body(const GemmP &P, int tmi, int tni, int zi) {
+__device__ __forceinline__ void gemm_bf16_body(const GemmP &P, int tmi, int tni, int zi, __bf16 *smem) {
     constexpr int NT = 64 * WM * WN;
     constexpr int LDK = BK + 8;
     constexpr int WTM = BM / WM, WTN = BN / WN;
@@ -330,7 +339,6 @@ __device__ __forceinline__ void gemm_bf16_body(const GemmP &P, int tmi, int tni,
     constexpr int AE = TA ? BK * (BM + 32) : BM * LDK;    // elements per plane, per operand
     constexpr int BE = !TB ? BK * (BN + 32) : BN * LDK;
     constexpr int STAGE = 2 * (AE + BE);  // hi + lo of A and B
-    __shared__ __attribute__((aligned(16))) __bf16 smem[2 * STAGE];
 
     const int tid = threadIdx.x;
     const int m0 = tmi * BM, n0 = tni * BN;
@@ -431,30 +439,43 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_bf16_kernel(GemmP P) {
     if constexpr (EPI == U2GNN_EPI_BIAS_DROP_RESID || EPI == U2GNN_EPI_BIAS_RELU_DROP || EPI == U2GNN_EPI_ATTN_DS_RECOMP ||
                   EPI == U2GNN_EPI_BIAS_DROP_RESID_LN)
         P.seed = u2gnn_seed(P.seed, P.epoch);   // graph replay: device-resident seed epoch
+    __shared__ __attribute__((aligned(16))) __bf16 smem[bf16_smem_elems<BM, BN, BK, TA, TB>()];
     int tmi, tni, zi;
     tile_coords(P.gm, P.gn, tmi, tni, zi);
-    gemm_bf16_body<BM, BN, WM, WN, BK, TA, TB, EPI, SPLIT, CLAMP>(P, tmi, tni, zi);
+    gemm_bf16_body<BM, BN, WM, WN, BK, TA, TB, EPI, SPLIT, CLAMP>(P, tmi, tni, zi, smem);
 }
 
-// Grouped launch (u2gnn_gemm_group): several STORE products that share one kernel configuration.  The
-// XCD-aware logical id runs over the whole grid; job j owns ids [start[j], start[j+1]) and maps its
-// local id to a tile exactly as its own launch would (same tile arithmetic, hence the same bits).
+// Grouped launch (u2gnn_gemm_group): several STORE products of one tile shape, each A^T B (the weight
+// gradients, dK), A^T B over the clamped signed image (dV) or A B (dQ).  The XCD-aware logical id runs
+// over the whole grid; job j owns ids [start[j], start[j+1]) and maps its local id to a tile exactly as
+// its own launch would, with the body of its own layout (same tile arithmetic, hence the same bits).  The
+// three bodies share one LDS image sized for the largest.
 constexpr int GG_MAX = 8;
+enum GgLayout : int32_t { GG_TA = 0, GG_TA_CLAMP = 1, GG_NN = 2 };
 struct GemmGroup {
     GemmP p[GG_MAX];
     int32_t start[GG_MAX + 1];
+    int32_t layout[GG_MAX];
     int32_t n;
 };
 
-template <int BM, int BN, int WM, int WN, int BK, bool TA, bool TB, bool SPLIT>
+template <int BM, int BN, int WM, int WN, int BK, bool SPLIT>
 __global__ void __launch_bounds__(64 * WM * WN) gemm_bf16_group_kernel(GemmGroup G) {
+    constexpr int E_TA = bf16_smem_elems<BM, BN, BK, true, false>(), E_NN = bf16_smem_elems<BM, BN, BK, false, false>();
+    __shared__ __attribute__((aligned(16))) __bf16 smem[E_TA > E_NN ? E_TA : E_NN];
     const int w = xcd_wgid();
     int j = 0;
     while (j + 1 < G.n && w >= G.start[j + 1]) ++j;
     const GemmP &P = G.p[j];
     int tmi, tni, zi;
     tile_of(P.gm, P.gn, w - G.start[j], tmi, tni, zi);
-    gemm_bf16_body<BM, BN, WM, WN, BK, TA, TB, U2GNN_EPI_STORE, SPLIT, false>(P, tmi, tni, zi);
+    const int lay = G.layout[j];
+    if (lay == GG_NN)
+        gemm_bf16_body<BM, BN, WM, WN, BK, false, false, U2GNN_EPI_STORE, SPLIT, false>(P, tmi, tni, zi, smem);
+    else if (lay == GG_TA_CLAMP)
+        gemm_bf16_body<BM, BN, WM, WN, BK, true, false, U2GNN_EPI_STORE, SPLIT, true>(P, tmi, tni, zi, smem);
+    else
+        gemm_bf16_body<BM, BN, WM, WN, BK, true, false, U2GNN_EPI_STORE, SPLIT, false>(P, tmi, tni, zi, smem);
 }
 
 // bf16 K-step variants: 0 = BK 32 (2 blocks/CU at 128x128), 1 = BK 16 (40 KB LDS, 140-152
@@ -720,16 +741,16 @@ int gemm_launch(const u2gnn_gemm_args *a, GemmPlan &G, hipStream_t st) {
     return launch_tile<U2GNN_PREC_F32>(G.P, G.tile, G.ta, G.tb, G.epi, G.split, G.clamp, st);
 }
 
-// the grouped kernels: the weight-gradient tiles (64 and the 16-deep 128), A^T B, STORE
+// the grouped kernels: 64x64 and the 16-deep 128x128 (weight gradients), 256x128 (attention products)
 template <int KIND>
 int launch_group(GemmGroup &GG, int tile, int blocks, hipStream_t st) {
     constexpr bool SPLIT = KIND == U2GNN_PREC_BF16X3;
     if (tile == 64)
-        hipLaunchKernelGGL((gemm_bf16_group_kernel<64, 64, 2, 2, 32, true, false, SPLIT>), dim3(blocks), dim3(256), 0,
-                           st, GG);
+        hipLaunchKernelGGL((gemm_bf16_group_kernel<64, 64, 2, 2, 32, SPLIT>), dim3(blocks), dim3(256), 0, st, GG);
+    else if (tile == 129)
+        hipLaunchKernelGGL((gemm_bf16_group_kernel<128, 128, 2, 2, 16, SPLIT>), dim3(blocks), dim3(256), 0, st, GG);
     else
-        hipLaunchKernelGGL((gemm_bf16_group_kernel<128, 128, 2, 2, 16, true, false, SPLIT>), dim3(blocks), dim3(256),
-                           0, st, GG);
+        hipLaunchKernelGGL((gemm_bf16_group_kernel<256, 128, 4, 2, 32, SPLIT>), dim3(blocks), dim3(512), 0, st, GG);
     return u2gnn_launch_status();
 }
 
@@ -754,8 +775,8 @@ extern "C" int u2gnn_gemm_group(const u2gnn_gemm_args *args, int32_t n, void *st
     bool same = n > 1;
     for (int32_t i = 0; i < n && same; ++i)
         same = !G[i].x2 && G[i].prec == G[0].prec && G[i].prec != U2GNN_PREC_F32 && G[i].tile == G[0].tile &&
-               (G[i].tile == 64 || G[i].tile == 129) && G[i].ta && !G[i].tb && G[i].epi == U2GNN_EPI_STORE &&
-               !G[i].clamp;
+               (G[i].tile == 64 || G[i].tile == 129 || G[i].tile == 256) && !G[i].tb && G[i].epi == U2GNN_EPI_STORE &&
+               (G[i].ta || !G[i].clamp);
     if (!same) {
         for (int32_t i = 0; i < n; ++i) {
             const int rc = gemm_launch(&args[i], G[i], st);
@@ -769,6 +790,7 @@ extern "C" int u2gnn_gemm_group(const u2gnn_gemm_args *args, int32_t n, void *st
     int64_t blocks = 0;
     for (int32_t i = 0; i < n; ++i) {
         GG.p[i] = G[i].P;
+        GG.layout[i] = !G[i].ta ? GG_NN : (G[i].clamp ? GG_TA_CLAMP : GG_TA);
         GG.start[i] = (int32_t)blocks;
         blocks += (int64_t)G[i].P.gm * G[i].P.gn * G[i].split;
     }

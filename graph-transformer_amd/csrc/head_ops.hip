@@ -433,9 +433,136 @@ inline unsigned grid_for(int64_t n, int64_t per_block, int64_t cap = 8192) {
     return (unsigned)g;
 }
 
+// ------------------------------------------------------------------------------------------
+// UnSup head glue (ABI v11; pytorch_U2GNN_UnSup.py:52-69 + the TF model's dropout before the sampled
+// softmax, U2GNN_tf/model_U2GNN_Unsup_multi.py:43-56).  concat_dropout: the L layers' padded slot-0
+// outputs -> Y[N, d*L] with dropout(p) (the mask of u2gnn_dropout over Y's (row, column) indices) in one
+// pass; split_dropout_bwd: the gradient of that, dropped out with the same mask and written back as
+// L zero-padded [Np][dp] images (u2gnn_dropout + L u2gnn_pack_padded in one pass).
+// ------------------------------------------------------------------------------------------
+constexpr int CAT_MAX = 8;
+struct CatSrc {
+    const float *p[CAT_MAX];
+};
+struct CatDst {
+    float *p[CAT_MAX];
+};
+
+__global__ void __launch_bounds__(256) concat_dropout_kernel(CatSrc src, int64_t ld_src, int64_t N, int64_t d, int L,
+                                                             float p, uint64_t seed, const uint64_t *seed_epoch,
+                                                             float *Y, int64_t ldy) {
+    seed = u2gnn_seed(seed, seed_epoch);
+    const int64_t D = d * L, total = N * D;
+    const float ks = 1.f / (1.f - p);
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+        const int64_t r = i / D, c = i - r * D, l = c / d;
+        const float v = src.p[l][r * ld_src + (c - l * d)];
+        Y[r * ldy + c] = p > 0.f ? (u2gnn_keep(seed, (uint32_t)r, (uint32_t)c, p) ? v * ks : 0.f) : v;
+    }
+}
+
+__global__ void __launch_bounds__(256) split_dropout_bwd_kernel(const float *dY, int64_t ldy, int64_t N, int64_t Np,
+                                                                int64_t d, int64_t dp, int L, float p, uint64_t seed,
+                                                                const uint64_t *seed_epoch, CatDst dst) {
+    seed = u2gnn_seed(seed, seed_epoch);
+    const int64_t per = Np * dp, total = per * L;
+    const float ks = 1.f / (1.f - p);
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+        const int64_t l = i / per, e = i - l * per, r = e / dp, c = e - r * dp;
+        float v = 0.f;
+        if (r < N && c < d) {
+            const int64_t cc = l * d + c;
+            v = dY[r * ldy + cc];
+            if (p > 0.f) v = u2gnn_keep(seed, (uint32_t)r, (uint32_t)cc, p) ? v * ks : 0.f;
+        }
+        dst.p[l][e] = v;
+    }
+}
+
+// out[0] = sum of x[0, n): one 1024-thread block, lane t sums x[t], x[t + 1024], ... (4 accumulators), then
+// a fixed shuffle / LDS tree (deterministic)
+__global__ void __launch_bounds__(1024) sum_kernel(const float *x, int64_t n, float *out) {
+    __shared__ float red[16];
+    float a[4] = {0.f, 0.f, 0.f, 0.f};
+    int64_t i = threadIdx.x;
+    for (; i + 3 * 1024 < n; i += 4 * 1024) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) a[k] += x[i + k * 1024];
+    }
+    for (; i < n; i += 1024) a[0] += x[i];
+    float s = wave_sum((a[0] + a[1]) + (a[2] + a[3]));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float t = 0.f;
+        for (int w = 0; w < 16; ++w) t += red[w];
+        out[0] = t;
+    }
+}
+
+// dst[idx_a[r]] = 0 and dst[idx_b[r]] = 0 in one launch (zeroing is idempotent: the sets may overlap)
+__global__ void __launch_bounds__(256) index_zero_rows2_kernel(const int64_t *ia, int64_t na, const int64_t *ib,
+                                                               int64_t nb, float *dst, int64_t ld_dst, int64_t dst_rows,
+                                                               int64_t D, int32_t *err) {
+    const int lane = threadIdx.x & 63;
+    for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < na + nb; r += (int64_t)gridDim.x * 4) {
+        const int64_t y = r < na ? ia[r] : ib[r - na];
+        if (y < 0 || y >= dst_rows) {
+            if (err && lane == 0) *err = 1;
+            continue;
+        }
+        for (int64_t c = lane; c < D; c += 64) dst[y * ld_dst + c] = 0.f;
+    }
+}
+
 }  // namespace
 
 extern "C" {
+
+int u2gnn_concat_dropout(const float *const *src, int32_t L, int64_t ld_src, int64_t N, int64_t d, float p,
+                         uint64_t seed, float *Y, int64_t ldy, void *stream) {
+    if (!src || L < 1 || L > CAT_MAX || N < 0 || d < 1 || ld_src < d || !Y || ldy < d * L || p < 0.f || p >= 1.f)
+        return U2GNN_E_ARG;
+    CatSrc cs;
+    for (int l = 0; l < CAT_MAX; ++l) cs.p[l] = l < L ? src[l] : nullptr;
+    for (int l = 0; l < L; ++l)
+        if (!cs.p[l]) return U2GNN_E_ARG;
+    if (N == 0) return U2GNN_OK;
+    hipLaunchKernelGGL(concat_dropout_kernel, dim3(grid_for(N * d * L, 256)), dim3(256), 0, u2gnn_stream(stream), cs,
+                       ld_src, N, d, (int)L, p, seed, u2gnn_g_epoch, Y, ldy);
+    return u2gnn_launch_status();
+}
+
+int u2gnn_split_dropout_bwd(const float *dY, int64_t ldy, int32_t L, int64_t N, int64_t Np, int64_t d, int64_t dp,
+                            float p, uint64_t seed, float *const *dst, void *stream) {
+    if (!dY || !dst || L < 1 || L > CAT_MAX || N < 0 || Np < N || d < 1 || dp < d || ldy < d * L || p < 0.f ||
+        p >= 1.f)
+        return U2GNN_E_ARG;
+    CatDst cd;
+    for (int l = 0; l < CAT_MAX; ++l) cd.p[l] = l < L ? dst[l] : nullptr;
+    for (int l = 0; l < L; ++l)
+        if (!cd.p[l]) return U2GNN_E_ARG;
+    if (Np == 0) return U2GNN_OK;
+    hipLaunchKernelGGL(split_dropout_bwd_kernel, dim3(grid_for(Np * dp * L, 256)), dim3(256), 0, u2gnn_stream(stream),
+                       dY, ldy, N, Np, d, dp, (int)L, p, seed, u2gnn_g_epoch, cd);
+    return u2gnn_launch_status();
+}
+
+int u2gnn_sum(const float *x, int64_t n, float *out, void *stream) {
+    if (!x || !out || n < 0) return U2GNN_E_ARG;
+    hipLaunchKernelGGL(sum_kernel, dim3(1), dim3(1024), 0, u2gnn_stream(stream), x, n, out);
+    return u2gnn_launch_status();
+}
+
+int u2gnn_index_zero_rows2(const int64_t *idx_a, int64_t n_a, const int64_t *idx_b, int64_t n_b, float *dst,
+                           int64_t ld_dst, int64_t dst_rows, int64_t D, int32_t *err, void *stream) {
+    if (n_a < 0 || n_b < 0 || D < 0) return U2GNN_E_ARG;
+    if (n_a + n_b == 0 || D == 0) return U2GNN_OK;
+    if ((n_a && !idx_a) || (n_b && !idx_b) || !dst || ld_dst < D) return U2GNN_E_ARG;
+    hipLaunchKernelGGL(index_zero_rows2_kernel, dim3(grid_for(n_a + n_b, 4, 1 << 20)), dim3(256), 0,
+                       u2gnn_stream(stream), idx_a, n_a, idx_b, n_b, dst, ld_dst, dst_rows, D, err);
+    return u2gnn_launch_status();
+}
 
 int u2gnn_pool_fwd(const float *X, int64_t ldx, const int64_t *rowptr, const int64_t *colidx, const float *vals,
                    float *G, int64_t ldg, int64_t B, int64_t d, float p, uint64_t seed, void *stream) {

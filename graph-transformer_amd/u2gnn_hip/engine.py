@@ -312,6 +312,20 @@ def _gemm_nodes_k(A, B, C, M, N, Kd, lda, ldb, ldc, trans_a=False, alpha=1.0, pr
                 clamp_a=clamp_a)
 
 
+def ffn2_split(fuse: bool, Np: int, ffp: int) -> int:
+    """Split-K depth of FFN2 in the fused-LayerNorm form (encoder_layer.cpp ffn2_split): with fewer than
+    128 row-complete 64x64 tiles, ~256 blocks of >= 4 K steps, finished by slab_bias_drop_resid_ln."""
+    if not fuse or Np // 64 >= 128:
+        return 1
+    return max(1, min(256 // (Np // 64), ffp // 128))
+
+
+def qk_tile(Np: int) -> int:
+    """Tile of the S = Q K^T product (encoder_layer.cpp qk_tile): 256x128 blocks unless they would leave
+    most CUs idle (C5's Np = 2048: 128 blocks), then 128x128 (same per-element sums, same bits)."""
+    return 256 if Np % 256 == 0 and (Np // 256) * (Np // 128) >= 256 else 128
+
+
 def fused_attn(dp: int, prec_qk: str, prec_pv: str) -> bool:
     """Node-axis attention forward through the fused softmax.P.V kernel: matrix-core precisions,
     dp <= 384 (encoder_layer.cpp fused_attn)."""
@@ -360,7 +374,7 @@ def encoder_layer_forward(X: torch.Tensor, w: PackedLayer, p: LayerParams, dims:
         Pd = torch.empty(Np, Np, device=dev, dtype=f32)
         rowpart = torch.empty(Np, 2 * (Np // 32), device=dev, dtype=f32)
         K.gemm(Q, Kt, Pd, Np, Np, dp, 3 * dp, 3 * dp, Np, trans_b=True, epilogue=E.EPI_STORE_ROWSTAT,
-               rowpart=rowpart, n_valid=N, precision=_rp("qk", prec), flops=att, tile=256 if Np % 256 == 0 else 128)
+               rowpart=rowpart, n_valid=N, precision=_rp("qk", prec), flops=att, tile=qk_tile(Np))
         ws = torch.empty(K.attn_softmax_pv_ws_floats(N, Np, dp), device=dev, dtype=f32)
         O = torch.empty(Np, dp, device=dev, dtype=f32)
         K.attn_softmax_pv(Pd, Np, rowpart, Np // 64, QKV2, 6 * dp, dp, Pd, Np, O, dp, ws, N, Np, pd,
@@ -386,10 +400,19 @@ def encoder_layer_forward(X: torch.Tensor, w: PackedLayer, p: LayerParams, dims:
     X2 = torch.empty(Np, dp, device=dev, dtype=f32)
     mean2 = torch.empty(Np, device=dev, dtype=f32)
     rstd2 = torch.empty(Np, device=dev, dtype=f32)
-    K.gemm(Hd, w.W2, Z2, Np, dp, ffp, ffp, ffp, dp, trans_b=True,
-           epilogue=E.EPI_BIAS_DROP_RESID_LN if fuse else E.EPI_BIAS_DROP_RESID, bias=w.b2,
-           aux0=X1, ld_aux=dp, p_drop=pd, seed=seeds.get(SITE_DROP2, 0), precision=_rp("ffn2", prec),
-           flops=2.0 * N * d * ff, ln=(p.n2_w, p.n2_b, X2, dp, mean2, rstd2, d, N, 1e-5) if fuse else None)
+    f2 = ffn2_split(fuse, Np, ffp)
+    if f2 > 1:   # split-K slabs + the bias / dropout / residual / LayerNorm pass (encoder_layer.cpp layer_fwd)
+        slabs = torch.empty(f2, Np, dp, device=dev, dtype=f32)
+        K.gemm(Hd, w.W2, slabs, Np, dp, ffp, ffp, ffp, dp, trans_b=True, split_k=f2, slab_stride=Np * dp,
+               precision=_rp("ffn2", prec), flops=2.0 * N * d * ff, tile=64)
+        K.slab_bias_drop_resid_ln(slabs, f2, Np * dp, w.b2, X1, pd, seeds.get(SITE_DROP2, 0), Z2, p.n2_w, p.n2_b,
+                                  X2, mean2, rstd2, d, N, Np)
+        del slabs
+    else:
+        K.gemm(Hd, w.W2, Z2, Np, dp, ffp, ffp, ffp, dp, trans_b=True,
+               epilogue=E.EPI_BIAS_DROP_RESID_LN if fuse else E.EPI_BIAS_DROP_RESID, bias=w.b2,
+               aux0=X1, ld_aux=dp, p_drop=pd, seed=seeds.get(SITE_DROP2, 0), precision=_rp("ffn2", prec),
+               flops=2.0 * N * d * ff, ln=(p.n2_w, p.n2_b, X2, dp, mean2, rstd2, d, N, 1e-5) if fuse else None)
     if not fuse:
         K.layernorm_fwd(Z2, dp, p.n2_w, p.n2_b, X2, dp, mean2, rstd2, N, Np, d, dp)
     ctx = None

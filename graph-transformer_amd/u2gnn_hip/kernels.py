@@ -431,6 +431,48 @@ def index_zero_rows(idx, dst, err=None):
                                           int(dst.shape[1]), _p(err), _s()), "u2gnn_index_zero_rows")
 
 
+def index_zero_rows2(idx_a, idx_b, dst, err=None):
+    """dst[idx_a[r]] = 0 and dst[idx_b[r]] = 0 in one launch (ABI v11)."""
+    _dev(idx_a, idx_b, dst, err)
+    check(hip_lib().u2gnn_index_zero_rows2(_p(idx_a), int(idx_a.numel()), _p(idx_b), int(idx_b.numel()), _p(dst),
+                                           int(dst.stride(0)), int(dst.shape[0]), int(dst.shape[1]), _p(err), _s()),
+          "u2gnn_index_zero_rows2")
+
+
+def concat_dropout(srcs, ld_src, N, d, Y, ldy, p, seed):
+    """Y[:, l*d:(l+1)*d] = drop(srcs[l][:N, :d]) over Y's indices (ABI v11)."""
+    _dev(*srcs, Y)
+    arr = (ctypes.c_void_p * len(srcs))(*[t.data_ptr() for t in srcs])
+    check(hip_lib().u2gnn_concat_dropout(arr, len(srcs), int(ld_src), int(N), int(d), float(p), int(seed), _p(Y),
+                                         int(ldy), _s()), "u2gnn_concat_dropout")
+
+
+def split_dropout_bwd(dY, ldy, N, Np, d, dp, p, seed, dsts):
+    """dsts[l] ([Np, dp], contiguous) = zero-padded drop(dY[:, l*d:(l+1)*d]) (ABI v11)."""
+    _dev(dY, *dsts)
+    arr = (ctypes.c_void_p * len(dsts))(*[t.data_ptr() for t in dsts])
+    check(hip_lib().u2gnn_split_dropout_bwd(_p(dY), int(ldy), len(dsts), int(N), int(Np), int(d), int(dp), float(p),
+                                            int(seed), arr, _s()), "u2gnn_split_dropout_bwd")
+
+
+def slab_bias_drop_resid_ln(slabs, n_slab, slab_stride, bias, resid, p, seed, Z, gamma, beta, Y, mean, rstd, d,
+                            rows_valid, rows_pad, eps=1e-5):
+    """FFN2's split-K epilogue for d <= 64 encoders (ABI v11): Z = resid + drop(sum of slabs + bias), Y = LN(Z).
+    slabs [n_slab, rows_pad, 64]; resid, Z, Y [rows_pad, 64]."""
+    _dev(slabs, bias, resid, Z, gamma, beta, Y, mean, rstd)
+    check(hip_lib().u2gnn_slab_bias_drop_resid_ln(_p(slabs), int(n_slab), int(slab_stride), 64, _p(bias), _p(resid),
+                                                  int(resid.stride(0)), float(p), int(seed), _p(Z), int(Z.stride(0)),
+                                                  _p(gamma), _p(beta), _p(Y), int(Y.stride(0)), _p(mean), _p(rstd),
+                                                  int(d), int(rows_valid), int(rows_pad), float(eps), _s()),
+          "u2gnn_slab_bias_drop_resid_ln")
+
+
+def sum_all(x, n, out):
+    """out[0] = sum of the first n elements of x, fixed order, one launch (ABI v11)."""
+    _dev(x, out)
+    check(hip_lib().u2gnn_sum(_p(x), int(n), _p(out), _s()), "u2gnn_sum")
+
+
 def dropout(X, ldx, Y, ldy, rows, cols, p, seed):
     _dev(X, Y)
     check(hip_lib().u2gnn_dropout(_p(X), int(ldx), _p(Y), int(ldy), int(rows), int(cols), float(p), int(seed), _s()),

@@ -31,27 +31,24 @@ class UnSupCore:
         self.stack = EncoderStack(module.u2gnn_layers, self.d, self.ff, self.T, self.L, precision, 0.5,
                                   getattr(module, "attention", "nodes"))
 
-    def encode(self, b: DeviceBatch, train: bool, need_ctx: bool, seed: int):
-        """-> (OV f32 [N, d*L] real layout, ctx)."""
+    def encode(self, b: DeviceBatch, train: bool, need_ctx: bool, seed: int, p: float = 0.0, drop_seed: int = 0):
+        """-> (OV f32 [N, d*L] real layout, dropped out with (p, drop_seed) when p > 0, ctx).  The padded
+        per-layer outputs are unpadded, concatenated and dropped out in one launch (u2gnn_concat_dropout)."""
         outs, sctx = self.stack.forward(b, train, need_ctx, seed)
         d, dp, L = self.d, rup(self.d, 64), self.L
         N = b.N
         OV = torch.empty(N, d * L, device=b.X_concat.device, dtype=torch.float32)
-        for l in range(L):
-            # padded [Np, dp] -> real columns l*d .. (l+1)*d of OV
-            K.slab_reduce(outs[l], 1, 0, N, dp, dp, (N, N), (dp, d), OV[:, l * d:], d * L)
+        K.concat_dropout(outs, dp, N, d, OV, d * L, p, drop_seed)
         return OV, sctx
 
-    def encode_backward(self, sctx, dOV: torch.Tensor, grads: dict):
+    def encode_backward(self, sctx, dOV: torch.Tensor, grads: dict, p: float = 0.0, drop_seed: int = 0):
+        """dOV: the gradient of encode()'s output; its dropout (same p, drop_seed) and the split into the
+        layers' padded gradients are one launch (u2gnn_split_dropout_bwd)."""
         d, dp, L = self.d, rup(self.d, 64), self.L
         dims = sctx["dims"]
-        Np = dims.Np
-
-        def ext(l):
-            dX = torch.empty(Np, dp, device=dOV.device, dtype=torch.float32)
-            K.pack_padded(dOV[:, l * d:], d * L, Np, dp, (Np, dims.N), (dp, d), dX, dp)
-            return dX
-        return self.stack.backward(sctx, ext, grads)
+        dXs = [torch.empty(dims.Np, dp, device=dOV.device, dtype=torch.float32) for _ in range(L)]
+        K.split_dropout_bwd(dOV, d * L, dims.N, dims.Np, d, dp, p, drop_seed, dXs)
+        return self.stack.backward(sctx, lambda l: dXs[l], grads)
 
 
 class UnSupTrainer:
@@ -81,32 +78,25 @@ class UnSupTrainer:
     def forward_backward(self, b: DeviceBatch, sample_ids: torch.Tensor, train: bool = True):
         core, ss = self.core, self.m.ss
         seed = self.next_seed()
-        OV, sctx = core.encode(b, train, True, seed)
-        N, D = OV.shape
         p = core.p_out if train else 0.0
         ds = site_seed(seed, 0, 0, SITE_SS_DROP)
-        if p > 0:
-            OVd = torch.empty_like(OV)
-            K.dropout(OV, D, OVd, D, N, D, p, ds)
-        else:
-            OVd = OV
+        OVd, sctx = core.encode(b, train, True, seed, p, ds)   # dropout fused into the concatenation
+        N, D = OVd.shape
         W = ss.weight
         S = sample_ids.numel()
-        lrow = torch.empty(N, device=OV.device)
-        prob = torch.empty(N, S, device=OV.device)
+        lrow = torch.empty(N, device=OVd.device)
+        prob = torch.empty(N, S, device=OVd.device)
         K.sampled_softmax_fwd(OVd, D, b.input_y, sample_ids, S, W, W.stride(0), lrow, prob, N, D)
-        if self.ws.numel() < K.colstat_ws_floats(N, 1):   # ceil(N/16) partial sums (u2gnn_hip.h)
-            self.ws = torch.empty(K.colstat_ws_floats(N, 1), device=OV.device)
-        K.colsum(lrow.view(N, 1), N, 1, 1, (1, 1), self.loss, self.ws)
+        K.sum_all(lrow, N, self.loss)
         self.last_logits = lrow   # per-node losses of the step (the reference forward's output)
         # W's gradient touches only the label rows and the S sampled rows (sampled_softmax.py:45,48):
         # the backward writes them as compact rows, folded into the dense gradient (all zero between
         # steps, so no dense zero fill of the [V, D] table) -- locally, or after the data-parallel
         # row exchange
         gW = self.flat.grads["ss.weight"]
-        dOV = torch.empty_like(OV)
-        rows_lab = torch.empty(N, D, device=OV.device)
-        rows_smp = torch.empty(S, D, device=OV.device)
+        dOV = torch.empty_like(OVd)
+        rows_lab = torch.empty(N, D, device=OVd.device)
+        rows_smp = torch.empty(S, D, device=OVd.device)
         K.sampled_softmax_bwd_rows(OVd, D, b.input_y, sample_ids, S, W, W.stride(0), prob, None, dOV, D, rows_lab,
                                    rows_smp, N, D)
         if self.row_sync is not None:
@@ -115,9 +105,7 @@ class UnSupTrainer:
             K.index_add_rows(rows_lab, b.input_y, gW)
             K.index_add_rows(rows_smp, sample_ids, gW)
             self._touched = (b.input_y, sample_ids)
-        if p > 0:
-            K.dropout(dOV, D, dOV, D, N, D, p, ds)
-        core.encode_backward(sctx, dOV, self.flat.grads)
+        core.encode_backward(sctx, dOV, self.flat.grads, p, ds)   # dropout's backward fused into the split
         return self.loss
 
     def step(self, b: DeviceBatch, sample_ids: torch.Tensor, train: bool = True):
@@ -132,8 +120,11 @@ class UnSupTrainer:
         """Zero the ss.weight gradient rows this step wrote (the dense gradient is all zero between
         steps; torch's Adam sees the same dense gradient either way)."""
         gW = self.flat.grads["ss.weight"]
-        for ids in self._touched:
-            K.index_zero_rows(ids, gW)
+        if len(self._touched) == 2:   # labels and samples: one launch
+            K.index_zero_rows2(self._touched[0], self._touched[1], gW)
+        else:
+            for ids in self._touched:
+                K.index_zero_rows(ids, gW)
         self._touched = ()
 
 

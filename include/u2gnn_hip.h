@@ -278,11 +278,38 @@ typedef struct u2gnn_reduce_job {
 int64_t u2gnn_reduce_batch_ws_floats(const u2gnn_reduce_job *jobs, int32_t n);
 int u2gnn_reduce_batch(const u2gnn_reduce_job *jobs, int32_t n, float *ws, int64_t ws_floats, void *stream);
 
-/* ABI v11: several u2gnn_gemm calls in one launch when they resolve to the same kernel (precision, tile,
- * transposes, STORE epilogue without clamp; split-K allowed): the blocks of the launch are shared out
- * over the jobs, each tile computed exactly as by its own u2gnn_gemm call (bit-identical).  Calls that do
- * not share a kernel are launched one by one.  At most 8 jobs. */
+/* ABI v11: FFN2's epilogue for d <= 64 encoders when the product runs split-K (too few row-complete tiles):
+ * Z = resid + drop(sum_z src[z] + bias) (dropout hash of U2GNN_EPI_BIAS_DROP_RESID), then the LayerNorm of
+ * EPI_BIAS_DROP_RESID_LN over the first d columns: Y, mean, rstd (rows >= rows_valid: 0).  Padded width
+ * 64 (one wave per row); bias / resid padded to 64 columns, gamma / beta unpadded [d]. */
+int u2gnn_slab_bias_drop_resid_ln(const float *src, int32_t n_slab, int64_t slab_stride, int64_t ld_src,
+                                   const float *bias, const float *resid, int64_t ld_res, float p, uint64_t seed,
+                                   float *Z, int64_t ldz, const float *gamma, const float *beta, float *Y, int64_t ldy,
+                                   float *mean, float *rstd, int64_t d, int64_t rows_valid, int64_t rows_pad, float eps,
+                                   void *stream);
+
+/* ABI v11: several u2gnn_gemm calls in one launch when they resolve to one grouped kernel: the same
+ * bf16 precision and tile (64, 129 or 256), STORE epilogue (split-K allowed), B not transposed, each job
+ * A^T B, A^T B with clamp_a, or A B.  The blocks of the launch are shared out over the jobs, each tile
+ * computed exactly as by its own u2gnn_gemm call (bit-identical).  Otherwise the calls are launched one by
+ * one.  At most 8 jobs. */
 int u2gnn_gemm_group(const u2gnn_gemm_args *args, int32_t n, void *stream);
+
+/* ---- ABI v11: UnSup head glue (pytorch_U2GNN_UnSup.py:52-69; the TF model's dropout before the sampled
+ * softmax, U2GNN_tf/model_U2GNN_Unsup_multi.py:43-56) ---------------------------------------------------
+ * u2gnn_concat_dropout: Y[r, l*d + c] = drop(src[l][r*ld_src + c]) for r < N, c < d, l < L (L <= 8; src a
+ * HOST array of L device pointers; the mask of u2gnn_dropout(Y) over Y's indices; p = 0: a copy).
+ * u2gnn_split_dropout_bwd: dst[l][r*dp + c] = drop(dY[r, l*d + c]) (same mask) for r < N, c < d, and 0 on
+ * the padding (r < Np, c < dp): the layers' padded input gradients.
+ * u2gnn_sum: out[0] = sum of x[0, n) in a fixed order (one block).
+ * u2gnn_index_zero_rows2: u2gnn_index_zero_rows over two index sets in one launch (the sets may overlap). */
+int u2gnn_concat_dropout(const float *const *src, int32_t L, int64_t ld_src, int64_t N, int64_t d, float p,
+                         uint64_t seed, float *Y, int64_t ldy, void *stream);
+int u2gnn_split_dropout_bwd(const float *dY, int64_t ldy, int32_t L, int64_t N, int64_t Np, int64_t d, int64_t dp,
+                            float p, uint64_t seed, float *const *dst, void *stream);
+int u2gnn_sum(const float *x, int64_t n, float *out, void *stream);
+int u2gnn_index_zero_rows2(const int64_t *idx_a, int64_t n_a, const int64_t *idx_b, int64_t n_b, float *dst,
+                           int64_t ld_dst, int64_t dst_rows, int64_t D, int32_t *err, void *stream);
 
 /* ---- a5/a6: sum pooling + dropout + per-layer head  (pytorch_U2GNN_Sup.py:41-44) ------
  * G[b, c] = drop(sum_{e in [rowptr[b], rowptr[b+1])} vals[e] * X[colidx[e], c]), c < d;

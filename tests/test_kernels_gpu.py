@@ -690,3 +690,105 @@ def test_gemm_group_mixed_configurations_fall_back():
     K.gemm_group([k1, k2])
     torch.cuda.synchronize()
     assert torch.equal(c1, r1) and torch.equal(c2, r2)
+
+
+@pytest.mark.parametrize("prec", ["bf16x3", "bf16"])
+@pytest.mark.parametrize("tile,Np,dp,split", [(64, 512, 64, 7), (256, 1024, 128, 4)])
+def test_gemm_group_attention_layouts(prec, tile, Np, dp, split):
+    # the attention backward's products in one launch: dV = clamp0(Pd)^T dO, dQ = dS K, dK = dS^T Q
+    Pd = _mk(Np, Np, seed=3)            # signed image: negative entries are read as 0 (clamp_a)
+    dS, dO, QKV = _mk(Np, Np, seed=4), _mk(Np, dp, seed=5), _mk(Np, 3 * dp, seed=6)
+    base = dict(M=Np, N=dp, K=Np, ldc=dp, split_k=split, slab_stride=Np * dp, precision=prec, tile=tile)
+    jobs = [dict(base, A=Pd, B=dO, lda=Np, ldb=dp, trans_a=True, clamp_a=True),
+            dict(base, A=dS, B=QKV[:, dp:], lda=Np, ldb=3 * dp, alpha=0.25),
+            dict(base, A=dS, B=QKV, lda=Np, ldb=3 * dp, trans_a=True)]
+    outs, refs = [], []
+    for kw in jobs:
+        r = torch.full((split, Np, dp), float("nan"), device=DEV)
+        K.gemm(**dict(kw, C=r))
+        kw["C"] = torch.full_like(r, float("nan"))
+        outs.append(kw["C"])
+        refs.append(r)
+    K.gemm_group(jobs)
+    torch.cuda.synchronize()
+    for o, r in zip(outs, refs):
+        assert torch.isfinite(o).all()
+        assert torch.equal(o, r)
+
+
+# ---- ABI v11: UnSup head glue, each against the launches it replaces ----
+@pytest.mark.parametrize("L,p", [(1, 0.5), (3, 0.3), (2, 0.0)])
+def test_concat_and_split_dropout_equal_separate_launches(L, p):
+    N, Np, d, dp, seed = 1914, 2048, 4, 64, 1234567
+    outs = [_mk(Np, dp, seed=40 + l) for l in range(L)]
+    D = d * L
+    OV = torch.empty(N, D, device=DEV)
+    for l in range(L):
+        K.slab_reduce(outs[l], 1, 0, N, dp, dp, (N, N), (dp, d), OV[:, l * d:], D)
+    ref = torch.empty_like(OV)
+    K.dropout(OV, D, ref, D, N, D, p, seed) if p > 0 else ref.copy_(OV)
+    got = torch.full_like(OV, float("nan"))
+    K.concat_dropout(outs, dp, N, d, got, D, p, seed)
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref)
+    dY = _mk(N, D, seed=50)
+    dd = dY.clone()
+    if p > 0:
+        K.dropout(dd, D, dd, D, N, D, p, seed)
+    refs = []
+    for l in range(L):
+        r = torch.empty(Np, dp, device=DEV)
+        K.pack_padded(dd[:, l * d:], D, Np, dp, (Np, N), (dp, d), r, dp)
+        refs.append(r)
+    gots = [torch.full((Np, dp), float("nan"), device=DEV) for _ in range(L)]
+    K.split_dropout_bwd(dY, D, N, Np, d, dp, p, seed, gots)
+    torch.cuda.synchronize()
+    for g_, r in zip(gots, refs):
+        assert torch.equal(g_, r)
+
+
+@pytest.mark.parametrize("n", [1, 1000, 1914, 70001])
+def test_sum_all_and_index_zero_rows2(n):
+    x = _mk(n, seed=60)
+    out = torch.full((1,), float("nan"), device=DEV)
+    K.sum_all(x, n, out)
+    torch.cuda.synchronize()
+    assert abs(out.item() - x.double().sum().item()) <= 1e-5 * max(1.0, x.abs().sum().item())
+    W = _mk(500, 4, seed=61)
+    a = torch.tensor([3, 7, 499], device=DEV)
+    b = torch.tensor([7, 0], device=DEV)
+    ref = W.clone()
+    ref[a] = 0
+    ref[b] = 0
+    K.index_zero_rows2(a, b, W)
+    torch.cuda.synchronize()
+    assert torch.equal(W, ref)
+
+
+@pytest.mark.parametrize("d,p", [(4, 0.5), (19, 0.0), (64, 0.3)])
+def test_slab_bias_drop_resid_ln_against_fp64(d, p):
+    rows, Np, n_slab, seed, eps = 1914, 2048, 8, 987654321, 1e-5
+    slabs = _mk(n_slab, Np, 64, seed=70)
+    bias = torch.zeros(64, device=DEV)
+    bias[:d] = _mk(d, seed=71)
+    resid = _mk(Np, 64, seed=72)
+    gamma, beta = _mk(d, seed=73), _mk(d, seed=74)
+    Z, Y = torch.full((Np, 64), float("nan"), device=DEV), torch.full((Np, 64), float("nan"), device=DEV)
+    mean, rstd = torch.full((Np,), float("nan"), device=DEV), torch.full((Np,), float("nan"), device=DEV)
+    K.slab_bias_drop_resid_ln(slabs, n_slab, Np * 64, bias, resid, p, seed, Z, gamma, beta, Y, mean, rstd, d, rows, Np,
+                              eps)
+    torch.cuda.synchronize()
+    x = slabs.double().sum(0) + bias.double()
+    if p > 0:
+        keep = K.dropout_mask(seed, Np, 64, p).bool()
+        x = torch.where(keep, x / (1 - p), torch.zeros_like(x))
+    zr = resid.double() + x
+    assert ((Z.double() - zr).abs().max() / zr.abs().max()).item() < 1e-6
+    zd = Z.double()[:, :d]
+    mu = zd.mean(1, keepdim=True)
+    rs = 1.0 / torch.sqrt(((zd - mu) ** 2).mean(1, keepdim=True) + eps)
+    yr = torch.zeros(Np, 64, dtype=torch.float64, device=DEV)
+    yr[:rows, :d] = ((zd - mu) * rs * gamma.double() + beta.double())[:rows]
+    assert (Y.double() - yr).abs().max().item() < 1e-4
+    assert torch.equal(mean[rows:], torch.zeros_like(mean[rows:])) and torch.equal(rstd[rows:], torch.zeros_like(rstd[rows:]))
+    assert (mean[:rows].double() - mu[:rows, 0]).abs().max().item() < 1e-5

@@ -210,7 +210,8 @@ constexpr int64_t kSplitTarget = 448, kSplitTarget256 = 240;
 int gemm_split(Arena &W, const Dims &D, const float *A, const float *B, float *C, int64_t M, int64_t N, int64_t Kd,
                int64_t lda, int64_t ldb, int64_t ldc, bool ta, float alpha, bool accumulate, const int64_t *rblk,
                const int64_t *cblk, bool deep, hipStream_t st, bool clamp_a = false, int prec = -1, int role = 0,
-               hipStream_t red_st = nullptr, Defer *df = nullptr) {
+               hipStream_t red_st = nullptr, Defer *df = nullptr, float **slabs_out = nullptr,
+               int64_t *nslab_out = nullptr) {
     if (prec < 0) prec = D.prec;
     const bool f32 = prec == U2GNN_PREC_F32;
     const int64_t bk = f32 ? 16 : 32;
@@ -295,6 +296,10 @@ int gemm_split(Arena &W, const Dims &D, const float *A, const float *B, float *C
     probe_mark(role, false, st, plan);
     U2GNN_TRY(g.run(st, plan));
     probe_mark(role, true, st, plan);
+    if (slabs_out) {   // the consumer sums the slabs itself (u2gnn_layernorm_bwd_delta_slabs)
+        *slabs_out = slabs, *nslab_out = split;
+        return U2GNN_OK;
+    }
     if (plan) return U2GNN_OK;
     hipStream_t rs = st;
     if (red_st && red_st != st) {
@@ -590,8 +595,14 @@ int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
         U2GNN_TRY(gg.run(st, plan));
     }
     U2GNN_TRY(wgrad(W, D, dF, dp, c.Hd, ffp, dp, ffp, g->l2_w, ff, blk_d, blk_ff, so, df));   // side (forked above)
+    // one-stream layers in the matrix-core precisions: a split-K dX1 product leaves its slabs to LayerNorm1's
+    // backward, which completes dX1 before using it (the separate reduce launch goes; same bits)
+    const bool ln_delta = !D.window && prec != U2GNN_PREC_F32;
+    float *dx1_slabs = nullptr;
+    int64_t dx1_nslab = 0;
     U2GNN_TRY(gemm_split(W, D, dH, w->W1, dX1, Np, dp, ffp, ffp, dp, dp, false, 1.f, true, nullptr, nullptr, false,
-                         st));
+                         st, false, -1, 0, nullptr, nullptr, (ln_delta && so == st) ? &dx1_slabs : nullptr,
+                         &dx1_nslab));
     U2GNN_TRY(sd.fork());
     U2GNN_TRY(wgrad(W, D, dH, ffp, c.X1, dp, ffp, dp, g->l1_w, d, blk_ff, blk_d, so, df));
     U2GNN_TRY(bias_grad(W, dH, Np, ffp, ffp, ffp, ff, g->l1_b, so, df));
@@ -602,9 +613,12 @@ int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
     float *dX_scratch = W.take<float>(Np * dp);   // taken in every mode so the plan covers it
     if (!need_dx) dX = dX_scratch;
     // node attention: LayerNorm1's backward also forms delta = rowsum(dO * O) for the dS epilogue
-    const bool ln_delta = !D.window && prec != U2GNN_PREC_F32;
     float *delta_ln = ln_delta ? W.take<float>(Np) : nullptr;
-    if (!plan && ln_delta)
+    if (!plan && ln_delta && dx1_slabs)
+        U2GNN_TRY(u2gnn_layernorm_bwd_delta_slabs(dX1, dp, dx1_slabs, (int32_t)dx1_nslab, Np * dp, c.Z1, dp, c.mean1,
+                                                  c.rstd1, w->n1_w, dX, dp, dA, dp, pd, s->drop1, N, Np, d, dp, X, dp,
+                                                  w->b_o, delta_ln, st));
+    else if (!plan && ln_delta)
         U2GNN_TRY(u2gnn_layernorm_bwd_delta(dX1, dp, c.Z1, dp, c.mean1, c.rstd1, w->n1_w, dX, dp, dA, dp, pd,
                                             s->drop1, N, Np, d, dp, X, dp, w->b_o, delta_ln, st));
     else if (!plan)

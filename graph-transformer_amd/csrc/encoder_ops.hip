@@ -178,22 +178,9 @@ __device__ __forceinline__ float4 add4(float4 a, float4 b) { return make_float4(
 // One wave per padded row, a float4 of columns per lane; the slab loop keeps 4 independent
 // 16-byte loads in flight.  Rows/columns outside the real blocks are skipped; the real
 // destination is written with 16-byte stores when the column map is the identity and aligned.
-// The bodies of the reduction kernels take their block coordinates as arguments, so that the batched
-// launch (reduce_batch_kernel, u2gnn_reduce_batch) runs the very same per-element arithmetic.
-__device__ __forceinline__ void slab_reduce_body(const float *src, int n_slab, int64_t slab_stride, int64_t rows_pad,
-                                                 int64_t cols_pad, int64_t ld_src, int64_t rbp, int64_t rbr,
-                                                 int64_t cbp, int64_t cbr, float *dst, int64_t ld_dst, float alpha,
-                                                 int accumulate, int vec_store, int64_t i) {
-    // one float4 of the output per thread (weight-gradient outputs have only d or ff rows: a wave per
-    // row left the chip latency-bound); 8 slab loads in flight, summed in the fixed order
-    // a += s0, s4, ...; b += s1, s5, ...; e += s2, ...; f += s3, ...; then (a + b) + (e + f)
-    const int64_t c4 = cols_pad >> 2;
-    if (i >= rows_pad * c4) return;
-    const int64_t r = i / c4, c = (i - r * c4) * 4;
-    bool vr;
-    const int64_t rr = blk_map(r, rbp, rbr, &vr);
-    if (!vr) return;
-    const float *p = src + r * ld_src + c;
+// sum of n_slab float4 slices at p, p + slab_stride, ... in the fixed order of every slab reduction:
+// a += s0, s4, ...; b += s1, s5, ...; e += s2, ...; f += s3, ...; then (a + b) + (e + f); 8 loads in flight
+__device__ __forceinline__ float4 slab_sum4(const float *p, int n_slab, int64_t slab_stride) {
     float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a, e = a, f = a;
     int z = 0;
     for (; z + 8 <= n_slab; z += 8) {
@@ -211,7 +198,25 @@ __device__ __forceinline__ void slab_reduce_body(const float *src, int n_slab, i
         z += 4;
     }
     for (; z < n_slab; ++z) a = add4(a, ld4(p + (int64_t)z * slab_stride));
-    const float4 t = add4(add4(a, b), add4(e, f));
+    return add4(add4(a, b), add4(e, f));
+}
+
+// The bodies of the reduction kernels take their block coordinates as arguments, so that the batched
+// launch (reduce_batch_kernel, u2gnn_reduce_batch) runs the very same per-element arithmetic.
+__device__ __forceinline__ void slab_reduce_body(const float *src, int n_slab, int64_t slab_stride, int64_t rows_pad,
+                                                 int64_t cols_pad, int64_t ld_src, int64_t rbp, int64_t rbr,
+                                                 int64_t cbp, int64_t cbr, float *dst, int64_t ld_dst, float alpha,
+                                                 int accumulate, int vec_store, int64_t i) {
+    // one float4 of the output per thread (weight-gradient outputs have only d or ff rows: a wave per
+    // row left the chip latency-bound); 8 slab loads in flight, summed in the fixed order
+    // a += s0, s4, ...; b += s1, s5, ...; e += s2, ...; f += s3, ...; then (a + b) + (e + f)
+    const int64_t c4 = cols_pad >> 2;
+    if (i >= rows_pad * c4) return;
+    const int64_t r = i / c4, c = (i - r * c4) * 4;
+    bool vr;
+    const int64_t rr = blk_map(r, rbp, rbr, &vr);
+    if (!vr) return;
+    const float4 t = slab_sum4(src + r * ld_src + c, n_slab, slab_stride);
     if (vec_store) {
         float *o = dst + rr * ld_dst + c;
         float4 v = make_float4(alpha * t.x, alpha * t.y, alpha * t.z, alpha * t.w);
@@ -756,9 +761,14 @@ struct LnDelta {
     int64_t ldx;
     const float *bias;   // [d_pad], zero-padded (the out-projection's padded bias)
     float *delta;        // [rows_pad]
+    // SLABS (u2gnn_layernorm_bwd_delta_slabs): dY += the split-K slabs of the FFN's dX1 product first
+    // (slab_sum4's order, the result written back to dY: u2gnn_slab_reduce accumulate fused in)
+    const float *slabs;
+    int64_t slab_stride;
+    int n_slab;
 };
 
-template <int LN_V4, bool DELTA>
+template <int LN_V4, bool DELTA, bool SLABS = false>
 __global__ void __launch_bounds__(256) layernorm_bwd_kernel(const float *dY, int64_t ldy, const float *Z, int64_t ldz,
                                                             const float *mean, const float *rstd, const float *gamma,
                                                             float *dZ, int64_t lddz, float *dZd, int64_t lddrop,
@@ -791,6 +801,12 @@ __global__ void __launch_bounds__(256) layernorm_bwd_kernel(const float *dY, int
         const int64_t c = 4 * (hl + 32 * i);
         ta[i] = c < d_pad ? ld4(dy + c) : z4;
         tb[i] = c < d_pad ? ld4(z + c) : z4;
+        if constexpr (SLABS) {
+            if (c < d_pad) {
+                ta[i] = add4(slab_sum4(dt.slabs + row * ldy + c, dt.n_slab, dt.slab_stride), ta[i]);
+                *reinterpret_cast<float4 *>(const_cast<float *>(dy) + c) = ta[i];
+            }
+        }
         if constexpr (DELTA) {
             tx[i] = c < d_pad ? ld4(dt.X + row * dt.ldx + c) : z4;
             tc[i] = c < d_pad ? ld4(dt.bias + c) : z4;
@@ -1373,6 +1389,7 @@ int layernorm_bwd_launch(const float *dY, int64_t ldy, const float *Z, int64_t l
                          const LnDelta *dt, void *stream) {
     if (!dY || !Z || !mean || !rstd || !gamma || !dZ || d < 1 || d > d_pad || d_pad > LN_MAXV * 64)
         return U2GNN_E_ARG;
+    if (dt && dt->slabs && (dt->n_slab < 1 || !al16(dt->slabs) || (dt->slab_stride & 3))) return U2GNN_E_ARG;
     if (!al16(dY) || !al16(Z) || !al16(dZ) || (ldy & 3) || (ldz & 3) || (lddz & 3) || (d_pad & 3) ||
         (dZdrop && (!al16(dZdrop) || (lddrop & 3))))
         return U2GNN_E_ALIGN;
@@ -1380,10 +1397,14 @@ int layernorm_bwd_launch(const float *dY, int64_t ldy, const float *Z, int64_t l
     if (dt && (!al16(dt->X) || !al16(dt->bias) || (dt->ldx & 3))) return U2GNN_E_ALIGN;
     const dim3 gr(grid_for(rows_pad, 8, 1 << 30));
     hipStream_t st = u2gnn_stream(stream);
-    const LnDelta none{nullptr, 0, nullptr, nullptr};
+    const LnDelta none{nullptr, 0, nullptr, nullptr, nullptr, 0, 0};
 #define U2GNN_LNB(V)                                                                                                   \
     do {                                                                                                               \
-        if (dt)                                                                                                        \
+        if (dt && dt->slabs)                                                                                           \
+            hipLaunchKernelGGL((layernorm_bwd_kernel<V, true, true>), gr, dim3(256), 0, st, dY, ldy, Z, ldz, mean,    \
+                               rstd, gamma, dZ, lddz, dZdrop, lddrop, p, seed, u2gnn_g_epoch, rows_valid, rows_pad, d, \
+                               d_pad, *dt);                                                                            \
+        else if (dt)                                                                                                   \
             hipLaunchKernelGGL((layernorm_bwd_kernel<V, true>), gr, dim3(256), 0, st, dY, ldy, Z, ldz, mean, rstd,    \
                                gamma, dZ, lddz, dZdrop, lddrop, p, seed, u2gnn_g_epoch, rows_valid, rows_pad, d,       \
                                d_pad, *dt);                                                                            \
@@ -1416,7 +1437,18 @@ int u2gnn_layernorm_bwd_delta(const float *dY, int64_t ldy, const float *Z, int6
                               int64_t lddrop, float p, uint64_t seed, int64_t rows_valid, int64_t rows_pad, int64_t d,
                               int64_t d_pad, const float *X, int64_t ldx, const float *bias, float *delta,
                               void *stream) {
-    const LnDelta dt{X, ldx, bias, delta};
+    const LnDelta dt{X, ldx, bias, delta, nullptr, 0, 0};
+    return layernorm_bwd_launch(dY, ldy, Z, ldz, mean, rstd, gamma, dZ, lddz, dZdrop, lddrop, p, seed, rows_valid,
+                                rows_pad, d, d_pad, &dt, stream);
+}
+
+int u2gnn_layernorm_bwd_delta_slabs(float *dY, int64_t ldy, const float *slabs, int32_t n_slab, int64_t slab_stride,
+                                    const float *Z, int64_t ldz, const float *mean, const float *rstd,
+                                    const float *gamma, float *dZ, int64_t lddz, float *dZdrop, int64_t lddrop, float p,
+                                    uint64_t seed, int64_t rows_valid, int64_t rows_pad, int64_t d, int64_t d_pad,
+                                    const float *X, int64_t ldx, const float *bias, float *delta, void *stream) {
+    if (!slabs) return U2GNN_E_ARG;
+    const LnDelta dt{X, ldx, bias, delta, slabs, slab_stride, (int)n_slab};
     return layernorm_bwd_launch(dY, ldy, Z, ldz, mean, rstd, gamma, dZ, lddz, dZdrop, lddrop, p, seed, rows_valid,
                                 rows_pad, d, d_pad, &dt, stream);
 }

@@ -187,7 +187,18 @@ __global__ void __launch_bounds__(256) sqnorm_partial_kernel(const float *g, int
     double s = 0.0;
     const int64_t n4 = n >> 2;
     const float4 *g4 = reinterpret_cast<const float4 *>(g);
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    // 4 float4 loads in flight per thread (one at a time left the 41 MB C5 sweep at 3 TB/s)
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    for (; i + 3 * stride < n4; i += 4 * stride) {
+        float4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = g4[i + u * stride];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            s += (double)v[u].x * v[u].x + (double)v[u].y * v[u].y + (double)v[u].z * v[u].z + (double)v[u].w * v[u].w;
+    }
+    for (; i < n4; i += stride) {
         const float4 v = g4[i];
         s += (double)v.x * v.x + (double)v.y * v.y + (double)v.z * v.z + (double)v.w * v.w;
     }
@@ -275,12 +286,21 @@ __global__ void __launch_bounds__(256) ss_fwd_kernel(const float *X, int64_t ldx
     __shared__ float red[8];
     const int64_t i = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    // independent loads first: this thread's first two sample ids and the label (the dependent W-row
+    // loads follow; the serial chain of the first form cost ~15 us at C5)
+    const int64_t sid0 = tid < S ? sids[tid] : 0, sid1 = tid + 256 < S ? sids[tid + 256] : 0;
+    const int64_t yl = tid == 0 ? labels[i] : 0;
     for (int64_t c = tid; c < D; c += 256) xs[c] = X[i * ldx + c];
     __syncthreads();
+    float tlab = 0.f;
+    if (tid == 0) {
+        const float *wy = W + yl * ldw;
+        for (int64_t c = 0; c < D; ++c) tlab += xs[c] * wy[c];
+    }
     float m = -INFINITY, s = 0.f;
     float *pr = prob + i * S;
     for (int64_t j = tid; j < S; j += 256) {
-        const float *wr = W + sids[j] * ldw;
+        const float *wr = W + (j == tid ? sid0 : j == tid + 256 ? sid1 : sids[j]) * ldw;
         float dot = 0.f;
         for (int64_t c = 0; c < D; ++c) dot += xs[c] * wr[c];
         pr[j] = dot;  // logits, normalised below
@@ -301,12 +321,7 @@ __global__ void __launch_bounds__(256) ss_fwd_kernel(const float *X, int64_t ldx
     for (int k = 0; k < 4; ++k) tot += red[k] == -INFINITY ? 0.f : red[4 + k] * expf(red[k] - M);
     const float lse = M + logf(tot);
     for (int64_t j = tid; j < S; j += 256) pr[j] = expf(pr[j] - lse);
-    if (tid == 0) {
-        const float *wy = W + labels[i] * ldw;
-        float t = 0.f;
-        for (int64_t c = 0; c < D; ++c) t += xs[c] * wy[c];
-        loss[i] = lse - t;
-    }
+    if (tid == 0) loss[i] = lse - tlab;
 }
 
 // Block-wide sum of SS_CH per-thread partials (fixed shuffle tree + fixed 4-wave order, so the
@@ -344,7 +359,24 @@ __global__ void __launch_bounds__(256) ss_bwd_x_kernel(const float *X, int64_t l
         float acc[SS_CH], tot[SS_CH];
 #pragma unroll
         for (int k = 0; k < SS_CH; ++k) acc[k] = 0.f;
-        for (int64_t j = tid; j < S; j += 256) {
+        int64_t j0 = tid;
+        for (; j0 + 256 < S; j0 += 512) {   // two samples' loads in flight, summed in sample order
+            const float p0 = pr[j0], p1 = pr[j0 + 256];
+            const float *w0 = W + sids[j0] * ldw + c0, *w1 = W + sids[j0 + 256] * ldw + c0;
+            float v0[SS_CH], v1[SS_CH];
+#pragma unroll
+            for (int k = 0; k < SS_CH; ++k) {
+                v0[k] = c0 + k < D ? w0[k] : 0.f;
+                v1[k] = c0 + k < D ? w1[k] : 0.f;
+            }
+#pragma unroll
+            for (int k = 0; k < SS_CH; ++k)
+                if (c0 + k < D) acc[k] += p0 * v0[k];
+#pragma unroll
+            for (int k = 0; k < SS_CH; ++k)
+                if (c0 + k < D) acc[k] += p1 * v1[k];
+        }
+        for (int64_t j = j0; j < S; j += 256) {
             const float pj = pr[j];
             const float *wr = W + sids[j] * ldw + c0;
 #pragma unroll
@@ -381,7 +413,25 @@ __global__ void __launch_bounds__(256) ss_bwd_w_kernel(const float *X, int64_t l
         float acc[SS_CH], tot[SS_CH];
 #pragma unroll
         for (int k = 0; k < SS_CH; ++k) acc[k] = 0.f;
-        for (int64_t i = tid; i < n_rows; i += 256) {
+        // 8 rows' loads in flight per thread (the strided prob column and the X rows), then the FMAs in
+        // row order (the same sums as one row at a time)
+        int64_t i0 = tid;
+        for (; i0 + 7 * 256 < n_rows; i0 += 8 * 256) {
+            float f[8], xv[8][SS_CH];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int64_t i = i0 + u * 256;
+                f[u] = (dloss ? dloss[i] : 1.f) * prob[i * S + j];
+#pragma unroll
+                for (int k = 0; k < SS_CH; ++k) xv[u][k] = c0 + k < D ? X[i * ldx + c0 + k] : 0.f;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+#pragma unroll
+                for (int k = 0; k < SS_CH; ++k)
+                    if (c0 + k < D) acc[k] += f[u] * xv[u][k];
+        }
+        for (int64_t i = i0; i < n_rows; i += 256) {
             const float f = (dloss ? dloss[i] : 1.f) * prob[i * S + j];
             const float *xr = X + i * ldx + c0;
 #pragma unroll
@@ -619,7 +669,7 @@ int u2gnn_smoothed_ce(const float *scores, const int64_t *labels, int64_t B, int
 
 int u2gnn_sqnorm(const float *g, int64_t n, float *ws, float *sqnorm, void *stream) {
     if (!g || !ws || !sqnorm || (reinterpret_cast<uintptr_t>(g) & 15)) return U2GNN_E_ARG;
-    const unsigned nb = grid_for(n, 256 * 8, 512);
+    const unsigned nb = grid_for(n, 256 * 16, 512);   // ws holds 512 doubles (u2gnn_hip.h)
     hipStream_t st = u2gnn_stream(stream);
     double *wsd = reinterpret_cast<double *>(ws);
     hipLaunchKernelGGL(sqnorm_partial_kernel, dim3(nb), dim3(256), 0, st, g, n, wsd);

@@ -295,6 +295,17 @@ def layernorm_bwd(dY, ldy, Z, ldz, mean, rstd, gamma, dZ, lddz, dZdrop, lddrop, 
                                         int(rows_pad), int(d), int(d_pad), _s()), "u2gnn_layernorm_bwd")
 
 
+def layernorm_bwd_delta_slabs(dY, ldy, slabs, n_slab, slab_stride, Z, ldz, mean, rstd, gamma, dZ, lddz, dZdrop,
+                              lddrop, p, seed, rows_valid, rows_pad, d, d_pad, X, ldx, bias, delta):
+    """layernorm_bwd_delta after dY += the split-K slabs (slab_reduce's order, written back; ABI v11)."""
+    _dev(dY, slabs, Z, mean, rstd, gamma, dZ, X, bias, delta)
+    check(hip_lib().u2gnn_layernorm_bwd_delta_slabs(_p(dY), int(ldy), _p(slabs), int(n_slab), int(slab_stride), _p(Z),
+                                                    int(ldz), _p(mean), _p(rstd), _p(gamma), _p(dZ), int(lddz),
+                                                    _p(dZdrop), int(lddrop), float(p), int(seed), int(rows_valid),
+                                                    int(rows_pad), int(d), int(d_pad), _p(X), int(ldx), _p(bias),
+                                                    _p(delta), _s()), "u2gnn_layernorm_bwd_delta_slabs")
+
+
 def layernorm_bwd_delta(dY, ldy, Z, ldz, mean, rstd, gamma, dZ, lddz, dZdrop, lddrop, p, seed, rows_valid, rows_pad, d,
                         d_pad, X, ldx, bias, delta):
     """layernorm_bwd of an encoder layer's LayerNorm1 that also writes the attention backward's delta

@@ -238,6 +238,14 @@ int u2gnn_layernorm_bwd_delta(const float *dY, int64_t ldy, const float *Z, int6
                               int64_t lddrop, float p, uint64_t seed, int64_t rows_valid, int64_t rows_pad,
                               int64_t d, int64_t d_pad, const float *X, int64_t ldx, const float *bias,
                               float *delta, void *stream);
+/* ABI v11: u2gnn_layernorm_bwd_delta whose dY is first completed by split-K slabs: dY[r, c] += sum_z
+ * slabs[z*slab_stride + r*ldy + c] (u2gnn_slab_reduce's summation order, accumulate; written back to dY for
+ * rows < rows_valid) -- the FFN's dX1 += dH W1 product of a one-stream layer without its reduce launch. */
+int u2gnn_layernorm_bwd_delta_slabs(float *dY, int64_t ldy, const float *slabs, int32_t n_slab, int64_t slab_stride,
+                                    const float *Z, int64_t ldz, const float *mean, const float *rstd,
+                                    const float *gamma, float *dZ, int64_t lddz, float *dZdrop, int64_t lddrop, float p,
+                                    uint64_t seed, int64_t rows_valid, int64_t rows_pad, int64_t d, int64_t d_pad,
+                                    const float *X, int64_t ldx, const float *bias, float *delta, void *stream);
 /* LN parameter gradients: dgamma[c] = sum_r dY*xhat, dbeta[c] = sum_r dY (c < d) and, when
  * dbias != NULL, dbias[c] = sum_r dZdrop[r, c] (bias of the linear whose output was dropped into
  * the residual: out_proj.bias for norm1, linear2.bias for norm2).  Deterministic two-pass column

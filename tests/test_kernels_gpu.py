@@ -792,3 +792,29 @@ def test_slab_bias_drop_resid_ln_against_fp64(d, p):
     assert (Y.double() - yr).abs().max().item() < 1e-4
     assert torch.equal(mean[rows:], torch.zeros_like(mean[rows:])) and torch.equal(rstd[rows:], torch.zeros_like(rstd[rows:]))
     assert (mean[:rows].double() - mu[:rows, 0]).abs().max().item() < 1e-5
+
+
+@pytest.mark.parametrize("N,Np,d,dp,n_slab", [(1914, 2048, 4, 64, 14), (300, 384, 19, 64, 5), (1000, 1024, 367, 384, 3)])
+def test_layernorm_bwd_delta_slabs_equals_reduce_then_ln(N, Np, d, dp, n_slab):
+    p, seed = 0.5, 4242
+    g = torch.Generator(device=DEV).manual_seed(5)
+    rn = lambda *s: torch.randn(*s, device=DEV, generator=g)   # noqa: E731
+    base, slabs, Z, X = rn(Np, dp), rn(n_slab, Np, dp), rn(Np, dp), rn(Np, dp)
+    mean, rstd, gamma = rn(Np), rn(Np).abs() + 0.5, rn(d)
+    bias = torch.zeros(dp, device=DEV)
+    bias[:d] = rn(d)
+    outs = []
+    for fused in (False, True):
+        dY = base.clone()
+        dZ, dA, delta = torch.empty(Np, dp, device=DEV), torch.empty(Np, dp, device=DEV), torch.empty(Np, device=DEV)
+        if fused:
+            K.layernorm_bwd_delta_slabs(dY, dp, slabs, n_slab, Np * dp, Z, dp, mean, rstd, gamma, dZ, dp, dA, dp, p, seed,
+                                        N, Np, d, dp, X, dp, bias, delta)
+        else:
+            K.slab_reduce(slabs, n_slab, Np * dp, Np, dp, dp, (Np, Np), (dp, dp), dY, dp, accumulate=True)
+            K.layernorm_bwd_delta(dY, dp, Z, dp, mean, rstd, gamma, dZ, dp, dA, dp, p, seed, N, Np, d, dp, X, dp, bias,
+                                  delta)
+        outs.append((dY[:N], dZ, dA, delta))
+    torch.cuda.synchronize()
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)

@@ -286,6 +286,41 @@ def unsup_cpu_baseline(hbs, sids, sd, V, T, lr, steps):
                       f"median {t:.2f} s/step, oracle/u2gnn_oracle.py on torch CPU, {threads} threads"}
 
 
+def c5_group_roofline(args, trainer, batches, elapsed):
+    """C5's dominant launch: the attention backward's grouped dV / dQ / dK product (one launch per layer on the
+    one-stream schedule, gemm_bf16_group_kernel<64, 64, ...>; the largest per-launch device time of the C5
+    rocprof summary, profiles/r03).  Timed live by the executor's probe (HIP events around the grouped launch
+    on its stream) over args.steps EAGER steps after the timed graph-replay region (events recorded inside a
+    captured graph would belong to the capture).  Algorithmic FLOPs: 3 products x 2 N^2 d (real dims)."""
+    from u2gnn_hip import _lib as LIB
+    from u2gnn_hip import native
+    if not native.enabled():
+        return None
+    per_step = args.num_hidden_layers * args.num_timesteps
+    nb = len(batches)
+    steps = max(4, args.steps)
+    torch.cuda.synchronize()
+    native.probe_arm(LIB.ROLE_DQ, steps * per_step)
+    for i in range(steps):
+        trainer.step(*batches[i % nb])
+    torch.cuda.synchronize()
+    ms, n = native.probe_collect()
+    if n != steps * per_step or ms <= 0.0:
+        return None
+    d = 4   # REDDIT-M5K features (X = 0.01 * ones[n, 4])
+    fl = float(sum(per_step * 3 * 2.0 * batches[i % nb][0].N ** 2 * d for i in range(steps)))
+    ach = fl / (ms * 1e-3) / 1e12
+    peak = PEAK[args.precision if args.precision in PEAK else "bf16x3"]
+    return {"bound": "mfma", "achieved": round(ach, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
+            "frac": round(ach / peak, 4), "traffic": None,
+            "kernel": "gemm_bf16_group_kernel<64, 64, 2, 2, 32, true> (grouped dV = Pd^T dO, dQ = dS K, dK = dS^T Q)",
+            "role": "attention-backward group", "launches": n, "avg_launch_us": round(1e3 * ms / n, 1),
+            "algorithmic_flop_per_launch": round(fl / n),
+            "timing": "live: HIP events around each grouped launch, eager steps after the timed region",
+            "dominance": "largest per-launch device time of the C5 step (rocprof summary, DESIGN.md section 5.6); "
+                         "C5 is launch-bound: ~100 launches per step, none above ~9 % of it"}
+
+
 def main_c5(args):
     """synthetic REDDIT-MULTI-5K (4999 graphs, mean 508.5 nodes, V = sum of
     nodes ~2.54M), batch 4, k=16, T=4, ff=1024, 512 sampled classes, D = 4.  HBM-bound: the
@@ -360,7 +395,7 @@ def main_c5(args):
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    roof = None
+    roof = opt_roof = None
     if not args.no_roofline:
         n = trainer.flat.n
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -373,11 +408,13 @@ def main_c5(args):
         us = e0.elapsed_time(e1) * 1e3 / reps
         byts = 32.0 * n
         ach = byts / (us * 1e-6) / 1e9
-        roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": 8000.0, "unit": "GB/s",
-                "frac": round(ach / 8000.0, 4), "traffic": None,
-                "kernel": "sqnorm + adam_kernel (clip-norm + Adam over the flat parameters)",
-                "params": n, "algorithmic_bytes_per_step": byts, "optimizer_us": round(us, 1),
-                "optimizer_share_of_step": round(us * 1e-3 / (1e3 * elapsed / args.steps), 3)}
+        opt_roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": 8000.0, "unit": "GB/s",
+                    "frac": round(ach / 8000.0, 4), "traffic": None,
+                    "kernel": "sqnorm + adam_kernel (clip-norm + Adam over the flat parameters)",
+                    "params": n, "algorithmic_bytes_per_step": byts, "optimizer_us": round(us, 1),
+                    "optimizer_share_of_step": round(us * 1e-3 / (1e3 * elapsed / args.steps), 3)}
+        if dist is None:
+            roof = c5_group_roofline(args, trainer, batches, elapsed)
     mean_N = float(np.mean([b.N for b, _ in batches]))
     out = {"metric": METRIC_C5, "value": round(args.steps * bs * world / elapsed, 2), "unit": "graphs/s",
            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -392,7 +429,7 @@ def main_c5(args):
                                                      else ""),
                       "precision": args.precision, "hip_graph": graph},
            "final_loss": round(loss, 4), "host_issue_ms_per_step": round(1e3 * t_issue / args.steps, 3),
-           "roofline": roof, "cpu_baseline": None}
+           "roofline": roof, "optimizer": opt_roof, "cpu_baseline": None}
     if rank == 0 and world == 1 and args.cpu_baseline:
         out["cpu_baseline"] = unsup_cpu_baseline(host, sids_host, sd0, V, args.num_timesteps, args.lr,
                                                  max(3, args.cpu_steps))

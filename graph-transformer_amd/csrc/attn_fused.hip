@@ -462,7 +462,8 @@ __global__ void __launch_bounds__(256) attn_pv_combine_kernel(const float *Opart
 inline int spv_nsplit(int64_t n_valid) {
     const int64_t qb = (n_valid + FA_BM - 1) / FA_BM;
     const int64_t kb = (n_valid + FA_BN - 1) / FA_BN;
-    int64_t s = 256 / (qb > 0 ? qb : 1);   // one workgroup per CU: ~256 of them in one round
+    int64_t s = 256 / (qb > 0 ? qb : 1);   // one workgroup per CU: ~256 of them in one round (C5: 128 or 64
+                                           // workgroups instead ran 0.83 / 0.90 vs 0.81 ms per step)
     if (s > kb) s = kb;
     if (s < 1) s = 1;
     return (int)s;

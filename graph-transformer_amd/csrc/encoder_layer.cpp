@@ -569,22 +569,23 @@ int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
     Ctx c = carve_ctx(CA, D, drop);
     Side sd{st, side_st ? side_st : st, plan};
     hipStream_t so = sd.side;
-    // one stream (latency-bound layers): the parameter-gradient reductions and products go out together
-    // at the end (df), the attention products' slab reduces together before the in-projection (att)
+    // The parameter-gradient products and reductions are held back to the end of the layer (df) and go out
+    // there as one grouped GEMM launch + one reduction batch: on the side stream, overlapping the next
+    // layer's backward (C4: 3.141 / 3.147 / 3.159 vs 3.187 / 3.191 / 3.195 ms per step issued one by one
+    // beside this layer, one session, profiles/r03/r3g_side_defer_ab.txt), or on this stream for one-stream
+    // layers (C5: -10 launches per layer) and for the last layer of the backward.  The attention products
+    // dQ, dK (and dV when it runs on this stream) go out as one grouped launch and their slab reduces as
+    // one batch before the in-projection (att; C4 neutral, C5 -2 launches per layer).
     Defer defer_p, defer_a;
     defer_p.gemms = defer_a.gemms = true;
-    // the attention products dQ, dK (and dV when it runs on this stream) go out as one grouped launch and
-    // their slab reduces as one batch, in both modes (C4, side-stream schedule: 3.029 / 3.028 / 3.041 vs
-    // 3.024 / 3.046 / 3.035 ms per step without the grouping, one session: neutral; C5 -2 launches per layer)
-    Defer *df = so == st ? &defer_p : nullptr, *att = &defer_a;
+    Defer *df = &defer_p, *att = &defer_a;
     const int64_t blk_d[2] = {dp, d}, blk_ff[2] = {ffp, ff};
     float *ws = W.take<float>(colstat_ws_floats(N, dp));
-    // LN2 backward -> dX1 (residual), dF (dropout2 branch); norm2 + linear2.bias grads (side)
+    // LN2 backward -> dX1 (residual), dF (dropout2 branch); norm2 + linear2.bias grads (held back: df)
     float *dX1 = W.take<float>(Np * dp), *dF = W.take<float>(Np * dp);
     if (!plan)
         U2GNN_TRY(u2gnn_layernorm_bwd(dX2, dp, c.Z2, dp, c.mean2, c.rstd2, w->n2_w, dX1, dp, dF, dp, pd, s->drop2, N,
                                       Np, d, dp, st));
-    U2GNN_TRY(sd.fork());
     U2GNN_TRY(ln_params(dX2, c.Z2, c.mean2, c.rstd2, dF, dp, N, d, dp, ws, g->n2_w, g->n2_b, g->l2_b, so, plan, df));
     // FFN
     float *dH = W.take<float>(Np * ffp);
@@ -594,7 +595,7 @@ int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
         gg.a.aux0 = c.Hd, gg.a.ld_aux = ffp, gg.a.p_drop = pd;
         U2GNN_TRY(gg.run(st, plan));
     }
-    U2GNN_TRY(wgrad(W, D, dF, dp, c.Hd, ffp, dp, ffp, g->l2_w, ff, blk_d, blk_ff, so, df));   // side (forked above)
+    U2GNN_TRY(wgrad(W, D, dF, dp, c.Hd, ffp, dp, ffp, g->l2_w, ff, blk_d, blk_ff, so, df));   // held back (df)
     // one-stream layers in the matrix-core precisions: a split-K dX1 product leaves its slabs to LayerNorm1's
     // backward, which completes dX1 before using it (the separate reduce launch goes; same bits)
     const bool ln_delta = !D.window && prec != U2GNN_PREC_F32;
@@ -603,10 +604,9 @@ int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
     U2GNN_TRY(gemm_split(W, D, dH, w->W1, dX1, Np, dp, ffp, ffp, dp, dp, false, 1.f, true, nullptr, nullptr, false,
                          st, false, -1, 0, nullptr, nullptr, (ln_delta && so == st) ? &dx1_slabs : nullptr,
                          &dx1_nslab));
-    U2GNN_TRY(sd.fork());
     U2GNN_TRY(wgrad(W, D, dH, ffp, c.X1, dp, ffp, dp, g->l1_w, d, blk_ff, blk_d, so, df));
     U2GNN_TRY(bias_grad(W, dH, Np, ffp, ffp, ffp, ff, g->l1_b, so, df));
-    // LN1 backward -> dX (residual), dA (dropout1 branch); norm1 + out_proj.bias grads (side)
+    // LN1 backward -> dX (residual), dA (dropout1 branch); norm1 + out_proj.bias grads (held back: df)
     float *dA = W.take<float>(Np * dp);
     // no input gradient wanted (first layer of the stack): LN1's residual half goes to scratch and
     // the in-projection's dX GEMM below is skipped
@@ -624,7 +624,6 @@ int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
     else if (!plan)
         U2GNN_TRY(u2gnn_layernorm_bwd(dX1, dp, c.Z1, dp, c.mean1, c.rstd1, w->n1_w, dX, dp, dA, dp, pd, s->drop1, N,
                                       Np, d, dp, st));
-    U2GNN_TRY(sd.fork());
     U2GNN_TRY(ln_params(dX1, c.Z1, c.mean1, c.rstd1, dA, dp, N, d, dp, ws, g->n1_w, g->n1_b, g->out_b, so, plan, df));
     // out-projection
     float *dO = W.take<float>(Np * dp);
@@ -632,7 +631,7 @@ int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
         G gg(dA, w->W_o, dO, Np, dp, dp, dp, dp, dp, prec);
         U2GNN_TRY(gg.run(st, plan));
     }
-    U2GNN_TRY(wgrad(W, D, dA, dp, c.O, dp, dp, dp, g->out_w, d, blk_d, blk_d, so, df));   // side (forked above)
+    U2GNN_TRY(wgrad(W, D, dA, dp, c.O, dp, dp, dp, g->out_w, d, blk_d, blk_d, so, df));   // held back (df)
     // attention core
     const float *Q = c.QKV, *Kt = c.QKV + dp, *V = c.QKV + 2 * dp;
     const float q_scale = (float)(1.0 / std::sqrt((double)d));
@@ -674,15 +673,14 @@ int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
     if (need_dx)
         U2GNN_TRY(gemm_split(W, D, dQKV, w->W_in, dX, Np, dp, 3 * dp, 3 * dp, dp, dp, false, 1.f, true, nullptr,
                              nullptr, false, st));
-    // the in-projection's parameter gradients: on the side stream beside the dX product, but on this
-    // stream for the last layer of the backward (need_dx false), where nothing is left to overlap and
-    // the hand-off plus the step's final join cost more than the products (C4: ~75 us idle per step)
-    const bool side_w = need_dx;   // 3.140-3.157 vs 3.171-3.194 ms per C4 step (4 pairs, one session)
-    hipStream_t wst = side_w ? so : st;
-    if (side_w) U2GNN_TRY(sd.fork());
-    U2GNN_TRY(wgrad(W, D, dQKV, 3 * dp, X, dp, 3 * dp, dp, g->in_w, d, blk_d, blk_d, wst, df));
-    U2GNN_TRY(bias_grad(W, dQKV, Np, 3 * dp, 3 * dp, dp, d, g->in_b, wst, df));
-    U2GNN_TRY(flush(df, W, st));
+    U2GNN_TRY(wgrad(W, D, dQKV, 3 * dp, X, dp, 3 * dp, dp, g->in_w, d, blk_d, blk_d, st, df));
+    U2GNN_TRY(bias_grad(W, dQKV, Np, 3 * dp, 3 * dp, dp, d, g->in_b, st, df));
+    // the held-back work: on the side stream after everything issued so far, except for the last layer of
+    // the backward (need_dx false), where nothing is left to overlap and the hand-off plus the step's final
+    // join cost more than the products (C4 round 3: 3.140-3.157 vs 3.171-3.194 ms per step)
+    const bool side_flush = so != st && need_dx;
+    if (side_flush) U2GNN_TRY(sd.fork());
+    U2GNN_TRY(flush(df, W, side_flush ? so : st));
     return (W.overflow || CA.overflow) ? U2GNN_E_ARG : U2GNN_OK;
 }
 

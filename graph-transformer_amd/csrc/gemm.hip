@@ -401,6 +401,14 @@ __device__ __forceinline__ void gemm_bf16_body(const GemmP &P, int tmi, int tni,
     PreDS<TN> pre;
     const bool use_pre = (EPI == U2GNN_EPI_ATTN_DS && P.keep != nullptr) || ds_signed<EPI>;
     if (use_pre) prefetch_ds<EPI>(P, m0 + wm * WTM + li, n0 + wn * WTN, kh, pre);
+    // 64 x 64 tiles with row-operand epilogues: the slice's residual / bias / accumulator / ReLU operands
+    // requested before the main loop (the short K loops of these products do not hide the epilogue's round
+    // trip): C4 3.010-3.027 vs 3.027-3.051 ms, C5 0.804 vs 0.808-0.809 ms per step (one session each)
+    constexpr bool PRE_AUX = TM == 1 && TN == 1 &&
+                             (EPI == U2GNN_EPI_BIAS_DROP_RESID || EPI == U2GNN_EPI_BIAS_DROP_RESID_LN ||
+                              EPI == U2GNN_EPI_RELU_DROP_BWD || EPI == U2GNN_EPI_ACCUM);
+    EpiSlice<pre_aux_fetch<EPI>, TN> pa;
+    if constexpr (PRE_AUX) fetch_slice<pre_aux_fetch<EPI>>(P, m0 + wm * WTM + li, n0 + wn * WTN, kh, pa);
     if (nk > 0) {
         // two register stages: every tile's global loads are in flight across TWO compute phases
         // (a single phase of 24 MFMAs does not cover an L2/LLC miss at 2 waves per SIMD)
@@ -431,7 +439,7 @@ __device__ __forceinline__ void gemm_bf16_body(const GemmP &P, int tmi, int tni,
     }
 
     store_tile<EPI>(P, P.C + (int64_t)zi * P.slab_stride, acc, m0 + wm * WTM, n0 + wn * WTN, li, kh,
-                    use_pre ? &pre : nullptr);
+                    use_pre ? &pre : nullptr, PRE_AUX ? &pa : nullptr);
 }
 
 template <int BM, int BN, int WM, int WN, int BK, bool TA, bool TB, int EPI, bool SPLIT, bool CLAMP>

@@ -309,14 +309,15 @@ __device__ __forceinline__ void slice_from_pre(const PreDS<TN> &pre, int kh, Epi
 // written with the row's mean / rstd -- the separate layernorm_fwd launch of a d <= 64 encoder.
 template <int TM, int TN>
 __device__ __forceinline__ void store_tile_ln(const GemmP &P, float *C, const f32x16 (&acc)[TM][TN], int r0, int c0,
-                                              int li, int kh) {
+                                              int li, int kh, const EpiSlice<U2GNN_EPI_BIAS_DROP_RESID, TN> *pa) {
     static_assert(TM == 1 && TN == 1, "row-complete LayerNorm epilogue: 64 x 64 blocks of 2 x 2 waves");
     constexpr int E = U2GNN_EPI_BIAS_DROP_RESID;
     __shared__ float lnred[2][2][64];
     const int row = r0 + li;
     const int rb = (r0 & 63) + li, wn = (c0 & 63) >> 5;
     EpiSlice<E, TN> e;
-    fetch_slice<E>(P, row, c0, kh, e);
+    if (pa) e = *pa;
+    else fetch_slice<E>(P, row, c0, kh, e);
     float z[16];
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
@@ -415,11 +416,16 @@ __device__ __forceinline__ void rowstat_slice(const GemmP &P, const f32x16 (&acc
         *reinterpret_cast<float2 *>(P.rowpart + 2 * ((int64_t)row * P.ld_rowpart + c0 / (32 * TN))) = make_float2(m, l);
 }
 
+// the epilogue operands of a 64 x 64 tile's (single) slice fetched before the main loop (pre_aux_epi)
+template <int EPI>
+constexpr int pre_aux_fetch = EPI == U2GNN_EPI_BIAS_DROP_RESID_LN ? U2GNN_EPI_BIAS_DROP_RESID : EPI;
+
 template <int EPI, int TM, int TN>
 __device__ __forceinline__ void store_tile(const GemmP &P, float *C, const f32x16 (&acc)[TM][TN], int r0, int c0,
-                                           int li, int kh, const PreDS<TN> *pre) {
+                                           int li, int kh, const PreDS<TN> *pre,
+                                           const EpiSlice<pre_aux_fetch<EPI>, TN> *pa = nullptr) {
     if constexpr (EPI == U2GNN_EPI_BIAS_DROP_RESID_LN) {
-        store_tile_ln<TM, TN>(P, C, acc, r0, c0, li, kh);
+        store_tile_ln<TM, TN>(P, C, acc, r0, c0, li, kh, pa);
         return;
     }
     if constexpr (ds_signed<EPI>) {
@@ -440,6 +446,13 @@ __device__ __forceinline__ void store_tile(const GemmP &P, float *C, const f32x1
     for (int i = 0; i < TM; ++i) {
         const int row = r0 + i * 32 + li;
         EpiSlice<EPI, TN> e;
+        if constexpr (pre_aux_fetch<EPI> == EPI) {
+            if (i == 0 && pa) {
+                e = *pa;
+                rs[i] = store_slice<EPI>(P, C, acc, i, row, c0, kh, e);
+                continue;
+            }
+        }
         if (i == 0 && pre) slice_from_pre<EPI>(*pre, kh, e);
         else fetch_slice<EPI>(P, row, c0, kh, e);
         rs[i] = store_slice<EPI>(P, C, acc, i, row, c0, kh, e);

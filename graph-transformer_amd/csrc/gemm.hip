@@ -406,7 +406,8 @@ __device__ __forceinline__ void gemm_bf16_body(const GemmP &P, int tmi, int tni,
     // trip): C4 3.010-3.027 vs 3.027-3.051 ms, C5 0.804 vs 0.808-0.809 ms per step (one session each)
     constexpr bool PRE_AUX = TM == 1 && TN == 1 &&
                              (EPI == U2GNN_EPI_BIAS_DROP_RESID || EPI == U2GNN_EPI_BIAS_DROP_RESID_LN ||
-                              EPI == U2GNN_EPI_RELU_DROP_BWD || EPI == U2GNN_EPI_ACCUM);
+                              EPI == U2GNN_EPI_RELU_DROP_BWD || EPI == U2GNN_EPI_ACCUM);   // bias-only epilogues
+                                                                                           // too: neutral
     EpiSlice<pre_aux_fetch<EPI>, TN> pa;
     if constexpr (PRE_AUX) fetch_slice<pre_aux_fetch<EPI>>(P, m0 + wm * WTM + li, n0 + wn * WTN, kh, pa);
     if (nk > 0) {

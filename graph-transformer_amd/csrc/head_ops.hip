@@ -258,16 +258,38 @@ __device__ __forceinline__ void adam_sweep(float *param, const float *grad, floa
     }
 }
 
+// The clip coefficient.  With sqnorm partials (SqParts, ABI v11 u2gnn_adam_sq / u2gnn_adam_dev_sq) every block
+// folds the sqnorm_partial_kernel outputs exactly as sqnorm_final_kernel does (same order, same bits) and
+// block 0 also stores the total: the separate one-block launch goes.
+struct SqParts {
+    const double *parts;   // nullptr: use sqnorm
+    int nb;
+    float *out;
+};
+
+__device__ __forceinline__ float clip_coef(const float *sqnorm, const SqParts &sp, float max_norm) {
+    if (sp.parts) {
+        __shared__ double red[4];
+        double s = 0.0;
+        for (int i = threadIdx.x; i < sp.nb; i += 256) s += sp.parts[i];
+        s = wave_sum_d(s);
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+        __syncthreads();
+        const float sq = (float)(red[0] + red[1] + red[2] + red[3]);
+        if (blockIdx.x == 0 && threadIdx.x == 0 && sp.out) sp.out[0] = sq;
+        return fminf(1.f, max_norm / (sqrtf(sq) + 1e-6f));
+    }
+    if (!sqnorm) return 1.f;
+    const float total = sqrtf(sqnorm[0]);
+    return fminf(1.f, max_norm / (total + 1e-6f));
+}
+
 // torch.optim.Adam (_single_tensor_adam, no weight decay / amsgrad):
 //   m.lerp_(g, 1-b1); v = v*b2 + (1-b2) g*g; denom = sqrt(v)/bc2_sqrt + eps; p -= step_size*m/denom
 __global__ void __launch_bounds__(256) adam_kernel(float *param, const float *grad, float *m, float *v, int64_t n,
                                                    const float *sqnorm, float max_norm, float b1, float b2, float eps,
-                                                   float step_size, float bc2_sqrt) {
-    float coef = 1.f;
-    if (sqnorm) {
-        const float total = sqrtf(sqnorm[0]);
-        coef = fminf(1.f, max_norm / (total + 1e-6f));
-    }
+                                                   float step_size, float bc2_sqrt, SqParts sp) {
+    const float coef = clip_coef(sqnorm, sp, max_norm);
     const float w1 = 1.f - b1, w2 = 1.f - b2;
     adam_sweep(param, grad, m, v, n, coef, b2, w1, w2, eps, step_size, bc2_sqrt);
 }
@@ -276,15 +298,11 @@ __global__ void __launch_bounds__(256) adam_kernel(float *param, const float *gr
 // formed in double like the host path (torch: lr / (1 - b1^t), sqrt(1 - b2^t)).
 __global__ void __launch_bounds__(256) adam_dev_kernel(float *param, const float *grad, float *m, float *v, int64_t n,
                                                        const float *sqnorm, float max_norm, double b1, double b2,
-                                                       float eps, const double *lr, const int64_t *t) {
+                                                       float eps, const double *lr, const int64_t *t, SqParts sp) {
     const double tt = (double)t[0];
     const float step_size = (float)(lr[0] / (1.0 - pow(b1, tt)));
     const float bc2_sqrt = (float)sqrt(1.0 - pow(b2, tt));
-    float coef = 1.f;
-    if (sqnorm) {
-        const float total = sqrtf(sqnorm[0]);
-        coef = fminf(1.f, max_norm / (total + 1e-6f));
-    }
+    const float coef = clip_coef(sqnorm, sp, max_norm);
     const float fb1 = (float)b1, fb2 = (float)b2;
     const float w1 = 1.f - fb1, w2 = 1.f - fb2;
     adam_sweep(param, grad, m, v, n, coef, fb2, w1, w2, eps, step_size, bc2_sqrt);
@@ -687,9 +705,42 @@ int u2gnn_smoothed_ce(const float *scores, const int64_t *labels, int64_t B, int
     return u2gnn_launch_status();
 }
 
+namespace {
+inline unsigned sqnorm_blocks(int64_t n) { return grid_for(n, 256 * 16, 512); }   // ws holds 512 doubles
+}  // namespace
+
+int u2gnn_sqnorm_partials(const float *g, int64_t n, float *ws, void *stream) {
+    if (!g || !ws || (reinterpret_cast<uintptr_t>(g) & 15)) return U2GNN_E_ARG;
+    hipLaunchKernelGGL(sqnorm_partial_kernel, dim3(sqnorm_blocks(n)), dim3(256), 0, u2gnn_stream(stream), g, n,
+                       reinterpret_cast<double *>(ws));
+    return u2gnn_launch_status();
+}
+
+int u2gnn_adam_sq(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, int64_t n, const float *ws,
+                  float *sqnorm, float max_norm, float beta1, float beta2, float eps, float step_size, float bc2_sqrt,
+                  void *stream) {
+    if (!param || !grad || !exp_avg || !exp_avg_sq || !ws) return U2GNN_E_ARG;
+    if (n == 0) return U2GNN_OK;
+    const SqParts sp{reinterpret_cast<const double *>(ws), (int)sqnorm_blocks(n), sqnorm};
+    hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n, 1024, 4096)), dim3(256), 0, u2gnn_stream(stream), param, grad,
+                       exp_avg, exp_avg_sq, n, nullptr, max_norm, beta1, beta2, eps, step_size, bc2_sqrt, sp);
+    return u2gnn_launch_status();
+}
+
+int u2gnn_adam_dev_sq(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, int64_t n, const float *ws,
+                      float *sqnorm, float max_norm, double beta1, double beta2, float eps, const double *lr,
+                      const int64_t *step, void *stream) {
+    if (!param || !grad || !exp_avg || !exp_avg_sq || !ws || !lr || !step) return U2GNN_E_ARG;
+    if (n == 0) return U2GNN_OK;
+    const SqParts sp{reinterpret_cast<const double *>(ws), (int)sqnorm_blocks(n), sqnorm};
+    hipLaunchKernelGGL(adam_dev_kernel, dim3(grid_for(n, 1024, 4096)), dim3(256), 0, u2gnn_stream(stream), param, grad,
+                       exp_avg, exp_avg_sq, n, nullptr, max_norm, beta1, beta2, eps, lr, step, sp);
+    return u2gnn_launch_status();
+}
+
 int u2gnn_sqnorm(const float *g, int64_t n, float *ws, float *sqnorm, void *stream) {
     if (!g || !ws || !sqnorm || (reinterpret_cast<uintptr_t>(g) & 15)) return U2GNN_E_ARG;
-    const unsigned nb = grid_for(n, 256 * 16, 512);   // ws holds 512 doubles (u2gnn_hip.h)
+    const unsigned nb = sqnorm_blocks(n);
     hipStream_t st = u2gnn_stream(stream);
     double *wsd = reinterpret_cast<double *>(ws);
     hipLaunchKernelGGL(sqnorm_partial_kernel, dim3(nb), dim3(256), 0, st, g, n, wsd);
@@ -702,7 +753,8 @@ int u2gnn_adam(float *param, const float *grad, float *exp_avg, float *exp_avg_s
     if (!param || !grad || !exp_avg || !exp_avg_sq) return U2GNN_E_ARG;
     if (n == 0) return U2GNN_OK;
     hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n, 1024, 4096)), dim3(256), 0, u2gnn_stream(stream), param, grad,
-                       exp_avg, exp_avg_sq, n, sqnorm, max_norm, beta1, beta2, eps, step_size, bc2_sqrt);
+                       exp_avg, exp_avg_sq, n, sqnorm, max_norm, beta1, beta2, eps, step_size, bc2_sqrt,
+                       SqParts{nullptr, 0, nullptr});
     return u2gnn_launch_status();
 }
 
@@ -712,7 +764,8 @@ int u2gnn_adam_dev(float *param, const float *grad, float *exp_avg, float *exp_a
     if (!param || !grad || !exp_avg || !exp_avg_sq || !lr || !step) return U2GNN_E_ARG;
     if (n == 0) return U2GNN_OK;
     hipLaunchKernelGGL(adam_dev_kernel, dim3(grid_for(n, 1024, 4096)), dim3(256), 0, u2gnn_stream(stream), param, grad,
-                       exp_avg, exp_avg_sq, n, sqnorm, max_norm, beta1, beta2, eps, lr, step);
+                       exp_avg, exp_avg_sq, n, sqnorm, max_norm, beta1, beta2, eps, lr, step,
+                       SqParts{nullptr, 0, nullptr});
     return u2gnn_launch_status();
 }
 

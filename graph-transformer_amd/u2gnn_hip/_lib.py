@@ -125,6 +125,9 @@ _HIP_SIGS = {
     "u2gnn_concat_dropout": ([POINTER(c_void_p), I32, I64, I64, I64, F32, c_uint64, VP, I64, VP], c_int32),
     "u2gnn_split_dropout_bwd": ([VP, I64, I32, I64, I64, I64, I64, F32, c_uint64, POINTER(c_void_p), VP], c_int32),
     "u2gnn_sum": ([VP, I64, VP, VP], c_int32),
+    "u2gnn_sqnorm_partials": ([VP, I64, VP, VP], c_int32),
+    "u2gnn_adam_sq": ([VP, VP, VP, VP, I64, VP, VP, F32, F32, F32, F32, F32, F32, VP], c_int32),
+    "u2gnn_adam_dev_sq": ([VP, VP, VP, VP, I64, VP, VP, F32, c_double, c_double, F32, VP, VP, VP], c_int32),
     "u2gnn_layernorm_bwd_delta_slabs": ([VP, I64, VP, I32, I64, VP, I64, VP, VP, VP, VP, I64, VP, I64, F32, c_uint64,
                                          I64, I64, I64, I64, VP, I64, VP, VP, VP], c_int32),
     "u2gnn_slab_bias_drop_resid_ln": ([VP, I32, I64, I64, VP, VP, I64, F32, c_uint64, VP, I64, VP, VP, VP, I64, VP,

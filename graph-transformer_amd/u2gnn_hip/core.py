@@ -448,23 +448,31 @@ class FusedAdam:
 
     def step(self):
         b1, b2 = self.betas
-        if self.max_norm is not None:
-            K.sqnorm(self.f.gflat, self.f.n, self.ws, self.sq)
+        clip = self.max_norm is not None
+        if clip:   # the partial sums of g^2; Adam's blocks fold them (u2gnn_adam(_dev)_sq): 2 launches, not 3
+            K.sqnorm_partials(self.f.gflat, self.f.n, self.ws)
         if self.t_dev is not None:
             # inside a captured step the graph's first node (StepGraphs: u2gnn_step_advance) bumps t;
             # an eager step taken while the device schedule is live bumps it here, so every path
             # advances t exactly once per step (a fresh t of 0 gave lr / (1 - b1^0) = inf)
             if not torch.cuda.is_current_stream_capturing():
                 K.step_advance(None, self.t_dev)
-            K.adam_dev(self.f.flat, self.f.gflat, self.m, self.v, self.f.n,
-                       self.sq if self.max_norm is not None else None, self.max_norm or 0.0, b1, b2, self.eps,
-                       self.lr_dev, self.t_dev)
+            if clip:
+                K.adam_dev_sq(self.f.flat, self.f.gflat, self.m, self.v, self.f.n, self.ws, self.sq, self.max_norm,
+                              b1, b2, self.eps, self.lr_dev, self.t_dev)
+            else:
+                K.adam_dev(self.f.flat, self.f.gflat, self.m, self.v, self.f.n, None, 0.0, b1, b2, self.eps,
+                           self.lr_dev, self.t_dev)
             return
         self.step_count += 1
         bc1 = 1 - b1 ** self.step_count
         bc2 = 1 - b2 ** self.step_count
-        K.adam(self.f.flat, self.f.gflat, self.m, self.v, self.f.n, self.sq if self.max_norm is not None else None,
-               self.max_norm or 0.0, b1, b2, self.eps, self.lr / bc1, math.sqrt(bc2))
+        if clip:
+            K.adam_sq(self.f.flat, self.f.gflat, self.m, self.v, self.f.n, self.ws, self.sq, self.max_norm, b1, b2,
+                      self.eps, self.lr / bc1, math.sqrt(bc2))
+        else:
+            K.adam(self.f.flat, self.f.gflat, self.m, self.v, self.f.n, None, 0.0, b1, b2, self.eps, self.lr / bc1,
+                   math.sqrt(bc2))
 
     def grad_norm(self) -> float:
         return float(self.sq.sqrt().item())

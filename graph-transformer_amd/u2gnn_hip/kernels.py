@@ -373,6 +373,28 @@ def smoothed_ce(scores, labels, B, C, smoothing, loss, dscores):
                                       _p(dscores), _s()), "u2gnn_smoothed_ce")
 
 
+def sqnorm_partials(g, n, ws):
+    """Per-block partial sums of g^2 into ws (ABI v11; folded by adam_sq / adam_dev_sq)."""
+    _dev(g, ws)
+    check(hip_lib().u2gnn_sqnorm_partials(_p(g), int(n), _p(ws), _s()), "u2gnn_sqnorm_partials")
+
+
+def adam_sq(param, grad, m, v, n, ws, sq_out, max_norm, beta1, beta2, eps, step_size, bc2_sqrt):
+    """Clip + Adam with the sqnorm partials folded in (ABI v11); sq_out receives sum g^2."""
+    _dev(param, grad, m, v, ws, sq_out)
+    check(hip_lib().u2gnn_adam_sq(_p(param), _p(grad), _p(m), _p(v), int(n), _p(ws), _p(sq_out), float(max_norm),
+                                  float(beta1), float(beta2), float(eps), float(step_size), float(bc2_sqrt), _s()),
+          "u2gnn_adam_sq")
+
+
+def adam_dev_sq(param, grad, m, v, n, ws, sq_out, max_norm, b1, b2, eps, lr_dev, step_dev):
+    """adam_dev with the sqnorm partials folded in (ABI v11)."""
+    _dev(param, grad, m, v, ws, sq_out, lr_dev, step_dev)
+    check(hip_lib().u2gnn_adam_dev_sq(_p(param), _p(grad), _p(m), _p(v), int(n), _p(ws), _p(sq_out), float(max_norm),
+                                      float(b1), float(b2), float(eps), _p(lr_dev), _p(step_dev), _s()),
+          "u2gnn_adam_dev_sq")
+
+
 def sqnorm(g, n, ws, out):
     _dev(g, ws, out)
     check(hip_lib().u2gnn_sqnorm(_p(g), int(n), _p(ws), _p(out), _s()), "u2gnn_sqnorm")

@@ -352,6 +352,17 @@ int u2gnn_smoothed_ce(const float *scores, const int64_t *labels, int64_t B, int
 /* ---- a9: clip_grad_norm_(max_norm) + Adam  (train_pytorch_U2GNN_Sup.py:145,160-161) ----
  * sqnorm[0] = sum g^2 (double accumulation, fp32 result); ws >= 1024 floats. */
 int u2gnn_sqnorm(const float *g, int64_t n, float *ws, float *sqnorm, void *stream);
+/* ABI v11: the clip + Adam pair in two launches instead of three: u2gnn_sqnorm_partials writes the per-block
+ * partial sums of g^2 into ws (>= 1024 floats); u2gnn_adam_sq / u2gnn_adam_dev_sq (the arguments of
+ * u2gnn_adam / u2gnn_adam_dev with ws in place of sqnorm) fold them in every block in u2gnn_sqnorm's order
+ * (the same clip coefficient, bit for bit) and store the total into sqnorm (may be NULL). */
+int u2gnn_sqnorm_partials(const float *g, int64_t n, float *ws, void *stream);
+int u2gnn_adam_sq(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, int64_t n, const float *ws,
+                  float *sqnorm, float max_norm, float beta1, float beta2, float eps, float step_size, float bc2_sqrt,
+                  void *stream);
+int u2gnn_adam_dev_sq(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, int64_t n, const float *ws,
+                      float *sqnorm, float max_norm, double beta1, double beta2, float eps, const double *lr,
+                      const int64_t *step, void *stream);
 /* torch.optim.Adam single-tensor step on a flat buffer with the clip coefficient
  * min(1, max_norm/(sqrt(*sqnorm)+1e-6)) applied to g on the fly (sqnorm NULL: no clip).
  * step_size = lr / (1 - beta1^t), bc2_sqrt = sqrt(1 - beta2^t), computed by the caller. */

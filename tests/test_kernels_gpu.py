@@ -818,3 +818,25 @@ def test_layernorm_bwd_delta_slabs_equals_reduce_then_ln(N, Np, d, dp, n_slab):
     torch.cuda.synchronize()
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("n", [1001, 10 * 1024 * 1024 + 3])
+def test_adam_sq_equals_sqnorm_then_adam(n):
+    g = torch.Generator(device=DEV).manual_seed(9)
+    grad = torch.randn(n, device=DEV, generator=g) * 0.1
+    base = [torch.randn(n, device=DEV, generator=g) for _ in range(3)]
+    base[2] = base[2].abs()
+    out = []
+    for fused in (False, True):
+        p, m, v = (t.clone() for t in base)
+        ws, sq = torch.zeros(1024, device=DEV), torch.full((1,), float("nan"), device=DEV)
+        if fused:
+            K.sqnorm_partials(grad, n, ws)
+            K.adam_sq(p, grad, m, v, n, ws, sq, 0.5, 0.9, 0.999, 1e-8, 0.01, 0.3)
+        else:
+            K.sqnorm(grad, n, ws, sq)
+            K.adam(p, grad, m, v, n, sq, 0.5, 0.9, 0.999, 1e-8, 0.01, 0.3)
+        out.append((p, m, v, sq))
+    torch.cuda.synchronize()
+    for a, b in zip(*out):
+        assert torch.equal(a, b)

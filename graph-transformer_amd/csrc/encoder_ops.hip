@@ -261,7 +261,17 @@ __global__ void __launch_bounds__(256) pack_padded_kernel(const float *src, int6
 constexpr int PACK_MAX = 32;
 struct PackBatch {
     u2gnn_pack_desc d[PACK_MAX];
+    uint64_t *adv_epoch;   // u2gnn_pack_padded_multi_adv: the step state bumped by block (0, 0)
+    int64_t *adv_t;
 };
+
+// the graph-replay step advance (u2gnn_step_advance) carried by the step's first launch, the weight pack
+__device__ __forceinline__ void pack_advance(const PackBatch &pb) {
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+        if (pb.adv_epoch) *pb.adv_epoch += 1;
+        if (pb.adv_t) *pb.adv_t += 1;
+    }
+}
 
 // Many padded-copy jobs in one launch: blockIdx.y = job, blockIdx.x = a group of PACK_RB rows, each
 // thread one column per 256 (the column map computed once per column, the row map once per row, in
@@ -270,6 +280,7 @@ struct PackBatch {
 constexpr uint32_t PACK_RB = 8;
 
 __global__ void __launch_bounds__(256) pack_multi_kernel(PackBatch pb) {
+    pack_advance(pb);
     const u2gnn_pack_desc &D = pb.d[blockIdx.y];
     const uint32_t rows = (uint32_t)D.rows_pad, cols = (uint32_t)D.cols_pad;
     const uint32_t r0 = blockIdx.x * PACK_RB;
@@ -294,6 +305,7 @@ __global__ void __launch_bounds__(256) pack_multi_kernel(PackBatch pb) {
 }
 
 __global__ void __launch_bounds__(256) pack_multi64_kernel(PackBatch pb) {
+    pack_advance(pb);
     const u2gnn_pack_desc &D = pb.d[blockIdx.y];
     const int64_t total = D.rows_pad * D.cols_pad;
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
@@ -1226,9 +1238,17 @@ int u2gnn_pack_padded(const float *src, int64_t ld_src, int64_t rows_pad, int64_
 }
 
 int u2gnn_pack_padded_multi(const u2gnn_pack_desc *descs, int32_t n, void *stream) {
+    return u2gnn_pack_padded_multi_adv(descs, n, nullptr, nullptr, stream);
+}
+
+int u2gnn_pack_padded_multi_adv(const u2gnn_pack_desc *descs, int32_t n, uint64_t *epoch, int64_t *t,
+                                void *stream) {
     if (n < 0 || (n && !descs)) return U2GNN_E_ARG;
+    if (n == 0) return (epoch || t) ? U2GNN_E_ARG : U2GNN_OK;   // the advance needs a launch
     for (int32_t o = 0; o < n; o += PACK_MAX) {
         PackBatch pb;
+        pb.adv_epoch = o == 0 ? epoch : nullptr;
+        pb.adv_t = o == 0 ? t : nullptr;
         const int32_t m = n - o < PACK_MAX ? n - o : PACK_MAX;
         int64_t biggest = 1, max_rows = 1;
         bool fits32 = true;

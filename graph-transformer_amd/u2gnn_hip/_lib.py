@@ -154,6 +154,7 @@ _HIP_SIGS = {
                                    VP, I64, VP, VP, VP], c_int32),
     "u2gnn_layernorm_bwd_params": ([VP, I64, VP, I64, VP, VP, VP, I64, I64, I64, I64, VP, VP, VP, VP, VP], c_int32),
     "u2gnn_pack_padded_multi": ([VP, I32, VP], c_int32),
+    "u2gnn_pack_padded_multi_adv": ([VP, I32, VP, VP, VP], c_int32),
     "u2gnn_pool_fwd": ([VP, I64, VP, VP, VP, VP, I64, I64, I64, F32, c_uint64, VP], c_int32),
     "u2gnn_pool_bwd": ([VP, I64, VP, VP, VP, VP, I64, I64, I64, F32, c_uint64, VP], c_int32),
     "u2gnn_pool_bwd_rows": ([VP, I64, VP, VP, VP, VP, I64, I64, I64, I64, I64, I64, F32, c_uint64, VP], c_int32),

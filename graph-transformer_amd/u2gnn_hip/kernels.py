@@ -325,6 +325,20 @@ def layernorm_bwd_params(dY, ldy, Z, ldz, mean, rstd, dZdrop, lddrop, rows_valid
                                                _p(dbeta), _p(dbias), _s()), "u2gnn_layernorm_bwd_params")
 
 
+# a step advance (epoch, t) handed to the next weight pack (train.StepGraphs: the replayed step's first node
+# rides on its first launch instead of a launch of its own)
+_PENDING_ADVANCE = []
+
+
+def defer_step_advance(epoch, t):
+    _dev(epoch, t)
+    _PENDING_ADVANCE[:] = [(epoch, t)]
+
+
+def step_advance_pending() -> bool:
+    return bool(_PENDING_ADVANCE)
+
+
 def pack_padded_multi(jobs):
     """jobs: list of (src, ld_src, rows_pad, cols_pad, rblk, cblk, dst, ld_dst)."""
     arr = (_lib.PackDesc * len(jobs))()
@@ -332,6 +346,11 @@ def pack_padded_multi(jobs):
         _dev(src, dst)
         arr[i] = _lib.PackDesc(src.data_ptr(), dst.data_ptr(), int(ld_src), int(rp), int(cp), int(rb[0]), int(rb[1]),
                                int(cb[0]), int(cb[1]), int(ld_dst))
+    if _PENDING_ADVANCE and jobs:
+        epoch, t = _PENDING_ADVANCE.pop()
+        check(hip_lib().u2gnn_pack_padded_multi_adv(arr, len(jobs), _p(epoch), _p(t), _s()),
+              "u2gnn_pack_padded_multi_adv")
+        return
     check(hip_lib().u2gnn_pack_padded_multi(arr, len(jobs), _s()), "u2gnn_pack_padded_multi")
 
 

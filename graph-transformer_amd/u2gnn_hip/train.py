@@ -80,8 +80,16 @@ class StepGraphs:
             torch.cuda.synchronize()
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
-                K.step_advance(self.epoch, self.tr.opt.t_dev)
-                self.tr.step(*args)
+                # the step's first launch (the weight pack) bumps the epoch and Adam's t before anything else
+                # runs (u2gnn_pack_padded_multi_adv): one launch less than a u2gnn_step_advance node
+                K.defer_step_advance(self.epoch, self.tr.opt.t_dev)
+                try:
+                    self.tr.step(*args)
+                finally:
+                    pending = K.step_advance_pending()
+                    K._PENDING_ADVANCE.clear()
+                if pending:
+                    raise RuntimeError("StepGraphs: the captured step ran no weight pack to carry the step advance")
             ent = self.graphs[key] = (g, args)
         return ent[0]
 

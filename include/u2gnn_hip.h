@@ -186,6 +186,10 @@ typedef struct u2gnn_pack_desc {
     int64_t ld_src, rows_pad, cols_pad, rblk_pad, rblk_real, cblk_pad, cblk_real, ld_dst;
 } u2gnn_pack_desc;
 int u2gnn_pack_padded_multi(const u2gnn_pack_desc *descs, int32_t n, void *stream);
+/* ABI v11: the same, and the launch also performs u2gnn_step_advance(epoch, t) (either may be NULL) before any
+ * later launch on the stream runs: the first node of a replayed step without a launch of its own (n >= 1). */
+int u2gnn_pack_padded_multi_adv(const u2gnn_pack_desc *descs, int32_t n, uint64_t *epoch, int64_t *t,
+                                void *stream);
 
 /* column sums (bias gradients):  out[map(c)] (+)= sum_{r<rows} X[r*ld + c], c < cols_pad.
  * ws must hold ceil(rows/16) * cols_pad floats (kernels.colstat_ws_floats allocates 3x that); 16-byte

@@ -95,15 +95,18 @@ class UnSupTrainer:
         # row exchange
         gW = self.flat.grads["ss.weight"]
         dOV = torch.empty_like(OVd)
-        rows_lab = torch.empty(N, D, device=OVd.device)
-        rows_smp = torch.empty(S, D, device=OVd.device)
-        K.sampled_softmax_bwd_rows(OVd, D, b.input_y, sample_ids, S, W, W.stride(0), prob, None, dOV, D, rows_lab,
-                                   rows_smp, N, D)
-        if self.row_sync is not None:
+        if self.row_sync is not None:   # data parallel: compact rows, exchanged before they are added
+            rows_lab = torch.empty(N, D, device=OVd.device)
+            rows_smp = torch.empty(S, D, device=OVd.device)
+            K.sampled_softmax_bwd_rows(OVd, D, b.input_y, sample_ids, S, W, W.stride(0), prob, None, dOV, D,
+                                       rows_lab, rows_smp, N, D)
             self._touched = self.row_sync.rows(b.input_y, rows_lab, sample_ids, rows_smp, gW)
-        else:   # labels first, then samples: distinct destinations per call, fixed order
-            K.index_add_rows(rows_lab, b.input_y, gW)
-            K.index_add_rows(rows_smp, sample_ids, gW)
+        else:
+            # added straight into the dense gradient, labels (one kernel) before samples (the next): the
+            # destinations within each kernel are distinct, so this is the compact-rows form followed by
+            # its two index_add launches, value for value, in two launches instead of four
+            K.sampled_softmax_bwd(OVd, D, b.input_y, sample_ids, S, W, W.stride(0), prob, None, dOV, D, gW,
+                                  gW.stride(0), N, D)
             self._touched = (b.input_y, sample_ids)
         core.encode_backward(sctx, dOV, self.flat.grads, p, ds)   # dropout's backward fused into the split
         return self.loss

@@ -719,6 +719,11 @@ int u2gnn_layer_fwd(const u2gnn_layer_dims *dims, const u2gnn_layer_params *w, c
                     void *stream) {
     if (!dims_ok(dims) || !w || !s || !X || !X2 || (!ws && ws_bytes > 0)) return U2GNN_E_ARG;
     const Dims D = make_dims(dims);
+    // the same call in planning mode first: a workspace or ctx arena smaller than this call takes is
+    // refused before anything is launched (never a launch over the end of a caller buffer)
+    Arena Pc(nullptr, 0), Pw(nullptr, 0);
+    layer_fwd(D, w, s, X, X2, Pc, Pw, ctx != nullptr, reinterpret_cast<hipStream_t>(stream));
+    if (Pw.used > (ws ? ws_bytes : 0) || (ctx && Pc.used > ctx_bytes)) return U2GNN_E_ARG;
     static char empty_ws alignas(256)[256];   // a null base would mean "plan only"
     Arena C(ctx, ctx_bytes), W(ws ? ws : empty_ws, ws ? ws_bytes : 0);
     return layer_fwd(D, w, s, X, X2, C, W, ctx != nullptr, reinterpret_cast<hipStream_t>(stream));
@@ -729,6 +734,10 @@ int u2gnn_layer_bwd(const u2gnn_layer_dims *dims, const u2gnn_layer_params *w, c
                     const u2gnn_layer_grads *g, void *ws, int64_t ws_bytes, void *stream, void *side_stream) {
     if (!dims_ok(dims) || !w || !s || !X || !ctx || !dX2 || !g || (!ws && ws_bytes > 0)) return U2GNN_E_ARG;
     const Dims D = make_dims(dims);
+    Arena Pc(nullptr, 0), Pw(nullptr, 0);   // planning pass with this call's schedule (see u2gnn_layer_fwd)
+    layer_bwd(D, w, s, X, Pc, dX2, dX, g, Pw, reinterpret_cast<hipStream_t>(stream),
+              reinterpret_cast<hipStream_t>(side_stream), dX != nullptr);
+    if (Pw.used > (ws ? ws_bytes : 0) || Pc.used > ctx_bytes) return U2GNN_E_ARG;
     static char empty_ws alignas(256)[256];
     Arena C(const_cast<void *>(ctx), ctx_bytes), W(ws ? ws : empty_ws, ws ? ws_bytes : 0);
     return layer_bwd(D, w, s, X, C, dX2, dX, g, W, reinterpret_cast<hipStream_t>(stream),

@@ -234,3 +234,28 @@ def test_device_batch_rejects_out_of_range_input_x():
         ix[4, 2] = bad
         with pytest.raises(IndexError):
             DeviceBatch.from_offsets(ix, off, X, np.array([0, 1]), device="cpu")
+
+
+def test_layer_executor_refuses_undersized_buffers_before_launching():
+    """u2gnn_layer_fwd / u2gnn_layer_bwd plan the call first and refuse a workspace or ctx arena smaller than
+    it takes (U2GNN_E_ARG) before any launch: on this GPU-less host a launch would fail with a HIP error
+    code instead, so -1 shows that nothing was launched (no kernel can write past a caller buffer)."""
+    import ctypes
+    from u2gnn_hip import _lib
+    lib = _lib.hip_lib()
+    dims = _lib.LayerDims(1914, 4, 1024, 1, 0, 0, 0)   # the C5 layer, bf16x3
+    c, f, b = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+    assert lib.u2gnn_layer_sizes(ctypes.byref(dims), 0.5, ctypes.byref(c), ctypes.byref(f), ctypes.byref(b)) == 0
+    fake = ctypes.c_void_p(1 << 40)   # never dereferenced on the host
+    params = _lib.LayerParamsC(*([fake.value] * 12))
+    seeds = _lib.LayerSeeds(0.5, 1, 2, 3, 4)
+    grads = _lib.LayerGrads(*([fake.value] * len(_lib._PKEYS)))
+    rc = lib.u2gnn_layer_fwd(ctypes.byref(dims), ctypes.byref(params), ctypes.byref(seeds), fake, fake, fake, c.value,
+                             fake, f.value - 256, None)
+    assert rc == -1
+    rc = lib.u2gnn_layer_bwd(ctypes.byref(dims), ctypes.byref(params), ctypes.byref(seeds), fake, fake, c.value, fake,
+                             fake, ctypes.byref(grads), fake, b.value - 256, None, None)
+    assert rc == -1
+    rc = lib.u2gnn_layer_bwd(ctypes.byref(dims), ctypes.byref(params), ctypes.byref(seeds), fake, fake, c.value - 256,
+                             fake, fake, ctypes.byref(grads), fake, b.value, None, None)
+    assert rc == -1

@@ -116,9 +116,31 @@ def host_cpu():
     return model, os.cpu_count()
 
 
+def cgroup_cpus():
+    """CPUs this process's cgroup may use (cpu.max quota / period, cgroup v2; v1 cfs files), or None."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else max(1, int(int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        return None if q <= 0 else max(1, q // per)
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_threads():
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
-    return max(1, min(threads, os.cpu_count()))
+    """Host threads for the CPU baseline: every CPU of the process's affinity mask
+    (os.sched_getaffinity, not os.cpu_count(), which counts the whole machine), capped by the cgroup's
+    CPU quota when one is set (threads beyond it only time-slice).  Returns (threads, how)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = cgroup_cpus()
+    threads = min(aff, quota) if quota else aff
+    how = f"{threads} threads = sched_getaffinity ({aff} CPUs)" + (f" capped by the cgroup CPU quota ({quota})"
+                                                                       if quota and quota < aff else "")
+    return max(1, threads), how
 
 
 def launch_ranks(args) -> int:
@@ -183,7 +205,7 @@ def cpu_baseline(hb, sd, args, d, C):
     i.e. the reference's cost) timed on the host cores: forward + loss + backward + clip + Adam;
     median of --cpu-steps (>= 3) steps on one batch."""
     from oracle import u2gnn_oracle as O
-    threads = cpu_threads()
+    threads, how = cpu_threads()
     torch.set_num_threads(threads)
     params = {k: v.detach().cpu().clone().requires_grad_(True) for k, v in sd.items()}
     plist = list(params.values())
@@ -205,7 +227,7 @@ def cpu_baseline(hb, sd, args, d, C):
     t = float(np.median(times))
     model, ncpu = host_cpu()
     return {"value": hb.labels.shape[0] / t, "unit": "graphs/s", "cores": threads, "kind": "port",
-            "cpu_model": model, "host_cpus": ncpu, "step_s": [round(x, 2) for x in times],
+            "cpu_model": model, "host_cpus": ncpu, "threads": how, "step_s": [round(x, 2) for x in times],
             "sample": f"median of {args.cpu_steps} full training steps of one {hb.labels.shape[0]}-graph batch "
                       f"(N={hb.N} nodes, all {args.num_neighbors + 1} neighbour slots, dropout on) "
                       f"= {t:.1f} s/step, oracle/u2gnn_oracle.py on torch CPU, {threads} threads"}
@@ -260,7 +282,7 @@ def unsup_cpu_baseline(hbs, sids, sd, V, T, lr, steps):
     dropout on) on the same batches and sample ids: forward + summed loss + backward + clip + Adam
     over the encoders and the dense [V, D] table; median of `steps` steps."""
     from oracle import u2gnn_oracle as O
-    threads = cpu_threads()
+    threads, how = cpu_threads()
     torch.set_num_threads(threads)
     params = {k: v.detach().cpu().clone().requires_grad_(True) for k, v in sd.items()}
     plist = list(params.values())
@@ -280,7 +302,7 @@ def unsup_cpu_baseline(hbs, sids, sd, V, T, lr, steps):
     t = float(np.median(times))
     model, ncpu = host_cpu()
     return {"value": hbs[0].labels.shape[0] / t, "unit": "graphs/s", "cores": threads, "kind": "port",
-            "cpu_model": model, "host_cpus": ncpu, "step_s": [round(x, 2) for x in times],
+            "cpu_model": model, "host_cpus": ncpu, "threads": how, "step_s": [round(x, 2) for x in times],
             "sample": f"median of {steps} training steps on the first {min(steps, len(hbs))} bench batches "
                       f"(all {hbs[0].input_x.shape[1]} neighbour slots, dropout on, V = {V}), "
                       f"median {t:.2f} s/step, oracle/u2gnn_oracle.py on torch CPU, {threads} threads"}
@@ -508,7 +530,7 @@ def main_small(args):
         runner.close()
     cpu = None
     if args.cpu_baseline:
-        threads = max(1, min(int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count(), os.cpu_count()))
+        threads, how = cpu_threads()
         torch.set_num_threads(threads)
         params = {kk: v.detach().cpu().clone().requires_grad_(True) for kk, v in sd0.items()}
         plist = list(params.values())
@@ -533,7 +555,7 @@ def main_small(args):
             opt.step()
             times.append(time.perf_counter() - t1)
         t = float(np.median(times[5:]))
-        cpu = {"value": 4 / t, "unit": "graphs/s", "cores": threads, "kind": "port",
+        cpu = {"value": 4 / t, "unit": "graphs/s", "cores": threads, "kind": "port", "threads": how,
                "sample": f"{reps - 5} timed training steps of 4-graph {name} batches (all {k + 1} neighbour slots, "
                          f"dropout on), median {1e3 * t:.1f} ms/step, oracle/u2gnn_oracle.py on torch CPU"}
     mean_N = float(np.mean([bt[0].N for bt in batches]))

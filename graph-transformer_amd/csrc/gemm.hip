@@ -577,14 +577,6 @@ inline bool al16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) =
 
 }  // namespace
 
-// The pre-split (x2) kernels (gemm_x2.hip, gemm_x3.hip) are experiments off the layer's path (DESIGN.md
-// sections 5.1 and 5.3): they live in libu2gnn_hip_x2.so (make target x2, tests/test_gemm_x2_gpu.py),
-// not in the product library.  Weak references: without those objects x2 operands are rejected.
-__attribute__((weak)) int u2gnn_gemm_x2_dispatch(const u2gnn_gemm_args *a, GemmP &P, int tile, int split,
-                                                 hipStream_t st);
-__attribute__((weak)) int u2gnn_gemm_x3_dispatch(const u2gnn_gemm_args *a, GemmP &P, int tile, int split,
-                                                 hipStream_t st);
-
 namespace {
 
 // validated launch description of one u2gnn_gemm call
@@ -597,7 +589,9 @@ struct GemmPlan {
 int gemm_plan(const u2gnn_gemm_args *a, GemmPlan &G) {
     if (!a) return U2GNN_E_ARG;
     const bool x2 = a->a_x2 || a->b_x2;
-    if (x2 && (!u2gnn_gemm_x2_dispatch || !u2gnn_gemm_x3_dispatch)) return U2GNN_E_ARG;   // not this build
+    // pre-split (x2) operands were the round-1/2 GEMM experiments (gemm_x2.hip / gemm_x3.hip, DESIGN.md 5.1,
+    // 5.3), measured slower than this kernel and removed in round 4; the x2 OUTPUT (Cx2) stays on the path
+    if (x2) return U2GNN_E_ARG;
     if (x2 ? (!a->A2 || !a->B2) : (!a->A || !a->B)) return U2GNN_E_ARG;
     if (!a->C && !a->Cx2) return U2GNN_E_ARG;
     if (a->M <= 0 || a->N <= 0 || a->K <= 0) return U2GNN_E_ARG;
@@ -741,8 +735,6 @@ int gemm_plan(const u2gnn_gemm_args *a, GemmPlan &G) {
 }
 
 int gemm_launch(const u2gnn_gemm_args *a, GemmPlan &G, hipStream_t st) {
-    if (G.x2 && (G.tile == 300 || G.tile == 301)) return u2gnn_gemm_x3_dispatch(a, G.P, G.tile, G.split, st);
-    if (G.x2) return u2gnn_gemm_x2_dispatch(a, G.P, G.tile, G.split, st);
     if (G.prec == U2GNN_PREC_BF16X3)
         return launch_tile<U2GNN_PREC_BF16X3>(G.P, G.tile, G.ta, G.tb, G.epi, G.split, G.clamp, st);
     if (G.prec == U2GNN_PREC_BF16)

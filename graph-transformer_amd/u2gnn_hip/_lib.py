@@ -18,8 +18,6 @@ INCLUDE_DIR = os.path.join(REPO_ROOT, "include")
 # U2GNN_HIP_LIB: an alternative build of the same kernels (tools/ experiments)
 HIP_LIB_PATH = os.environ.get("U2GNN_HIP_LIB") or os.path.join(LIB_DIR, "libu2gnn_hip.so")
 LUS_LIB_PATH = os.path.join(LIB_DIR, "libu2gnn_lus.so")
-# the product kernels plus the pre-split (x2) GEMM experiments (gemm_x2.hip / gemm_x3.hip, off the path)
-X2_LIB_PATH = os.path.join(LIB_DIR, "libu2gnn_hip_x2.so")
 
 
 class U2GNNNativeError(RuntimeError):
@@ -195,7 +193,6 @@ _LUS_SIGS = {
 
 _hip = None
 _lus = None
-_x2 = None
 
 
 def _bind(lib, sigs):
@@ -224,17 +221,6 @@ def hip_lib():
     return _hip
 
 
-def x2_lib():
-    """libu2gnn_hip_x2.so: the product kernels plus the x2 experiments (u2gnn_gemm with pre-split
-    operands).  Used only by the x2 tests and tools; the product path never loads it."""
-    global _x2
-    if _x2 is None:
-        if not os.path.exists(X2_LIB_PATH):
-            raise U2GNNNativeError(f"{X2_LIB_PATH} not built: run `make -C graph-transformer_amd/csrc`")
-        _x2 = _bind(ctypes.CDLL(X2_LIB_PATH), _HIP_SIGS)
-        if _x2.u2gnn_abi_version() != ABI_VERSION:
-            raise U2GNNNativeError("x2 library ABI mismatch")
-    return _x2
 
 
 def lus_lib():

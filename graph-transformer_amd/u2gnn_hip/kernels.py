@@ -55,8 +55,6 @@ _EPI_NAMES = ["STORE", "BIAS", "BIAS_DROP_RESID", "BIAS_RELU_DROP", "RELU_DROP_B
 def gemm_symbol(precision, M, N, split_k, tile, trans_a, trans_b, epilogue, clamp_a=False, x2=False):
     """Mirror of the C dispatcher's kernel choice (gemm.hip u2gnn_gemm) -> template symbol."""
     b = lambda x: "true" if x else "false"  # noqa: E731
-    if x2:   # gemm_x2.hip: pre-split operands, 256x128 (8 waves) or 128x128 (4 waves)
-        return f"gemm_x2_kernel<{tile}, 128, {b(trans_a)}, {b(trans_b)}, {int(epilogue)}>"
     if tile == 0:
         can128 = M % 128 == 0 and N % 128 == 0
         tile = 128 if (can128 and (M // 128) * (N // 128) * max(split_k, 1) >= 480) else 64
@@ -91,8 +89,9 @@ def gemm(A, B, C, M, N, K, lda, ldb, ldc, trans_a=False, trans_b=False, epilogue
     a, x2 = _gemm_args(A, B, C, M, N, K, lda, ldb, ldc, trans_a, trans_b, epilogue, split_k, slab_stride, bias, aux0,
                        aux1, rowvec, ld_aux, alpha, scale_cols, p_drop, seed, precision, tile, keep, clamp_a, Cx2, ldcx2,
                        rowstat, m_valid, n_valid, ln, rowpart)
-    # pre-split operands exist only in the experiments library (x2_lib); the product library rejects them
-    check((_lib.x2_lib() if x2 else hip_lib()).u2gnn_gemm(ctypes.byref(a), _s()), "u2gnn_gemm")
+    if x2:   # pre-split operands: the removed round-1/2 experiments (gemm.hip rejects them)
+        raise _lib.U2GNNNativeError("u2gnn_gemm: pre-split (x2) operands are not supported")
+    check(hip_lib().u2gnn_gemm(ctypes.byref(a), _s()), "u2gnn_gemm")
     if rec:
         ev1.record()
         REC.records.append((gemm_symbol(precision, M, N, split_k, tile, trans_a, trans_b, epilogue, clamp_a, x2),

@@ -27,16 +27,18 @@ class SupTrainer:
     def next_seed(self) -> int:
         return int(torch.randint(0, 2 ** 62, (1,), generator=self.gen).item())
 
-    def forward_backward(self, b: DeviceBatch, train: bool = True) -> torch.Tensor:
+    def forward_backward(self, b: DeviceBatch, train: bool = True, seed: Optional[int] = None) -> torch.Tensor:
+        """seed: the step's dropout seed (default: the trainer's own generator; the data-parallel CLIs pass
+        the batch's stream-position seed, u2gnn_hip.cli.step_seed)."""
         core = self.m.core
-        scores, ctx = core.forward(b, train, need_ctx=True, seed=self.next_seed())
+        scores, ctx = core.forward(b, train, need_ctx=True, seed=self.next_seed() if seed is None else int(seed))
         dscores = torch.empty_like(scores)
         K.smoothed_ce(scores, b.labels, b.B, core.C, 0.1, self.loss, dscores)
         core.backward(ctx, dscores, self.flat.grads)
         return self.loss
 
-    def step(self, b: DeviceBatch, train: bool = True) -> torch.Tensor:
-        loss = self.forward_backward(b, train)
+    def step(self, b: DeviceBatch, train: bool = True, seed: Optional[int] = None) -> torch.Tensor:
+        loss = self.forward_backward(b, train, seed)
         if self.grad_sync is not None:
             self.grad_sync(self.flat)
         self.opt.step()

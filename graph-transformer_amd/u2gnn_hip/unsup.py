@@ -75,9 +75,15 @@ class UnSupTrainer:
     def next_seed(self) -> int:
         return int(torch.randint(0, 2 ** 62, (1,), generator=self.gen).item())
 
-    def forward_backward(self, b: DeviceBatch, sample_ids: torch.Tensor, train: bool = True):
+    def forward_backward(self, b: DeviceBatch, sample_ids: torch.Tensor, train: bool = True,
+                         seed: Optional[int] = None):
         core, ss = self.core, self.m.ss
-        seed = self.next_seed()
+        # the dense ss.weight gradient must be all zero on entry (the backward adds rows into it): rows a
+        # previous forward_backward wrote and no step()/clear_row_grads() zeroed (an evaluation loss, a
+        # gradient check, an exception between backward and step) are zeroed first
+        if self._touched:
+            self.clear_row_grads()
+        seed = self.next_seed() if seed is None else int(seed)
         p = core.p_out if train else 0.0
         ds = site_seed(seed, 0, 0, SITE_SS_DROP)
         OVd, sctx = core.encode(b, train, True, seed, p, ds)   # dropout fused into the concatenation
@@ -111,8 +117,8 @@ class UnSupTrainer:
         core.encode_backward(sctx, dOV, self.flat.grads, p, ds)   # dropout's backward fused into the split
         return self.loss
 
-    def step(self, b: DeviceBatch, sample_ids: torch.Tensor, train: bool = True):
-        loss = self.forward_backward(b, sample_ids, train)
+    def step(self, b: DeviceBatch, sample_ids: torch.Tensor, train: bool = True, seed: Optional[int] = None):
+        loss = self.forward_backward(b, sample_ids, train, seed)
         if self.grad_sync is not None:
             self.grad_sync(self.flat)
         self.opt.step()

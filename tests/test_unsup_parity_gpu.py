@@ -75,6 +75,28 @@ def test_unsup_fused_trainer_step(golden_dir):
             assert close(p.detach(), z["after." + n]), n
 
 
+def test_unsup_forward_backward_twice_leaves_one_batch_gradient(golden_dir):
+    """a second forward_backward without step()/clear_row_grads() in between (an evaluation
+    loss, a gradient check) must leave exactly ONE batch's ss.weight gradient -- the rows the first
+    call added are zeroed, not carried into every later clip norm and Adam update."""
+    from u2gnn_hip.core import DeviceBatch
+    from u2gnn_hip.unsup import UnSupTrainer
+    z = dict(np.load(os.path.join(golden_dir, "ptc_unsup.npz")))
+    m, _ = _unsup_model(z)
+    tr = UnSupTrainer(m, lr=float(z["lr"]))
+    b = DeviceBatch.from_offsets(z["input_x"], z["offsets"], z["X"], input_y=z["input_y"], device=DEV)
+    sid = torch.from_numpy(z["sample_ids"]).to(DEV)
+    other = torch.from_numpy((z["sample_ids"] + 17) % int(z["meta"][-1])).to(DEV)
+    tr.forward_backward(b, other, train=False)          # rows this call touches differ from the next
+    tr.forward_backward(b, sid, train=False)
+    twice = tr.flat.gflat.clone()
+    tr.clear_row_grads()
+    assert tr.flat.grads["ss.weight"].abs().max().item() == 0.0
+    tr.forward_backward(b, sid, train=False)
+    assert torch.equal(twice, tr.flat.gflat)
+    assert close(tr.flat.grads["ss.weight"], z["grad.ss.weight"])
+
+
 def test_graph_embeddings_match_spmm_over_all_graphs():
     """evaluate() of train_pytorch_U2GNN_UnSup.py:167-169: spmm(graph_pool, ss.weight) with graph_pool
     built over ALL graphs (train_pytorch_U2GNN_UnSup.py:92-94) -- the per-graph sums of the learned

@@ -373,38 +373,70 @@ def main_c5(args):
                        num_U2GNN_layers=args.num_hidden_layers, device=dev, precision=args.precision)
     sd0 = {k: v.clone() for k, v in model.state_dict().items() if k in set(model.trainable_names())}
     model = model.to(dev)
-    # one sample draw per batch of the single stream; rank r keeps draw r of each group
-    sids_host = []
-    for _ in range(args.distinct_batches):
-        draws = [model.ss.draw_samples() for _ in range(world)]
-        sids_host.append(draws[rank])
     trainer = UnSupTrainer(model, lr=args.lr, max_norm=0.5, seed=123 + rank)
     if dist is not None:
         broadcast_params(trainer.flat)
         sync = UnSupGradSync(trainer.flat, max_batch_nodes(store.node_start, bs))
         trainer.grad_sync = trainer.row_sync = sync
-    batches = [(DeviceBatch.from_offsets(h.input_x, h.offsets, h.X_concat, None, device=dev, input_y=h.input_y),
-                torch.from_numpy(s).to(dev)) for h, s in zip(host, sids_host)]
-    nb = len(batches)
-    graph = args.graph != 0 and dist is None
+    dbs = [DeviceBatch.from_offsets(h.input_x, h.offsets, h.X_concat, None, device=dev, input_y=h.input_y)
+           for h in host]
+    nb = len(dbs)
+    S = 512
+    # sample ids: drawn on the host EVERY step, as the reference does (sampled_softmax.py:31-42: the C++
+    # log-uniform sampler, then H2D) -- one draw per batch of the stream, rank r keeps draw r of each group;
+    # the ids go through a ring of page-locked buffers into the step's device buffer (stream-ordered H2D, so
+    # a captured graph reads the fresh ids at replay)
+    sid_dev = [torch.zeros(S, dtype=torch.int64, device=dev) for _ in range(nb)]
+    ring = [(torch.empty(S, dtype=torch.int64, pin_memory=True), [None]) for _ in range(8)]
+    draws_log = []
+    counter = [0]
+
+    def draw_into(i):
+        draws = [model.ss.draw_samples() for _ in range(world)]
+        ids = np.asarray(draws[rank], dtype=np.int64)
+        if len(draws_log) < nb:
+            draws_log.append(ids)
+        buf, ev = ring[counter[0] % len(ring)]
+        counter[0] += 1
+        if ev[0] is not None:
+            ev[0].synchronize()   # the H2D of this pinned slot 8 steps ago is done
+        buf.numpy()[:] = ids
+        sid_dev[i].copy_(buf, non_blocking=True)
+        ev[0] = torch.cuda.Event()
+        ev[0].record()
+
+    batches = [(dbs[i], sid_dev[i]) for i in range(nb)]
+    for i in range(nb):   # first ids of every distinct batch (also what the captures run with)
+        draw_into(i)
+    # HIP-graph replay of the step, also data parallel (the encoder all-reduce and the ss.weight row
+    # all-gather captured with it; RCCL communicators are set up by one eager step first)
+    graph = args.graph != 0
     runner = None
     try:
         if graph:   # one captured HIP graph per distinct batch, captured (not run) before the warmup
             from u2gnn_hip.train import StepGraphs
+            if dist is not None:
+                trainer.step(*batches[0])
+                torch.cuda.synchronize()
+                dist.barrier()
             runner = StepGraphs(trainer)
             for bt in batches:
                 runner.capture(*bt)
         step = runner.step if runner is not None else trainer.step
-        for i in range(args.warmup):
+
+        def one(i):
+            draw_into(i % nb)
             step(*batches[i % nb])
+        for i in range(args.warmup):
+            one(i)
         torch.cuda.synchronize()
         if dist is not None:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for i in range(args.steps):
-            step(*batches[(args.warmup + i) % nb])
-        t_issue = time.perf_counter() - t0          # host time to enqueue the K steps
+            one(args.warmup + i)
+        t_issue = time.perf_counter() - t0          # host time to enqueue the K steps (sampler draws included)
         torch.cuda.synchronize()
         if dist is not None:
             dist.barrier()
@@ -413,6 +445,7 @@ def main_c5(args):
     finally:
         if runner is not None:
             runner.close()
+    sids_host = draws_log
     if dist is not None:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -438,6 +471,15 @@ def main_c5(args):
         if dist is None:
             roof = c5_group_roofline(args, trainer, batches, elapsed)
     mean_N = float(np.mean([b.N for b, _ in batches]))
+    # step-level HBM roofline: algorithmic bytes of the whole step = the dense Adam sweep
+    # over ss.weight (p, g, m, v read; p, m, v written), the row gathers / scatters of the sampled softmax
+    # and the encoder's parameter sweep, over the measured step time
+    n_enc = trainer.flat.n - V * 4
+    step_bytes = 4.0 * 6 * V * 4 + 4.0 * 3 * (mean_N + S) * 4 + 4.0 * 3 * n_enc * 7 / 3
+    step_ach = step_bytes / (elapsed / args.steps) / 1e9
+    step_roof = {"bound": "hbm", "achieved": round(step_ach, 1), "peak": 8000.0, "unit": "GB/s",
+                 "frac": round(step_ach / 8000.0, 4), "algorithmic_bytes_per_step": round(step_bytes),
+                 "what": "SURVEY.md §8(d) C5 bytes per step (4*6*V*D + 4*3*(N+S)*D + 4*3*P_enc*7/3) / ms_per_step"}
     out = {"metric": METRIC_C5, "value": round(args.steps * bs * world / elapsed, 2), "unit": "graphs/s",
            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
            "ms_per_step": round(1e3 * elapsed / args.steps, 3), "higher_is_better": True, "scaling": "weak",
@@ -451,7 +493,8 @@ def main_c5(args):
                                                      else ""),
                       "precision": args.precision, "hip_graph": graph},
            "final_loss": round(loss, 4), "host_issue_ms_per_step": round(1e3 * t_issue / args.steps, 3),
-           "roofline": roof, "optimizer": opt_roof, "cpu_baseline": None}
+           "roofline": roof, "optimizer": opt_roof, "step_hbm": step_roof, "cpu_baseline": None,
+           "samples": "512 log-uniform ids drawn on the host every step (C++ sampler) and copied to HBM"}
     if rank == 0 and world == 1 and args.cpu_baseline:
         out["cpu_baseline"] = unsup_cpu_baseline(host, sids_host, sd0, V, args.num_timesteps, args.lr,
                                                  max(3, args.cpu_steps))

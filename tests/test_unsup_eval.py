@@ -1,11 +1,13 @@
 """UnSup evaluation (train_pytorch_U2GNN_UnSup.py:164-188): graph embeddings =
 spmm(graph_pool over ALL graphs, ss.weight), then 10-fold LogisticRegression(liblinear, tol=1e-3).
-Pinned by tests/golden/ptc_unsup_eval.npz (tests/golden/make_eval_golden.py: the oracle's
-restatement on PTC for a seeded ss.weight).  CPU: the oracle and the product's host half
-(util.separate_data_idx + unsup.fold_accuracies) reproduce the fixture exactly.  GPU: the product's
-device embeddings (u2gnn_pool_fwd over all graphs) give the same accuracies; fp32 sums in another
-order may move a test graph across the decision boundary, so at most one test graph per fold may
-differ."""
+Pinned by tests/golden/ptc_unsup_eval.npz (tests/golden/make_eval_golden.py, round 4: generated from the
+REFERENCE's util.load_data / separate_data_idx / get_graphpool, executed here, with evaluate()'s ten-line body
+-- spmm + LogisticRegression(liblinear) per fold -- restated, because the UnSup script itself cannot run;
+the fixture's numbers equal the oracle restatement's of rounds 2-3 exactly).  CPU: the oracle and the
+product's host half (util.separate_data_idx + unsup.fold_accuracies) reproduce the fixture exactly.  GPU:
+the product's device embeddings (u2gnn_pool_fwd over all graphs) give the same accuracies; fp32 sums in
+another order could move one test graph across a decision boundary, so at most ONE test prediction in
+total over the ten folds may differ, and the test reports which fold moved."""
 import os
 
 import numpy as np
@@ -60,6 +62,5 @@ def test_device_embeddings_evaluation_matches_fixture():
     start = GraphStore(graphs).node_start
     emb = graph_embeddings(torch.from_numpy(W).cuda(), start).cpu().numpy()
     got = np.asarray(fold_accuracies(emb, labels, folds))
-    one = np.array([1.0 / len(te) for _, te in folds])
-    assert np.all(np.abs(got - acc) <= one + 1e-12), (got, acc)
-    assert np.sum(got != acc) <= 2
+    moved = np.rint(np.abs(got - acc) * np.array([len(te) for _, te in folds])).astype(int)
+    assert moved.sum() <= 1, f"test predictions changed per fold: {moved.tolist()} ({got} vs {acc})"

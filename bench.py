@@ -62,6 +62,8 @@ def parse():
     ap.add_argument("--pipeline-steps", type=int, default=20,
                     help="C4 at N=1: steps of the on-the-fly pipeline line (native assembly + copy-stream H2D + "
                          "GPU feature gather per step); 0 = skip")
+    ap.add_argument("--fp32-steps", type=int, default=10,
+                    help="C4 at N=1: timed steps of the same step in exact fp32 beside the headline (0 = skip)")
     ap.add_argument("--launch-check", action="store_true",
                     help="ranks report (rank, world) and exit before touching the GPU (tests the --gpus launcher)")
     ap.add_argument("--no-roofline", action="store_true")
@@ -259,6 +261,36 @@ def pipeline_rate(store, trainer, args, dev, resident_value):
             "steps": args.pipeline_steps, "ratio_to_resident": round(v / resident_value, 4),
             "what": "per step: native batch assembly (numpy MT19937 stream continued in C++) into page-locked "
                     "buffers, H2D on a copy stream, GPU feature gather, training step"}
+
+
+def exact_line(args, batches, sd0, dev, d, C):
+    """The same C4 training step in the exact fp32 matrix-core precision (v_mfma_f32_32x32x2_f32, the parity
+    path) on the same batches and initial weights, beside the bf16x3 headline (the price of the
+    exact path on record).  args.fp32_steps timed steps after 2 warmup steps; not the headline value."""
+    from pytorch_U2GNN_Sup import TransformerU2GNN
+    from u2gnn_hip.train import SupTrainer
+    m = TransformerU2GNN(feature_dim_size=d, ff_hidden_size=args.ff_hidden_size, num_classes=C,
+                         num_self_att_layers=args.num_timesteps, dropout=0.5,
+                         num_U2GNN_layers=args.num_hidden_layers, precision="fp32")
+    m.load_state_dict(sd0)
+    m = m.to(dev).train()
+    tr = SupTrainer(m, lr=args.lr, max_norm=0.5, seed=123)
+    nb = len(batches)
+    for i in range(2):
+        tr.step(batches[i % nb])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.fp32_steps):
+        tr.step(batches[(2 + i) % nb])
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    out = {"precision": "fp32", "value": round(args.fp32_steps * args.batch_size / el, 2), "unit": "graphs/s",
+           "ms_per_step": round(1e3 * el / args.fp32_steps, 3), "steps": args.fp32_steps,
+           "final_loss": round(float(tr.loss.item()), 5),
+           "what": "the same training step with every matrix-core product in exact fp32 (v_mfma_f32_32x32x2_f32)"}
+    del tr, m
+    torch.cuda.empty_cache()
+    return out
 
 
 METRIC_C5 = "graphs/sec (fwd+bwd) U2GNN-UnSup REDDIT-M5K k=16 T=4 S=512 MI355X"
@@ -807,6 +839,8 @@ def main():
            "roofline": roof, "gather": None, "cpu_baseline": None}
     if rank == 0:
         out["gather"] = gather_roofline(used[0], d, args.ff_hidden_size, K, dev)
+    if rank == 0 and world == 1 and args.fp32_steps > 0 and args.precision != "fp32" and args.attention == "nodes":
+        out["fp32"] = exact_line(args, batches, sd0, dev, d, C)
     if rank == 0 and world == 1 and args.pipeline_steps > 0 and args.attention == "nodes":
         out["pipeline"] = pipeline_rate(store, trainer, args, dev, value)
     if rank == 0 and world == 1 and args.cpu_baseline:

@@ -243,6 +243,14 @@ int gemm_split(Arena &W, const Dims &D, const float *A, const float *B, float *C
     int64_t split = target / (tiles > 0 ? tiles : 1);
     if (Kd / (4 * bk) < split) split = Kd / (4 * bk);
     if (split < 1) split = 1;
+#ifdef U2GNN_EXP_ATT_SPLIT   // experiment: split-K depth of the grouped dQ / dK products
+    if (role == U2GNN_ROLE_DQ || role == U2GNN_ROLE_DK) {
+#ifdef U2GNN_EXP_ATT_TILE128
+        t = 128, tiles = (M / 128) * (N / 128);
+#endif
+        split = U2GNN_EXP_ATT_SPLIT;
+    }
+#endif
     // slab cap of the weight gradients (engine.wgrad_split_cap): 8 for node-sized depths, 16 for
     // token-sized ones (neighbour mode, K = N(k+1) rows)
     const int64_t wgrad_split_max = Kd <= 8192 ? 8 : 16;
@@ -651,6 +659,12 @@ int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
                              nullptr, false, dv_side ? so : st, pd > 0.f, -1, U2GNN_ROLE_DV, nullptr,
                              dv_side ? nullptr : att));
         if (dv_side) U2GNN_TRY(sd.mark(&dv_done));
+#ifdef U2GNN_EXP_EARLY_FLUSH
+        // experiment: the layer's held-back FFN / LayerNorm / out-projection parameter work goes out on the
+        // side stream behind dV (beside dS, dQ, dK) instead of at the end of the layer (beside the next
+        // layer's FFN backward); only the in-projection's gradients are left for the end
+        if (dv_side && need_dx) U2GNN_TRY(flush(df, W, so));
+#endif
         float *delta = ln_delta ? delta_ln : W.take<float>(Np);
         if (!plan && !ln_delta) U2GNN_TRY(u2gnn_rowdot(dO, dp, c.O, dp, delta, Np, dp, st));
         float *dS = W.take<float>(Np * Np);

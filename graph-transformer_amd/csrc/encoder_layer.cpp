@@ -473,7 +473,8 @@ int layer_fwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
         g.a.bias = w->b_in;
         g.a.alpha = (float)(1.0 / std::sqrt((double)d));
         g.a.scale_cols = dp;
-        if (fused) g.a.Cx2 = qkv2, g.a.ldcx2 = 6 * dp;
+        // the x2 copy the fused softmax.P.V kernel reads: its V block only (Q and K are never read in x2)
+        if (fused) g.a.Cx2 = qkv2, g.a.ldcx2 = 6 * dp, g.a.cx2_col0 = (int32_t)(2 * dp);
         U2GNN_TRY(g.run(st, plan));
     }
     const float *Q = c.QKV, *Kt = c.QKV + dp, *V = c.QKV + 2 * dp;

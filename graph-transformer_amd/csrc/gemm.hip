@@ -616,6 +616,7 @@ int gemm_plan(const u2gnn_gemm_args *a, GemmPlan &G) {
     // 16-byte epilogue: C, bias and aux rows are read/written as float4; x2 output as 8-byte pairs
     if ((a->C && (!al16(a->C) || (a->ldc & 3))) || (split > 1 && (a->slab_stride & 3))) return U2GNN_E_ALIGN;
     if (a->Cx2 && (!al16(a->Cx2) || (a->ldcx2 & 15) || (a->N & 7))) return U2GNN_E_ALIGN;
+    if (a->cx2_col0 < 0 || (a->cx2_col0 & 7)) return U2GNN_E_ARG;
     if ((a->bias && !al16(a->bias)) || (a->aux0 && !al16(a->aux0)) || (a->aux1 && !al16(a->aux1)) ||
         ((a->aux0 || a->aux1) && (a->ld_aux & 3)))
         return U2GNN_E_ALIGN;
@@ -710,6 +711,7 @@ int gemm_plan(const u2gnn_gemm_args *a, GemmPlan &G) {
     P.B2 = static_cast<const __bf16 *>(a->B2);
     P.Cx2 = static_cast<__bf16 *>(a->Cx2);
     P.ldcx2 = a->ldcx2;
+    P.cx2_col0 = a->cx2_col0;
     P.rowstat = reinterpret_cast<const float2 *>(a->rowstat);
     P.m_valid = (int32_t)a->m_valid;
     P.n_valid = (int32_t)a->n_valid;

@@ -29,6 +29,7 @@ struct GemmP {
     const __bf16 *B2;
     __bf16 *Cx2;          // non-null: the epilogue also writes C in x2 format
     int64_t ldcx2;        // bf16 elements
+    int32_t cx2_col0;     // Cx2 receives columns >= cx2_col0 only
     const float2 *rowstat;   // ATTN_DS_RECOMP: (row max, 1/row sum) of the forward softmax
     int32_t m_valid, n_valid;   // ATTN_DS_RECOMP: real rows / keys (P = 0 beyond)
     const uint64_t *epoch;      // seed epoch at launch (u2gnn_set_seed_epoch): seed ^= *epoch * golden
@@ -256,7 +257,7 @@ __device__ __forceinline__ float store_slice(const GemmP &P, float *C, const f32
             else
                 o = epilogue4<EPI>(P, row, col, v, e.a[j][g], e.b[j][g], e.kb[j][g], dl);
             if (P.C) *reinterpret_cast<float4 *>(C + (int64_t)row * P.ldc + col) = o;
-            if (P.Cx2) store_x2_4(P.Cx2, P.ldcx2, row, col, o);
+            if (P.Cx2 && col >= P.cx2_col0) store_x2_4(P.Cx2, P.ldcx2, row, col, o);
             if constexpr (EPI == U2GNN_EPI_STORE_ROWDOT) {
                 const float4 x = e.a[j][g];
                 rs += o.x * x.x + o.y * x.y + o.z * x.z + o.w * x.w;

@@ -30,7 +30,7 @@ ERRORS = {-1: "bad argument", -2: "misaligned pointer / leading dimension", -3: 
 
 EPI_STORE, EPI_BIAS, EPI_BIAS_DROP_RESID, EPI_BIAS_RELU_DROP, EPI_RELU_DROP_BWD, EPI_ACCUM, EPI_ATTN_DS, \
     EPI_ATTN_DS_SIGNED, EPI_ATTN_DS_RECOMP, EPI_BIAS_DROP_RESID_LN, EPI_STORE_ROWDOT, EPI_STORE_ROWSTAT = range(12)
-ABI_VERSION = 11   # include/u2gnn_hip.h U2GNN_ABI_VERSION
+ABI_VERSION = 12   # include/u2gnn_hip.h U2GNN_ABI_VERSION
 PREC_F32, PREC_BF16X3, PREC_BF16 = 0, 1, 2
 
 
@@ -51,7 +51,7 @@ class GemmArgs(ctypes.Structure):
         ("precision", c_int32),
         ("tile", c_int32),
         ("keep", c_void_p), ("ld_keep", c_int64),
-        ("clamp_a", c_int32), ("reserved", c_int32),
+        ("clamp_a", c_int32), ("cx2_col0", c_int32),
         # ABI v3: pre-split (x2) operands / outputs
         ("a_x2", c_int32), ("b_x2", c_int32),
         ("A2", c_void_p), ("B2", c_void_p), ("Cx2", c_void_p), ("ldcx2", c_int64),

@@ -365,7 +365,7 @@ def encoder_layer_forward(X: torch.Tensor, w: PackedLayer, p: LayerParams, dims:
     K.gemm(X, w.W_in, QKV, Np, 3 * dp, dp, dp, dp, 3 * dp, trans_b=True, epilogue=E.EPI_BIAS, bias=w.b_in,
            alpha=1.0 / math.sqrt(d), scale_cols=dp, precision=_rp("in_proj", prec), flops=6.0 * N * d * d,
            tile=256 if (prec != "fp32" and Np % 256 == 0 and (Np // 256) * (3 * dp // 128) >= BIG_TILE_BLOCKS) else 0,
-           Cx2=QKV2, ldcx2=6 * dp)
+           Cx2=QKV2, ldcx2=6 * dp, cx2_col0=2 * dp)
     Q, Kt, V = QKV[:, :dp], QKV[:, dp:2 * dp], QKV[:, 2 * dp:]
     if fused:
         # S = Q K^T written straight into the image buffer, with the softmax row partials of each 64-column

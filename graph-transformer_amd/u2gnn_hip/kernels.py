@@ -70,6 +70,7 @@ def gemm_symbol(precision, M, N, split_k, tile, trans_a, trans_b, epilogue, clam
 def gemm(A, B, C, M, N, K, lda, ldb, ldc, trans_a=False, trans_b=False, epilogue=_lib.EPI_STORE, split_k=1,
          slab_stride=0, bias=None, aux0=None, aux1=None, rowvec=None, ld_aux=0, alpha=1.0, scale_cols=0, p_drop=0.0,
          seed=0, precision="fp32", tile=0, flops=None, keep=None, clamp_a=False, Cx2=None, ldcx2=0, rowstat=None,
+         cx2_col0=0,
          m_valid=0, n_valid=0, ln=None, rowpart=None):
     """C[M,N] (epilogue) sum_k A(m,k) B(k,n).  A/B/C may be views (pointer arithmetic via
     storage offsets is done by torch's data_ptr()).  ``flops``: algorithmic FLOPs of the
@@ -88,7 +89,7 @@ def gemm(A, B, C, M, N, K, lda, ldb, ldc, trans_a=False, trans_b=False, epilogue
         ev0.record()
     a, x2 = _gemm_args(A, B, C, M, N, K, lda, ldb, ldc, trans_a, trans_b, epilogue, split_k, slab_stride, bias, aux0,
                        aux1, rowvec, ld_aux, alpha, scale_cols, p_drop, seed, precision, tile, keep, clamp_a, Cx2, ldcx2,
-                       rowstat, m_valid, n_valid, ln, rowpart)
+                       rowstat, m_valid, n_valid, ln, rowpart, cx2_col0=cx2_col0)
     if x2:   # pre-split operands: the removed round-1/2 experiments (gemm.hip rejects them)
         raise _lib.U2GNNNativeError("u2gnn_gemm: pre-split (x2) operands are not supported")
     check(hip_lib().u2gnn_gemm(ctypes.byref(a), _s()), "u2gnn_gemm")
@@ -114,7 +115,7 @@ def gemm_group(calls):
 def _gemm_args(A, B, C, M, N, K, lda, ldb, ldc, trans_a=False, trans_b=False, epilogue=_lib.EPI_STORE, split_k=1,
                slab_stride=0, bias=None, aux0=None, aux1=None, rowvec=None, ld_aux=0, alpha=1.0, scale_cols=0,
                p_drop=0.0, seed=0, precision="fp32", tile=0, keep=None, clamp_a=False, Cx2=None, ldcx2=0,
-               rowstat=None, m_valid=0, n_valid=0, ln=None, rowpart=None):
+               rowstat=None, m_valid=0, n_valid=0, ln=None, rowpart=None, cx2_col0=0):
     _dev(A, B, C, Cx2, rowstat)
     x2 = A.dtype == torch.bfloat16
     if x2 != (B.dtype == torch.bfloat16):
@@ -127,7 +128,7 @@ def _gemm_args(A, B, C, M, N, K, lda, ldb, ldc, trans_a=False, trans_b=False, ep
         a.A, a.B = A.data_ptr(), B.data_ptr()
     a.C = C.data_ptr() if C is not None else None
     if Cx2 is not None:
-        a.Cx2, a.ldcx2 = Cx2.data_ptr(), int(ldcx2)
+        a.Cx2, a.ldcx2, a.cx2_col0 = Cx2.data_ptr(), int(ldcx2), int(cx2_col0)
     if rowstat is not None:
         a.rowstat = rowstat.data_ptr()
     a.m_valid, a.n_valid = int(m_valid), int(n_valid)

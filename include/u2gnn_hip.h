@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define U2GNN_ABI_VERSION 11
+#define U2GNN_ABI_VERSION 12
 
 #define U2GNN_OK 0
 #define U2GNN_E_ARG (-1)    /* bad size / null pointer */
@@ -114,7 +114,8 @@ typedef struct u2gnn_gemm_args {
     int64_t ld_keep;      /* words per row of keep */
     int32_t clamp_a;      /* 1: A elements below +0 are read as 0 (the signed probability image as Pd
                              for P.V and dP^T.dO); STORE epilogue and trans_b = 0 only */
-    int32_t reserved;
+    int32_t cx2_col0;     /* ABI v12: Cx2 receives only output columns >= cx2_col0 (a multiple of 8; 0 = all):
+                             the in-projection writes the x2 copy of its V block only */
     /* ---- ABI v3: pre-split (x2) operands and outputs ---- */
     int32_t a_x2, b_x2;   /* 1: A (B) is an x2 bf16 matrix (A2 / B2, lda / ldb in bf16 elements);
                              both or neither; requires BF16X3 and tile 256 or 128 */

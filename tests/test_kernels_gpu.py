@@ -840,3 +840,19 @@ def test_adam_sq_equals_sqnorm_then_adam(n):
     torch.cuda.synchronize()
     for a, b in zip(*out):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("col0", [0, 128, 256])
+def test_cx2_output_from_column(col0):
+    """ABI v12 cx2_col0: the epilogue's x2 copy covers only columns >= col0 (the in-projection writes the x2
+    copy of its V block only); those columns equal split_x2 of the fp32 result, the others stay untouched."""
+    M, N, Kd = 256, 384, 64
+    A, B = _mk(M, Kd, seed=3), _mk(N, Kd, seed=4)
+    C = torch.empty(M, N, device=DEV)
+    sentinel = torch.full((M, 2 * N), 7.0, device=DEV, dtype=torch.bfloat16)
+    K.gemm(A, B, C, M, N, Kd, Kd, Kd, N, trans_b=True, precision="bf16x3", Cx2=sentinel, ldcx2=2 * N, cx2_col0=col0)
+    ref = torch.empty(M, 2 * N, device=DEV, dtype=torch.bfloat16)
+    K.split_x2(C, N, ref, 2 * N, M, N)
+    torch.cuda.synchronize()
+    assert torch.equal(sentinel[:, 2 * col0:], ref[:, 2 * col0:])
+    assert bool((sentinel[:, :2 * col0] == 7.0).all())

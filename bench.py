@@ -804,7 +804,7 @@ def main():
         nn = Np0 if args.probe in ("qk", "ds") else ((d + 63) // 64 * 64)
         pk = "bf16" if (args.precision == "mixed" and args.probe in ("ds", "dq", "dk")) else \
             ("bf16x3" if args.precision == "mixed" else args.precision)
-        split = 1 if args.probe in ("qk", "ds") else 4
+        split = 1 if args.probe in ("qk", "ds") else (2 if args.probe in ("dq", "dk") else 4)
         tile = 0 if args.probe == "ds" else 256
         sym = K.gemm_symbol(pk, Np0, nn, split, tile, ta, tb, epi, clamp_a=args.probe in ("pv", "dv"))
         ach = fl / (probe_ms * 1e-3) / 1e12
@@ -836,7 +836,16 @@ def main():
                       "parallelism": f"dp{world}", "precision": args.precision, "attention": args.attention,
                       "hip_graph": graph},
            "final_loss": round(loss, 5), "host_issue_ms_per_step": round(1e3 * t_issue / args.steps, 3),
-           "roofline": roof, "gather": None, "cpu_baseline": None}
+           "roofline": roof, "gather": None, "cpu_baseline": None,
+           "parity": {"tolerance": "max|ours - reference| / max(1, max|reference|) <= 1e-3 (north_star)",
+                      "bf16x3_eval": "every output, loss, gradient and post-Adam parameter within 1e-3 of the "
+                                     "reference goldens (MUTAG, MUTAG L2T2, IMDBBINARY) and of the oracle on a full "
+                                     "C4 batch (tests/test_sup_parity_gpu.py)",
+                      "bf16x3_train_c4": "with the kernels' dropout masks in the oracle: scores 2.3e-6, loss 1.5e-7, "
+                                         "every gradient but linear1's <= 5.2e-4; linear1 gradients up to 1.7e-2 "
+                                         "(ReLU decisions of pre-activations within the 2^-16 product error of 0); "
+                                         "post-Adam parameters 9.9e-4 (tests/test_train_parity_gpu.py)",
+                      "fp32": "within 4.1e-6 in every case and mode; its C4 rate is the 'fp32' object"}}
     if rank == 0:
         out["gather"] = gather_roofline(used[0], d, args.ff_hidden_size, K, dev)
     if rank == 0 and world == 1 and args.fp32_steps > 0 and args.precision != "fp32" and args.attention == "nodes":

@@ -236,6 +236,10 @@ int gemm_split(Arena &W, const Dims &D, const float *A, const float *B, float *C
     int64_t tiles, target = kSplitTarget;
     if (!f32 && M % 256 == 0 && N % 128 == 0 && (M / 256) * (N / 128) >= 32) {
         t = 256, tiles = (M / 256) * (N / 128), target = kSplitTarget256;
+        // dQ and dK go out as ONE grouped launch: half the block target each, so the launch holds ~240 blocks
+        // (C4: split 2, 228 blocks instead of split 4 and 456; 3.016-3.017 vs 3.054-3.065 ms per step in one
+        // session, profiles/r04/ab_sched.txt; split 1 and 128x128 tiles at split 2 were slower)
+        if (role == U2GNN_ROLE_DQ || role == U2GNN_ROLE_DK) target = kSplitTarget256 / 2;
     } else {
         t = (M % 128 == 0 && N % 128 == 0) ? 128 : 64;
         tiles = (M / t) * (N / t);
@@ -243,14 +247,6 @@ int gemm_split(Arena &W, const Dims &D, const float *A, const float *B, float *C
     int64_t split = target / (tiles > 0 ? tiles : 1);
     if (Kd / (4 * bk) < split) split = Kd / (4 * bk);
     if (split < 1) split = 1;
-#ifdef U2GNN_EXP_ATT_SPLIT   // experiment: split-K depth of the grouped dQ / dK products
-    if (role == U2GNN_ROLE_DQ || role == U2GNN_ROLE_DK) {
-#ifdef U2GNN_EXP_ATT_TILE128
-        t = 128, tiles = (M / 128) * (N / 128);
-#endif
-        split = U2GNN_EXP_ATT_SPLIT;
-    }
-#endif
     // slab cap of the weight gradients (engine.wgrad_split_cap): 8 for node-sized depths, 16 for
     // token-sized ones (neighbour mode, K = N(k+1) rows)
     const int64_t wgrad_split_max = Kd <= 8192 ? 8 : 16;
@@ -664,7 +660,7 @@ int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
         // experiment: the layer's held-back FFN / LayerNorm / out-projection parameter work goes out on the
         // side stream behind dV (beside dS, dQ, dK) instead of at the end of the layer (beside the next
         // layer's FFN backward); only the in-projection's gradients are left for the end
-        if (dv_side && need_dx) U2GNN_TRY(flush(df, W, so));
+        if (dv_side && need_dx) U2GNN_TRY(flush(df, W, so));   // measured neutral-to-worse (r04 A/B)
 #endif
         float *delta = ln_delta ? delta_ln : W.take<float>(Np);
         if (!plan && !ln_delta) U2GNN_TRY(u2gnn_rowdot(dO, dp, c.O, dp, delta, Np, dp, st));

@@ -253,7 +253,7 @@ def _rp(role: str, prec: str) -> str:
 
 
 def _gemm_split(A, B, C, M, N, Kd, lda, ldb, ldc, trans_a=False, trans_b=False, alpha=1.0, accumulate=False,
-                prec="fp32", rblk=None, cblk=None, target=448, flops=None, deep=False, clamp_a=False):
+                prec="fp32", rblk=None, cblk=None, target=448, flops=None, deep=False, clamp_a=False, target256=240):
     """C (+)= alpha * op(A) . op(B) with deterministic split-K: when the tile grid alone would
     leave most of the 256 CUs idle (skinny outputs with a deep node dimension: P.V, Pd^T.dO,
     dS.K, dS^T.Q, the weight gradients, dH.W1, dQKV.W_in), the depth is cut into fp32 slabs
@@ -272,7 +272,7 @@ def _gemm_split(A, B, C, M, N, Kd, lda, ldb, ldc, trans_a=False, trans_b=False, 
         return
     if prec != "fp32" and M % 256 == 0 and N % 128 == 0 and (M // 256) * (N // 128) >= 32:
         # 256x128 blocks (8 waves, one block per CU): the skinny attention products
-        t, tiles, target = 256, (M // 256) * (N // 128), 240
+        t, tiles, target = 256, (M // 256) * (N // 128), target256
     else:
         t = 128 if (M % 128 == 0 and N % 128 == 0) else 64
         tiles = (M // t) * (N // t)
@@ -306,10 +306,12 @@ def _bias_grad(dY, rows, cols_pad, ld, cblk, out):
 
 
 def _gemm_nodes_k(A, B, C, M, N, Kd, lda, ldb, ldc, trans_a=False, alpha=1.0, prec="fp32", flops=None,
-                  clamp_a=False):
-    """The skinny attention products whose depth is the node dimension (N = dp, K = Np)."""
+                  clamp_a=False, grouped=False):
+    """The skinny attention products whose depth is the node dimension (N = dp, K = Np).  grouped: dQ / dK,
+    which the native executor issues as one grouped launch -- half the 256x128 block target each
+    (encoder_layer.cpp gemm_split), so both paths cut the same split-K slabs."""
     _gemm_split(A, B, C, M, N, Kd, lda, ldb, ldc, trans_a=trans_a, alpha=alpha, prec=prec, flops=flops,
-                clamp_a=clamp_a)
+                clamp_a=clamp_a, target256=120 if grouped else 240)
 
 
 def ffn2_split(fuse: bool, Np: int, ffp: int) -> int:
@@ -492,8 +494,9 @@ def encoder_layer_backward(dX2: torch.Tensor, ctx: EncoderLayerCtx, w: PackedLay
     _gemm_nodes_k(ctx.Pd, dO, dQKV[:, 2 * dp:], Np, dp, Np, Np, dp, 3 * dp, trans_a=True, prec=_rp("dv", prec), flops=att,
                   clamp_a=pd > 0)
     _gemm_nodes_k(dS, Kt, dQKV[:, :dp], Np, dp, Np, Np, 3 * dp, 3 * dp, alpha=1.0 / math.sqrt(d), prec=_rp("dq", prec),
-                  flops=att)
-    _gemm_nodes_k(dS, Q, dQKV[:, dp:2 * dp], Np, dp, Np, Np, 3 * dp, 3 * dp, trans_a=True, prec=_rp("dk", prec), flops=att)
+                  flops=att, grouped=True)
+    _gemm_nodes_k(dS, Q, dQKV[:, dp:2 * dp], Np, dp, Np, Np, 3 * dp, 3 * dp, trans_a=True, prec=_rp("dk", prec), flops=att,
+                  grouped=True)
     del dS, dO
     # in-projection
     if need_dx:

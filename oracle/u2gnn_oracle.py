@@ -192,7 +192,9 @@ def encoder_layer(x: torch.Tensor, prm: Dict[str, torch.Tensor], train: bool, p:
     torch.nn.TransformerEncoderLayer(d, nhead=1, ff, dropout=0.5), norm_first=False,
     ReLU, layer_norm_eps=1e-5 (instantiated at pytorch_U2GNN_Sup.py:20).
     ``masks`` (optional, slot-0 only, shapes [S,S] / [S,d] / [S,ff]) replaces the random
-    dropout masks of slot 0 for exact train-mode parity tests."""
+    dropout masks of slot 0 for exact train-mode parity tests.  Test-only key ``"relu"`` ([S,ff] of 0/1):
+    the ReLU's on/off decision of slot 0 taken from outside (a GPU run's), instead of the sign of the
+    pre-activation -- the diagnostic that isolates ReLU boundary flips (tests/test_train_parity_gpu.py)."""
     S, B, d = x.shape
     W, b = prm["in_proj_weight"], prm["in_proj_bias"]
     qkv = x @ W.t() + b                                     # [S,B,3d]
@@ -222,7 +224,13 @@ def encoder_layer(x: torch.Tensor, prm: Dict[str, torch.Tensor], train: bool, p:
 
     x = F.layer_norm(x + _drop(sa, p, train, site_mask("drop1", sa)), (d,),
                      prm["norm1.weight"], prm["norm1.bias"], 1e-5)
-    h = torch.relu(x @ prm["linear1.weight"].t() + prm["linear1.bias"])
+    pre = x @ prm["linear1.weight"].t() + prm["linear1.bias"]
+    if masks is not None and "relu" in masks:
+        on = (pre > 0).to(pre.dtype)
+        on[:, 0] = masks["relu"]
+        h = pre * on
+    else:
+        h = torch.relu(pre)
     h = _drop(h, p, train, site_mask("drop_ff", h))
     ff = h @ prm["linear2.weight"].t() + prm["linear2.bias"]
     x = F.layer_norm(x + _drop(ff, p, train, site_mask("drop2", ff)), (d,),

@@ -68,8 +68,21 @@ def _case(name, golden_dir):
     return sd, (L, T, d, ff, C), z["b0_input_x"], z["b0_offsets"], z["b0_X"], z["b0_labels"], float(z["lr"])
 
 
-# Measured exceptions to TOL (case, precision) -> {quantity: bound}.  Empty = every quantity at 1e-3.
-TOL_TRAIN = {}
+# Measured exceptions to TOL (case, precision) -> {quantity: bound}; everything not listed is held at 1e-3.
+# C4 in bf16x3 (round 4, profiles/r04/train_parity_*.jsonl): scores 2.3e-6, loss 1.5e-7, clip norm 6.3e-6, every
+# gradient except linear1's <= 5.2e-4 -- but linear1.weight / .bias gradients 9e-5 .. 1.66e-2: a few of the
+# N x ff = 5 M pre-activations per layer lie within the 2^-16 product error of zero and switch the ReLU
+# (test_c4_bf16x3_train_deviation_is_the_relu_boundary: with the GPU's ReLU decisions in the oracle every
+# gradient is back under 1e-3).  Adam's first step moves every element by lr * g / |g|, so an element whose
+# gradient changes sign moves 2 lr = 1e-3 the other way: the post-Adam parameters measured 9.9e-4.  fp32 holds
+# 1e-3 everywhere (max 4.1e-6) and is the parity path; bench.py reports its C4 rate beside the headline.
+_L1 = {f"grad.u2gnn_layers.0.layers.{t}.linear1.{w}": 2.5e-2 for t in range(4) for w in ("weight", "bias")}
+_AFTER = {f"after.{n}": 1.5e-3 for n in
+          [f"u2gnn_layers.0.layers.{t}.{k}" for t in range(4) for k in
+           ("self_attn.in_proj_weight", "self_attn.in_proj_bias", "self_attn.out_proj.weight", "self_attn.out_proj.bias",
+            "linear1.weight", "linear1.bias", "linear2.weight", "linear2.bias", "norm1.weight", "norm1.bias",
+            "norm2.weight", "norm2.bias")] + ["predictions.0.weight", "predictions.0.bias"]}
+TOL_TRAIN = {("c4", "bf16x3"): dict(_L1, **_AFTER)}
 
 
 @pytest.mark.parametrize("precision", ["fp32", "bf16x3"])
@@ -123,3 +136,50 @@ def test_train_mode_step_matches_oracle_with_kernel_masks(golden_dir, name, prec
     bounds = TOL_TRAIN.get((name, precision), {})
     bad = {k: v for k, v in err.items() if v > bounds.get(k, TOL)}
     assert not bad, f"{name} {precision}: above tolerance: {bad}"
+
+
+def test_c4_bf16x3_train_deviation_is_the_relu_boundary(golden_dir):
+    """Where bf16x3 misses 1e-3 in train mode (C4: linear1 gradients, see TOL_TRAIN), the cause is the
+    ReLU's on/off decision of pre-activations within ~1e-5 of zero: split-bf16 products perturb them at the
+    2^-16 level and a flipped unit moves its row of dW1 by dH[n, j] X1[n, :].  Taking the ReLU decision of
+    the GPU run into the oracle (masks["relu"], from the saved dropped-ReLU image Hd: Hd > 0 is relu' * keep)
+    and comparing again must put EVERY quantity within 1e-3 -- the remaining difference is the continuous
+    2^-16 error of the products."""
+    import u2gnn_hip.native as native
+    from oracle import u2gnn_oracle as O
+    from pytorch_U2GNN_Sup import TransformerU2GNN
+    from u2gnn_hip import kernels as K
+    from u2gnn_hip.core import DeviceBatch
+    sd0, (L, T, d, ff, C), input_x, offsets, X, labels, lr = _case("c4", golden_dir)
+    m = TransformerU2GNN(d, ff, C, T, 0.5, L, precision="bf16x3")
+    m.load_state_dict(sd0)
+    m = m.to(DEV).train()
+    flat = m.flatten_parameters()
+    b = DeviceBatch.from_offsets(input_x, offsets, X, labels, device=DEV)
+    seed = 987654321
+    prev = native.set_enabled(False)   # the Python orchestration (bit-identical to the executor) exposes Hd
+    try:
+        scores, ctx = m.core.forward(b, train=True, need_ctx=True, seed=seed)
+        dsc = torch.empty_like(scores)
+        loss = torch.zeros(1, device=DEV)
+        K.smoothed_ce(scores, b.labels, b.B, C, 0.1, loss, dsc)
+        m.core.backward(ctx, dsc, flat.grads)
+        torch.cuda.synchronize()
+    finally:
+        native.set_enabled(prev)
+    grads_c = {n: flat.grads[n].detach().cpu().clone() for n in flat.names}
+    masks = _kernel_masks(seed, L, T, b.N, b.B, d, ff)
+    for t in range(T):
+        masks[(0, t)]["relu"] = (ctx["stack"]["layers"][0][t].Hd[:b.N, :ff].detach().cpu() > 0).float()
+    torch.set_num_threads(min(16, os.cpu_count()))
+    prm = {k: v.detach().clone().requires_grad_(True) for k, v in sd0.items()}
+    ref = O.sup_forward(prm, torch.from_numpy(np.asarray(input_x)), offsets, torch.from_numpy(np.asarray(X)), L, T,
+                        train=True, dropout=0.5, slots=1, masks=masks)
+    O.soft_cross_entropy(ref, O.label_smoothing(torch.from_numpy(np.asarray(labels)), C)).backward()
+    err = {n: rel_err(grads_c[n], prm[n].grad) for n in flat.names}
+    rep = os.environ.get("U2GNN_PARITY_REPORT")
+    if rep:
+        with open(rep, "a") as f:
+            f.write(json.dumps({"case": "c4_relu_injected", "precision": "bf16x3", "N": b.N, "errors": err}) + "\n")
+    bad = {k: v for k, v in err.items() if v > TOL}
+    assert not bad, f"with the GPU's ReLU decisions injected: {bad}"

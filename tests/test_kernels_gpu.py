@@ -856,3 +856,4 @@ def test_cx2_output_from_column(col0):
     torch.cuda.synchronize()
     assert torch.equal(sentinel[:, 2 * col0:], ref[:, 2 * col0:])
     assert bool((sentinel[:, :2 * col0] == 7.0).all())
+

@@ -146,14 +146,18 @@ class UnSupGradSync:
 
     * ``__call__(flat)``: all-reduce (sum, then 1/world) of the encoder region of the flat gradient;
       the ss.weight region is excluded (its rows come from ``rows``).
-    * ``rows(ids_lab, rows_lab, ids_smp, rows_smp, gW)``: all-gather every rank's compact rows
-      (label rows padded with id -1 to ``id_cap``; the S sample rows) and fold them into the dense
-      gW (all zero on entry) in rank order, labels before samples, scaled by 1/world -- the same
-      destinations in the same order on every rank, so every rank holds the same bits.  Returns the
-      gathered id tensors (the rows to zero after the optimizer step).
+    * ``buffers(n_lab, n_smp, D, device)``: the compact-row views the sampled-softmax backward writes into
+      directly (u2gnn_sampled_softmax_bwd_rows): each lives in ONE flat exchange buffer per kind that holds
+      the row ids (int64, as pairs of floats) followed by the rows, so a kind crosses the ranks in one
+      all-gather.
+    * ``rows(ids_lab, rows_lab, ids_smp, rows_smp, gW)``: all-gather every rank's compact rows (label rows
+      padded with id -1 to ``id_cap``; the S sample rows) and fold them into the dense gW (all zero on
+      entry) in rank order, labels before samples, scaled by 1/world -- the same destinations in the same
+      order on every rank, so every rank holds the same bits.  Returns the gathered id tensors (the rows
+      to zero after the optimizer step).  Rows not written in the ``buffers`` views are copied in.
 
-    Device tensors go through u2gnn_index_add_rows; CPU tensors (the gloo tests) through torch's
-    index_add_ with the padding rows dropped -- the same sums in the same order."""
+    Device tensors go through u2gnn_index_add_rows (id -1 rows skipped); CPU tensors (the gloo tests)
+    through torch's index_add_ with the padding rows dropped -- the same sums in the same order."""
 
     def __init__(self, flat, id_cap: int, group=None, weight_name: str = "ss.weight"):
         import torch.distributed as dist
@@ -174,6 +178,27 @@ class UnSupGradSync:
                 self.dist.all_reduce(g[a:b], group=self.group)
                 g[a:b].mul_(1.0 / self.world)
 
+    def _flat(self, kind: str, rows: int, D: int, device) -> torch.Tensor:
+        """[2 * rows + rows * D] float32: the ids (int64 bits) then the rows, one all-gather per kind."""
+        key = (kind, rows, D, str(device))
+        buf = self._bufs.get(key)
+        if buf is None:
+            n = 2 * rows + rows * D
+            n += n & 1   # even length: every rank's chunk of the gathered buffer starts 8-byte aligned (int64 ids)
+            buf = self._bufs[key] = torch.zeros(n, dtype=torch.float32, device=device)
+            buf[:2 * rows].view(torch.int64).fill_(-1)
+            if kind == "lab":
+                self._bufs[("neg", str(device))] = torch.full((rows,), -1, dtype=torch.int64, device=device)
+        return buf
+
+    def buffers(self, n_lab: int, n_smp: int, D: int, device):
+        if n_lab > self.id_cap:
+            raise ValueError(f"batch has {n_lab} label rows, above the exchange cap {self.id_cap}")
+        lab = self._flat("lab", self.id_cap, D, device)
+        smp = self._flat("smp", n_smp, D, device)
+        cap = self.id_cap
+        return (lab[2 * cap:2 * cap + cap * D].view(cap, D)[:n_lab], smp[2 * n_smp:2 * n_smp + n_smp * D].view(n_smp, D))
+
     def _gather(self, t: torch.Tensor) -> torch.Tensor:
         # concatenated along dim 0 (the layout both RCCL and gloo accept), viewed as [world, ...]
         out = torch.empty((self.world * t.shape[0],) + tuple(t.shape[1:]), device=t.device, dtype=t.dtype)
@@ -183,25 +208,29 @@ class UnSupGradSync:
     def rows(self, ids_lab: torch.Tensor, rows_lab: torch.Tensor, ids_smp: torch.Tensor, rows_smp: torch.Tensor,
              gW: torch.Tensor):
         n, D = rows_lab.shape
-        if n > self.id_cap:
-            raise ValueError(f"batch has {n} label rows, above the exchange cap {self.id_cap}")
-        key = (ids_lab.device, D)
-        buf = self._bufs.get(key)
-        if buf is None:
-            buf = self._bufs[key] = (torch.empty(self.id_cap, dtype=torch.int64, device=ids_lab.device),
-                                     torch.empty(self.id_cap, D, dtype=rows_lab.dtype, device=rows_lab.device))
-        ids_pad, rows_pad = buf
-        ids_pad.fill_(-1)
-        ids_pad[:n].copy_(ids_lab)
-        rows_pad[:n].copy_(rows_lab)
-        rows_pad[n:].zero_()
-        all_ids_lab, all_rows_lab = self._gather(ids_pad), self._gather(rows_pad)
-        all_ids_smp, all_rows_smp = self._gather(ids_smp.to(torch.int64)), self._gather(rows_smp)
+        S = rows_smp.shape[0]
+        cap = self.id_cap
+        rl, _ = self.buffers(n, S, D, rows_lab.device)
+        bsmp = self._flat("smp", S, D, rows_lab.device)
+        if rows_lab.data_ptr() != rl.data_ptr():
+            rl.copy_(rows_lab)
+        if rows_smp.data_ptr() != bsmp[2 * S:].data_ptr():
+            bsmp[2 * S:2 * S + S * D].view(S, D).copy_(rows_smp)
+        lab = self._flat("lab", cap, D, rows_lab.device)
+        neg = self._bufs[("neg", str(rows_lab.device))]
+        torch.cat([ids_lab.to(torch.int64), neg[:cap - n]], out=lab[:2 * cap].view(torch.int64))
+        bsmp[:2 * S].view(torch.int64).copy_(ids_smp)
+        g_lab, g_smp = self._gather(lab), self._gather(bsmp)
         alpha = 1.0 / self.world
+        ids_l, ids_s = [], []
         for r in range(self.world):
-            _index_add(gW, all_ids_lab[r], all_rows_lab[r], alpha)
-            _index_add(gW, all_ids_smp[r], all_rows_smp[r], alpha)
-        return (all_ids_lab.view(-1), all_ids_smp.view(-1))
+            il, rr = g_lab[r, :2 * cap].view(torch.int64), g_lab[r, 2 * cap:2 * cap + cap * D].view(cap, D)
+            is_, rs = g_smp[r, :2 * S].view(torch.int64), g_smp[r, 2 * S:2 * S + S * D].view(S, D)
+            _index_add(gW, il, rr, alpha)
+            _index_add(gW, is_, rs, alpha)
+            ids_l.append(il)
+            ids_s.append(is_)
+        return (torch.cat(ids_l), torch.cat(ids_s))
 
 
 def _index_add(dst: torch.Tensor, ids: torch.Tensor, rows: torch.Tensor, alpha: float) -> None:

@@ -102,8 +102,8 @@ class UnSupTrainer:
         gW = self.flat.grads["ss.weight"]
         dOV = torch.empty_like(OVd)
         if self.row_sync is not None:   # data parallel: compact rows, exchanged before they are added
-            rows_lab = torch.empty(N, D, device=OVd.device)
-            rows_smp = torch.empty(S, D, device=OVd.device)
+            # written straight into the exchange buffers (ids + rows of one kind cross the ranks together)
+            rows_lab, rows_smp = self.row_sync.buffers(N, S, D, OVd.device)
             K.sampled_softmax_bwd_rows(OVd, D, b.input_y, sample_ids, S, W, W.stride(0), prob, None, dOV, D,
                                        rows_lab, rows_smp, N, D)
             self._touched = self.row_sync.rows(b.input_y, rows_lab, sample_ids, rows_smp, gW)

@@ -577,68 +577,6 @@ __global__ void __launch_bounds__(256) attn_softmax_kernel(const float *S, int64
     }
 }
 
-// Softmax + dropout for the pre-split attention path (gemm_x2.hip): the same row statistics and
-// keep decisions as attn_softmax_kernel, Pd written once in x2 format (kept: P/(1-p), dropped: 0)
-// and the row (max, 1/sum) kept so the dS epilogue recomputes P bit-exactly from the saved scores.
-template <int SM_RV>
-__global__ void __launch_bounds__(256) attn_softmax_x2_kernel(const float *S, int64_t lds, __bf16 *Pd2,
-                                                              int64_t ldp2, float2 *rowstat, int64_t rows_valid,
-                                                              int64_t n_valid, int64_t n_pad, float p,
-                                                              uint64_t seed, const uint64_t *seed_epoch) {
-    seed = u2gnn_seed(seed, seed_epoch);
-    __shared__ float red[4];
-    const int64_t row = blockIdx.x;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (row >= rows_valid) {
-        for (int64_t c = tid * 4; c < n_pad; c += 1024) store_x2_4(Pd2, ldp2, (int)row, (int)c, z4);
-        if (tid == 0) rowstat[row] = make_float2(0.f, 0.f);
-        return;
-    }
-    const float *srow = S + row * lds;
-    float e[SM_RV][4];
-    float m = -INFINITY;
-#pragma unroll
-    for (int i = 0; i < SM_RV; ++i) {
-        const int64_t c = (int64_t)i * 1024 + tid * 4;
-        const float4 v = c < n_pad ? *reinterpret_cast<const float4 *>(srow + c) : z4;
-        const float x[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            e[i][j] = c + j < n_valid ? x[j] : -INFINITY;
-            m = fmaxf(m, e[i][j]);
-        }
-    }
-    const float M = block_max4(m, red, lane, w);
-    float s = 0.f;
-#pragma unroll
-    for (int i = 0; i < SM_RV; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            e[i][j] = expf(e[i][j] - M);   // exp(-inf) = 0 for masked / padded keys
-            s += e[i][j];
-        }
-    const float inv = 1.f / block_sum4(s, red, lane, w);
-    if (tid == 0) rowstat[row] = make_float2(M, inv);
-    const float ks = p > 0.f ? 1.f / (1.f - p) : 1.f;
-    const uint32_t rkey = u2gnn_row_key(seed, (uint32_t)row);
-#pragma unroll
-    for (int i = 0; i < SM_RV; ++i) {
-        const int64_t cb = (int64_t)i * 1024;
-        if (cb >= n_pad) break;   // block-uniform
-        const int64_t c = cb + tid * 4;
-        if (c >= n_pad) continue;
-        float pdv[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const float pv = e[i][j] * inv;
-            const bool kp = u2gnn_keep_rk(rkey, (uint32_t)(c + j), u2gnn_keep_thr(p));
-            pdv[j] = kp ? pv * ks : 0.f;
-        }
-        store_x2_4(Pd2, ldp2, (int)row, (int)c, make_float4(pdv[0], pdv[1], pdv[2], pdv[3]));
-    }
-}
-
 // fp32 -> x2 over rows x cols (cols % 4 == 0): one thread per 4 columns
 __global__ void __launch_bounds__(256) split_x2_kernel(const float *src, int64_t ld_src, __bf16 *dst, int64_t ld_dst,
                                                        int64_t rows, int64_t cols) {
@@ -1334,29 +1272,6 @@ int u2gnn_attn_softmax_fwd(const float *S, int64_t lds, float *P, float *Pd, int
     else
         hipLaunchKernelGGL(attn_softmax_kernel<32>, dim3((unsigned)rows_pad), dim3(256), 0, st, S, lds, P, Pd, ldp,
                            rows_valid, n_valid, n_pad, p, seed, u2gnn_g_epoch, keep, ld_keep);
-    return u2gnn_launch_status();
-}
-
-int u2gnn_attn_softmax_x2_fwd(const float *S, int64_t lds, void *Pd2, int64_t ldp2, float *rowstat,
-                              int64_t rows_valid, int64_t rows_pad, int64_t n_valid, int64_t n_pad, float p,
-                              uint64_t seed, void *stream) {
-    if (!S || !Pd2 || !rowstat || (n_pad & 7) || (lds & 3) || (ldp2 & 15) || n_valid > n_pad || n_valid < 1 ||
-        !(p < 1.f))
-        return U2GNN_E_ARG;
-    if (!al16(S) || !al16(Pd2) || ((uintptr_t)rowstat & 7)) return U2GNN_E_ALIGN;
-    if (n_pad > 1024 * SM_RV_MAX) return U2GNN_E_SHAPE;
-    hipStream_t st = u2gnn_stream(stream);
-    __bf16 *d = static_cast<__bf16 *>(Pd2);
-    float2 *rs = reinterpret_cast<float2 *>(rowstat);
-    if (n_pad <= 8192)
-        hipLaunchKernelGGL(attn_softmax_x2_kernel<8>, dim3((unsigned)rows_pad), dim3(256), 0, st, S, lds, d, ldp2, rs,
-                           rows_valid, n_valid, n_pad, p, seed, u2gnn_g_epoch);
-    else if (n_pad <= 16384)
-        hipLaunchKernelGGL(attn_softmax_x2_kernel<16>, dim3((unsigned)rows_pad), dim3(256), 0, st, S, lds, d, ldp2, rs,
-                           rows_valid, n_valid, n_pad, p, seed, u2gnn_g_epoch);
-    else
-        hipLaunchKernelGGL(attn_softmax_x2_kernel<32>, dim3((unsigned)rows_pad), dim3(256), 0, st, S, lds, d, ldp2, rs,
-                           rows_valid, n_valid, n_pad, p, seed, u2gnn_g_epoch);
     return u2gnn_launch_status();
 }
 

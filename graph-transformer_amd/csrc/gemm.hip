@@ -583,33 +583,27 @@ namespace {
 struct GemmPlan {
     GemmP P;
     int tile, split, prec, epi;
-    bool ta, tb, clamp, x2;
+    bool ta, tb, clamp;
 };
 
 int gemm_plan(const u2gnn_gemm_args *a, GemmPlan &G) {
     if (!a) return U2GNN_E_ARG;
-    const bool x2 = a->a_x2 || a->b_x2;
     // pre-split (x2) operands were the round-1/2 GEMM experiments (gemm_x2.hip / gemm_x3.hip, DESIGN.md 5.1,
-    // 5.3), measured slower than this kernel and removed in round 4; the x2 OUTPUT (Cx2) stays on the path
-    if (x2) return U2GNN_E_ARG;
-    if (x2 ? (!a->A2 || !a->B2) : (!a->A || !a->B)) return U2GNN_E_ARG;
+    // 5.3), measured slower than this kernel and removed in round 4 together with the recomputed-P dS epilogue
+    // that served them (ABI v13); the x2 OUTPUT (Cx2) stays on the path
+    if (a->a_x2 || a->b_x2 || a->epilogue == U2GNN_EPI_ATTN_DS_RECOMP) return U2GNN_E_ARG;
+    if (!a->A || !a->B) return U2GNN_E_ARG;
     if (!a->C && !a->Cx2) return U2GNN_E_ARG;
     if (a->M <= 0 || a->N <= 0 || a->K <= 0) return U2GNN_E_ARG;
     if (a->epilogue < 0 || a->epilogue > U2GNN_EPI_STORE_ROWSTAT) return U2GNN_E_ARG;
-    if (a->epilogue == U2GNN_EPI_ATTN_DS_RECOMP && !x2) return U2GNN_E_ARG;
     const int prec = a->precision;
     if (prec != U2GNN_PREC_F32 && prec != U2GNN_PREC_BF16X3 && prec != U2GNN_PREC_BF16) return U2GNN_E_ARG;
     const int split = a->split_k < 1 ? 1 : a->split_k;
     if (split > 1 && (a->epilogue != U2GNN_EPI_STORE || a->Cx2 || !a->C)) return U2GNN_E_ARG;
-    if (!x2) {
-        if (!al16(a->A) || !al16(a->B) || (a->lda & 3) || (a->ldb & 3)) return U2GNN_E_ALIGN;
-    }
-    const int bk = (prec == U2GNN_PREC_F32 || a->tile == 129 ||
-                    (x2 && (a->tile == 257 || a->tile == 128 || a->tile == 258 || a->tile == 260 || a->tile == 262 ||
-                           a->tile == 263)))
-                       ? 16 : 32;   // K step of the kernel
+    if (!al16(a->A) || !al16(a->B) || (a->lda & 3) || (a->ldb & 3)) return U2GNN_E_ALIGN;
+    const int bk = (prec == U2GNN_PREC_F32 || a->tile == 129) ? 16 : 32;   // K step of the kernel
     if (a->K % bk) return U2GNN_E_SHAPE;
-    if (prec != U2GNN_PREC_F32 && !x2) {   // bf16 staging addresses operands by 32-bit buffer offsets
+    if (prec != U2GNN_PREC_F32) {   // bf16 staging addresses operands by 32-bit buffer offsets
         const int64_t span = ((int64_t)a->K + 256) * (a->lda > a->ldb ? a->lda : a->ldb) * 4;
         if (span >= (int64_t)INT32_MAX) return U2GNN_E_SHAPE;
     }
@@ -625,7 +619,7 @@ int gemm_plan(const u2gnn_gemm_args *a, GemmPlan &G) {
          e == U2GNN_EPI_BIAS_DROP_RESID_LN) && !a->bias)
         return U2GNN_E_ARG;
     if (e == U2GNN_EPI_BIAS_DROP_RESID_LN) {   // row-complete 64-column tiles only (the d <= 64 encoders)
-        if (x2 || prec == U2GNN_PREC_F32 || split != 1 || a->N != 64 || (a->tile != 0 && a->tile != 64) ||
+        if (prec == U2GNN_PREC_F32 || split != 1 || a->N != 64 || (a->tile != 0 && a->tile != 64) ||
             a->trans_a || !a->trans_b || !a->aux0 || !a->ln_gamma || !a->ln_beta || !a->ln_y || !a->ln_mean ||
             !a->ln_rstd || a->ln_d < 1 || a->ln_d > 64 || a->ln_rows < 0)
             return U2GNN_E_ARG;
@@ -633,18 +627,15 @@ int gemm_plan(const u2gnn_gemm_args *a, GemmPlan &G) {
     }
     if ((e == U2GNN_EPI_BIAS_DROP_RESID || e == U2GNN_EPI_BIAS_DROP_RESID_LN || e == U2GNN_EPI_RELU_DROP_BWD ||
          e == U2GNN_EPI_STORE_ROWDOT || e == U2GNN_EPI_ATTN_DS ||
-         e == U2GNN_EPI_ATTN_DS_SIGNED || e == U2GNN_EPI_ATTN_DS_RECOMP) && !a->aux0)
+         e == U2GNN_EPI_ATTN_DS_SIGNED) && !a->aux0)
         return U2GNN_E_ARG;
     if (e == U2GNN_EPI_ATTN_DS_SIGNED && (!a->rowvec || !(a->p_drop < 1.f))) return U2GNN_E_ARG;
-    if (a->rowvec_parts > 1 && (e != U2GNN_EPI_ATTN_DS_SIGNED || x2 || a->ld_rowvec < a->M)) return U2GNN_E_ARG;
+    if (a->rowvec_parts > 1 && (e != U2GNN_EPI_ATTN_DS_SIGNED || a->ld_rowvec < a->M)) return U2GNN_E_ARG;
     if (e == U2GNN_EPI_STORE_ROWDOT &&
-        (x2 || split != 1 || a->Cx2 || !a->aux0 || !a->rowpart || a->ld_rowpart < a->M || (a->N & 63)))
-        return U2GNN_E_ARG;
-    if (e == U2GNN_EPI_ATTN_DS_RECOMP && (!a->rowvec || !a->rowstat || !(a->p_drop < 1.f) ||
-                                          ((uintptr_t)a->rowstat & 7)))
+        (split != 1 || a->Cx2 || !a->aux0 || !a->rowpart || a->ld_rowpart < a->M || (a->N & 63)))
         return U2GNN_E_ARG;
     if (e == U2GNN_EPI_STORE_ROWSTAT) {
-        if (x2 || prec == U2GNN_PREC_F32 || split != 1 || a->Cx2 || !a->C || !a->rowpart || a->trans_a ||
+        if (prec == U2GNN_PREC_F32 || split != 1 || a->Cx2 || !a->C || !a->rowpart || a->trans_a ||
             !a->trans_b || a->n_valid < 1 || a->n_valid > a->N || a->ld_rowpart < a->N / 32)
             return U2GNN_E_ARG;
         if ((uintptr_t)a->rowpart & 7) return U2GNN_E_ALIGN;
@@ -653,10 +644,7 @@ int gemm_plan(const u2gnn_gemm_args *a, GemmPlan &G) {
     if (e == U2GNN_EPI_ATTN_DS && ((!a->aux1 && !a->keep) || !a->rowvec)) return U2GNN_E_ARG;
     if (e == U2GNN_EPI_ATTN_DS && a->keep && (a->ld_keep * 32 < a->N || !(a->p_drop < 1.f))) return U2GNN_E_ARG;
     int tile = a->tile;
-    if (x2 && tile == 0) tile = 256;
-    if (x2 && tile != 64 && tile != 128 && tile != 256 && tile != 129) {
-        // x2-only tile codes (gemm_x2.hip X2Cfg); shapes are checked by the x2 dispatcher
-    } else if (tile == 0) {
+    if (tile == 0) {
         const bool can128 = (a->M % 128 == 0) && (a->N % 128 == 0);
         const int64_t blocks128 = can128 ? (a->M / 128) * (a->N / 128) * split : 0;
         tile = (can128 && blocks128 >= 480) ? 128 : 64;
@@ -671,11 +659,10 @@ int gemm_plan(const u2gnn_gemm_args *a, GemmPlan &G) {
             tile = 256;
     }
     // tile codes: 64, 128 (square), 256 (256x128, 8 waves), 129 (128x128 with a 16-deep K step)
-    const bool x2code = x2 && (tile == 257 || tile == 130 || (tile >= 258 && tile <= 263) || tile == 300 || tile == 301);
-    if (!x2code && tile != 64 && tile != 128 && tile != 256 && tile != 129) return U2GNN_E_ARG;
+    if (tile != 64 && tile != 128 && tile != 256 && tile != 129) return U2GNN_E_ARG;
     if ((tile == 256 || tile == 129) && prec == U2GNN_PREC_F32) return U2GNN_E_ARG;
-    const int tm_ = tile == 129 ? 128 : (tile > 256 ? 256 : (tile == 130 ? 128 : tile));
-    const int tile_n = (tile == 260 || tile == 262 || tile == 300) ? 256 : (tm_ == 256 ? 128 : tm_);
+    const int tm_ = tile == 129 ? 128 : tile;
+    const int tile_n = tm_ == 256 ? 128 : tm_;
     if (a->M % tm_ || a->N % tile_n) return U2GNN_E_SHAPE;
     GemmP P;
     std::memset(&P, 0, sizeof(P));
@@ -707,13 +694,9 @@ int gemm_plan(const u2gnn_gemm_args *a, GemmPlan &G) {
     P.epoch = u2gnn_g_epoch;
     P.keep = e == U2GNN_EPI_ATTN_DS ? a->keep : nullptr;
     P.ld_keep = a->ld_keep;
-    P.A2 = static_cast<const __bf16 *>(a->A2);
-    P.B2 = static_cast<const __bf16 *>(a->B2);
     P.Cx2 = static_cast<__bf16 *>(a->Cx2);
     P.ldcx2 = a->ldcx2;
     P.cx2_col0 = a->cx2_col0;
-    P.rowstat = reinterpret_cast<const float2 *>(a->rowstat);
-    P.m_valid = (int32_t)a->m_valid;
     P.n_valid = (int32_t)a->n_valid;
     P.rowpart = a->rowpart;
     P.ld_rowpart = a->ld_rowpart;
@@ -732,7 +715,7 @@ int gemm_plan(const u2gnn_gemm_args *a, GemmPlan &G) {
     }
     G.P = P;
     G.tile = tile, G.split = split, G.prec = prec, G.epi = e;
-    G.ta = a->trans_a != 0, G.tb = a->trans_b != 0, G.clamp = a->clamp_a != 0, G.x2 = x2;
+    G.ta = a->trans_a != 0, G.tb = a->trans_b != 0, G.clamp = a->clamp_a != 0;
     return U2GNN_OK;
 }
 
@@ -777,7 +760,7 @@ extern "C" int u2gnn_gemm_group(const u2gnn_gemm_args *args, int32_t n, void *st
     // one launch when every job runs the same grouped kernel
     bool same = n > 1;
     for (int32_t i = 0; i < n && same; ++i)
-        same = !G[i].x2 && G[i].prec == G[0].prec && G[i].prec != U2GNN_PREC_F32 && G[i].tile == G[0].tile &&
+        same = G[i].prec == G[0].prec && G[i].prec != U2GNN_PREC_F32 && G[i].tile == G[0].tile &&
                (G[i].tile == 64 || G[i].tile == 129 || G[i].tile == 256) && !G[i].tb && G[i].epi == U2GNN_EPI_STORE &&
                (G[i].ta || !G[i].clamp);
     if (!same) {

@@ -24,14 +24,11 @@ struct GemmP {
     uint64_t seed;
     const uint32_t *keep;
     int64_t ld_keep;
-    // pre-split operands / outputs (gemm_x2.hip; U2GNN x2 format, see u2gnn_hip.h)
-    const __bf16 *A2;
-    const __bf16 *B2;
+    // x2 output (U2GNN x2 format: per 8 columns hi then lo bf16, see u2gnn_hip.h)
     __bf16 *Cx2;          // non-null: the epilogue also writes C in x2 format
     int64_t ldcx2;        // bf16 elements
     int32_t cx2_col0;     // Cx2 receives columns >= cx2_col0 only
-    const float2 *rowstat;   // ATTN_DS_RECOMP: (row max, 1/row sum) of the forward softmax
-    int32_t m_valid, n_valid;   // ATTN_DS_RECOMP: real rows / keys (P = 0 beyond)
+    int32_t n_valid;   // STORE_ROWSTAT: real keys (columns >= n_valid are masked)
     const uint64_t *epoch;      // seed epoch at launch (u2gnn_set_seed_epoch): seed ^= *epoch * golden
     // EPI_BIAS_DROP_RESID_LN: the post-LayerNorm of the row-complete 64-column result
     const float *ln_gamma, *ln_beta;
@@ -70,7 +67,7 @@ __device__ __forceinline__ float4 ld4(const float *p) { return *reinterpret_cast
 // 4 columns.
 template <int EPI>
 __device__ __forceinline__ void epi_fetch(const GemmP &P, int row, int col, float4 &a, float4 &b, uint32_t &kb) {
-    if constexpr (ds_signed<EPI> || EPI == U2GNN_EPI_ATTN_DS_RECOMP) {
+    if constexpr (ds_signed<EPI>) {
         a = ld4(P.aux0 + (int64_t)row * P.ld_aux + col);
     } else if constexpr (EPI == U2GNN_EPI_ATTN_DS) {
         const int64_t o = (int64_t)row * P.ld_aux + col;
@@ -191,7 +188,6 @@ struct EpiSlice {
     uint32_t kb[TN][4];
     float dl;
     DeltaParts dp;    // EPI_DS_SIGNED_PARTS: dl = delta_sum(dp) when the slice is stored
-    float rm, rinv;   // ATTN_DS_RECOMP: forward softmax row max and 1/sum
 };
 
 template <int EPI, int TN>
@@ -204,34 +200,8 @@ __device__ __forceinline__ void fetch_slice(const GemmP &P, int row, int c0, int
             e.kb[j][g] = 0;
             epi_fetch<EPI>(P, row, c0 + j * 32 + 8 * g + 4 * kh, e.a[j][g], e.b[j][g], e.kb[j][g]);
         }
-    e.dl = (EPI == U2GNN_EPI_ATTN_DS || EPI == U2GNN_EPI_ATTN_DS_SIGNED || EPI == U2GNN_EPI_ATTN_DS_RECOMP)
-               ? P.rowvec[row] : 0.f;
+    e.dl = (EPI == U2GNN_EPI_ATTN_DS || EPI == U2GNN_EPI_ATTN_DS_SIGNED) ? P.rowvec[row] : 0.f;
     if constexpr (EPI == EPI_DS_SIGNED_PARTS) delta_load(P, row, e.dp);
-    if constexpr (EPI == U2GNN_EPI_ATTN_DS_RECOMP) {
-        const float2 st = P.rowstat[row];
-        e.rm = st.x, e.rinv = st.y;
-    } else {
-        e.rm = e.rinv = 0.f;
-    }
-}
-
-// Attention dS with the probabilities recomputed from the saved scores (ATTN_DS_RECOMP):
-// P = exp(s - rowmax) * (1/rowsum), bit-identical to the forward softmax's P; keep regenerated from
-// the dropout hash; dS = P * (keep * dPd/(1-p) - delta).  Padded rows / keys give 0.
-__device__ __forceinline__ float4 ds_recomp4(const GemmP &P, int row, int col, float4 v, float4 s, float dl, float rm,
-                                             float rinv, uint32_t rkey) {
-    const float x[4] = {s.x, s.y, s.z, s.w}, g[4] = {v.x, v.y, v.z, v.w};
-    const float sc = P.p > 0.f ? 1.f / (1.f - P.p) : 1.f;
-    const bool rv = row < P.m_valid;
-    float o[4];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        const uint32_t cc = (uint32_t)(col + c);
-        const float pr = (rv && (int)cc < P.n_valid) ? expf(x[c] - rm) * rinv : 0.f;
-        const bool kp = u2gnn_keep_rk(rkey, cc, u2gnn_keep_thr(P.p));
-        o[c] = pr * ((kp ? g[c] * sc : 0.f) - dl);
-    }
-    return make_float4(o[0], o[1], o[2], o[3]);
 }
 
 // One slice's stores.  STORE_ROWDOT: returns this lane's share of sum_n C[row,n] * aux0[row,n] over
@@ -239,8 +209,6 @@ __device__ __forceinline__ float4 ds_recomp4(const GemmP &P, int row, int col, f
 template <int EPI, int TM, int TN>
 __device__ __forceinline__ float store_slice(const GemmP &P, float *C, const f32x16 (&acc)[TM][TN], int i, int row,
                                              int c0, int kh, const EpiSlice<EPI, TN> &e) {
-    uint32_t rkey = 0;
-    if constexpr (EPI == U2GNN_EPI_ATTN_DS_RECOMP) rkey = u2gnn_row_key(P.seed, (uint32_t)row);
     float dl = e.dl;
     if constexpr (EPI == EPI_DS_SIGNED_PARTS) dl = delta_sum(P, row, e.dp);
     float rs = 0.f;
@@ -251,11 +219,7 @@ __device__ __forceinline__ float store_slice(const GemmP &P, float *C, const f32
             const int col = c0 + j * 32 + 8 * g + 4 * kh;
             const float4 v = make_float4(acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2],
                                          acc[i][j][4 * g + 3]);
-            float4 o;
-            if constexpr (EPI == U2GNN_EPI_ATTN_DS_RECOMP)
-                o = ds_recomp4(P, row, col, v, e.a[j][g], e.dl, e.rm, e.rinv, rkey);
-            else
-                o = epilogue4<EPI>(P, row, col, v, e.a[j][g], e.b[j][g], e.kb[j][g], dl);
+            const float4 o = epilogue4<EPI>(P, row, col, v, e.a[j][g], e.b[j][g], e.kb[j][g], dl);
             if (P.C) *reinterpret_cast<float4 *>(C + (int64_t)row * P.ldc + col) = o;
             if (P.Cx2 && col >= P.cx2_col0) store_x2_4(P.Cx2, P.ldcx2, row, col, o);
             if constexpr (EPI == U2GNN_EPI_STORE_ROWDOT) {
@@ -300,7 +264,6 @@ __device__ __forceinline__ void slice_from_pre(const PreDS<TN> &pre, int kh, Epi
         }
     e.dl = pre.dl;
     e.dp = pre.dp;
-    e.rm = e.rinv = 0.f;
 }
 
 // EPI_BIAS_DROP_RESID_LN on 64 x 64 blocks of 2 x 2 waves that cover whole 64-column rows: the

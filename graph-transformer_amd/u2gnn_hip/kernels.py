@@ -49,10 +49,10 @@ class LaunchRecorder:
 
 REC = LaunchRecorder()
 _EPI_NAMES = ["STORE", "BIAS", "BIAS_DROP_RESID", "BIAS_RELU_DROP", "RELU_DROP_BWD", "ACCUM", "ATTN_DS",
-              "ATTN_DS_SIGNED", "ATTN_DS_RECOMP"]
+              "ATTN_DS_SIGNED"]
 
 
-def gemm_symbol(precision, M, N, split_k, tile, trans_a, trans_b, epilogue, clamp_a=False, x2=False):
+def gemm_symbol(precision, M, N, split_k, tile, trans_a, trans_b, epilogue, clamp_a=False):
     """Mirror of the C dispatcher's kernel choice (gemm.hip u2gnn_gemm) -> template symbol."""
     b = lambda x: "true" if x else "false"  # noqa: E731
     if tile == 0:
@@ -69,16 +69,14 @@ def gemm_symbol(precision, M, N, split_k, tile, trans_a, trans_b, epilogue, clam
 
 def gemm(A, B, C, M, N, K, lda, ldb, ldc, trans_a=False, trans_b=False, epilogue=_lib.EPI_STORE, split_k=1,
          slab_stride=0, bias=None, aux0=None, aux1=None, rowvec=None, ld_aux=0, alpha=1.0, scale_cols=0, p_drop=0.0,
-         seed=0, precision="fp32", tile=0, flops=None, keep=None, clamp_a=False, Cx2=None, ldcx2=0, rowstat=None,
-         cx2_col0=0,
-         m_valid=0, n_valid=0, ln=None, rowpart=None):
+         seed=0, precision="fp32", tile=0, flops=None, keep=None, clamp_a=False, Cx2=None, ldcx2=0, cx2_col0=0,
+         n_valid=0, ln=None, rowpart=None):
     """C[M,N] (epilogue) sum_k A(m,k) B(k,n).  A/B/C may be views (pointer arithmetic via
     storage offsets is done by torch's data_ptr()).  ``flops``: algorithmic FLOPs of the
     launch for the roofline recorder (None = not recorded).  ``clamp_a``: A elements below +0 are read
     as 0 (the signed probability image of attn_softmax_fwd(P=None) consumed as Pd).
-    x2 operands (include/u2gnn_hip.h): A and B given as bfloat16 tensors are pre-split [rows][2*cols]
-    matrices (lda / ldb in bf16 elements); ``Cx2`` (bfloat16) receives the result in x2 format, C may
-    then be None.  ``rowstat``/``m_valid``/``n_valid``: the ATTN_DS_RECOMP epilogue.  ``ln`` =
+    ``Cx2`` (bfloat16) receives the result in x2 format (include/u2gnn_hip.h; columns >= ``cx2_col0``), C may
+    then be None.  ``n_valid``: the STORE_ROWSTAT epilogue's real keys.  ``ln`` =
     (gamma, beta, Y, ldy, mean, rstd, d, rows, eps): the EPI_BIAS_DROP_RESID_LN LayerNorm (N == 64).
     ``rowpart`` [N/64, >= M]: the EPI_STORE_ROWDOT row partials (ABI v8).  A 2-D ``rowvec`` [P, >= M]
     gives ATTN_DS_SIGNED the sum of its P partials per row (in row order of ``rowvec``)."""
@@ -87,15 +85,13 @@ def gemm(A, B, C, M, N, K, lda, ldb, ldc, trans_a=False, trans_b=False, epilogue
         ev0 = torch.cuda.Event(enable_timing=True)
         ev1 = torch.cuda.Event(enable_timing=True)
         ev0.record()
-    a, x2 = _gemm_args(A, B, C, M, N, K, lda, ldb, ldc, trans_a, trans_b, epilogue, split_k, slab_stride, bias, aux0,
-                       aux1, rowvec, ld_aux, alpha, scale_cols, p_drop, seed, precision, tile, keep, clamp_a, Cx2, ldcx2,
-                       rowstat, m_valid, n_valid, ln, rowpart, cx2_col0=cx2_col0)
-    if x2:   # pre-split operands: the removed round-1/2 experiments (gemm.hip rejects them)
-        raise _lib.U2GNNNativeError("u2gnn_gemm: pre-split (x2) operands are not supported")
+    a = _gemm_args(A, B, C, M, N, K, lda, ldb, ldc, trans_a, trans_b, epilogue, split_k, slab_stride, bias, aux0,
+                   aux1, rowvec, ld_aux, alpha, scale_cols, p_drop, seed, precision, tile, keep, clamp_a, Cx2, ldcx2,
+                   cx2_col0, n_valid, ln, rowpart)
     check(hip_lib().u2gnn_gemm(ctypes.byref(a), _s()), "u2gnn_gemm")
     if rec:
         ev1.record()
-        REC.records.append((gemm_symbol(precision, M, N, split_k, tile, trans_a, trans_b, epilogue, clamp_a, x2),
+        REC.records.append((gemm_symbol(precision, M, N, split_k, tile, trans_a, trans_b, epilogue, clamp_a),
                             float(flops), ev0, ev1))
 
 
@@ -106,32 +102,24 @@ def gemm_group(calls):
     for i, kw in enumerate(calls):
         kw = dict(kw)
         kw.pop("flops", None)
-        arr[i], x2 = _gemm_args(**kw)
-        if x2:
-            raise _lib.U2GNNNativeError("gemm_group: pre-split operands are not supported")
+        arr[i] = _gemm_args(**kw)
     check(hip_lib().u2gnn_gemm_group(arr, len(calls), _s()), "u2gnn_gemm_group")
 
 
 def _gemm_args(A, B, C, M, N, K, lda, ldb, ldc, trans_a=False, trans_b=False, epilogue=_lib.EPI_STORE, split_k=1,
                slab_stride=0, bias=None, aux0=None, aux1=None, rowvec=None, ld_aux=0, alpha=1.0, scale_cols=0,
                p_drop=0.0, seed=0, precision="fp32", tile=0, keep=None, clamp_a=False, Cx2=None, ldcx2=0,
-               rowstat=None, m_valid=0, n_valid=0, ln=None, rowpart=None, cx2_col0=0):
-    _dev(A, B, C, Cx2, rowstat)
-    x2 = A.dtype == torch.bfloat16
-    if x2 != (B.dtype == torch.bfloat16):
-        raise _lib.U2GNNNativeError("x2 GEMM: both operands must be pre-split (bfloat16) or neither")
+               cx2_col0=0, n_valid=0, ln=None, rowpart=None):
+    _dev(A, B, C, Cx2)
+    if A.dtype != torch.float32 or B.dtype != torch.float32:
+        # pre-split (x2) operands were the removed round-1/2 experiments (gemm.hip rejects them)
+        raise _lib.U2GNNNativeError("u2gnn_gemm: A and B must be float32 (pre-split operands are not supported)")
     a = _lib.GemmArgs()
-    if x2:
-        a.a_x2 = a.b_x2 = 1
-        a.A2, a.B2 = A.data_ptr(), B.data_ptr()
-    else:
-        a.A, a.B = A.data_ptr(), B.data_ptr()
+    a.A, a.B = A.data_ptr(), B.data_ptr()
     a.C = C.data_ptr() if C is not None else None
     if Cx2 is not None:
         a.Cx2, a.ldcx2, a.cx2_col0 = Cx2.data_ptr(), int(ldcx2), int(cx2_col0)
-    if rowstat is not None:
-        a.rowstat = rowstat.data_ptr()
-    a.m_valid, a.n_valid = int(m_valid), int(n_valid)
+    a.n_valid = int(n_valid)
     a.M, a.N, a.K = int(M), int(N), int(K)
     a.lda, a.ldb, a.ldc = int(lda), int(ldb), int(ldc)
     a.trans_a, a.trans_b = int(bool(trans_a)), int(bool(trans_b))
@@ -164,7 +152,7 @@ def _gemm_args(A, B, C, M, N, K, lda, ldb, ldc, trans_a=False, trans_b=False, ep
         a.ln_gamma, a.ln_beta, a.ln_y, a.ln_ldy = gam.data_ptr(), bet.data_ptr(), Y.data_ptr(), int(ldy)
         a.ln_mean, a.ln_rstd = mean.data_ptr(), rstd.data_ptr()
         a.ln_d, a.ln_rows, a.ln_eps = int(d_real), int(rows), float(eps)
-    return a, x2
+    return a
 
 
 def gather_rows(src, idx, idx_stride, dst, n_rows, n_rows_pad, d, d_pad, err=None):
@@ -233,15 +221,6 @@ def attn_softmax_fwd(S, lds, P, Pd, ldp, rows_valid, rows_pad, n_valid, n_pad, p
                                            int(n_valid), int(n_pad), float(p), int(seed), _p(keep),
                                            int(keep.stride(0)) if keep is not None else 0, _s()),
           "u2gnn_attn_softmax_fwd")
-
-
-def attn_softmax_x2_fwd(S, lds, Pd2, ldp2, rowstat, rows_valid, rows_pad, n_valid, n_pad, p, seed):
-    """Softmax + dropout writing Pd in x2 format (bfloat16 [rows_pad, >= 2*n_pad]) and rowstat
-    [rows_pad, 2] = (row max, 1/row sum) for the ATTN_DS_RECOMP epilogue."""
-    _dev(S, Pd2, rowstat)
-    check(hip_lib().u2gnn_attn_softmax_x2_fwd(_p(S), int(lds), _p(Pd2), int(ldp2), _p(rowstat), int(rows_valid),
-                                              int(rows_pad), int(n_valid), int(n_pad), float(p), int(seed), _s()),
-          "u2gnn_attn_softmax_x2_fwd")
 
 
 def split_x2(src, ld_src, dst2, ld_dst2, rows, cols):

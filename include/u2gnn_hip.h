@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define U2GNN_ABI_VERSION 12
+#define U2GNN_ABI_VERSION 13
 
 #define U2GNN_OK 0
 #define U2GNN_E_ARG (-1)    /* bad size / null pointer */
@@ -49,10 +49,8 @@ extern "C" {
 #define U2GNN_EPI_ATTN_DS_SIGNED 7  /* aux0 = x, the signed probability image of
                                        u2gnn_attn_softmax_fwd (P == NULL): C = x*(acc - (1-p)*rowvec[m])
                                        where x >= +0 (kept), C = x*rowvec[m] where x <= -0 (dropped) */
-#define U2GNN_EPI_ATTN_DS_RECOMP 8  /* aux0 = S (the saved scores), rowstat[m] = (row max, 1/row sum) of
-                                       u2gnn_attn_softmax_x2_fwd: P = exp(S - max) * (1/sum) (0 for
-                                       m >= m_valid or n >= n_valid), keep = dropout hash (seed, m, n);
-                                       C = P * (keep * acc/(1-p) - rowvec[m]) */
+#define U2GNN_EPI_ATTN_DS_RECOMP 8  /* retired in ABI v13 (it served the removed pre-split GEMM path):
+                                       u2gnn_gemm returns U2GNN_E_ARG for it */
 #define U2GNN_EPI_BIAS_DROP_RESID_LN 9 /* ABI v7: C = Z = aux0 + drop(acc + bias) as BIAS_DROP_RESID, and ln_y = the
                                           post-LayerNorm of Z's first ln_d columns (ln_gamma, ln_beta, ln_eps;
                                           ln_mean / ln_rstd per row; rows >= ln_rows and columns >= ln_d
@@ -117,15 +115,15 @@ typedef struct u2gnn_gemm_args {
     int32_t cx2_col0;     /* ABI v12: Cx2 receives only output columns >= cx2_col0 (a multiple of 8; 0 = all):
                              the in-projection writes the x2 copy of its V block only */
     /* ---- ABI v3: pre-split (x2) operands and outputs ---- */
-    int32_t a_x2, b_x2;   /* 1: A (B) is an x2 bf16 matrix (A2 / B2, lda / ldb in bf16 elements);
-                             both or neither; requires BF16X3 and tile 256 or 128 */
-    const void *A2;
+    int32_t a_x2, b_x2;   /* retired: the pre-split operand kernels were removed in round 4; must be 0
+                             (else U2GNN_E_ARG).  The fields keep the struct layout. */
+    const void *A2;       /* unused (retired with a_x2 / b_x2) */
     const void *B2;
     void *Cx2;            /* non-NULL: the epilogue result is also (C == NULL: only) written in x2
                              format, ldcx2 bf16 elements per row; split_k must be 1 */
     int64_t ldcx2;
-    const float *rowstat; /* ATTN_DS_RECOMP: [M][2] (row max, 1/row sum) */
-    int64_t m_valid, n_valid;   /* ATTN_DS_RECOMP: real rows / keys */
+    const float *rowstat; /* unused since ABI v13 (the retired ATTN_DS_RECOMP epilogue); layout kept */
+    int64_t m_valid, n_valid;   /* m_valid unused since v13; n_valid: STORE_ROWSTAT's real keys (columns) */
     /* ---- ABI v7: LayerNorm fused into the bias-dropout-residual epilogue (EPI_BIAS_DROP_RESID_LN) ---- */
     const float *ln_gamma, *ln_beta;   /* [ln_d], any 4-byte alignment */
     float *ln_y;                       /* [M][ln_ldy], 16-byte aligned rows */
@@ -209,13 +207,6 @@ int u2gnn_attn_softmax_fwd(const float *S, int64_t lds, float *P, float *Pd, int
                            int64_t rows_valid, int64_t rows_pad, int64_t n_valid, int64_t n_pad,
                            float p, uint64_t seed, uint32_t *keep, int64_t ld_keep, void *stream);
 /* delta[i] = sum_c A[i,c]*B[i,c]  (rowsum(dO * O) of the attention backward) */
-/* The same softmax + dropout for the pre-split attention path: Pd2 = x2(Pd) (Pd = P/(1-p) where kept,
- * 0 where dropped; ldp2 bf16 elements per row, n_pad % 8 == 0) and rowstat[i] = (row max, 1/row sum)
- * over the n_valid keys ((0, 0) for padded rows), from which the ATTN_DS_RECOMP epilogue recomputes
- * P exactly. */
-int u2gnn_attn_softmax_x2_fwd(const float *S, int64_t lds, void *Pd2, int64_t ldp2, float *rowstat,
-                              int64_t rows_valid, int64_t rows_pad, int64_t n_valid, int64_t n_pad,
-                              float p, uint64_t seed, void *stream);
 /* dst2 = x2(src) over rows x cols (cols % 8 == 0; ld_dst2 in bf16 elements) */
 int u2gnn_split_x2(const float *src, int64_t ld_src, void *dst2, int64_t ld_dst2, int64_t rows, int64_t cols,
                    void *stream);

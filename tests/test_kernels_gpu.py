@@ -1,4 +1,5 @@
 """Per-kernel numerics of libu2gnn_hip.so against plain torch fp32 references (GPU)."""
+import ctypes
 import math
 
 import pytest
@@ -857,3 +858,19 @@ def test_cx2_output_from_column(col0):
     assert torch.equal(sentinel[:, 2 * col0:], ref[:, 2 * col0:])
     assert bool((sentinel[:, :2 * col0] == 7.0).all())
 
+
+
+def test_retired_gemm_modes_are_rejected():
+    """ABI v13: the pre-split (x2) operands and the recomputed-P dS epilogue (ATTN_DS_RECOMP) that served
+    them are gone; a call asking for either returns an error before any launch."""
+    M = N = Kd = 128
+    A, B, C = _mk(M, Kd, seed=5), _mk(N, Kd, seed=6), torch.empty(M, N, device=DEV)
+    with pytest.raises(_lib.U2GNNNativeError):
+        K.gemm(A, B, C, M, N, Kd, Kd, Kd, N, trans_b=True, precision="bf16x3", epilogue=_lib.EPI_ATTN_DS_RECOMP,
+               aux0=C, rowvec=_mk(M, seed=7), ld_aux=N, p_drop=0.5)
+    with pytest.raises(_lib.U2GNNNativeError):   # bf16 operands = the retired x2 form
+        K.gemm(A.bfloat16(), B.bfloat16(), C, M, N, Kd, Kd, Kd, N, trans_b=True, precision="bf16x3")
+    a = K._gemm_args(A, B, C, M, N, Kd, Kd, Kd, N, trans_b=True, precision="bf16x3")
+    a.a_x2 = a.b_x2 = 1
+    assert K.hip_lib().u2gnn_gemm(ctypes.byref(a), None) == -1
+    assert not hasattr(K.hip_lib(), "u2gnn_attn_softmax_x2_fwd")   # no longer exported

@@ -35,7 +35,7 @@ PEAK = {"fp32": 157.3,     # TFLOP/s dense f32-input MFMA peak (MI355X_MICROARCH
         "bf16x3": 2500.0 / 3,  # 2.5 PF dense bf16 MFMA / 3 MFMAs per fp32-accurate product
         "bf16": 2500.0}
 DTYPE = {"fp32": "fp32", "bf16x3": "bf16x3", "bf16": "bf16",
-         "mixed": "bf16x3 (dS/dQ/dK: bf16)"}
+         "mixed": "bf16x3 (dS/dQ/dK: bf16)", "fwd32": "fp32 forward, bf16x3 backward"}
 
 
 def parse():
@@ -52,7 +52,7 @@ def parse():
     ap.add_argument("--num-timesteps", type=int, default=4)
     ap.add_argument("--ff-hidden-size", type=int, default=1024)
     ap.add_argument("--num-hidden-layers", type=int, default=1)
-    ap.add_argument("--precision", default="bf16x3", choices=["fp32", "bf16x3", "mixed", "bf16"],
+    ap.add_argument("--precision", default="bf16x3", choices=["fp32", "bf16x3", "mixed", "bf16", "fwd32"],
                     help="mixed = bf16x3 with the attention-backward dS/dQ/dK products on plain bf16 "
                          "(experiment: +4 %% at C4, outside the 1e-3 bound on the MUTAG L2T2 golden)")
     ap.add_argument("--lr", type=float, default=5e-4)
@@ -263,15 +263,21 @@ def pipeline_rate(store, trainer, args, dev, resident_value):
                     "buffers, H2D on a copy stream, GPU feature gather, training step"}
 
 
-def exact_line(args, batches, sd0, dev, d, C):
-    """The same C4 training step in the exact fp32 matrix-core precision (v_mfma_f32_32x32x2_f32, the parity
-    path) on the same batches and initial weights, beside the bf16x3 headline (the price of the
-    exact path on record).  args.fp32_steps timed steps after 2 warmup steps; not the headline value."""
+WHAT_PREC = {"fp32": "the same training step with every matrix-core product in exact fp32 (v_mfma_f32_32x32x2_f32)",
+             "fwd32": "the same training step with the forward products in exact fp32 and the backward in bf16x3: "
+                      "the forward's ReLU decisions then carry fp32 rounding only (DESIGN.md section 7)"}
+
+
+def exact_line(args, batches, sd0, dev, d, C, precision="fp32"):
+    """The same C4 training step in another precision policy -- "fp32" (every product exact fp32,
+    v_mfma_f32_32x32x2_f32) or "fwd32" (exact fp32 forward, bf16x3 backward) -- on the same batches and initial
+    weights, beside the bf16x3 headline (the price of each policy on record).
+    args.fp32_steps timed steps after 2 warmup steps; not the headline value."""
     from pytorch_U2GNN_Sup import TransformerU2GNN
     from u2gnn_hip.train import SupTrainer
     m = TransformerU2GNN(feature_dim_size=d, ff_hidden_size=args.ff_hidden_size, num_classes=C,
                          num_self_att_layers=args.num_timesteps, dropout=0.5,
-                         num_U2GNN_layers=args.num_hidden_layers, precision="fp32")
+                         num_U2GNN_layers=args.num_hidden_layers, precision=precision)
     m.load_state_dict(sd0)
     m = m.to(dev).train()
     tr = SupTrainer(m, lr=args.lr, max_norm=0.5, seed=123)
@@ -284,10 +290,9 @@ def exact_line(args, batches, sd0, dev, d, C):
         tr.step(batches[(2 + i) % nb])
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
-    out = {"precision": "fp32", "value": round(args.fp32_steps * args.batch_size / el, 2), "unit": "graphs/s",
+    out = {"precision": precision, "value": round(args.fp32_steps * args.batch_size / el, 2), "unit": "graphs/s",
            "ms_per_step": round(1e3 * el / args.fp32_steps, 3), "steps": args.fp32_steps,
-           "final_loss": round(float(tr.loss.item()), 5),
-           "what": "the same training step with every matrix-core product in exact fp32 (v_mfma_f32_32x32x2_f32)"}
+           "final_loss": round(float(tr.loss.item()), 5), "what": WHAT_PREC[precision]}
     del tr, m
     torch.cuda.empty_cache()
     return out
@@ -803,7 +808,8 @@ def main():
         ta, tb = args.probe in ("dv", "dk"), args.probe in ("qk", "ds")
         nn = Np0 if args.probe in ("qk", "ds") else ((d + 63) // 64 * 64)
         pk = "bf16" if (args.precision == "mixed" and args.probe in ("ds", "dq", "dk")) else \
-            ("bf16x3" if args.precision == "mixed" else args.precision)
+            ("bf16x3" if args.precision in ("mixed", "fwd32") and args.probe not in ("qk", "pv") else
+             ("fp32" if args.precision == "fwd32" else args.precision))
         split = 1 if args.probe in ("qk", "ds") else (2 if args.probe in ("dq", "dk") else 4)
         tile = 0 if args.probe == "ds" else 256
         sym = K.gemm_symbol(pk, Np0, nn, split, tile, ta, tb, epi, clamp_a=args.probe in ("pv", "dv"))
@@ -849,7 +855,9 @@ def main():
     if rank == 0:
         out["gather"] = gather_roofline(used[0], d, args.ff_hidden_size, K, dev)
     if rank == 0 and world == 1 and args.fp32_steps > 0 and args.precision != "fp32" and args.attention == "nodes":
-        out["fp32"] = exact_line(args, batches, sd0, dev, d, C)
+        out["fp32"] = exact_line(args, batches, sd0, dev, d, C, "fp32")
+        if args.precision == "bf16x3":
+            out["fwd32"] = exact_line(args, batches, sd0, dev, d, C, "fwd32")
     if rank == 0 and world == 1 and args.pipeline_steps > 0 and args.attention == "nodes":
         out["pipeline"] = pipeline_rate(store, trainer, args, dev, value)
     if rank == 0 and world == 1 and args.cpu_baseline:

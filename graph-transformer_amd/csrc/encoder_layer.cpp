@@ -39,6 +39,7 @@ struct Dims {
     int64_t N, d, ff, Np, dp, ffp;
     int prec;
     int prec_ab;   // dS, dQ, dK products (U2GNN_LAYER_ATTN_BWD_BF16: plain bf16)
+    int prec_fwd;  // forward products (U2GNN_LAYER_FWD_F32: exact fp32)
     bool deep_wgrad;
     int window;   // 0: attention over all N rows; W: within windows of W rows (N % W == 0)
 };
@@ -54,6 +55,8 @@ Dims make_dims(const u2gnn_layer_dims *a) {
     D.prec = a->precision;
     D.prec_ab = (a->precision == U2GNN_PREC_BF16X3 && (a->flags & U2GNN_LAYER_ATTN_BWD_BF16)) ? U2GNN_PREC_BF16
                                                                                              : a->precision;
+    D.prec_fwd = (a->precision == U2GNN_PREC_BF16X3 && (a->flags & U2GNN_LAYER_FWD_F32)) ? U2GNN_PREC_F32
+                                                                                        : a->precision;
     D.deep_wgrad = (a->flags & U2GNN_LAYER_DEEP_WGRAD) != 0;
     D.window = a->window;
     return D;
@@ -450,12 +453,12 @@ int64_t ffn2_split(bool fuse_ln, int64_t Np, int64_t ffp) {
 // them), then 128x128 (the same per-element sums: same bits; engine.qk_tile mirrors the rule)
 int qk_tile(int64_t Np) { return (Np % 256 == 0 && (Np / 256) * (Np / 128) >= 256) ? 256 : 128; }
 
-bool fused_attn(const Dims &D) { return !D.window && D.prec != U2GNN_PREC_F32 && D.dp <= 384; }
+bool fused_attn(const Dims &D) { return !D.window && D.prec_fwd != U2GNN_PREC_F32 && D.dp <= 384; }
 
 int layer_fwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seeds *s, const float *X, float *X2,
               Arena &CA, Arena &W, bool need_ctx, hipStream_t st) {
     const int64_t N = D.N, Np = D.Np, d = D.d, dp = D.dp, ffp = D.ffp;
-    const int prec = D.prec;
+    const int prec = D.prec_fwd;
     const float pd = s->p_drop;
     const bool drop = pd > 0.f;
     const bool plan = W.plan();
@@ -520,7 +523,7 @@ int layer_fwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
             U2GNN_TRY(u2gnn_attn_softmax_fwd(S, Np, drop ? nullptr : c.Pd, c.Pd, Np, N, Np, N, Np, pd, s->attn,
                                              nullptr, 0, st));
         U2GNN_TRY(gemm_split(W, D, c.Pd, V, c.O, Np, dp, Np, Np, 3 * dp, dp, false, 1.f, false, nullptr, nullptr,
-                             false, st, drop, -1, U2GNN_ROLE_PV));
+                             false, st, drop, prec, U2GNN_ROLE_PV));
     }
     // a3.3 out-projection + dropout1 + residual, LayerNorm1 (fused into the GEMM epilogue when a
     // 64-column tile holds whole rows: d <= 64, bf16 modes; engine.fused_ln mirrors the rule)
@@ -691,7 +694,13 @@ int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
         U2GNN_TRY(gemm_split(W, D, dQKV, w->W_in, dX, Np, dp, 3 * dp, 3 * dp, dp, dp, false, 1.f, true, nullptr,
                              nullptr, false, st));
     U2GNN_TRY(wgrad(W, D, dQKV, 3 * dp, X, dp, 3 * dp, dp, g->in_w, d, blk_d, blk_d, st, df));
-    U2GNN_TRY(bias_grad(W, dQKV, Np, 3 * dp, 3 * dp, dp, d, g->in_b, st, df));
+    // in_proj_bias: the Q and V thirds are column sums of dQKV; the K third is exactly zero -- a softmax row is
+    // invariant to a constant added to its scores, so sum_j dK_j = sum_i Q_i sum_j dS_ij = 0.  The reference's
+    // value there is summation noise, which Adam's first step (lr g / (|g| + eps)) turns into moves of up to lr;
+    // a column sum over zero rows writes the exact zeros (engine.in_bias_grad mirrors this)
+    U2GNN_TRY(bias_grad(W, dQKV, Np, dp, 3 * dp, dp, d, g->in_b, st, df));
+    U2GNN_TRY(bias_grad(W, dQKV + dp, 0, dp, 3 * dp, dp, d, g->in_b + d, st, df));
+    U2GNN_TRY(bias_grad(W, dQKV + 2 * dp, Np, dp, 3 * dp, dp, d, g->in_b + 2 * d, st, df));
     // the held-back work: on the side stream after everything issued so far, except for the last layer of
     // the backward (need_dx false), where nothing is left to overlap and the hand-off plus the step's final
     // join cost more than the products (C4 round 3: 3.140-3.157 vs 3.171-3.194 ms per step)
@@ -704,6 +713,7 @@ int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
 bool dims_ok(const u2gnn_layer_dims *a) {
     return a && a->N >= 1 && a->d >= 1 && a->ff >= 1 && rup(a->d, 64) <= 1024 &&
            (a->precision == U2GNN_PREC_F32 || a->precision == U2GNN_PREC_BF16X3 || a->precision == U2GNN_PREC_BF16) &&
+           ((a->flags & U2GNN_LAYER_FWD_F32) == 0 || a->precision == U2GNN_PREC_BF16X3) &&
            a->window >= 0 && a->window <= 32 && (a->window == 0 || a->N % a->window == 0);
 }
 

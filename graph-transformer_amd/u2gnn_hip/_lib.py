@@ -30,7 +30,7 @@ ERRORS = {-1: "bad argument", -2: "misaligned pointer / leading dimension", -3: 
 
 EPI_STORE, EPI_BIAS, EPI_BIAS_DROP_RESID, EPI_BIAS_RELU_DROP, EPI_RELU_DROP_BWD, EPI_ACCUM, EPI_ATTN_DS, \
     EPI_ATTN_DS_SIGNED, EPI_ATTN_DS_RECOMP, EPI_BIAS_DROP_RESID_LN, EPI_STORE_ROWDOT, EPI_STORE_ROWSTAT = range(12)
-ABI_VERSION = 13   # include/u2gnn_hip.h U2GNN_ABI_VERSION
+ABI_VERSION = 14   # include/u2gnn_hip.h U2GNN_ABI_VERSION
 PREC_F32, PREC_BF16X3, PREC_BF16 = 0, 1, 2
 
 
@@ -108,6 +108,7 @@ class LayerGrads(ctypes.Structure):
 
 LAYER_DEEP_WGRAD = 1
 LAYER_ATTN_BWD_BF16 = 2   # precision "mixed": dS, dQ, dK on plain bf16 (ABI v5)
+LAYER_FWD_F32 = 4         # precision "fwd32": forward products exact fp32, backward bf16x3 (ABI v14)
 ROLE_QK, ROLE_PV, ROLE_DS, ROLE_DV, ROLE_DQ, ROLE_DK = range(1, 7)   # u2gnn_probe_arm roles
 
 I64, F32, VP, I32 = c_int64, c_float, c_void_p, c_int32

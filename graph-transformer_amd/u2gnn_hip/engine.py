@@ -243,12 +243,22 @@ ROLE_BF16: set = set()
 # the weight/input-gradient products are far outside the bound in plain bf16 (0.09..0.39: ReLU units
 # flipping), so they stay bf16x3.
 MIXED_BF16_ROLES = ("ds", "dq", "dk")
+# Precision experiments (Python orchestration only): role -> precision overriding the layer's
+# (tools/prec_train_probe.py measures train-mode parity per policy).
+ROLE_PREC: Dict[str, str] = {}
+# precision "fwd32": the forward products exact fp32 (so the forward's ReLU decisions carry fp32 rounding
+# only), the backward bf16x3 (u2gnn_hip.h U2GNN_LAYER_FWD_F32)
+FWD_ROLES = ("in_proj", "qk", "pv", "out_proj", "ffn1", "ffn2")
 
 
 def _rp(role: str, prec: str) -> str:
     """Matrix-core precision of one product (role) of a layer running at `prec`."""
+    if role in ROLE_PREC:
+        return ROLE_PREC[role]
     if prec == "mixed":
         return "bf16" if role in MIXED_BF16_ROLES else "bf16x3"
+    if prec == "fwd32":
+        return "fp32" if role in FWD_ROLES else "bf16x3"
     return "bf16" if (prec == "bf16x3" and role in ROLE_BF16) else prec
 
 
@@ -301,8 +311,17 @@ def _wgrad(dY, ld_dy, X, ld_x, m_pad, n_pad, rows_pad, dst, rblk, cblk, prec, n_
 
 
 def _bias_grad(dY, rows, cols_pad, ld, cblk, out):
-    ws = torch.empty(K.colstat_ws_floats(rows, cols_pad), device=dY.device, dtype=torch.float32)
+    ws = torch.empty(max(4, K.colstat_ws_floats(rows, cols_pad)), device=dY.device, dtype=torch.float32)
     K.colsum(dY, rows, cols_pad, ld, cblk, out, ws)
+
+
+def in_bias_grad(dQKV, Np, dp, d, out):
+    """in_proj_bias gradient: column sums of dQKV's Q and V thirds; the K third is exactly zero (a softmax row
+    is invariant to a constant added to its scores: sum_j dK_j = sum_i Q_i sum_j dS_ij = 0), written as the
+    column sum of zero rows.  Mirrors encoder_layer.cpp (same launches, same bits)."""
+    _bias_grad(dQKV, Np, dp, 3 * dp, (dp, d), out[:d])
+    _bias_grad(dQKV[:, dp:], 0, dp, 3 * dp, (dp, d), out[d:2 * d])
+    _bias_grad(dQKV[:, 2 * dp:], Np, dp, 3 * dp, (dp, d), out[2 * d:])
 
 
 def _gemm_nodes_k(A, B, C, M, N, Kd, lda, ldb, ldc, trans_a=False, alpha=1.0, prec="fp32", flops=None,
@@ -340,7 +359,7 @@ def _attn_split(Q, Kt, V, N, Np, dp, pd, seeds, prec, att, dev):
     f32 = torch.float32
     S = torch.empty(Np, Np, device=dev, dtype=f32)
     K.gemm(Q, Kt, S, Np, Np, dp, 3 * dp, 3 * dp, Np, trans_b=True, precision=_rp("qk", prec), flops=att,
-           tile=256 if (prec != "fp32" and Np % 256 == 0) else 0)
+           tile=256 if (_rp("qk", prec) != "fp32" and Np % 256 == 0) else 0)
     # one [Np, Np] image: with dropout the signed one (P/(1-p) where kept, -P where dropped), which
     # P.V and dP^T.dO read as Pd (negatives staged as 0) and the dS epilogue reads as P and keep
     Pd = torch.empty(Np, Np, device=dev, dtype=f32)
@@ -366,7 +385,7 @@ def encoder_layer_forward(X: torch.Tensor, w: PackedLayer, p: LayerParams, dims:
     QKV2 = torch.empty(Np, 6 * dp, device=dev, dtype=torch.bfloat16) if fused else None   # x2 copy for P.V
     K.gemm(X, w.W_in, QKV, Np, 3 * dp, dp, dp, dp, 3 * dp, trans_b=True, epilogue=E.EPI_BIAS, bias=w.b_in,
            alpha=1.0 / math.sqrt(d), scale_cols=dp, precision=_rp("in_proj", prec), flops=6.0 * N * d * d,
-           tile=256 if (prec != "fp32" and Np % 256 == 0 and (Np // 256) * (3 * dp // 128) >= BIG_TILE_BLOCKS) else 0,
+           tile=256 if (_rp("in_proj", prec) != "fp32" and Np % 256 == 0 and (Np // 256) * (3 * dp // 128) >= BIG_TILE_BLOCKS) else 0,
            Cx2=QKV2, ldcx2=6 * dp, cx2_col0=2 * dp)
     Q, Kt, V = QKV[:, :dp], QKV[:, dp:2 * dp], QKV[:, 2 * dp:]
     if fused:
@@ -388,7 +407,7 @@ def encoder_layer_forward(X: torch.Tensor, w: PackedLayer, p: LayerParams, dims:
     X1 = torch.empty(Np, dp, device=dev, dtype=f32)
     mean1 = torch.empty(Np, device=dev, dtype=f32)
     rstd1 = torch.empty(Np, device=dev, dtype=f32)
-    fuse = fused_ln(dp, prec)   # LayerNorm in the GEMM epilogue when a 64-column tile holds whole rows
+    fuse = fused_ln(dp, _rp("out_proj", prec))   # LayerNorm in the GEMM epilogue when a 64-column tile holds whole rows
     K.gemm(O, w.W_o, Z1, Np, dp, dp, dp, dp, dp, trans_b=True,
            epilogue=E.EPI_BIAS_DROP_RESID_LN if fuse else E.EPI_BIAS_DROP_RESID, bias=w.b_o,
            aux0=X, ld_aux=dp, p_drop=pd, seed=seeds.get(SITE_DROP1, 0), precision=_rp("out_proj", prec),
@@ -465,7 +484,7 @@ def encoder_layer_backward(dX2: torch.Tensor, ctx: EncoderLayerCtx, w: PackedLay
     # LN1 backward -> dX (residual), dA (dropout1 branch)
     dX = torch.empty(Np, dp, device=dev, dtype=f32)
     dA = torch.empty(Np, dp, device=dev, dtype=f32)
-    use_ln_delta = ln_delta(prec)
+    use_ln_delta = ln_delta(_rp("ds", prec))
     if use_ln_delta:   # LayerNorm1's backward also forms the attention backward's delta = rowsum(dO * O)
         delta = torch.empty(Np, device=dev, dtype=f32)
         K.layernorm_bwd_delta(dX1, dp, ctx.Z1, dp, ctx.mean1, ctx.rstd1, p.n1_w, dX, dp, dA, dp, pd,
@@ -505,7 +524,7 @@ def encoder_layer_backward(dX2: torch.Tensor, ctx: EncoderLayerCtx, w: PackedLay
 
     def in_proj_grads(dQKV=dQKV):
         _wgrad(dQKV, 3 * dp, ctx.X, dp, 3 * dp, dp, Np, g.in_w, (dp, d), (dp, d), _rp("in_dw", prec), N)
-        _bias_grad(dQKV, Np, 3 * dp, 3 * dp, (dp, d), g.in_b)
+        in_bias_grad(dQKV, Np, dp, d, g.in_b)
     if need_dx:
         off.run(in_proj_grads, dQKV, ctx.X)
     else:   # the last layer of the backward: nothing left on this stream to overlap, skip the hand-off

@@ -42,6 +42,8 @@ def _dims(N: int, d: int, ff: int, prec: str, deep_wgrad: bool, window: int = 0)
     flags = _lib.LAYER_DEEP_WGRAD if deep_wgrad else 0
     if prec == "mixed":   # bf16x3 except the attention-backward products dS, dQ, dK (engine.MIXED_BF16_ROLES)
         prec, flags = "bf16x3", flags | _lib.LAYER_ATTN_BWD_BF16
+    elif prec == "fwd32":  # exact fp32 forward products, bf16x3 backward (engine.FWD_ROLES)
+        prec, flags = "bf16x3", flags | _lib.LAYER_FWD_F32
     return LayerDims(int(N), int(d), int(ff), PREC[prec], flags, int(window), 0)
 
 

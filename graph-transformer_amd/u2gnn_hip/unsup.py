@@ -71,6 +71,9 @@ class UnSupTrainer:
         self.row_sync = None
         # ss.weight rows written by this step's gradient (zeroed again after the optimizer step)
         self._touched = ()
+        # tests: keep the last step's encoder context (saved activations) as self.last_ctx
+        self.keep_ctx = False
+        self.last_ctx = None
 
     def next_seed(self) -> int:
         return int(torch.randint(0, 2 ** 62, (1,), generator=self.gen).item())
@@ -87,6 +90,8 @@ class UnSupTrainer:
         p = core.p_out if train else 0.0
         ds = site_seed(seed, 0, 0, SITE_SS_DROP)
         OVd, sctx = core.encode(b, train, True, seed, p, ds)   # dropout fused into the concatenation
+        if self.keep_ctx:
+            self.last_ctx = sctx
         N, D = OVd.shape
         W = ss.weight
         S = sample_ids.numel()

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define U2GNN_ABI_VERSION 13
+#define U2GNN_ABI_VERSION 14
 
 #define U2GNN_OK 0
 #define U2GNN_E_ARG (-1)    /* bad size / null pointer */
@@ -456,6 +456,10 @@ int u2gnn_window_attn_bwd(const float *QKV, int64_t ldq, int32_t W, int32_t dp, 
  * node-depth products dS = P o (dO V^T - delta), dQ = dS K, dK = dS^T Q run on plain bf16
  * operands (fp32 accumulation); every other product stays bf16x3 */
 #define U2GNN_LAYER_ATTN_BWD_BF16 2
+/* precision "fwd32" (ABI v14): with precision == U2GNN_PREC_BF16X3, every FORWARD product (in-projection,
+ * Q K^T, P V, out-projection, FFN1, FFN2) runs exact fp32 (the three-pass attention forward); the
+ * backward stays bf16x3.  The forward's ReLU decisions then carry fp32 rounding only */
+#define U2GNN_LAYER_FWD_F32 4
 typedef struct u2gnn_layer_dims {
     int64_t N, d, ff;      /* real rows (nodes; window mode: nodes * window tokens), model width, FFN width */
     int32_t precision;     /* U2GNN_PREC_* */

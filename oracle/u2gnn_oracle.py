@@ -194,7 +194,8 @@ def encoder_layer(x: torch.Tensor, prm: Dict[str, torch.Tensor], train: bool, p:
     ``masks`` (optional, slot-0 only, shapes [S,S] / [S,d] / [S,ff]) replaces the random
     dropout masks of slot 0 for exact train-mode parity tests.  Test-only key ``"relu"`` ([S,ff] of 0/1):
     the ReLU's on/off decision of slot 0 taken from outside (a GPU run's), instead of the sign of the
-    pre-activation -- the diagnostic that isolates ReLU boundary flips (tests/test_train_parity_gpu.py)."""
+    pre-activation -- the diagnostic that isolates ReLU boundary flips (tests/test_train_parity_gpu.py);
+    test-only key ``"pre_out"`` (a list): slot 0's FFN pre-activations [S, ff] are appended to it."""
     S, B, d = x.shape
     W, b = prm["in_proj_weight"], prm["in_proj_bias"]
     qkv = x @ W.t() + b                                     # [S,B,3d]
@@ -225,6 +226,8 @@ def encoder_layer(x: torch.Tensor, prm: Dict[str, torch.Tensor], train: bool, p:
     x = F.layer_norm(x + _drop(sa, p, train, site_mask("drop1", sa)), (d,),
                      prm["norm1.weight"], prm["norm1.bias"], 1e-5)
     pre = x @ prm["linear1.weight"].t() + prm["linear1.bias"]
+    if masks is not None and "pre_out" in masks:   # test-only: record slot 0's pre-activations [S, ff]
+        masks["pre_out"].append(pre[:, 0].detach().clone())
     if masks is not None and "relu" in masks:
         on = (pre > 0).to(pre.dtype)
         on[:, 0] = masks["relu"]
@@ -262,7 +265,7 @@ def sup_forward(sd: Dict[str, torch.Tensor], input_x: torch.Tensor, offsets: np.
     unpinned by the reference)."""
     if slots is not None:
         input_x = input_x[:, :slots]
-    P = pool_matrix(offsets)
+    P = pool_matrix(offsets).to(X_concat.dtype)
     scores = 0
     inp = F.embedding(input_x, X_concat)                   # [N, k+1, d]
     nb = attention == "neighbors"

@@ -1,0 +1,127 @@
+"""Helpers of the train-mode (dropout on) parity tests (tests/test_train_parity_gpu.py,
+tests/test_unsup_train_parity_gpu.py).  Test infrastructure only.
+
+Why the tests look the way they do (profiles/r05/prec_train_*.jsonl): in train mode
+every parameter gradient behind a ReLU is a DIScontinuous function of the forward -- a unit whose
+pre-activation z lies within the rounding error of 0 may switch sides, and a switched unit moves its row of
+dW1 by dH[n, j] * X1[n, :] (~1e-2 at C4).  On C4 batches the reference's own fp32 arithmetic (the oracle,
+torch CPU fp32) switches 0-2 units per step against a float64 run of the same maths (|z| <= 2.3e-7) and its
+linear1 gradients then miss the fp64 ones by up to 2e-2 (2 of 8 seeds); the GPU's fp32 path switches 0-2
+(4 of 8 seeds above 1e-3), bf16x3 6-20 (|z| <= 8.6e-6).  So "every gradient within 1e-3 of the oracle" is
+not a property any implementation that is not bit-identical to the oracle's summation order can have in
+train mode.  The tests therefore check, strictly and without per-quantity exceptions:
+  (1) every quantity -- outputs, loss, clip norm, every gradient, every post-Adam parameter -- within 1e-3
+      of the oracle run with the GPU's own ReLU decisions (masks["relu"]), i.e. the same discrete choices;
+  (2) every GPU decision that differs from the plain oracle's is a unit with |z_oracle| <= 2 * delta_z, where
+      delta_z = max |z_gpu - z_oracle| over the kept units both runs switch on (z_gpu = Hd * (1 - p) from
+      the saved dropped-ReLU image): a unit switches sides only within the measured forward disagreement
+      of 0, not because of a wrong unit; and there are at most MAX_FLIP_FRAC of the kept units;
+  (3) the continuous quantities (outputs, loss, clip norm) within 1e-3 of the plain oracle.
+Post-Adam parameters have the same kind of discontinuity: Adam's first step moves an element by
+lr * g / (|g| + eps), i.e. by ~lr in the direction of sign(g).  Where a gradient element lies within the
+two computations' disagreement of zero (|g_oracle| <= 2 * max|g_gpu - g_oracle| of its tensor: the element's
+sign is not determined by either fp32 computation -- e.g. the key bias, whose exact gradient is 0, or C5's
+symmetric d = 4 layer), the two steps may go opposite ways.  after_err() therefore holds every post-Adam
+element to 1e-3 unless its gradient is sign-unresolved in that sense, and reports how many elements used
+that clause (a handful per step, listed in the report).
+"""
+import torch
+
+TOL = 1e-3
+# the measured forward disagreement |z_gpu - z_oracle| at the ReLU input sets where decisions may differ
+# (C4, 8 seeds: differing decisions at |z| <= 8.6e-6 in bf16x3, <= 5.1e-7 with exact fp32 forward products;
+# C5, whose d = 4 inputs are all equal, has a worse-conditioned forward: 2.7e-5 in fp32)
+FLIP_MARGIN = 2.0
+MAX_FLIP_FRAC = 1e-5
+P_ENC = 0.5   # encoder dropout (pytorch_U2GNN_Sup.py:20)
+
+def rel_err(a, b):
+    a = torch.as_tensor(a).double().cpu()
+    b = torch.as_tensor(b).double().cpu()
+    if a.numel() == 0:
+        return 0.0
+    return ((a - b).abs().max() / max(1.0, b.abs().max().item())).item()
+
+
+def layer_masks(seed, l, t, N, d, ff):
+    """The kernels' own dropout masks of encoder layer (l, t) (site seeds of EncoderStack.forward),
+    real-sized [N, N] / [N, d] / [N, ff] float 0/1, for the oracle's masks[(l, t)]."""
+    from u2gnn_hip import kernels as K
+    from u2gnn_hip.engine import SITE_ATTN, SITE_DROP1, SITE_DROP2, SITE_DROPFF, row_pad, rup, site_seed
+    Np, dp, ffp = row_pad(N), rup(d, 64), rup(ff, 64)
+
+    def mk(s, r, c):
+        return K.dropout_mask(s, r, c, 0.5).float().cpu()
+    return {"attn": mk(site_seed(seed, l, t, SITE_ATTN), Np, Np)[:N, :N],
+            "drop1": mk(site_seed(seed, l, t, SITE_DROP1), Np, dp)[:N, :d],
+            "drop_ff": mk(site_seed(seed, l, t, SITE_DROPFF), Np, ffp)[:N, :ff],
+            "drop2": mk(site_seed(seed, l, t, SITE_DROP2), Np, dp)[:N, :d]}
+
+
+def gpu_decisions(stack_ctx, N, ff):
+    """{(l, t): [N, ff] float} of a Python-orchestration run: the saved dropped-ReLU image Hd times (1 - p),
+    i.e. the GPU's pre-activation z where relu' * keep = 1 and 0 elsewhere (Hd > 0 is the decision)."""
+    out = {}
+    for l, row in enumerate(stack_ctx["layers"]):
+        for t, c in enumerate(row):
+            out[(l, t)] = c.Hd[:N, :ff].detach().cpu() * (1.0 - P_ENC)
+    return out
+
+
+def add_capture(masks, keys):
+    for k in keys:
+        masks[k]["pre_out"] = []
+
+
+def inject(masks, dec, keys):
+    """A copy of masks with the GPU's decisions as masks[(l, t)]["relu"] (no capture lists)."""
+    out = {}
+    for k, v in masks.items():
+        if k in keys:
+            out[k] = {kk: vv for kk, vv in v.items() if kk != "pre_out"}
+            out[k]["relu"] = (dec[k] > 0).float()
+        else:
+            out[k] = v
+    return out
+
+
+def flip_stats(masks, dec, keys):
+    """(differing decisions among kept units, kept units, max |z_oracle| over them, delta_z) against the plain
+    oracle's captured pre-activations; delta_z = max |z_gpu - z_oracle| over kept units both switch on."""
+    n, kept, mx, dz = 0, 0, 0.0, 0.0
+    for k in keys:
+        pre = masks[k]["pre_out"][0]
+        keep = masks[k]["drop_ff"] > 0
+        on = dec[k] > 0
+        diff = keep & (on != (pre > 0))
+        n += int(diff.sum())
+        kept += int(keep.sum())
+        if diff.any():
+            mx = max(mx, float(pre[diff].abs().max()))
+        both = keep & on & (pre > 0)
+        if both.any():
+            dz = max(dz, float((dec[k][both].double() - pre[both].double()).abs().max()))
+    return n, kept, mx, dz
+
+
+def assert_flips_at_boundary(stats, what):
+    n, kept, mx, dz = stats
+    assert mx <= FLIP_MARGIN * dz or n == 0, \
+        f"{what}: a ReLU decision differs at |z| = {mx:.3g}, beyond {FLIP_MARGIN} x the forward disagreement {dz:.3g}"
+    assert n <= max(2, int(MAX_FLIP_FRAC * kept)), f"{what}: {n} differing ReLU decisions of {kept} kept units"
+
+
+def after_err(after_gpu, after_ref, g_gpu, g_ref):
+    """(max relative post-Adam error over the elements whose gradient sign is resolved, elements above TOL
+    whose gradient is sign-unresolved, raw max relative error) -- see the module docstring."""
+    a = torch.as_tensor(after_gpu).double().cpu()
+    b = torch.as_tensor(after_ref).double().cpu()
+    gg = torch.as_tensor(g_gpu).double().cpu()
+    gr = torch.as_tensor(g_ref).double().cpu()
+    if a.numel() == 0:
+        return 0.0, 0, 0.0
+    scale = max(1.0, b.abs().max().item())
+    e = (a - b).abs() / scale
+    unresolved = gr.abs() <= 2.0 * (gg - gr).abs().max()
+    resolved_err = float(e[~unresolved].max()) if bool((~unresolved).any()) else 0.0
+    return resolved_err, int(((e > TOL) & unresolved).sum()), float(e.max())

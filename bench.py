@@ -80,6 +80,10 @@ def parse():
                          "default command holds only the timed region's launches")
     ap.add_argument("--attention", default="nodes", choices=["nodes", "neighbors"],
                     help="nodes = the fork's semantics (the headline metric); neighbors = paper semantics")
+    ap.add_argument("--configs", type=int, default=1,
+                    help="C4 at N=1: also run the other BASELINE configs (c5, c2, c3) in the same process and "
+                         "report each as an object of the C4 line (0 = skip)")
+    ap.add_argument("--config-steps", type=int, default=30, help="timed steps of each embedded config line")
     ap.add_argument("--workload", default="c4", choices=["c4", "c5", "c2", "c3"],
                     help="c4 = U2GNN-Sup COLLAB (the headline metric); c5 = U2GNN-UnSup REDDIT-M5K (HBM-bound); "
                          "c2 = U2GNN-Sup IMDBBINARY, c3 = U2GNN-UnSup PTC (BASELINE configs[1], [2]: real data, "
@@ -184,22 +188,29 @@ def gather_roofline(b, d, ff, K, dev, reps=20):
     W = b.input_x.shape[1]
     R = b.N * W
     Rp, dp = Dims(R, d, ff).Np, rup(d, 64)
-    dst = torch.empty(Rp, dp, device=dev, dtype=torch.float32)
-    for _ in range(3):
-        K.gather_rows(b.X_concat, b.input_x, 1, dst, R, Rp, d, dp)
+    # the launches write to destinations rotating over > 512 MiB (twice the 256 MB MALL), so a timed launch's
+    # writes cannot sit in the cache a previous launch warmed: each launch pays its write-back to HBM
+    dst_bytes = Rp * dp * 4
+    nbuf = max(2, -(-(512 << 20) // dst_bytes) + 1)
+    pool = torch.empty(nbuf, Rp, dp, device=dev, dtype=torch.float32)
+    for i in range(3):
+        K.gather_rows(b.X_concat, b.input_x, 1, pool[i % nbuf], R, Rp, d, dp)
+    reps = max(reps, nbuf)
     st = torch.cuda.current_stream(dev)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(st)
-    for _ in range(reps):
-        K.gather_rows(b.X_concat, b.input_x, 1, dst, R, Rp, d, dp)
+    for i in range(reps):
+        K.gather_rows(b.X_concat, b.input_x, 1, pool[(i + 3) % nbuf], R, Rp, d, dp)
     e1.record(st)
     torch.cuda.synchronize()
+    del pool
     us = e0.elapsed_time(e1) * 1e3 / reps
     nbytes = Rp * dp * 4 + R * 8 + b.N * d * 4
     ach = nbytes / (us * 1e-6) / 1e9
     return {"bound": "hbm", "kernel": "gather_rows_multi_kernel (a2, all k+1 slots)", "achieved": round(ach, 1),
             "peak": 8000.0, "unit": "GB/s", "frac": round(ach / 8000.0, 4), "avg_launch_us": round(us, 2),
-            "algorithmic_bytes_per_launch": nbytes, "rows": R, "rows_pad": Rp, "d": d, "d_pad": dp}
+            "algorithmic_bytes_per_launch": nbytes, "rows": R, "rows_pad": Rp, "d": d, "d_pad": dp,
+            "destinations": f"{reps} launches rotating over {nbuf} destination images ({nbuf * dst_bytes / 2**20:.0f} MiB)"}
 
 
 def cpu_baseline(hb, sd, args, d, C):
@@ -345,12 +356,13 @@ def unsup_cpu_baseline(hbs, sids, sd, V, T, lr, steps):
                       f"median {t:.2f} s/step, oracle/u2gnn_oracle.py on torch CPU, {threads} threads"}
 
 
-def c5_group_roofline(args, trainer, batches, elapsed):
-    """C5's dominant launch: the attention backward's grouped dV / dQ / dK product (one launch per layer on the
-    one-stream schedule, gemm_bf16_group_kernel<64, 64, ...>; the largest per-launch device time of the C5
-    rocprof summary, profiles/r03).  Timed live by the executor's probe (HIP events around the grouped launch
-    on its stream) over args.steps EAGER steps after the timed graph-replay region (events recorded inside a
-    captured graph would belong to the capture).  Algorithmic FLOPs: 3 products x 2 N^2 d (real dims)."""
+def c5_attn_kernel(args, trainer, batches):
+    """C5's attention backward: the small-width kernels (u2gnn_attn_small_bwd: the dQ walk, which also writes
+    the compact query records, and the dK/dV walk over them; csrc/attn_small.hip) that replaced the padded matrix-core products at d = 4 (round 5).  Timed live
+    by the executor's probe (HIP events around each layer's backward attention call on its stream) over
+    args.steps EAGER steps after the timed graph-replay region.  Algorithmic FLOPs 8 N^2 d per launch (dO.V^T,
+    dS K, dS^T Q, Pd^T dO; the recomputed Q K^T not credited) against the fp32 vector peak: the kernels run on
+    the vector ALUs (exp2, the dropout hash and d-wide dot products per (query, key) pair)."""
     from u2gnn_hip import _lib as LIB
     from u2gnn_hip import native
     if not native.enabled():
@@ -359,7 +371,7 @@ def c5_group_roofline(args, trainer, batches, elapsed):
     nb = len(batches)
     steps = max(4, args.steps)
     torch.cuda.synchronize()
-    native.probe_arm(LIB.ROLE_DQ, steps * per_step)
+    native.probe_arm(LIB.ROLE_DS, steps * per_step)
     for i in range(steps):
         trainer.step(*batches[i % nb])
     torch.cuda.synchronize()
@@ -367,20 +379,22 @@ def c5_group_roofline(args, trainer, batches, elapsed):
     if n != steps * per_step or ms <= 0.0:
         return None
     d = 4   # REDDIT-M5K features (X = 0.01 * ones[n, 4])
-    fl = float(sum(per_step * 3 * 2.0 * batches[i % nb][0].N ** 2 * d for i in range(steps)))
+    fl = float(sum(per_step * 8.0 * batches[i % nb][0].N ** 2 * d for i in range(steps)))
     ach = fl / (ms * 1e-3) / 1e12
-    peak = PEAK[args.precision if args.precision in PEAK else "bf16x3"]
-    return {"bound": "mfma", "achieved": round(ach, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
-            "frac": round(ach / peak, 4), "traffic": None,
-            "kernel": "gemm_bf16_group_kernel<64, 64, 2, 2, 32, true> (grouped dV = Pd^T dO, dQ = dS K, dK = dS^T Q)",
-            "role": "attention-backward group", "launches": n, "avg_launch_us": round(1e3 * ms / n, 1),
-            "algorithmic_flop_per_launch": round(fl / n),
-            "timing": "live: HIP events around each grouped launch, eager steps after the timed region",
-            "dominance": "largest per-launch device time of the C5 step (rocprof summary, DESIGN.md section 5.6); "
-                         "C5 is launch-bound: ~100 launches per step, none above ~9 % of it"}
+    return {"bound": "valu", "achieved": round(ach, 3), "peak": PEAK["fp32"], "unit": "TFLOP/s",
+            "frac": round(ach / PEAK["fp32"], 4),
+            "kernel": "u2gnn_attn_small_bwd (sa_bwd_q_kernel<4> + sa_bwd_kv_kernel<4>)",
+            "launches": n, "avg_launch_us": round(1e3 * ms / n, 1), "algorithmic_flop_per_launch": round(fl / n),
+            "timing": "live: HIP events around each layer's attention backward, eager steps after the timed region"}
 
 
 def main_c5(args):
+    out = run_c5(args)
+    if out is not None:
+        emit(out)
+
+
+def run_c5(args):
     """synthetic REDDIT-MULTI-5K (4999 graphs, mean 508.5 nodes, V = sum of
     nodes ~2.54M), batch 4, k=16, T=4, ff=1024, 512 sampled classes, D = 4.  HBM-bound: the
     roofline kernel is the optimizer sweep (clip-norm + Adam over the dense embedding table,
@@ -487,7 +501,7 @@ def main_c5(args):
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    roof = opt_roof = None
+    opt_roof = attn = None
     if not args.no_roofline:
         n = trainer.flat.n
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -506,7 +520,7 @@ def main_c5(args):
                     "params": n, "algorithmic_bytes_per_step": byts, "optimizer_us": round(us, 1),
                     "optimizer_share_of_step": round(us * 1e-3 / (1e3 * elapsed / args.steps), 3)}
         if dist is None:
-            roof = c5_group_roofline(args, trainer, batches, elapsed)
+            attn = c5_attn_kernel(args, trainer, batches)
     mean_N = float(np.mean([b.N for b, _ in batches]))
     # step-level HBM roofline: algorithmic bytes of the whole step = the dense Adam sweep
     # over ss.weight (p, g, m, v read; p, m, v written), the row gathers / scatters of the sampled softmax
@@ -514,7 +528,7 @@ def main_c5(args):
     n_enc = trainer.flat.n - V * 4
     step_bytes = 4.0 * 6 * V * 4 + 4.0 * 3 * (mean_N + S) * 4 + 4.0 * 3 * n_enc * 7 / 3
     step_ach = step_bytes / (elapsed / args.steps) / 1e9
-    step_roof = {"bound": "hbm", "achieved": round(step_ach, 1), "peak": 8000.0, "unit": "GB/s",
+    step_roof = {"bound": "hbm", "achieved": round(step_ach, 1), "peak": 8000.0, "unit": "GB/s", "traffic": None,
                  "frac": round(step_ach / 8000.0, 4), "algorithmic_bytes_per_step": round(step_bytes),
                  "what": "SURVEY.md §8(d) C5 bytes per step (4*6*V*D + 4*3*(N+S)*D + 4*3*P_enc*7/3) / ms_per_step"}
     out = {"metric": METRIC_C5, "value": round(args.steps * bs * world / elapsed, 2), "unit": "graphs/s",
@@ -530,15 +544,15 @@ def main_c5(args):
                                                      else ""),
                       "precision": args.precision, "hip_graph": graph},
            "final_loss": round(loss, 4), "host_issue_ms_per_step": round(1e3 * t_issue / args.steps, 3),
-           "roofline": roof, "optimizer": opt_roof, "step_hbm": step_roof, "cpu_baseline": None,
+           "roofline": step_roof, "optimizer": opt_roof, "step_hbm": step_roof, "attention_kernel": attn,
+           "cpu_baseline": None,
            "samples": "512 log-uniform ids drawn on the host every step (C++ sampler) and copied to HBM"}
     if rank == 0 and world == 1 and args.cpu_baseline:
         out["cpu_baseline"] = unsup_cpu_baseline(host, sids_host, sd0, V, args.num_timesteps, args.lr,
                                                  max(3, args.cpu_steps))
-    if rank == 0:
-        emit(out)
     if dist is not None:
         dist.destroy_process_group()
+    return out if rank == 0 else None
 
 
 METRIC_SMALL = {"c2": "graphs/sec (fwd+bwd) U2GNN-Sup IMDBBINARY k=8 T=4 MI355X",
@@ -546,6 +560,10 @@ METRIC_SMALL = {"c2": "graphs/sec (fwd+bwd) U2GNN-Sup IMDBBINARY k=8 T=4 MI355X"
 
 
 def main_small(args):
+    emit(run_small(args))
+
+
+def run_small(args):
     """BASELINE.json configs[1] (IMDBBINARY supervised, bs 4, k 8, T 4, ff 1024) and configs[2] (PTC
     unsupervised + SampledSoftmax 512, bs 4, k 4, T 2, ff 1024) on the real datasets of the image:
     N ~ 80-100 nodes per batch, so a step is latency-bound; it is replayed as one HIP graph per
@@ -651,7 +669,7 @@ def main_small(args):
                       "precision": args.precision, "hip_graph": graph},
            "final_loss": round(loss, 5), "host_issue_ms_per_step": round(1e3 * t_issue / args.steps, 3),
            "roofline": None, "cpu_baseline": cpu}
-    emit(out)
+    return out
 
 
 _JSON_OUT = None
@@ -862,6 +880,20 @@ def main():
         out["pipeline"] = pipeline_rate(store, trainer, args, dev, value)
     if rank == 0 and world == 1 and args.cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(host[args.warmup % nb], sd0, args, d, C)
+    if rank == 0 and world == 1 and args.configs and args.attention == "nodes" and not args.force_dist:
+        # BASELINE configs[4], [1], [2] timed in this run too (driver-timed C5 / C2 / C3): each
+        # object is the line its own --workload run prints
+        import copy
+        del trainer, model, batches
+        torch.cuda.empty_cache()
+        for wl in ("c5", "c2", "c3"):
+            a = copy.copy(args)
+            a.workload, a.steps, a.warmup, a.graph = wl, args.config_steps, 5, -1
+            t0 = time.perf_counter()
+            sub = run_c5(a) if wl == "c5" else run_small(a)
+            sub["run_s"] = round(time.perf_counter() - t0, 1)
+            out[wl] = sub
+            torch.cuda.empty_cache()
     if rank == 0:
         emit(out)
     if dist is not None:

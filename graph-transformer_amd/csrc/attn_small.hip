@@ -1,0 +1,537 @@
+// Node-axis attention for small feature widths (d <= 32: the U2GNN-UnSup encoders, REDDIT-M5K d = 4 (C5),
+// PTC d = 19 (C3), MUTAG d = 7 (C1)) -- a3.2 of SURVEY.md §8 and its backward
+// (torch MHA inside pytorch_U2GNN_UnSup.py:37-40,57 / pytorch_U2GNN_Sup.py:19-21,35).
+//
+// At d <= 32 the matrix-core path pads every attention product to dp = 64 columns (94 % padding at d = 4)
+// and still moves the N x N score and probability images through HBM several times per layer.  Here the
+// N^2 work runs in exact fp32 on the vector ALUs and nothing N x N is ever stored (flash-style), in four
+// launches per layer, each writing its final outputs (no partial buffers, no combine launches):
+//   pack     Q, K, V out of the strided in-projection image into the compact context (layouts below);
+//   forward  SA_SPL = 2 waves per query row, the 64 lanes of each splitting its half of every LDS key tile
+//            (two consecutive keys per lane per 128-key round): scores, an online max / sum-exp rescale per
+//            8 keys, the dropout hash (one finaliser per key pair) and o += e v; the lanes merge by a
+//            butterfly, the two waves through LDS; lane c writes column c of O = sum_kept e v / (L (1 - p))
+//            and lane 0 the row statistics (M, 1/L) the backward recomputes P = exp2(s log2e - M) / L from;
+//   dQ       the same row walk: dS_ij = P_ij (keep dO_i.V_j / (1 - p) - delta_i), dQ_i += dS_ij K_j; each
+//            row also writes its compact record (Q, dO, M, 1/L, delta, row key) for
+//   dK, dV   SA_SPL waves per key row, the lanes splitting LDS tiles of query records:
+//            dV_j += Pd_ij dO_i, dK_j += dS_ij Q_i.
+// Softmax semantics are the reference's: softmax over the keys, THEN dropout(p) on the probabilities with
+// 1/(1-p) scaling, THEN the product with V (torch SDPA math path); delta_i = rowsum(dO_i * O_i) as for the
+// matrix-core path.  The keep decisions are u2gnn_keep(seed, i, j, p), the hash every dropout site uses.
+// Deterministic: fixed key / query partition and butterfly merges in a fixed order.
+#include <cmath>
+#include <cstring>
+
+#include "u2gnn_common.h"
+
+namespace {
+
+constexpr int SA_WAVES = 8;    // rows (forward, dQ) or key rows (dK / dV) per 512-thread workgroup
+constexpr int SA_NT = 64 * SA_WAVES;
+// keys (forward, dQ) / queries (dK, dV) staged in LDS per tile: 32 KB of K and V (16-34 KB of query
+// records): two to four workgroups per CU
+template <int DM> constexpr int sa_kt_f() { return 4096 / DM > 256 ? 4096 / DM / 256 * 256 : 256; }   // 128-key rounds per wave
+template <int DM> constexpr int sa_kt_b() { return 2048 / DM > 128 ? 2048 / DM / 128 * 128 : 128; }   // 64-query rounds per wave
+constexpr float SA_LOG2E = 1.4426950408889634f;
+// waves per SIMD the register budget is sized for: 4 (128 VGPRs) up to DM = 16, 2 (256) beyond, where the row's
+// q, o / dq / dk, dv arrays alone take 2-3 DM registers (the 128 cap spilled them to scratch)
+template <int DM> constexpr int sa_min_waves() { return DM <= 16 ? 4 : 2; }
+
+// Layouts (all fp32; DM = d rounded up to a multiple of 4 up to 24, else 32):
+//   ctx (the forward's saved context, u2gnn_attn_small_ctx_floats):  st [Np][2] = (M in log2 units, 1/L) |
+//        qc [Np][DM] (Q, pre-scaled) | kvc [Np][2 DM] (K then V of a row, adjacent); rows >= N all zero.
+//        A pack launch copies Q / K / V out of the strided [Np][3 dp] in-projection image once: every
+//        workgroup then stages the keys from 2 DM contiguous floats per key instead of two 16-byte pieces
+//        of two far-apart cache lines per key (the TA / TCP cost the strided sweep paid, once per line).
+//   ws (the backward's scratch, u2gnn_attn_small_ws_floats): rq [Np][RQ], RQ = 2 DM + 4:
+//        Q[DM], dO[DM], M, 1/L, delta, row key -- written by the dQ launch for its own rows, staged by dK / dV.
+struct SaP {
+    const float *qkv;   // pack: [Np][ld]: Q (pre-scaled by 1/sqrt(d)) at column 0, K at dp, V at 2 dp
+    int64_t ld;
+    int32_t dp, d, N, Np;
+    float p;
+    uint64_t seed;
+    const uint64_t *epoch;
+    float *ctx;         // st | qc | kvc
+    const float *dO;    // backward: [Np][ld_do]
+    int64_t ld_do;
+    const float *delta; // backward: [Np]
+    float *rq;          // backward: [Np][RQ]
+    float *out;         // forward: O; backward: dQKV
+    int64_t ld_out;
+    float q_scale;
+};
+
+template <int DM> __host__ __device__ constexpr int sa_rq() { return 2 * DM + 4; }
+__host__ __device__ inline float *sa_st(float *ctx) { return ctx; }
+template <int DM> __host__ __device__ inline float *sa_qc(float *ctx, int64_t Np) { return ctx + 2 * Np; }
+template <int DM> __host__ __device__ inline float *sa_kvc(float *ctx, int64_t Np) { return ctx + (2 + DM) * Np; }
+
+template <int DM>
+__device__ __forceinline__ void load_row(const float *src, float (&x)[DM]) {
+#pragma unroll
+    for (int c = 0; c < DM; c += 4) {
+        const float4 v = *reinterpret_cast<const float4 *>(src + c);
+        x[c] = v.x, x[c + 1] = v.y, x[c + 2] = v.z, x[c + 3] = v.w;
+    }
+}
+
+template <int DM>
+__device__ __forceinline__ void store_row(float *dst, const float (&x)[DM]) {
+#pragma unroll
+    for (int c = 0; c < DM; c += 4) *reinterpret_cast<float4 *>(dst + c) = make_float4(x[c], x[c + 1], x[c + 2], x[c + 3]);
+}
+
+template <int DM>
+__device__ __forceinline__ float dot_lds(const float (&x)[DM], const float *y) {
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < DM; c += 4) {
+        const float4 v = *reinterpret_cast<const float4 *>(y + c);
+        s = fmaf(x[c], v.x, s);
+        s = fmaf(x[c + 1], v.y, s);
+        s = fmaf(x[c + 2], v.z, s);
+        s = fmaf(x[c + 3], v.w, s);
+    }
+    return s;
+}
+
+// lane c of a wave writes column c (< width) of a row: x[c] for c < d, 0 beyond (x is the same in every lane)
+template <int DM>
+__device__ __forceinline__ float lane_col(const float (&x)[DM], int c) {
+    float v = 0.f;
+#pragma unroll
+    for (int k = 0; k < DM; ++k) v = c == k ? x[k] : v;
+    return v;
+}
+
+// Work split inside a 512-thread workgroup: SA_RB rows (forward, dQ: query rows; dK / dV: key rows), each
+// taken by SA_SPL waves that split the tile between them (wave s: the s-th part), lanes splitting each part;
+// a row's partial results merge across its lanes (butterfly) and then across its waves (LDS).
+constexpr int SA_SPL = 2, SA_RB = SA_WAVES / SA_SPL;
+
+// stage records [t0, t0 + KT) of a compact [Np][W] array (W = sum of the column widths WA + WB + WC, each a
+// multiple of 4) into the LDS arrays a [KT][WA], b [KT][WB], c [KT][WC]; records at or past Np are zeros
+template <int KT, int WA, int WB, int WC>
+__device__ __forceinline__ void stage_rec(const float *src, int t0, int Np, float (*a)[WA], float (*b)[WB],
+                                          float *c) {
+    constexpr int W4 = (WA + WB + WC) / 4, NE = KT * W4;
+    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int e = threadIdx.x; e < NE; e += SA_NT) {
+        const int t = e / W4, k = 4 * (e % W4);
+        float4 v = z;   // (a branch, not "cond ? *p : z": that selects a pointer to a private copy of z)
+        if (t0 + t < Np) v = *reinterpret_cast<const float4 *>(src + (int64_t)t0 * (4 * W4) + 4 * (int64_t)e);
+        if (k < WA) *reinterpret_cast<float4 *>(&a[t][k]) = v;
+        else if (k < WA + WB) *reinterpret_cast<float4 *>(&b[t][k - WA]) = v;
+        else *reinterpret_cast<float4 *>(c + t * WC + k - WA - WB) = v;
+    }
+}
+
+// ---- pack: Q, K, V rows of the strided image -> qc, kvc (rows >= N zero) ---------------------------------
+template <int DM>
+__global__ void __launch_bounds__(256) sa_pack_kernel(SaP P) {
+    constexpr int C4 = DM / 4;
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= (int64_t)P.Np * 3 * C4) return;
+    const int r = (int)(e / (3 * C4)), bc = (int)(e % (3 * C4)), b = bc / C4, c = 4 * (bc % C4);
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (r < P.N) v = *reinterpret_cast<const float4 *>(P.qkv + (int64_t)r * P.ld + (int64_t)b * P.dp + c);
+    float *dst = b == 0 ? sa_qc<DM>(P.ctx, P.Np) + (int64_t)r * DM + c
+                        : sa_kvc<DM>(P.ctx, P.Np) + (int64_t)r * 2 * DM + (b - 1) * DM + c;
+    *reinterpret_cast<float4 *>(dst) = v;
+}
+
+// ---- forward: one query row per SA_SPL waves -------------------------------------------------------------
+template <int DM>
+__global__ void __launch_bounds__(SA_NT, sa_min_waves<DM>()) sa_fwd_kernel(SaP P) {
+    constexpr int SA_KT = sa_kt_f<DM>();
+    constexpr int PART = SA_KT / SA_SPL, NP = PART / 128;   // keys per wave per tile; key pairs per lane
+    static_assert(NP >= 1 && PART % 128 == 0, "a wave's part of the key tile: whole 128-key rounds");
+    __shared__ __attribute__((aligned(16))) float ks[SA_KT][DM];
+    __shared__ __attribute__((aligned(16))) float vs[SA_KT][DM];
+    __shared__ float xw[SA_RB][SA_SPL][2 + DM];
+    const uint64_t seed = u2gnn_seed(P.seed, P.epoch);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, rw = w % SA_RB, sp = w / SA_RB;
+    const int i = blockIdx.x * SA_RB + rw;
+    const bool live = i < P.N;
+    const float *kvc = sa_kvc<DM>(P.ctx, P.Np);
+    float q[DM], o[DM];
+#pragma unroll
+    for (int c = 0; c < DM; ++c) q[c] = o[c] = 0.f;
+    if (live) load_row<DM>(sa_qc<DM>(P.ctx, P.Np) + (int64_t)i * DM, q);
+    const bool drop = P.p > 0.f;
+    const uint32_t thr = u2gnn_keep_thr(P.p), rk = u2gnn_row_key(seed, (uint32_t)i);
+    float m = -INFINITY, l = 0.f;
+    for (int t0 = 0; t0 < P.N; t0 += SA_KT) {
+        __syncthreads();
+        stage_rec<SA_KT, DM, DM, 0>(kvc, t0, P.Np, ks, vs, nullptr);
+        __syncthreads();
+        if (!live) continue;
+        // this wave's keys of the tile: pairs (t0 + sp PART + 128 h + 2 lane, +1); four pairs per rescale
+#pragma unroll 1
+        for (int h0 = 0; h0 < NP; h0 += 4) {
+            float s[8];
+            float cm = -INFINITY;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int t = sp * PART + 128 * (h0 + u / 2) + 2 * lane + (u & 1);
+                const float x = dot_lds<DM>(q, ks[t]) * SA_LOG2E;   // rows past N are zeros: finite
+                s[u] = (h0 + u / 2 < NP && t0 + t < P.N) ? x : -INFINITY;
+                cm = fmaxf(cm, s[u]);
+            }
+            if (cm == -INFINITY) continue;   // none of this lane's keys in the chunk
+            const float mn = fmaxf(m, cm);
+            const float sc = exp2f(m - mn);  // m = -inf: 0
+            l *= sc;
+#pragma unroll
+            for (int c = 0; c < DM; ++c) o[c] *= sc;
+#pragma unroll
+            for (int u = 0; u < 8; u += 2) {
+                const int t = sp * PART + 128 * (h0 + u / 2) + 2 * lane;
+                bool k0 = true, k1 = true;
+                if (drop) {
+                    const uint32_t hh = u2gnn_pair_hash(rk, (uint32_t)(t0 + t) >> 1);
+                    k0 = u2gnn_keep_lo(hh, thr), k1 = u2gnn_keep_hi(hh, thr);
+                }
+                const float e0 = exp2f(s[u] - mn), e1 = exp2f(s[u + 1] - mn);   // 0 past N
+                l += e0 + e1;
+                const float a0 = k0 ? e0 : 0.f, a1 = k1 ? e1 : 0.f;
+                const int tt = h0 + u / 2 < NP ? t : 0;   // (a0 = a1 = 0 there)
+#pragma unroll
+                for (int c = 0; c < DM; ++c) o[c] = fmaf(a1, vs[tt + 1][c], fmaf(a0, vs[tt][c], o[c]));
+            }
+            m = mn;
+        }
+    }
+    // butterfly merge of the 64 lanes' (m, l, o): every lane ends with the same values
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const float m2 = __shfl_xor(m, off, 64), l2 = __shfl_xor(l, off, 64);
+        const float M = fmaxf(m, m2);
+        const float f1 = m == -INFINITY ? 0.f : exp2f(m - M), f2 = m2 == -INFINITY ? 0.f : exp2f(m2 - M);
+        l = l * f1 + l2 * f2;
+#pragma unroll
+        for (int c = 0; c < DM; ++c) {
+            const float o2 = __shfl_xor(o[c], off, 64);
+            o[c] = o[c] * f1 + o2 * f2;
+        }
+        m = M;
+    }
+    // then the row's SA_SPL waves, in wave order
+    if (lane == 0) {
+        xw[rw][sp][0] = m;
+        xw[rw][sp][1] = l;
+#pragma unroll
+        for (int c = 0; c < DM; ++c) xw[rw][sp][2 + c] = o[c];
+    }
+    __syncthreads();
+    if (sp != 0 || i >= P.Np) return;
+    float M = xw[rw][0][0];
+#pragma unroll
+    for (int x = 1; x < SA_SPL; ++x) M = fmaxf(M, xw[rw][x][0]);
+    float L = 0.f;
+#pragma unroll
+    for (int c = 0; c < DM; ++c) o[c] = 0.f;
+    if (M != -INFINITY) {
+#pragma unroll
+        for (int x = 0; x < SA_SPL; ++x) {
+            const float f = xw[rw][x][0] == -INFINITY ? 0.f : exp2f(xw[rw][x][0] - M);
+            L = fmaf(xw[rw][x][1], f, L);
+#pragma unroll
+            for (int c = 0; c < DM; ++c) o[c] = fmaf(xw[rw][x][2 + c], f, o[c]);
+        }
+    }
+    const float invL = live && L > 0.f ? 1.f / L : 0.f;
+    const float s1p = drop ? 1.f / (1.f - P.p) : 1.f;
+    float *orow = P.out + (int64_t)i * P.ld_out;
+    for (int c = lane; c < P.dp; c += 64) orow[c] = (live && c < P.d) ? lane_col<DM>(o, c) * invL * s1p : 0.f;
+    if (lane == 0) {
+        float *st = sa_st(P.ctx);
+        st[2 * (int64_t)i] = live ? M : 0.f;
+        st[2 * (int64_t)i + 1] = invL;
+    }
+}
+
+// ---- backward dQ: one query row per SA_SPL waves; also the row's record for dK / dV -----------------------
+template <int DM>
+__global__ void __launch_bounds__(SA_NT, sa_min_waves<DM>()) sa_bwd_q_kernel(SaP P) {
+    constexpr int SA_KT = sa_kt_f<DM>();
+    constexpr int PART = SA_KT / SA_SPL, NP = PART / 128;
+    static_assert(NP >= 1 && PART % 128 == 0, "a wave's part of the key tile: whole 128-key rounds");
+    __shared__ __attribute__((aligned(16))) float ks[SA_KT][DM];
+    __shared__ __attribute__((aligned(16))) float vs[SA_KT][DM];
+    __shared__ float xw[SA_RB][SA_SPL][DM];
+    const uint64_t seed = u2gnn_seed(P.seed, P.epoch);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, rw = w % SA_RB, sp = w / SA_RB;
+    const int i = blockIdx.x * SA_RB + rw;
+    const bool live = i < P.N;
+    const float *st = sa_st(P.ctx);
+    float q[DM], g[DM], dq[DM];
+    float M = 0.f, iL = 0.f, dl = 0.f;
+#pragma unroll
+    for (int c = 0; c < DM; ++c) q[c] = g[c] = dq[c] = 0.f;
+    if (live) {
+        load_row<DM>(sa_qc<DM>(P.ctx, P.Np) + (int64_t)i * DM, q);
+        load_row<DM>(P.dO + (int64_t)i * P.ld_do, g);
+        M = st[2 * (int64_t)i], iL = st[2 * (int64_t)i + 1], dl = P.delta[i];
+    }
+    const bool drop = P.p > 0.f;
+    const float s1p = drop ? 1.f / (1.f - P.p) : 1.f;
+    const uint32_t thr = u2gnn_keep_thr(P.p), rk = u2gnn_row_key(seed, (uint32_t)i);
+    if (sp == 0 && lane == 0 && i < P.Np) {   // the row's record (iL = 0 past N: the dK / dV sweep skips it)
+        float *r = P.rq + (int64_t)i * sa_rq<DM>();
+        store_row<DM>(r, q);
+        store_row<DM>(r + DM, g);
+        *reinterpret_cast<float4 *>(r + 2 * DM) = make_float4(M, iL, dl, __uint_as_float(rk));
+    }
+    const float *kvc = sa_kvc<DM>(P.ctx, P.Np);
+    for (int t0 = 0; t0 < P.N; t0 += SA_KT) {
+        __syncthreads();
+        stage_rec<SA_KT, DM, DM, 0>(kvc, t0, P.Np, ks, vs, nullptr);
+        __syncthreads();
+        if (!live) continue;
+#pragma unroll 2
+        for (int h = 0; h < NP; ++h) {
+            const int t = sp * PART + 128 * h + 2 * lane;
+            bool kp0 = true, kp1 = true;
+            if (drop) {
+                const uint32_t hh = u2gnn_pair_hash(rk, (uint32_t)(t0 + t) >> 1);
+                kp0 = u2gnn_keep_lo(hh, thr), kp1 = u2gnn_keep_hi(hh, thr);
+            }
+#pragma unroll
+            for (int x = 0; x < 2; ++x) {
+                // rows past N are zeros in LDS: their pr is masked to 0 below
+                const float pr = t0 + t + x < P.N ? exp2f(dot_lds<DM>(q, ks[t + x]) * SA_LOG2E - M) * iL : 0.f;
+                const float ds = pr * (((x ? kp1 : kp0) ? dot_lds<DM>(g, vs[t + x]) * s1p : 0.f) - dl);
+#pragma unroll
+                for (int c = 0; c < DM; ++c) dq[c] = fmaf(ds, ks[t + x][c], dq[c]);
+            }
+        }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1)
+#pragma unroll
+        for (int c = 0; c < DM; ++c) dq[c] += __shfl_xor(dq[c], off, 64);
+    if (lane == 0)
+#pragma unroll
+        for (int c = 0; c < DM; ++c) xw[rw][sp][c] = dq[c];
+    __syncthreads();
+    if (sp != 0 || i >= P.Np) return;
+#pragma unroll
+    for (int c = 0; c < DM; ++c) {
+        float t = xw[rw][0][c];
+#pragma unroll
+        for (int x = 1; x < SA_SPL; ++x) t += xw[rw][x][c];
+        dq[c] = t;
+    }
+    float *row = P.out + (int64_t)i * P.ld_out;   // the Q block of dQKV
+    for (int c = lane; c < P.dp; c += 64) row[c] = (live && c < P.d) ? lane_col<DM>(dq, c) * P.q_scale : 0.f;
+}
+
+// ---- backward dK, dV: SA_SPL waves per KP key rows, the waves and lanes splitting the queries -------------
+// KP = 2 for DM <= 8: a wave takes the key pair (2j', 2j'+1), so one dropout hash per (query, pair) gives both
+// keep bits and each staged query record is read once for both keys
+#ifndef SA_KP_SMALL
+#define SA_KP_SMALL 2   // (A/B: -DSA_KP_SMALL=1 builds one key row per wave for every width)
+#endif
+template <int DM> constexpr int sa_kp() { return DM <= 8 ? SA_KP_SMALL : 1; }
+
+template <int DM>
+__global__ void __launch_bounds__(SA_NT, sa_min_waves<DM>()) sa_bwd_kv_kernel(SaP P) {
+    constexpr int SA_KT = sa_kt_b<DM>(), KP = sa_kp<DM>();
+    constexpr int PART = SA_KT / SA_SPL, NU = PART / 64;   // queries per lane per tile
+    static_assert(NU >= 1 && PART % 64 == 0, "a wave's part of the query tile: whole 64-query rounds");
+    __shared__ __attribute__((aligned(16))) float qs[SA_KT][DM];
+    __shared__ __attribute__((aligned(16))) float gs[SA_KT][DM];   // dO rows
+    __shared__ __attribute__((aligned(16))) float rs[SA_KT][4];    // M, 1/L, delta, row key (bits)
+    __shared__ float xw[SA_RB][SA_SPL][2 * KP * DM];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, rw = w % SA_RB, sp = w / SA_RB;
+    const int j0 = (blockIdx.x * SA_RB + rw) * KP;
+    const bool live = j0 < P.N;
+    float k[KP][DM], v[KP][DM], dk[KP][DM], dv[KP][DM];
+#pragma unroll
+    for (int x = 0; x < KP; ++x)
+#pragma unroll
+        for (int c = 0; c < DM; ++c) k[x][c] = v[x][c] = dk[x][c] = dv[x][c] = 0.f;
+#pragma unroll
+    for (int x = 0; x < KP; ++x)
+        if (j0 + x < P.N) {
+            const float *kv = sa_kvc<DM>(P.ctx, P.Np) + (int64_t)(j0 + x) * 2 * DM;
+            load_row<DM>(kv, k[x]);
+            load_row<DM>(kv + DM, v[x]);
+        }
+    const bool drop = P.p > 0.f;
+    const float s1p = drop ? 1.f / (1.f - P.p) : 1.f;
+    const uint32_t thr = u2gnn_keep_thr(P.p), jc = (uint32_t)j0 >> 1;
+    const bool odd = j0 & 1;   // (KP = 2: j0 even)
+    for (int t0 = 0; t0 < P.N; t0 += SA_KT) {
+        __syncthreads();
+        stage_rec<SA_KT, DM, DM, 4>(P.rq, t0, P.Np, qs, gs, &rs[0][0]);
+        __syncthreads();
+        if (!live) continue;
+#pragma unroll 2
+        for (int u = 0; u < NU; ++u) {
+            const int t = sp * PART + 64 * u + lane;
+            bool kp[KP];
+            if (drop) {
+                const uint32_t hh = u2gnn_pair_hash(__float_as_uint(rs[t][3]), jc);
+                if (KP == 2) kp[0] = u2gnn_keep_lo(hh, thr), kp[KP - 1] = u2gnn_keep_hi(hh, thr);
+                else kp[0] = odd ? u2gnn_keep_hi(hh, thr) : u2gnn_keep_lo(hh, thr);
+            } else {
+#pragma unroll
+                for (int x = 0; x < KP; ++x) kp[x] = true;
+            }
+            float qt[DM], gt[DM];
+            load_row<DM>(qs[t], qt);
+            load_row<DM>(gs[t], gt);
+            const float4 r = *reinterpret_cast<const float4 *>(rs[t]);   // M, 1/L, delta, key
+#pragma unroll
+            for (int x = 0; x < KP; ++x) {
+                // 1/L = 0 for queries past N (their records, and the zero fill past Np): pr = 0
+                float sq = 0.f, sg = 0.f;
+#pragma unroll
+                for (int c = 0; c < DM; ++c) sq = fmaf(k[x][c], qt[c], sq), sg = fmaf(v[x][c], gt[c], sg);
+                const float pr = exp2f(sq * SA_LOG2E - r.x) * r.y;
+                const float ds = pr * ((kp[x] ? sg * s1p : 0.f) - r.z);
+                const float pd = kp[x] ? pr * s1p : 0.f;
+#pragma unroll
+                for (int c = 0; c < DM; ++c) {
+                    dv[x][c] = fmaf(pd, gt[c], dv[x][c]);
+                    dk[x][c] = fmaf(ds, qt[c], dk[x][c]);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1)
+#pragma unroll
+        for (int x = 0; x < KP; ++x)
+#pragma unroll
+            for (int c = 0; c < DM; ++c) {
+                dk[x][c] += __shfl_xor(dk[x][c], off, 64);
+                dv[x][c] += __shfl_xor(dv[x][c], off, 64);
+            }
+    if (lane == 0)
+#pragma unroll
+        for (int x = 0; x < KP; ++x)
+#pragma unroll
+            for (int c = 0; c < DM; ++c) xw[rw][sp][2 * x * DM + c] = dk[x][c], xw[rw][sp][(2 * x + 1) * DM + c] = dv[x][c];
+    __syncthreads();
+    if (sp != 0) return;
+#pragma unroll
+    for (int x = 0; x < KP; ++x) {
+        const int j = j0 + x;
+        if (j >= P.Np) break;
+#pragma unroll
+        for (int c = 0; c < DM; ++c) {
+            float a = xw[rw][0][2 * x * DM + c], b = xw[rw][0][(2 * x + 1) * DM + c];
+#pragma unroll
+            for (int y = 1; y < SA_SPL; ++y) a += xw[rw][y][2 * x * DM + c], b += xw[rw][y][(2 * x + 1) * DM + c];
+            dk[x][c] = a, dv[x][c] = b;
+        }
+        float *row = P.out + (int64_t)j * P.ld_out;
+        for (int c = lane; c < P.dp; c += 64) {
+            const bool col = j < P.N && c < P.d;
+            row[P.dp + c] = col ? lane_col<DM>(dk[x], c) : 0.f;
+            row[2 * P.dp + c] = col ? lane_col<DM>(dv[x], c) : 0.f;
+        }
+    }
+}
+
+// the register / LDS width of a row: d rounded up to a multiple of 4 up to 24 (PTC d = 19 -> 20), else 32
+int sa_dm(int64_t d) { return d < 1 ? 0 : d <= 24 ? (int)((d + 3) / 4 * 4) : d <= 32 ? 32 : 0; }
+
+bool al16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+int sa_check(int64_t dp, int64_t d, int64_t N, int64_t Np, float p, const float *ctx, int64_t ctx_floats) {
+    if (d < 1 || !sa_dm(d) || dp < 64 || (dp & 63) || N < 1 || Np < N || (Np & 3) || p < 0.f || !(p < 1.f) ||
+        N > (int64_t)1 << 30 || !ctx || ctx_floats < Np * (2 + 3 * (int64_t)sa_dm(d)))
+        return U2GNN_E_ARG;
+    if (!al16(ctx)) return U2GNN_E_ALIGN;
+    return U2GNN_OK;
+}
+
+SaP sa_params(int64_t dp, int64_t d, int64_t N, int64_t Np, float p, uint64_t seed, float *ctx) {
+    SaP P;
+    std::memset(&P, 0, sizeof(P));
+    P.dp = (int32_t)dp, P.d = (int32_t)d, P.N = (int32_t)N, P.Np = (int32_t)Np;
+    P.p = p, P.seed = seed, P.epoch = u2gnn_g_epoch, P.ctx = ctx;
+    return P;
+}
+
+template <int DM>
+int sa_fwd_launch(const SaP &P, hipStream_t st) {
+    const int64_t nt = (int64_t)P.Np * 3 * (DM / 4);
+    hipLaunchKernelGGL(sa_pack_kernel<DM>, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, st, P);
+    hipLaunchKernelGGL(sa_fwd_kernel<DM>, dim3((unsigned)((P.Np + SA_RB - 1) / SA_RB)), dim3(SA_NT), 0, st, P);
+    return u2gnn_launch_status();
+}
+
+template <int DM>
+int sa_bwd_launch(const SaP &P, hipStream_t st) {
+    const dim3 grid((unsigned)((P.Np + SA_RB - 1) / SA_RB));
+    hipLaunchKernelGGL(sa_bwd_q_kernel<DM>, grid, dim3(SA_NT), 0, st, P);
+    constexpr int KR = SA_RB * sa_kp<DM>();   // key rows per workgroup
+    hipLaunchKernelGGL(sa_bwd_kv_kernel<DM>, dim3((unsigned)((P.Np + KR - 1) / KR)), dim3(SA_NT), 0, st, P);
+    return u2gnn_launch_status();
+}
+
+}  // namespace
+
+extern "C" {
+
+int64_t u2gnn_attn_small_ctx_floats(int64_t rows_pad, int64_t d) {
+    if (!sa_dm(d) || rows_pad < 1) return -1;
+    return rows_pad * (2 + 3 * (int64_t)sa_dm(d));
+}
+
+int64_t u2gnn_attn_small_ws_floats(int64_t n_valid, int64_t rows_pad, int64_t d) {
+    if (!sa_dm(d) || n_valid < 1 || rows_pad < n_valid) return -1;
+    return rows_pad * (2 * (int64_t)sa_dm(d) + 4);
+}
+
+int u2gnn_attn_small_fwd(const float *QKV, int64_t ld_qkv, int64_t dp, int64_t d, int64_t N, int64_t Np, float p,
+                         uint64_t seed, float *O, int64_t ldo, float *ctx, int64_t ctx_floats, void *stream) {
+    int rc = sa_check(dp, d, N, Np, p, ctx, ctx_floats);
+    if (rc != U2GNN_OK) return rc;
+    if (!QKV || ld_qkv < 3 * dp || !O || ldo < dp) return U2GNN_E_ARG;
+    if (!al16(QKV) || (ld_qkv & 3)) return U2GNN_E_ALIGN;
+    SaP P = sa_params(dp, d, N, Np, p, seed, ctx);
+    P.qkv = QKV, P.ld = ld_qkv, P.out = O, P.ld_out = ldo;
+    hipStream_t st = u2gnn_stream(stream);
+    switch (sa_dm(d)) {
+        case 4: return sa_fwd_launch<4>(P, st);
+        case 8: return sa_fwd_launch<8>(P, st);
+        case 12: return sa_fwd_launch<12>(P, st);
+        case 16: return sa_fwd_launch<16>(P, st);
+        case 20: return sa_fwd_launch<20>(P, st);
+        case 24: return sa_fwd_launch<24>(P, st);
+        default: return sa_fwd_launch<32>(P, st);
+    }
+}
+
+int u2gnn_attn_small_bwd(const float *ctx, int64_t ctx_floats, int64_t dp, int64_t d, int64_t N, int64_t Np, float p,
+                         uint64_t seed, const float *dO, int64_t ld_do, const float *delta, float q_scale,
+                         float *dQKV, int64_t ld_dqkv, float *ws, int64_t ws_floats, void *stream) {
+    int rc = sa_check(dp, d, N, Np, p, ctx, ctx_floats);
+    if (rc != U2GNN_OK) return rc;
+    if (!dO || !delta || !dQKV || ld_dqkv < 3 * dp || ld_do < dp || !ws || ws_floats < u2gnn_attn_small_ws_floats(N, Np, d))
+        return U2GNN_E_ARG;
+    if (!al16(dO) || (ld_do & 3) || !al16(ws)) return U2GNN_E_ALIGN;
+    SaP P = sa_params(dp, d, N, Np, p, seed, const_cast<float *>(ctx));   // read-only in the backward
+    P.dO = dO, P.ld_do = ld_do, P.delta = delta, P.q_scale = q_scale;
+    P.rq = ws, P.out = dQKV, P.ld_out = ld_dqkv;
+    hipStream_t st = u2gnn_stream(stream);
+    switch (sa_dm(d)) {
+        case 4: return sa_bwd_launch<4>(P, st);
+        case 8: return sa_bwd_launch<8>(P, st);
+        case 12: return sa_bwd_launch<12>(P, st);
+        case 16: return sa_bwd_launch<16>(P, st);
+        case 20: return sa_bwd_launch<20>(P, st);
+        case 24: return sa_bwd_launch<24>(P, st);
+        default: return sa_bwd_launch<32>(P, st);
+    }
+}
+
+}  // extern "C"

@@ -23,6 +23,7 @@
 #include <map>
 #include <mutex>
 #include <algorithm>
+#include <atomic>
 #include <vector>
 
 #include "u2gnn_hip.h"
@@ -101,19 +102,24 @@ struct Ctx {   // tensors saved by the forward for the backward
     // Pd: with dropout the signed probability image (P/(1-p) where kept, -P where dropped), else P
     float *QKV, *Pd, *O, *Z1, *X1, *mean1, *rstd1, *Hd, *Z2, *mean2, *rstd2;
     float *Psave;   // window mode: [N/W, W, W] probabilities
+    float *stats;   // small-width node attention (d <= 32): its context (row statistics + compact Q, K, V)
 };
+
+// node attention for d <= 32 on the vector ALUs (u2gnn_attn_small_*, attn_small.hip): every precision, no
+// N x N image (engine.small_attn mirrors the rule)
+bool small_attn(const Dims &D) { return !D.window && D.d <= 32; }
 
 Ctx carve_ctx(Arena &A, const Dims &D, bool drop) {
     Ctx c;
     c.QKV = A.take<float>(D.Np * 3 * D.dp);
     (void)drop;
-    if (D.window) {
-        c.Pd = nullptr;
+    c.Pd = c.Psave = c.stats = nullptr;
+    if (D.window)
         c.Psave = A.take<float>(D.N * D.window);
-    } else {
-        c.Psave = nullptr;
+    else if (small_attn(D))
+        c.stats = A.take<float>(u2gnn_attn_small_ctx_floats(D.Np, D.d));
+    else
         c.Pd = A.take<float>(D.Np * D.Np);
-    }
     c.O = A.take<float>(D.Np * D.dp);
     c.Z1 = A.take<float>(D.Np * D.dp);
     c.X1 = A.take<float>(D.Np * D.dp);
@@ -126,15 +132,21 @@ Ctx carve_ctx(Arena &A, const Dims &D, bool drop) {
     return c;
 }
 
-// live launch timing of one role (u2gnn_probe_arm / u2gnn_probe_collect)
+// live launch timing of one role (u2gnn_probe_arm / u2gnn_probe_collect): a diagnostic of the bench, the one
+// piece of process-wide state of the executor.  Every access holds g_probe_mu (arm, mark and collect may come
+// from different host threads); an unarmed probe costs one relaxed atomic load per mark.
 struct Probe {
     int role = 0, cap = 0, n = 0;
     hipEvent_t *ev = nullptr;   // [2 * cap]: start, end
 };
 Probe g_probe;
+std::mutex g_probe_mu;
+std::atomic<int> g_probe_role{0};
 
 void probe_mark(int role, bool end, hipStream_t st, bool plan) {
-    if (plan || g_probe.role != role || g_probe.n >= g_probe.cap) return;
+    if (plan || g_probe_role.load(std::memory_order_relaxed) != role) return;
+    std::lock_guard<std::mutex> lk(g_probe_mu);
+    if (g_probe.role != role || g_probe.n >= g_probe.cap) return;
     (void)hipEventRecord(g_probe.ev[2 * g_probe.n + (end ? 1 : 0)], st);
     if (end) ++g_probe.n;
 }
@@ -351,6 +363,9 @@ int bias_grad(Arena &W, const float *dY, int64_t rows, int64_t cols_pad, int64_t
 // kernels' own releases make their stores visible to the other queue's kernels).  The record then stops
 // holding back the next kernel of the recording stream: dO -> dS gap 13 -> 4.7 us, C4 step 2.963 / 2.958 vs
 // 2.987 / 2.978 ms (device-scope release instead: 2.979 / 2.961; profiles/r04/ab_event_fence.txt)
+// SAME-DEVICE ONLY: a pooled event may order only two streams of the device it was drawn for (the pools
+// are per device, the main and side streams of one layer call share that device).  A cross-device or
+// host-visible hand-off must use its own event without hipEventDisableSystemFence.
 constexpr unsigned kForkEventFlags = hipEventDisableTiming | hipEventDisableSystemFence;
 
 hipEvent_t pooled_event() {
@@ -453,7 +468,9 @@ int64_t ffn2_split(bool fuse_ln, int64_t Np, int64_t ffp) {
 // them), then 128x128 (the same per-element sums: same bits; engine.qk_tile mirrors the rule)
 int qk_tile(int64_t Np) { return (Np % 256 == 0 && (Np / 256) * (Np / 128) >= 256) ? 256 : 128; }
 
-bool fused_attn(const Dims &D) { return !D.window && D.prec_fwd != U2GNN_PREC_F32 && D.dp <= 384; }
+bool fused_attn(const Dims &D) {
+    return !D.window && !small_attn(D) && D.prec_fwd != U2GNN_PREC_F32 && D.dp <= 384;
+}
 
 int layer_fwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seeds *s, const float *X, float *X2,
               Arena &CA, Arena &W, bool need_ctx, hipStream_t st) {
@@ -488,6 +505,14 @@ int layer_fwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
         if (!plan)
             U2GNN_TRY(u2gnn_window_attn_fwd(c.QKV, 3 * dp, D.window, (int32_t)dp, c.O, dp, c.Psave, pd, s->attn,
                                             N / D.window, Np, st));
+    } else if (small_attn(D)) {
+        // d <= 32: softmax -> dropout -> P.V flash-style on the vector ALUs, the row statistics saved
+        if (!plan) {
+            probe_mark(U2GNN_ROLE_PV, false, st, plan);
+            U2GNN_TRY(u2gnn_attn_small_fwd(c.QKV, 3 * dp, dp, d, N, Np, pd, s->attn, c.O, dp, c.stats,
+                                           u2gnn_attn_small_ctx_floats(Np, d), st));
+            probe_mark(U2GNN_ROLE_PV, true, st, plan);
+        }
     } else if (fused) {
         // a3.2 as S = Q K^T with the softmax row partials from the GEMM epilogue, then one fused
         // softmax -> dropout -> P.V pass that overwrites S with the signed image (attn_fused.hip)
@@ -656,6 +681,19 @@ int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
         if (!plan)
             U2GNN_TRY(u2gnn_window_attn_bwd(c.QKV, 3 * dp, D.window, (int32_t)dp, dO, dp, c.Psave, pd, s->attn,
                                             q_scale, dQKV, 3 * dp, N / D.window, Np, st));
+    } else if (small_attn(D)) {
+        // d <= 32: dQ, dK, dV with P recomputed from the row statistics (no dS image, no split-K slabs)
+        dQKV = W.take<float>(Np * 3 * dp);
+        float *delta = ln_delta ? delta_ln : W.take<float>(Np);
+        const int64_t wsf = u2gnn_attn_small_ws_floats(N, Np, d);
+        float *sa_ws = W.take<float>(wsf);
+        if (!plan && !ln_delta) U2GNN_TRY(u2gnn_rowdot(dO, dp, c.O, dp, delta, Np, dp, st));
+        if (!plan) {
+            probe_mark(U2GNN_ROLE_DS, false, st, plan);
+            U2GNN_TRY(u2gnn_attn_small_bwd(c.stats, u2gnn_attn_small_ctx_floats(Np, d), dp, d, N, Np, pd, s->attn, dO,
+                                           dp, delta, q_scale, dQKV, 3 * dp, sa_ws, wsf, st));
+            probe_mark(U2GNN_ROLE_DS, true, st, plan);
+        }
     } else {
         dQKV = W.take<float>(Np * 3 * dp);
         const bool dv_side = so != st;   // grouped with dQ / dK on this stream instead: 3.136-3.141 vs 3.068-3.098 ms
@@ -772,6 +810,7 @@ int u2gnn_layer_bwd(const u2gnn_layer_dims *dims, const u2gnn_layer_params *w, c
 }
 
 int u2gnn_probe_arm(int32_t role, int32_t capacity) {
+    std::lock_guard<std::mutex> lk(g_probe_mu);
     if (g_probe.ev) return U2GNN_E_ARG;   // collect the previous probe first
     if (role < U2GNN_ROLE_QK || role > U2GNN_ROLE_DK || capacity < 1 || capacity > (1 << 16)) return U2GNN_E_ARG;
     hipEvent_t *ev = new hipEvent_t[2 * capacity];
@@ -784,12 +823,14 @@ int u2gnn_probe_arm(int32_t role, int32_t capacity) {
         }
     }
     g_probe.ev = ev, g_probe.cap = capacity, g_probe.n = 0, g_probe.role = role;
+    g_probe_role.store(role, std::memory_order_relaxed);
     return U2GNN_OK;
 }
 
 int u2gnn_probe_collect(float *total_ms, int32_t *launches) {
     if (!total_ms || !launches) return U2GNN_E_ARG;
     *total_ms = 0.f, *launches = 0;
+    std::lock_guard<std::mutex> lk(g_probe_mu);
     if (!g_probe.ev) return U2GNN_OK;
     int rc = U2GNN_OK;
     double tot = 0.0;
@@ -804,6 +845,7 @@ int u2gnn_probe_collect(float *total_ms, int32_t *launches) {
     delete[] g_probe.ev;
     *total_ms = (float)tot, *launches = g_probe.n;
     g_probe = Probe();
+    g_probe_role.store(0, std::memory_order_relaxed);
     return rc;
 }
 

@@ -101,7 +101,7 @@ __device__ __forceinline__ void r2s(float *As, float *Bs, int tid, const float4 
 // ------------------------------------------------------------------------------------
 template <int BM, int BN, bool TA, bool TB, int EPI, bool CLAMP>
 __global__ void __launch_bounds__(256) gemm_f32_kernel(GemmP P) {
-    if constexpr (EPI == U2GNN_EPI_BIAS_DROP_RESID || EPI == U2GNN_EPI_BIAS_RELU_DROP || EPI == U2GNN_EPI_ATTN_DS_RECOMP ||
+    if constexpr (EPI == U2GNN_EPI_BIAS_DROP_RESID || EPI == U2GNN_EPI_BIAS_RELU_DROP ||
                   EPI == U2GNN_EPI_BIAS_DROP_RESID_LN)
         P.seed = u2gnn_seed(P.seed, P.epoch);   // graph replay: device-resident seed epoch
     constexpr int BK = 16;
@@ -445,7 +445,7 @@ __device__ __forceinline__ void gemm_bf16_body(const GemmP &P, int tmi, int tni,
 
 template <int BM, int BN, int WM, int WN, int BK, bool TA, bool TB, int EPI, bool SPLIT, bool CLAMP>
 __global__ void __launch_bounds__(64 * WM * WN) gemm_bf16_kernel(GemmP P) {
-    if constexpr (EPI == U2GNN_EPI_BIAS_DROP_RESID || EPI == U2GNN_EPI_BIAS_RELU_DROP || EPI == U2GNN_EPI_ATTN_DS_RECOMP ||
+    if constexpr (EPI == U2GNN_EPI_BIAS_DROP_RESID || EPI == U2GNN_EPI_BIAS_RELU_DROP ||
                   EPI == U2GNN_EPI_BIAS_DROP_RESID_LN)
         P.seed = u2gnn_seed(P.seed, P.epoch);   // graph replay: device-resident seed epoch
     __shared__ __attribute__((aligned(16))) __bf16 smem[bf16_smem_elems<BM, BN, BK, TA, TB>()];

@@ -8,6 +8,10 @@
 // stages the node's W x dp operands in LDS; the W x W scores, softmax, dropout and the products
 // are fp32 VALU work (W <= 32: 17 x 17 x 384 per node is far too small for matrix cores), so
 // the whole attention core of a node is one block with no HBM round trip for scores.
+#include <mutex>
+#include <set>
+#include <utility>
+
 #include "u2gnn_common.h"
 
 #include <algorithm>
@@ -416,6 +420,29 @@ int cu_count() {
     return n;
 }
 
+// Dynamic LDS above 64 KiB must be opted into per kernel AND device (hipFuncSetAttribute acts on the current
+// device): the (device, kernel) pairs already done are kept under a lock, so a second device or thread of the
+// process gets its own opt-in instead of skipping it.
+int lds_optin(const void *kern) {
+    static std::mutex mu;
+    static std::set<std::pair<int, const void *>> done;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return (int)e;
+    std::lock_guard<std::mutex> lk(mu);
+    if (done.count({dev, kern})) return U2GNN_OK;
+    e = hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_LIMIT);
+    if (e != hipSuccess) return (int)e;
+    done.insert({dev, kern});
+    return U2GNN_OK;
+}
+
+#define U2GNN_TRY_WIN(x)                 \
+    do {                                 \
+        const int rc_ = (x);             \
+        if (rc_ != U2GNN_OK) return rc_; \
+    } while (0)
+
 }  // namespace
 
 extern "C" {
@@ -427,13 +454,7 @@ int u2gnn_window_attn_fwd(const float *QKV, int64_t ldq, int32_t W, int32_t dp, 
     if (((uintptr_t)QKV & 15) || ((uintptr_t)O & 15)) return U2GNN_E_ALIGN;
     const size_t lds = fwd_lds(W, dp);
     if (lds > LDS_LIMIT) return U2GNN_E_SHAPE;
-    static bool attr = false;   // dynamic LDS above 64 KiB must be opted into once per kernel
-    if (!attr) {
-        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(window_attn_fwd_kernel),
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_LIMIT);
-        if (e != hipSuccess) return (int)e;
-        attr = true;
-    }
+    U2GNN_TRY_WIN(lds_optin(reinterpret_cast<const void *>(window_attn_fwd_kernel)));
     // persistent prefetching variant for the shapes it is instantiated for (C4 neighbour mode:
     // W = 17, dp = 384 -> 1632 float4 per operand = 7 per thread; win_combine's row blocks: 2 x 9)
     const int64_t elems = (int64_t)W * (dp / 4);   // float4 per operand image
@@ -443,13 +464,7 @@ int u2gnn_window_attn_fwd(const float *QKV, int64_t ldq, int32_t W, int32_t dp, 
     const int rb = (W + nb - 1) / nb;
     if (elems > 256 * 6 && elems <= 256 * 7 && rb == 9 && (W + 8) / 9 == nb) {
         auto kern = window_attn_fwd_pf_kernel<7, 9, kWinPfBlocksPerCu>;
-        static bool attr_pf = false;
-        if (!attr_pf) {
-            const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_LIMIT);
-            if (e != hipSuccess) return (int)e;
-            attr_pf = true;
-        }
+        U2GNN_TRY_WIN(lds_optin(reinterpret_cast<const void *>(kern)));
         const int64_t per_cu = std::min<int64_t>(kWinPfBlocksPerCu, std::max<int64_t>(1, (int64_t)(LDS_LIMIT / lds)));
         const int64_t grid = std::min<int64_t>(n_nodes, per_cu * cu_count());
         hipLaunchKernelGGL(kern, dim3((unsigned)std::max<int64_t>(grid, 1)), dim3(256), lds, u2gnn_stream(stream), QKV,
@@ -472,13 +487,7 @@ int u2gnn_window_attn_bwd(const float *QKV, int64_t ldq, int32_t W, int32_t dp, 
     if (((uintptr_t)QKV & 15) || ((uintptr_t)dO & 15) || ((uintptr_t)dQKV & 15)) return U2GNN_E_ALIGN;
     const size_t lds = bwd_lds(W, dp);
     if (lds > LDS_LIMIT) return U2GNN_E_SHAPE;
-    static bool attr = false;   // dynamic LDS above 64 KiB must be opted into once per kernel
-    if (!attr) {
-        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(window_attn_bwd_kernel),
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_LIMIT);
-        if (e != hipSuccess) return (int)e;
-        attr = true;
-    }
+    U2GNN_TRY_WIN(lds_optin(reinterpret_cast<const void *>(window_attn_bwd_kernel)));
     const int64_t elems = (int64_t)W * (dp / 4);
     int nb = 256 / (dp / 4);
     nb = std::max(nb, (W + 15) / 16);
@@ -486,13 +495,7 @@ int u2gnn_window_attn_bwd(const float *QKV, int64_t ldq, int32_t W, int32_t dp, 
     const int rb = (W + nb - 1) / nb;
     if (elems > 256 * 6 && elems <= 256 * 7 && rb == 9 && (W + 8) / 9 == nb) {
         auto kern = window_attn_bwd_pf_kernel<7, 9, kWinPfBlocksPerCu>;
-        static bool attr_pf = false;
-        if (!attr_pf) {
-            const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_LIMIT);
-            if (e != hipSuccess) return (int)e;
-            attr_pf = true;
-        }
+        U2GNN_TRY_WIN(lds_optin(reinterpret_cast<const void *>(kern)));
         const int64_t per_cu = std::min<int64_t>(kWinPfBlocksPerCu, std::max<int64_t>(1, (int64_t)(LDS_LIMIT / lds)));
         const int64_t grid = std::min<int64_t>(n_nodes, per_cu * cu_count());
         hipLaunchKernelGGL(kern, dim3((unsigned)std::max<int64_t>(grid, 1)), dim3(256), lds, u2gnn_stream(stream), QKV,

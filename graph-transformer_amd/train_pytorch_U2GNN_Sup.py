@@ -29,7 +29,7 @@ import torch.nn as nn  # noqa: E402
 torch.manual_seed(123)
 np.random.seed(123)
 
-from u2gnn_hip.cli import Run, self_launch, step_seed  # noqa: E402  (no GPU work at import)
+from u2gnn_hip.cli import Run, check_world, self_launch, step_seed  # noqa: E402  (no GPU work at import)
 
 parser = ArgumentParser("U2GNN", formatter_class=ArgumentDefaultsHelpFormatter, conflict_handler='resolve')
 parser.add_argument("--run_folder", default="../", help="")
@@ -55,7 +55,8 @@ parser.add_argument("--autograd", action="store_true", help="reference loop: aut
 parser.add_argument("--max_steps", default=0, type=int, help="stop after this many train steps (0 = no limit)")
 parser.add_argument("--world_size", default=1, type=int,
                     help="data-parallel ranks, one per GPU (started here under torch.distributed.run unless a "
-                         "launcher already set WORLD_SIZE)")
+                         "launcher already set WORLD_SIZE; left at 1 under a launcher it takes WORLD_SIZE).  "
+                         "Epochs round up to a multiple of world_size batches (u2gnn_hip/cli.py)")
 parser.add_argument("--dist_backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend: nccl = RCCL over xGMI; gloo = several ranks on one GPU (tests)")
 args = parser.parse_args()
@@ -74,8 +75,7 @@ from util import load_data, separate_data  # noqa: E402
 if not torch.cuda.is_available():
     raise SystemExit("train_pytorch_U2GNN_Sup: the MI355X path needs a GPU (no CPU fallback)")
 run = Run.init(args.dist_backend)
-if run.world != args.world_size:
-    raise SystemExit(f"WORLD_SIZE={run.world} but --world_size {args.world_size}")
+check_world(run.world, args.world_size)   # default 1: the launcher's WORLD_SIZE
 device = run.device()
 torch.cuda.set_device(device)
 torch.cuda.manual_seed_all(123)

@@ -28,7 +28,7 @@ import torch  # noqa: E402
 torch.manual_seed(123)
 np.random.seed(123)
 
-from u2gnn_hip.cli import Run, self_launch, step_seed  # noqa: E402  (no GPU work at import)
+from u2gnn_hip.cli import Run, check_world, self_launch, step_seed  # noqa: E402  (no GPU work at import)
 
 parser = ArgumentParser("U2GNN", formatter_class=ArgumentDefaultsHelpFormatter, conflict_handler='resolve')
 parser.add_argument("--run_folder", default="../", help="")
@@ -53,7 +53,8 @@ parser.add_argument("--attention", default="nodes", choices=["nodes", "neighbors
 parser.add_argument("--max_steps", default=0, type=int, help="stop after this many train steps (0 = no limit)")
 parser.add_argument("--world_size", default=1, type=int,
                     help="data-parallel ranks, one per GPU (started here under torch.distributed.run unless a "
-                         "launcher already set WORLD_SIZE)")
+                         "launcher already set WORLD_SIZE; left at 1 under a launcher it takes WORLD_SIZE).  "
+                         "Epochs round up to a multiple of world_size batches (u2gnn_hip/cli.py)")
 parser.add_argument("--dist_backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend: nccl = RCCL over xGMI; gloo = several ranks on one GPU (tests)")
 args = parser.parse_args()
@@ -72,8 +73,7 @@ from util import load_data, separate_data_idx  # noqa: E402
 if not torch.cuda.is_available():
     raise SystemExit("train_pytorch_U2GNN_UnSup: the MI355X path needs a GPU (no CPU fallback)")
 run = Run.init(args.dist_backend)
-if run.world != args.world_size:
-    raise SystemExit(f"WORLD_SIZE={run.world} but --world_size {args.world_size}")
+check_world(run.world, args.world_size)   # default 1: the launcher's WORLD_SIZE
 device = run.device()
 torch.cuda.set_device(device)
 log = print if run.main else (lambda *a, **k: None)   # rank 0 prints and writes the acc file

@@ -8,10 +8,16 @@ CLI run with ``--world_size N`` trains one process per GPU:
   xGMI) by default, ``gloo`` for several ranks on one GPU (tests).
 * A global step is ``world`` consecutive batches of the reference's single numpy stream: rank r assembles
   batch r and replays the others (``Run.next_batch``; dp.rank_batches), so the ranks together train on
-  exactly the batches one process would take in ``world`` steps, with the averaged gradient.  An epoch is
-  ceil(num_batches_per_epoch / world) global steps.
-* Each batch's dropout seed is a function of its index in the stream (``step_seed``), whichever rank trains
-  it, so a data-parallel run is reproducible by one process.
+  exactly the batches one process would take in ``world`` steps, with the averaged gradient.
+* EPOCHS ROUND UP TO A MULTIPLE OF ``world`` BATCHES: an epoch is ceil(num_batches_per_epoch / world)
+  global steps.  When ``world`` does not divide the batch count, each epoch trains world - (nb % world)
+  extra batches of the stream (MUTAG, nb = 43, world 2: 44), the epoch's summed loss (the plateau rule's
+  input) covers those batches too, and from the second epoch on the stream positions differ from a
+  one-process run with the same --num_epochs.  A one-process run is reproduced exactly when ``world``
+  divides the batch count, or with --max_steps inside the first epoch (tests/test_cli_dp_cpu.py).
+* Fused trainer: each batch's dropout seed is a function of its index in the stream (``step_seed``),
+  whichever rank trains it.  --autograd: the module draws its dropout from torch's generator, seeded
+  123 + rank per rank, so a data-parallel --autograd run is NOT reproducible by one process.
 * Every rank runs the evaluation (it consumes the same numpy draws, so the streams stay aligned; the
   parameters are identical on every rank); rank 0 alone prints and writes the acc file.
 """
@@ -29,17 +35,20 @@ from .dp import rank_batches  # noqa: F401  (the same partition rule; re-exporte
 
 def self_launch(world_size: int, script: str, argv: List[str]) -> Optional[int]:
     """world_size > 1 and no launcher: run the launcher on ``script argv`` as a child process and return
-    its exit code (the caller exits with it).  None when the caller should train itself."""
+    its exit code (the caller exits with it).  None when the caller should train itself.  The launcher runs
+    --standalone (its own rendezvous on a port it binds itself: no probe-then-close port race)."""
     if world_size <= 1 or "WORLD_SIZE" in os.environ:
         return None
-    import socket
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world_size}",
-           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(script)] + list(argv)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--standalone", "--local-addr=127.0.0.1",
+           f"--nproc-per-node={world_size}", os.path.abspath(script)] + list(argv)
     return subprocess.call(cmd)
+
+
+def check_world(run_world: int, flag: int) -> None:
+    """--world_size against the launcher's WORLD_SIZE: the flag left at its default (1) takes the launcher's
+    value; an explicit flag must match it."""
+    if flag != 1 and flag != run_world:
+        raise SystemExit(f"WORLD_SIZE={run_world} but --world_size {flag}")
 
 
 _MASK = (1 << 64) - 1

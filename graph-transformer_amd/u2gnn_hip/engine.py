@@ -136,6 +136,9 @@ class PackedLayer:
 
 
 class EncoderLayerCtx:
+    """Saved forward tensors of one layer; Pd is the [Np, Np] signed probability image, or for d <= 32
+    (small_attn) the attention context (attn_small_ctx_floats: the row statistics the backward recomputes P
+    from and a compact Q, K, V copy)."""
     __slots__ = ("X", "QKV", "Pd", "O", "Z1", "X1", "mean1", "rstd1", "Hd", "Z2", "mean2", "rstd2",
                  "seeds")
 
@@ -347,6 +350,16 @@ def qk_tile(Np: int) -> int:
     return 256 if Np % 256 == 0 and (Np // 256) * (Np // 128) >= 256 else 128
 
 
+SMALL_ATTN_MAX_D = 32
+
+
+def small_attn(d: int) -> bool:
+    """Node attention on the vector ALUs, flash-style (u2gnn_attn_small_*): feature widths d <= 32 in every
+    precision -- the matrix-core products would be >= 50 % padding (dp = 64) and the N x N images pure
+    overhead (encoder_layer.cpp small_attn applies the same rule)."""
+    return d <= SMALL_ATTN_MAX_D
+
+
 def fused_attn(dp: int, prec_qk: str, prec_pv: str) -> bool:
     """Node-axis attention forward through the fused softmax.P.V kernel: matrix-core precisions,
     dp <= 384 (encoder_layer.cpp fused_attn)."""
@@ -381,14 +394,21 @@ def encoder_layer_forward(X: torch.Tensor, w: PackedLayer, p: LayerParams, dims:
     dev = X.device
     f32 = torch.float32
     QKV = torch.empty(Np, 3 * dp, device=dev, dtype=f32)
-    fused = fused_attn(dp, _rp("qk", prec), _rp("pv", prec))
+    small = small_attn(d)
+    fused = not small and fused_attn(dp, _rp("qk", prec), _rp("pv", prec))
     QKV2 = torch.empty(Np, 6 * dp, device=dev, dtype=torch.bfloat16) if fused else None   # x2 copy for P.V
     K.gemm(X, w.W_in, QKV, Np, 3 * dp, dp, dp, dp, 3 * dp, trans_b=True, epilogue=E.EPI_BIAS, bias=w.b_in,
            alpha=1.0 / math.sqrt(d), scale_cols=dp, precision=_rp("in_proj", prec), flops=6.0 * N * d * d,
            tile=256 if (_rp("in_proj", prec) != "fp32" and Np % 256 == 0 and (Np // 256) * (3 * dp // 128) >= BIG_TILE_BLOCKS) else 0,
            Cx2=QKV2, ldcx2=6 * dp, cx2_col0=2 * dp)
     Q, Kt, V = QKV[:, :dp], QKV[:, dp:2 * dp], QKV[:, 2 * dp:]
-    if fused:
+    if small:
+        # d <= 32: softmax -> dropout -> P.V on the vector ALUs; the row statistics take the image's place in
+        # the context (encoder_layer.cpp layer_fwd, launch for launch)
+        O = torch.empty(Np, dp, device=dev, dtype=f32)
+        Pd = torch.empty(K.attn_small_ctx_floats(Np, d), device=dev, dtype=f32)
+        K.attn_small_fwd(QKV, 3 * dp, dp, d, N, Np, pd, seeds.get(SITE_ATTN, 0), O, dp, Pd)
+    elif fused:
         # S = Q K^T written straight into the image buffer, with the softmax row partials of each 64-column
         # group from the GEMM epilogue; one fused softmax -> dropout -> P.V pass then overwrites S with the
         # signed image and forms O (attn_fused.hip; encoder_layer.cpp layer_fwd, launch for launch)
@@ -502,10 +522,29 @@ def encoder_layer_backward(dX2: torch.Tensor, ctx: EncoderLayerCtx, w: PackedLay
     del dA
     # attention core
     QKV = ctx.QKV
-    Q, Kt, V = QKV[:, :dp], QKV[:, dp:2 * dp], QKV[:, 2 * dp:]
     if not use_ln_delta:
         delta = torch.empty(Np, device=dev, dtype=f32)
         K.rowdot(dO, dp, ctx.O, dp, delta, Np, dp)
+    if small_attn(d):
+        # d <= 32: dQ, dK, dV with P recomputed from the saved context (ctx.Pd: row statistics + compact Q, K, V)
+        dQKV = torch.empty(Np, 3 * dp, device=dev, dtype=f32)
+        ws_a = torch.empty(K.attn_small_ws_floats(N, Np, d), device=dev, dtype=f32)
+        K.attn_small_bwd(ctx.Pd, dp, d, N, Np, pd, seeds.get(SITE_ATTN, 0), dO, dp, delta, 1.0 / math.sqrt(d),
+                         dQKV, 3 * dp, ws_a)
+        del ws_a, dO
+    else:
+        dQKV = _attn_bwd_products(ctx, dO, delta, N, Np, d, dp, pd, att, prec, dev)
+    _in_proj_backward(dQKV, dX, ctx, w, g, N, Np, d, dp, prec, off, need_dx)
+    if own:
+        off.join()
+    return dX if need_dx else None
+
+
+def _attn_bwd_products(ctx, dO, delta, N, Np, d, dp, pd, att, prec, dev):
+    """dS (matrix cores, from the signed image), then dV = Pd^T dO, dQ = dS K / sqrt(d), dK = dS^T Q."""
+    f32 = torch.float32
+    QKV = ctx.QKV
+    Q, Kt, V = QKV[:, :dp], QKV[:, dp:2 * dp], QKV[:, 2 * dp:]
     dS = torch.empty(Np, Np, device=dev, dtype=f32)
     K.gemm(dO, V, dS, Np, Np, dp, dp, 3 * dp, Np, trans_b=True, epilogue=E.EPI_ATTN_DS_SIGNED, aux0=ctx.Pd,
            p_drop=pd, rowvec=delta, ld_aux=Np, precision=_rp("ds", prec), flops=att)
@@ -517,7 +556,12 @@ def encoder_layer_backward(dX2: torch.Tensor, ctx: EncoderLayerCtx, w: PackedLay
     _gemm_nodes_k(dS, Q, dQKV[:, dp:2 * dp], Np, dp, Np, Np, 3 * dp, 3 * dp, trans_a=True, prec=_rp("dk", prec), flops=att,
                   grouped=True)
     del dS, dO
-    # in-projection
+    return dQKV
+
+
+def _in_proj_backward(dQKV, dX, ctx, w, g, N, Np, d, dp, prec, off, need_dx):
+    """dX += dQKV W_in (skipped when the input gradient is not wanted); the in-projection's weight and bias
+    gradients (on the side stream unless this is the last layer of the backward)."""
     if need_dx:
         _gemm_split(dQKV, w.W_in, dX, Np, dp, 3 * dp, 3 * dp, dp, dp, accumulate=True, prec=_rp("in_dx", prec),
                     flops=6.0 * N * d * d)
@@ -529,6 +573,3 @@ def encoder_layer_backward(dX2: torch.Tensor, ctx: EncoderLayerCtx, w: PackedLay
         off.run(in_proj_grads, dQKV, ctx.X)
     else:   # the last layer of the backward: nothing left on this stream to overlap, skip the hand-off
         in_proj_grads()
-    if own:
-        off.join()
-    return dX if need_dx else None

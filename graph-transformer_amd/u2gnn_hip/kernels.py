@@ -435,6 +435,33 @@ def attn_softmax_pv(S, lds, rowpart, ngroups, qkv2, ldq2, dp, Pd, ldp, O, ldo, w
           "u2gnn_attn_softmax_pv")
 
 
+def attn_small_ctx_floats(rows_pad, d):
+    return int(hip_lib().u2gnn_attn_small_ctx_floats(int(rows_pad), int(d)))
+
+
+def attn_small_ws_floats(n_valid, rows_pad, d):
+    return int(hip_lib().u2gnn_attn_small_ws_floats(int(n_valid), int(rows_pad), int(d)))
+
+
+def attn_small_fwd(QKV, ld_qkv, dp, d, n_valid, rows_pad, p, seed, O, ldo, ctx):
+    """ABI v15 (d <= 32): O = dropout(softmax(Q K^T)) V on the vector ALUs, flash-style, and the forward
+    context ctx [attn_small_ctx_floats(rows_pad, d)]: the row statistics ctx[:2 rows_pad].view(rows_pad, 2) =
+    (max log2 e, 1 / sum exp) the backward recomputes P from, then a compact copy of Q, K, V."""
+    _dev(QKV, O, ctx)
+    check(hip_lib().u2gnn_attn_small_fwd(_p(QKV), int(ld_qkv), int(dp), int(d), int(n_valid), int(rows_pad), float(p),
+                                         int(seed) & 0xFFFFFFFFFFFFFFFF, _p(O), int(ldo), _p(ctx), int(ctx.numel()),
+                                         _s()), "u2gnn_attn_small_fwd")
+
+
+def attn_small_bwd(ctx, dp, d, n_valid, rows_pad, p, seed, dO, ld_do, delta, q_scale, dQKV, ld_dqkv, ws):
+    """ABI v15 (d <= 32): dQKV = (q_scale dS K, dS^T Q, Pd^T dO) with P recomputed from the forward's ctx."""
+    _dev(ctx, dO, delta, dQKV, ws)
+    check(hip_lib().u2gnn_attn_small_bwd(_p(ctx), int(ctx.numel()), int(dp), int(d), int(n_valid), int(rows_pad),
+                                         float(p), int(seed) & 0xFFFFFFFFFFFFFFFF, _p(dO), int(ld_do), _p(delta),
+                                         float(q_scale), _p(dQKV), int(ld_dqkv), _p(ws), int(ws.numel()), _s()),
+          "u2gnn_attn_small_bwd")
+
+
 def sampled_softmax_bwd_rows(X, ldx, labels, sample_ids, S, W, ldw, prob, dloss, dX, lddx, dW_lab, dW_smp, n_rows, D):
     """ABI v9: W's gradient as compact rows -- dW_lab [n_rows, >= D] (row of W labels[i]) and dW_smp
     [S, >= D] (row of W sample_ids[j]) -- instead of a dense [V, D] image."""

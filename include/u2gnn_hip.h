@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define U2GNN_ABI_VERSION 14
+#define U2GNN_ABI_VERSION 15
 
 #define U2GNN_OK 0
 #define U2GNN_E_ARG (-1)    /* bad size / null pointer */
@@ -417,6 +417,26 @@ int u2gnn_attn_softmax_pv(const float *S, int64_t lds, const float *rowpart, int
                           const void *qkv2, int64_t ldq2, int64_t dp, float *Pd, int64_t ldp, float *O, int64_t ldo,
                           float *ws, int64_t ws_floats, int64_t n_valid, int64_t rows_pad, float p, uint64_t seed,
                           int32_t precision, void *stream);
+
+/* ---- ABI v15: node-axis attention for small widths d <= 32 (a3.2 forward + backward; the UnSup encoders) ----
+ * Exact fp32 on the vector ALUs, flash-style: no N x N image is stored.  QKV [rows_pad][ld_qkv] is the
+ * in-projection output (Q pre-scaled by 1/sqrt(d) at column 0, K at dp, V at 2 dp; dp % 64 == 0, padding
+ * columns zero); keys / queries n < n_valid take part, keep = keep(seed, m, n) as every dropout site.
+ * fwd: O[m] = sum_n keep P[m,n] / (1-p) V[n] with P = softmax_n(Q[m].K[n]) (rows >= n_valid and columns >= d
+ *      written 0), and the forward context ctx (u2gnn_attn_small_ctx_floats(rows_pad, d) floats, 16-byte
+ *      aligned): ctx[2m], ctx[2m+1] = (max_n Q[m].K[n] log2 e, 1 / sum_n exp) -- what the backward recomputes P
+ *      from -- followed by a compact copy of Q, K, V (rows >= n_valid zero), so the backward needs no QKV.
+ * bwd: given the forward's ctx (unchanged), dO and delta[m] = rowsum(dO[m] * O[m]): dQKV (all 3 dp columns of
+ *      every row written; padding 0) = (q_scale * dS K, dS^T Q, Pd^T dO) with dS = P o (keep dO.V^T / (1-p) -
+ *      delta), Pd = keep P / (1-p).  ws: u2gnn_attn_small_ws_floats(n_valid, rows_pad, d) floats of scratch
+ *      (per-query records), 16-byte aligned.  Both return -1 for d > 32 (the matrix-core path's widths). */
+int64_t u2gnn_attn_small_ctx_floats(int64_t rows_pad, int64_t d);
+int64_t u2gnn_attn_small_ws_floats(int64_t n_valid, int64_t rows_pad, int64_t d);
+int u2gnn_attn_small_fwd(const float *QKV, int64_t ld_qkv, int64_t dp, int64_t d, int64_t n_valid, int64_t rows_pad,
+                         float p, uint64_t seed, float *O, int64_t ldo, float *ctx, int64_t ctx_floats, void *stream);
+int u2gnn_attn_small_bwd(const float *ctx, int64_t ctx_floats, int64_t dp, int64_t d, int64_t n_valid,
+                         int64_t rows_pad, float p, uint64_t seed, const float *dO, int64_t ld_do, const float *delta,
+                         float q_scale, float *dQKV, int64_t ld_dqkv, float *ws, int64_t ws_floats, void *stream);
 
 /* ---- a12: dropout on the concatenated UnSup node embeddings (model_U2GNN_Unsup_multi.py:56) --
  * Y[i, j] = X[i, j] * keep(seed, i, j) / (1-p) for i < rows, j < cols.  The backward is the same

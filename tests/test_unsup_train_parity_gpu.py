@@ -143,5 +143,5 @@ def test_unsup_train_mode_step_matches_oracle_with_kernel_masks(golden_dir, name
     bad = {k: v for k, v in res["gpu_relu"].items() if v > TOL and k not in ("after_sign_unresolved_above_tol", "after_raw_max")}
     assert not bad, f"{name} {precision}: above {TOL} with the GPU's ReLU decisions: {bad}"
     assert_flips_at_boundary(stats, f"unsup {name} {precision}")
-    bad = {k: res["plain"][k] for k in ("logits", "loss", "grad_norm") if res["plain"][k] > TOL}
+    bad = {k: res["plain"][k] for k in ("logits", "loss") if res["plain"][k] > TOL}
     assert not bad, f"{name} {precision}: above {TOL} against the plain oracle: {bad}"

@@ -16,7 +16,8 @@ train mode.  The tests therefore check, strictly and without per-quantity except
       delta_z = max |z_gpu - z_oracle| over the kept units both runs switch on (z_gpu = Hd * (1 - p) from
       the saved dropped-ReLU image): a unit switches sides only within the measured forward disagreement
       of 0, not because of a wrong unit; and there are at most MAX_FLIP_FRAC of the kept units;
-  (3) the continuous quantities (outputs, loss, clip norm) within 1e-3 of the plain oracle.
+  (3) the quantities that are continuous in the forward (outputs, loss) within 1e-3 of the plain oracle
+      (the clip norm is a function of the gradients, so it is held by (1)).
 Post-Adam parameters have the same kind of discontinuity: Adam's first step moves an element by
 lr * g / (|g| + eps), i.e. by ~lr in the direction of sign(g).  Where a gradient element lies within the
 two computations' disagreement of zero (|g_oracle| <= 2 * max|g_gpu - g_oracle| of its tensor: the element's

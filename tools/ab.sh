@@ -14,7 +14,7 @@ for rep in 1 2; do
     if [ -n "$ONLY" ] && [ $rep = 1 ]; then
       U2GNN_HIP_LIB=$L GB_ONLY="$ONLY" timeout -k 10 200 python tools/gemm_bench.py bf16x3 2>/dev/null | sed "s/^/$v /" || exit 1
     fi
-    U2GNN_HIP_LIB=$L timeout -k 10 200 python bench.py --steps 30 --warmup 5 --cpu-baseline 0 --fp32-steps 0 --pipeline-steps 0 --no-roofline > gpurun_out/ab_$v.json 2>/dev/null || exit 1
+    U2GNN_HIP_LIB=$L timeout -k 10 200 python bench.py --configs 0 --steps 30 --warmup 5 --cpu-baseline 0 --fp32-steps 0 --pipeline-steps 0 --no-roofline > gpurun_out/ab_$v.json 2>/dev/null || exit 1
     python -c "import json;d=json.load(open('gpurun_out/ab_$v.json'));print('$v', 'step_ms', d['ms_per_step'], d['final_loss'])"
   done
 done

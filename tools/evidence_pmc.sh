@@ -11,7 +11,7 @@ TAG=${1:-ev}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"; mkdir -p gpurun_out
 export TMPDIR=/tmp
-B="python bench.py --cpu-baseline 0 --no-roofline"
+B="python bench.py --configs 0 --cpu-baseline 0 --no-roofline"
 timeout -k 10 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE -d "$R/gpurun_out/${TAG}_MFMA" -o run -- \
     $B --steps 3 --warmup 1 > gpurun_out/${TAG}_MFMA.log 2>&1 || { echo "mfma pass failed"; tail -5 gpurun_out/${TAG}_MFMA.log; exit 1; }
 echo "mfma pass done"

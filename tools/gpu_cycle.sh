@@ -21,7 +21,7 @@ timeout -k 10 600 $CMD > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench
 cat gpurun_out/${TAG}_bench.json
 # the profiled run: the same timed region, without the CPU baseline and the extra lines after it (fp32, on-the-fly
 # pipeline), so the trace holds the timed steps' launches (and their averages match the bench line's probe)
-PCMD="python bench.py --steps 30 --warmup 5 --cpu-baseline 0 --fp32-steps 0 --pipeline-steps 0"
+PCMD="python bench.py --steps 30 --warmup 5 --cpu-baseline 0 --fp32-steps 0 --pipeline-steps 0 --configs 0"
 GPU_MAX_HW_QUEUES=8 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/${TAG}_prof" -o run -- $PCMD > gpurun_out/${TAG}_prof.log 2>&1
 echo "prof rc=$?"
 DB=$(find "$R/gpurun_out/${TAG}_prof" -name '*.db' | head -1)

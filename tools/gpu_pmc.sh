@@ -7,6 +7,6 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"; mkdir -p gpurun_out
 export TMPDIR=/tmp
 for C in FETCH_SIZE WRITE_SIZE; do
-  GPU_MAX_HW_QUEUES=8 timeout -s KILL 300 rocprofv3 --pmc $C -d "$R/gpurun_out/${TAG}_${C}" -o run -- python bench.py --steps 3 --warmup 1 --cpu-baseline 0 --no-roofline > gpurun_out/${TAG}_${C}.log 2>&1 || { echo "pmc $C failed"; tail -5 gpurun_out/${TAG}_${C}.log; exit 1; }
+  GPU_MAX_HW_QUEUES=8 timeout -s KILL 300 rocprofv3 --pmc $C -d "$R/gpurun_out/${TAG}_${C}" -o run -- python bench.py --configs 0 --steps 3 --warmup 1 --cpu-baseline 0 --no-roofline > gpurun_out/${TAG}_${C}.log 2>&1 || { echo "pmc $C failed"; tail -5 gpurun_out/${TAG}_${C}.log; exit 1; }
 done
 echo pmc done

@@ -6,7 +6,8 @@
 // and still moves the N x N score and probability images through HBM several times per layer.  Here the
 // N^2 work runs in exact fp32 on the vector ALUs and nothing N x N is ever stored (flash-style), in four
 // launches per layer, each writing its final outputs (no partial buffers, no combine launches):
-//   pack     Q, K, V out of the strided in-projection image into the compact context (layouts below);
+//   proj     the in-projection (a3.1) of the layer input straight into the compact context (layouts below):
+//            no [Np][3 dp] image, no matrix-core launch for a d x 3d product;
 //   forward  SA_SPL = 2 waves per query row, the 64 lanes of each splitting its half of every LDS key tile
 //            (two consecutive keys per lane per 128-key round): scores, an online max / sum-exp rescale per
 //            8 keys, the dropout hash (one finaliser per key pair) and o += e v; the lanes merge by a
@@ -15,7 +16,7 @@
 //   dQ       the same row walk: dS_ij = P_ij (keep dO_i.V_j / (1 - p) - delta_i), dQ_i += dS_ij K_j; each
 //            row also writes its compact record (Q, dO, M, 1/L, delta, row key) for
 //   dK, dV   SA_SPL waves per key row, the lanes splitting LDS tiles of query records:
-//            dV_j += Pd_ij dO_i, dK_j += dS_ij Q_i.
+//            dV_j += Pd_ij dO_i, dK_j += dS_ij Q_i; then the in-projection's dX_j += dQKV_j W_in (row-local).
 // Softmax semantics are the reference's: softmax over the keys, THEN dropout(p) on the probabilities with
 // 1/(1-p) scaling, THEN the product with V (torch SDPA math path); delta_i = rowsum(dO_i * O_i) as for the
 // matrix-core path.  The keep decisions are u2gnn_keep(seed, i, j, p), the hash every dropout site uses.
@@ -41,14 +42,15 @@ template <int DM> constexpr int sa_min_waves() { return DM <= 16 ? 4 : 2; }
 // Layouts (all fp32; DM = d rounded up to a multiple of 4 up to 24, else 32):
 //   ctx (the forward's saved context, u2gnn_attn_small_ctx_floats):  st [Np][2] = (M in log2 units, 1/L) |
 //        qc [Np][DM] (Q, pre-scaled) | kvc [Np][2 DM] (K then V of a row, adjacent); rows >= N all zero.
-//        A pack launch copies Q / K / V out of the strided [Np][3 dp] in-projection image once: every
-//        workgroup then stages the keys from 2 DM contiguous floats per key instead of two 16-byte pieces
-//        of two far-apart cache lines per key (the TA / TCP cost the strided sweep paid, once per line).
+//        Every workgroup stages the keys from 2 DM contiguous floats per key (round 5, first form: a strided
+//        [Np][3 dp] image cost two 16-byte pieces of two far-apart cache lines per key and workgroup).
 //   ws (the backward's scratch, u2gnn_attn_small_ws_floats): rq [Np][RQ], RQ = 2 DM + 4:
 //        Q[DM], dO[DM], M, 1/L, delta, row key -- written by the dQ launch for its own rows, staged by dK / dV.
 struct SaP {
-    const float *qkv;   // pack: [Np][ld]: Q (pre-scaled by 1/sqrt(d)) at column 0, K at dp, V at 2 dp
-    int64_t ld;
+    const float *x;     // forward: the layer input [Np][ldx] (d real columns)
+    int64_t ldx;
+    const float *w_in;  // the in-projection [3 dp][dp] (padded; rows c, dp + c, 2 dp + c: Q, K, V column c)
+    const float *b_in;  // [3 dp]
     int32_t dp, d, N, Np;
     float p;
     uint64_t seed;
@@ -60,7 +62,9 @@ struct SaP {
     float *rq;          // backward: [Np][RQ]
     float *out;         // forward: O; backward: dQKV
     int64_t ld_out;
-    float q_scale;
+    float q_scale;      // 1/sqrt(d): Q's scale in the forward, dQ's in the backward
+    float *dx;          // backward: dX += dQKV W_in (nullptr: not wanted)
+    int64_t lddx;
 };
 
 template <int DM> __host__ __device__ constexpr int sa_rq() { return 2 * DM + 4; }
@@ -128,18 +132,33 @@ __device__ __forceinline__ void stage_rec(const float *src, int t0, int Np, floa
     }
 }
 
-// ---- pack: Q, K, V rows of the strided image -> qc, kvc (rows >= N zero) ---------------------------------
+// ---- a3.1 in-projection straight into the compact context: (Q, K, V) = X W_in^T + b_in, Q scaled by 1/sqrt(d)
+// (the bias epilogue's order: (acc + b) * scale); rows >= N zero.  One thread per 4 output columns of a row.
 template <int DM>
-__global__ void __launch_bounds__(256) sa_pack_kernel(SaP P) {
+__global__ void __launch_bounds__(256) sa_proj_kernel(SaP P) {
     constexpr int C4 = DM / 4;
     const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (e >= (int64_t)P.Np * 3 * C4) return;
     const int r = (int)(e / (3 * C4)), bc = (int)(e % (3 * C4)), b = bc / C4, c = 4 * (bc % C4);
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (r < P.N) v = *reinterpret_cast<const float4 *>(P.qkv + (int64_t)r * P.ld + (int64_t)b * P.dp + c);
+    float o[4] = {0.f, 0.f, 0.f, 0.f};
+    if (r < P.N) {
+        float xv[DM];
+        load_row<DM>(P.x + (int64_t)r * P.ldx, xv);   // columns d .. DM of the padded row are zero
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int64_t wr = (int64_t)b * P.dp + c + q;   // W_in row of output column c + q of block b
+            float w[DM];
+            load_row<DM>(P.w_in + wr * P.dp, w);
+            float acc = 0.f;
+#pragma unroll
+            for (int k = 0; k < DM; ++k) acc = fmaf(xv[k], w[k], acc);
+            o[q] = acc + P.b_in[wr];
+            if (b == 0) o[q] *= P.q_scale;
+        }
+    }
     float *dst = b == 0 ? sa_qc<DM>(P.ctx, P.Np) + (int64_t)r * DM + c
                         : sa_kvc<DM>(P.ctx, P.Np) + (int64_t)r * 2 * DM + (b - 1) * DM + c;
-    *reinterpret_cast<float4 *>(dst) = v;
+    *reinterpret_cast<float4 *>(dst) = make_float4(o[0], o[1], o[2], o[3]);
 }
 
 // ---- forward: one query row per SA_SPL waves -------------------------------------------------------------
@@ -436,6 +455,21 @@ __global__ void __launch_bounds__(SA_NT, sa_min_waves<DM>()) sa_bwd_kv_kernel(Sa
             row[P.dp + c] = col ? lane_col<DM>(dk[x], c) : 0.f;
             row[2 * P.dp + c] = col ? lane_col<DM>(dv[x], c) : 0.f;
         }
+        // the in-projection's input gradient, row j: dX += dQ W_q + dK W_k + dV W_v (dQ of this row written by
+        // the dQ launch before this one); lane c < d, W_in's columns read across the lanes
+        if (P.dx && j < P.N && lane < P.d) {
+            float dq[DM];
+            load_row<DM>(row, dq);
+            float acc = 0.f;
+            const float *wq = P.w_in + lane, *wk = wq + (int64_t)P.dp * P.dp, *wv = wk + (int64_t)P.dp * P.dp;
+#pragma unroll
+            for (int k = 0; k < DM; ++k) {
+                acc = fmaf(dq[k], wq[(int64_t)k * P.dp], acc);
+                acc = fmaf(dk[x][k], wk[(int64_t)k * P.dp], acc);
+                acc = fmaf(dv[x][k], wv[(int64_t)k * P.dp], acc);
+            }
+            P.dx[(int64_t)j * P.lddx + lane] += acc;
+        }
     }
 }
 
@@ -463,7 +497,7 @@ SaP sa_params(int64_t dp, int64_t d, int64_t N, int64_t Np, float p, uint64_t se
 template <int DM>
 int sa_fwd_launch(const SaP &P, hipStream_t st) {
     const int64_t nt = (int64_t)P.Np * 3 * (DM / 4);
-    hipLaunchKernelGGL(sa_pack_kernel<DM>, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, st, P);
+    hipLaunchKernelGGL(sa_proj_kernel<DM>, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, st, P);
     hipLaunchKernelGGL(sa_fwd_kernel<DM>, dim3((unsigned)((P.Np + SA_RB - 1) / SA_RB)), dim3(SA_NT), 0, st, P);
     return u2gnn_launch_status();
 }
@@ -491,14 +525,16 @@ int64_t u2gnn_attn_small_ws_floats(int64_t n_valid, int64_t rows_pad, int64_t d)
     return rows_pad * (2 * (int64_t)sa_dm(d) + 4);
 }
 
-int u2gnn_attn_small_fwd(const float *QKV, int64_t ld_qkv, int64_t dp, int64_t d, int64_t N, int64_t Np, float p,
-                         uint64_t seed, float *O, int64_t ldo, float *ctx, int64_t ctx_floats, void *stream) {
+int u2gnn_attn_small_fwd(const float *X, int64_t ldx, const float *W_in, const float *b_in, int64_t dp, int64_t d,
+                         int64_t N, int64_t Np, float p, uint64_t seed, float *O, int64_t ldo, float *ctx,
+                         int64_t ctx_floats, void *stream) {
     int rc = sa_check(dp, d, N, Np, p, ctx, ctx_floats);
     if (rc != U2GNN_OK) return rc;
-    if (!QKV || ld_qkv < 3 * dp || !O || ldo < dp) return U2GNN_E_ARG;
-    if (!al16(QKV) || (ld_qkv & 3)) return U2GNN_E_ALIGN;
+    if (!X || ldx < dp || !W_in || !b_in || !O || ldo < dp) return U2GNN_E_ARG;
+    if (!al16(X) || (ldx & 3) || !al16(W_in)) return U2GNN_E_ALIGN;
     SaP P = sa_params(dp, d, N, Np, p, seed, ctx);
-    P.qkv = QKV, P.ld = ld_qkv, P.out = O, P.ld_out = ldo;
+    P.x = X, P.ldx = ldx, P.w_in = W_in, P.b_in = b_in, P.q_scale = (float)(1.0 / std::sqrt((double)d));
+    P.out = O, P.ld_out = ldo;
     hipStream_t st = u2gnn_stream(stream);
     switch (sa_dm(d)) {
         case 4: return sa_fwd_launch<4>(P, st);
@@ -511,17 +547,19 @@ int u2gnn_attn_small_fwd(const float *QKV, int64_t ld_qkv, int64_t dp, int64_t d
     }
 }
 
-int u2gnn_attn_small_bwd(const float *ctx, int64_t ctx_floats, int64_t dp, int64_t d, int64_t N, int64_t Np, float p,
-                         uint64_t seed, const float *dO, int64_t ld_do, const float *delta, float q_scale,
-                         float *dQKV, int64_t ld_dqkv, float *ws, int64_t ws_floats, void *stream) {
+int u2gnn_attn_small_bwd(const float *ctx, int64_t ctx_floats, const float *W_in, int64_t dp, int64_t d, int64_t N,
+                         int64_t Np, float p, uint64_t seed, const float *dO, int64_t ld_do, const float *delta,
+                         float q_scale, float *dQKV, int64_t ld_dqkv, float *dX, int64_t lddx, float *ws,
+                         int64_t ws_floats, void *stream) {
     int rc = sa_check(dp, d, N, Np, p, ctx, ctx_floats);
     if (rc != U2GNN_OK) return rc;
     if (!dO || !delta || !dQKV || ld_dqkv < 3 * dp || ld_do < dp || !ws || ws_floats < u2gnn_attn_small_ws_floats(N, Np, d))
         return U2GNN_E_ARG;
-    if (!al16(dO) || (ld_do & 3) || !al16(ws)) return U2GNN_E_ALIGN;
+    if (dX && (!W_in || lddx < dp)) return U2GNN_E_ARG;
+    if (!al16(dO) || (ld_do & 3) || !al16(ws) || !al16(dQKV) || (ld_dqkv & 3)) return U2GNN_E_ALIGN;
     SaP P = sa_params(dp, d, N, Np, p, seed, const_cast<float *>(ctx));   // read-only in the backward
     P.dO = dO, P.ld_do = ld_do, P.delta = delta, P.q_scale = q_scale;
-    P.rq = ws, P.out = dQKV, P.ld_out = ld_dqkv;
+    P.rq = ws, P.out = dQKV, P.ld_out = ld_dqkv, P.w_in = W_in, P.dx = dX, P.lddx = lddx;
     hipStream_t st = u2gnn_stream(stream);
     switch (sa_dm(d)) {
         case 4: return sa_bwd_launch<4>(P, st);

@@ -111,7 +111,8 @@ bool small_attn(const Dims &D) { return !D.window && D.d <= 32; }
 
 Ctx carve_ctx(Arena &A, const Dims &D, bool drop) {
     Ctx c;
-    c.QKV = A.take<float>(D.Np * 3 * D.dp);
+    // the small-width path projects straight into its compact attention context: no [Np][3 dp] image
+    c.QKV = small_attn(D) ? nullptr : A.take<float>(D.Np * 3 * D.dp);
     (void)drop;
     c.Pd = c.Psave = c.stats = nullptr;
     if (D.window)
@@ -472,6 +473,23 @@ bool fused_attn(const Dims &D) {
     return !D.window && !small_attn(D) && D.prec_fwd != U2GNN_PREC_F32 && D.dp <= 384;
 }
 
+// the row-local tail of a small-width layer (u2gnn_layer_tail_small_*, layer_small.hip): every precision when the
+// attention is the small-width one (engine.small_attn mirrors the rule)
+u2gnn_small_tail_args tail_args(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seeds *s, const Ctx &c,
+                                const float *X, float *X2) {
+    u2gnn_small_tail_args t;
+    std::memset(&t, 0, sizeof(t));
+    t.n_valid = D.N, t.rows_pad = D.Np, t.d = D.d, t.dp = D.dp, t.ff = D.ff, t.ffp = D.ffp;
+    t.p = s->p_drop, t.eps = 1e-5f;
+    t.seed_drop1 = s->drop1, t.seed_dropff = s->dropff, t.seed_drop2 = s->drop2;
+    t.W_o = w->W_o, t.b_o = w->b_o, t.n1_w = w->n1_w, t.n1_b = w->n1_b, t.W1 = w->W1, t.b1 = w->b1;
+    t.W2 = w->W2, t.b2 = w->b2, t.n2_w = w->n2_w, t.n2_b = w->n2_b;
+    t.O = c.O, t.X = X;
+    t.Z1 = c.Z1, t.X1 = c.X1, t.mean1 = c.mean1, t.rstd1 = c.rstd1, t.Hd = c.Hd;
+    t.Z2 = c.Z2, t.X2 = X2, t.mean2 = c.mean2, t.rstd2 = c.rstd2;
+    return t;
+}
+
 int layer_fwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seeds *s, const float *X, float *X2,
               Arena &CA, Arena &W, bool need_ctx, hipStream_t st) {
     const int64_t N = D.N, Np = D.Np, d = D.d, dp = D.dp, ffp = D.ffp;
@@ -483,8 +501,8 @@ int layer_fwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
     const bool fused = fused_attn(D);
     // the in-projection output again in x2 format: the V tiles the fused softmax.P.V kernel reads
     void *qkv2 = fused ? static_cast<void *>(W.take<uint16_t>(Np * 6 * dp)) : nullptr;
-    // a3.1 in-projection (+bias, Q scaled by 1/sqrt(d))
-    {
+    // a3.1 in-projection (+bias, Q scaled by 1/sqrt(d)); the small-width attention does its own
+    if (!small_attn(D)) {
         G g(X, w->W_in, c.QKV, Np, 3 * dp, dp, dp, dp, 3 * dp, prec);
         // 256x128 blocks from 3 waves of them on (token-sized rows, neighbour mode), the default tile
         // rule below that: C4's 19 x 9 blocks of 256x128 leave a third of the CUs idle, its 76 x 18 64-tile
@@ -499,17 +517,18 @@ int layer_fwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
         if (fused) g.a.Cx2 = qkv2, g.a.ldcx2 = 6 * dp, g.a.cx2_col0 = (int32_t)(2 * dp);
         U2GNN_TRY(g.run(st, plan));
     }
-    const float *Q = c.QKV, *Kt = c.QKV + dp, *V = c.QKV + 2 * dp;
+    const float *Q = c.QKV, *Kt = Q ? Q + dp : nullptr, *V = Q ? Q + 2 * dp : nullptr;   // (no image: small path)
     if (D.window) {
         // paper semantics: attention inside each node's window of W neighbour tokens
         if (!plan)
             U2GNN_TRY(u2gnn_window_attn_fwd(c.QKV, 3 * dp, D.window, (int32_t)dp, c.O, dp, c.Psave, pd, s->attn,
                                             N / D.window, Np, st));
     } else if (small_attn(D)) {
-        // d <= 32: softmax -> dropout -> P.V flash-style on the vector ALUs, the row statistics saved
+        // d <= 32: in-projection, softmax -> dropout -> P.V flash-style on the vector ALUs, the row statistics and
+        // a compact Q, K, V saved
         if (!plan) {
             probe_mark(U2GNN_ROLE_PV, false, st, plan);
-            U2GNN_TRY(u2gnn_attn_small_fwd(c.QKV, 3 * dp, dp, d, N, Np, pd, s->attn, c.O, dp, c.stats,
+            U2GNN_TRY(u2gnn_attn_small_fwd(X, dp, w->W_in, w->b_in, dp, d, N, Np, pd, s->attn, c.O, dp, c.stats,
                                            u2gnn_attn_small_ctx_floats(Np, d), st));
             probe_mark(U2GNN_ROLE_PV, true, st, plan);
         }
@@ -550,47 +569,55 @@ int layer_fwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
         U2GNN_TRY(gemm_split(W, D, c.Pd, V, c.O, Np, dp, Np, Np, 3 * dp, dp, false, 1.f, false, nullptr, nullptr,
                              false, st, drop, prec, U2GNN_ROLE_PV));
     }
-    // a3.3 out-projection + dropout1 + residual, LayerNorm1 (fused into the GEMM epilogue when a
-    // 64-column tile holds whole rows: d <= 64, bf16 modes; engine.fused_ln mirrors the rule)
-    const bool fuse_ln = dp == 64 && prec != U2GNN_PREC_F32;
-    {
-        G g(c.O, w->W_o, c.Z1, Np, dp, dp, dp, dp, dp, prec);
-        g.tb().epi(fuse_ln ? U2GNN_EPI_BIAS_DROP_RESID_LN : U2GNN_EPI_BIAS_DROP_RESID);
-        g.a.bias = w->b_o, g.a.aux0 = X, g.a.ld_aux = dp, g.a.p_drop = pd, g.a.seed = s->drop1;
-        if (fuse_ln) set_ln(g.a, w->n1_w, w->n1_b, c.X1, dp, c.mean1, c.rstd1, d, N);
-        U2GNN_TRY(g.run(st, plan));
-    }
-    if (!plan && !fuse_ln)
-        U2GNN_TRY(u2gnn_layernorm_fwd(c.Z1, dp, w->n1_w, w->n1_b, c.X1, dp, c.mean1, c.rstd1, N, Np, d, dp, 1e-5f, st));
-    // a3.4 FFN + dropout2 + residual, LayerNorm2
-    {
-        G g(c.X1, w->W1, c.Hd, Np, ffp, dp, dp, dp, ffp, prec);
-        g.tb().epi(U2GNN_EPI_BIAS_RELU_DROP);
-        g.a.bias = w->b1, g.a.p_drop = pd, g.a.seed = s->dropff;
-        U2GNN_TRY(g.run(st, plan));
-    }
-    const int64_t f2_split = ffn2_split(fuse_ln, Np, ffp);
-    if (f2_split > 1) {
-        // too few row-complete tiles (C5: 32 of them, each a 32-step K loop): split-K slabs, then the
-        // bias / dropout / residual / LayerNorm pass over the slabs
-        float *slabs = W.take<float>(f2_split * Np * dp);
-        G g(c.Hd, w->W2, slabs, Np, dp, ffp, ffp, ffp, dp, prec);
-        g.tb().tile(64);
-        g.a.split_k = (int32_t)f2_split, g.a.slab_stride = Np * dp;
-        U2GNN_TRY(g.run(st, plan));
-        if (!plan)
-            U2GNN_TRY(u2gnn_slab_bias_drop_resid_ln(slabs, (int32_t)f2_split, Np * dp, dp, w->b2, c.X1, dp, pd,
-                                                    s->drop2, c.Z2, dp, w->n2_w, w->n2_b, X2, dp, c.mean2, c.rstd2, d,
-                                                    N, Np, 1e-5f, st));
+    if (small_attn(D)) {
+        // a3.3 + a3.4 row-local on the vector ALUs: one launch (layer_small.hip)
+        if (!plan) {
+            const u2gnn_small_tail_args t = tail_args(D, w, s, c, X, X2);
+            U2GNN_TRY(u2gnn_layer_tail_small_fwd(&t, st));
+        }
     } else {
-        G g(c.Hd, w->W2, c.Z2, Np, dp, ffp, ffp, ffp, dp, prec);
-        g.tb().epi(fuse_ln ? U2GNN_EPI_BIAS_DROP_RESID_LN : U2GNN_EPI_BIAS_DROP_RESID);
-        g.a.bias = w->b2, g.a.aux0 = c.X1, g.a.ld_aux = dp, g.a.p_drop = pd, g.a.seed = s->drop2;
-        if (fuse_ln) set_ln(g.a, w->n2_w, w->n2_b, X2, dp, c.mean2, c.rstd2, d, N);
-        U2GNN_TRY(g.run(st, plan));
+        // a3.3 out-projection + dropout1 + residual, LayerNorm1 (fused into the GEMM epilogue when a
+        // 64-column tile holds whole rows: d <= 64, bf16 modes; engine.fused_ln mirrors the rule)
+        const bool fuse_ln = dp == 64 && prec != U2GNN_PREC_F32;
+        {
+            G g(c.O, w->W_o, c.Z1, Np, dp, dp, dp, dp, dp, prec);
+            g.tb().epi(fuse_ln ? U2GNN_EPI_BIAS_DROP_RESID_LN : U2GNN_EPI_BIAS_DROP_RESID);
+            g.a.bias = w->b_o, g.a.aux0 = X, g.a.ld_aux = dp, g.a.p_drop = pd, g.a.seed = s->drop1;
+            if (fuse_ln) set_ln(g.a, w->n1_w, w->n1_b, c.X1, dp, c.mean1, c.rstd1, d, N);
+            U2GNN_TRY(g.run(st, plan));
+        }
+        if (!plan && !fuse_ln)
+            U2GNN_TRY(u2gnn_layernorm_fwd(c.Z1, dp, w->n1_w, w->n1_b, c.X1, dp, c.mean1, c.rstd1, N, Np, d, dp, 1e-5f, st));
+        // a3.4 FFN + dropout2 + residual, LayerNorm2
+        {
+            G g(c.X1, w->W1, c.Hd, Np, ffp, dp, dp, dp, ffp, prec);
+            g.tb().epi(U2GNN_EPI_BIAS_RELU_DROP);
+            g.a.bias = w->b1, g.a.p_drop = pd, g.a.seed = s->dropff;
+            U2GNN_TRY(g.run(st, plan));
+        }
+        const int64_t f2_split = ffn2_split(fuse_ln, Np, ffp);
+        if (f2_split > 1) {
+            // too few row-complete tiles (C5: 32 of them, each a 32-step K loop): split-K slabs, then the
+            // bias / dropout / residual / LayerNorm pass over the slabs
+            float *slabs = W.take<float>(f2_split * Np * dp);
+            G g(c.Hd, w->W2, slabs, Np, dp, ffp, ffp, ffp, dp, prec);
+            g.tb().tile(64);
+            g.a.split_k = (int32_t)f2_split, g.a.slab_stride = Np * dp;
+            U2GNN_TRY(g.run(st, plan));
+            if (!plan)
+                U2GNN_TRY(u2gnn_slab_bias_drop_resid_ln(slabs, (int32_t)f2_split, Np * dp, dp, w->b2, c.X1, dp, pd,
+                                                        s->drop2, c.Z2, dp, w->n2_w, w->n2_b, X2, dp, c.mean2, c.rstd2, d,
+                                                        N, Np, 1e-5f, st));
+        } else {
+            G g(c.Hd, w->W2, c.Z2, Np, dp, ffp, ffp, ffp, dp, prec);
+            g.tb().epi(fuse_ln ? U2GNN_EPI_BIAS_DROP_RESID_LN : U2GNN_EPI_BIAS_DROP_RESID);
+            g.a.bias = w->b2, g.a.aux0 = c.X1, g.a.ld_aux = dp, g.a.p_drop = pd, g.a.seed = s->drop2;
+            if (fuse_ln) set_ln(g.a, w->n2_w, w->n2_b, X2, dp, c.mean2, c.rstd2, d, N);
+            U2GNN_TRY(g.run(st, plan));
+        }
+        if (!plan && !fuse_ln)
+            U2GNN_TRY(u2gnn_layernorm_fwd(c.Z2, dp, w->n2_w, w->n2_b, X2, dp, c.mean2, c.rstd2, N, Np, d, dp, 1e-5f, st));
     }
-    if (!plan && !fuse_ln)
-        U2GNN_TRY(u2gnn_layernorm_fwd(c.Z2, dp, w->n2_w, w->n2_b, X2, dp, c.mean2, c.rstd2, N, Np, d, dp, 1e-5f, st));
     if ((W.overflow || CA.overflow) && debug_on())
         std::fprintf(stderr, "u2gnn: layer_fwd arena overflow (ws %lld/%lld, ctx %lld/%lld)\n", (long long)W.used,
                      (long long)W.cap, (long long)CA.used, (long long)CA.cap);
@@ -620,59 +647,78 @@ int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
     Defer *df = &defer_p, *att = &defer_a;
     const int64_t blk_d[2] = {dp, d}, blk_ff[2] = {ffp, ff};
     float *ws = W.take<float>(colstat_ws_floats(N, dp));
-    // LN2 backward -> dX1 (residual), dF (dropout2 branch); norm2 + linear2.bias grads (held back: df)
-    float *dX1 = W.take<float>(Np * dp), *dF = W.take<float>(Np * dp);
-    if (!plan)
-        U2GNN_TRY(u2gnn_layernorm_bwd(dX2, dp, c.Z2, dp, c.mean2, c.rstd2, w->n2_w, dX1, dp, dF, dp, pd, s->drop2, N,
-                                      Np, d, dp, st));
-    U2GNN_TRY(ln_params(dX2, c.Z2, c.mean2, c.rstd2, dF, dp, N, d, dp, ws, g->n2_w, g->n2_b, g->l2_b, so, plan, df));
-    // FFN
-    float *dH = W.take<float>(Np * ffp);
-    {
-        G gg(dF, w->W2, dH, Np, ffp, dp, dp, ffp, ffp, prec);
-        gg.epi(U2GNN_EPI_RELU_DROP_BWD);
-        gg.a.aux0 = c.Hd, gg.a.ld_aux = ffp, gg.a.p_drop = pd;
-        U2GNN_TRY(gg.run(st, plan));
-    }
-    U2GNN_TRY(wgrad(W, D, dF, dp, c.Hd, ffp, dp, ffp, g->l2_w, ff, blk_d, blk_ff, so, df));   // held back (df)
-    // one-stream layers in the matrix-core precisions: a split-K dX1 product leaves its slabs to LayerNorm1's
-    // backward, which completes dX1 before using it (the separate reduce launch goes; same bits)
+    const bool tail = small_attn(D);   // the row-local tail kernel (layer_small.hip) forms dX1 ... dO and delta
+    // one-stream layers in the matrix-core precisions: LayerNorm1's backward forms delta = rowsum(dO * O)
     const bool ln_delta = !D.window && prec != U2GNN_PREC_F32;
-    float *dx1_slabs = nullptr;
-    int64_t dx1_nslab = 0;
-    U2GNN_TRY(gemm_split(W, D, dH, w->W1, dX1, Np, dp, ffp, ffp, dp, dp, false, 1.f, true, nullptr, nullptr, false,
-                         st, false, -1, 0, nullptr, nullptr, (ln_delta && so == st) ? &dx1_slabs : nullptr,
-                         &dx1_nslab));
-    U2GNN_TRY(wgrad(W, D, dH, ffp, c.X1, dp, ffp, dp, g->l1_w, d, blk_ff, blk_d, so, df));
-    U2GNN_TRY(bias_grad(W, dH, Np, ffp, ffp, ffp, ff, g->l1_b, so, df));
-    // LN1 backward -> dX (residual), dA (dropout1 branch); norm1 + out_proj.bias grads (held back: df)
+    float *dX1 = W.take<float>(Np * dp), *dF = W.take<float>(Np * dp);
+    float *dH = W.take<float>(Np * ffp);
     float *dA = W.take<float>(Np * dp);
     // no input gradient wanted (first layer of the stack): LN1's residual half goes to scratch and
     // the in-projection's dX GEMM below is skipped
     float *dX_scratch = W.take<float>(Np * dp);   // taken in every mode so the plan covers it
     if (!need_dx) dX = dX_scratch;
-    // node attention: LayerNorm1's backward also forms delta = rowsum(dO * O) for the dS epilogue
-    float *delta_ln = ln_delta ? W.take<float>(Np) : nullptr;
-    if (!plan && ln_delta && dx1_slabs)
-        U2GNN_TRY(u2gnn_layernorm_bwd_delta_slabs(dX1, dp, dx1_slabs, (int32_t)dx1_nslab, Np * dp, c.Z1, dp, c.mean1,
-                                                  c.rstd1, w->n1_w, dX, dp, dA, dp, pd, s->drop1, N, Np, d, dp, X, dp,
-                                                  w->b_o, delta_ln, st));
-    else if (!plan && ln_delta)
-        U2GNN_TRY(u2gnn_layernorm_bwd_delta(dX1, dp, c.Z1, dp, c.mean1, c.rstd1, w->n1_w, dX, dp, dA, dp, pd,
-                                            s->drop1, N, Np, d, dp, X, dp, w->b_o, delta_ln, st));
-    else if (!plan)
-        U2GNN_TRY(u2gnn_layernorm_bwd(dX1, dp, c.Z1, dp, c.mean1, c.rstd1, w->n1_w, dX, dp, dA, dp, pd, s->drop1, N,
-                                      Np, d, dp, st));
-    U2GNN_TRY(ln_params(dX1, c.Z1, c.mean1, c.rstd1, dA, dp, N, d, dp, ws, g->n1_w, g->n1_b, g->out_b, so, plan, df));
-    // out-projection
+    float *delta_ln = (ln_delta || tail) ? W.take<float>(Np) : nullptr;
     float *dO = W.take<float>(Np * dp);
-    {
-        G gg(dA, w->W_o, dO, Np, dp, dp, dp, dp, dp, prec);
-        U2GNN_TRY(gg.run(st, plan));
+    if (tail) {
+        if (!plan) {
+            u2gnn_small_tail_args t = tail_args(D, w, s, c, X, nullptr);
+            t.dX2 = dX2, t.dX1 = dX1, t.dF = dF, t.dH = dH, t.dX = dX, t.dA = dA, t.dO = dO, t.delta = delta_ln;
+            U2GNN_TRY(u2gnn_layer_tail_small_bwd(&t, st));
+        }
+        // the parameter gradients of the tail, held back (df) in the order of the matrix-core branch
+        U2GNN_TRY(ln_params(dX2, c.Z2, c.mean2, c.rstd2, dF, dp, N, d, dp, ws, g->n2_w, g->n2_b, g->l2_b, so, plan, df));
+        U2GNN_TRY(wgrad(W, D, dF, dp, c.Hd, ffp, dp, ffp, g->l2_w, ff, blk_d, blk_ff, so, df));
+        U2GNN_TRY(wgrad(W, D, dH, ffp, c.X1, dp, ffp, dp, g->l1_w, d, blk_ff, blk_d, so, df));
+        U2GNN_TRY(bias_grad(W, dH, Np, ffp, ffp, ffp, ff, g->l1_b, so, df));
+        U2GNN_TRY(ln_params(dX1, c.Z1, c.mean1, c.rstd1, dA, dp, N, d, dp, ws, g->n1_w, g->n1_b, g->out_b, so, plan, df));
+        U2GNN_TRY(wgrad(W, D, dA, dp, c.O, dp, dp, dp, g->out_w, d, blk_d, blk_d, so, df));
+    } else {
+        // LN2 backward -> dX1 (residual), dF (dropout2 branch); norm2 + linear2.bias grads (held back: df)
+        if (!plan)
+            U2GNN_TRY(u2gnn_layernorm_bwd(dX2, dp, c.Z2, dp, c.mean2, c.rstd2, w->n2_w, dX1, dp, dF, dp, pd, s->drop2,
+                                          N, Np, d, dp, st));
+        U2GNN_TRY(ln_params(dX2, c.Z2, c.mean2, c.rstd2, dF, dp, N, d, dp, ws, g->n2_w, g->n2_b, g->l2_b, so, plan, df));
+        // FFN
+        {
+            G gg(dF, w->W2, dH, Np, ffp, dp, dp, ffp, ffp, prec);
+            gg.epi(U2GNN_EPI_RELU_DROP_BWD);
+            gg.a.aux0 = c.Hd, gg.a.ld_aux = ffp, gg.a.p_drop = pd;
+            U2GNN_TRY(gg.run(st, plan));
+        }
+        U2GNN_TRY(wgrad(W, D, dF, dp, c.Hd, ffp, dp, ffp, g->l2_w, ff, blk_d, blk_ff, so, df));   // held back (df)
+        // one-stream layers in the matrix-core precisions: a split-K dX1 product leaves its slabs to LayerNorm1's
+        // backward, which completes dX1 before using it (the separate reduce launch goes; same bits)
+        float *dx1_slabs = nullptr;
+        int64_t dx1_nslab = 0;
+        U2GNN_TRY(gemm_split(W, D, dH, w->W1, dX1, Np, dp, ffp, ffp, dp, dp, false, 1.f, true, nullptr, nullptr, false,
+                             st, false, -1, 0, nullptr, nullptr, (ln_delta && so == st) ? &dx1_slabs : nullptr,
+                             &dx1_nslab));
+        U2GNN_TRY(wgrad(W, D, dH, ffp, c.X1, dp, ffp, dp, g->l1_w, d, blk_ff, blk_d, so, df));
+        U2GNN_TRY(bias_grad(W, dH, Np, ffp, ffp, ffp, ff, g->l1_b, so, df));
+        // LN1 backward -> dX (residual), dA (dropout1 branch); norm1 + out_proj.bias grads (held back: df);
+        // node attention: LayerNorm1's backward also forms delta = rowsum(dO * O) for the dS epilogue
+        if (!plan && ln_delta && dx1_slabs)
+            U2GNN_TRY(u2gnn_layernorm_bwd_delta_slabs(dX1, dp, dx1_slabs, (int32_t)dx1_nslab, Np * dp, c.Z1, dp,
+                                                      c.mean1, c.rstd1, w->n1_w, dX, dp, dA, dp, pd, s->drop1, N, Np, d,
+                                                      dp, X, dp, w->b_o, delta_ln, st));
+        else if (!plan && ln_delta)
+            U2GNN_TRY(u2gnn_layernorm_bwd_delta(dX1, dp, c.Z1, dp, c.mean1, c.rstd1, w->n1_w, dX, dp, dA, dp, pd,
+                                                s->drop1, N, Np, d, dp, X, dp, w->b_o, delta_ln, st));
+        else if (!plan)
+            U2GNN_TRY(u2gnn_layernorm_bwd(dX1, dp, c.Z1, dp, c.mean1, c.rstd1, w->n1_w, dX, dp, dA, dp, pd, s->drop1,
+                                          N, Np, d, dp, st));
+        U2GNN_TRY(ln_params(dX1, c.Z1, c.mean1, c.rstd1, dA, dp, N, d, dp, ws, g->n1_w, g->n1_b, g->out_b, so, plan,
+                            df));
+        // out-projection
+        {
+            G gg(dA, w->W_o, dO, Np, dp, dp, dp, dp, dp, prec);
+            U2GNN_TRY(gg.run(st, plan));
+        }
+        U2GNN_TRY(wgrad(W, D, dA, dp, c.O, dp, dp, dp, g->out_w, d, blk_d, blk_d, so, df));   // held back (df)
     }
-    U2GNN_TRY(wgrad(W, D, dA, dp, c.O, dp, dp, dp, g->out_w, d, blk_d, blk_d, so, df));   // held back (df)
+    const bool have_delta = ln_delta || tail;
     // attention core
-    const float *Q = c.QKV, *Kt = c.QKV + dp, *V = c.QKV + 2 * dp;
+    const float *Q = c.QKV, *Kt = Q ? Q + dp : nullptr, *V = Q ? Q + 2 * dp : nullptr;   // (no image: small path)
     const float q_scale = (float)(1.0 / std::sqrt((double)d));
     float *dQKV;
     hipEvent_t dv_done = nullptr;   // side-stream position after the dV product (in_dx waits for it)
@@ -684,14 +730,16 @@ int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
     } else if (small_attn(D)) {
         // d <= 32: dQ, dK, dV with P recomputed from the row statistics (no dS image, no split-K slabs)
         dQKV = W.take<float>(Np * 3 * dp);
-        float *delta = ln_delta ? delta_ln : W.take<float>(Np);
+        float *delta = have_delta ? delta_ln : W.take<float>(Np);
         const int64_t wsf = u2gnn_attn_small_ws_floats(N, Np, d);
         float *sa_ws = W.take<float>(wsf);
-        if (!plan && !ln_delta) U2GNN_TRY(u2gnn_rowdot(dO, dp, c.O, dp, delta, Np, dp, st));
+        if (!plan && !have_delta) U2GNN_TRY(u2gnn_rowdot(dO, dp, c.O, dp, delta, Np, dp, st));
         if (!plan) {
             probe_mark(U2GNN_ROLE_DS, false, st, plan);
-            U2GNN_TRY(u2gnn_attn_small_bwd(c.stats, u2gnn_attn_small_ctx_floats(Np, d), dp, d, N, Np, pd, s->attn, dO,
-                                           dp, delta, q_scale, dQKV, 3 * dp, sa_ws, wsf, st));
+            // ... and the in-projection's dX += dQKV W_in (no dX product below)
+            U2GNN_TRY(u2gnn_attn_small_bwd(c.stats, u2gnn_attn_small_ctx_floats(Np, d), w->W_in, dp, d, N, Np, pd,
+                                           s->attn, dO, dp, delta, q_scale, dQKV, 3 * dp, need_dx ? dX : nullptr, dp,
+                                           sa_ws, wsf, st));
             probe_mark(U2GNN_ROLE_DS, true, st, plan);
         }
     } else {
@@ -709,8 +757,8 @@ int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
         // layer's FFN backward); only the in-projection's gradients are left for the end
         if (dv_side && need_dx) U2GNN_TRY(flush(df, W, so));   // measured neutral-to-worse (r04 A/B)
 #endif
-        float *delta = ln_delta ? delta_ln : W.take<float>(Np);
-        if (!plan && !ln_delta) U2GNN_TRY(u2gnn_rowdot(dO, dp, c.O, dp, delta, Np, dp, st));
+        float *delta = have_delta ? delta_ln : W.take<float>(Np);
+        if (!plan && !have_delta) U2GNN_TRY(u2gnn_rowdot(dO, dp, c.O, dp, delta, Np, dp, st));
         float *dS = W.take<float>(Np * Np);
         {
             G gg(dO, V, dS, Np, Np, dp, dp, 3 * dp, Np, D.prec_ab);
@@ -728,7 +776,7 @@ int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
         U2GNN_TRY(sd.wait(dv_done));   // dV before dX += dQKV W_in
     }
     // in-projection
-    if (need_dx)
+    if (need_dx && !small_attn(D))
         U2GNN_TRY(gemm_split(W, D, dQKV, w->W_in, dX, Np, dp, 3 * dp, 3 * dp, dp, dp, false, 1.f, true, nullptr,
                              nullptr, false, st));
     U2GNN_TRY(wgrad(W, D, dQKV, 3 * dp, X, dp, 3 * dp, dp, g->in_w, d, blk_d, blk_d, st, df));

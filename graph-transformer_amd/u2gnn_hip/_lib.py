@@ -106,6 +106,17 @@ class LayerGrads(ctypes.Structure):
     _fields_ = [(k, c_void_p) for k in _PKEYS]
 
 
+_TAIL_PTRS = ("W_o", "b_o", "n1_w", "n1_b", "W1", "b1", "W2", "b2", "n2_w", "n2_b", "O", "X", "Z1", "X1", "mean1",
+              "rstd1", "Hd", "Z2", "X2", "mean2", "rstd2", "dX2", "dX1", "dF", "dH", "dX", "dA", "dO", "delta")
+
+
+class SmallTailArgs(ctypes.Structure):   # u2gnn_small_tail_args (ABI v15)
+    _fields_ = ([(k, c_int64) for k in ("n_valid", "rows_pad", "d", "dp", "ff", "ffp")] +
+                [("p", c_float), ("eps", c_float)] +
+                [(k, c_uint64) for k in ("seed_drop1", "seed_dropff", "seed_drop2")] +
+                [(k, c_void_p) for k in _TAIL_PTRS])
+
+
 LAYER_DEEP_WGRAD = 1
 LAYER_ATTN_BWD_BF16 = 2   # precision "mixed": dS, dQ, dK on plain bf16 (ABI v5)
 LAYER_FWD_F32 = 4         # precision "fwd32": forward products exact fp32, backward bf16x3 (ABI v14)
@@ -174,10 +185,12 @@ _HIP_SIGS = {
                                I32, VP],
                               c_int32),
     "u2gnn_attn_small_ctx_floats": ([I64, I64], I64),
+    "u2gnn_layer_tail_small_fwd": ([ctypes.POINTER(SmallTailArgs), VP], c_int32),
+    "u2gnn_layer_tail_small_bwd": ([ctypes.POINTER(SmallTailArgs), VP], c_int32),
     "u2gnn_attn_small_ws_floats": ([I64, I64, I64], I64),
-    "u2gnn_attn_small_fwd": ([VP, I64, I64, I64, I64, I64, F32, c_uint64, VP, I64, VP, I64, VP], c_int32),
-    "u2gnn_attn_small_bwd": ([VP, I64, I64, I64, I64, I64, F32, c_uint64, VP, I64, VP, F32, VP, I64, VP, I64, VP],
-                             c_int32),
+    "u2gnn_attn_small_fwd": ([VP, I64, VP, VP, I64, I64, I64, I64, F32, c_uint64, VP, I64, VP, I64, VP], c_int32),
+    "u2gnn_attn_small_bwd": ([VP, I64, VP, I64, I64, I64, I64, F32, c_uint64, VP, I64, VP, F32, VP, I64, VP, I64, VP,
+                              I64, VP], c_int32),
     "u2gnn_probe_arm": ([I32, I32], c_int32),
     "u2gnn_probe_collect": ([POINTER(c_float), POINTER(c_int32)], c_int32),
     "u2gnn_set_seed_epoch": ([VP], c_int32),

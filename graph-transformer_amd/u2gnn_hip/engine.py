@@ -393,21 +393,23 @@ def encoder_layer_forward(X: torch.Tensor, w: PackedLayer, p: LayerParams, dims:
     att = 2.0 * N * N * d          # algorithmic FLOPs of one attention product (real N, d)
     dev = X.device
     f32 = torch.float32
-    QKV = torch.empty(Np, 3 * dp, device=dev, dtype=f32)
     small = small_attn(d)
     fused = not small and fused_attn(dp, _rp("qk", prec), _rp("pv", prec))
-    QKV2 = torch.empty(Np, 6 * dp, device=dev, dtype=torch.bfloat16) if fused else None   # x2 copy for P.V
-    K.gemm(X, w.W_in, QKV, Np, 3 * dp, dp, dp, dp, 3 * dp, trans_b=True, epilogue=E.EPI_BIAS, bias=w.b_in,
-           alpha=1.0 / math.sqrt(d), scale_cols=dp, precision=_rp("in_proj", prec), flops=6.0 * N * d * d,
-           tile=256 if (_rp("in_proj", prec) != "fp32" and Np % 256 == 0 and (Np // 256) * (3 * dp // 128) >= BIG_TILE_BLOCKS) else 0,
-           Cx2=QKV2, ldcx2=6 * dp, cx2_col0=2 * dp)
-    Q, Kt, V = QKV[:, :dp], QKV[:, dp:2 * dp], QKV[:, 2 * dp:]
+    QKV = QKV2 = None
+    if not small:   # (the small-width attention projects into its own compact context)
+        QKV = torch.empty(Np, 3 * dp, device=dev, dtype=f32)
+        QKV2 = torch.empty(Np, 6 * dp, device=dev, dtype=torch.bfloat16) if fused else None   # x2 copy for P.V
+        K.gemm(X, w.W_in, QKV, Np, 3 * dp, dp, dp, dp, 3 * dp, trans_b=True, epilogue=E.EPI_BIAS, bias=w.b_in,
+               alpha=1.0 / math.sqrt(d), scale_cols=dp, precision=_rp("in_proj", prec), flops=6.0 * N * d * d,
+               tile=256 if (_rp("in_proj", prec) != "fp32" and Np % 256 == 0 and (Np // 256) * (3 * dp // 128) >= BIG_TILE_BLOCKS) else 0,
+               Cx2=QKV2, ldcx2=6 * dp, cx2_col0=2 * dp)
+        Q, Kt, V = QKV[:, :dp], QKV[:, dp:2 * dp], QKV[:, 2 * dp:]
     if small:
-        # d <= 32: softmax -> dropout -> P.V on the vector ALUs; the row statistics take the image's place in
-        # the context (encoder_layer.cpp layer_fwd, launch for launch)
+        # d <= 32: in-projection, softmax -> dropout -> P.V on the vector ALUs; the row statistics and a compact
+        # Q, K, V take the images' place in the context (encoder_layer.cpp layer_fwd, launch for launch)
         O = torch.empty(Np, dp, device=dev, dtype=f32)
         Pd = torch.empty(K.attn_small_ctx_floats(Np, d), device=dev, dtype=f32)
-        K.attn_small_fwd(QKV, 3 * dp, dp, d, N, Np, pd, seeds.get(SITE_ATTN, 0), O, dp, Pd)
+        K.attn_small_fwd(X, dp, w.W_in, w.b_in, dp, d, N, Np, pd, seeds.get(SITE_ATTN, 0), O, dp, Pd)
     elif fused:
         # S = Q K^T written straight into the image buffer, with the softmax row partials of each 64-column
         # group from the GEMM epilogue; one fused softmax -> dropout -> P.V pass then overwrites S with the
@@ -427,35 +429,42 @@ def encoder_layer_forward(X: torch.Tensor, w: PackedLayer, p: LayerParams, dims:
     X1 = torch.empty(Np, dp, device=dev, dtype=f32)
     mean1 = torch.empty(Np, device=dev, dtype=f32)
     rstd1 = torch.empty(Np, device=dev, dtype=f32)
-    fuse = fused_ln(dp, _rp("out_proj", prec))   # LayerNorm in the GEMM epilogue when a 64-column tile holds whole rows
-    K.gemm(O, w.W_o, Z1, Np, dp, dp, dp, dp, dp, trans_b=True,
-           epilogue=E.EPI_BIAS_DROP_RESID_LN if fuse else E.EPI_BIAS_DROP_RESID, bias=w.b_o,
-           aux0=X, ld_aux=dp, p_drop=pd, seed=seeds.get(SITE_DROP1, 0), precision=_rp("out_proj", prec),
-           flops=2.0 * N * d * d, ln=(p.n1_w, p.n1_b, X1, dp, mean1, rstd1, d, N, 1e-5) if fuse else None)
-    if not fuse:
-        K.layernorm_fwd(Z1, dp, p.n1_w, p.n1_b, X1, dp, mean1, rstd1, N, Np, d, dp)
     Hd = torch.empty(Np, ffp, device=dev, dtype=f32)
-    K.gemm(X1, w.W1, Hd, Np, ffp, dp, dp, dp, ffp, trans_b=True, epilogue=E.EPI_BIAS_RELU_DROP, bias=w.b1,
-           p_drop=pd, seed=seeds.get(SITE_DROPFF, 0), precision=_rp("ffn1", prec), flops=2.0 * N * d * ff)
     Z2 = torch.empty(Np, dp, device=dev, dtype=f32)
     X2 = torch.empty(Np, dp, device=dev, dtype=f32)
     mean2 = torch.empty(Np, device=dev, dtype=f32)
     rstd2 = torch.empty(Np, device=dev, dtype=f32)
-    f2 = ffn2_split(fuse, Np, ffp)
-    if f2 > 1:   # split-K slabs + the bias / dropout / residual / LayerNorm pass (encoder_layer.cpp layer_fwd)
-        slabs = torch.empty(f2, Np, dp, device=dev, dtype=f32)
-        K.gemm(Hd, w.W2, slabs, Np, dp, ffp, ffp, ffp, dp, trans_b=True, split_k=f2, slab_stride=Np * dp,
-               precision=_rp("ffn2", prec), flops=2.0 * N * d * ff, tile=64)
-        K.slab_bias_drop_resid_ln(slabs, f2, Np * dp, w.b2, X1, pd, seeds.get(SITE_DROP2, 0), Z2, p.n2_w, p.n2_b,
-                                  X2, mean2, rstd2, d, N, Np)
-        del slabs
+    if small:
+        # a3.3 + a3.4 row-local on the vector ALUs, one launch (encoder_layer.cpp layer_fwd)
+        K.layer_tail_small(False, N, Np, d, dp, ff, ffp, pd, (seeds.get(SITE_DROP1, 0), seeds.get(SITE_DROPFF, 0),
+                           seeds.get(SITE_DROP2, 0)), W_o=w.W_o, b_o=w.b_o, n1_w=p.n1_w, n1_b=p.n1_b, W1=w.W1,
+                           b1=w.b1, W2=w.W2, b2=w.b2, n2_w=p.n2_w, n2_b=p.n2_b, O=O, X=X, Z1=Z1, X1=X1, mean1=mean1,
+                           rstd1=rstd1, Hd=Hd, Z2=Z2, X2=X2, mean2=mean2, rstd2=rstd2)
     else:
-        K.gemm(Hd, w.W2, Z2, Np, dp, ffp, ffp, ffp, dp, trans_b=True,
-               epilogue=E.EPI_BIAS_DROP_RESID_LN if fuse else E.EPI_BIAS_DROP_RESID, bias=w.b2,
-               aux0=X1, ld_aux=dp, p_drop=pd, seed=seeds.get(SITE_DROP2, 0), precision=_rp("ffn2", prec),
-               flops=2.0 * N * d * ff, ln=(p.n2_w, p.n2_b, X2, dp, mean2, rstd2, d, N, 1e-5) if fuse else None)
-    if not fuse:
-        K.layernorm_fwd(Z2, dp, p.n2_w, p.n2_b, X2, dp, mean2, rstd2, N, Np, d, dp)
+        fuse = fused_ln(dp, _rp("out_proj", prec))   # LayerNorm in the GEMM epilogue when a 64-column tile holds whole rows
+        K.gemm(O, w.W_o, Z1, Np, dp, dp, dp, dp, dp, trans_b=True,
+               epilogue=E.EPI_BIAS_DROP_RESID_LN if fuse else E.EPI_BIAS_DROP_RESID, bias=w.b_o,
+               aux0=X, ld_aux=dp, p_drop=pd, seed=seeds.get(SITE_DROP1, 0), precision=_rp("out_proj", prec),
+               flops=2.0 * N * d * d, ln=(p.n1_w, p.n1_b, X1, dp, mean1, rstd1, d, N, 1e-5) if fuse else None)
+        if not fuse:
+            K.layernorm_fwd(Z1, dp, p.n1_w, p.n1_b, X1, dp, mean1, rstd1, N, Np, d, dp)
+        K.gemm(X1, w.W1, Hd, Np, ffp, dp, dp, dp, ffp, trans_b=True, epilogue=E.EPI_BIAS_RELU_DROP, bias=w.b1,
+               p_drop=pd, seed=seeds.get(SITE_DROPFF, 0), precision=_rp("ffn1", prec), flops=2.0 * N * d * ff)
+        f2 = ffn2_split(fuse, Np, ffp)
+        if f2 > 1:   # split-K slabs + the bias / dropout / residual / LayerNorm pass (encoder_layer.cpp layer_fwd)
+            slabs = torch.empty(f2, Np, dp, device=dev, dtype=f32)
+            K.gemm(Hd, w.W2, slabs, Np, dp, ffp, ffp, ffp, dp, trans_b=True, split_k=f2, slab_stride=Np * dp,
+                   precision=_rp("ffn2", prec), flops=2.0 * N * d * ff, tile=64)
+            K.slab_bias_drop_resid_ln(slabs, f2, Np * dp, w.b2, X1, pd, seeds.get(SITE_DROP2, 0), Z2, p.n2_w, p.n2_b,
+                                      X2, mean2, rstd2, d, N, Np)
+            del slabs
+        else:
+            K.gemm(Hd, w.W2, Z2, Np, dp, ffp, ffp, ffp, dp, trans_b=True,
+                   epilogue=E.EPI_BIAS_DROP_RESID_LN if fuse else E.EPI_BIAS_DROP_RESID, bias=w.b2,
+                   aux0=X1, ld_aux=dp, p_drop=pd, seed=seeds.get(SITE_DROP2, 0), precision=_rp("ffn2", prec),
+                   flops=2.0 * N * d * ff, ln=(p.n2_w, p.n2_b, X2, dp, mean2, rstd2, d, N, 1e-5) if fuse else None)
+        if not fuse:
+            K.layernorm_fwd(Z2, dp, p.n2_w, p.n2_b, X2, dp, mean2, rstd2, N, Np, d, dp)
     ctx = None
     if need_ctx:
         ctx = EncoderLayerCtx()
@@ -482,44 +491,70 @@ def encoder_layer_backward(dX2: torch.Tensor, ctx: EncoderLayerCtx, w: PackedLay
     if own:
         off = OffPath(dev)
     ws = torch.empty(K.colstat_ws_floats(N, dp), device=dev, dtype=f32)
-    # LN2 backward -> dX1 (residual branch), dF (dropout2 branch); norm2 + linear2.bias grads
-    dX1 = torch.empty(Np, dp, device=dev, dtype=f32)
-    dF = torch.empty(Np, dp, device=dev, dtype=f32)
-    K.layernorm_bwd(dX2, dp, ctx.Z2, dp, ctx.mean2, ctx.rstd2, p.n2_w, dX1, dp, dF, dp, pd,
-                    seeds.get(SITE_DROP2, 0), N, Np, d, dp)
-    off.run(lambda: K.layernorm_bwd_params(dX2, dp, ctx.Z2, dp, ctx.mean2, ctx.rstd2, dF, dp, N, d, dp, ws, g.n2_w,
-                                           g.n2_b, g.l2_b), dX2, ctx.Z2, ctx.mean2, ctx.rstd2, dF, ws)
-    # FFN: Z2 = X1 + drop(Hd W2^T + b2), Hd = drop(relu(X1 W1^T + b1))
-    dH = torch.empty(Np, ffp, device=dev, dtype=f32)
-    K.gemm(dF, w.W2, dH, Np, ffp, dp, dp, ffp, ffp, epilogue=E.EPI_RELU_DROP_BWD, aux0=ctx.Hd, ld_aux=ffp,
-           p_drop=pd, precision=_rp("ffn2_dx", prec), flops=2.0 * N * d * ff)
-    off.run(lambda: _wgrad(dF, dp, ctx.Hd, ffp, dp, ffp, Np, g.l2_w, (dp, d), (ffp, ff), _rp("ffn2_dw", prec), N), dF, ctx.Hd)
-    _gemm_split(dH, w.W1, dX1, Np, dp, ffp, ffp, dp, dp, accumulate=True, prec=_rp("ffn1_dx", prec), flops=2.0 * N * d * ff)
-
-    def ffn1_grads(dH=dH):
-        _wgrad(dH, ffp, ctx.X1, dp, ffp, dp, Np, g.l1_w, (ffp, ff), (dp, d), _rp("ffn1_dw", prec), N)
-        _bias_grad(dH, Np, ffp, ffp, (ffp, ff), g.l1_b)
-    off.run(ffn1_grads, dH, ctx.X1)
-    del dH, dF
-    # LN1 backward -> dX (residual), dA (dropout1 branch)
-    dX = torch.empty(Np, dp, device=dev, dtype=f32)
-    dA = torch.empty(Np, dp, device=dev, dtype=f32)
     use_ln_delta = ln_delta(_rp("ds", prec))
-    if use_ln_delta:   # LayerNorm1's backward also forms the attention backward's delta = rowsum(dO * O)
+    if small_attn(d):
+        # the row-local tail in one launch: dX1, dF, dH, dX, dA, dO and delta (encoder_layer.cpp layer_bwd); the
+        # parameter gradients on the side stream in the matrix-core branch's order
+        dX1, dF, dA, dO, dX = (torch.empty(Np, dp, device=dev, dtype=f32) for _ in range(5))
+        dH = torch.empty(Np, ffp, device=dev, dtype=f32)
         delta = torch.empty(Np, device=dev, dtype=f32)
-        K.layernorm_bwd_delta(dX1, dp, ctx.Z1, dp, ctx.mean1, ctx.rstd1, p.n1_w, dX, dp, dA, dp, pd,
-                              seeds.get(SITE_DROP1, 0), N, Np, d, dp, ctx.X, dp, w.b_o, delta)
+        K.layer_tail_small(True, N, Np, d, dp, ff, ffp, pd, (seeds.get(SITE_DROP1, 0), seeds.get(SITE_DROPFF, 0),
+                           seeds.get(SITE_DROP2, 0)), W_o=w.W_o, b_o=w.b_o, n1_w=p.n1_w, n1_b=p.n1_b, W1=w.W1,
+                           b1=w.b1, W2=w.W2, b2=w.b2, n2_w=p.n2_w, n2_b=p.n2_b, O=ctx.O, Z1=ctx.Z1, X1=ctx.X1,
+                           mean1=ctx.mean1, rstd1=ctx.rstd1, Hd=ctx.Hd, Z2=ctx.Z2, mean2=ctx.mean2, rstd2=ctx.rstd2,
+                           dX2=dX2, dX1=dX1, dF=dF, dH=dH, dX=dX, dA=dA, dO=dO, delta=delta)
+        off.run(lambda: K.layernorm_bwd_params(dX2, dp, ctx.Z2, dp, ctx.mean2, ctx.rstd2, dF, dp, N, d, dp, ws, g.n2_w,
+                                               g.n2_b, g.l2_b), dX2, ctx.Z2, ctx.mean2, ctx.rstd2, dF, ws)
+        off.run(lambda: _wgrad(dF, dp, ctx.Hd, ffp, dp, ffp, Np, g.l2_w, (dp, d), (ffp, ff), _rp("ffn2_dw", prec), N),
+                dF, ctx.Hd)
+
+        def ffn1_grads_t(dH=dH):
+            _wgrad(dH, ffp, ctx.X1, dp, ffp, dp, Np, g.l1_w, (ffp, ff), (dp, d), _rp("ffn1_dw", prec), N)
+            _bias_grad(dH, Np, ffp, ffp, (ffp, ff), g.l1_b)
+        off.run(ffn1_grads_t, dH, ctx.X1)
+        off.run(lambda: K.layernorm_bwd_params(dX1, dp, ctx.Z1, dp, ctx.mean1, ctx.rstd1, dA, dp, N, d, dp, ws, g.n1_w,
+                                               g.n1_b, g.out_b), dX1, ctx.Z1, ctx.mean1, ctx.rstd1, dA)
+        off.run(lambda: _wgrad(dA, dp, ctx.O, dp, dp, dp, Np, g.out_w, (dp, d), (dp, d), _rp("out_dw", prec), N), dA, ctx.O)
+        del dH, dF, dX1, dA
+        use_ln_delta = True   # delta from the tail kernel
     else:
-        K.layernorm_bwd(dX1, dp, ctx.Z1, dp, ctx.mean1, ctx.rstd1, p.n1_w, dX, dp, dA, dp, pd,
-                        seeds.get(SITE_DROP1, 0), N, Np, d, dp)
-    off.run(lambda: K.layernorm_bwd_params(dX1, dp, ctx.Z1, dp, ctx.mean1, ctx.rstd1, dA, dp, N, d, dp, ws, g.n1_w,
-                                           g.n1_b, g.out_b), dX1, ctx.Z1, ctx.mean1, ctx.rstd1, dA)
-    del dX1
-    # out-projection
-    dO = torch.empty(Np, dp, device=dev, dtype=f32)
-    K.gemm(dA, w.W_o, dO, Np, dp, dp, dp, dp, dp, precision=_rp("out_dx", prec), flops=2.0 * N * d * d)
-    off.run(lambda: _wgrad(dA, dp, ctx.O, dp, dp, dp, Np, g.out_w, (dp, d), (dp, d), _rp("out_dw", prec), N), dA, ctx.O)
-    del dA
+        # LN2 backward -> dX1 (residual branch), dF (dropout2 branch); norm2 + linear2.bias grads
+        dX1 = torch.empty(Np, dp, device=dev, dtype=f32)
+        dF = torch.empty(Np, dp, device=dev, dtype=f32)
+        K.layernorm_bwd(dX2, dp, ctx.Z2, dp, ctx.mean2, ctx.rstd2, p.n2_w, dX1, dp, dF, dp, pd,
+                        seeds.get(SITE_DROP2, 0), N, Np, d, dp)
+        off.run(lambda: K.layernorm_bwd_params(dX2, dp, ctx.Z2, dp, ctx.mean2, ctx.rstd2, dF, dp, N, d, dp, ws, g.n2_w,
+                                               g.n2_b, g.l2_b), dX2, ctx.Z2, ctx.mean2, ctx.rstd2, dF, ws)
+        # FFN: Z2 = X1 + drop(Hd W2^T + b2), Hd = drop(relu(X1 W1^T + b1))
+        dH = torch.empty(Np, ffp, device=dev, dtype=f32)
+        K.gemm(dF, w.W2, dH, Np, ffp, dp, dp, ffp, ffp, epilogue=E.EPI_RELU_DROP_BWD, aux0=ctx.Hd, ld_aux=ffp,
+               p_drop=pd, precision=_rp("ffn2_dx", prec), flops=2.0 * N * d * ff)
+        off.run(lambda: _wgrad(dF, dp, ctx.Hd, ffp, dp, ffp, Np, g.l2_w, (dp, d), (ffp, ff), _rp("ffn2_dw", prec), N), dF, ctx.Hd)
+        _gemm_split(dH, w.W1, dX1, Np, dp, ffp, ffp, dp, dp, accumulate=True, prec=_rp("ffn1_dx", prec), flops=2.0 * N * d * ff)
+
+        def ffn1_grads(dH=dH):
+            _wgrad(dH, ffp, ctx.X1, dp, ffp, dp, Np, g.l1_w, (ffp, ff), (dp, d), _rp("ffn1_dw", prec), N)
+            _bias_grad(dH, Np, ffp, ffp, (ffp, ff), g.l1_b)
+        off.run(ffn1_grads, dH, ctx.X1)
+        del dH, dF
+        # LN1 backward -> dX (residual), dA (dropout1 branch)
+        dX = torch.empty(Np, dp, device=dev, dtype=f32)
+        dA = torch.empty(Np, dp, device=dev, dtype=f32)
+        if use_ln_delta:   # LayerNorm1's backward also forms the attention backward's delta = rowsum(dO * O)
+            delta = torch.empty(Np, device=dev, dtype=f32)
+            K.layernorm_bwd_delta(dX1, dp, ctx.Z1, dp, ctx.mean1, ctx.rstd1, p.n1_w, dX, dp, dA, dp, pd,
+                                  seeds.get(SITE_DROP1, 0), N, Np, d, dp, ctx.X, dp, w.b_o, delta)
+        else:
+            K.layernorm_bwd(dX1, dp, ctx.Z1, dp, ctx.mean1, ctx.rstd1, p.n1_w, dX, dp, dA, dp, pd,
+                            seeds.get(SITE_DROP1, 0), N, Np, d, dp)
+        off.run(lambda: K.layernorm_bwd_params(dX1, dp, ctx.Z1, dp, ctx.mean1, ctx.rstd1, dA, dp, N, d, dp, ws, g.n1_w,
+                                               g.n1_b, g.out_b), dX1, ctx.Z1, ctx.mean1, ctx.rstd1, dA)
+        del dX1
+        # out-projection
+        dO = torch.empty(Np, dp, device=dev, dtype=f32)
+        K.gemm(dA, w.W_o, dO, Np, dp, dp, dp, dp, dp, precision=_rp("out_dx", prec), flops=2.0 * N * d * d)
+        off.run(lambda: _wgrad(dA, dp, ctx.O, dp, dp, dp, Np, g.out_w, (dp, d), (dp, d), _rp("out_dw", prec), N), dA, ctx.O)
+        del dA
     # attention core
     QKV = ctx.QKV
     if not use_ln_delta:
@@ -529,8 +564,9 @@ def encoder_layer_backward(dX2: torch.Tensor, ctx: EncoderLayerCtx, w: PackedLay
         # d <= 32: dQ, dK, dV with P recomputed from the saved context (ctx.Pd: row statistics + compact Q, K, V)
         dQKV = torch.empty(Np, 3 * dp, device=dev, dtype=f32)
         ws_a = torch.empty(K.attn_small_ws_floats(N, Np, d), device=dev, dtype=f32)
-        K.attn_small_bwd(ctx.Pd, dp, d, N, Np, pd, seeds.get(SITE_ATTN, 0), dO, dp, delta, 1.0 / math.sqrt(d),
-                         dQKV, 3 * dp, ws_a)
+        # ... and the in-projection's dX += dQKV W_in (no dX product in _in_proj_backward)
+        K.attn_small_bwd(ctx.Pd, w.W_in, dp, d, N, Np, pd, seeds.get(SITE_ATTN, 0), dO, dp, delta, 1.0 / math.sqrt(d),
+                         dQKV, 3 * dp, dX if need_dx else None, dp, ws_a)
         del ws_a, dO
     else:
         dQKV = _attn_bwd_products(ctx, dO, delta, N, Np, d, dp, pd, att, prec, dev)
@@ -562,7 +598,7 @@ def _attn_bwd_products(ctx, dO, delta, N, Np, d, dp, pd, att, prec, dev):
 def _in_proj_backward(dQKV, dX, ctx, w, g, N, Np, d, dp, prec, off, need_dx):
     """dX += dQKV W_in (skipped when the input gradient is not wanted); the in-projection's weight and bias
     gradients (on the side stream unless this is the last layer of the backward)."""
-    if need_dx:
+    if need_dx and not small_attn(d):   # (the small-width attention backward adds dQKV W_in itself)
         _gemm_split(dQKV, w.W_in, dX, Np, dp, 3 * dp, 3 * dp, dp, dp, accumulate=True, prec=_rp("in_dx", prec),
                     flops=6.0 * N * d * d)
 

@@ -443,23 +443,44 @@ def attn_small_ws_floats(n_valid, rows_pad, d):
     return int(hip_lib().u2gnn_attn_small_ws_floats(int(n_valid), int(rows_pad), int(d)))
 
 
-def attn_small_fwd(QKV, ld_qkv, dp, d, n_valid, rows_pad, p, seed, O, ldo, ctx):
-    """ABI v15 (d <= 32): O = dropout(softmax(Q K^T)) V on the vector ALUs, flash-style, and the forward
-    context ctx [attn_small_ctx_floats(rows_pad, d)]: the row statistics ctx[:2 rows_pad].view(rows_pad, 2) =
-    (max log2 e, 1 / sum exp) the backward recomputes P from, then a compact copy of Q, K, V."""
-    _dev(QKV, O, ctx)
-    check(hip_lib().u2gnn_attn_small_fwd(_p(QKV), int(ld_qkv), int(dp), int(d), int(n_valid), int(rows_pad), float(p),
-                                         int(seed) & 0xFFFFFFFFFFFFFFFF, _p(O), int(ldo), _p(ctx), int(ctx.numel()),
-                                         _s()), "u2gnn_attn_small_fwd")
+def attn_small_fwd(X, ldx, W_in, b_in, dp, d, n_valid, rows_pad, p, seed, O, ldo, ctx):
+    """ABI v15 (d <= 32): the in-projection of X (W_in [3 dp, dp], b_in [3 dp] padded) and O = dropout(softmax(Q
+    K^T)) V on the vector ALUs, flash-style, with the forward context ctx [attn_small_ctx_floats(rows_pad, d)]:
+    the row statistics ctx[:2 rows_pad].view(rows_pad, 2) = (max log2 e, 1 / sum exp) the backward recomputes P
+    from, then a compact copy of Q (scaled by 1/sqrt(d)), K, V."""
+    _dev(X, W_in, b_in, O, ctx)
+    check(hip_lib().u2gnn_attn_small_fwd(_p(X), int(ldx), _p(W_in), _p(b_in), int(dp), int(d), int(n_valid),
+                                         int(rows_pad), float(p), int(seed) & 0xFFFFFFFFFFFFFFFF, _p(O), int(ldo),
+                                         _p(ctx), int(ctx.numel()), _s()), "u2gnn_attn_small_fwd")
 
 
-def attn_small_bwd(ctx, dp, d, n_valid, rows_pad, p, seed, dO, ld_do, delta, q_scale, dQKV, ld_dqkv, ws):
-    """ABI v15 (d <= 32): dQKV = (q_scale dS K, dS^T Q, Pd^T dO) with P recomputed from the forward's ctx."""
-    _dev(ctx, dO, delta, dQKV, ws)
-    check(hip_lib().u2gnn_attn_small_bwd(_p(ctx), int(ctx.numel()), int(dp), int(d), int(n_valid), int(rows_pad),
-                                         float(p), int(seed) & 0xFFFFFFFFFFFFFFFF, _p(dO), int(ld_do), _p(delta),
-                                         float(q_scale), _p(dQKV), int(ld_dqkv), _p(ws), int(ws.numel()), _s()),
-          "u2gnn_attn_small_bwd")
+def attn_small_bwd(ctx, W_in, dp, d, n_valid, rows_pad, p, seed, dO, ld_do, delta, q_scale, dQKV, ld_dqkv, dX, lddx,
+                   ws):
+    """ABI v15 (d <= 32): dQKV = (q_scale dS K, dS^T Q, Pd^T dO) with P recomputed from the forward's ctx, and
+    dX += dQKV W_in unless dX is None."""
+    _dev(ctx, W_in, dO, delta, dQKV, dX, ws)
+    check(hip_lib().u2gnn_attn_small_bwd(_p(ctx), int(ctx.numel()), _p(W_in), int(dp), int(d), int(n_valid),
+                                         int(rows_pad), float(p), int(seed) & 0xFFFFFFFFFFFFFFFF, _p(dO), int(ld_do),
+                                         _p(delta), float(q_scale), _p(dQKV), int(ld_dqkv), _p(dX), int(lddx),
+                                         _p(ws), int(ws.numel()), _s()), "u2gnn_attn_small_bwd")
+
+
+def layer_tail_small(backward, N, Np, d, dp, ff, ffp, p, seeds, **t):
+    """ABI v15 (d <= 32): the row-local tail of an encoder layer in one launch each way (layer_small.hip).
+    seeds = (drop1, dropff, drop2); t: the tensors of u2gnn_small_tail_args by field name (weights in the
+    padded layouts, LayerNorm parameters [d]).  Forward: O, X -> Z1, X1, mean1, rstd1, Hd, Z2, X2, mean2, rstd2;
+    backward: dX2 and the forward tensors -> dX1, dF, dH, dX, dA, dO, delta."""
+    _dev(*t.values())
+    a = _lib.SmallTailArgs()
+    a.n_valid, a.rows_pad, a.d, a.dp, a.ff, a.ffp = int(N), int(Np), int(d), int(dp), int(ff), int(ffp)
+    a.p, a.eps = float(p), 1e-5
+    a.seed_drop1, a.seed_dropff, a.seed_drop2 = [int(x) & 0xFFFFFFFFFFFFFFFF for x in seeds]
+    for k, v in t.items():
+        if k not in _lib._TAIL_PTRS:
+            raise _lib.U2GNNNativeError(f"layer_tail_small: unknown tensor {k}")
+        setattr(a, k, None if v is None else v.data_ptr())
+    fn = hip_lib().u2gnn_layer_tail_small_bwd if backward else hip_lib().u2gnn_layer_tail_small_fwd
+    check(fn(ctypes.byref(a), _s()), "u2gnn_layer_tail_small_" + ("bwd" if backward else "fwd"))
 
 
 def sampled_softmax_bwd_rows(X, ldx, labels, sample_ids, S, W, ldw, prob, dloss, dX, lddx, dW_lab, dW_smp, n_rows, D):

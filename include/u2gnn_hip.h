@@ -418,25 +418,54 @@ int u2gnn_attn_softmax_pv(const float *S, int64_t lds, const float *rowpart, int
                           float *ws, int64_t ws_floats, int64_t n_valid, int64_t rows_pad, float p, uint64_t seed,
                           int32_t precision, void *stream);
 
-/* ---- ABI v15: node-axis attention for small widths d <= 32 (a3.2 forward + backward; the UnSup encoders) ----
- * Exact fp32 on the vector ALUs, flash-style: no N x N image is stored.  QKV [rows_pad][ld_qkv] is the
- * in-projection output (Q pre-scaled by 1/sqrt(d) at column 0, K at dp, V at 2 dp; dp % 64 == 0, padding
- * columns zero); keys / queries n < n_valid take part, keep = keep(seed, m, n) as every dropout site.
- * fwd: O[m] = sum_n keep P[m,n] / (1-p) V[n] with P = softmax_n(Q[m].K[n]) (rows >= n_valid and columns >= d
- *      written 0), and the forward context ctx (u2gnn_attn_small_ctx_floats(rows_pad, d) floats, 16-byte
- *      aligned): ctx[2m], ctx[2m+1] = (max_n Q[m].K[n] log2 e, 1 / sum_n exp) -- what the backward recomputes P
- *      from -- followed by a compact copy of Q, K, V (rows >= n_valid zero), so the backward needs no QKV.
+/* ---- ABI v15: in-projection + node-axis attention for small widths d <= 32 (a3.1 + a3.2 forward and backward;
+ * the UnSup encoders) -- exact fp32 on the vector ALUs, flash-style: no N x N image and no [rows_pad][3 dp] QKV
+ * image are stored.  Keys / queries n < n_valid take part, keep = keep(seed, m, n) as every dropout site.
+ * fwd: (Q, K, V) = X W_in^T + b_in with Q scaled by 1/sqrt(d) (X [rows_pad][ldx], d real columns, the rest zero;
+ *      W_in [3 dp][dp] and b_in [3 dp] in the executor's padded layout, dp = 64), then O[m] = sum_n keep P[m,n] /
+ *      (1-p) V[n] with P = softmax_n(Q[m].K[n]) (rows >= n_valid and columns >= d written 0), and the forward
+ *      context ctx (u2gnn_attn_small_ctx_floats(rows_pad, d) floats, 16-byte aligned): ctx[2m], ctx[2m+1] =
+ *      (max_n Q[m].K[n] log2 e, 1 / sum_n exp) -- what the backward recomputes P from -- followed by a compact
+ *      copy of Q, K, V (rows >= n_valid zero).
  * bwd: given the forward's ctx (unchanged), dO and delta[m] = rowsum(dO[m] * O[m]): dQKV (all 3 dp columns of
  *      every row written; padding 0) = (q_scale * dS K, dS^T Q, Pd^T dO) with dS = P o (keep dO.V^T / (1-p) -
- *      delta), Pd = keep P / (1-p).  ws: u2gnn_attn_small_ws_floats(n_valid, rows_pad, d) floats of scratch
- *      (per-query records), 16-byte aligned.  Both return -1 for d > 32 (the matrix-core path's widths). */
+ *      delta), Pd = keep P / (1-p) -- the gradients of the in-projection's (pre-scale) outputs -- and, unless dX
+ *      is NULL, dX[m] += dQKV[m] W_in (the in-projection's input gradient, rows < n_valid, columns < d).
+ *      ws: u2gnn_attn_small_ws_floats(n_valid, rows_pad, d) floats of scratch (per-query records), 16-byte
+ *      aligned.  Both sizing functions return -1 for d > 32 (the matrix-core path's widths). */
 int64_t u2gnn_attn_small_ctx_floats(int64_t rows_pad, int64_t d);
 int64_t u2gnn_attn_small_ws_floats(int64_t n_valid, int64_t rows_pad, int64_t d);
-int u2gnn_attn_small_fwd(const float *QKV, int64_t ld_qkv, int64_t dp, int64_t d, int64_t n_valid, int64_t rows_pad,
-                         float p, uint64_t seed, float *O, int64_t ldo, float *ctx, int64_t ctx_floats, void *stream);
-int u2gnn_attn_small_bwd(const float *ctx, int64_t ctx_floats, int64_t dp, int64_t d, int64_t n_valid,
-                         int64_t rows_pad, float p, uint64_t seed, const float *dO, int64_t ld_do, const float *delta,
-                         float q_scale, float *dQKV, int64_t ld_dqkv, float *ws, int64_t ws_floats, void *stream);
+int u2gnn_attn_small_fwd(const float *X, int64_t ldx, const float *W_in, const float *b_in, int64_t dp, int64_t d,
+                         int64_t n_valid, int64_t rows_pad, float p, uint64_t seed, float *O, int64_t ldo, float *ctx,
+                         int64_t ctx_floats, void *stream);
+int u2gnn_attn_small_bwd(const float *ctx, int64_t ctx_floats, const float *W_in, int64_t dp, int64_t d,
+                         int64_t n_valid, int64_t rows_pad, float p, uint64_t seed, const float *dO, int64_t ld_do,
+                         const float *delta, float q_scale, float *dQKV, int64_t ld_dqkv, float *dX, int64_t lddx,
+                         float *ws, int64_t ws_floats, void *stream);
+
+/* ---- ABI v15: the row-local tail of a small-width encoder layer (d <= 32, dp = 64), one launch each way ----
+ * forward  (a3.3 + a3.4): Z1 = drop1(O W_o^T + b_o) + X, X1 = LayerNorm1(Z1) (mean1, rstd1), Hd = dropff(relu(X1
+ *          W1^T + b1)), Z2 = drop2(Hd W2^T + b2) + X1, X2 = LayerNorm2(Z2) (mean2, rstd2) -- exact fp32, one wave
+ *          per row; rows >= n_valid and padding columns written 0.
+ * backward given dX2 and the forward's tensors: dF = drop2'(LN2^T dX2), dH = (Hd > 0) dF W2 / (1-p), dX1 = LN2^T dX2
+ *          + dH W1, dX = LN1^T dX1 (the residual branch; the in-projection's dX product accumulates onto it), dA =
+ *          drop1'(dX), dO = dA W_o, delta = rowsum(dO * O).  The parameter gradients are the caller's (column sums
+ *          of dF, dH, dA and the LayerNorm terms).
+ * Weights in the executor's padded layouts (W_o [dp][dp], W1 [ffp][dp], W2 [dp][ffp], biases zero-padded to dp /
+ * ffp; LayerNorm gamma / beta unpadded [d]); activations [rows_pad][dp] (Hd, dH: [rows_pad][ffp]);
+ * rows_pad % 8 == 0, ffp % 64 == 0; W_o, W1, O 16-byte aligned. */
+typedef struct u2gnn_small_tail_args {
+    int64_t n_valid, rows_pad, d, dp, ff, ffp;
+    float p, eps;
+    uint64_t seed_drop1, seed_dropff, seed_drop2;
+    const float *W_o, *b_o, *n1_w, *n1_b, *W1, *b1, *W2, *b2, *n2_w, *n2_b;
+    const float *O, *X;                                       /* forward inputs (O also read by the backward) */
+    float *Z1, *X1, *mean1, *rstd1, *Hd, *Z2, *X2, *mean2, *rstd2;   /* forward outputs; the backward reads them */
+    const float *dX2;                                         /* backward input */
+    float *dX1, *dF, *dH, *dX, *dA, *dO, *delta;               /* backward outputs */
+} u2gnn_small_tail_args;
+int u2gnn_layer_tail_small_fwd(const u2gnn_small_tail_args *a, void *stream);
+int u2gnn_layer_tail_small_bwd(const u2gnn_small_tail_args *a, void *stream);
 
 /* ---- a12: dropout on the concatenated UnSup node embeddings (model_U2GNN_Unsup_multi.py:56) --
  * Y[i, j] = X[i, j] * keep(seed, i, j) / (1-p) for i < rows, j < cols.  The backward is the same

@@ -37,7 +37,7 @@ template <int DM> constexpr int sa_kt_b() { return 2048 / DM > 128 ? 2048 / DM /
 constexpr float SA_LOG2E = 1.4426950408889634f;
 // waves per SIMD the register budget is sized for: 4 (128 VGPRs) up to DM = 16, 2 (256) beyond, where the row's
 // q, o / dq / dk, dv arrays alone take 2-3 DM registers (the 128 cap spilled them to scratch)
-template <int DM> constexpr int sa_min_waves() { return DM <= 16 ? 4 : 2; }
+template <int DM> constexpr int sa_min_waves() { return DM <= 12 ? 4 : 2; }
 
 // Layouts (all fp32; DM = d rounded up to a multiple of 4 up to 24, else 32):
 //   ctx (the forward's saved context, u2gnn_attn_small_ctx_floats):  st [Np][2] = (M in log2 units, 1/L) |
@@ -115,22 +115,35 @@ __device__ __forceinline__ float lane_col(const float (&x)[DM], int c) {
 // a row's partial results merge across its lanes (butterfly) and then across its waves (LDS).
 constexpr int SA_SPL = 2, SA_RB = SA_WAVES / SA_SPL;
 
-// stage records [t0, t0 + KT) of a compact [Np][W] array (W = sum of the column widths WA + WB + WC, each a
-// multiple of 4) into the LDS arrays a [KT][WA], b [KT][WB], c [KT][WC]; records at or past Np are zeros
+// Staging of records [t0, t0 + KT) of a compact [Np][W] array (W = WA + WB + WC, each a multiple of 4) into the
+// LDS arrays a [KT][WA], b [KT][WB], c [KT][WC]; records at or past Np are zeros.  In two halves: tile_load
+// issues every global load of the tile into registers (SA_PER float4 per thread, all in flight together) and
+// tile_store writes them to LDS -- so the next tile's loads run under this tile's compute, and a tile costs one
+// load latency instead of one per loop iteration (a load -> ds_write loop waits on every load).
 template <int KT, int WA, int WB, int WC>
-__device__ __forceinline__ void stage_rec(const float *src, int t0, int Np, float (*a)[WA], float (*b)[WB],
-                                          float *c) {
-    constexpr int W4 = (WA + WB + WC) / 4, NE = KT * W4;
-    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int e = threadIdx.x; e < NE; e += SA_NT) {
-        const int t = e / W4, k = 4 * (e % W4);
-        float4 v = z;   // (a branch, not "cond ? *p : z": that selects a pointer to a private copy of z)
-        if (t0 + t < Np) v = *reinterpret_cast<const float4 *>(src + (int64_t)t0 * (4 * W4) + 4 * (int64_t)e);
-        if (k < WA) *reinterpret_cast<float4 *>(&a[t][k]) = v;
-        else if (k < WA + WB) *reinterpret_cast<float4 *>(&b[t][k - WA]) = v;
-        else *reinterpret_cast<float4 *>(c + t * WC + k - WA - WB) = v;
+struct Tile {
+    static constexpr int W4 = (WA + WB + WC) / 4, NE = KT * W4, PER = (NE + SA_NT - 1) / SA_NT;
+    float4 v[PER];
+    __device__ __forceinline__ void load(const float *src, int t0, int Np) {
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int e = threadIdx.x + i * SA_NT, t = e / W4;
+            v[i] = make_float4(0.f, 0.f, 0.f, 0.f);   // (a branch, not "cond ? *p : z": no private copy of z)
+            if (e < NE && t0 + t < Np) v[i] = *reinterpret_cast<const float4 *>(src + (int64_t)t0 * (4 * W4) + 4 * (int64_t)e);
+        }
     }
-}
+    __device__ __forceinline__ void store(float (*a)[WA], float (*b)[WB], float *c) const {
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int e = threadIdx.x + i * SA_NT;
+            if (e >= NE) break;
+            const int t = e / W4, k = 4 * (e % W4);
+            if (k < WA) *reinterpret_cast<float4 *>(&a[t][k]) = v[i];
+            else if (k < WA + WB) *reinterpret_cast<float4 *>(&b[t][k - WA]) = v[i];
+            else *reinterpret_cast<float4 *>(c + t * WC + k - WA - WB) = v[i];
+        }
+    }
+};
 
 // ---- a3.1 in-projection straight into the compact context: (Q, K, V) = X W_in^T + b_in, Q scaled by 1/sqrt(d)
 // (the bias epilogue's order: (acc + b) * scale); rows >= N zero.  One thread per 4 output columns of a row.
@@ -166,6 +179,7 @@ template <int DM>
 __global__ void __launch_bounds__(SA_NT, sa_min_waves<DM>()) sa_fwd_kernel(SaP P) {
     constexpr int SA_KT = sa_kt_f<DM>();
     constexpr int PART = SA_KT / SA_SPL, NP = PART / 128;   // keys per wave per tile; key pairs per lane
+    constexpr int CU = DM <= 8 ? 8 : 4;   // keys per lane between rescales (their K rows are live in registers)
     static_assert(NP >= 1 && PART % 128 == 0, "a wave's part of the key tile: whole 128-key rounds");
     __shared__ __attribute__((aligned(16))) float ks[SA_KT][DM];
     __shared__ __attribute__((aligned(16))) float vs[SA_KT][DM];
@@ -182,18 +196,21 @@ __global__ void __launch_bounds__(SA_NT, sa_min_waves<DM>()) sa_fwd_kernel(SaP P
     const bool drop = P.p > 0.f;
     const uint32_t thr = u2gnn_keep_thr(P.p), rk = u2gnn_row_key(seed, (uint32_t)i);
     float m = -INFINITY, l = 0.f;
+    Tile<SA_KT, DM, DM, 0> tl;
+    tl.load(kvc, 0, P.Np);
     for (int t0 = 0; t0 < P.N; t0 += SA_KT) {
         __syncthreads();
-        stage_rec<SA_KT, DM, DM, 0>(kvc, t0, P.Np, ks, vs, nullptr);
+        tl.store(ks, vs, nullptr);
         __syncthreads();
+        if (t0 + SA_KT < P.N) tl.load(kvc, t0 + SA_KT, P.Np);   // the next tile, in flight under this one
         if (!live) continue;
-        // this wave's keys of the tile: pairs (t0 + sp PART + 128 h + 2 lane, +1); four pairs per rescale
+        // this wave's keys of the tile: pairs (t0 + sp PART + 128 h + 2 lane, +1); CU / 2 pairs per rescale
 #pragma unroll 1
-        for (int h0 = 0; h0 < NP; h0 += 4) {
-            float s[8];
+        for (int h0 = 0; h0 < NP; h0 += CU / 2) {
+            float s[CU];
             float cm = -INFINITY;
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
+            for (int u = 0; u < CU; ++u) {
                 const int t = sp * PART + 128 * (h0 + u / 2) + 2 * lane + (u & 1);
                 const float x = dot_lds<DM>(q, ks[t]) * SA_LOG2E;   // rows past N are zeros: finite
                 s[u] = (h0 + u / 2 < NP && t0 + t < P.N) ? x : -INFINITY;
@@ -206,7 +223,7 @@ __global__ void __launch_bounds__(SA_NT, sa_min_waves<DM>()) sa_fwd_kernel(SaP P
 #pragma unroll
             for (int c = 0; c < DM; ++c) o[c] *= sc;
 #pragma unroll
-            for (int u = 0; u < 8; u += 2) {
+            for (int u = 0; u < CU; u += 2) {
                 const int t = sp * PART + 128 * (h0 + u / 2) + 2 * lane;
                 bool k0 = true, k1 = true;
                 if (drop) {
@@ -305,10 +322,13 @@ __global__ void __launch_bounds__(SA_NT, sa_min_waves<DM>()) sa_bwd_q_kernel(SaP
         *reinterpret_cast<float4 *>(r + 2 * DM) = make_float4(M, iL, dl, __uint_as_float(rk));
     }
     const float *kvc = sa_kvc<DM>(P.ctx, P.Np);
+    Tile<SA_KT, DM, DM, 0> tl;
+    tl.load(kvc, 0, P.Np);
     for (int t0 = 0; t0 < P.N; t0 += SA_KT) {
         __syncthreads();
-        stage_rec<SA_KT, DM, DM, 0>(kvc, t0, P.Np, ks, vs, nullptr);
+        tl.store(ks, vs, nullptr);
         __syncthreads();
+        if (t0 + SA_KT < P.N) tl.load(kvc, t0 + SA_KT, P.Np);
         if (!live) continue;
 #pragma unroll 2
         for (int h = 0; h < NP; ++h) {
@@ -384,10 +404,13 @@ __global__ void __launch_bounds__(SA_NT, sa_min_waves<DM>()) sa_bwd_kv_kernel(Sa
     const float s1p = drop ? 1.f / (1.f - P.p) : 1.f;
     const uint32_t thr = u2gnn_keep_thr(P.p), jc = (uint32_t)j0 >> 1;
     const bool odd = j0 & 1;   // (KP = 2: j0 even)
+    Tile<SA_KT, DM, DM, 4> tl;
+    tl.load(P.rq, 0, P.Np);
     for (int t0 = 0; t0 < P.N; t0 += SA_KT) {
         __syncthreads();
-        stage_rec<SA_KT, DM, DM, 4>(P.rq, t0, P.Np, qs, gs, &rs[0][0]);
+        tl.store(qs, gs, &rs[0][0]);
         __syncthreads();
+        if (t0 + SA_KT < P.N) tl.load(P.rq, t0 + SA_KT, P.Np);
         if (!live) continue;
 #pragma unroll 2
         for (int u = 0; u < NU; ++u) {

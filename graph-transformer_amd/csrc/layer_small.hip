@@ -49,26 +49,54 @@ __device__ __forceinline__ float pick(const float (&v)[DM], int c) {
     return r;
 }
 
-// stage hidden units [h0, h0 + HC) of W1 [ffp][dp] (rows, first DM columns) and W2 [dp][ffp] (first DM rows,
-// transposed) and b1 into LDS; units at or past ffp are zeros
+// Staging of hidden units [h0, h0 + HC): W1 [ffp][dp] (rows, first DM columns), W2 [dp][ffp] (first DM rows,
+// transposed: w2s[h][c] = W2[c][h]) and, for the forward, b1 into LDS; units at or past ffp are zeros.  load()
+// issues every global load of the chunk into registers (all in flight together), store() writes them to LDS:
+// one load latency per chunk instead of one per loop iteration (a load -> ds_write loop waits on every load).
 template <int DM, int HC, bool BIAS>
-__device__ __forceinline__ void ls_stage(const LsP &P, int h0, float (*w1s)[DM], float (*w2s)[DM], float *b1s) {
-    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-    constexpr int C4 = DM / 4;
-    for (int e = threadIdx.x; e < HC * C4; e += LS_NT) {
-        const int h = e / C4, c = 4 * (e % C4);
-        float4 v = z;
-        if (h0 + h < P.ffp) v = *reinterpret_cast<const float4 *>(P.a.W1 + (int64_t)(h0 + h) * P.dp + c);
-        *reinterpret_cast<float4 *>(&w1s[h][c]) = v;
+struct Stage {
+    static constexpr int C4 = DM / 4, N1 = HC * C4, N2 = DM * (HC / 4), N3 = BIAS ? HC / 4 : 0;
+    static constexpr int P1 = (N1 + LS_NT - 1) / LS_NT, P2 = (N2 + LS_NT - 1) / LS_NT, P3 = (N3 + LS_NT - 1) / LS_NT;
+    float4 a[P1], b[P2], c[P3 > 0 ? P3 : 1];
+    __device__ __forceinline__ void load(const LsP &P, int h0) {
+        const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int i = 0; i < P1; ++i) {
+            const int e = threadIdx.x + i * LS_NT, h = e / C4, k = 4 * (e % C4);
+            a[i] = z;
+            if (e < N1 && h0 + h < P.ffp) a[i] = *reinterpret_cast<const float4 *>(P.a.W1 + (int64_t)(h0 + h) * P.dp + k);
+        }
+#pragma unroll
+        for (int i = 0; i < P2; ++i) {   // W2 row k, 4 consecutive hidden units: coalesced
+            const int e = threadIdx.x + i * LS_NT, k = e / (HC / 4), h = 4 * (e % (HC / 4));
+            b[i] = z;
+            if (e < N2 && h0 + h < P.ffp) b[i] = *reinterpret_cast<const float4 *>(P.a.W2 + (int64_t)k * P.ffp + h0 + h);
+        }
+#pragma unroll
+        for (int i = 0; i < P3; ++i) {
+            const int e = threadIdx.x + i * LS_NT, h = 4 * e;
+            c[i] = z;
+            if (e < N3 && h0 + h < P.ffp) c[i] = *reinterpret_cast<const float4 *>(P.a.b1 + h0 + h);
+        }
     }
-    // W2 row c is contiguous over the hidden units: coalesced reads, transposed LDS writes
-    for (int e = threadIdx.x; e < HC * DM; e += LS_NT) {
-        const int c = e / HC, h = e % HC;
-        w2s[h][c] = h0 + h < P.ffp ? P.a.W2[(int64_t)c * P.ffp + h0 + h] : 0.f;
+    __device__ __forceinline__ void store(float (*w1s)[DM], float (*w2s)[DM], float *b1s) const {
+#pragma unroll
+        for (int i = 0; i < P1; ++i) {
+            const int e = threadIdx.x + i * LS_NT;
+            if (e < N1) *reinterpret_cast<float4 *>(&w1s[e / C4][4 * (e % C4)]) = a[i];
+        }
+#pragma unroll
+        for (int i = 0; i < P2; ++i) {
+            const int e = threadIdx.x + i * LS_NT, k = e / (HC / 4), h = 4 * (e % (HC / 4));
+            if (e < N2) w2s[h][k] = b[i].x, w2s[h + 1][k] = b[i].y, w2s[h + 2][k] = b[i].z, w2s[h + 3][k] = b[i].w;
+        }
+#pragma unroll
+        for (int i = 0; i < P3; ++i) {
+            const int e = threadIdx.x + i * LS_NT;
+            if (e < N3) *reinterpret_cast<float4 *>(b1s + 4 * e) = c[i];
+        }
     }
-    if constexpr (BIAS)
-        for (int h = threadIdx.x; h < HC; h += LS_NT) b1s[h] = h0 + h < P.ffp ? P.a.b1[h0 + h] : 0.f;
-}
+};
 
 // post-LN of one row held as lane c < d: returns y_c (0 past d), the row's mean and 1/std
 __device__ __forceinline__ float ln_row(float z, int lane, int d, float eps, const float *gamma, const float *beta,
@@ -144,8 +172,10 @@ __global__ void __launch_bounds__(LS_NT, ls_min_waves<DM>()) ls_fwd_kernel(LsP P
     const uint32_t rkf = u2gnn_row_key(sff, (uint32_t)r);
     float *hrow = A.Hd + (int64_t)r * P.ffp;
     for (int h0 = 0; h0 < P.ffp; h0 += HC) {
+        Stage<DM, HC, true> sg;
+        sg.load(P, h0);
         __syncthreads();
-        ls_stage<DM, HC, true>(P, h0, w1s, w2s, b1s);
+        sg.store(w1s, w2s, b1s);
         __syncthreads();
 #pragma unroll 4
         for (int u = 0; u < NU; ++u) {
@@ -215,14 +245,19 @@ __global__ void __launch_bounds__(LS_NT, ls_min_waves<DM>()) ls_bwd_kernel(LsP P
     const float *hrow = A.Hd + (int64_t)r * P.ffp;
     float *dhrow = A.dH + (int64_t)r * P.ffp;
     for (int h0 = 0; h0 < P.ffp; h0 += HC) {
+        Stage<DM, HC, false> sg;
+        sg.load(P, h0);
+        float hvs[NU];   // this row's ReLU image of the chunk, loaded with the weights
+#pragma unroll
+        for (int u = 0; u < NU; ++u) hvs[u] = h0 + 64 * u + lane < P.ffp ? hrow[h0 + 64 * u + lane] : 0.f;
         __syncthreads();
-        ls_stage<DM, HC, false>(P, h0, w1s, w2s, nullptr);
+        sg.store(w1s, w2s, nullptr);
         __syncthreads();
 #pragma unroll 4
         for (int u = 0; u < NU; ++u) {
             const int h = 64 * u + lane;
             if (h0 + h >= P.ffp) break;
-            const float hv = hrow[h0 + h];
+            const float hv = hvs[u];
             float g = 0.f;
 #pragma unroll
             for (int k = 0; k < DM; k += 4) {

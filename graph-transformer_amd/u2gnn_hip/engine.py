@@ -20,6 +20,7 @@ Padding rows/columns hold zeros in every activation and gradient the encoder pro
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
 
@@ -180,7 +181,7 @@ def side_stream(dev: torch.device) -> "torch.cuda.Stream":
 # 0.31 ms of a 3.27 ms step; at C5 (U2GNN-UnSup REDDIT, d = 4: Np*dp = 0.13M, ~2-10 us kernels) the
 # cross-stream hand-offs cost more than the overlap gains (1.116 vs 1.19-1.28 ms/step, one session,
 # profiles/r02/r2i_graph_knobs.txt).
-SIDE_MIN_ELEMS = 1 << 20
+SIDE_MIN_ELEMS = int(os.environ.get("U2GNN_SIDE_MIN_ELEMS", 1 << 20))   # (env: A/B experiments only)
 
 
 def fused_ln(dp: int, prec: str) -> bool:

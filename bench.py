@@ -865,10 +865,14 @@ def main():
                       "bf16x3_eval": "every output, loss, gradient and post-Adam parameter within 1e-3 of the "
                                      "reference goldens (MUTAG, MUTAG L2T2, IMDBBINARY) and of the oracle on a full "
                                      "C4 batch (tests/test_sup_parity_gpu.py)",
-                      "bf16x3_train_c4": "with the kernels' dropout masks in the oracle: scores 2.3e-6, loss 1.5e-7, "
-                                         "every gradient but linear1's <= 5.2e-4; linear1 gradients up to 1.7e-2 "
-                                         "(ReLU decisions of pre-activations within the 2^-16 product error of 0); "
-                                         "post-Adam parameters 9.9e-4 (tests/test_train_parity_gpu.py)",
+                      "bf16x3_train_c4": "train mode, the kernels' dropout masks in the oracle, no per-quantity "
+                                         "exception (tests/test_train_parity_gpu.py, DESIGN section 7): with the GPU's "
+                                         "own ReLU decisions every output, gradient and post-Adam parameter within "
+                                         "1.03e-5 / 2.1e-5; the 11 decisions that differ from the plain oracle's are "
+                                         "units with |z| <= 6.2e-6 (forward disagreement 2.2e-5); against the plain "
+                                         "oracle the linear1 gradients are NOT held to 1e-3 (up to 1.7e-2: a switched "
+                                         "boundary unit moves its dW1 row; the reference's own fp32 misses its fp64 "
+                                         "run by up to 2e-2); outputs and loss within 1e-3 of it",
                       "fp32": "within 4.1e-6 in every case and mode; its C4 rate is the 'fp32' object"}}
     if rank == 0:
         out["gather"] = gather_roofline(used[0], d, args.ff_hidden_size, K, dev)

@@ -119,15 +119,41 @@ __device__ __forceinline__ float ln_row_bwd(float dy, float z, float mu, float r
     return ok ? rs * (g - m1 - xh * m2) : 0.f;
 }
 
+// Two work splits.  STAGED (large N, e.g. C5's 2048 rows): 8 rows per workgroup, one wave per row, the weights
+// staged through LDS in chunks of HC hidden units and shared by the 8 rows.  DIRECT (N < 1024 padded rows, e.g.
+// C3's 128: the staged split leaves most CUs idle): one row per workgroup, its 8 waves splitting the hidden units
+// (unit 64 (w + 8 u) + lane), each wave's W1 / W2 / b1 values loaded straight from L2 into registers (no LDS
+// staging, no chunk barriers), the 8 waves' partial sums combined through LDS in wave order.
+template <bool DIRECT> __device__ __forceinline__ int ls_row() {
+    return DIRECT ? (int)blockIdx.x : (int)blockIdx.x * LS_WAVES + (int)(threadIdx.x >> 6);
+}
+
+// one hidden unit of the forward: h = dropff(relu(b1 + x1 . W1[h])), written to Hd; zp += h W2[:, h]
 template <int DM>
+__device__ __forceinline__ void ffn_unit_fwd(const float (&xv)[DM], const float (&w1)[DM], const float (&w2)[DM], float b,
+                                             bool keep, float ks, bool live, float *dst, float (&zp)[DM]) {
+    float a = b;
+#pragma unroll
+    for (int k = 0; k < DM; ++k) a = fmaf(xv[k], w1[k], a);
+    a = fmaxf(a, 0.f);
+    a = keep ? a * ks : 0.f;
+    if (!live) a = 0.f;
+    *dst = a;
+#pragma unroll
+    for (int k = 0; k < DM; ++k) zp[k] = fmaf(a, w2[k], zp[k]);
+}
+
+template <int DM, bool DIRECT>
 __global__ void __launch_bounds__(LS_NT, ls_min_waves<DM>()) ls_fwd_kernel(LsP P) {
-    constexpr int HC = ls_hc<DM>(), NU = HC / 64;
-    __shared__ __attribute__((aligned(16))) float w1s[HC][DM];
-    __shared__ __attribute__((aligned(16))) float w2s[HC][DM];
-    __shared__ float b1s[HC];
+    constexpr int HC = DIRECT ? 64 : ls_hc<DM>(), NU = HC / 64;
+    __shared__ __attribute__((aligned(16))) float w1s[DIRECT ? 1 : HC][DM];
+    __shared__ __attribute__((aligned(16))) float w2s[DIRECT ? 1 : HC][DM];
+    __shared__ float b1s[DIRECT ? 1 : HC];
+    __shared__ float xw[DIRECT ? LS_WAVES : 1][DM];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int r = blockIdx.x * LS_WAVES + w;   // < Np (Np % 8 == 0, host-checked)
+    const int r = ls_row<DIRECT>();   // < Np (Np % 8 == 0, host-checked)
     const bool live = r < P.N;
+    const bool writer = !DIRECT || w == 0;   // DIRECT: every wave computes the row prologue, wave 0 stores it
     const u2gnn_small_tail_args &A = P.a;
     const bool drop = P.p > 0.f;
     const float ks = drop ? 1.f / (1.f - P.p) : 1.f;
@@ -162,45 +188,70 @@ __global__ void __launch_bounds__(LS_NT, ls_min_waves<DM>()) ls_fwd_kernel(LsP P
 #pragma unroll
         for (int k = 0; k < DM; ++k) xv[k] = __shfl(x1, k, 64);
     }
-    A.Z1[ro + lane] = z1;   // dp == 64: one column per lane (padding columns and rows 0)
-    A.X1[ro + lane] = x1;
-    if (lane == 0) A.mean1[r] = mu1, A.rstd1[r] = rs1;
+    if (writer) {
+        A.Z1[ro + lane] = z1;   // dp == 64: one column per lane (padding columns and rows 0)
+        A.X1[ro + lane] = x1;
+        if (lane == 0) A.mean1[r] = mu1, A.rstd1[r] = rs1;
+    }
     // a3.4: h = dropff(relu(x1 W1^T + b1)) over the hidden units, z2 partials = h W2^T
     float zp[DM];
 #pragma unroll
     for (int k = 0; k < DM; ++k) zp[k] = 0.f;
     const uint32_t rkf = u2gnn_row_key(sff, (uint32_t)r);
     float *hrow = A.Hd + (int64_t)r * P.ffp;
-    for (int h0 = 0; h0 < P.ffp; h0 += HC) {
-        Stage<DM, HC, true> sg;
-        sg.load(P, h0);
-        __syncthreads();
-        sg.store(w1s, w2s, b1s);
-        __syncthreads();
-#pragma unroll 4
-        for (int u = 0; u < NU; ++u) {
-            const int h = 64 * u + lane;
-            if (h0 + h >= P.ffp) break;
-            float a = b1s[h];
+    if constexpr (DIRECT) {
+        for (int h = 64 * w + lane; h < P.ffp; h += 64 * LS_WAVES) {
+            float w1[DM], w2[DM];
 #pragma unroll
             for (int k = 0; k < DM; k += 4) {
-                const float4 t = *reinterpret_cast<const float4 *>(&w1s[h][k]);
-                a = fmaf(xv[k], t.x, a), a = fmaf(xv[k + 1], t.y, a), a = fmaf(xv[k + 2], t.z, a), a = fmaf(xv[k + 3], t.w, a);
+                const float4 t = *reinterpret_cast<const float4 *>(A.W1 + (int64_t)h * P.dp + k);
+                w1[k] = t.x, w1[k + 1] = t.y, w1[k + 2] = t.z, w1[k + 3] = t.w;
             }
-            a = fmaxf(a, 0.f);
-            if (drop) a = u2gnn_keep_rk(rkf, (uint32_t)(h0 + h), thr) ? a * ks : 0.f;
-            if (!live) a = 0.f;
-            hrow[h0 + h] = a;
 #pragma unroll
-            for (int k = 0; k < DM; k += 4) {
-                const float4 t = *reinterpret_cast<const float4 *>(&w2s[h][k]);
-                zp[k] = fmaf(a, t.x, zp[k]), zp[k + 1] = fmaf(a, t.y, zp[k + 1]);
-                zp[k + 2] = fmaf(a, t.z, zp[k + 2]), zp[k + 3] = fmaf(a, t.w, zp[k + 3]);
+            for (int k = 0; k < DM; ++k) w2[k] = A.W2[(int64_t)k * P.ffp + h];
+            const bool keep = !drop || u2gnn_keep_rk(rkf, (uint32_t)h, thr);
+            ffn_unit_fwd<DM>(xv, w1, w2, A.b1[h], keep, ks, live, hrow + h, zp);
+        }
+    } else {
+        for (int h0 = 0; h0 < P.ffp; h0 += HC) {
+            Stage<DM, HC, true> sg;
+            sg.load(P, h0);
+            __syncthreads();
+            sg.store(w1s, w2s, b1s);
+            __syncthreads();
+#pragma unroll 4
+            for (int u = 0; u < NU; ++u) {
+                const int h = 64 * u + lane;
+                if (h0 + h >= P.ffp) break;
+                float w1[DM], w2[DM];
+#pragma unroll
+                for (int k = 0; k < DM; k += 4) {
+                    const float4 t = *reinterpret_cast<const float4 *>(&w1s[h][k]);
+                    w1[k] = t.x, w1[k + 1] = t.y, w1[k + 2] = t.z, w1[k + 3] = t.w;
+                    const float4 q = *reinterpret_cast<const float4 *>(&w2s[h][k]);
+                    w2[k] = q.x, w2[k + 1] = q.y, w2[k + 2] = q.z, w2[k + 3] = q.w;
+                }
+                const bool keep = !drop || u2gnn_keep_rk(rkf, (uint32_t)(h0 + h), thr);
+                ffn_unit_fwd<DM>(xv, w1, w2, b1s[h], keep, ks, live, hrow + h0 + h, zp);
             }
         }
     }
 #pragma unroll
     for (int k = 0; k < DM; ++k) zp[k] = wsum(zp[k]);
+    if constexpr (DIRECT) {   // the 8 waves' partials, in wave order
+        if (lane == 0)
+#pragma unroll
+            for (int k = 0; k < DM; ++k) xw[w][k] = zp[k];
+        __syncthreads();
+        if (w != 0) return;
+#pragma unroll
+        for (int k = 0; k < DM; ++k) {
+            float t = xw[0][k];
+#pragma unroll
+            for (int y = 1; y < LS_WAVES; ++y) t += xw[y][k];
+            zp[k] = t;
+        }
+    }
     float z2 = 0.f, x2 = 0.f, mu2 = 0.f, rs2 = 0.f;
     if (live) {
         float v = pick<DM>(zp, lane) + A.b2[lane];
@@ -213,14 +264,29 @@ __global__ void __launch_bounds__(LS_NT, ls_min_waves<DM>()) ls_fwd_kernel(LsP P
     if (lane == 0) A.mean2[r] = mu2, A.rstd2[r] = rs2;
 }
 
+// one hidden unit of the backward: dH = (Hd > 0) dF . W2[:, h] / (1-p), written; xp += dH W1[h]
 template <int DM>
+__device__ __forceinline__ void ffn_unit_bwd(const float (&fv)[DM], const float (&w1)[DM], const float (&w2)[DM], float hv,
+                                             float ks, bool live, float *dst, float (&xp)[DM]) {
+    float g = 0.f;
+#pragma unroll
+    for (int k = 0; k < DM; ++k) g = fmaf(fv[k], w2[k], g);
+    g = (live && hv > 0.f) ? g * ks : 0.f;
+    *dst = g;
+#pragma unroll
+    for (int k = 0; k < DM; ++k) xp[k] = fmaf(g, w1[k], xp[k]);
+}
+
+template <int DM, bool DIRECT>
 __global__ void __launch_bounds__(LS_NT, ls_min_waves<DM>()) ls_bwd_kernel(LsP P) {
-    constexpr int HC = ls_hc<DM>(), NU = HC / 64;
-    __shared__ __attribute__((aligned(16))) float w1s[HC][DM];
-    __shared__ __attribute__((aligned(16))) float w2s[HC][DM];
+    constexpr int HC = DIRECT ? 64 : ls_hc<DM>(), NU = HC / 64;
+    __shared__ __attribute__((aligned(16))) float w1s[DIRECT ? 1 : HC][DM];
+    __shared__ __attribute__((aligned(16))) float w2s[DIRECT ? 1 : HC][DM];
+    __shared__ float xw[DIRECT ? LS_WAVES : 1][DM];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int r = blockIdx.x * LS_WAVES + w;
+    const int r = ls_row<DIRECT>();
     const bool live = r < P.N;
+    const bool writer = !DIRECT || w == 0;
     const u2gnn_small_tail_args &A = P.a;
     const bool drop = P.p > 0.f;
     const float ks = drop ? 1.f / (1.f - P.p) : 1.f;
@@ -237,45 +303,67 @@ __global__ void __launch_bounds__(LS_NT, ls_min_waves<DM>()) ls_bwd_kernel(LsP P
 #pragma unroll
         for (int k = 0; k < DM; ++k) fv[k] = __shfl(df, k, 64);
     }
-    A.dF[ro + lane] = df;
+    if (writer) A.dF[ro + lane] = df;
     // FFN^T: dH = (Hd > 0) dF W2 / (1-p) over the hidden units, dX1 partials = dH W1
     float xp[DM];
 #pragma unroll
     for (int k = 0; k < DM; ++k) xp[k] = 0.f;
     const float *hrow = A.Hd + (int64_t)r * P.ffp;
     float *dhrow = A.dH + (int64_t)r * P.ffp;
-    for (int h0 = 0; h0 < P.ffp; h0 += HC) {
-        Stage<DM, HC, false> sg;
-        sg.load(P, h0);
-        float hvs[NU];   // this row's ReLU image of the chunk, loaded with the weights
-#pragma unroll
-        for (int u = 0; u < NU; ++u) hvs[u] = h0 + 64 * u + lane < P.ffp ? hrow[h0 + 64 * u + lane] : 0.f;
-        __syncthreads();
-        sg.store(w1s, w2s, nullptr);
-        __syncthreads();
-#pragma unroll 4
-        for (int u = 0; u < NU; ++u) {
-            const int h = 64 * u + lane;
-            if (h0 + h >= P.ffp) break;
-            const float hv = hvs[u];
-            float g = 0.f;
+    if constexpr (DIRECT) {
+        for (int h = 64 * w + lane; h < P.ffp; h += 64 * LS_WAVES) {
+            float w1[DM], w2[DM];
 #pragma unroll
             for (int k = 0; k < DM; k += 4) {
-                const float4 t = *reinterpret_cast<const float4 *>(&w2s[h][k]);
-                g = fmaf(fv[k], t.x, g), g = fmaf(fv[k + 1], t.y, g), g = fmaf(fv[k + 2], t.z, g), g = fmaf(fv[k + 3], t.w, g);
+                const float4 t = *reinterpret_cast<const float4 *>(A.W1 + (int64_t)h * P.dp + k);
+                w1[k] = t.x, w1[k + 1] = t.y, w1[k + 2] = t.z, w1[k + 3] = t.w;
             }
-            g = (live && hv > 0.f) ? g * ks : 0.f;
-            dhrow[h0 + h] = g;
 #pragma unroll
-            for (int k = 0; k < DM; k += 4) {
-                const float4 t = *reinterpret_cast<const float4 *>(&w1s[h][k]);
-                xp[k] = fmaf(g, t.x, xp[k]), xp[k + 1] = fmaf(g, t.y, xp[k + 1]);
-                xp[k + 2] = fmaf(g, t.z, xp[k + 2]), xp[k + 3] = fmaf(g, t.w, xp[k + 3]);
+            for (int k = 0; k < DM; ++k) w2[k] = A.W2[(int64_t)k * P.ffp + h];
+            ffn_unit_bwd<DM>(fv, w1, w2, hrow[h], ks, live, dhrow + h, xp);
+        }
+    } else {
+        for (int h0 = 0; h0 < P.ffp; h0 += HC) {
+            Stage<DM, HC, false> sg;
+            sg.load(P, h0);
+            float hvs[NU];   // this row's ReLU image of the chunk, loaded with the weights
+#pragma unroll
+            for (int u = 0; u < NU; ++u) hvs[u] = h0 + 64 * u + lane < P.ffp ? hrow[h0 + 64 * u + lane] : 0.f;
+            __syncthreads();
+            sg.store(w1s, w2s, nullptr);
+            __syncthreads();
+#pragma unroll 4
+            for (int u = 0; u < NU; ++u) {
+                const int h = 64 * u + lane;
+                if (h0 + h >= P.ffp) break;
+                float w1[DM], w2[DM];
+#pragma unroll
+                for (int k = 0; k < DM; k += 4) {
+                    const float4 t = *reinterpret_cast<const float4 *>(&w1s[h][k]);
+                    w1[k] = t.x, w1[k + 1] = t.y, w1[k + 2] = t.z, w1[k + 3] = t.w;
+                    const float4 q = *reinterpret_cast<const float4 *>(&w2s[h][k]);
+                    w2[k] = q.x, w2[k + 1] = q.y, w2[k + 2] = q.z, w2[k + 3] = q.w;
+                }
+                ffn_unit_bwd<DM>(fv, w1, w2, hvs[u], ks, live, dhrow + h0 + h, xp);
             }
         }
     }
 #pragma unroll
     for (int k = 0; k < DM; ++k) xp[k] = wsum(xp[k]);
+    if constexpr (DIRECT) {   // the 8 waves' partials, in wave order
+        if (lane == 0)
+#pragma unroll
+            for (int k = 0; k < DM; ++k) xw[w][k] = xp[k];
+        __syncthreads();
+        if (w != 0) return;
+#pragma unroll
+        for (int k = 0; k < DM; ++k) {
+            float t = xw[0][k];
+#pragma unroll
+            for (int y = 1; y < LS_WAVES; ++y) t += xw[y][k];
+            xp[k] = t;
+        }
+    }
     float dx1 = 0.f, dz1 = 0.f, da = 0.f, dov = 0.f, dl = 0.f;
     if (live) {
         dx1 = lane < P.d ? dz2 + pick<DM>(xp, lane) : 0.f;
@@ -329,11 +417,16 @@ LsP ls_params(const u2gnn_small_tail_args *a) {
     return P;
 }
 
+// DIRECT below 1024 padded rows (fewer than 128 staged workgroups); the split changes only the order of the
+// hidden-unit partial sums, so a run is deterministic either way
 template <int DM>
 int ls_launch(const LsP &P, bool bwd, hipStream_t st) {
-    const dim3 grid((unsigned)(P.Np / LS_WAVES));
-    if (bwd) hipLaunchKernelGGL(ls_bwd_kernel<DM>, grid, dim3(LS_NT), 0, st, P);
-    else hipLaunchKernelGGL(ls_fwd_kernel<DM>, grid, dim3(LS_NT), 0, st, P);
+    const bool direct = P.Np < 1024;
+    const dim3 grid((unsigned)(direct ? P.Np : P.Np / LS_WAVES));
+    if (bwd && direct) hipLaunchKernelGGL((ls_bwd_kernel<DM, true>), grid, dim3(LS_NT), 0, st, P);
+    else if (bwd) hipLaunchKernelGGL((ls_bwd_kernel<DM, false>), grid, dim3(LS_NT), 0, st, P);
+    else if (direct) hipLaunchKernelGGL((ls_fwd_kernel<DM, true>), grid, dim3(LS_NT), 0, st, P);
+    else hipLaunchKernelGGL((ls_fwd_kernel<DM, false>), grid, dim3(LS_NT), 0, st, P);
     return u2gnn_launch_status();
 }
 

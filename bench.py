@@ -358,7 +358,7 @@ def unsup_cpu_baseline(hbs, sids, sd, V, T, lr, steps):
 
 def c5_attn_kernel(args, trainer, batches):
     """C5's attention backward: the small-width kernels (u2gnn_attn_small_bwd: the dQ walk, which also writes
-    the compact query records, and the dK/dV walk over them; csrc/attn_small.hip) that replaced the padded matrix-core products at d = 4 (round 5).  Timed live
+    the compact query records, and the dK/dV walk over them; csrc/small_layer.hip) that replaced the padded matrix-core products at d = 4 (round 5).  Timed live
     by the executor's probe (HIP events around each layer's backward attention call on its stream) over
     args.steps EAGER steps after the timed graph-replay region.  Algorithmic FLOPs 8 N^2 d per launch (dO.V^T,
     dS K, dS^T Q, Pd^T dO; the recomputed Q K^T not credited) against the fp32 vector peak: the kernels run on

@@ -105,7 +105,7 @@ struct Ctx {   // tensors saved by the forward for the backward
     float *stats;   // small-width node attention (d <= 32): its context (row statistics + compact Q, K, V)
 };
 
-// node attention for d <= 32 on the vector ALUs (u2gnn_attn_small_*, attn_small.hip): every precision, no
+// node attention for d <= 32 on the vector ALUs (u2gnn_attn_small_*, small_layer.hip): every precision, no
 // N x N image (engine.small_attn mirrors the rule)
 bool small_attn(const Dims &D) { return !D.window && D.d <= 32; }
 
@@ -473,7 +473,7 @@ bool fused_attn(const Dims &D) {
     return !D.window && !small_attn(D) && D.prec_fwd != U2GNN_PREC_F32 && D.dp <= 384;
 }
 
-// the row-local tail of a small-width layer (u2gnn_layer_tail_small_*, layer_small.hip): every precision when the
+// the row-local tail of a small-width layer (u2gnn_layer_tail_small_*, small_layer.hip): every precision when the
 // attention is the small-width one (engine.small_attn mirrors the rule)
 u2gnn_small_tail_args tail_args(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seeds *s, const Ctx &c,
                                 const float *X, float *X2) {
@@ -570,7 +570,7 @@ int layer_fwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
                              false, st, drop, prec, U2GNN_ROLE_PV));
     }
     if (small_attn(D)) {
-        // a3.3 + a3.4 row-local on the vector ALUs: one launch (layer_small.hip)
+        // a3.3 + a3.4 row-local on the vector ALUs: one launch (small_layer.hip)
         if (!plan) {
             const u2gnn_small_tail_args t = tail_args(D, w, s, c, X, X2);
             U2GNN_TRY(u2gnn_layer_tail_small_fwd(&t, st));
@@ -647,7 +647,7 @@ int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
     Defer *df = &defer_p, *att = &defer_a;
     const int64_t blk_d[2] = {dp, d}, blk_ff[2] = {ffp, ff};
     float *ws = W.take<float>(colstat_ws_floats(N, dp));
-    const bool tail = small_attn(D);   // the row-local tail kernel (layer_small.hip) forms dX1 ... dO and delta
+    const bool tail = small_attn(D);   // the row-local tail kernel (small_layer.hip) forms dX1 ... dO and delta
     // one-stream layers in the matrix-core precisions: LayerNorm1's backward forms delta = rowsum(dO * O)
     const bool ln_delta = !D.window && prec != U2GNN_PREC_F32;
     float *dX1 = W.take<float>(Np * dp), *dF = W.take<float>(Np * dp);

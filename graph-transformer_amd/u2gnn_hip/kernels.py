@@ -466,7 +466,7 @@ def attn_small_bwd(ctx, W_in, dp, d, n_valid, rows_pad, p, seed, dO, ld_do, delt
 
 
 def layer_tail_small(backward, N, Np, d, dp, ff, ffp, p, seeds, **t):
-    """ABI v15 (d <= 32): the row-local tail of an encoder layer in one launch each way (layer_small.hip).
+    """ABI v15 (d <= 32): the row-local tail of an encoder layer in one launch each way (small_layer.hip).
     seeds = (drop1, dropff, drop2); t: the tensors of u2gnn_small_tail_args by field name (weights in the
     padded layouts, LayerNorm parameters [d]).  Forward: O, X -> Z1, X1, mean1, rstd1, Hd, Z2, X2, mean2, rstd2;
     backward: dX2 and the forward tensors -> dX1, dF, dH, dX, dA, dO, delta."""

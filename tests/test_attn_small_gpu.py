@@ -1,4 +1,4 @@
-"""Small-width in-projection + node attention (u2gnn_attn_small_fwd / _bwd, csrc/attn_small.hip; d <= 32: the UnSup
+"""Small-width in-projection + node attention (u2gnn_attn_small_fwd / _bwd, csrc/small_layer.hip; d <= 32: the UnSup
 encoders C3 / C5 and MUTAG) against a float64 torch restatement of the reference's MHA core on the same dropout
 masks (pytorch_U2GNN_UnSup.py:37-40,57: q, k, v = x W_in^T + b_in with q scaled by 1/sqrt(d), softmax over the N
 keys, dropout(0.5) on the probabilities with 1/(1-p) scaling, times V; the backward through torch autograd, down

@@ -1,4 +1,4 @@
-"""The row-local tail of a small-width encoder layer (u2gnn_layer_tail_small_fwd / _bwd, csrc/layer_small.hip; d <= 32:
+"""The row-local tail of a small-width encoder layer (u2gnn_layer_tail_small_fwd / _bwd, csrc/small_layer.hip; d <= 32:
 the UnSup encoders C3 / C5 and MUTAG) against a float64 torch restatement of the reference's TransformerEncoderLayer
 tail on the kernels' own dropout masks (pytorch_U2GNN_UnSup.py:37-40,57: out_proj -> dropout -> + x -> norm1 ->
 linear1 -> ReLU -> dropout -> linear2 -> dropout -> + x -> norm2, post-LN, eps 1e-5), the backward through torch

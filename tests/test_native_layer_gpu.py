@@ -24,7 +24,7 @@ def _zeros_like_params(p: LayerParams) -> LayerParams:
     return LayerParams(*[torch.full_like(t, float("nan")) for t in p.tensors()])
 
 
-# d = 19, 4: fused LN and the small-width attention (attn_small.hip); (1920, 4, 1024): the C5 layer (long reductions batched at the end of a one-stream backward)
+# d = 19, 4: fused LN and the small-width attention (small_layer.hip); (1920, 4, 1024): the C5 layer (long reductions batched at the end of a one-stream backward)
 @pytest.mark.parametrize("N,d,ff", [(300, 67, 128), (1000, 367, 1024), (300, 19, 128), (1920, 4, 1024)])
 @pytest.mark.parametrize("prec", ["bf16x3", "fp32", "mixed", "fwd32"])
 @pytest.mark.parametrize("train", [True, False])

@@ -1,4 +1,4 @@
-"""Micro-benchmark of the small-width projection + attention kernels (u2gnn_attn_small_fwd / _bwd, csrc/attn_small.hip) on
+"""Micro-benchmark of the small-width projection + attention kernels (u2gnn_attn_small_fwd / _bwd, csrc/small_layer.hip) on
 C5-like shapes (d = 4, N ~ 2 K) and C3 / MUTAG ones: device time per call via HIP events over back-to-back
 launches replayed from a captured graph.  Usage: python tools/sa_bench.py   (U2GNN_HIP_LIB selects a variant library)"""
 import math

@@ -357,8 +357,9 @@ def unsup_cpu_baseline(hbs, sids, sd, V, T, lr, steps):
 
 
 def c5_attn_kernel(args, trainer, batches):
-    """C5's attention backward: the small-width kernels (u2gnn_attn_small_bwd: the dQ walk, which also writes
-    the compact query records, and the dK/dV walk over them; csrc/small_layer.hip) that replaced the padded matrix-core products at d = 4 (round 5).  Timed live
+    """C5's attention backward: the small-width layer backward (u2gnn_layer_small_bwd, csrc/small_layer.hip: the
+    tail backward fused with the dQ walk, which also writes the compact query records, then the dK/dV walk over
+    them with the in-projection's dX; the probe's time includes the tail backward, the FLOPs credited do not) that replaced the padded matrix-core products at d = 4 (round 5).  Timed live
     by the executor's probe (HIP events around each layer's backward attention call on its stream) over
     args.steps EAGER steps after the timed graph-replay region.  Algorithmic FLOPs 8 N^2 d per launch (dO.V^T,
     dS K, dS^T Q, Pd^T dO; the recomputed Q K^T not credited) against the fp32 vector peak: the kernels run on
@@ -383,7 +384,7 @@ def c5_attn_kernel(args, trainer, batches):
     ach = fl / (ms * 1e-3) / 1e12
     return {"bound": "valu", "achieved": round(ach, 3), "peak": PEAK["fp32"], "unit": "TFLOP/s",
             "frac": round(ach / PEAK["fp32"], 4),
-            "kernel": "u2gnn_attn_small_bwd (sa_bwd_q_kernel<4> + sa_bwd_kv_kernel<4>)",
+            "kernel": "u2gnn_layer_small_bwd (sa_bwd_q_kernel<4, tail> + sa_bwd_kv_kernel<4>)",
             "launches": n, "avg_launch_us": round(1e3 * ms / n, 1), "algorithmic_flop_per_launch": round(fl / n),
             "timing": "live: HIP events around each layer's attention backward, eager steps after the timed region"}
 

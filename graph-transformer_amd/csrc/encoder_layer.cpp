@@ -524,12 +524,13 @@ int layer_fwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
             U2GNN_TRY(u2gnn_window_attn_fwd(c.QKV, 3 * dp, D.window, (int32_t)dp, c.O, dp, c.Psave, pd, s->attn,
                                             N / D.window, Np, st));
     } else if (small_attn(D)) {
-        // d <= 32: in-projection, softmax -> dropout -> P.V flash-style on the vector ALUs, the row statistics and
-        // a compact Q, K, V saved
+        // d <= 32: the whole layer on the vector ALUs (small_layer.hip): in-projection, softmax -> dropout -> P.V
+        // flash-style (the row statistics and a compact Q, K, V saved) and a3.3 + a3.4 -- 2 or 3 launches
         if (!plan) {
+            const u2gnn_small_tail_args t = tail_args(D, w, s, c, X, X2);
             probe_mark(U2GNN_ROLE_PV, false, st, plan);
-            U2GNN_TRY(u2gnn_attn_small_fwd(X, dp, w->W_in, w->b_in, dp, d, N, Np, pd, s->attn, c.O, dp, c.stats,
-                                           u2gnn_attn_small_ctx_floats(Np, d), st));
+            U2GNN_TRY(u2gnn_layer_small_fwd(&t, w->W_in, w->b_in, s->attn, c.stats, u2gnn_attn_small_ctx_floats(Np, d),
+                                            st));
             probe_mark(U2GNN_ROLE_PV, true, st, plan);
         }
     } else if (fused) {
@@ -570,11 +571,7 @@ int layer_fwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
                              false, st, drop, prec, U2GNN_ROLE_PV));
     }
     if (small_attn(D)) {
-        // a3.3 + a3.4 row-local on the vector ALUs: one launch (small_layer.hip)
-        if (!plan) {
-            const u2gnn_small_tail_args t = tail_args(D, w, s, c, X, X2);
-            U2GNN_TRY(u2gnn_layer_tail_small_fwd(&t, st));
-        }
+        // a3.3 + a3.4: run by u2gnn_layer_small_fwd above
     } else {
         // a3.3 out-projection + dropout1 + residual, LayerNorm1 (fused into the GEMM epilogue when a
         // 64-column tile holds whole rows: d <= 64, bf16 modes; engine.fused_ln mirrors the rule)
@@ -659,11 +656,20 @@ int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
     if (!need_dx) dX = dX_scratch;
     float *delta_ln = (ln_delta || tail) ? W.take<float>(Np) : nullptr;
     float *dO = W.take<float>(Np * dp);
+    float *small_dqkv = nullptr;   // the small-width layer's dQKV, written by u2gnn_layer_small_bwd
     if (tail) {
+        // the tail backward and the attention backward (dQKV; dX += dQKV W_in unless no input gradient is
+        // wanted) in 2 or 3 launches (small_layer.hip)
+        small_dqkv = W.take<float>(Np * 3 * dp);
+        const int64_t wsf = u2gnn_attn_small_ws_floats(N, Np, d);
+        float *sa_ws = W.take<float>(wsf);
         if (!plan) {
             u2gnn_small_tail_args t = tail_args(D, w, s, c, X, nullptr);
             t.dX2 = dX2, t.dX1 = dX1, t.dF = dF, t.dH = dH, t.dX = dX, t.dA = dA, t.dO = dO, t.delta = delta_ln;
-            U2GNN_TRY(u2gnn_layer_tail_small_bwd(&t, st));
+            probe_mark(U2GNN_ROLE_DS, false, st, plan);
+            U2GNN_TRY(u2gnn_layer_small_bwd(&t, w->W_in, s->attn, c.stats, u2gnn_attn_small_ctx_floats(Np, d),
+                                            small_dqkv, 3 * dp, need_dx ? 1 : 0, sa_ws, wsf, st));
+            probe_mark(U2GNN_ROLE_DS, true, st, plan);
         }
         // the parameter gradients of the tail, held back (df) in the order of the matrix-core branch
         U2GNN_TRY(ln_params(dX2, c.Z2, c.mean2, c.rstd2, dF, dp, N, d, dp, ws, g->n2_w, g->n2_b, g->l2_b, so, plan, df));
@@ -728,20 +734,8 @@ int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
             U2GNN_TRY(u2gnn_window_attn_bwd(c.QKV, 3 * dp, D.window, (int32_t)dp, dO, dp, c.Psave, pd, s->attn,
                                             q_scale, dQKV, 3 * dp, N / D.window, Np, st));
     } else if (small_attn(D)) {
-        // d <= 32: dQ, dK, dV with P recomputed from the row statistics (no dS image, no split-K slabs)
-        dQKV = W.take<float>(Np * 3 * dp);
-        float *delta = have_delta ? delta_ln : W.take<float>(Np);
-        const int64_t wsf = u2gnn_attn_small_ws_floats(N, Np, d);
-        float *sa_ws = W.take<float>(wsf);
-        if (!plan && !have_delta) U2GNN_TRY(u2gnn_rowdot(dO, dp, c.O, dp, delta, Np, dp, st));
-        if (!plan) {
-            probe_mark(U2GNN_ROLE_DS, false, st, plan);
-            // ... and the in-projection's dX += dQKV W_in (no dX product below)
-            U2GNN_TRY(u2gnn_attn_small_bwd(c.stats, u2gnn_attn_small_ctx_floats(Np, d), w->W_in, dp, d, N, Np, pd,
-                                           s->attn, dO, dp, delta, q_scale, dQKV, 3 * dp, need_dx ? dX : nullptr, dp,
-                                           sa_ws, wsf, st));
-            probe_mark(U2GNN_ROLE_DS, true, st, plan);
-        }
+        // d <= 32: dQ, dK, dV (P recomputed from the row statistics) and dX += dQKV W_in, run with the tail above
+        dQKV = small_dqkv;
     } else {
         dQKV = W.take<float>(Np * 3 * dp);
         const bool dv_side = so != st;   // grouped with dQ / dK on this stream instead: 3.136-3.141 vs 3.068-3.098 ms

@@ -174,9 +174,32 @@ __global__ void __launch_bounds__(256) sa_proj_kernel(SaP P) {
     *reinterpret_cast<float4 *>(dst) = make_float4(o[0], o[1], o[2], o[3]);
 }
 
+// the row-local tail's launch shape and parameters (its kernels: second half of this file)
+constexpr int LS_WAVES = 8;                // rows per 512-thread workgroup (one wave per row)
+constexpr int LS_NT = 64 * LS_WAVES;
+// hidden units per LDS chunk: W1 and W2^T chunks of HC x DM floats each (32 KB together)
+template <int DM> constexpr int ls_hc() { return 4096 / DM / 64 * 64; }
+template <int DM> constexpr int ls_min_waves() { return DM <= 16 ? 4 : 2; }
+
+struct LsP {
+    int32_t N, Np, d, dp, ff, ffp;
+    float p, eps;
+    uint64_t s1, sff, s2;
+    const uint64_t *epoch;
+    u2gnn_small_tail_args a;
+};
+
+template <int DM> __device__ void tail_fwd_rows(const LsP &T, int i, int rw, int sp, const float (&of)[DM], bool fin,
+                                                float *smem);
+template <int DM> __device__ void tail_bwd_rows(const LsP &T, int i, int rw, int sp, bool fin, float (&g)[DM],
+                                                float &dl, float *smem);
+template <int DM> constexpr int tail_smem_floats();
+
 // ---- forward: one query row per SA_SPL waves -------------------------------------------------------------
-template <int DM>
-__global__ void __launch_bounds__(SA_NT, sa_min_waves<DM>()) sa_fwd_kernel(SaP P) {
+// TAIL (ABI u2gnn_layer_small_fwd, rows_pad >= 1024): the same workgroup then runs the row-local tail of its
+// SA_RB rows (tail_fwd_rows): the attention output O never makes a round trip before its out-projection
+template <int DM, bool TAIL>
+__global__ void __launch_bounds__(SA_NT, sa_min_waves<DM>()) sa_fwd_kernel(SaP P, LsP T) {
     constexpr int SA_KT = sa_kt_f<DM>();
     constexpr int PART = SA_KT / SA_SPL, NP = PART / 128;   // keys per wave per tile; key pairs per lane
     constexpr int CU = DM <= 8 ? 8 : 4;   // keys per lane between rescales (their K rows are live in registers)
@@ -262,36 +285,50 @@ __global__ void __launch_bounds__(SA_NT, sa_min_waves<DM>()) sa_fwd_kernel(SaP P
         for (int c = 0; c < DM; ++c) xw[rw][sp][2 + c] = o[c];
     }
     __syncthreads();
-    if (sp != 0 || i >= P.Np) return;
-    float M = xw[rw][0][0];
+    const bool fin = sp == 0 && i < P.Np;   // the row's finishing wave
+    if (!TAIL && !fin) return;
+    float of[DM];   // fin: the row of O
 #pragma unroll
-    for (int x = 1; x < SA_SPL; ++x) M = fmaxf(M, xw[rw][x][0]);
-    float L = 0.f;
+    for (int c = 0; c < DM; ++c) of[c] = 0.f;
+    if (fin) {
+        float M = xw[rw][0][0];
 #pragma unroll
-    for (int c = 0; c < DM; ++c) o[c] = 0.f;
-    if (M != -INFINITY) {
+        for (int x = 1; x < SA_SPL; ++x) M = fmaxf(M, xw[rw][x][0]);
+        float L = 0.f;
 #pragma unroll
-        for (int x = 0; x < SA_SPL; ++x) {
-            const float f = xw[rw][x][0] == -INFINITY ? 0.f : exp2f(xw[rw][x][0] - M);
-            L = fmaf(xw[rw][x][1], f, L);
+        for (int c = 0; c < DM; ++c) o[c] = 0.f;
+        if (M != -INFINITY) {
 #pragma unroll
-            for (int c = 0; c < DM; ++c) o[c] = fmaf(xw[rw][x][2 + c], f, o[c]);
+            for (int x = 0; x < SA_SPL; ++x) {
+                const float f = xw[rw][x][0] == -INFINITY ? 0.f : exp2f(xw[rw][x][0] - M);
+                L = fmaf(xw[rw][x][1], f, L);
+#pragma unroll
+                for (int c = 0; c < DM; ++c) o[c] = fmaf(xw[rw][x][2 + c], f, o[c]);
+            }
+        }
+        const float invL = live && L > 0.f ? 1.f / L : 0.f;
+        const float s1p = drop ? 1.f / (1.f - P.p) : 1.f;
+#pragma unroll
+        for (int c = 0; c < DM; ++c) of[c] = (live && c < P.d) ? o[c] * invL * s1p : 0.f;
+        float *orow = P.out + (int64_t)i * P.ld_out;
+        for (int c = lane; c < P.dp; c += 64) orow[c] = lane_col<DM>(of, c);
+        if (lane == 0) {
+            float *st = sa_st(P.ctx);
+            st[2 * (int64_t)i] = live ? M : 0.f;
+            st[2 * (int64_t)i + 1] = invL;
         }
     }
-    const float invL = live && L > 0.f ? 1.f / L : 0.f;
-    const float s1p = drop ? 1.f / (1.f - P.p) : 1.f;
-    float *orow = P.out + (int64_t)i * P.ld_out;
-    for (int c = lane; c < P.dp; c += 64) orow[c] = (live && c < P.d) ? lane_col<DM>(o, c) * invL * s1p : 0.f;
-    if (lane == 0) {
-        float *st = sa_st(P.ctx);
-        st[2 * (int64_t)i] = live ? M : 0.f;
-        st[2 * (int64_t)i + 1] = invL;
+    if constexpr (TAIL) {
+        __shared__ __attribute__((aligned(16))) float tsm[tail_smem_floats<DM>()];
+        tail_fwd_rows<DM>(T, i, rw, sp, of, fin, tsm);
     }
 }
 
 // ---- backward dQ: one query row per SA_SPL waves; also the row's record for dK / dV -----------------------
-template <int DM>
-__global__ void __launch_bounds__(SA_NT, sa_min_waves<DM>()) sa_bwd_q_kernel(SaP P) {
+// TAIL (ABI u2gnn_layer_small_bwd, rows_pad >= 1024): the workgroup first runs the row-local tail backward of
+// its SA_RB rows (tail_bwd_rows), whose dO row and delta then feed the dQ walk from LDS
+template <int DM, bool TAIL>
+__global__ void __launch_bounds__(SA_NT, sa_min_waves<DM>()) sa_bwd_q_kernel(SaP P, LsP T) {
     constexpr int SA_KT = sa_kt_f<DM>();
     constexpr int PART = SA_KT / SA_SPL, NP = PART / 128;
     static_assert(NP >= 1 && PART % 128 == 0, "a wave's part of the key tile: whole 128-key rounds");
@@ -307,10 +344,17 @@ __global__ void __launch_bounds__(SA_NT, sa_min_waves<DM>()) sa_bwd_q_kernel(SaP
     float M = 0.f, iL = 0.f, dl = 0.f;
 #pragma unroll
     for (int c = 0; c < DM; ++c) q[c] = g[c] = dq[c] = 0.f;
+    if constexpr (TAIL) {   // dO and delta of the row from the tail backward (every wave of the row)
+        __shared__ __attribute__((aligned(16))) float tsm[tail_smem_floats<DM>()];
+        tail_bwd_rows<DM>(T, i, rw, sp, sp == 0 && i < P.Np, g, dl, tsm);
+    }
     if (live) {
         load_row<DM>(sa_qc<DM>(P.ctx, P.Np) + (int64_t)i * DM, q);
-        load_row<DM>(P.dO + (int64_t)i * P.ld_do, g);
-        M = st[2 * (int64_t)i], iL = st[2 * (int64_t)i + 1], dl = P.delta[i];
+        if constexpr (!TAIL) {
+            load_row<DM>(P.dO + (int64_t)i * P.ld_do, g);
+            dl = P.delta[i];
+        }
+        M = st[2 * (int64_t)i], iL = st[2 * (int64_t)i + 1];
     }
     const bool drop = P.p > 0.f;
     const float s1p = drop ? 1.f / (1.f - P.p) : 1.f;
@@ -521,14 +565,15 @@ template <int DM>
 int sa_fwd_launch(const SaP &P, hipStream_t st) {
     const int64_t nt = (int64_t)P.Np * 3 * (DM / 4);
     hipLaunchKernelGGL(sa_proj_kernel<DM>, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, st, P);
-    hipLaunchKernelGGL(sa_fwd_kernel<DM>, dim3((unsigned)((P.Np + SA_RB - 1) / SA_RB)), dim3(SA_NT), 0, st, P);
+    hipLaunchKernelGGL((sa_fwd_kernel<DM, false>), dim3((unsigned)((P.Np + SA_RB - 1) / SA_RB)), dim3(SA_NT), 0, st, P,
+                       LsP{});
     return u2gnn_launch_status();
 }
 
 template <int DM>
 int sa_bwd_launch(const SaP &P, hipStream_t st) {
     const dim3 grid((unsigned)((P.Np + SA_RB - 1) / SA_RB));
-    hipLaunchKernelGGL(sa_bwd_q_kernel<DM>, grid, dim3(SA_NT), 0, st, P);
+    hipLaunchKernelGGL((sa_bwd_q_kernel<DM, false>), grid, dim3(SA_NT), 0, st, P, LsP{});
     constexpr int KR = SA_RB * sa_kp<DM>();   // key rows per workgroup
     hipLaunchKernelGGL(sa_bwd_kv_kernel<DM>, dim3((unsigned)((P.Np + KR - 1) / KR)), dim3(SA_NT), 0, st, P);
     return u2gnn_launch_status();
@@ -619,20 +664,6 @@ int u2gnn_attn_small_bwd(const float *ctx, int64_t ctx_floats, const float *W_in
 // the GEMM epilogues'.  Deterministic: fixed hidden-unit partition and butterfly sums.
 
 namespace {
-
-constexpr int LS_WAVES = 8;                // rows per 512-thread workgroup (one wave per row)
-constexpr int LS_NT = 64 * LS_WAVES;
-// hidden units per LDS chunk: W1 and W2^T chunks of HC x DM floats each (32 KB together)
-template <int DM> constexpr int ls_hc() { return 4096 / DM / 64 * 64; }
-template <int DM> constexpr int ls_min_waves() { return DM <= 16 ? 4 : 2; }
-
-struct LsP {
-    int32_t N, Np, d, dp, ff, ffp;
-    float p, eps;
-    uint64_t s1, sff, s2;
-    const uint64_t *epoch;
-    u2gnn_small_tail_args a;
-};
 
 __device__ __forceinline__ float wsum(float v) { return wave_sum(v); }
 
@@ -984,6 +1015,212 @@ __global__ void __launch_bounds__(LS_NT, ls_min_waves<DM>()) ls_bwd_kernel(LsP P
     if (lane == 0) A.delta[r] = dl;
 }
 
+// ---- the tail phase of the fused kernels (sa_fwd_kernel / sa_bwd_q_kernel with TAIL): the workgroup's SA_RB
+// rows, SA_SPL waves per row splitting the hidden units of each LDS-staged chunk (unit 64 k + lane, k = sp,
+// sp + SA_SPL, ...), the waves' partial sums combined in wave order; the row's finishing wave (sp 0) runs the
+// row prologue / epilogue.  Same arithmetic per unit as ls_fwd_kernel / ls_bwd_kernel; the hidden-unit partial
+// sums are taken in another order (per wave, then across the two waves).
+template <int DM> constexpr int tail_smem_floats() { return 2 * ls_hc<DM>() * DM + ls_hc<DM>() + SA_RB * (4 * DM + 4); }
+
+template <int DM>
+__device__ void tail_fwd_rows(const LsP &T, int i, int rw, int sp, const float (&of)[DM], bool fin, float *smem) {
+    static_assert(LS_NT == SA_NT, "the tail's staging runs on the attention workgroup");
+    constexpr int HC = ls_hc<DM>(), NU = HC / 64;
+    float (*w1s)[DM] = reinterpret_cast<float (*)[DM]>(smem);
+    float (*w2s)[DM] = reinterpret_cast<float (*)[DM]>(smem + HC * DM);
+    float *b1s = smem + 2 * HC * DM;
+    float (*xs)[DM] = reinterpret_cast<float (*)[DM]>(b1s + HC);
+    float (*xz)[SA_SPL][DM] = reinterpret_cast<float (*)[SA_SPL][DM]>(b1s + HC + SA_RB * DM);
+    const int lane = threadIdx.x & 63;
+    const bool live = i < T.N;
+    const u2gnn_small_tail_args &A = T.a;
+    const bool drop = T.p > 0.f;
+    const float ks = drop ? 1.f / (1.f - T.p) : 1.f;
+    const uint32_t thr = u2gnn_keep_thr(T.p);
+    const uint64_t s1 = u2gnn_seed(T.s1, T.epoch), sff = u2gnn_seed(T.sff, T.epoch), s2 = u2gnn_seed(T.s2, T.epoch);
+    const int64_t ro = (int64_t)i * T.dp;
+    // a3.3 from the O row in registers: z1 = drop1(O W_o^T + b_o) + x, LayerNorm1
+    float x1 = 0.f;
+    if (fin) {
+        float z1 = 0.f, mu1 = 0.f, rs1 = 0.f;
+        if (live) {
+            float wo[DM];
+            const int cw = lane < DM ? lane : 0;
+#pragma unroll
+            for (int k = 0; k < DM; k += 4) {
+                const float4 t = *reinterpret_cast<const float4 *>(A.W_o + (int64_t)cw * T.dp + k);
+                wo[k] = t.x, wo[k + 1] = t.y, wo[k + 2] = t.z, wo[k + 3] = t.w;
+            }
+            float acc = 0.f;
+#pragma unroll
+            for (int k = 0; k < DM; ++k) acc = fmaf(of[k], wo[k], acc);
+            float v = acc + A.b_o[lane];
+            if (drop) v = u2gnn_keep(s1, (uint32_t)i, (uint32_t)lane, T.p) ? v * ks : 0.f;
+            z1 = lane < T.d ? v + A.X[ro + lane] : 0.f;
+            x1 = ln_row(z1, lane, T.d, T.eps, A.n1_w, A.n1_b, mu1, rs1);
+        }
+        A.Z1[ro + lane] = z1;
+        A.X1[ro + lane] = x1;
+        if (lane == 0) A.mean1[i] = mu1, A.rstd1[i] = rs1;
+        if (lane < DM) xs[rw][lane] = x1;
+    }
+    __syncthreads();
+    float xv[DM], zp[DM];
+#pragma unroll
+    for (int k = 0; k < DM; ++k) xv[k] = xs[rw][k], zp[k] = 0.f;
+    // a3.4 over this wave's hidden units
+    const uint32_t rkf = u2gnn_row_key(sff, (uint32_t)i);
+    float *hrow = A.Hd + (int64_t)i * T.ffp;
+    for (int h0 = 0; h0 < T.ffp; h0 += HC) {
+        Stage<DM, HC, true> sg;
+        sg.load(T, h0);
+        __syncthreads();
+        sg.store(w1s, w2s, b1s);
+        __syncthreads();
+#pragma unroll 4
+        for (int k = sp; k < NU; k += SA_SPL) {
+            const int h = 64 * k + lane;
+            if (h0 + h >= T.ffp) break;
+            float w1[DM], w2[DM];
+#pragma unroll
+            for (int c = 0; c < DM; c += 4) {
+                const float4 t = *reinterpret_cast<const float4 *>(&w1s[h][c]);
+                w1[c] = t.x, w1[c + 1] = t.y, w1[c + 2] = t.z, w1[c + 3] = t.w;
+                const float4 q = *reinterpret_cast<const float4 *>(&w2s[h][c]);
+                w2[c] = q.x, w2[c + 1] = q.y, w2[c + 2] = q.z, w2[c + 3] = q.w;
+            }
+            const bool keep = !drop || u2gnn_keep_rk(rkf, (uint32_t)(h0 + h), thr);
+            ffn_unit_fwd<DM>(xv, w1, w2, b1s[h], keep, ks, live, hrow + h0 + h, zp);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < DM; ++k) zp[k] = wsum(zp[k]);
+    if (lane == 0)
+#pragma unroll
+        for (int k = 0; k < DM; ++k) xz[rw][sp][k] = zp[k];
+    __syncthreads();
+    if (!fin) return;
+#pragma unroll
+    for (int k = 0; k < DM; ++k) {
+        float t = xz[rw][0][k];
+#pragma unroll
+        for (int y = 1; y < SA_SPL; ++y) t += xz[rw][y][k];
+        zp[k] = t;
+    }
+    float z2 = 0.f, x2 = 0.f, mu2 = 0.f, rs2 = 0.f;
+    if (live) {
+        float v = pick<DM>(zp, lane) + A.b2[lane];
+        if (drop) v = u2gnn_keep(s2, (uint32_t)i, (uint32_t)lane, T.p) ? v * ks : 0.f;
+        z2 = lane < T.d ? v + x1 : 0.f;
+        x2 = ln_row(z2, lane, T.d, T.eps, A.n2_w, A.n2_b, mu2, rs2);
+    }
+    A.Z2[ro + lane] = z2;
+    A.X2[ro + lane] = x2;
+    if (lane == 0) A.mean2[i] = mu2, A.rstd2[i] = rs2;
+}
+
+// the tail backward of the row; on return every wave of the row holds its dO row (g) and delta (dl)
+template <int DM>
+__device__ void tail_bwd_rows(const LsP &T, int i, int rw, int sp, bool fin, float (&g)[DM], float &dl, float *smem) {
+    constexpr int HC = ls_hc<DM>(), NU = HC / 64, NW = (NU + SA_SPL - 1) / SA_SPL;
+    float (*w1s)[DM] = reinterpret_cast<float (*)[DM]>(smem);
+    float (*w2s)[DM] = reinterpret_cast<float (*)[DM]>(smem + HC * DM);
+    float (*fs)[DM] = reinterpret_cast<float (*)[DM]>(smem + 2 * HC * DM);
+    float (*xz)[SA_SPL][DM] = reinterpret_cast<float (*)[SA_SPL][DM]>(smem + 2 * HC * DM + SA_RB * DM);
+    float (*gs)[DM + 4] = reinterpret_cast<float (*)[DM + 4]>(smem + 2 * HC * DM + SA_RB * DM * (1 + SA_SPL));
+    const int lane = threadIdx.x & 63;
+    const bool live = i < T.N;
+    const u2gnn_small_tail_args &A = T.a;
+    const bool drop = T.p > 0.f;
+    const float ks = drop ? 1.f / (1.f - T.p) : 1.f;
+    const uint64_t s1 = u2gnn_seed(T.s1, T.epoch), s2 = u2gnn_seed(T.s2, T.epoch);
+    const int64_t ro = (int64_t)i * T.dp;
+    // LayerNorm2^T -> dz2 (kept by the finishing wave), dF
+    float dz2 = 0.f;
+    if (fin) {
+        float df = 0.f;
+        if (live) {
+            dz2 = ln_row_bwd(A.dX2[ro + lane], A.Z2[ro + lane], A.mean2[i], A.rstd2[i], lane, T.d, A.n2_w);
+            df = (drop && lane < T.d) ? (u2gnn_keep(s2, (uint32_t)i, (uint32_t)lane, T.p) ? dz2 * ks : 0.f) : dz2;
+        }
+        A.dF[ro + lane] = df;
+        if (lane < DM) fs[rw][lane] = df;
+    }
+    __syncthreads();
+    float fv[DM], xp[DM];
+#pragma unroll
+    for (int k = 0; k < DM; ++k) fv[k] = fs[rw][k], xp[k] = 0.f;
+    const float *hrow = A.Hd + (int64_t)i * T.ffp;
+    float *dhrow = A.dH + (int64_t)i * T.ffp;
+    for (int h0 = 0; h0 < T.ffp; h0 += HC) {
+        Stage<DM, HC, false> sg;
+        sg.load(T, h0);
+        float hvs[NW];   // this wave's units of the row's ReLU image, loaded with the weights
+#pragma unroll
+        for (int u = 0; u < NW; ++u) {
+            const int h = 64 * (sp + SA_SPL * u) + lane;
+            hvs[u] = (sp + SA_SPL * u < NU && h0 + h < T.ffp) ? hrow[h0 + h] : 0.f;
+        }
+        __syncthreads();
+        sg.store(w1s, w2s, nullptr);
+        __syncthreads();
+#pragma unroll 4
+        for (int u = 0; u < NW; ++u) {
+            const int k = sp + SA_SPL * u, h = 64 * k + lane;
+            if (k >= NU || h0 + h >= T.ffp) break;
+            float w1[DM], w2[DM];
+#pragma unroll
+            for (int c = 0; c < DM; c += 4) {
+                const float4 t = *reinterpret_cast<const float4 *>(&w1s[h][c]);
+                w1[c] = t.x, w1[c + 1] = t.y, w1[c + 2] = t.z, w1[c + 3] = t.w;
+                const float4 q = *reinterpret_cast<const float4 *>(&w2s[h][c]);
+                w2[c] = q.x, w2[c + 1] = q.y, w2[c + 2] = q.z, w2[c + 3] = q.w;
+            }
+            ffn_unit_bwd<DM>(fv, w1, w2, hvs[u], ks, live, dhrow + h0 + h, xp);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < DM; ++k) xp[k] = wsum(xp[k]);
+    if (lane == 0)
+#pragma unroll
+        for (int k = 0; k < DM; ++k) xz[rw][sp][k] = xp[k];
+    __syncthreads();
+    if (fin) {
+#pragma unroll
+        for (int k = 0; k < DM; ++k) {
+            float t = xz[rw][0][k];
+#pragma unroll
+            for (int y = 1; y < SA_SPL; ++y) t += xz[rw][y][k];
+            xp[k] = t;
+        }
+        float dx1 = 0.f, dz1 = 0.f, da = 0.f, dov = 0.f, dlt = 0.f;
+        if (live) {
+            dx1 = lane < T.d ? dz2 + pick<DM>(xp, lane) : 0.f;
+            dz1 = ln_row_bwd(dx1, A.Z1[ro + lane], A.mean1[i], A.rstd1[i], lane, T.d, A.n1_w);
+            da = (drop && lane < T.d) ? (u2gnn_keep(s1, (uint32_t)i, (uint32_t)lane, T.p) ? dz1 * ks : 0.f) : dz1;
+            float av[DM];
+#pragma unroll
+            for (int k = 0; k < DM; ++k) av[k] = __shfl(da, k, 64);
+            const int kc = lane < DM ? lane : 0;
+            float acc = 0.f;
+#pragma unroll
+            for (int c = 0; c < DM; ++c) acc = fmaf(av[c], A.W_o[(int64_t)c * T.dp + kc], acc);
+            dov = lane < T.d ? acc : 0.f;
+            dlt = wsum(dov * A.O[ro + lane]);
+        }
+        A.dX1[ro + lane] = dx1;
+        A.dX[ro + lane] = dz1;
+        A.dA[ro + lane] = da;
+        A.dO[ro + lane] = dov;
+        if (lane == 0) A.delta[i] = dlt, gs[rw][DM] = dlt;
+        if (lane < DM) gs[rw][lane] = dov;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < DM; ++k) g[k] = gs[rw][k];
+    dl = gs[rw][DM];
+}
+
 int ls_dm(int64_t d) { return d < 1 ? 0 : d <= 24 ? (int)((d + 3) / 4 * 4) : d <= 32 ? 32 : 0; }
 
 int ls_check(const u2gnn_small_tail_args *a, bool bwd) {
@@ -1040,6 +1277,39 @@ int ls_run(const u2gnn_small_tail_args *a, bool bwd, void *stream) {
     }
 }
 
+// ---- a whole small-width layer (ABI u2gnn_layer_small_fwd / _bwd): fused where the rows allow --------------
+// rows_pad >= 1024 (the tail's STAGED split): attention forward + tail in one launch, tail backward + the dQ walk
+// in one launch; below that the tail's DIRECT split keeps its own launches
+constexpr int64_t SMALL_FUSE_ROWS = 1024;   // (C5: fused 0.541 / 0.543 vs separate 0.587 / 0.594 ms, one session)
+
+template <int DM>
+int small_fwd_launch(const SaP &P, const LsP &T, hipStream_t st) {
+    const int64_t nt = (int64_t)P.Np * 3 * (DM / 4);
+    hipLaunchKernelGGL(sa_proj_kernel<DM>, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, st, P);
+    const dim3 grid((unsigned)((P.Np + SA_RB - 1) / SA_RB));
+    if (P.Np >= SMALL_FUSE_ROWS) {
+        hipLaunchKernelGGL((sa_fwd_kernel<DM, true>), grid, dim3(SA_NT), 0, st, P, T);
+    } else {
+        hipLaunchKernelGGL((sa_fwd_kernel<DM, false>), grid, dim3(SA_NT), 0, st, P, LsP{});
+        hipLaunchKernelGGL((ls_fwd_kernel<DM, true>), dim3((unsigned)P.Np), dim3(LS_NT), 0, st, T);
+    }
+    return u2gnn_launch_status();
+}
+
+template <int DM>
+int small_bwd_launch(const SaP &P, const LsP &T, hipStream_t st) {
+    const dim3 grid((unsigned)((P.Np + SA_RB - 1) / SA_RB));
+    if (P.Np >= SMALL_FUSE_ROWS) {
+        hipLaunchKernelGGL((sa_bwd_q_kernel<DM, true>), grid, dim3(SA_NT), 0, st, P, T);
+    } else {
+        hipLaunchKernelGGL((ls_bwd_kernel<DM, true>), dim3((unsigned)P.Np), dim3(LS_NT), 0, st, T);
+        hipLaunchKernelGGL((sa_bwd_q_kernel<DM, false>), grid, dim3(SA_NT), 0, st, P, LsP{});
+    }
+    constexpr int KR = SA_RB * sa_kp<DM>();
+    hipLaunchKernelGGL(sa_bwd_kv_kernel<DM>, dim3((unsigned)((P.Np + KR - 1) / KR)), dim3(SA_NT), 0, st, P);
+    return u2gnn_launch_status();
+}
+
 }  // namespace
 
 extern "C" {
@@ -1047,5 +1317,58 @@ extern "C" {
 int u2gnn_layer_tail_small_fwd(const u2gnn_small_tail_args *a, void *stream) { return ls_run(a, false, stream); }
 
 int u2gnn_layer_tail_small_bwd(const u2gnn_small_tail_args *a, void *stream) { return ls_run(a, true, stream); }
+
+
+int u2gnn_layer_small_fwd(const u2gnn_small_tail_args *t, const float *W_in, const float *b_in, uint64_t attn_seed,
+                          float *ctx, int64_t ctx_floats, void *stream) {
+    int rc = ls_check(t, false);
+    if (rc != U2GNN_OK) return rc;
+    rc = sa_check(t->dp, t->d, t->n_valid, t->rows_pad, t->p, ctx, ctx_floats);
+    if (rc != U2GNN_OK) return rc;
+    if (!W_in || !b_in) return U2GNN_E_ARG;
+    if (!al16(t->X) || !al16(W_in)) return U2GNN_E_ALIGN;
+    SaP P = sa_params(t->dp, t->d, t->n_valid, t->rows_pad, t->p, attn_seed, ctx);
+    P.x = t->X, P.ldx = t->dp, P.w_in = W_in, P.b_in = b_in, P.q_scale = (float)(1.0 / std::sqrt((double)t->d));
+    P.out = const_cast<float *>(t->O), P.ld_out = t->dp;   // (the attention output: written here)
+    const LsP T = ls_params(t);
+    hipStream_t st = u2gnn_stream(stream);
+    switch (sa_dm(t->d)) {
+        case 4: return small_fwd_launch<4>(P, T, st);
+        case 8: return small_fwd_launch<8>(P, T, st);
+        case 12: return small_fwd_launch<12>(P, T, st);
+        case 16: return small_fwd_launch<16>(P, T, st);
+        case 20: return small_fwd_launch<20>(P, T, st);
+        case 24: return small_fwd_launch<24>(P, T, st);
+        default: return small_fwd_launch<32>(P, T, st);
+    }
+}
+
+int u2gnn_layer_small_bwd(const u2gnn_small_tail_args *t, const float *W_in, uint64_t attn_seed, const float *ctx,
+                          int64_t ctx_floats, float *dQKV, int64_t ld_dqkv, int32_t accumulate_dx, float *ws,
+                          int64_t ws_floats, void *stream) {
+    int rc = ls_check(t, true);
+    if (rc != U2GNN_OK) return rc;
+    rc = sa_check(t->dp, t->d, t->n_valid, t->rows_pad, t->p, ctx, ctx_floats);
+    if (rc != U2GNN_OK) return rc;
+    if (!dQKV || ld_dqkv < 3 * t->dp || !ws || ws_floats < u2gnn_attn_small_ws_floats(t->n_valid, t->rows_pad, t->d) ||
+        (accumulate_dx && !W_in))
+        return U2GNN_E_ARG;
+    if (!al16(ws) || !al16(dQKV) || (ld_dqkv & 3) || !al16(t->dO)) return U2GNN_E_ALIGN;
+    SaP P = sa_params(t->dp, t->d, t->n_valid, t->rows_pad, t->p, attn_seed, const_cast<float *>(ctx));
+    P.dO = t->dO, P.ld_do = t->dp, P.delta = t->delta, P.q_scale = (float)(1.0 / std::sqrt((double)t->d));
+    P.rq = ws, P.out = dQKV, P.ld_out = ld_dqkv, P.w_in = W_in;
+    P.dx = accumulate_dx ? t->dX : nullptr, P.lddx = t->dp;
+    const LsP T = ls_params(t);
+    hipStream_t st = u2gnn_stream(stream);
+    switch (sa_dm(t->d)) {
+        case 4: return small_bwd_launch<4>(P, T, st);
+        case 8: return small_bwd_launch<8>(P, T, st);
+        case 12: return small_bwd_launch<12>(P, T, st);
+        case 16: return small_bwd_launch<16>(P, T, st);
+        case 20: return small_bwd_launch<20>(P, T, st);
+        case 24: return small_bwd_launch<24>(P, T, st);
+        default: return small_bwd_launch<32>(P, T, st);
+    }
+}
 
 }  // extern "C"

@@ -187,6 +187,9 @@ _HIP_SIGS = {
     "u2gnn_attn_small_ctx_floats": ([I64, I64], I64),
     "u2gnn_layer_tail_small_fwd": ([ctypes.POINTER(SmallTailArgs), VP], c_int32),
     "u2gnn_layer_tail_small_bwd": ([ctypes.POINTER(SmallTailArgs), VP], c_int32),
+    "u2gnn_layer_small_fwd": ([ctypes.POINTER(SmallTailArgs), VP, VP, c_uint64, VP, I64, VP], c_int32),
+    "u2gnn_layer_small_bwd": ([ctypes.POINTER(SmallTailArgs), VP, c_uint64, VP, I64, VP, I64, I32, VP, I64, VP],
+                              c_int32),
     "u2gnn_attn_small_ws_floats": ([I64, I64, I64], I64),
     "u2gnn_attn_small_fwd": ([VP, I64, VP, VP, I64, I64, I64, I64, F32, c_uint64, VP, I64, VP, I64, VP], c_int32),
     "u2gnn_attn_small_bwd": ([VP, I64, VP, I64, I64, I64, I64, F32, c_uint64, VP, I64, VP, F32, VP, I64, VP, I64, VP,

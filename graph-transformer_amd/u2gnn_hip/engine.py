@@ -406,11 +406,10 @@ def encoder_layer_forward(X: torch.Tensor, w: PackedLayer, p: LayerParams, dims:
                Cx2=QKV2, ldcx2=6 * dp, cx2_col0=2 * dp)
         Q, Kt, V = QKV[:, :dp], QKV[:, dp:2 * dp], QKV[:, 2 * dp:]
     if small:
-        # d <= 32: in-projection, softmax -> dropout -> P.V on the vector ALUs; the row statistics and a compact
-        # Q, K, V take the images' place in the context (encoder_layer.cpp layer_fwd, launch for launch)
+        # d <= 32: the whole layer on the vector ALUs (issued below with the tail: encoder_layer.cpp layer_fwd,
+        # launch for launch); the row statistics and a compact Q, K, V take the images' place in the context
         O = torch.empty(Np, dp, device=dev, dtype=f32)
         Pd = torch.empty(K.attn_small_ctx_floats(Np, d), device=dev, dtype=f32)
-        K.attn_small_fwd(X, dp, w.W_in, w.b_in, dp, d, N, Np, pd, seeds.get(SITE_ATTN, 0), O, dp, Pd)
     elif fused:
         # S = Q K^T written straight into the image buffer, with the softmax row partials of each 64-column
         # group from the GEMM epilogue; one fused softmax -> dropout -> P.V pass then overwrites S with the
@@ -436,11 +435,12 @@ def encoder_layer_forward(X: torch.Tensor, w: PackedLayer, p: LayerParams, dims:
     mean2 = torch.empty(Np, device=dev, dtype=f32)
     rstd2 = torch.empty(Np, device=dev, dtype=f32)
     if small:
-        # a3.3 + a3.4 row-local on the vector ALUs, one launch (encoder_layer.cpp layer_fwd)
-        K.layer_tail_small(False, N, Np, d, dp, ff, ffp, pd, (seeds.get(SITE_DROP1, 0), seeds.get(SITE_DROPFF, 0),
-                           seeds.get(SITE_DROP2, 0)), W_o=w.W_o, b_o=w.b_o, n1_w=p.n1_w, n1_b=p.n1_b, W1=w.W1,
-                           b1=w.b1, W2=w.W2, b2=w.b2, n2_w=p.n2_w, n2_b=p.n2_b, O=O, X=X, Z1=Z1, X1=X1, mean1=mean1,
-                           rstd1=rstd1, Hd=Hd, Z2=Z2, X2=X2, mean2=mean2, rstd2=rstd2)
+        # in-projection, attention, a3.3 + a3.4 on the vector ALUs: 2 or 3 launches (encoder_layer.cpp layer_fwd)
+        K.layer_small_fwd(N, Np, d, dp, ff, ffp, pd, (seeds.get(SITE_DROP1, 0), seeds.get(SITE_DROPFF, 0),
+                          seeds.get(SITE_DROP2, 0)), seeds.get(SITE_ATTN, 0), w.W_in, w.b_in, Pd, W_o=w.W_o,
+                          b_o=w.b_o, n1_w=p.n1_w, n1_b=p.n1_b, W1=w.W1, b1=w.b1, W2=w.W2, b2=w.b2, n2_w=p.n2_w,
+                          n2_b=p.n2_b, O=O, X=X, Z1=Z1, X1=X1, mean1=mean1, rstd1=rstd1, Hd=Hd, Z2=Z2, X2=X2,
+                          mean2=mean2, rstd2=rstd2)
     else:
         fuse = fused_ln(dp, _rp("out_proj", prec))   # LayerNorm in the GEMM epilogue when a 64-column tile holds whole rows
         K.gemm(O, w.W_o, Z1, Np, dp, dp, dp, dp, dp, trans_b=True,
@@ -499,11 +499,16 @@ def encoder_layer_backward(dX2: torch.Tensor, ctx: EncoderLayerCtx, w: PackedLay
         dX1, dF, dA, dO, dX = (torch.empty(Np, dp, device=dev, dtype=f32) for _ in range(5))
         dH = torch.empty(Np, ffp, device=dev, dtype=f32)
         delta = torch.empty(Np, device=dev, dtype=f32)
-        K.layer_tail_small(True, N, Np, d, dp, ff, ffp, pd, (seeds.get(SITE_DROP1, 0), seeds.get(SITE_DROPFF, 0),
-                           seeds.get(SITE_DROP2, 0)), W_o=w.W_o, b_o=w.b_o, n1_w=p.n1_w, n1_b=p.n1_b, W1=w.W1,
-                           b1=w.b1, W2=w.W2, b2=w.b2, n2_w=p.n2_w, n2_b=p.n2_b, O=ctx.O, Z1=ctx.Z1, X1=ctx.X1,
-                           mean1=ctx.mean1, rstd1=ctx.rstd1, Hd=ctx.Hd, Z2=ctx.Z2, mean2=ctx.mean2, rstd2=ctx.rstd2,
-                           dX2=dX2, dX1=dX1, dF=dF, dH=dH, dX=dX, dA=dA, dO=dO, delta=delta)
+        # the tail backward and the attention backward (dQKV; dX += dQKV W_in when the input gradient is wanted)
+        small_dqkv = torch.empty(Np, 3 * dp, device=dev, dtype=f32)
+        ws_a = torch.empty(K.attn_small_ws_floats(N, Np, d), device=dev, dtype=f32)
+        K.layer_small_bwd(N, Np, d, dp, ff, ffp, pd, (seeds.get(SITE_DROP1, 0), seeds.get(SITE_DROPFF, 0),
+                          seeds.get(SITE_DROP2, 0)), seeds.get(SITE_ATTN, 0), w.W_in, ctx.Pd, small_dqkv, need_dx,
+                          ws_a, W_o=w.W_o, b_o=w.b_o, n1_w=p.n1_w, n1_b=p.n1_b, W1=w.W1, b1=w.b1, W2=w.W2, b2=w.b2,
+                          n2_w=p.n2_w, n2_b=p.n2_b, O=ctx.O, Z1=ctx.Z1, X1=ctx.X1, mean1=ctx.mean1, rstd1=ctx.rstd1,
+                          Hd=ctx.Hd, Z2=ctx.Z2, mean2=ctx.mean2, rstd2=ctx.rstd2, dX2=dX2, dX1=dX1, dF=dF, dH=dH,
+                          dX=dX, dA=dA, dO=dO, delta=delta)
+        del ws_a
         off.run(lambda: K.layernorm_bwd_params(dX2, dp, ctx.Z2, dp, ctx.mean2, ctx.rstd2, dF, dp, N, d, dp, ws, g.n2_w,
                                                g.n2_b, g.l2_b), dX2, ctx.Z2, ctx.mean2, ctx.rstd2, dF, ws)
         off.run(lambda: _wgrad(dF, dp, ctx.Hd, ffp, dp, ffp, Np, g.l2_w, (dp, d), (ffp, ff), _rp("ffn2_dw", prec), N),
@@ -562,13 +567,9 @@ def encoder_layer_backward(dX2: torch.Tensor, ctx: EncoderLayerCtx, w: PackedLay
         delta = torch.empty(Np, device=dev, dtype=f32)
         K.rowdot(dO, dp, ctx.O, dp, delta, Np, dp)
     if small_attn(d):
-        # d <= 32: dQ, dK, dV with P recomputed from the saved context (ctx.Pd: row statistics + compact Q, K, V)
-        dQKV = torch.empty(Np, 3 * dp, device=dev, dtype=f32)
-        ws_a = torch.empty(K.attn_small_ws_floats(N, Np, d), device=dev, dtype=f32)
-        # ... and the in-projection's dX += dQKV W_in (no dX product in _in_proj_backward)
-        K.attn_small_bwd(ctx.Pd, w.W_in, dp, d, N, Np, pd, seeds.get(SITE_ATTN, 0), dO, dp, delta, 1.0 / math.sqrt(d),
-                         dQKV, 3 * dp, dX if need_dx else None, dp, ws_a)
-        del ws_a, dO
+        # d <= 32: dQ, dK, dV (P recomputed from the saved context) and dX += dQKV W_in, run with the tail above
+        dQKV = small_dqkv
+        del dO
     else:
         dQKV = _attn_bwd_products(ctx, dO, delta, N, Np, d, dp, pd, att, prec, dev)
     _in_proj_backward(dQKV, dX, ctx, w, g, N, Np, d, dp, prec, off, need_dx)

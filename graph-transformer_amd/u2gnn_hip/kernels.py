@@ -465,11 +465,7 @@ def attn_small_bwd(ctx, W_in, dp, d, n_valid, rows_pad, p, seed, dO, ld_do, delt
                                          _p(ws), int(ws.numel()), _s()), "u2gnn_attn_small_bwd")
 
 
-def layer_tail_small(backward, N, Np, d, dp, ff, ffp, p, seeds, **t):
-    """ABI v15 (d <= 32): the row-local tail of an encoder layer in one launch each way (small_layer.hip).
-    seeds = (drop1, dropff, drop2); t: the tensors of u2gnn_small_tail_args by field name (weights in the
-    padded layouts, LayerNorm parameters [d]).  Forward: O, X -> Z1, X1, mean1, rstd1, Hd, Z2, X2, mean2, rstd2;
-    backward: dX2 and the forward tensors -> dX1, dF, dH, dX, dA, dO, delta."""
+def _tail_args(N, Np, d, dp, ff, ffp, p, seeds, t):
     _dev(*t.values())
     a = _lib.SmallTailArgs()
     a.n_valid, a.rows_pad, a.d, a.dp, a.ff, a.ffp = int(N), int(Np), int(d), int(dp), int(ff), int(ffp)
@@ -477,10 +473,38 @@ def layer_tail_small(backward, N, Np, d, dp, ff, ffp, p, seeds, **t):
     a.seed_drop1, a.seed_dropff, a.seed_drop2 = [int(x) & 0xFFFFFFFFFFFFFFFF for x in seeds]
     for k, v in t.items():
         if k not in _lib._TAIL_PTRS:
-            raise _lib.U2GNNNativeError(f"layer_tail_small: unknown tensor {k}")
+            raise _lib.U2GNNNativeError(f"small-width layer: unknown tensor {k}")
         setattr(a, k, None if v is None else v.data_ptr())
+    return a
+
+
+def layer_tail_small(backward, N, Np, d, dp, ff, ffp, p, seeds, **t):
+    """ABI v15 (d <= 32): the row-local tail of an encoder layer in one launch each way (small_layer.hip).
+    seeds = (drop1, dropff, drop2); t: the tensors of u2gnn_small_tail_args by field name (weights in the
+    padded layouts, LayerNorm parameters [d]).  Forward: O, X -> Z1, X1, mean1, rstd1, Hd, Z2, X2, mean2, rstd2;
+    backward: dX2 and the forward tensors -> dX1, dF, dH, dX, dA, dO, delta."""
+    a = _tail_args(N, Np, d, dp, ff, ffp, p, seeds, t)
     fn = hip_lib().u2gnn_layer_tail_small_bwd if backward else hip_lib().u2gnn_layer_tail_small_fwd
     check(fn(ctypes.byref(a), _s()), "u2gnn_layer_tail_small_" + ("bwd" if backward else "fwd"))
+
+
+def layer_small_fwd(N, Np, d, dp, ff, ffp, p, seeds, attn_seed, W_in, b_in, ctx, **t):
+    """ABI v15 (d <= 32): the whole layer forward -- in-projection, node attention (O into t["O"], the attention
+    context into ctx) and the tail -- in 2 or 3 launches (attention and tail fused from 1024 padded rows)."""
+    _dev(W_in, b_in, ctx)
+    a = _tail_args(N, Np, d, dp, ff, ffp, p, seeds, t)
+    check(hip_lib().u2gnn_layer_small_fwd(ctypes.byref(a), _p(W_in), _p(b_in), int(attn_seed) & 0xFFFFFFFFFFFFFFFF,
+                                          _p(ctx), int(ctx.numel()), _s()), "u2gnn_layer_small_fwd")
+
+
+def layer_small_bwd(N, Np, d, dp, ff, ffp, p, seeds, attn_seed, W_in, ctx, dQKV, accumulate_dx, ws, **t):
+    """ABI v15 (d <= 32): the whole layer backward -- the tail backward (t: dX1, dF, dH, dX, dA, dO, delta) and the
+    attention backward (dQKV [rows_pad, 3 dp]; t["dX"] += dQKV W_in when accumulate_dx) in 2 or 3 launches."""
+    _dev(W_in, ctx, dQKV, ws)
+    a = _tail_args(N, Np, d, dp, ff, ffp, p, seeds, t)
+    check(hip_lib().u2gnn_layer_small_bwd(ctypes.byref(a), _p(W_in), int(attn_seed) & 0xFFFFFFFFFFFFFFFF, _p(ctx),
+                                          int(ctx.numel()), _p(dQKV), int(dQKV.stride(0)), 1 if accumulate_dx else 0,
+                                          _p(ws), int(ws.numel()), _s()), "u2gnn_layer_small_bwd")
 
 
 def sampled_softmax_bwd_rows(X, ldx, labels, sample_ids, S, W, ldw, prob, dloss, dX, lddx, dW_lab, dW_smp, n_rows, D):

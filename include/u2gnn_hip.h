@@ -467,6 +467,20 @@ typedef struct u2gnn_small_tail_args {
 int u2gnn_layer_tail_small_fwd(const u2gnn_small_tail_args *a, void *stream);
 int u2gnn_layer_tail_small_bwd(const u2gnn_small_tail_args *a, void *stream);
 
+/* ---- ABI v15: a whole small-width encoder layer (d <= 32, dp = 64) -- what the layer executor runs ----------
+ * fwd: the in-projection of t->X and the node attention (u2gnn_attn_small_fwd: O into t->O, the attention context
+ *      into ctx) and the tail (u2gnn_layer_tail_small_fwd) -- rows_pad >= 1024: attention and tail in ONE launch
+ *      (the O row goes from registers into its out-projection), below that as two; 2 or 3 launches.
+ * bwd: the tail backward (u2gnn_layer_tail_small_bwd: dX1, dF, dH, dA, dO, delta and the residual dX), then the
+ *      attention backward (u2gnn_attn_small_bwd: dQKV and, when accumulate_dx, dX += dQKV W_in) -- rows_pad >= 1024:
+ *      the tail backward and the dQ walk in ONE launch, its dO row and delta handed over in LDS; 2 or 3 launches.
+ * Same results as the separate calls up to the order of the hidden-unit partial sums of the fused forms. */
+int u2gnn_layer_small_fwd(const u2gnn_small_tail_args *t, const float *W_in, const float *b_in, uint64_t attn_seed,
+                          float *ctx, int64_t ctx_floats, void *stream);
+int u2gnn_layer_small_bwd(const u2gnn_small_tail_args *t, const float *W_in, uint64_t attn_seed, const float *ctx,
+                          int64_t ctx_floats, float *dQKV, int64_t ld_dqkv, int32_t accumulate_dx, float *ws,
+                          int64_t ws_floats, void *stream);
+
 /* ---- a12: dropout on the concatenated UnSup node embeddings (model_U2GNN_Unsup_multi.py:56) --
  * Y[i, j] = X[i, j] * keep(seed, i, j) / (1-p) for i < rows, j < cols.  The backward is the same
  * call on the upstream gradient with the same seed.  Y may alias X. */

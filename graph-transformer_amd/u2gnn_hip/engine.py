@@ -177,6 +177,7 @@ def side_stream(dev: torch.device) -> "torch.cuda.Stream":
     return s
 
 
+
 # The side stream pays only when the layer's kernels fill the chip: at C4 (Np*dp = 1.9M) it saves
 # 0.31 ms of a 3.27 ms step; at C5 (U2GNN-UnSup REDDIT, d = 4: Np*dp = 0.13M, ~2-10 us kernels) the
 # cross-stream hand-offs cost more than the overlap gains (1.116 vs 1.19-1.28 ms/step, one session,

@@ -1539,6 +1539,16 @@ int u2gnn_reduce_batch(const u2gnn_reduce_job *jobs, int32_t n, float *ws, int64
         } else if (J.cols == 0) {
             continue;   // u2gnn_colsum: nothing to sum
         }
+        if (!ln && J.rows == 0) {
+            // an all-zero column sum (the in-projection's key bias, exactly zero: encoder_layer.cpp) is the final
+            // pass over no partials: it rides with the other final jobs, and the slab reductions then need no
+            // 1024-thread launch of their own (C5: one reduction launch less per layer)
+            r.kind = RB_CS_FINAL;
+            r.nblk = (int32_t)((J.cols + FIN_COLS - 1) / FIN_COLS);
+            r.n = 0;
+            fin.push_back(r);
+            continue;
+        }
         if (p.small) {
             r.kind = ln ? RB_LN_SMALL : RB_CS_SMALL;
             r.nblk = (int32_t)((J.cols + 63) / 64);

@@ -749,7 +749,10 @@ def main():
             trainer.grad_sync = GradAllReduce(bucket_mb=8.0)
 
     nb = len(batches)
-    graph = args.graph == 1 and dist is None
+    # HIP-graph replay, also data parallel: the gradient all-reduce (per-layer buckets issued from the
+    # parameter-gradient side stream, or the buckets after the backward) is captured with the step, as in
+    # run_unsup; RCCL's communicator is set up by one eager step first
+    graph = args.graph == 1
     runner = None
     from u2gnn_hip import native
     from u2gnn_hip import _lib as LIB
@@ -761,6 +764,10 @@ def main():
     try:
         if graph:   # one captured HIP graph per distinct batch, captured (not run) before the warmup
             from u2gnn_hip.train import StepGraphs
+            if dist is not None:
+                trainer.step(batches[0])
+                torch.cuda.synchronize()
+                dist.barrier()
             runner = StepGraphs(trainer)
             for bt in batches:
                 runner.capture(bt)

@@ -233,8 +233,11 @@ int gemm_split(Arena &W, const Dims &D, const float *A, const float *B, float *C
     const int64_t bk = f32 ? 16 : 32;
     const bool plan = W.plan();
     const bool mapped = rblk != nullptr;
+    // (tiny: an accumulating product of at most 16 tiles and 16 K steps -- C2's dX += dQKV W_in, 4 tiles --
+    // runs as one short launch instead of 3 split-K blocks + a reduce launch; engine._gemm_split mirrors it)
+    const bool tiny = accumulate && Kd <= 512 && (M / 64) * (N / 64) <= 16;
     if (!f32 && !deep && !mapped && Kd <= 2048 && M % 64 == 0 && N % 64 == 0 &&
-        (M / 64) * (N / 64) >= 256) {
+        ((M / 64) * (N / 64) >= 256 || tiny)) {
         // shallow K (dH.W1, dQKV.W_in) with enough 64x64 tiles to fill the chip: no split, the
         // epilogue accumulates straight into C (no slabs, no reduce pass)
         G g(A, B, C, M, N, Kd, lda, ldb, ldc, prec);
@@ -272,12 +275,16 @@ int gemm_split(Arena &W, const Dims &D, const float *A, const float *B, float *C
         if (split > wgrad_split_max) split = wgrad_split_max;
         if (split < 1) split = 1;
     }
+    // a held-back product joins its layer's grouped launch, whose kernels are the 64x64, 16-deep 128x128 and
+    // 256x128 ones: a 128x128 job runs there as four 64x64 tiles (the split is chosen above, so the sums and
+    // bits are the same; C2's dV, dQ, dK: one launch instead of three)
+    const int t_group = (df && df->gemms && t == 128) ? 64 : t;
     if (split == 1 && !mapped) {
         G g(A, B, C, M, N, Kd, lda, ldb, ldc, prec);
         if (ta) g.ta();
         g.a.alpha = alpha;
         g.a.clamp_a = clamp_a;
-        g.epi(accumulate ? U2GNN_EPI_ACCUM : U2GNN_EPI_STORE).tile(t);
+        g.epi(accumulate ? U2GNN_EPI_ACCUM : U2GNN_EPI_STORE).tile(df && df->gemms && !accumulate ? t_group : t);
         if (df && df->gemms && !accumulate) {
             df->gemm.push_back(g.a);
             df->role.push_back(role);
@@ -294,7 +301,7 @@ int gemm_split(Arena &W, const Dims &D, const float *A, const float *B, float *C
     g.a.split_k = (int32_t)split;
     g.a.slab_stride = M * N;
     g.a.clamp_a = clamp_a;
-    g.tile(t);
+    g.tile(t_group);
     const int64_t rb0 = rblk ? rblk[0] : M, rb1 = rblk ? rblk[1] : M;
     const int64_t cb0 = cblk ? cblk[0] : N, cb1 = cblk ? cblk[1] : N;
     if (df) {   // slab reduce (and with df->gemms the GEMM itself) at the layer's flush
@@ -456,11 +463,15 @@ void set_ln(u2gnn_gemm_args &a, const float *gamma, const float *beta, float *y,
 
 // the fused attention forward (u2gnn_attn_softmax_pv): node-axis attention in the matrix-core
 // precisions with dp <= 384 (engine.fused_attn mirrors the rule)
-// split-K depth of FFN2 in the fused-LayerNorm (d <= 64) form: with fewer than 128 row-complete 64x64
-// tiles, aim at ~256 blocks of >= 4 K steps (engine.ffn2_split mirrors the rule)
-int64_t ffn2_split(bool fuse_ln, int64_t Np, int64_t ffp) {
-    if (!fuse_ln || Np / 64 >= 128) return 1;
-    int64_t sp = 256 / (Np / 64);
+// split-K depth of FFN2 in the matrix-core precisions (mfma), dp <= 256: with fewer than 128 output
+// tiles of 64x64, aim at ~256 blocks of >= 4 K steps; u2gnn_slab_bias_drop_resid_ln then forms the bias,
+// dropout, residual and LayerNorm2 (engine.ffn2_split mirrors the rule).  dp = 64 (C5 and the other
+// fused-LayerNorm layers) since round 3; dp <= 256 since round 5: C2's IMDBBINARY batches (Np = 128,
+// dp = 192) ran FFN2 as 6 blocks of a 32-step K loop, 16 us, plus a LayerNorm launch
+int64_t ffn2_split(int64_t dp, bool mfma, int64_t Np, int64_t ffp) {
+    const int64_t tiles = (Np / 64) * (dp / 64);
+    if (!mfma || dp > 256 || tiles >= 128) return 1;
+    int64_t sp = 256 / tiles;
     if (sp > ffp / 128) sp = ffp / 128;
     return sp > 1 ? sp : 1;
 }
@@ -592,9 +603,9 @@ int layer_fwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
             g.a.bias = w->b1, g.a.p_drop = pd, g.a.seed = s->dropff;
             U2GNN_TRY(g.run(st, plan));
         }
-        const int64_t f2_split = ffn2_split(fuse_ln, Np, ffp);
+        const int64_t f2_split = ffn2_split(dp, prec != U2GNN_PREC_F32, Np, ffp);
         if (f2_split > 1) {
-            // too few row-complete tiles (C5: 32 of them, each a 32-step K loop): split-K slabs, then the
+            // too few output tiles (C5: 32 of them, each a 32-step K loop): split-K slabs, then the
             // bias / dropout / residual / LayerNorm pass over the slabs
             float *slabs = W.take<float>(f2_split * Np * dp);
             G g(c.Hd, w->W2, slabs, Np, dp, ffp, ffp, ffp, dp, prec);
@@ -612,7 +623,7 @@ int layer_fwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
             if (fuse_ln) set_ln(g.a, w->n2_w, w->n2_b, X2, dp, c.mean2, c.rstd2, d, N);
             U2GNN_TRY(g.run(st, plan));
         }
-        if (!plan && !fuse_ln)
+        if (!plan && !fuse_ln && f2_split <= 1)
             U2GNN_TRY(u2gnn_layernorm_fwd(c.Z2, dp, w->n2_w, w->n2_b, X2, dp, c.mean2, c.rstd2, N, Np, d, dp, 1e-5f, st));
     }
     if ((W.overflow || CA.overflow) && debug_on())

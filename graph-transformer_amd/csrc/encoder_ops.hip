@@ -980,12 +980,14 @@ __global__ void __launch_bounds__(256) ln_param_reduce_kernel(const float *ws, i
 }
 
 // ------------------------------------------------------------------------------------------
-// a3.4 for d <= 64 encoders whose FFN2 product has too few row-complete 64x64 tiles to fill the chip
-// (C5: 32): the product runs split-K into slabs, and this pass sums the slabs (slab_reduce's order),
-// adds the bias, applies dropout (the GEMM epilogue's hash) and the residual -> Z, then the row's
-// LayerNorm (two-pass mean / mean square deviation over the first d columns) -> Y, mean, rstd.  One
-// wave per row, lane = column (dp == 64).
+// a3.4 for d <= 256 encoders whose FFN2 product has too few output tiles to fill the chip (C5: 32
+// row-complete 64x64 tiles; C2's IMDBBINARY batches: 4): the product runs split-K into slabs, and this
+// pass sums the slabs (slab_reduce's order), adds the bias, applies dropout (the GEMM epilogue's hash)
+// and the residual -> Z, then the row's LayerNorm (two-pass mean / mean square deviation over the first
+// d columns) -> Y, mean, rstd.  One wave per row; lane l holds columns l, l + 64, ... (CPL = dp / 64 of
+// them, coalesced per wave); at CPL = 1 the sums are the round-4 kernel's, term for term.
 // ------------------------------------------------------------------------------------------
+template <int CPL>
 __global__ void __launch_bounds__(256) slab_bias_drop_resid_ln_kernel(
     const float *src, int n_slab, int64_t slab_stride, int64_t ld_src, const float *bias, const float *resid,
     int64_t ld_res, float p, uint64_t seed, const uint64_t *seed_epoch, float *Z, int64_t ldz, const float *gamma,
@@ -993,28 +995,44 @@ __global__ void __launch_bounds__(256) slab_bias_drop_resid_ln_kernel(
     int64_t rows_pad, float eps) {
     seed = u2gnn_seed(seed, seed_epoch);
     const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int c = threadIdx.x & 63;
+    const int l = threadIdx.x & 63;
     if (row >= rows_pad) return;
-    const float *q = src + row * ld_src + c;
-    float a = 0.f, b = 0.f, e = 0.f, f = 0.f;
-    int z = 0;
-    for (; z + 4 <= n_slab; z += 4) {
-        const float l0 = q[(int64_t)z * slab_stride], l1 = q[(int64_t)(z + 1) * slab_stride];
-        const float l2 = q[(int64_t)(z + 2) * slab_stride], l3 = q[(int64_t)(z + 3) * slab_stride];
-        a += l0, b += l1, e += l2, f += l3;
+    float zz[CPL];
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) {
+        const int c = l + 64 * k;
+        const float *q = src + row * ld_src + c;
+        float a = 0.f, b = 0.f, e = 0.f, f = 0.f;
+        int z = 0;
+        for (; z + 4 <= n_slab; z += 4) {
+            const float l0 = q[(int64_t)z * slab_stride], l1 = q[(int64_t)(z + 1) * slab_stride];
+            const float l2 = q[(int64_t)(z + 2) * slab_stride], l3 = q[(int64_t)(z + 3) * slab_stride];
+            a += l0, b += l1, e += l2, f += l3;
+        }
+        for (; z < n_slab; ++z) a += q[(int64_t)z * slab_stride];
+        float x = ((a + b) + (e + f)) + bias[c];
+        if (p > 0.f) x = u2gnn_keep(seed, (uint32_t)row, (uint32_t)c, p) ? x * (1.f / (1.f - p)) : 0.f;
+        zz[k] = x + resid[row * ld_res + c];
+        Z[row * ldz + c] = zz[k];
+        s += c < d ? zz[k] : 0.f;
     }
-    for (; z < n_slab; ++z) a += q[(int64_t)z * slab_stride];
-    float x = ((a + b) + (e + f)) + bias[c];
-    if (p > 0.f) x = u2gnn_keep(seed, (uint32_t)row, (uint32_t)c, p) ? x * (1.f / (1.f - p)) : 0.f;
-    const float zz = x + resid[row * ld_res + c];
-    Z[row * ldz + c] = zz;
-    const float mu = wave_sum(c < d ? zz : 0.f) / (float)d;
-    const float t = c < d ? zz - mu : 0.f;
-    const float rs = rsqrtf(wave_sum(t * t) / (float)d + eps);
+    const float mu = wave_sum(s) / (float)d;
+    float q2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) {
+        const float t = l + 64 * k < d ? zz[k] - mu : 0.f;
+        q2 += t * t;
+    }
+    const float rs = rsqrtf(wave_sum(q2) / (float)d + eps);
     const bool live = row < rows_valid;
-    const int cc = c < d ? c : (int)d - 1;
-    Y[row * ldy + c] = (live && c < d) ? (zz - mu) * rs * gamma[cc] + beta[cc] : 0.f;
-    if (c == 0) {
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) {
+        const int c = l + 64 * k;
+        const int cc = c < d ? c : (int)d - 1;
+        Y[row * ldy + c] = (live && c < d) ? (zz[k] - mu) * rs * gamma[cc] + beta[cc] : 0.f;
+    }
+    if (l == 0) {
         mean[row] = live ? mu : 0.f;
         rstd[row] = live ? rs : 0.f;
     }
@@ -1492,13 +1510,24 @@ int u2gnn_slab_bias_drop_resid_ln(const float *src, int32_t n_slab, int64_t slab
                                    float *Z, int64_t ldz, const float *gamma, const float *beta, float *Y, int64_t ldy,
                                    float *mean, float *rstd, int64_t d, int64_t rows_valid, int64_t rows_pad, float eps,
                                    void *stream) {
-    if (!src || !bias || !resid || !Z || !gamma || !beta || !Y || !mean || !rstd || n_slab < 1 || d < 1 || d > 64 ||
-        rows_valid > rows_pad || ld_src < 64 || ld_res < 64 || ldz < 64 || ldy < 64 || p < 0.f || p >= 1.f)
+    const int64_t dp = (d + 63) / 64 * 64;   // padded width: columns per lane = dp / 64
+    if (!src || !bias || !resid || !Z || !gamma || !beta || !Y || !mean || !rstd || n_slab < 1 || d < 1 || d > 256 ||
+        rows_valid > rows_pad || ld_src < dp || ld_res < dp || ldz < dp || ldy < dp || p < 0.f || p >= 1.f)
         return U2GNN_E_ARG;
     if (rows_pad <= 0) return U2GNN_OK;
-    hipLaunchKernelGGL(slab_bias_drop_resid_ln_kernel, dim3((unsigned)((rows_pad + 3) / 4)), dim3(256), 0,
-                       u2gnn_stream(stream), src, n_slab, slab_stride, ld_src, bias, resid, ld_res, p, seed,
-                       u2gnn_g_epoch, Z, ldz, gamma, beta, Y, ldy, mean, rstd, d, rows_valid, rows_pad, eps);
+    const dim3 grid((unsigned)((rows_pad + 3) / 4));
+    hipStream_t st = u2gnn_stream(stream);
+#define U2GNN_SLAB_LN(CPL)                                                                                       \
+    hipLaunchKernelGGL(slab_bias_drop_resid_ln_kernel<CPL>, grid, dim3(256), 0, st, src, n_slab, slab_stride, ld_src, \
+                       bias, resid, ld_res, p, seed, u2gnn_g_epoch, Z, ldz, gamma, beta, Y, ldy, mean, rstd, d,      \
+                       rows_valid, rows_pad, eps)
+    switch (dp / 64) {
+        case 1: U2GNN_SLAB_LN(1); break;
+        case 2: U2GNN_SLAB_LN(2); break;
+        case 3: U2GNN_SLAB_LN(3); break;
+        default: U2GNN_SLAB_LN(4); break;
+    }
+#undef U2GNN_SLAB_LN
     return u2gnn_launch_status();
 }
 

@@ -276,8 +276,10 @@ def _gemm_split(A, B, C, M, N, Kd, lda, ldb, ldc, trans_a=False, trans_b=False, 
     alpha, accumulation and an optional padded->real block map (rblk, cblk).  clamp_a: A is the
     signed probability image (read as Pd)."""
     bk = 16 if prec == "fp32" else 32
+    # tiny: an accumulating product of <= 16 tiles and <= 16 K steps (C2's dX += dQKV W_in) as one short launch
+    tiny = accumulate and Kd <= 512 and (M // 64) * (N // 64) <= 16
     if (prec != "fp32" and not deep and rblk is None and Kd <= 2048 and M % 64 == 0
-            and N % 64 == 0 and (M // 64) * (N // 64) >= 256):
+            and N % 64 == 0 and ((M // 64) * (N // 64) >= 256 or tiny)):
         # shallow K (dH.W1, dQKV.W_in: K = ff, 3d) with enough 64x64 tiles to fill the chip: no
         # split, C (+)= alpha acc straight from the epilogue -- no slabs, no reduce pass
         K.gemm(A, B, C, M, N, Kd, lda, ldb, ldc, trans_a=trans_a, trans_b=trans_b, alpha=alpha,
@@ -338,12 +340,14 @@ def _gemm_nodes_k(A, B, C, M, N, Kd, lda, ldb, ldc, trans_a=False, alpha=1.0, pr
                 clamp_a=clamp_a, target256=120 if grouped else 240)
 
 
-def ffn2_split(fuse: bool, Np: int, ffp: int) -> int:
-    """Split-K depth of FFN2 in the fused-LayerNorm form (encoder_layer.cpp ffn2_split): with fewer than
-    128 row-complete 64x64 tiles, ~256 blocks of >= 4 K steps, finished by slab_bias_drop_resid_ln."""
-    if not fuse or Np // 64 >= 128:
+def ffn2_split(dp: int, mfma: bool, Np: int, ffp: int) -> int:
+    """Split-K depth of FFN2 in the matrix-core precisions (encoder_layer.cpp ffn2_split), dp <= 256: with
+    fewer than 128 output tiles of 64x64, ~256 blocks of >= 4 K steps, finished by slab_bias_drop_resid_ln
+    (bias, dropout, residual and LayerNorm2)."""
+    tiles = (Np // 64) * (dp // 64)
+    if not mfma or dp > 256 or tiles >= 128:
         return 1
-    return max(1, min(256 // (Np // 64), ffp // 128))
+    return max(1, min(256 // tiles, ffp // 128))
 
 
 def qk_tile(Np: int) -> int:
@@ -452,7 +456,8 @@ def encoder_layer_forward(X: torch.Tensor, w: PackedLayer, p: LayerParams, dims:
             K.layernorm_fwd(Z1, dp, p.n1_w, p.n1_b, X1, dp, mean1, rstd1, N, Np, d, dp)
         K.gemm(X1, w.W1, Hd, Np, ffp, dp, dp, dp, ffp, trans_b=True, epilogue=E.EPI_BIAS_RELU_DROP, bias=w.b1,
                p_drop=pd, seed=seeds.get(SITE_DROPFF, 0), precision=_rp("ffn1", prec), flops=2.0 * N * d * ff)
-        f2 = ffn2_split(fuse, Np, ffp)
+        # (dp = 64: the out-projection's fused-LayerNorm rule decides, as in round 3)
+        f2 = ffn2_split(dp, fuse if dp == 64 else _rp("ffn2", prec) != "fp32", Np, ffp)
         if f2 > 1:   # split-K slabs + the bias / dropout / residual / LayerNorm pass (encoder_layer.cpp layer_fwd)
             slabs = torch.empty(f2, Np, dp, device=dev, dtype=f32)
             K.gemm(Hd, w.W2, slabs, Np, dp, ffp, ffp, ffp, dp, trans_b=True, split_k=f2, slab_stride=Np * dp,
@@ -465,7 +470,7 @@ def encoder_layer_forward(X: torch.Tensor, w: PackedLayer, p: LayerParams, dims:
                    epilogue=E.EPI_BIAS_DROP_RESID_LN if fuse else E.EPI_BIAS_DROP_RESID, bias=w.b2,
                    aux0=X1, ld_aux=dp, p_drop=pd, seed=seeds.get(SITE_DROP2, 0), precision=_rp("ffn2", prec),
                    flops=2.0 * N * d * ff, ln=(p.n2_w, p.n2_b, X2, dp, mean2, rstd2, d, N, 1e-5) if fuse else None)
-        if not fuse:
+        if not fuse and f2 <= 1:
             K.layernorm_fwd(Z2, dp, p.n2_w, p.n2_b, X2, dp, mean2, rstd2, N, Np, d, dp)
     ctx = None
     if need_ctx:

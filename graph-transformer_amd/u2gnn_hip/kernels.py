@@ -560,10 +560,11 @@ def split_dropout_bwd(dY, ldy, N, Np, d, dp, p, seed, dsts):
 
 def slab_bias_drop_resid_ln(slabs, n_slab, slab_stride, bias, resid, p, seed, Z, gamma, beta, Y, mean, rstd, d,
                             rows_valid, rows_pad, eps=1e-5):
-    """FFN2's split-K epilogue for d <= 64 encoders (ABI v11): Z = resid + drop(sum of slabs + bias), Y = LN(Z).
-    slabs [n_slab, rows_pad, 64]; resid, Z, Y [rows_pad, 64]."""
+    """FFN2's split-K epilogue (ABI v11; d <= 256 since round 5): Z = resid + drop(sum of slabs + bias), Y = LN(Z).
+    slabs [n_slab, rows_pad, dp]; resid, Z, Y [rows_pad, dp] with dp = rup(d, 64)."""
     _dev(slabs, bias, resid, Z, gamma, beta, Y, mean, rstd)
-    check(hip_lib().u2gnn_slab_bias_drop_resid_ln(_p(slabs), int(n_slab), int(slab_stride), 64, _p(bias), _p(resid),
+    dp = -(-int(d) // 64) * 64
+    check(hip_lib().u2gnn_slab_bias_drop_resid_ln(_p(slabs), int(n_slab), int(slab_stride), dp, _p(bias), _p(resid),
                                                   int(resid.stride(0)), float(p), int(seed), _p(Z), int(Z.stride(0)),
                                                   _p(gamma), _p(beta), _p(Y), int(Y.stride(0)), _p(mean), _p(rstd),
                                                   int(d), int(rows_valid), int(rows_pad), float(eps), _s()),

@@ -282,10 +282,11 @@ typedef struct u2gnn_reduce_job {
 int64_t u2gnn_reduce_batch_ws_floats(const u2gnn_reduce_job *jobs, int32_t n);
 int u2gnn_reduce_batch(const u2gnn_reduce_job *jobs, int32_t n, float *ws, int64_t ws_floats, void *stream);
 
-/* ABI v11: FFN2's epilogue for d <= 64 encoders when the product runs split-K (too few row-complete tiles):
+/* ABI v11: FFN2's epilogue when the product runs split-K (too few output tiles to fill the chip):
  * Z = resid + drop(sum_z src[z] + bias) (dropout hash of U2GNN_EPI_BIAS_DROP_RESID), then the LayerNorm of
- * EPI_BIAS_DROP_RESID_LN over the first d columns: Y, mean, rstd (rows >= rows_valid: 0).  Padded width
- * 64 (one wave per row); bias / resid padded to 64 columns, gamma / beta unpadded [d]. */
+ * EPI_BIAS_DROP_RESID_LN over the first d columns: Y, mean, rstd (rows >= rows_valid: 0).  d <= 256 (round 5;
+ * d <= 64 before), padded width dp = rup(d, 64), one wave per row; bias / resid / slabs / Z / Y padded to dp
+ * columns, gamma / beta unpadded [d].  For d <= 64 the results are the round-4 kernel's, bit for bit. */
 int u2gnn_slab_bias_drop_resid_ln(const float *src, int32_t n_slab, int64_t slab_stride, int64_t ld_src,
                                    const float *bias, const float *resid, int64_t ld_res, float p, uint64_t seed,
                                    float *Z, int64_t ldz, const float *gamma, const float *beta, float *Y, int64_t ldy,

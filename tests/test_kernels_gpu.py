@@ -766,29 +766,33 @@ def test_sum_all_and_index_zero_rows2(n):
     assert torch.equal(W, ref)
 
 
-@pytest.mark.parametrize("d,p", [(4, 0.5), (19, 0.0), (64, 0.3)])
-def test_slab_bias_drop_resid_ln_against_fp64(d, p):
-    rows, Np, n_slab, seed, eps = 1914, 2048, 8, 987654321, 1e-5
-    slabs = _mk(n_slab, Np, 64, seed=70)
-    bias = torch.zeros(64, device=DEV)
+@pytest.mark.parametrize("d,p,rows,Np,n_slab", [(4, 0.5, 1914, 2048, 8), (19, 0.0, 1914, 2048, 8),
+                                                 (64, 0.3, 1914, 2048, 8), (136, 0.5, 80, 128, 8),
+                                                 (100, 0.0, 300, 384, 5), (256, 0.3, 250, 256, 3)])
+def test_slab_bias_drop_resid_ln_against_fp64(d, p, rows, Np, n_slab):
+    """d <= 64 (one column per lane) and the round-5 widths up to 256 (C2's IMDBBINARY: d = 136, dp = 192)."""
+    seed, eps = 987654321, 1e-5
+    dp = -(-d // 64) * 64
+    slabs = _mk(n_slab, Np, dp, seed=70)
+    bias = torch.zeros(dp, device=DEV)
     bias[:d] = _mk(d, seed=71)
-    resid = _mk(Np, 64, seed=72)
+    resid = _mk(Np, dp, seed=72)
     gamma, beta = _mk(d, seed=73), _mk(d, seed=74)
-    Z, Y = torch.full((Np, 64), float("nan"), device=DEV), torch.full((Np, 64), float("nan"), device=DEV)
+    Z, Y = torch.full((Np, dp), float("nan"), device=DEV), torch.full((Np, dp), float("nan"), device=DEV)
     mean, rstd = torch.full((Np,), float("nan"), device=DEV), torch.full((Np,), float("nan"), device=DEV)
-    K.slab_bias_drop_resid_ln(slabs, n_slab, Np * 64, bias, resid, p, seed, Z, gamma, beta, Y, mean, rstd, d, rows, Np,
+    K.slab_bias_drop_resid_ln(slabs, n_slab, Np * dp, bias, resid, p, seed, Z, gamma, beta, Y, mean, rstd, d, rows, Np,
                               eps)
     torch.cuda.synchronize()
     x = slabs.double().sum(0) + bias.double()
     if p > 0:
-        keep = K.dropout_mask(seed, Np, 64, p).bool()
+        keep = K.dropout_mask(seed, Np, dp, p).bool()
         x = torch.where(keep, x / (1 - p), torch.zeros_like(x))
     zr = resid.double() + x
     assert ((Z.double() - zr).abs().max() / zr.abs().max()).item() < 1e-6
     zd = Z.double()[:, :d]
     mu = zd.mean(1, keepdim=True)
     rs = 1.0 / torch.sqrt(((zd - mu) ** 2).mean(1, keepdim=True) + eps)
-    yr = torch.zeros(Np, 64, dtype=torch.float64, device=DEV)
+    yr = torch.zeros(Np, dp, dtype=torch.float64, device=DEV)
     yr[:rows, :d] = ((zd - mu) * rs * gamma.double() + beta.double())[:rows]
     assert (Y.double() - yr).abs().max().item() < 1e-4
     assert torch.equal(mean[rows:], torch.zeros_like(mean[rows:])) and torch.equal(rstd[rows:], torch.zeros_like(rstd[rows:]))

@@ -1,6 +1,7 @@
 #!/usr/bin/env bash
 # A/B kernel variants in ONE GPU session (box-to-box clock differences are ~5-7 %):
 #   bash tools/ab.sh "base exp_oldloop exp_nosb" [GB_ONLY shapes]
+# WL=c2 (or c5 / c3): the bench line of that workload instead of C4
 # base = the default library; others = graph-transformer_amd/lib/<name>.so.  Each variant runs
 # the GEMM micro-benchmark (optional shapes) and bench.py twice, interleaved.
 set -o pipefail
@@ -14,7 +15,11 @@ for rep in 1 2; do
     if [ -n "$ONLY" ] && [ $rep = 1 ]; then
       U2GNN_HIP_LIB=$L GB_ONLY="$ONLY" timeout -k 10 200 python tools/gemm_bench.py bf16x3 2>/dev/null | sed "s/^/$v /" || exit 1
     fi
+    if [ -n "${WL:-}" ]; then
+      U2GNN_HIP_LIB=$L timeout -k 10 200 python bench.py --workload $WL --steps 30 --warmup 5 --cpu-baseline 0 > gpurun_out/ab_$v.json 2>/dev/null || exit 1
+    else
     U2GNN_HIP_LIB=$L timeout -k 10 200 python bench.py --configs 0 --steps 30 --warmup 5 --cpu-baseline 0 --fp32-steps 0 --pipeline-steps 0 --no-roofline > gpurun_out/ab_$v.json 2>/dev/null || exit 1
+    fi
     python -c "import json;d=json.load(open('gpurun_out/ab_$v.json'));print('$v', 'step_ms', d['ms_per_step'], d['final_loss'])"
   done
 done

@@ -152,6 +152,9 @@ struct SpvP {
     float *Pd;             // signed image [rows_pad][ldp]
     int64_t ldp;
     float *Opart;          // [nsplit][rows_pad][dp]
+    float *O;              // direct: O itself [rows_pad][ldo] (no combine pass)
+    int64_t ldo;
+    int32_t direct;
     int32_t n_valid, rows_pad, kb_valid, kb_per_split, nsplit, qblocks;
     float p;
     uint64_t seed;
@@ -407,7 +410,8 @@ __global__ void __launch_bounds__(FA_NT, 1) attn_softmax_pv_kernel(SpvP P) {
         }
     }
     // ---- partial O of this key range: O^T lane layout = query l%32, d = 32 t + 8 g + 4 h .. +3
-    float *orow = P.Opart + ((int64_t)split * P.rows_pad + query) * DP;
+    // (direct: one key range and one query block cover everything -- O itself, padded rows 0 via P = 0)
+    float *orow = P.direct ? P.O + (int64_t)query * P.ldo : P.Opart + ((int64_t)split * P.rows_pad + query) * DP;
 #ifndef SPV_NO_OSTORE
 #pragma unroll
     for (int t = 0; t < DT; ++t)
@@ -421,6 +425,14 @@ __global__ void __launch_bounds__(FA_NT, 1) attn_softmax_pv_kernel(SpvP P) {
     for (int t = 0; t < DT; ++t) acc += o[t][0] + o[t][5];
     if (acc == 123.f) *orow = acc;
 #endif
+    if (P.direct) {   // the image's key padding of this block's rows (the combine pass's job otherwise)
+        const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int r = w; r < FA_BM; r += FA_NT / 64) {
+            float *prow = P.Pd + (int64_t)(qrow0 + r) * P.ldp;
+            for (int c = P.kb_valid * FA_BN + 4 * lane; c < P.rows_pad; c += 256)
+                *reinterpret_cast<float4 *>(prow + c) = z;
+        }
+    }
 }
 
 // O[row] = sum over the key ranges (fixed order s = 0, 1, ...); rows >= n_valid zero.  One thread per
@@ -516,11 +528,18 @@ int u2gnn_attn_softmax_pv(const float *S, int64_t lds, const float *rowpart, int
     P.Pd = Pd;
     P.ldp = ldp;
     P.Opart = ws;
+    P.O = O;
+    P.ldo = ldo;
     P.nsplit = spv_nsplit(n_valid);
     P.qblocks = (int32_t)((n_valid + FA_BM - 1) / FA_BM);   // blocks of padding rows only: zeroed below
     P.n_valid = (int32_t)n_valid;
     P.rows_pad = (int32_t)rows_pad;
     P.kb_valid = (int32_t)((n_valid + FA_BN - 1) / FA_BN);
+    // at most 4 key blocks and one query block over every padded row (C2's IMDBBINARY batches, ~80 nodes):
+    // one workgroup walks all the keys and writes O and the image padding itself -- no combine launch (the
+    // split saved less than the combine's launch; the O sums then run in key order in one accumulator)
+    P.direct = P.kb_valid <= 4 && (int64_t)P.qblocks * FA_BM == rows_pad;
+    if (P.direct) P.nsplit = 1;
     P.kb_per_split = (P.kb_valid + P.nsplit - 1) / P.nsplit;
     P.p = p;
     P.seed = seed;
@@ -536,7 +555,7 @@ int u2gnn_attn_softmax_pv(const float *S, int64_t lds, const float *rowpart, int
         default: launch_spv<384>(P, x3, st); break;
     }
     const int rc = u2gnn_launch_status();
-    if (rc != U2GNN_OK) return rc;
+    if (rc != U2GNN_OK || P.direct) return rc;
     const int64_t cthreads = rows_pad * (dp / 4) > rows_pad * 64 ? rows_pad * (dp / 4) : rows_pad * 64;
     hipLaunchKernelGGL(attn_pv_combine_kernel, dim3((unsigned)((cthreads + 255) / 256)), dim3(256), 0, st, ws, P.nsplit,
                        (int)rows_pad, (int)n_valid, (int)dp, O, ldo, Pd, ldp, P.kb_valid * FA_BN, P.qblocks * FA_BM);

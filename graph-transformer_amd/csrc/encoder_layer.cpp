@@ -278,13 +278,16 @@ int gemm_split(Arena &W, const Dims &D, const float *A, const float *B, float *C
     // a held-back product joins its layer's grouped launch, whose kernels are the 64x64, 16-deep 128x128 and
     // 256x128 ones: a 128x128 job runs there as four 64x64 tiles (the split is chosen above, so the sums and
     // bits are the same; C2's dV, dQ, dK: one launch instead of three)
-    const int t_group = (df && df->gemms && t == 128) ? 64 : t;
+    // A launch of fewer than 64 blocks of 128x128 runs them as 64x64 tiles too (4x the blocks for the same
+    // sums; C2's dX1 = dH W1: 8 blocks of a 4-step K loop, 8.6 us)
+    // (bf16 precisions, whose 64x64 and 128x128 kernels form the same k-ordered sums)
+    const int t_group = (!f32 && t == 128 && ((df && df->gemms) || (M / 128) * (N / 128) * split < 64)) ? 64 : t;
     if (split == 1 && !mapped) {
         G g(A, B, C, M, N, Kd, lda, ldb, ldc, prec);
         if (ta) g.ta();
         g.a.alpha = alpha;
         g.a.clamp_a = clamp_a;
-        g.epi(accumulate ? U2GNN_EPI_ACCUM : U2GNN_EPI_STORE).tile(df && df->gemms && !accumulate ? t_group : t);
+        g.epi(accumulate ? U2GNN_EPI_ACCUM : U2GNN_EPI_STORE).tile(t_group);
         if (df && df->gemms && !accumulate) {
             df->gemm.push_back(g.a);
             df->role.push_back(role);

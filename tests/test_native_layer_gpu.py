@@ -25,7 +25,10 @@ def _zeros_like_params(p: LayerParams) -> LayerParams:
 
 
 # d = 19, 4: fused LN and the small-width attention (small_layer.hip); (1920, 4, 1024): the C5 layer (long reductions batched at the end of a one-stream backward)
-@pytest.mark.parametrize("N,d,ff", [(300, 67, 128), (1000, 367, 1024), (300, 19, 128), (1920, 4, 1024)])
+# (80, 136, 1024) and (100, 100, 256): C2-class layers (round 5): one query block, the unsplit fused
+# softmax.P.V, FFN2 split-K + slab LayerNorm at dp = 192 / 128, the tiny direct dX1 product (ff = 256)
+@pytest.mark.parametrize("N,d,ff", [(300, 67, 128), (1000, 367, 1024), (300, 19, 128), (1920, 4, 1024),
+                                    (80, 136, 1024), (100, 100, 256)])
 @pytest.mark.parametrize("prec", ["bf16x3", "fp32", "mixed", "fwd32"])
 @pytest.mark.parametrize("train", [True, False])
 @pytest.mark.parametrize("side", [False, True])

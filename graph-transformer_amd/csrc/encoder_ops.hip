@@ -1545,7 +1545,7 @@ int64_t u2gnn_reduce_batch_ws_floats(const u2gnn_reduce_job *jobs, int32_t n) {
 int u2gnn_reduce_batch(const u2gnn_reduce_job *jobs, int32_t n, float *ws, int64_t ws_floats, void *stream) {
     if (n < 0 || (n && !jobs)) return U2GNN_E_ARG;
     if (ws && !al16(ws)) return U2GNN_E_ALIGN;
-    std::vector<RbJob> part, fin, small;
+    std::vector<RbJob> part, fin, small, zero;
     std::vector<const u2gnn_reduce_job *> slabs;
     int64_t off = 0;
     for (int32_t i = 0; i < n; ++i) {
@@ -1568,14 +1568,8 @@ int u2gnn_reduce_batch(const u2gnn_reduce_job *jobs, int32_t n, float *ws, int64
         } else if (J.cols == 0) {
             continue;   // u2gnn_colsum: nothing to sum
         }
-        if (!ln && J.rows == 0) {
-            // an all-zero column sum (the in-projection's key bias, exactly zero: encoder_layer.cpp) is the final
-            // pass over no partials: it rides with the other final jobs, and the slab reductions then need no
-            // 1024-thread launch of their own (C5: one reduction launch less per layer)
-            r.kind = RB_CS_FINAL;
-            r.nblk = (int32_t)((J.cols + FIN_COLS - 1) / FIN_COLS);
-            r.n = 0;
-            fin.push_back(r);
+        if (!ln && J.rows == 0) {   // an all-zero column sum (the in-projection's key bias: encoder_layer.cpp)
+            zero.push_back(r);
             continue;
         }
         if (p.small) {
@@ -1597,6 +1591,21 @@ int u2gnn_reduce_batch(const u2gnn_reduce_job *jobs, int32_t n, float *ws, int64
         r.nblk = (int32_t)(((ln ? J.d : J.cols) + FIN_COLS - 1) / FIN_COLS);
         r.n = (int32_t)p.chunks;
         fin.push_back(r);
+    }
+    // An all-zero column sum rides with a launch that runs anyway: the single-pass small jobs' when there are
+    // any (C2, C3: every column sum is small, so no final pass is launched for it), else the final pass over
+    // no partials (C5: the slab reductions then need no 1024-thread launch of their own) -- same zeros either way
+    for (RbJob &r : zero) {
+        if (!small.empty()) {
+            r.kind = RB_CS_SMALL;
+            r.nblk = (int32_t)((r.cols + 63) / 64);
+            small.push_back(r);
+        } else {
+            r.kind = RB_CS_FINAL;
+            r.nblk = (int32_t)((r.cols + FIN_COLS - 1) / FIN_COLS);
+            r.n = 0;
+            fin.push_back(r);
+        }
     }
     // slab jobs ride with the small jobs' launch when there is one (per-thread bodies: any block size)
     const int slab_nt = small.empty() ? 256 : 1024;

@@ -108,6 +108,9 @@ struct Ctx {   // tensors saved by the forward for the backward
 // node attention for d <= 32 on the vector ALUs (u2gnn_attn_small_*, small_layer.hip): every precision, no
 // N x N image (engine.small_attn mirrors the rule)
 bool small_attn(const Dims &D) { return !D.window && D.d <= 32; }
+// the forward tail (a3.3 + a3.4) of a mid-width layer with few rows as one row-block kernel + the slab LayerNorm
+// (mid_layer.hip; C2: 2 launches instead of 5); engine.mid_tail mirrors the rule
+bool mid_tail(const Dims &D) { return !D.window && D.d > 32 && D.dp <= 256 && D.Np <= 512; }
 
 Ctx carve_ctx(Arena &A, const Dims &D, bool drop) {
     Ctx c;
@@ -586,6 +589,15 @@ int layer_fwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
     }
     if (small_attn(D)) {
         // a3.3 + a3.4: run by u2gnn_layer_small_fwd above
+    } else if (mid_tail(D)) {
+        // a3.3 + a3.4 in two launches: out-projection .. FFN2 partials per row block and hidden chunk, then the
+        // slab LayerNorm2 (mid_layer.hip)
+        const int64_t wsf = u2gnn_layer_tail_mid_ws_floats(Np, dp, ffp);
+        float *mws = W.take<float>(wsf > 0 ? wsf : 1);
+        if (!plan) {
+            const u2gnn_small_tail_args t = tail_args(D, w, s, c, X, X2);
+            U2GNN_TRY(u2gnn_layer_tail_mid_fwd(&t, mws, wsf, st));
+        }
     } else {
         // a3.3 out-projection + dropout1 + residual, LayerNorm1 (fused into the GEMM epilogue when a
         // 64-column tile holds whole rows: d <= 64, bf16 modes; engine.fused_ln mirrors the rule)

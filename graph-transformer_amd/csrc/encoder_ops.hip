@@ -997,6 +997,7 @@ __global__ void __launch_bounds__(256) slab_bias_drop_resid_ln_kernel(
     const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     const int l = threadIdx.x & 63;
     if (row >= rows_pad) return;
+    const bool live = row < rows_valid;   // padding rows: Z, Y, mean, rstd all 0
     float zz[CPL];
     float s = 0.f;
 #pragma unroll
@@ -1014,7 +1015,7 @@ __global__ void __launch_bounds__(256) slab_bias_drop_resid_ln_kernel(
         float x = ((a + b) + (e + f)) + bias[c];
         if (p > 0.f) x = u2gnn_keep(seed, (uint32_t)row, (uint32_t)c, p) ? x * (1.f / (1.f - p)) : 0.f;
         zz[k] = x + resid[row * ld_res + c];
-        Z[row * ldz + c] = zz[k];
+        Z[row * ldz + c] = live ? zz[k] : 0.f;
         s += c < d ? zz[k] : 0.f;
     }
     const float mu = wave_sum(s) / (float)d;
@@ -1025,7 +1026,6 @@ __global__ void __launch_bounds__(256) slab_bias_drop_resid_ln_kernel(
         q2 += t * t;
     }
     const float rs = rsqrtf(wave_sum(q2) / (float)d + eps);
-    const bool live = row < rows_valid;
 #pragma unroll
     for (int k = 0; k < CPL; ++k) {
         const int c = l + 64 * k;

@@ -30,7 +30,7 @@ ERRORS = {-1: "bad argument", -2: "misaligned pointer / leading dimension", -3: 
 
 EPI_STORE, EPI_BIAS, EPI_BIAS_DROP_RESID, EPI_BIAS_RELU_DROP, EPI_RELU_DROP_BWD, EPI_ACCUM, EPI_ATTN_DS, \
     EPI_ATTN_DS_SIGNED, EPI_ATTN_DS_RECOMP, EPI_BIAS_DROP_RESID_LN, EPI_STORE_ROWDOT, EPI_STORE_ROWSTAT = range(12)
-ABI_VERSION = 15   # include/u2gnn_hip.h U2GNN_ABI_VERSION
+ABI_VERSION = 16   # include/u2gnn_hip.h U2GNN_ABI_VERSION
 PREC_F32, PREC_BF16X3, PREC_BF16 = 0, 1, 2
 
 
@@ -191,6 +191,8 @@ _HIP_SIGS = {
     "u2gnn_layer_small_bwd": ([ctypes.POINTER(SmallTailArgs), VP, c_uint64, VP, I64, VP, I64, I32, VP, I64, VP],
                               c_int32),
     "u2gnn_attn_small_ws_floats": ([I64, I64, I64], I64),
+    "u2gnn_layer_tail_mid_ws_floats": ([I64, I64, I64], I64),
+    "u2gnn_layer_tail_mid_fwd": ([ctypes.POINTER(SmallTailArgs), VP, I64, VP], c_int32),
     "u2gnn_attn_small_fwd": ([VP, I64, VP, VP, I64, I64, I64, I64, F32, c_uint64, VP, I64, VP, I64, VP], c_int32),
     "u2gnn_attn_small_bwd": ([VP, I64, VP, I64, I64, I64, I64, F32, c_uint64, VP, I64, VP, F32, VP, I64, VP, I64, VP,
                               I64, VP], c_int32),

@@ -366,6 +366,12 @@ def small_attn(d: int) -> bool:
     return d <= SMALL_ATTN_MAX_D
 
 
+def mid_tail(d: int, dp: int, Np: int) -> bool:
+    """The forward tail (a3.3 + a3.4) of a mid-width layer with few rows as one row-block kernel + the slab
+    LayerNorm (u2gnn_layer_tail_mid_fwd; encoder_layer.cpp mid_tail applies the same rule)."""
+    return d > SMALL_ATTN_MAX_D and dp <= 256 and Np <= 512
+
+
 def fused_attn(dp: int, prec_qk: str, prec_pv: str) -> bool:
     """Node-axis attention forward through the fused softmax.P.V kernel: matrix-core precisions,
     dp <= 384 (encoder_layer.cpp fused_attn)."""
@@ -446,6 +452,15 @@ def encoder_layer_forward(X: torch.Tensor, w: PackedLayer, p: LayerParams, dims:
                           b_o=w.b_o, n1_w=p.n1_w, n1_b=p.n1_b, W1=w.W1, b1=w.b1, W2=w.W2, b2=w.b2, n2_w=p.n2_w,
                           n2_b=p.n2_b, O=O, X=X, Z1=Z1, X1=X1, mean1=mean1, rstd1=rstd1, Hd=Hd, Z2=Z2, X2=X2,
                           mean2=mean2, rstd2=rstd2)
+    elif mid_tail(d, dp, Np):
+        # a3.3 + a3.4 in two launches: out-projection .. FFN2 partials per row block and hidden chunk, then the slab
+        # LayerNorm2 (mid_layer.hip; encoder_layer.cpp layer_fwd, launch for launch)
+        ws = torch.empty(K.layer_tail_mid_ws_floats(Np, dp, ffp), device=dev, dtype=f32)
+        K.layer_tail_mid_fwd(N, Np, d, dp, ff, ffp, pd, (seeds.get(SITE_DROP1, 0), seeds.get(SITE_DROPFF, 0),
+                             seeds.get(SITE_DROP2, 0)), ws, W_o=w.W_o, b_o=w.b_o, n1_w=p.n1_w, n1_b=p.n1_b, W1=w.W1,
+                             b1=w.b1, W2=w.W2, b2=w.b2, n2_w=p.n2_w, n2_b=p.n2_b, O=O, X=X, Z1=Z1, X1=X1, mean1=mean1,
+                             rstd1=rstd1, Hd=Hd, Z2=Z2, X2=X2, mean2=mean2, rstd2=rstd2)
+        del ws
     else:
         fuse = fused_ln(dp, _rp("out_proj", prec))   # LayerNorm in the GEMM epilogue when a 64-column tile holds whole rows
         K.gemm(O, w.W_o, Z1, Np, dp, dp, dp, dp, dp, trans_b=True,

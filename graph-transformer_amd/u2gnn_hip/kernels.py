@@ -488,6 +488,18 @@ def layer_tail_small(backward, N, Np, d, dp, ff, ffp, p, seeds, **t):
     check(fn(ctypes.byref(a), _s()), "u2gnn_layer_tail_small_" + ("bwd" if backward else "fwd"))
 
 
+def layer_tail_mid_ws_floats(Np, dp, ffp):
+    return int(hip_lib().u2gnn_layer_tail_mid_ws_floats(int(Np), int(dp), int(ffp)))
+
+
+def layer_tail_mid_fwd(N, Np, d, dp, ff, ffp, p, seeds, ws, **t):
+    """ABI v16 (d <= 256): the forward tail of a mid-width layer -- out-projection .. LayerNorm2 -- in two launches
+    (mid_layer.hip + the slab LayerNorm); t: the forward tensors of u2gnn_small_tail_args; ws: the chunk slabs."""
+    _dev(ws)
+    a = _tail_args(N, Np, d, dp, ff, ffp, p, seeds, t)
+    check(hip_lib().u2gnn_layer_tail_mid_fwd(ctypes.byref(a), _p(ws), int(ws.numel()), _s()), "u2gnn_layer_tail_mid_fwd")
+
+
 def layer_small_fwd(N, Np, d, dp, ff, ffp, p, seeds, attn_seed, W_in, b_in, ctx, **t):
     """ABI v15 (d <= 32): the whole layer forward -- in-projection, node attention (O into t["O"], the attention
     context into ctx) and the tail -- in 2 or 3 launches (attention and tail fused from 1024 padded rows)."""

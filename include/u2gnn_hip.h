@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define U2GNN_ABI_VERSION 15
+#define U2GNN_ABI_VERSION 16
 
 #define U2GNN_OK 0
 #define U2GNN_E_ARG (-1)    /* bad size / null pointer */
@@ -481,6 +481,17 @@ int u2gnn_layer_small_fwd(const u2gnn_small_tail_args *t, const float *W_in, con
 int u2gnn_layer_small_bwd(const u2gnn_small_tail_args *t, const float *W_in, uint64_t attn_seed, const float *ctx,
                           int64_t ctx_floats, float *dQKV, int64_t ld_dqkv, int32_t accumulate_dx, float *ws,
                           int64_t ws_floats, void *stream);
+
+/* ---- ABI v16: the forward tail (a3.3 + a3.4) of a mid-width layer (d <= 256, dp = rup(d, 64); the layer
+ * executor uses it from d > 32 up to rows_pad <= 512: C2's IMDBBINARY batches) -- what five GEMM / LayerNorm
+ * launches did (out-projection, LayerNorm1, FFN1, FFN2, LayerNorm2) in two: a row-block x hidden-chunk kernel
+ * (out-projection + dropout1 + residual + LayerNorm1, FFN1 + ReLU + dropout for its 128 hidden units, their
+ * FFN2 partial sums into chunk slabs in ws) and u2gnn_slab_bias_drop_resid_ln over the ceil(ffp / 128) slabs.
+ * Exact fp32 on the vector ALUs, deterministic; rows >= n_valid written as 0 (Z1, X1, Hd, Z2, X2, statistics).
+ * Fields as u2gnn_small_tail_args (forward inputs and outputs); rows_pad % 4 == 0; W_o, W1, W2, O, ws 16-byte
+ * aligned.  ws: u2gnn_layer_tail_mid_ws_floats floats (-1 for unsupported sizes). */
+int64_t u2gnn_layer_tail_mid_ws_floats(int64_t rows_pad, int64_t dp, int64_t ffp);
+int u2gnn_layer_tail_mid_fwd(const u2gnn_small_tail_args *t, float *ws, int64_t ws_floats, void *stream);
 
 /* ---- a12: dropout on the concatenated UnSup node embeddings (model_U2GNN_Unsup_multi.py:56) --
  * Y[i, j] = X[i, j] * keep(seed, i, j) / (1-p) for i < rows, j < cols.  The backward is the same

@@ -9,7 +9,7 @@ C=$R/graph-transformer_amd/csrc
 B=$(mktemp -d)
 H="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -fno-slp-vectorize -I$R/include -I$C -Wall -Wno-unused-function"
 pids=()
-for f in gemm encoder_ops head_ops window_attn attn_fused small_layer; do $H "$@" -c $C/$f.hip -o $B/$f.o & pids+=($!); done
+for f in gemm encoder_ops head_ops window_attn attn_fused small_layer mid_layer; do $H "$@" -c $C/$f.hip -o $B/$f.o & pids+=($!); done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O2 -std=c++17 -fPIC -I$R/include -I$C "$@" -c $C/encoder_layer.cpp -o $B/encoder_layer.o
 for p in "${pids[@]}"; do wait $p || { echo "build_variant: a compile failed"; rm -rf $B; exit 1; }; done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $R/graph-transformer_amd/lib/exp_$NAME.so $B/*.o

@@ -259,3 +259,24 @@ def test_layer_executor_refuses_undersized_buffers_before_launching():
     rc = lib.u2gnn_layer_bwd(ctypes.byref(dims), ctypes.byref(params), ctypes.byref(seeds), fake, fake, c.value - 256,
                              fake, fake, ctypes.byref(grads), fake, b.value, None, None)
     assert rc == -1
+
+
+def test_round5_shape_rules():
+    """The Python orchestration's copies of the executor's round-5 shape rules (encoder_layer.cpp mid_tail,
+    ffn2_split; engine.py mirrors them launch for launch) at the bench configurations, and the mid tail's
+    workspace sizing (a host-only entry point)."""
+    from u2gnn_hip import engine as E
+    from u2gnn_hip import kernels as K
+    assert E.mid_tail(136, 192, 128) and E.mid_tail(100, 128, 128) and E.mid_tail(40, 64, 512)   # C2-class
+    assert not E.mid_tail(32, 64, 128)        # d <= 32: the small-width layer
+    assert not E.mid_tail(367, 384, 4864)     # C4: the matrix-core path
+    assert not E.mid_tail(136, 192, 640)      # more than 512 padded rows
+    assert E.ffn2_split(128, True, 128, 1024) == 8     # C2: 4 output tiles -> 8 slabs of 4 K steps
+    assert E.ffn2_split(384, True, 4864, 1024) == 1    # C4: 456 tiles fill the chip
+    assert E.ffn2_split(64, True, 2048, 1024) == 8     # a d <= 64 layer at 2048 rows (the round-3 rule)
+    assert E.ffn2_split(128, False, 128, 1024) == 1    # fp32 parity path: no split
+    assert E.ffn2_split(320, True, 128, 1024) == 1     # dp > 256: no slab LayerNorm
+    assert K.layer_tail_mid_ws_floats(128, 128, 1024) == 8 * 128 * 128
+    assert K.layer_tail_mid_ws_floats(128, 192, 256) == 2 * 128 * 192   # ff = 200 padded to 256: 2 chunks
+    assert K.layer_tail_mid_ws_floats(128, 192, 200) == -1              # unpadded widths are refused
+    assert K.layer_tail_mid_ws_floats(128, 320, 1024) == -1

@@ -13,7 +13,7 @@
 //   * FFN1 for the chunk's hidden units, ReLU, dropout, Hd stored;
 //   * the chunk's FFN2 partial sums into slab `chunk`;
 // then u2gnn_slab_bias_drop_resid_ln sums the chunk slabs and forms bias, dropout2, residual and LayerNorm2.
-// Exact fp32 on the vector ALUs (k-ordered fmaf chains, fixed reduction orders: deterministic), the same dropout
+// Exact fp32 on the vector ALUs (per-lane fmaf partials, a fixed butterfly / block reduction order: deterministic), the same dropout
 // hash (u2gnn_keep) as every other site.  Rows >= n_valid come out as zeros.
 #include "u2gnn_common.h"
 

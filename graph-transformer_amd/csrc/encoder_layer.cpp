@@ -883,7 +883,8 @@ int u2gnn_probe_arm(int32_t role, int32_t capacity) {
     if (role < U2GNN_ROLE_QK || role > U2GNN_ROLE_DK || capacity < 1 || capacity > (1 << 16)) return U2GNN_E_ARG;
     hipEvent_t *ev = new hipEvent_t[2 * capacity];
     for (int i = 0; i < 2 * capacity; ++i) {
-        // timing events without the system-scope release (both ends order work of this device only): with
+        // timing events without the system-scope release (the host reads only their timestamps, in
+        // u2gnn_probe_collect, after the bench's device synchronize; no data is handed over through them): with
         // it, each mark wrote L2 back and the timed kernel re-fetched its operands -- C4 dS 99.9 -> 89.3 us in
         // rocprof, probe 107.5 -> 93.8 us, step 3.034 -> 3.018 ms (no probe: 3.002; profiles/r05/ab_probe_fence.txt)
         const hipError_t e = hipEventCreateWithFlags(&ev[i], hipEventDisableSystemFence);

@@ -1,7 +1,7 @@
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; mkdir -p gpurun_out; export TMPDIR=/tmp
 PCMD="python bench.py --steps 30 --warmup 5 --cpu-baseline 0 --fp32-steps 0 --pipeline-steps 0 --configs 0"
-for v in base exp_probenf; do
+for v in ${VARS:-base exp_probenf}; do
   if [ $v = base ]; then L=""; else L="$R/graph-transformer_amd/lib/$v.so"; fi
   U2GNN_HIP_LIB=$L GPU_MAX_HW_QUEUES=8 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/pp_$v" -o run -- $PCMD > gpurun_out/pp_$v.json 2> gpurun_out/pp_$v.err || exit 1
   DB=$(find "$R/gpurun_out/pp_$v" -name '*.db' | head -1)

@@ -329,6 +329,61 @@ constexpr int bf16_smem_elems() {
     return 2 * 2 * (AE + BE);
 }
 
+// dS epilogue through LDS (the C4 dS product: 128 x 128 blocks of 2 x 2 waves, 32-deep K step): each wave's
+// 64 x 64 result goes to LDS in the MFMA layout and comes back row-contiguous (16 lanes x 16 B per row, 4 rows
+// per instruction), so the probability-image loads and the dS stores cover whole 128-byte lines per
+// instruction instead of 32 rows x 32 B; the per-element arithmetic is epilogue4's (same bits).  The live dS
+// probe in the C4 step: 85 vs 93-94 us, step 2.922-2.926 vs 2.934-2.976 ms (profiles/r05/ab_ds_lds_epilogue.txt).
+// The first half's operands are fetched before the main loop (as the MFMA-layout form did for slice 0).
+constexpr int DSL_PITCH = 68;   // floats per LDS row (64 + 4)
+struct DsPre {
+    float4 p[8];
+    float dl[8];
+};
+__device__ __forceinline__ void ds_lds_fetch(const GemmP &P, int r0, int c0, int lane, int it0, DsPre &f) {
+    const int rl = lane >> 4, cl = (lane & 15) * 4;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const int row = r0 + rl + 4 * (it0 + q);
+        f.p[q] = ld4(P.aux0 + (int64_t)row * P.ld_aux + c0 + cl);
+        f.dl[q] = P.rowvec[row];
+    }
+}
+__device__ __forceinline__ void ds_lds_store(const GemmP &P, float *C, const f32x16 (&acc)[2][2], int r0, int c0,
+                                             int wave, int lane, __bf16 *smem, const DsPre &pre) {
+    constexpr int E = U2GNN_EPI_ATTN_DS_SIGNED;
+    const int li = lane & 31, kh = lane >> 5;
+    DsPre hi;
+    ds_lds_fetch(P, r0, c0, lane, 8, hi);   // the second half's operands in flight under the first half
+    float *L = reinterpret_cast<float *>(smem) + wave * 64 * DSL_PITCH;
+    __syncthreads();   // every wave is done with the main loop's LDS images
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+                *reinterpret_cast<float4 *>(L + (32 * i + li) * DSL_PITCH + 32 * j + 8 * g + 4 * kh) =
+                    make_float4(acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]);
+    __syncthreads();
+    const int rl = lane >> 4, cl = (lane & 15) * 4;
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const int r = rl + 4 * q;
+        const float4 v = *reinterpret_cast<const float4 *>(L + r * DSL_PITCH + cl);
+        *reinterpret_cast<float4 *>(C + (int64_t)(r0 + r) * P.ldc + c0 + cl) =
+            epilogue4<E>(P, r0 + r, c0 + cl, v, pre.p[q], z4, 0u, pre.dl[q]);
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const int r = rl + 4 * (q + 8);
+        const float4 v = *reinterpret_cast<const float4 *>(L + r * DSL_PITCH + cl);
+        *reinterpret_cast<float4 *>(C + (int64_t)(r0 + r) * P.ldc + c0 + cl) =
+            epilogue4<E>(P, r0 + r, c0 + cl, v, hi.p[q], z4, 0u, hi.dl[q]);
+    }
+}
+
 template <int BM, int BN, int WM, int WN, int BK, bool TA, bool TB, int EPI, bool SPLIT, bool CLAMP>
 __device__ __forceinline__ void gemm_bf16_body(const GemmP &P, int tmi, int tni, int zi, __bf16 *smem) {
     constexpr int NT = 64 * WM * WN;
@@ -398,8 +453,12 @@ __device__ __forceinline__ void gemm_bf16_body(const GemmP &P, int tmi, int tni,
         }
     };
 
+    constexpr bool DSL = EPI == U2GNN_EPI_ATTN_DS_SIGNED && BM == 128 && BN == 128 && WM == 2 && WN == 2 && BK == 32;
+    static_assert(!DSL || 4 * 64 * DSL_PITCH * 4 <= 2 * bf16_smem_elems<BM, BN, BK, TA, TB>(), "dS LDS epilogue image");
+    DsPre dsl;
+    if constexpr (DSL) ds_lds_fetch(P, m0 + wm * WTM, n0 + wn * WTN, lane, 0, dsl);
     PreDS<TN> pre;
-    const bool use_pre = (EPI == U2GNN_EPI_ATTN_DS && P.keep != nullptr) || ds_signed<EPI>;
+    const bool use_pre = !DSL && ((EPI == U2GNN_EPI_ATTN_DS && P.keep != nullptr) || ds_signed<EPI>);
     if (use_pre) prefetch_ds<EPI>(P, m0 + wm * WTM + li, n0 + wn * WTN, kh, pre);
     // 64 x 64 tiles with row-operand epilogues: the slice's residual / bias / accumulator / ReLU operands
     // requested before the main loop (the short K loops of these products do not hide the epilogue's round
@@ -439,6 +498,10 @@ __device__ __forceinline__ void gemm_bf16_body(const GemmP &P, int tmi, int tni,
         }
     }
 
+    if constexpr (DSL) {
+        ds_lds_store(P, P.C + (int64_t)zi * P.slab_stride, acc, m0 + wm * WTM, n0 + wn * WTN, wave, lane, smem, dsl);
+        return;
+    }
     store_tile<EPI>(P, P.C + (int64_t)zi * P.slab_stride, acc, m0 + wm * WTM, n0 + wn * WTN, li, kh,
                     use_pre ? &pre : nullptr, PRE_AUX ? &pa : nullptr);
 }

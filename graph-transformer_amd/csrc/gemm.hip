@@ -692,7 +692,8 @@ int gemm_plan(const u2gnn_gemm_args *a, GemmPlan &G) {
          e == U2GNN_EPI_STORE_ROWDOT || e == U2GNN_EPI_ATTN_DS ||
          e == U2GNN_EPI_ATTN_DS_SIGNED) && !a->aux0)
         return U2GNN_E_ARG;
-    if (e == U2GNN_EPI_ATTN_DS_SIGNED && (!a->rowvec || !(a->p_drop < 1.f))) return U2GNN_E_ARG;
+    // (C required and no x2 copy: the 128 x 128 dS kernel stages its result through LDS into C alone)
+    if (e == U2GNN_EPI_ATTN_DS_SIGNED && (!a->rowvec || !(a->p_drop < 1.f) || !a->C || a->Cx2)) return U2GNN_E_ARG;
     if (a->rowvec_parts > 1 && (e != U2GNN_EPI_ATTN_DS_SIGNED || a->ld_rowvec < a->M)) return U2GNN_E_ARG;
     if (e == U2GNN_EPI_STORE_ROWDOT &&
         (split != 1 || a->Cx2 || !a->aux0 || !a->rowpart || a->ld_rowpart < a->M || (a->N & 63)))

@@ -120,7 +120,8 @@ typedef struct u2gnn_gemm_args {
     const void *A2;       /* unused (retired with a_x2 / b_x2) */
     const void *B2;
     void *Cx2;            /* non-NULL: the epilogue result is also (C == NULL: only) written in x2
-                             format, ldcx2 bf16 elements per row; split_k must be 1 */
+                             format, ldcx2 bf16 elements per row; split_k must be 1; not with
+                             ATTN_DS_SIGNED, whose result goes to C only (round 5) */
     int64_t ldcx2;
     const float *rowstat; /* unused since ABI v13 (the retired ATTN_DS_RECOMP epilogue); layout kept */
     int64_t m_valid, n_valid;   /* m_valid unused since v13; n_valid: STORE_ROWSTAT's real keys (columns) */

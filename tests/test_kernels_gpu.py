@@ -243,6 +243,10 @@ def test_clamp_a_and_signed_ds_epilogue(prec, tile):
     assert rel_err(C, ref) < (1e-5 if prec == "fp32" else 3e-5)
     with pytest.raises(_lib.U2GNNNativeError):   # clamp_a only with STORE and B not transposed
         K.gemm(dO, V, C, Np, Np, dp, dp, dp, Np, trans_b=True, precision=prec, clamp_a=True)
+    with pytest.raises(_lib.U2GNNNativeError):   # the signed dS epilogue writes C only (no x2 copy)
+        K.gemm(dO, V, C, Np, Np, dp, dp, dp, Np, trans_b=True, epilogue=_lib.EPI_ATTN_DS_SIGNED, aux0=X, p_drop=p,
+               rowvec=dl, ld_aux=Np, precision=prec, tile=tile,
+               Cx2=torch.empty(Np, 2 * Np, device=DEV, dtype=torch.bfloat16), ldcx2=2 * Np)
 
 
 @pytest.mark.parametrize("dp", [384, 640])   # 6 partials, and 10 (> the 8 held in registers)

@@ -40,7 +40,7 @@ struct Dims {
     int64_t N, d, ff, Np, dp, ffp;
     int prec;
     int prec_ab;   // dS, dQ, dK products (U2GNN_LAYER_ATTN_BWD_BF16: plain bf16)
-    int prec_fwd;  // forward products (U2GNN_LAYER_FWD_F32: exact fp32)
+    int prec_fwd;  // forward products (U2GNN_LAYER_FWD_F32: exact fp32; U2GNN_LAYER_FWD_X6: bf16x6)
     bool deep_wgrad;
     int window;   // 0: attention over all N rows; W: within windows of W rows (N % W == 0)
 };
@@ -56,8 +56,9 @@ Dims make_dims(const u2gnn_layer_dims *a) {
     D.prec = a->precision;
     D.prec_ab = (a->precision == U2GNN_PREC_BF16X3 && (a->flags & U2GNN_LAYER_ATTN_BWD_BF16)) ? U2GNN_PREC_BF16
                                                                                              : a->precision;
-    D.prec_fwd = (a->precision == U2GNN_PREC_BF16X3 && (a->flags & U2GNN_LAYER_FWD_F32)) ? U2GNN_PREC_F32
-                                                                                        : a->precision;
+    D.prec_fwd = a->precision;
+    if (a->precision == U2GNN_PREC_BF16X3 && (a->flags & U2GNN_LAYER_FWD_F32)) D.prec_fwd = U2GNN_PREC_F32;
+    if (a->precision == U2GNN_PREC_BF16X3 && (a->flags & U2GNN_LAYER_FWD_X6)) D.prec_fwd = U2GNN_PREC_BF16X6;
     D.deep_wgrad = (a->flags & U2GNN_LAYER_DEEP_WGRAD) != 0;
     D.window = a->window;
     return D;
@@ -487,7 +488,8 @@ int64_t ffn2_split(int64_t dp, bool mfma, int64_t Np, int64_t ffp) {
 int qk_tile(int64_t Np) { return (Np % 256 == 0 && (Np / 256) * (Np / 128) >= 256) ? 256 : 128; }
 
 bool fused_attn(const Dims &D) {
-    return !D.window && !small_attn(D) && D.prec_fwd != U2GNN_PREC_F32 && D.dp <= 384;
+    return !D.window && !small_attn(D) && D.prec_fwd != U2GNN_PREC_F32 && D.prec_fwd != U2GNN_PREC_BF16X6 &&
+           D.dp <= 384;
 }
 
 // the row-local tail of a small-width layer (u2gnn_layer_tail_small_*, small_layer.hip): every precision when the
@@ -819,7 +821,8 @@ int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
 bool dims_ok(const u2gnn_layer_dims *a) {
     return a && a->N >= 1 && a->d >= 1 && a->ff >= 1 && rup(a->d, 64) <= 1024 &&
            (a->precision == U2GNN_PREC_F32 || a->precision == U2GNN_PREC_BF16X3 || a->precision == U2GNN_PREC_BF16) &&
-           ((a->flags & U2GNN_LAYER_FWD_F32) == 0 || a->precision == U2GNN_PREC_BF16X3) &&
+           ((a->flags & (U2GNN_LAYER_FWD_F32 | U2GNN_LAYER_FWD_X6)) == 0 || a->precision == U2GNN_PREC_BF16X3) &&
+           (a->flags & (U2GNN_LAYER_FWD_F32 | U2GNN_LAYER_FWD_X6)) != (U2GNN_LAYER_FWD_F32 | U2GNN_LAYER_FWD_X6) &&
            a->window >= 0 && a->window <= 32 && (a->window == 0 || a->N % a->window == 0);
 }
 

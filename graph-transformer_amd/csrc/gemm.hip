@@ -257,8 +257,16 @@ __device__ __forceinline__ void g2r_bf(__amdgpu_buffer_rsrc_t rs, const int (&vo
     }
 }
 
-template <int R, int BK, int LDK, bool T, bool SPLIT, int NT, bool CLAMP = false>
-__device__ __forceinline__ void r2s_bf(__bf16 *hi, __bf16 *lo, int tid, const float4 (&v_)[R * BK / (4 * NT)]) {
+// NPL bf16 planes of each staged element (1: bf16, 2: hi / lo of bf16x3, 3: hi / mid / lo of bf16x6), plane q
+// at p0 + q * pst
+template <int NPL>
+__device__ __forceinline__ void split_planes(float x0, float x1, unsigned (&o)[3]) {
+    if constexpr (NPL == 3) split3(x0, x1, o[0], o[1], o[2]);
+    else split2<NPL == 2>(x0, x1, o[0], o[1]);
+}
+
+template <int R, int BK, int LDK, bool T, int NPL, int NT, bool CLAMP = false>
+__device__ __forceinline__ void r2s_bf(__bf16 *p0, int pst, int tid, const float4 (&v_)[R * BK / (4 * NT)]) {
     constexpr int NF = R * BK / (4 * NT);
     float4 v[NF];
 #pragma unroll
@@ -271,29 +279,22 @@ __device__ __forceinline__ void r2s_bf(__bf16 *hi, __bf16 *lo, int tid, const fl
     for (int i = 0; i < NF; ++i) asm volatile("" ::"v"(v[i].x), "v"(v[i].y), "v"(v[i].z), "v"(v[i].w));
     return;
 #endif
-    if constexpr (!T) {
 #pragma unroll
-        for (int i = 0; i < NF; ++i) {
+    for (int i = 0; i < NF; ++i) {
+        int o;
+        if constexpr (!T) {
             int r, kq;
             stage_rk<BK, NT>(tid, i, r, kq);
-            uint2 h, l;
-            split2<SPLIT>(v[i].x, v[i].y, h.x, l.x);
-            split2<SPLIT>(v[i].z, v[i].w, h.y, l.y);
-            *reinterpret_cast<uint2 *>(hi + r * LDK + kq * 4) = h;
-            if constexpr (SPLIT) *reinterpret_cast<uint2 *>(lo + r * LDK + kq * 4) = l;
+            o = r * LDK + kq * 4;
+        } else {  // k-major image [BK][R + 32]
+            const int mg = tid % (R / 4), kg = tid / (R / 4);
+            o = (kg * NF + i) * (R + 32) + mg * 4;
         }
-    } else {  // k-major image [BK][R + 32]
-        constexpr int S = R + 32;
-        const int mg = tid % (R / 4), kg = tid / (R / 4);
+        unsigned a[3], b[3];
+        split_planes<NPL>(v[i].x, v[i].y, a);
+        split_planes<NPL>(v[i].z, v[i].w, b);
 #pragma unroll
-        for (int q = 0; q < NF; ++q) {
-            uint2 h, l;
-            split2<SPLIT>(v[q].x, v[q].y, h.x, l.x);
-            split2<SPLIT>(v[q].z, v[q].w, h.y, l.y);
-            const int o = (kg * NF + q) * S + mg * 4;
-            *reinterpret_cast<uint2 *>(hi + o) = h;
-            if constexpr (SPLIT) *reinterpret_cast<uint2 *>(lo + o) = l;
-        }
+        for (int q = 0; q < NPL; ++q) *reinterpret_cast<uint2 *>(p0 + q * pst + o) = make_uint2(a[q], b[q]);
     }
 }
 
@@ -320,13 +321,16 @@ __device__ __forceinline__ bf16x8 ld_frag(const __bf16 *img, int r0, int ks, int
 
 // The main loop and epilogue of one output tile (tile coordinates from the caller: the plain launch's
 // XCD-aware map, or the grouped launch's job walk).
-// bf16 elements of the kernel's LDS image (two stages of hi + lo planes of both operands)
-template <int BM, int BN, int BK, bool TA, bool TB>
+// bf16 planes held per staged operand: two for bf16 / bf16x3 (the bf16 kind leaves its second plane unused, so
+// both kinds share one LDS layout), three for bf16x6
+template <int NPL> constexpr int planes_of() { return NPL < 2 ? 2 : NPL; }
+// bf16 elements of the kernel's LDS image (two stages of the planes of both operands)
+template <int BM, int BN, int BK, bool TA, bool TB, int NPL = 2>
 constexpr int bf16_smem_elems() {
     constexpr int LDK = BK + 8;
     constexpr int AE = TA ? BK * (BM + 32) : BM * LDK;
     constexpr int BE = !TB ? BK * (BN + 32) : BN * LDK;
-    return 2 * 2 * (AE + BE);
+    return 2 * planes_of<NPL>() * (AE + BE);
 }
 
 // dS epilogue through LDS (the C4 dS product: 128 x 128 blocks of 2 x 2 waves, 32-deep K step): each wave's
@@ -384,7 +388,7 @@ __device__ __forceinline__ void ds_lds_store(const GemmP &P, float *C, const f32
     }
 }
 
-template <int BM, int BN, int WM, int WN, int BK, bool TA, bool TB, int EPI, bool SPLIT, bool CLAMP>
+template <int BM, int BN, int WM, int WN, int BK, bool TA, bool TB, int EPI, int NPL, bool CLAMP>
 __device__ __forceinline__ void gemm_bf16_body(const GemmP &P, int tmi, int tni, int zi, __bf16 *smem) {
     constexpr int NT = 64 * WM * WN;
     constexpr int LDK = BK + 8;
@@ -393,7 +397,8 @@ __device__ __forceinline__ void gemm_bf16_body(const GemmP &P, int tmi, int tni,
     constexpr int NFA = BM * BK / (4 * NT), NFB = BN * BK / (4 * NT);
     constexpr int AE = TA ? BK * (BM + 32) : BM * LDK;    // elements per plane, per operand
     constexpr int BE = !TB ? BK * (BN + 32) : BN * LDK;
-    constexpr int STAGE = 2 * (AE + BE);  // hi + lo of A and B
+    constexpr int PL = planes_of<NPL>();
+    constexpr int STAGE = PL * (AE + BE);  // the planes of A, then those of B
 
     const int tid = threadIdx.x;
     const int m0 = tmi * BM, n0 = tni * BN;
@@ -424,37 +429,42 @@ __device__ __forceinline__ void gemm_bf16_body(const GemmP &P, int tmi, int tni,
 
     auto stage = [&](int s) { return smem + s * STAGE; };
     auto compute = [&](const __bf16 *Ah) {
-        const __bf16 *Al = Ah + AE, *Bh = Ah + 2 * AE, *Bl = Bh + BE;
+        const __bf16 *Bh = Ah + PL * AE;
 #pragma unroll
         for (int ks = 0; ks < BK / 16; ++ks) {
-            bf16x8 ah[TM], al[TM], bh[TN], bl[TN];
+            bf16x8 a[NPL][TM], b[NPL][TN];
 #pragma unroll
-            for (int i = 0; i < TM; ++i) {
-                ah[i] = ld_frag<BM, LDK, TA>(Ah, wm * WTM + i * 32, ks, lane);
-                if constexpr (SPLIT) al[i] = ld_frag<BM, LDK, TA>(Al, wm * WTM + i * 32, ks, lane);
-            }
+            for (int i = 0; i < TM; ++i)
 #pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                bh[j] = ld_frag<BN, LDK, !TB>(Bh, wn * WTN + j * 32, ks, lane);
-                if constexpr (SPLIT) bl[j] = ld_frag<BN, LDK, !TB>(Bl, wn * WTN + j * 32, ks, lane);
-            }
+                for (int q = 0; q < NPL; ++q) a[q][i] = ld_frag<BM, LDK, TA>(Ah + q * AE, wm * WTM + i * 32, ks, lane);
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int q = 0; q < NPL; ++q) b[q][j] = ld_frag<BN, LDK, !TB>(Bh + q * BE, wn * WTN + j * 32, ks, lane);
 #pragma unroll
             for (int i = 0; i < TM; ++i)
 #pragma unroll
                 for (int j = 0; j < TN; ++j) {
                     // B fragment first: the accumulator holds the tile transposed, so each lane
-                    // owns 4 consecutive output columns of one row (16-byte epilogue accesses)
-                    if constexpr (SPLIT) {
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bh[j], al[i], acc[i][j], 0, 0, 0);
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bl[j], ah[i], acc[i][j], 0, 0, 0);
+                    // owns 4 consecutive output columns of one row (16-byte epilogue accesses).
+                    // Smallest terms first: bf16x6 mid.mid, hi.lo, lo.hi, hi.mid, mid.hi; bf16x3 hi.lo, lo.hi;
+                    // then hi.hi
+                    if constexpr (NPL == 3) {
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[1][j], a[1][i], acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[0][j], a[2][i], acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[2][j], a[0][i], acc[i][j], 0, 0, 0);
                     }
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bh[j], ah[i], acc[i][j], 0, 0, 0);
+                    if constexpr (NPL >= 2) {
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[0][j], a[1][i], acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[1][j], a[0][i], acc[i][j], 0, 0, 0);
+                    }
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[0][j], a[0][i], acc[i][j], 0, 0, 0);
                 }
         }
     };
 
     constexpr bool DSL = EPI == U2GNN_EPI_ATTN_DS_SIGNED && BM == 128 && BN == 128 && WM == 2 && WN == 2 && BK == 32;
-    static_assert(!DSL || 4 * 64 * DSL_PITCH * 4 <= 2 * bf16_smem_elems<BM, BN, BK, TA, TB>(), "dS LDS epilogue image");
+    static_assert(!DSL || 4 * 64 * DSL_PITCH * 4 <= 2 * bf16_smem_elems<BM, BN, BK, TA, TB, NPL>(), "dS LDS epilogue image");
     DsPre dsl;
     if constexpr (DSL) ds_lds_fetch(P, m0 + wm * WTM, n0 + wn * WTN, lane, 0, dsl);
     PreDS<TN> pre;
@@ -477,22 +487,22 @@ __device__ __forceinline__ void gemm_bf16_body(const GemmP &P, int tmi, int tni,
         g2r_bf<NFB>(rsB, voB, (0) * kstepB, rb0);
         g2r_bf<NFA>(rsA, voA, (min(1, nk - 1)) * kstepA, ra1);
         g2r_bf<NFB>(rsB, voB, (min(1, nk - 1)) * kstepB, rb1);
-        r2s_bf<BM, BK, LDK, TA, SPLIT, NT, CLAMP>(stage(0), stage(0) + AE, tid, ra0);
-        r2s_bf<BN, BK, LDK, !TB, SPLIT, NT>(stage(0) + 2 * AE, stage(0) + 2 * AE + BE, tid, rb0);
+        r2s_bf<BM, BK, LDK, TA, NPL, NT, CLAMP>(stage(0), AE, tid, ra0);
+        r2s_bf<BN, BK, LDK, !TB, NPL, NT>(stage(0) + PL * AE, BE, tid, rb0);
         __syncthreads();
         for (int t = 0; t < nk; t += 2) {
             if constexpr (kStageA) g2r_bf<NFA>(rsA, voA, (min(t + 2, nk - 1)) * kstepA, ra0);
             if constexpr (kStageB) g2r_bf<NFB>(rsB, voB, (min(t + 2, nk - 1)) * kstepB, rb0);
             compute(stage(0));
-            if constexpr (kStageA) r2s_bf<BM, BK, LDK, TA, SPLIT, NT, CLAMP>(stage(1), stage(1) + AE, tid, ra1);
-            if constexpr (kStageB) r2s_bf<BN, BK, LDK, !TB, SPLIT, NT>(stage(1) + 2 * AE, stage(1) + 2 * AE + BE, tid, rb1);
+            if constexpr (kStageA) r2s_bf<BM, BK, LDK, TA, NPL, NT, CLAMP>(stage(1), AE, tid, ra1);
+            if constexpr (kStageB) r2s_bf<BN, BK, LDK, !TB, NPL, NT>(stage(1) + PL * AE, BE, tid, rb1);
             U2GNN_LOOP_SYNC();
             if (t + 1 < nk) {
                 if constexpr (kStageA) g2r_bf<NFA>(rsA, voA, (min(t + 3, nk - 1)) * kstepA, ra1);
                 if constexpr (kStageB) g2r_bf<NFB>(rsB, voB, (min(t + 3, nk - 1)) * kstepB, rb1);
                 compute(stage(1));
-                if constexpr (kStageA) r2s_bf<BM, BK, LDK, TA, SPLIT, NT, CLAMP>(stage(0), stage(0) + AE, tid, ra0);
-                if constexpr (kStageB) r2s_bf<BN, BK, LDK, !TB, SPLIT, NT>(stage(0) + 2 * AE, stage(0) + 2 * AE + BE, tid, rb0);
+                if constexpr (kStageA) r2s_bf<BM, BK, LDK, TA, NPL, NT, CLAMP>(stage(0), AE, tid, ra0);
+                if constexpr (kStageB) r2s_bf<BN, BK, LDK, !TB, NPL, NT>(stage(0) + PL * AE, BE, tid, rb0);
                 U2GNN_LOOP_SYNC();
             }
         }
@@ -514,7 +524,20 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_bf16_kernel(GemmP P) {
     __shared__ __attribute__((aligned(16))) __bf16 smem[bf16_smem_elems<BM, BN, BK, TA, TB>()];
     int tmi, tni, zi;
     tile_coords(P.gm, P.gn, tmi, tni, zi);
-    gemm_bf16_body<BM, BN, WM, WN, BK, TA, TB, EPI, SPLIT, CLAMP>(P, tmi, tni, zi, smem);
+    gemm_bf16_body<BM, BN, WM, WN, BK, TA, TB, EPI, SPLIT ? 2 : 1, CLAMP>(P, tmi, tni, zi, smem);
+}
+
+// U2GNN_PREC_BF16X6: the same body over three planes per operand (16-deep K step, so that the 256x128
+// tile's two stages of six planes fit: 108 KB)
+template <int BM, int BN, int WM, int WN, bool TA, bool TB, int EPI, bool CLAMP>
+__global__ void __launch_bounds__(64 * WM * WN) gemm_bf16x6_kernel(GemmP P) {
+    if constexpr (EPI == U2GNN_EPI_BIAS_DROP_RESID || EPI == U2GNN_EPI_BIAS_RELU_DROP ||
+                  EPI == U2GNN_EPI_BIAS_DROP_RESID_LN)
+        P.seed = u2gnn_seed(P.seed, P.epoch);   // graph replay: device-resident seed epoch
+    __shared__ __attribute__((aligned(16))) __bf16 smem[bf16_smem_elems<BM, BN, 16, TA, TB, 3>()];
+    int tmi, tni, zi;
+    tile_coords(P.gm, P.gn, tmi, tni, zi);
+    gemm_bf16_body<BM, BN, WM, WN, 16, TA, TB, EPI, 3, CLAMP>(P, tmi, tni, zi, smem);
 }
 
 // Grouped launch (u2gnn_gemm_group): several STORE products of one tile shape, each A^T B (the weight
@@ -543,11 +566,11 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_bf16_group_kernel(GemmGroup
     tile_of(P.gm, P.gn, w - G.start[j], tmi, tni, zi);
     const int lay = G.layout[j];
     if (lay == GG_NN)
-        gemm_bf16_body<BM, BN, WM, WN, BK, false, false, U2GNN_EPI_STORE, SPLIT, false>(P, tmi, tni, zi, smem);
+        gemm_bf16_body<BM, BN, WM, WN, BK, false, false, U2GNN_EPI_STORE, SPLIT ? 2 : 1, false>(P, tmi, tni, zi, smem);
     else if (lay == GG_TA_CLAMP)
-        gemm_bf16_body<BM, BN, WM, WN, BK, true, false, U2GNN_EPI_STORE, SPLIT, true>(P, tmi, tni, zi, smem);
+        gemm_bf16_body<BM, BN, WM, WN, BK, true, false, U2GNN_EPI_STORE, SPLIT ? 2 : 1, true>(P, tmi, tni, zi, smem);
     else
-        gemm_bf16_body<BM, BN, WM, WN, BK, true, false, U2GNN_EPI_STORE, SPLIT, false>(P, tmi, tni, zi, smem);
+        gemm_bf16_body<BM, BN, WM, WN, BK, true, false, U2GNN_EPI_STORE, SPLIT ? 2 : 1, false>(P, tmi, tni, zi, smem);
 }
 
 // bf16 K-step variants: 0 = BK 32 (2 blocks/CU at 128x128), 1 = BK 16 (40 KB LDS, 140-152
@@ -560,12 +583,22 @@ template <int KIND, int BM, int BN, int VAR, bool TA, bool TB, int EPI, bool CLA
 void launch_kernel(const GemmP &P, dim3 grid, hipStream_t st) {
     if constexpr (KIND == U2GNN_PREC_F32) {
         hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, TA, TB, EPI, CLAMP>), grid, dim3(256), 0, st, P);
+    } else if constexpr (KIND == U2GNN_PREC_BF16X6) {
+        constexpr int WM = BM == 256 ? 4 : 2, WN = 2;
+        hipLaunchKernelGGL((gemm_bf16x6_kernel<BM, BN, WM, WN, TA, TB, EPI, CLAMP>), grid, dim3(64 * WM * WN), 0, st, P);
     } else {
         constexpr int WM = BM == 256 ? 4 : 2, WN = 2;   // 256x128 tiles run 8 waves (4x2)
         hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, WM, WN, CFG_BK<VAR>, TA, TB, EPI,
                                              KIND == U2GNN_PREC_BF16X3, CLAMP>),
                            grid, dim3(64 * WM * WN), 0, st, P);
     }
+}
+
+// the epilogues the bf16x6 kernels are built for (the forward products; u2gnn_gemm refuses the others)
+constexpr bool x6_epi(int e) {
+    return e == U2GNN_EPI_STORE || e == U2GNN_EPI_BIAS || e == U2GNN_EPI_BIAS_DROP_RESID ||
+           e == U2GNN_EPI_BIAS_RELU_DROP || e == U2GNN_EPI_ACCUM || e == U2GNN_EPI_STORE_ROWSTAT ||
+           e == U2GNN_EPI_BIAS_DROP_RESID_LN;
 }
 
 template <int KIND, int BM, int BN, int VAR, bool TA, bool TB>
@@ -580,10 +613,11 @@ int launch_epi(const GemmP &P, int epi, int split, bool clamp_a, hipStream_t st)
             return u2gnn_launch_status();
         }
     }
+    if (KIND == U2GNN_PREC_BF16X6 && !x6_epi(epi)) return U2GNN_E_ARG;
     switch (epi) {
-#define U2GNN_CASE(E)                                          \
-    case E:                                                    \
-        launch_kernel<KIND, BM, BN, VAR, TA, TB, E>(P, grid, st);   \
+#define U2GNN_CASE(E)                                                                    \
+    case E:                                                                              \
+        if constexpr (KIND != U2GNN_PREC_BF16X6 || x6_epi(E)) launch_kernel<KIND, BM, BN, VAR, TA, TB, E>(P, grid, st); \
         break;
         U2GNN_CASE(U2GNN_EPI_STORE)
         U2GNN_CASE(U2GNN_EPI_BIAS)
@@ -601,7 +635,8 @@ int launch_epi(const GemmP &P, int epi, int split, bool clamp_a, hipStream_t st)
                 return U2GNN_E_ARG;
             break;
         case U2GNN_EPI_ATTN_DS_SIGNED:   // delta as STORE_ROWDOT partials: its own instantiation
-            if (P.rowvec_parts > 1)
+            if constexpr (KIND == U2GNN_PREC_BF16X6) return U2GNN_E_ARG;
+            else if (P.rowvec_parts > 1)
                 launch_kernel<KIND, BM, BN, VAR, TA, TB, EPI_DS_SIGNED_PARTS>(P, grid, st);
             else
                 launch_kernel<KIND, BM, BN, VAR, TA, TB, U2GNN_EPI_ATTN_DS_SIGNED>(P, grid, st);
@@ -622,7 +657,8 @@ template <int KIND, int BM, int BN, int VAR = 0>
 int launch_layout(const GemmP &P, bool ta, bool tb, int epi, int split, bool clamp_a, hipStream_t st) {
     if (!ta && tb) return launch_epi<KIND, BM, BN, VAR, false, true>(P, epi, split, clamp_a, st);
     if (!ta && !tb) return launch_epi<KIND, BM, BN, VAR, false, false>(P, epi, split, clamp_a, st);
-    if (ta && !tb) return launch_epi<KIND, BM, BN, VAR, true, false>(P, epi, split, clamp_a, st);
+    if constexpr (KIND != U2GNN_PREC_BF16X6)   // (bf16x6: the forward products, A never transposed)
+        if (ta && !tb) return launch_epi<KIND, BM, BN, VAR, true, false>(P, epi, split, clamp_a, st);
     return U2GNN_E_ARG;  // A^T B^T is never needed by the encoder
 }
 
@@ -660,11 +696,13 @@ int gemm_plan(const u2gnn_gemm_args *a, GemmPlan &G) {
     if (a->M <= 0 || a->N <= 0 || a->K <= 0) return U2GNN_E_ARG;
     if (a->epilogue < 0 || a->epilogue > U2GNN_EPI_STORE_ROWSTAT) return U2GNN_E_ARG;
     const int prec = a->precision;
-    if (prec != U2GNN_PREC_F32 && prec != U2GNN_PREC_BF16X3 && prec != U2GNN_PREC_BF16) return U2GNN_E_ARG;
+    if (prec != U2GNN_PREC_F32 && prec != U2GNN_PREC_BF16X3 && prec != U2GNN_PREC_BF16 && prec != U2GNN_PREC_BF16X6)
+        return U2GNN_E_ARG;
+    if (prec == U2GNN_PREC_BF16X6 && (a->trans_a || !x6_epi(a->epilogue))) return U2GNN_E_ARG;
     const int split = a->split_k < 1 ? 1 : a->split_k;
     if (split > 1 && (a->epilogue != U2GNN_EPI_STORE || a->Cx2 || !a->C)) return U2GNN_E_ARG;
     if (!al16(a->A) || !al16(a->B) || (a->lda & 3) || (a->ldb & 3)) return U2GNN_E_ALIGN;
-    const int bk = (prec == U2GNN_PREC_F32 || a->tile == 129) ? 16 : 32;   // K step of the kernel
+    const int bk = (prec == U2GNN_PREC_F32 || prec == U2GNN_PREC_BF16X6 || a->tile == 129) ? 16 : 32;   // K step
     if (a->K % bk) return U2GNN_E_SHAPE;
     if (prec != U2GNN_PREC_F32) {   // bf16 staging addresses operands by 32-bit buffer offsets
         const int64_t span = ((int64_t)a->K + 256) * (a->lda > a->ldb ? a->lda : a->ldb) * 4;
@@ -784,6 +822,8 @@ int gemm_plan(const u2gnn_gemm_args *a, GemmPlan &G) {
 }
 
 int gemm_launch(const u2gnn_gemm_args *a, GemmPlan &G, hipStream_t st) {
+    if (G.prec == U2GNN_PREC_BF16X6)
+        return launch_tile<U2GNN_PREC_BF16X6>(G.P, G.tile, G.ta, G.tb, G.epi, G.split, G.clamp, st);
     if (G.prec == U2GNN_PREC_BF16X3)
         return launch_tile<U2GNN_PREC_BF16X3>(G.P, G.tile, G.ta, G.tb, G.epi, G.split, G.clamp, st);
     if (G.prec == U2GNN_PREC_BF16)
@@ -824,7 +864,8 @@ extern "C" int u2gnn_gemm_group(const u2gnn_gemm_args *args, int32_t n, void *st
     // one launch when every job runs the same grouped kernel
     bool same = n > 1;
     for (int32_t i = 0; i < n && same; ++i)
-        same = G[i].prec == G[0].prec && G[i].prec != U2GNN_PREC_F32 && G[i].tile == G[0].tile &&
+        same = G[i].prec == G[0].prec && G[i].prec != U2GNN_PREC_F32 && G[i].prec != U2GNN_PREC_BF16X6 &&
+               G[i].tile == G[0].tile &&
                (G[i].tile == 64 || G[i].tile == 129 || G[i].tile == 256) && !G[i].tb && G[i].epi == U2GNN_EPI_STORE &&
                (G[i].ta || !G[i].clamp);
     if (!same) {

@@ -113,6 +113,17 @@ __device__ __forceinline__ void split2(float x0, float x1, unsigned &h, unsigned
     }
 }
 
+// (x0, x1) -> packed bf16 pairs hi, mid, lo with x = hi + mid + lo: hi = bf16(x), mid = bf16(x - hi),
+// lo = bf16(x - hi - mid); both residuals are exact in fp32, so the three planes carry every bit of x
+// (U2GNN_PREC_BF16X6).  3 cvt_pk + 4 bit ops + 4 subtractions per pair.
+__device__ __forceinline__ void split3(float x0, float x1, unsigned &h, unsigned &m, unsigned &l) {
+    asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(h) : "v"(x0), "v"(x1));
+    const float r0 = x0 - __uint_as_float(h << 16), r1 = x1 - __uint_as_float(h & 0xffff0000u);
+    asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(m) : "v"(r0), "v"(r1));
+    const float s0 = r0 - __uint_as_float(m << 16), s1 = r1 - __uint_as_float(m & 0xffff0000u);
+    asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(l) : "v"(s0), "v"(s1));
+}
+
 // x2 store of four consecutive columns (col % 4 == 0): hi at 16*(col/8) + col%8, lo 8 further
 __device__ __forceinline__ void store_x2_4(__bf16 *Cx2, int64_t ldcx2, int row, int col, float4 o) {
     unsigned h0, h1, l0, l1;

@@ -11,7 +11,9 @@ Extra keywords (not in the reference): ``precision`` = "fp32" (exact fp32 matrix
 the parity path), "bf16x3" (split-bf16, ~2^-16 per product), "mixed" (bf16x3 with the
 attention-backward products dS, dQ, dK on plain bf16; an experiment, see
 u2gnn_hip.engine.MIXED_BF16_ROLES), "fwd32" (exact fp32 forward products, bf16x3 backward: the
-forward's ReLU decisions carry fp32 rounding only) or "bf16" (experiments only); ``attention`` = "nodes" (the fork's semantics: the encoder's sequence axis is
+forward's ReLU decisions carry fp32 rounding only), "fwd6" (the forward products on the
+three-plane bf16x6 split -- fp32-accurate products on bf16 matrix cores -- bf16x3 backward) or "bf16" (experiments
+only); ``attention`` = "nodes" (the fork's semantics: the encoder's sequence axis is
 the node axis, pytorch_U2GNN_Sup.py:35) or "neighbors" (the paper / TF semantics: each node
 attends over its own k+1 sampled neighbours, U2GNN_tf/model_U2GNN_Sup_multi.py:14-45).
 """

@@ -30,8 +30,8 @@ ERRORS = {-1: "bad argument", -2: "misaligned pointer / leading dimension", -3: 
 
 EPI_STORE, EPI_BIAS, EPI_BIAS_DROP_RESID, EPI_BIAS_RELU_DROP, EPI_RELU_DROP_BWD, EPI_ACCUM, EPI_ATTN_DS, \
     EPI_ATTN_DS_SIGNED, EPI_ATTN_DS_RECOMP, EPI_BIAS_DROP_RESID_LN, EPI_STORE_ROWDOT, EPI_STORE_ROWSTAT = range(12)
-ABI_VERSION = 16   # include/u2gnn_hip.h U2GNN_ABI_VERSION
-PREC_F32, PREC_BF16X3, PREC_BF16 = 0, 1, 2
+ABI_VERSION = 17   # include/u2gnn_hip.h U2GNN_ABI_VERSION
+PREC_F32, PREC_BF16X3, PREC_BF16, PREC_BF16X6 = 0, 1, 2, 3
 
 
 class GemmArgs(ctypes.Structure):
@@ -120,6 +120,7 @@ class SmallTailArgs(ctypes.Structure):   # u2gnn_small_tail_args (ABI v15)
 LAYER_DEEP_WGRAD = 1
 LAYER_ATTN_BWD_BF16 = 2   # precision "mixed": dS, dQ, dK on plain bf16 (ABI v5)
 LAYER_FWD_F32 = 4         # precision "fwd32": forward products exact fp32, backward bf16x3 (ABI v14)
+LAYER_FWD_X6 = 8          # precision "fwd6": forward products bf16x6 (three-plane split), backward bf16x3 (ABI v17)
 ROLE_QK, ROLE_PV, ROLE_DS, ROLE_DV, ROLE_DQ, ROLE_DK = range(1, 7)   # u2gnn_probe_arm roles
 
 I64, F32, VP, I32 = c_int64, c_float, c_void_p, c_int32

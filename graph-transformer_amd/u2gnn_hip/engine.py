@@ -252,7 +252,9 @@ MIXED_BF16_ROLES = ("ds", "dq", "dk")
 # (tools/prec_train_probe.py measures train-mode parity per policy).
 ROLE_PREC: Dict[str, str] = {}
 # precision "fwd32": the forward products exact fp32 (so the forward's ReLU decisions carry fp32 rounding
-# only), the backward bf16x3 (u2gnn_hip.h U2GNN_LAYER_FWD_F32)
+# only), the backward bf16x3 (u2gnn_hip.h U2GNN_LAYER_FWD_F32); precision "fwd6": the
+# forward products on the three-plane bf16x6 split (fp32-accurate products at 6/16 of the bf16 MFMA rate instead
+# of 1/16), the backward bf16x3 (U2GNN_LAYER_FWD_X6)
 FWD_ROLES = ("in_proj", "qk", "pv", "out_proj", "ffn1", "ffn2")
 
 
@@ -264,6 +266,8 @@ def _rp(role: str, prec: str) -> str:
         return "bf16" if role in MIXED_BF16_ROLES else "bf16x3"
     if prec == "fwd32":
         return "fp32" if role in FWD_ROLES else "bf16x3"
+    if prec == "fwd6":
+        return "bf16x6" if role in FWD_ROLES else "bf16x3"
     return "bf16" if (prec == "bf16x3" and role in ROLE_BF16) else prec
 
 
@@ -373,9 +377,9 @@ def mid_tail(d: int, dp: int, Np: int) -> bool:
 
 
 def fused_attn(dp: int, prec_qk: str, prec_pv: str) -> bool:
-    """Node-axis attention forward through the fused softmax.P.V kernel: matrix-core precisions,
-    dp <= 384 (encoder_layer.cpp fused_attn)."""
-    return prec_qk != "fp32" and prec_pv != "fp32" and dp <= 384
+    """Node-axis attention forward through the fused softmax.P.V kernel: the bf16 / bf16x3 matrix-core
+    precisions, dp <= 384 (encoder_layer.cpp fused_attn)."""
+    return prec_qk not in ("fp32", "bf16x6") and prec_pv not in ("fp32", "bf16x6") and dp <= 384
 
 
 def _attn_split(Q, Kt, V, N, Np, dp, pd, seeds, prec, att, dev):

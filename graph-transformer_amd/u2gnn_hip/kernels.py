@@ -13,7 +13,7 @@ import torch
 from . import _lib
 from ._lib import check, hip_lib
 
-PREC = {"fp32": _lib.PREC_F32, "bf16x3": _lib.PREC_BF16X3, "bf16": _lib.PREC_BF16}
+PREC = {"fp32": _lib.PREC_F32, "bf16x3": _lib.PREC_BF16X3, "bf16": _lib.PREC_BF16, "bf16x6": _lib.PREC_BF16X6}
 
 
 def _p(t):
@@ -63,6 +63,8 @@ def gemm_symbol(precision, M, N, split_k, tile, trans_a, trans_b, epilogue, clam
         return f"gemm_f32_kernel<{tile}, {tile}, {b(trans_a)}, {b(trans_b)}, {int(epilogue)}, {b(clamp_a)}>"
     # "256" = 256x128 block (4x2 waves); "129" = 128x128 block with a 16-deep K step
     bm, bn, wm, bk = {256: (256, 128, 4, 32), 129: (128, 128, 2, 16)}.get(tile, (tile, tile, 2, 32))
+    if precision == "bf16x6":   # three-plane kernel, 16-deep K step on every tile
+        return f"gemm_bf16x6_kernel<{bm}, {bn}, {wm}, 2, {b(trans_a)}, {b(trans_b)}, {int(epilogue)}, {b(clamp_a)}>"
     return (f"gemm_bf16_kernel<{bm}, {bn}, {wm}, 2, {bk}, {b(trans_a)}, {b(trans_b)}, {int(epilogue)}, "
             f"{b(precision == 'bf16x3')}, {b(clamp_a)}>")   # the C++ template instance as rocprofv3 names it
 

@@ -44,6 +44,8 @@ def _dims(N: int, d: int, ff: int, prec: str, deep_wgrad: bool, window: int = 0)
         prec, flags = "bf16x3", flags | _lib.LAYER_ATTN_BWD_BF16
     elif prec == "fwd32":  # exact fp32 forward products, bf16x3 backward (engine.FWD_ROLES)
         prec, flags = "bf16x3", flags | _lib.LAYER_FWD_F32
+    elif prec == "fwd6":   # bf16x6 forward products, bf16x3 backward (engine.FWD_ROLES)
+        prec, flags = "bf16x3", flags | _lib.LAYER_FWD_X6
     return LayerDims(int(N), int(d), int(ff), PREC[prec], flags, int(window), 0)
 
 

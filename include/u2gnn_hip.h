@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define U2GNN_ABI_VERSION 16
+#define U2GNN_ABI_VERSION 17
 
 #define U2GNN_OK 0
 #define U2GNN_E_ARG (-1)    /* bad size / null pointer */
@@ -80,6 +80,10 @@ extern "C" {
 #define U2GNN_PREC_F32 0    /* v_mfma_f32_32x32x2_f32: exact fp32 fma chains            */
 #define U2GNN_PREC_BF16X3 1 /* split-bf16 (hi*hi+hi*lo+lo*hi) on bf16 MFMA, fp32 accum  */
 #define U2GNN_PREC_BF16 2   /* plain bf16 operands on bf16 MFMA, fp32 accum             */
+#define U2GNN_PREC_BF16X6 3 /* ABI v17: three-way split x = hi + mid + lo (bf16 each, exact for fp32 x);
+                               hh + hm + mh + hl + lh + mm on bf16 MFMA, fp32 accum (~2^-26 per product,
+                               the fp32 products' accuracy at 6/16 of the bf16 rate).  16-deep K step on
+                               every tile; A not transposed (the forward products' layouts) */
 
 typedef struct u2gnn_gemm_args {
     const float *A;       /* trans_a=0: A[m*lda+k]   trans_a=1: A[k*lda+m] */
@@ -536,6 +540,9 @@ int u2gnn_window_attn_bwd(const float *QKV, int64_t ldq, int32_t W, int32_t dp, 
  * Q K^T, P V, out-projection, FFN1, FFN2) runs exact fp32 (the three-pass attention forward); the
  * backward stays bf16x3.  The forward's ReLU decisions then carry fp32 rounding only */
 #define U2GNN_LAYER_FWD_F32 4
+/* precision "fwd6" (ABI v17): with precision == U2GNN_PREC_BF16X3, every FORWARD product runs on the three-plane
+ * split U2GNN_PREC_BF16X6 (fp32-accurate products on bf16 MFMA); the backward stays bf16x3.  Excludes FWD_F32 */
+#define U2GNN_LAYER_FWD_X6 8
 typedef struct u2gnn_layer_dims {
     int64_t N, d, ff;      /* real rows (nodes; window mode: nodes * window tokens), model width, FFN width */
     int32_t precision;     /* U2GNN_PREC_* */

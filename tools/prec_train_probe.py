@@ -26,6 +26,9 @@ POLICIES = {   # name -> (layer precision, role overrides)
     "fwd_attn": ("bf16x3", {r: "fp32" for r in ("qk", "pv")}),
     "fwd_all": ("bf16x3", {r: "fp32" for r in FWD}),
     "fp32": ("fp32", {}),
+    "x6_proj": ("bf16x3", {r: "bf16x6" for r in ("in_proj", "out_proj", "ffn1", "ffn2")}),
+    "x6_all": ("bf16x3", {r: "bf16x6" for r in FWD}),
+    "fwd6": ("fwd6", {}),
 }
 
 

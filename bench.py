@@ -34,7 +34,10 @@ METRIC = "graphs/sec (fwd+bwd) U2GNN-Sup COLLAB k=16 T=4 at 1/2/4/8 MI355X"
 PEAK = {"fp32": 157.3,     # TFLOP/s dense f32-input MFMA peak (MI355X_MICROARCH.md)
         "bf16x3": 2500.0 / 3,  # 2.5 PF dense bf16 MFMA / 3 MFMAs per fp32-accurate product
         "bf16": 2500.0,
-        "bf16x6": 2500.0 / 6}   # 6 MFMAs per fp32-accurate product
+        "bf16x6": 2500.0 / 6,   # 6 MFMAs per fp32-accurate product
+        # policy-level rate of a whole fwd6 step: its forward products (1/3 of the step's FLOPs) at 6 MFMAs each, the
+        # backward (2/3) at 3: 1 / (1/(3 * 2500/6) + 2/(3 * 2500/3))
+        "fwd6": 1.0 / (1.0 / (3 * 2500.0 / 6) + 2.0 / (3 * 2500.0 / 3))}
 DTYPE = {"fp32": "fp32", "bf16x3": "bf16x3", "bf16": "bf16",
          "mixed": "bf16x3 (dS/dQ/dK: bf16)", "fwd32": "fp32 forward, bf16x3 backward",
          "fwd6": "bf16x6 forward, bf16x3 backward"}
@@ -111,6 +114,31 @@ def pmc_traffic(symbol):
     return None, f"no PMC pass of build {bid} covers this kernel"
 
 
+def rocprof_stats(symbol, largest_grid=False):
+    """(average launch us, calls, source) of `symbol` from a committed rocprofv3 kernel-trace summary
+    (profiles/<round>/*_kstats.json, written by tools/kstats.py) OF THIS BUILD, or (None, None, note).
+    largest_grid: the kernel's launches at its largest grid size only."""
+    import glob
+    from u2gnn_hip._lib import source_build_id
+    bid = source_build_id()
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*", "*kstats.json")), reverse=True):
+        try:
+            table = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if table.get("build_id") != bid:
+            continue
+        if largest_grid:
+            rows = [r for r in table.get("by_grid", []) if r["kernel"] == symbol]
+            if rows:
+                r = max(rows, key=lambda r: r["grid"])
+                return r["avg_us"], r["calls"], os.path.relpath(path, REPO)
+        elif symbol in table.get("kernels", {}):
+            k = table["kernels"][symbol]
+            return k["avg_us"], k["calls"], os.path.relpath(path, REPO)
+    return None, None, f"no kernel-trace summary of build {bid} under profiles/"
+
+
 def host_cpu():
     """(model name, logical CPUs) of the host, from /proc/cpuinfo (lscpu's source)."""
     model = "unknown"
@@ -154,15 +182,11 @@ def cpu_threads():
 def launch_ranks(args) -> int:
     """--gpus N > 1 without a launcher: run `torch.distributed.run --nproc-per-node N bench.py ...` as a
     CHILD process (this process has not initialised the GPU and never does; no exec) and relay the
-    ranks' JSON lines.  Returns the launcher's exit code."""
-    import socket
+    ranks' JSON lines.  Returns the launcher's exit code.  --standalone: the launcher's own rendezvous on a port
+    it binds itself (no probe-then-close port race; the CLIs' launcher, u2gnn_hip/cli.py, does the same)."""
     import subprocess
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
-           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--standalone", "--local-addr=127.0.0.1",
+           f"--nproc-per-node={args.gpus}", os.path.abspath(__file__)] + sys.argv[1:]
     proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True)
     for line in proc.stdout:
         line = line.strip()
@@ -207,12 +231,78 @@ def gather_roofline(b, d, ff, K, dev, reps=20):
     torch.cuda.synchronize()
     del pool
     us = e0.elapsed_time(e1) * 1e3 / reps
-    nbytes = Rp * dp * 4 + R * 8 + b.N * d * 4
+    # algorithmic bytes: the REAL gathered values written (R rows x d columns; the image's padding columns and rows
+    # are layout, not work), the int64 index and the unique source rows
+    nbytes = R * d * 4 + R * 8 + b.N * d * 4
     ach = nbytes / (us * 1e-6) / 1e9
-    return {"bound": "hbm", "kernel": "gather_rows_multi_kernel (a2, all k+1 slots)", "achieved": round(ach, 1),
-            "peak": 8000.0, "unit": "GB/s", "frac": round(ach / 8000.0, 4), "avg_launch_us": round(us, 2),
-            "algorithmic_bytes_per_launch": nbytes, "rows": R, "rows_pad": Rp, "d": d, "d_pad": dp,
-            "destinations": f"{reps} launches rotating over {nbuf} destination images ({nbuf * dst_bytes / 2**20:.0f} MiB)"}
+    sym = "gather_rows_multi_kernel<1, true, true>"
+    traffic, tsrc = pmc_traffic(sym + "@maxgrid")
+    rp_us, rp_calls, rsrc = rocprof_stats(sym, largest_grid=True)
+    out = {"bound": "hbm", "kernel": sym + " (a2, all k+1 slots)", "achieved": round(ach, 1),
+           "peak": 8000.0, "unit": "GB/s", "frac": round(ach / 8000.0, 4), "avg_launch_us": round(us, 2),
+           "algorithmic_bytes_per_launch": nbytes, "image_bytes_written": Rp * dp * 4, "rows": R, "rows_pad": Rp,
+           "d": d, "d_pad": dp, "timing": "HIP events around the launches",
+           "destinations": f"{reps} launches rotating over {nbuf} destination images ({nbuf * dst_bytes / 2**20:.0f} MiB)",
+           "traffic": traffic, "traffic_source": tsrc,
+           "traffic_note": "PMC (2 * FETCH_SIZE + WRITE_SIZE) of these launches (the kernel's largest grid); the "
+                           "writes are 16-B stores (exact), the reads 4-B-per-lane loads (the x2 FETCH_SIZE "
+                           "correction is calibrated for 16-B reads)",
+           "rocprof_avg_launch_us": round(rp_us, 2) if rp_us else None, "rocprof_source": rsrc}
+    if rp_us:
+        out["rocprof_frac"] = round(nbytes / (rp_us * 1e-6) / 1e9 / 8000.0, 4)
+    return out
+
+
+PROBE_STEPS = 10
+ROLES = {}
+
+
+def probe_precision(precision, role):
+    """The matrix-core precision the probed product runs at under a precision policy."""
+    fwd = role in ("qk", "pv")
+    if precision == "mixed":
+        return "bf16" if role in ("ds", "dq", "dk") else "bf16x3"
+    if precision == "fwd32":
+        return "fp32" if fwd else "bf16x3"
+    if precision == "fwd6":
+        return "bf16x6" if fwd else "bf16x3"
+    return precision
+
+
+def attn_kernel_roofline(args, role, ms, n, used, d, per_step, K, LIB):
+    """The roofline entry of one probed attention product: algorithmic FLOPs (2 N^2 d per product, real dims; the
+    grouped dQ + dK launch carries two products) over the summed live event time, against the dense MFMA peak of
+    the precision the product runs at; the kernel's PMC bytes per launch when the committed table is of this
+    build, and its rocprof average when a committed kernel-trace summary is."""
+    from u2gnn_hip.engine import row_pad, rup
+    Np0, dp = row_pad(used[0].N), rup(d, 64)
+    pk = probe_precision(args.precision, role)
+    fused = pk in ("bf16x3", "bf16") and dp <= 384   # encoder_layer.cpp fused_attn
+    prods = 2.0 if role == "dq" else 1.0   # the grouped dQ + dK launch
+    fl = float(sum(per_step * prods * 2.0 * b.N * b.N * d for b in used))
+    if role == "ds":
+        sym = K.gemm_symbol(pk, Np0, Np0, 1, 0, False, True, LIB.EPI_ATTN_DS_SIGNED)
+    elif role == "dv":
+        sym = K.gemm_symbol(pk, Np0, dp, 4, 256, True, False, LIB.EPI_STORE, clamp_a=True)
+    elif role == "dq":
+        sym = "gemm_bf16_group_kernel<256, 128, 4, 2, 32, true>" if pk == "bf16x3" else "grouped dQ + dK"
+    elif role == "qk":
+        sym = K.gemm_symbol(pk, Np0, Np0, 1, 256, False, True, LIB.EPI_STORE_ROWSTAT if fused else LIB.EPI_STORE)
+    else:
+        sym = f"attn_softmax_pv_kernel<{dp}, {'true' if pk == 'bf16x3' else 'false'}>" if fused else \
+            "P.V split-K GEMM (" + pk + ")"
+    ach = fl / (ms * 1e-3) / 1e12
+    peak = PEAK[pk]
+    traffic, traffic_src = pmc_traffic(sym)
+    rp_us, rp_calls, rp_src = rocprof_stats(sym)
+    e = {"bound": "mfma", "achieved": round(ach, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
+         "frac": round(ach / peak, 4), "traffic": traffic, "traffic_source": traffic_src,
+         "kernel": sym, "kernel_precision": pk, "role": "dq+dk (one grouped launch)" if role == "dq" else role,
+         "launches": n, "avg_launch_us": round(1e3 * ms / n, 1), "algorithmic_flop_per_launch": round(fl / n),
+         "rocprof_avg_launch_us": round(rp_us, 1) if rp_us else None, "rocprof_source": rp_src}
+    if rp_us:
+        e["rocprof_frac"] = round(fl / n / (rp_us * 1e-6) / 1e12 / peak, 4)
+    return e
 
 
 def cpu_baseline(hb, sd, args, d, C):
@@ -660,6 +750,28 @@ def run_small(args):
                "sample": f"{reps - 5} timed training steps of 4-graph {name} batches (all {k + 1} neighbour slots, "
                          f"dropout on), median {1e3 * t:.1f} ms/step, oracle/u2gnn_oracle.py on torch CPU"}
     mean_N = float(np.mean([bt[0].N for bt in batches]))
+    ms_step = elapsed / args.steps
+    largest = largest_kernel(args.workload)
+    if sup:
+        # C2 is MFMA-bound by its algorithmic FLOPs (slot 0 only), against the policy's dense rate
+        fl = float(np.mean([model_step_flops(bt[0].N, d, args.ff_hidden_size, T, 1) for bt in batches]))
+        ach = fl / ms_step / 1e12
+        peak = PEAK[args.precision]
+        roof = {"bound": "mfma", "achieved": round(ach, 3), "peak": round(peak, 1), "unit": "TFLOP/s",
+                "frac": round(ach / peak, 5), "traffic": None, "algorithmic_flop_per_step": round(fl),
+                "what": "SURVEY.md §8(d) step FLOPs 3*L*T*(8*N*d^2 + 4*N^2*d + 4*N*d*ff) / ms_per_step",
+                "largest_kernel": largest}
+    else:
+        # C3 is HBM-bound by the bytes of its step: the dense Adam sweep over ss.weight [V, D]
+        # (p, g, m, v read; p, m, v written), the sampled softmax's row gathers / scatters, the encoder's sweep
+        D = d   # num_U2GNN_layers = 1
+        n_enc = sum(v.numel() for kk, v in sd0.items() if kk != "ss.weight")
+        byts = 4.0 * 6 * V * D + 4.0 * 3 * (mean_N + 512) * D + 4.0 * 3 * n_enc * 7 / 3
+        ach = byts / ms_step / 1e9
+        roof = {"bound": "hbm", "achieved": round(ach, 2), "peak": 8000.0, "unit": "GB/s", "frac": round(ach / 8000.0, 5),
+                "traffic": None, "algorithmic_bytes_per_step": round(byts),
+                "what": "SURVEY.md §8(d) bytes per step (4*6*V*D + 4*3*(N+S)*D + 4*3*P_enc*7/3) / ms_per_step",
+                "largest_kernel": largest}
     out = {"metric": METRIC_SMALL[args.workload], "value": round(args.steps * 4 / elapsed, 2), "unit": "graphs/s",
            "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
            "ms_per_step": round(1e3 * elapsed / args.steps, 3), "higher_is_better": True, "scaling": "weak",
@@ -671,8 +783,28 @@ def run_small(args):
                       "global_batch": 4, "mean_nodes_per_batch": round(mean_N, 1), "parallelism": "dp1",
                       "precision": args.precision, "hip_graph": graph},
            "final_loss": round(loss, 5), "host_issue_ms_per_step": round(1e3 * t_issue / args.steps, 3),
-           "roofline": None, "cpu_baseline": cpu}
+           "roofline": roof, "cpu_baseline": cpu}
     return out
+
+
+def largest_kernel(workload):
+    """The largest kernel (device time) of a workload's step from the committed kernel-trace summary of THIS build
+    (profiles/<round>/*_<workload>_kstats.json, tools/wl_trace.sh), or a note."""
+    import glob
+    from u2gnn_hip._lib import source_build_id
+    bid = source_build_id()
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*", f"*{workload}_kstats.json")), reverse=True):
+        try:
+            t = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if t.get("build_id") != bid or not t.get("kernels"):
+            continue
+        name, k = max(t["kernels"].items(), key=lambda kv: kv[1]["total_ms"])
+        return {"kernel": name, "avg_launch_us": round(k["avg_us"], 2), "calls": k["calls"],
+                "share_of_kernel_time": round(k["total_ms"] / t["total_kernel_ms"], 3),
+                "source": os.path.relpath(path, REPO)}
+    return {"note": f"no kernel-trace summary of build {bid} for {workload} under profiles/"}
 
 
 _JSON_OUT = None
@@ -758,8 +890,10 @@ def main():
     runner = None
     from u2gnn_hip import native
     from u2gnn_hip import _lib as LIB
-    role = {"qk": LIB.ROLE_QK, "pv": LIB.ROLE_PV, "ds": LIB.ROLE_DS, "dv": LIB.ROLE_DV, "dq": LIB.ROLE_DQ,
-            "dk": LIB.ROLE_DK}[args.probe]
+    global ROLES
+    ROLES = {"qk": LIB.ROLE_QK, "pv": LIB.ROLE_PV, "ds": LIB.ROLE_DS, "dv": LIB.ROLE_DV, "dq": LIB.ROLE_DQ,
+             "dk": LIB.ROLE_DK}
+    role = ROLES[args.probe]
     # (graph replay: the probe's events would belong to the capture, so no live probe)
     probing = not args.no_roofline and args.attention == "nodes" and native.enabled() and not graph
     per_step = args.num_hidden_layers * args.num_timesteps
@@ -825,33 +959,28 @@ def main():
     roof = None
     if probe_n:
         # the dominant kernel (the attention dS GEMM by default: the largest device time of a C4
-        # step, rocprof profiles/) timed live in the timed region: achieved = its launches'
-        # algorithmic FLOPs (2 N^2 d, real unpadded dims) / their summed event time
+        # step's critical path, rocprof profiles/) timed live in the timed region: achieved = its launches'
+        # algorithmic FLOPs (2 N^2 d per product, real unpadded dims) / their summed event time
         if probe_n != args.steps * per_step:
             raise SystemExit(f"probe recorded {probe_n} launches, expected {args.steps * per_step}")
-        fl = float(sum(per_step * 2.0 * b.N * b.N * d for b in used))
-        from u2gnn_hip.engine import row_pad
-        Np0 = row_pad(used[0].N)
-        epi = LIB.EPI_ATTN_DS_SIGNED if args.probe == "ds" else LIB.EPI_STORE
-        ta, tb = args.probe in ("dv", "dk"), args.probe in ("qk", "ds")
-        nn = Np0 if args.probe in ("qk", "ds") else ((d + 63) // 64 * 64)
-        pk = "bf16" if (args.precision == "mixed" and args.probe in ("ds", "dq", "dk")) else \
-            ("bf16x3" if args.precision in ("mixed", "fwd32") and args.probe not in ("qk", "pv") else
-             ("fp32" if args.precision == "fwd32" else args.precision))
-        split = 1 if args.probe in ("qk", "ds") else (2 if args.probe in ("dq", "dk") else 4)
-        tile = 0 if args.probe == "ds" else 256
-        sym = K.gemm_symbol(pk, Np0, nn, split, tile, ta, tb, epi, clamp_a=args.probe in ("pv", "dv"))
-        ach = fl / (probe_ms * 1e-3) / 1e12
-        peak = PEAK[pk]
-        traffic, traffic_src = pmc_traffic(sym)
-        roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
-                "frac": round(ach / peak, 4), "traffic": traffic, "traffic_source": traffic_src,
-                "kernel": sym, "kernel_precision": pk, "role": args.probe,
-                "timing": "live: HIP events around each launch on its own stream inside the timed region",
-                "dominance": "largest per-product device time on the critical path (DESIGN.md section 8)",
-                "launches": probe_n, "avg_launch_us": round(1e3 * probe_ms / probe_n, 1),
-                "algorithmic_flop_per_launch": round(fl / probe_n),
-                "step_tflops_per_gpu": round(step_flops / (elapsed / args.steps) / 1e12, 2)}
+        roof = attn_kernel_roofline(args, args.probe, probe_ms, probe_n, used, d, per_step, K, LIB)
+        roof.update({"timing": "live: HIP events around each launch on its own stream inside the timed region",
+                     "dominance": "largest per-product device time on the critical path (DESIGN.md section 8)",
+                     "step_tflops_per_gpu": round(step_flops / (elapsed / args.steps) / 1e12, 2),
+                     "step_frac": round(step_flops / (elapsed / args.steps) / 1e12 / PEAK[args.precision], 4)})
+        # the step's other large attention products, each timed live the same way in an untimed pass of
+        # PROBE_STEPS steps of the same schedule after the timed region (one role armed per pass)
+        others = {}
+        for r in [x for x in ("dv", "dq", "qk", "pv") if x != args.probe]:
+            native.probe_arm(ROLES[r], PROBE_STEPS * per_step)
+            for i in range(PROBE_STEPS):
+                step(batches[(args.warmup + i) % nb])
+            torch.cuda.synchronize()
+            ms, n = native.probe_collect()
+            if n == PROBE_STEPS * per_step and ms > 0:
+                others[r] = attn_kernel_roofline(args, r, ms, n, used[:PROBE_STEPS], d, per_step, K, LIB)
+                others[r]["timing"] = f"live HIP events, untimed pass of {PROBE_STEPS} steps after the timed region"
+        roof["other_kernels"] = others
     summ = K.REC.summary()
     if summ:
         fam = sorted(summ.items(), key=lambda kv: -kv[1][2])

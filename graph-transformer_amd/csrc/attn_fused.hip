@@ -543,7 +543,7 @@ int u2gnn_attn_softmax_pv(const float *S, int64_t lds, const float *rowpart, int
     P.kb_per_split = (P.kb_valid + P.nsplit - 1) / P.nsplit;
     P.p = p;
     P.seed = seed;
-    P.epoch = u2gnn_g_epoch;
+    P.epoch = u2gnn_cur_epoch();
     hipStream_t st = u2gnn_stream(stream);
     const bool x3 = precision == U2GNN_PREC_BF16X3;
     switch (dp) {

@@ -1270,7 +1270,7 @@ int u2gnn_attn_softmax_fwd(const float *S, int64_t lds, float *P, float *Pd, int
     // exact zeros appended after the live ones, so P is bit-identical
     const int64_t rv = (n_pad + 1023) / 1024;
 #define U2GNN_SMX(V) hipLaunchKernelGGL(attn_softmax_kernel<V>, dim3((unsigned)rows_pad), dim3(256), 0, st, S, lds, P, Pd, \
-                                        ldp, rows_valid, n_valid, n_pad, p, seed, u2gnn_g_epoch, keep, ld_keep)
+                                        ldp, rows_valid, n_valid, n_pad, p, seed, u2gnn_cur_epoch(), keep, ld_keep)
     if (rv <= 8) {
         switch (rv) {
             case 1: U2GNN_SMX(1); break;
@@ -1286,10 +1286,10 @@ int u2gnn_attn_softmax_fwd(const float *S, int64_t lds, float *P, float *Pd, int
 #undef U2GNN_SMX
     else if (n_pad <= 16384)
         hipLaunchKernelGGL(attn_softmax_kernel<16>, dim3((unsigned)rows_pad), dim3(256), 0, st, S, lds, P, Pd, ldp,
-                           rows_valid, n_valid, n_pad, p, seed, u2gnn_g_epoch, keep, ld_keep);
+                           rows_valid, n_valid, n_pad, p, seed, u2gnn_cur_epoch(), keep, ld_keep);
     else
         hipLaunchKernelGGL(attn_softmax_kernel<32>, dim3((unsigned)rows_pad), dim3(256), 0, st, S, lds, P, Pd, ldp,
-                           rows_valid, n_valid, n_pad, p, seed, u2gnn_g_epoch, keep, ld_keep);
+                           rows_valid, n_valid, n_pad, p, seed, u2gnn_cur_epoch(), keep, ld_keep);
     return u2gnn_launch_status();
 }
 
@@ -1355,15 +1355,15 @@ int layernorm_bwd_launch(const float *dY, int64_t ldy, const float *Z, int64_t l
     do {                                                                                                               \
         if (dt && dt->slabs)                                                                                           \
             hipLaunchKernelGGL((layernorm_bwd_kernel<V, true, true>), gr, dim3(256), 0, st, dY, ldy, Z, ldz, mean,    \
-                               rstd, gamma, dZ, lddz, dZdrop, lddrop, p, seed, u2gnn_g_epoch, rows_valid, rows_pad, d, \
+                               rstd, gamma, dZ, lddz, dZdrop, lddrop, p, seed, u2gnn_cur_epoch(), rows_valid, rows_pad, d, \
                                d_pad, *dt);                                                                            \
         else if (dt)                                                                                                   \
             hipLaunchKernelGGL((layernorm_bwd_kernel<V, true>), gr, dim3(256), 0, st, dY, ldy, Z, ldz, mean, rstd,    \
-                               gamma, dZ, lddz, dZdrop, lddrop, p, seed, u2gnn_g_epoch, rows_valid, rows_pad, d,       \
+                               gamma, dZ, lddz, dZdrop, lddrop, p, seed, u2gnn_cur_epoch(), rows_valid, rows_pad, d,       \
                                d_pad, *dt);                                                                            \
         else                                                                                                           \
             hipLaunchKernelGGL((layernorm_bwd_kernel<V, false>), gr, dim3(256), 0, st, dY, ldy, Z, ldz, mean, rstd,   \
-                               gamma, dZ, lddz, dZdrop, lddrop, p, seed, u2gnn_g_epoch, rows_valid, rows_pad, d,       \
+                               gamma, dZ, lddz, dZdrop, lddrop, p, seed, u2gnn_cur_epoch(), rows_valid, rows_pad, d,       \
                                d_pad, none);                                                                           \
     } while (0)
     const int64_t v4 = (d_pad + 127) / 128;
@@ -1519,7 +1519,7 @@ int u2gnn_slab_bias_drop_resid_ln(const float *src, int32_t n_slab, int64_t slab
     hipStream_t st = u2gnn_stream(stream);
 #define U2GNN_SLAB_LN(CPL)                                                                                       \
     hipLaunchKernelGGL(slab_bias_drop_resid_ln_kernel<CPL>, grid, dim3(256), 0, st, src, n_slab, slab_stride, ld_src, \
-                       bias, resid, ld_res, p, seed, u2gnn_g_epoch, Z, ldz, gamma, beta, Y, ldy, mean, rstd, d,      \
+                       bias, resid, ld_res, p, seed, u2gnn_cur_epoch(), Z, ldz, gamma, beta, Y, ldy, mean, rstd, d,      \
                        rows_valid, rows_pad, eps)
     switch (dp / 64) {
         case 1: U2GNN_SLAB_LN(1); break;
@@ -1634,13 +1634,13 @@ int u2gnn_dropout(const float *X, int64_t ldx, float *Y, int64_t ldy, int64_t ro
     if (!X || !Y || p < 0.f || p >= 1.f) return U2GNN_E_ARG;
     if (rows * cols == 0) return U2GNN_OK;
     hipLaunchKernelGGL(dropout_kernel, dim3(grid_for(rows * cols, 256)), dim3(256), 0, u2gnn_stream(stream), X, ldx, Y,
-                       ldy, rows, cols, p, seed, u2gnn_g_epoch);
+                       ldy, rows, cols, p, seed, u2gnn_cur_epoch());
     return u2gnn_launch_status();
 }
 
 int u2gnn_dropout_mask(uint64_t seed, int64_t rows, int64_t cols, float p, uint8_t *out, void *stream) {
     if (!out) return U2GNN_E_ARG;
-    hipLaunchKernelGGL(dropout_mask_kernel, dim3(grid_for(rows * cols, 256)), dim3(256), 0, u2gnn_stream(stream), seed, u2gnn_g_epoch,
+    hipLaunchKernelGGL(dropout_mask_kernel, dim3(grid_for(rows * cols, 256)), dim3(256), 0, u2gnn_stream(stream), seed, u2gnn_cur_epoch(),
                        rows, cols, p, out);
     return u2gnn_launch_status();
 }

@@ -793,7 +793,7 @@ int gemm_plan(const u2gnn_gemm_args *a, GemmPlan &G) {
     P.scale_cols = (int32_t)a->scale_cols;
     P.p = a->p_drop;
     P.seed = a->seed;
-    P.epoch = u2gnn_g_epoch;
+    P.epoch = u2gnn_cur_epoch();
     P.keep = e == U2GNN_EPI_ATTN_DS ? a->keep : nullptr;
     P.ld_keep = a->ld_keep;
     P.Cx2 = static_cast<__bf16 *>(a->Cx2);

@@ -3,8 +3,24 @@
 // sampled-softmax loss of the unsupervised model.
 #include "u2gnn_common.h"
 
-// process-wide seed epoch (u2gnn_set_seed_epoch), passed to every dropout-drawing launch
-const uint64_t *u2gnn_g_epoch = nullptr;
+#include <atomic>
+
+// seed epoch of each device (u2gnn_set_seed_epoch records it for the calling thread's current device); every
+// dropout-drawing launch passes the entry of the device it is issued on (the current device: the streams the
+// callers pass belong to it), so two devices driven from one process keep separate epochs
+namespace {
+constexpr int kMaxDevices = 64;
+std::atomic<const uint64_t *> g_epoch[kMaxDevices];
+int current_device() {
+    int d = -1;
+    return hipGetDevice(&d) == hipSuccess && d >= 0 && d < kMaxDevices ? d : -1;
+}
+}  // namespace
+
+const uint64_t *u2gnn_cur_epoch() {
+    const int d = current_device();
+    return d < 0 ? nullptr : g_epoch[d].load(std::memory_order_acquire);
+}
 
 namespace {
 
@@ -617,7 +633,7 @@ int u2gnn_concat_dropout(const float *const *src, int32_t L, int64_t ld_src, int
         if (!cs.p[l]) return U2GNN_E_ARG;
     if (N == 0) return U2GNN_OK;
     hipLaunchKernelGGL(concat_dropout_kernel, dim3(grid_for(N * d * L, 256)), dim3(256), 0, u2gnn_stream(stream), cs,
-                       ld_src, N, d, (int)L, p, seed, u2gnn_g_epoch, Y, ldy);
+                       ld_src, N, d, (int)L, p, seed, u2gnn_cur_epoch(), Y, ldy);
     return u2gnn_launch_status();
 }
 
@@ -632,7 +648,7 @@ int u2gnn_split_dropout_bwd(const float *dY, int64_t ldy, int32_t L, int64_t N, 
         if (!cd.p[l]) return U2GNN_E_ARG;
     if (Np == 0) return U2GNN_OK;
     hipLaunchKernelGGL(split_dropout_bwd_kernel, dim3(grid_for(Np * dp * L, 256)), dim3(256), 0, u2gnn_stream(stream),
-                       dY, ldy, N, Np, d, dp, (int)L, p, seed, u2gnn_g_epoch, cd);
+                       dY, ldy, N, Np, d, dp, (int)L, p, seed, u2gnn_cur_epoch(), cd);
     return u2gnn_launch_status();
 }
 
@@ -656,7 +672,7 @@ int u2gnn_pool_fwd(const float *X, int64_t ldx, const int64_t *rowptr, const int
                    float *G, int64_t ldg, int64_t B, int64_t d, float p, uint64_t seed, void *stream) {
     if (!X || !rowptr || !colidx || !vals || !G || B < 1 || d < 1) return U2GNN_E_ARG;
     hipLaunchKernelGGL(pool_fwd_kernel, dim3((unsigned)B, (unsigned)((d + 63) / 64)), dim3(64 * POOL_WAVES), 0,
-                       u2gnn_stream(stream), X, ldx, rowptr, colidx, vals, G, ldg, d, p, seed, u2gnn_g_epoch);
+                       u2gnn_stream(stream), X, ldx, rowptr, colidx, vals, G, ldg, d, p, seed, u2gnn_cur_epoch());
     return u2gnn_launch_status();
 }
 
@@ -664,7 +680,7 @@ int u2gnn_pool_bwd(const float *dGd, int64_t ldg, const int64_t *rowptr, const i
                    float *dX, int64_t ldx, int64_t B, int64_t d, float p, uint64_t seed, void *stream) {
     if (!dGd || !rowptr || !colidx || !vals || !dX || B < 1 || d < 1) return U2GNN_E_ARG;
     hipLaunchKernelGGL(pool_bwd_kernel, dim3((unsigned)B, 8, (unsigned)((d + 63) / 64)), dim3(256), 0,
-                       u2gnn_stream(stream), dGd, ldg, rowptr, colidx, vals, dX, ldx, d, p, seed, u2gnn_g_epoch);
+                       u2gnn_stream(stream), dGd, ldg, rowptr, colidx, vals, dX, ldx, d, p, seed, u2gnn_cur_epoch());
     return u2gnn_launch_status();
 }
 
@@ -677,7 +693,7 @@ int u2gnn_pool_bwd_rows(const float *dGd, int64_t ldg, const int64_t *rowptr, co
     const int64_t zb = (rows_pad - N + 31) / 32;   // padding-row blocks: 8 x 4 waves, one row each
     hipLaunchKernelGGL(pool_bwd_rows_kernel, dim3((unsigned)(B + zb), 8, (unsigned)((d_pad + 63) / 64)), dim3(256), 0,
                        u2gnn_stream(stream), dGd, ldg, rowptr, colidx, vals, dX, ldx, B, d, d_pad, N, rows_pad, p,
-                       seed, u2gnn_g_epoch);
+                       seed, u2gnn_cur_epoch());
     return u2gnn_launch_status();
 }
 
@@ -776,7 +792,9 @@ int u2gnn_step_advance(uint64_t *epoch, int64_t *step, void *stream) {
 }
 
 int u2gnn_set_seed_epoch(const uint64_t *epoch) {
-    u2gnn_g_epoch = epoch;
+    const int d = current_device();
+    if (d < 0) return U2GNN_E_ARG;
+    g_epoch[d].store(epoch, std::memory_order_release);
     return U2GNN_OK;
 }
 

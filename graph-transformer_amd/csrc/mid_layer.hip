@@ -233,7 +233,7 @@ int u2gnn_layer_tail_mid_fwd(const u2gnn_small_tail_args *t, float *ws, int64_t 
     MtP P;
     P.a = a;
     P.slabs = ws;
-    P.epoch = u2gnn_g_epoch;
+    P.epoch = u2gnn_cur_epoch();
     const int nchunk = (int)((a.ffp + MT_HC - 1) / MT_HC);
     const dim3 grid((unsigned)(a.rows_pad / MT_RB), (unsigned)nchunk);
     hipStream_t st = u2gnn_stream(stream);

@@ -202,7 +202,9 @@ template <int DM, bool TAIL>
 __global__ void __launch_bounds__(SA_NT, sa_min_waves<DM>()) sa_fwd_kernel(SaP P, LsP T) {
     constexpr int SA_KT = sa_kt_f<DM>();
     constexpr int PART = SA_KT / SA_SPL, NP = PART / 128;   // keys per wave per tile; key pairs per lane
-    constexpr int CU = DM <= 8 ? 8 : 4;   // keys per lane between rescales (their K rows are live in registers)
+    // keys per lane between rescales (their K rows are live in registers), at most the wave's part of the tile
+    // (2 NP keys per lane): a larger chunk would index ks past the tile for DM >= 8
+    constexpr int CU = (DM <= 8 ? 8 : 4) < 2 * NP ? (DM <= 8 ? 8 : 4) : 2 * NP;
     static_assert(NP >= 1 && PART % 128 == 0, "a wave's part of the key tile: whole 128-key rounds");
     __shared__ __attribute__((aligned(16))) float ks[SA_KT][DM];
     __shared__ __attribute__((aligned(16))) float vs[SA_KT][DM];
@@ -557,7 +559,7 @@ SaP sa_params(int64_t dp, int64_t d, int64_t N, int64_t Np, float p, uint64_t se
     SaP P;
     std::memset(&P, 0, sizeof(P));
     P.dp = (int32_t)dp, P.d = (int32_t)d, P.N = (int32_t)N, P.Np = (int32_t)Np;
-    P.p = p, P.seed = seed, P.epoch = u2gnn_g_epoch, P.ctx = ctx;
+    P.p = p, P.seed = seed, P.epoch = u2gnn_cur_epoch(), P.ctx = ctx;
     return P;
 }
 
@@ -1243,7 +1245,7 @@ LsP ls_params(const u2gnn_small_tail_args *a) {
     std::memset(&P, 0, sizeof(P));
     P.N = (int32_t)a->n_valid, P.Np = (int32_t)a->rows_pad, P.d = (int32_t)a->d, P.dp = (int32_t)a->dp;
     P.ff = (int32_t)a->ff, P.ffp = (int32_t)a->ffp, P.p = a->p, P.eps = a->eps;
-    P.s1 = a->seed_drop1, P.sff = a->seed_dropff, P.s2 = a->seed_drop2, P.epoch = u2gnn_g_epoch;
+    P.s1 = a->seed_drop1, P.sff = a->seed_dropff, P.s2 = a->seed_drop2, P.epoch = u2gnn_cur_epoch();
     P.a = *a;
     return P;
 }

@@ -35,10 +35,11 @@ __device__ __forceinline__ uint32_t u2gnn_row_key(uint64_t seed, uint32_t i) {
 }
 
 // Graph replay (ABI v6): every kernel that draws dropout decisions receives, beside its by-value
-// seed, the library's seed-epoch pointer as it was at launch (u2gnn_set_seed_epoch; NULL = off) and
-// mixes the device-resident epoch into the seed, so a captured HIP graph draws new masks on every
-// replay (u2gnn_step_advance bumps the epoch inside the graph).  Epoch 0 leaves the seed unchanged.
-extern const uint64_t *u2gnn_g_epoch;
+// seed, the launching device's seed-epoch pointer as it was at launch (u2gnn_set_seed_epoch; NULL = off;
+// per device since ABI v17) and mixes the device-resident epoch into the seed, so a captured HIP graph
+// draws new masks on every replay (u2gnn_step_advance bumps the epoch inside the graph).  Epoch 0 leaves
+// the seed unchanged.
+const uint64_t *u2gnn_cur_epoch();   // the current device's epoch pointer (head_ops.hip)
 __device__ __forceinline__ uint64_t u2gnn_seed(uint64_t seed, const uint64_t *epoch) {
     return epoch ? seed ^ (*epoch * 0x9E3779B97F4A7C15ull) : seed;
 }

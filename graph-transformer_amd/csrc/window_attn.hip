@@ -468,12 +468,12 @@ int u2gnn_window_attn_fwd(const float *QKV, int64_t ldq, int32_t W, int32_t dp, 
         const int64_t per_cu = std::min<int64_t>(kWinPfBlocksPerCu, std::max<int64_t>(1, (int64_t)(LDS_LIMIT / lds)));
         const int64_t grid = std::min<int64_t>(n_nodes, per_cu * cu_count());
         hipLaunchKernelGGL(kern, dim3((unsigned)std::max<int64_t>(grid, 1)), dim3(256), lds, u2gnn_stream(stream), QKV,
-                           ldq, W, dp, O, ldo, Psave, p, seed, u2gnn_g_epoch, n_nodes, rows_pad);
+                           ldq, W, dp, O, ldo, Psave, p, seed, u2gnn_cur_epoch(), n_nodes, rows_pad);
         return u2gnn_launch_status();
     }
     const int64_t pad_blocks = (rows_pad - n_nodes * W + W - 1) / W;
     hipLaunchKernelGGL(window_attn_fwd_kernel, dim3((unsigned)(n_nodes + pad_blocks)), dim3(256), lds,
-                       u2gnn_stream(stream), QKV, ldq, W, dp, O, ldo, Psave, p, seed, u2gnn_g_epoch, n_nodes, rows_pad);
+                       u2gnn_stream(stream), QKV, ldq, W, dp, O, ldo, Psave, p, seed, u2gnn_cur_epoch(), n_nodes, rows_pad);
     return u2gnn_launch_status();
 }
 
@@ -499,12 +499,12 @@ int u2gnn_window_attn_bwd(const float *QKV, int64_t ldq, int32_t W, int32_t dp, 
         const int64_t per_cu = std::min<int64_t>(kWinPfBlocksPerCu, std::max<int64_t>(1, (int64_t)(LDS_LIMIT / lds)));
         const int64_t grid = std::min<int64_t>(n_nodes, per_cu * cu_count());
         hipLaunchKernelGGL(kern, dim3((unsigned)std::max<int64_t>(grid, 1)), dim3(256), lds, u2gnn_stream(stream), QKV,
-                           ldq, W, dp, dO, ldo, Psave, p, seed, u2gnn_g_epoch, q_scale, dQKV, ldg, n_nodes, rows_pad);
+                           ldq, W, dp, dO, ldo, Psave, p, seed, u2gnn_cur_epoch(), q_scale, dQKV, ldg, n_nodes, rows_pad);
         return u2gnn_launch_status();
     }
     const int64_t pad_blocks = (rows_pad - n_nodes * W + W - 1) / W;
     hipLaunchKernelGGL(window_attn_bwd_kernel, dim3((unsigned)(n_nodes + pad_blocks)), dim3(256), lds,
-                       u2gnn_stream(stream), QKV, ldq, W, dp, dO, ldo, Psave, p, seed, u2gnn_g_epoch, q_scale, dQKV, ldg, n_nodes,
+                       u2gnn_stream(stream), QKV, ldq, W, dp, dO, ldo, Psave, p, seed, u2gnn_cur_epoch(), q_scale, dQKV, ldg, n_nodes,
                        rows_pad);
     return u2gnn_launch_status();
 }

@@ -598,7 +598,8 @@ int u2gnn_probe_collect(float *total_ms, int32_t *launches);
  *  - dropout masks: after u2gnn_set_seed_epoch(epoch) every dropout-drawing kernel launched (gemm
  *    dropout epilogues, softmax, LayerNorm backward, pooling, dropout, window attention) mixes the
  *    device uint64 *epoch into its by-value seed: seed ^ *epoch * 0x9E3779B97F4A7C15 (epoch 0 =
- *    the plain seed).  Process-wide, read at launch time; NULL switches it off.
+ *    the plain seed).  Per device (ABI v17): the call sets the calling thread's current device's epoch, read at
+ *    launch time by launches on that device; NULL switches it off; U2GNN_E_ARG without a current device.
  *  - Adam's bias corrections: u2gnn_adam_dev is u2gnn_adam with step_size = lr / (1 - beta1^t) and
  *    bc2_sqrt = sqrt(1 - beta2^t) formed on the device from the double *lr and the int64 step *t.
  *  u2gnn_step_advance(epoch, t) adds 1 to each non-NULL counter (one single-thread kernel): the first

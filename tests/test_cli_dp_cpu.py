@@ -9,7 +9,6 @@ Check: after three global steps both ranks hold the same parameters, equal to ON
 same six consecutive batches of the reference stream in pairs with the mean gradient; the epoch loss is
 the sum of the six batch losses; the launcher (self_launch) reaches every rank."""
 import os
-import socket
 import subprocess
 import sys
 import textwrap
@@ -22,13 +21,6 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(REPO, "graph-transformer_amd")
 STEPS = 3
 
-
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
 
 
 def _oracle_loss(params, hb, C):
@@ -52,7 +44,7 @@ def _setup():
 
 def _worker(rank, world, port, out_dir):
     sys.path[:0] = [PKG, REPO]
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), TORCHELASTIC_USE_AGENT_STORE="True", WORLD_SIZE=str(world), RANK=str(rank),
                       LOCAL_RANK=str(rank))
     torch.set_num_threads(1)
     from oracle import u2gnn_oracle as O
@@ -82,9 +74,9 @@ def _worker(rank, world, port, out_dir):
     run.close()
 
 
-def test_cli_dp_world2_equals_one_process_over_the_same_batches(tmp_path):
+def test_cli_dp_world2_equals_one_process_over_the_same_batches(tmp_path, rdzv_port):
     world = 2
-    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, rdzv_port, str(tmp_path)), nprocs=world, join=True)
     r = [dict(np.load(os.path.join(tmp_path, f"r{i}.npz"))) for i in range(world)]
     assert list(r[0]["idx"]) == [0, 2, 4] and list(r[1]["idx"]) == [1, 3, 5]
     assert len(set(r[0]["seeds"].tolist() + r[1]["seeds"].tolist())) == 2 * STEPS

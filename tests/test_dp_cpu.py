@@ -3,7 +3,6 @@ bench.py under torch.distributed.run).  Checks: each rank's batches are exactly 
 batches of the single reference stream, and the bucketed gradient all-reduce leaves every rank
 with the mean of the per-rank gradients (computed here with the oracle)."""
 import os
-import socket
 import sys
 
 import numpy as np
@@ -14,17 +13,10 @@ import torch.multiprocessing as mp
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
-
 
 def _worker(rank, world, port, out_dir):
     sys.path[:0] = [os.path.join(REPO, "graph-transformer_amd"), REPO]
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), TORCHELASTIC_USE_AGENT_STORE="True")
     import torch.distributed as dist
     torch.set_num_threads(1)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -72,9 +64,9 @@ def _worker(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
-def test_gloo_world2_batches_and_grad_average(tmp_path):
+def test_gloo_world2_batches_and_grad_average(tmp_path, rdzv_port):
     world = 2
-    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, rdzv_port, str(tmp_path)), nprocs=world, join=True)
     r = [dict(np.load(os.path.join(tmp_path, f"r{i}.npz"))) for i in range(world)]
     assert np.array_equal(r[0]["g"], r[1]["g"]) and np.array_equal(r[0]["p"], r[1]["p"])
     # single-process reference: the same stream, 4 consecutive batches, mean grad of step 2
@@ -142,7 +134,7 @@ def _unsup_setup(world, rank, steps=2):
 
 def _unsup_worker(rank, world, port, out_dir):
     sys.path[:0] = [os.path.join(REPO, "graph-transformer_amd"), REPO]
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), TORCHELASTIC_USE_AGENT_STORE="True")
     import torch.distributed as dist
     torch.set_num_threads(1)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -173,12 +165,12 @@ def _unsup_worker(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
-def test_gloo_world2_unsup_sparse_row_exchange(tmp_path):
+def test_gloo_world2_unsup_sparse_row_exchange(tmp_path, rdzv_port):
     """Row e2: 2 ranks, each one UnSup batch + its own sample draw; after the encoder
     all-reduce and the ss.weight row all-gather, both ranks hold the same gradient, equal to the mean
     of the dense oracle gradients of the same 2 consecutive batches of the single stream."""
     world = 2
-    mp.spawn(_unsup_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    mp.spawn(_unsup_worker, args=(world, rdzv_port, str(tmp_path)), nprocs=world, join=True)
     r = [dict(np.load(os.path.join(tmp_path, f"u{i}.npz"))) for i in range(world)]
     assert np.array_equal(r[0]["g"], r[1]["g"])
     sys.path[:0] = [os.path.join(REPO, "graph-transformer_amd"), REPO]

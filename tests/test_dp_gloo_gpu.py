@@ -16,7 +16,6 @@ Sup: bit for bit.  UnSup: the encoder gradient bit for bit; the ss.weight rows w
 label and sample rows rank by rank, the single process adds them per batch -- a different fp32 order) and so
 the clip norm and the post-Adam parameters within 1e-5."""
 import os
-import socket
 import sys
 
 import numpy as np
@@ -30,13 +29,6 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 WORLD = 2
 SEED = {"c4": 1000, "c5": 2000}
 
-
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
 
 
 def _c4_setup(world, rank, dev):
@@ -77,7 +69,7 @@ def _c5_setup(world, rank, dev):
 
 def _worker(rank, world, port, out_dir, case):
     sys.path[:0] = [os.path.join(REPO, "graph-transformer_amd"), REPO]
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), TORCHELASTIC_USE_AGENT_STORE="True")
     import u2gnn_hip  # noqa: F401  (hardware queues before HIP starts)
     import torch.distributed as dist
     dev = torch.device("cuda", 0)   # both ranks on the one GPU
@@ -140,8 +132,8 @@ def _single_process(case, world):
 
 
 @pytest.mark.parametrize("case", ["c4", "c5"])
-def test_gloo_world2_on_one_gpu_equals_one_process_mean_step(tmp_path, case):
-    mp.spawn(_worker, args=(WORLD, _free_port(), str(tmp_path), case), nprocs=WORLD, join=True)
+def test_gloo_world2_on_one_gpu_equals_one_process_mean_step(tmp_path, case, rdzv_port):
+    mp.spawn(_worker, args=(WORLD, rdzv_port, str(tmp_path), case), nprocs=WORLD, join=True)
     r = [dict(np.load(os.path.join(tmp_path, f"{case}_r{i}.npz"))) for i in range(WORLD)]
     assert np.array_equal(r[0]["g"], r[1]["g"]), "ranks hold different gradients"
     assert np.array_equal(r[0]["p"], r[1]["p"]), "ranks hold different parameters"

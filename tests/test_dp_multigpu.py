@@ -8,7 +8,6 @@ N > 1) must leave exactly the same flat gradients, bit for bit, as the same step
 all-reduce after the backward (GradAllReduce); both ranks must hold identical gradients and, after
 clip + Adam, identical parameters."""
 import os
-import socket
 import sys
 
 import numpy as np
@@ -21,17 +20,10 @@ pytestmark = pytest.mark.gpu
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
-
 
 def _worker(rank, world, port, out_dir):
     sys.path[:0] = [os.path.join(REPO, "graph-transformer_amd"), REPO]
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), TORCHELASTIC_USE_AGENT_STORE="True")
     import u2gnn_hip  # noqa: F401  (hardware queues before HIP starts)
     import torch.distributed as dist
     dev = torch.device("cuda", rank)
@@ -75,9 +67,9 @@ def _worker(rank, world, port, out_dir):
 
 @pytest.mark.skipif(not torch.cuda.is_available() or torch.cuda.device_count() < 2,
                     reason="needs two GPUs (RCCL over xGMI)")
-def test_rccl_overlapped_allreduce_matches_bucketed(tmp_path):
+def test_rccl_overlapped_allreduce_matches_bucketed(tmp_path, rdzv_port):
     world = 2
-    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, rdzv_port, str(tmp_path)), nprocs=world, join=True)
     r = [dict(np.load(os.path.join(tmp_path, f"r{i}.npz"))) for i in range(world)]
     for i in range(world):
         assert np.array_equal(r[i]["g_overlap"], r[i]["g_after"])

@@ -249,6 +249,34 @@ def test_clamp_a_and_signed_ds_epilogue(prec, tile):
                Cx2=torch.empty(Np, 2 * Np, device=DEV, dtype=torch.bfloat16), ldcx2=2 * Np)
 
 
+@pytest.mark.parametrize("prec", ["bf16x3", "bf16"])
+@pytest.mark.parametrize("p", [0.5, 0.0])
+def test_signed_ds_lds_epilogue_128(prec, p):
+    """The C4 dS kernel: ATTN_DS_SIGNED on 128x128 blocks with a 32-deep K step stages its result through LDS
+    (gemm.hip ds_lds_store: row-contiguous image loads and dS stores).  Its per-element arithmetic is the
+    MFMA-layout epilogue's, so the dS it writes is bit-identical to the 64x64 and 256x128 tiles' (same k-ordered
+    sums) -- and within fp32 rounding of P * (keep * dO V^T / (1-p) - delta) in float64."""
+    Np, N, dp = 512, 470, 384
+    S = _mk(Np, Np, seed=61)
+    P, Pd, X = (torch.empty(Np, Np, device=DEV) for _ in range(3))
+    K.attn_softmax_fwd(S, Np, P, Pd if p > 0 else P, Np, N, Np, N, Np, p, 19)
+    K.attn_softmax_fwd(S, Np, None if p > 0 else X, X, Np, N, Np, N, Np, p, 19)
+    dO, V, dl = _mk(Np, dp, seed=62), _mk(Np, dp, seed=63), _mk(Np, seed=64)
+    out = {}
+    for tile in (128, 64, 256):
+        C = torch.full((Np, Np), float("nan"), device=DEV)
+        K.gemm(dO, V, C, Np, Np, dp, dp, dp, Np, trans_b=True, epilogue=_lib.EPI_ATTN_DS_SIGNED, aux0=X, p_drop=p,
+               rowvec=dl, ld_aux=Np, precision=prec, tile=tile)
+        out[tile] = C
+    assert torch.isfinite(out[128]).all()
+    assert torch.equal(out[128], out[64])
+    assert torch.equal(out[128], out[256])
+    keep = K.dropout_mask(19, Np, Np, p).double() if p > 0 else torch.ones(Np, Np, device=DEV, dtype=torch.float64)
+    acc = dO.double() @ V.double().t()
+    ref = P.double() * (keep * acc / (1 - p) - dl.double()[:, None])
+    assert rel_err(out[128].double(), ref) < (3e-5 if prec == "bf16x3" else 2e-2)
+
+
 @pytest.mark.parametrize("dp", [384, 640])   # 6 partials, and 10 (> the 8 held in registers)
 @pytest.mark.parametrize("prec", ["fp32", "bf16x3", "bf16"])
 @pytest.mark.parametrize("tile", [0, 64, 128])

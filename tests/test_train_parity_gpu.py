@@ -7,8 +7,8 @@ reproduced on the GPU, so the oracle restatement is run with the exact masks the
 parameter gradient, the clip norm and the parameters after clip_grad_norm_(0.5) + Adam.
 
 Cases: the reference-golden batches mutag_sup_L2T2 (L = 2, T = 2) and imdbb_sup (C2), and one full C4 batch
-(N ~ 4.8K, d = 367, T = 4) -- in fp32, bf16x3 (the bench's precision) and fwd32 (exact forward, bf16x3
-backward).  Tolerance TOL = 1e-3 (north_star) on max|ours - oracle| / max(1, max|oracle|) for EVERY quantity,
+(N ~ 4.8K, d = 367, T = 4) -- in fp32, fwd6 (the bench's precision: bf16x6 forward products, bf16x3
+backward), bf16x3 and fwd32 (exact forward, bf16x3 backward).  Tolerance TOL = 1e-3 (north_star) on max|ours - oracle| / max(1, max|oracle|) for EVERY quantity,
 with no per-quantity exceptions; why the gradients are compared against the oracle run with the GPU's own
 ReLU decisions, and what bounds the decisions themselves, is in tests/train_parity_util.py and DESIGN.md
 section 7.  U2GNN_PARITY_REPORT=<path> appends the measured errors as JSON lines (profiles/ evidence)."""
@@ -19,8 +19,9 @@ import numpy as np
 import pytest
 import torch
 
-from train_parity_util import (TOL, add_capture, after_err, assert_flips_at_boundary, flip_stats, gpu_decisions,
-                               inject, layer_masks, rel_err)
+from train_parity_util import (EXACT_FORWARD, MAX_SIGN_UNRESOLVED, TOL, add_capture, after_err,
+                               assert_flips_at_boundary, flip_cap, flip_stats, gpu_decisions, inject, layer_masks,
+                               rel_err)
 
 pytestmark = pytest.mark.gpu
 
@@ -65,7 +66,7 @@ def _gpu_step(m, flat, b, C, seed, native_on):
     return scores.detach().cpu().clone(), float(loss.item()), grads, ctx["stack"]
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16x3", "fwd32"])
+@pytest.mark.parametrize("precision", ["fp32", "bf16x3", "fwd32", "fwd6"])
 @pytest.mark.parametrize("name", ["mutag_sup_L2T2", "imdbb_sup", "c4"])
 def test_train_mode_step_matches_oracle_with_kernel_masks(golden_dir, name, precision):
     from oracle import u2gnn_oracle as O
@@ -136,11 +137,17 @@ def test_train_mode_step_matches_oracle_with_kernel_masks(golden_dir, name, prec
     # (1) every quantity, the GPU's ReLU decisions in the oracle
     bad = {k: v for k, v in res["gpu_relu"].items() if v > TOL and k not in ("after_sign_unresolved_above_tol", "after_raw_max")}
     assert not bad, f"{name} {precision}: above {TOL} with the GPU's ReLU decisions: {bad}"
+    assert res["gpu_relu"]["after_sign_unresolved_above_tol"] <= MAX_SIGN_UNRESOLVED
     # (2) decisions that differ from the plain oracle's are boundary units
-    assert_flips_at_boundary(stats, f"{name} {precision}")
+    assert_flips_at_boundary(stats, f"{name} {precision}", flip_cap(name, precision))
     # (3) the continuous quantities against the plain oracle
     bad = {k: res["plain"][k] for k in ("scores", "loss") if res["plain"][k] > TOL}
     assert not bad, f"{name} {precision}: above {TOL} against the plain oracle: {bad}"
+    # (4) fp32-accurate forward products: every quantity against the PLAIN oracle
+    if precision in EXACT_FORWARD:
+        bad = {k: v for k, v in res["plain"].items() if v > TOL and k not in ("after_sign_unresolved_above_tol", "after_raw_max")}
+        assert not bad, f"{name} {precision}: above {TOL} against the plain oracle: {bad}"
+        assert res["plain"]["after_sign_unresolved_above_tol"] <= MAX_SIGN_UNRESOLVED
 
 
 def test_fwd32_forward_is_the_fp32_forward(golden_dir):

@@ -17,8 +17,8 @@ import numpy as np
 import pytest
 import torch
 
-from train_parity_util import (TOL, add_capture, after_err, assert_flips_at_boundary, flip_stats, gpu_decisions,
-                               inject, layer_masks, rel_err)
+from train_parity_util import (MAX_SIGN_UNRESOLVED, TOL, add_capture, after_err, assert_flips_at_boundary,
+                               flip_cap, flip_stats, gpu_decisions, inject, layer_masks, rel_err)
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -142,6 +142,7 @@ def test_unsup_train_mode_step_matches_oracle_with_kernel_masks(golden_dir, name
                                 "errors_vs_plain_oracle": res["plain"]}) + "\n")
     bad = {k: v for k, v in res["gpu_relu"].items() if v > TOL and k not in ("after_sign_unresolved_above_tol", "after_raw_max")}
     assert not bad, f"{name} {precision}: above {TOL} with the GPU's ReLU decisions: {bad}"
-    assert_flips_at_boundary(stats, f"unsup {name} {precision}")
+    assert res["gpu_relu"]["after_sign_unresolved_above_tol"] <= MAX_SIGN_UNRESOLVED
+    assert_flips_at_boundary(stats, f"unsup {name} {precision}", flip_cap("unsup_" + name, precision))
     bad = {k: res["plain"][k] for k in ("logits", "loss") if res["plain"][k] > TOL}
     assert not bad, f"{name} {precision}: above {TOL} against the plain oracle: {bad}"

@@ -15,9 +15,12 @@ train mode.  The tests therefore check, strictly and without per-quantity except
   (2) every GPU decision that differs from the plain oracle's is a unit with |z_oracle| <= 2 * delta_z, where
       delta_z = max |z_gpu - z_oracle| over the kept units both runs switch on (z_gpu = Hd * (1 - p) from
       the saved dropped-ReLU image): a unit switches sides only within the measured forward disagreement
-      of 0, not because of a wrong unit; and there are at most MAX_FLIP_FRAC of the kept units;
+      of 0, not because of a wrong unit; and there are at most FLIP_CAP of them (absolute, per case);
   (3) the quantities that are continuous in the forward (outputs, loss) within 1e-3 of the plain oracle
-      (the clip norm is a function of the gradients, so it is held by (1)).
+      (the clip norm is a function of the gradients, so it is held by (1));
+  (4) for the policies with fp32-accurate forward products (EXACT_FORWARD: fp32, fwd32, fwd6), EVERY quantity
+      within 1e-3 of the PLAIN oracle at the tests' seed (round 6: their ReLU decisions carry fp32-level
+      rounding, 0-3 differing units per C4 step over 8 seeds against bf16x3's 6-18; profiles/r06/).
 Post-Adam parameters have the same kind of discontinuity: Adam's first step moves an element by
 lr * g / (|g| + eps), i.e. by ~lr in the direction of sign(g).  Where a gradient element lies within the
 two computations' disagreement of zero (|g_oracle| <= 2 * max|g_gpu - g_oracle| of its tensor: the element's
@@ -33,7 +36,16 @@ TOL = 1e-3
 # (C4, 8 seeds: differing decisions at |z| <= 8.6e-6 in bf16x3, <= 5.1e-7 with exact fp32 forward products;
 # C5, whose d = 4 inputs are all equal, has a worse-conditioned forward: 2.7e-5 in fp32)
 FLIP_MARGIN = 2.0
-MAX_FLIP_FRAC = 1e-5
+# absolute caps on the differing ReLU decisions of one step at the tests' seed: about twice the count measured
+# there (profiles/r05/train_parity.jsonl, profiles/r06/): C4 bf16x3 11, C5 fp32 11 / bf16x3 17 (d = 4, all node
+# features equal: the worst-conditioned forward), every other case and policy 0 -- a case measured at 0 gets 2
+FLIP_CAP = {("c4", "bf16x3"): 22, ("unsup_c5", "fp32"): 22, ("unsup_c5", "bf16x3"): 34}
+# post-Adam elements whose gradient sign the two fp32 computations do not determine (below): at most this many
+# above TOL per step (C5 measured 1 with the GPU's ReLU decisions)
+MAX_SIGN_UNRESOLVED = 4
+# precision policies whose forward products are fp32-accurate (exact fp32, or the bf16x6 split): held to the
+# PLAIN oracle at TOL on every quantity where the reference's own fp32 arithmetic decides the same units
+EXACT_FORWARD = ("fp32", "fwd32", "fwd6")
 P_ENC = 0.5   # encoder dropout (pytorch_U2GNN_Sup.py:20)
 
 def rel_err(a, b):
@@ -105,16 +117,23 @@ def flip_stats(masks, dec, keys):
     return n, kept, mx, dz
 
 
-def assert_flips_at_boundary(stats, what):
+def flip_cap(case, precision):
+    return FLIP_CAP.get((case, precision), 2)
+
+
+def assert_flips_at_boundary(stats, what, cap):
     n, kept, mx, dz = stats
     assert mx <= FLIP_MARGIN * dz or n == 0, \
         f"{what}: a ReLU decision differs at |z| = {mx:.3g}, beyond {FLIP_MARGIN} x the forward disagreement {dz:.3g}"
-    assert n <= max(2, int(MAX_FLIP_FRAC * kept)), f"{what}: {n} differing ReLU decisions of {kept} kept units"
+    assert n <= cap, f"{what}: {n} differing ReLU decisions of {kept} kept units (cap {cap})"
 
 
 def after_err(after_gpu, after_ref, g_gpu, g_ref):
     """(max relative post-Adam error over the elements whose gradient sign is resolved, elements above TOL
-    whose gradient is sign-unresolved, raw max relative error) -- see the module docstring."""
+    whose gradient is sign-unresolved, raw max relative error) -- see the module docstring.  An element is
+    sign-unresolved when ITS OWN gradient disagreement reaches half its oracle gradient (|g_oracle| <=
+    2 |g_gpu - g_oracle|, element by element): one large error elsewhere in the tensor excuses nothing, and the
+    callers bound the count (MAX_SIGN_UNRESOLVED)."""
     a = torch.as_tensor(after_gpu).double().cpu()
     b = torch.as_tensor(after_ref).double().cpu()
     gg = torch.as_tensor(g_gpu).double().cpu()
@@ -123,6 +142,6 @@ def after_err(after_gpu, after_ref, g_gpu, g_ref):
         return 0.0, 0, 0.0
     scale = max(1.0, b.abs().max().item())
     e = (a - b).abs() / scale
-    unresolved = gr.abs() <= 2.0 * (gg - gr).abs().max()
+    unresolved = gr.abs() <= 2.0 * (gg - gr).abs()
     resolved_err = float(e[~unresolved].max()) if bool((~unresolved).any()) else 0.0
     return resolved_err, int(((e > TOL) & unresolved).sum()), float(e.max())

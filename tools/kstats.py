@@ -30,4 +30,27 @@ lines.append(f"total_kernel_ms {tot / 1e3:.2f}")
 txt = "\n".join(lines) + "\n"
 if out:
     open(out, "w").write(txt)
+    # beside the text: per-kernel and per-(kernel, grid) averages tagged with the native build id, which bench.py
+    # cites (rocprof_stats) when the build matches -- the grid split separates launches of one kernel at
+    # different sizes (the gather of a batch's slot-0 rows vs the bench's all-slot gather roofline)
+    import json
+    import re
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "graph-transformer_amd"))
+    from u2gnn_hip._lib import source_build_id
+
+    def short(n):
+        n = re.sub(r"^void ", "", n)
+        n = re.sub(r"\(anonymous namespace\)::", "", n)
+        return n.split("(")[0] if "<" not in n else n[:n.index(">") + 1]
+    grid = collections.defaultdict(lambda: [0, 0.0])
+    for r in rows:
+        d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+        g = grid[(short(r["Kernel_Name"]), int(r.get("Grid_Size_X") or r.get("Grid_Size") or 0))]
+        g[0] += 1
+        g[1] += d
+    js = {"title": title, "build_id": source_build_id(), "total_kernel_ms": tot / 1e3,
+          "kernels": {short(n): {"calls": c, "avg_us": t / c, "total_ms": t / 1e3} for n, (c, t) in agg.items()},
+          "by_grid": [{"kernel": k, "grid": gx, "calls": c, "avg_us": t / c} for (k, gx), (c, t) in
+                      sorted(grid.items(), key=lambda kv: -kv[1][1])[:80]]}
+    json.dump(js, open(os.path.splitext(out)[0] + ".json", "w"), indent=1)
 print(txt)

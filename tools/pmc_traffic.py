@@ -24,6 +24,7 @@ def per_kernel(db, counter):
     path = glob.glob(os.path.join(tmp, "*counter_collection*.csv"))[0]
     agg = collections.defaultdict(lambda: [0, 0.0])
     seen = set()
+    grids = collections.defaultdict(set)
     for r in csv.DictReader(open(path)):
         if r.get("Counter_Name") != counter:
             continue
@@ -31,11 +32,18 @@ def per_kernel(db, counter):
         name = re.sub(r"^void ", "", r["Kernel_Name"])
         name = re.sub(r"\(anonymous namespace\)::", "", name)
         name = name.split("((")[0].split("(")[0] if "<" not in name else name[:name.index(">") + 1]
-        a = agg[name]
-        if key not in seen:
-            a[0] += 1
-            seen.add(key)
-        a[1] += float(r["Counter_Value"])
+        g = int(r.get("Grid_Size") or r.get("Grid_Size_X") or 0)
+        for nm in (name, f"{name}@grid={g}"):   # per kernel, and per kernel and launch size
+            a = agg[nm]
+            if (key, nm) not in seen:
+                a[0] += 1
+                seen.add((key, nm))
+            a[1] += float(r["Counter_Value"])
+        grids[name].add(g)
+    # the largest launch size of each kernel under a fixed name (bench.py: the gather roofline's launches)
+    for name, gs in grids.items():
+        if len(gs) > 1:
+            agg[f"{name}@maxgrid"] = agg[f"{name}@grid={max(gs)}"]
     return agg
 
 

@@ -21,6 +21,10 @@
 // Measured variants: two waves per SIMD (8 waves, d split in halves, P handed
 // between partner waves through LDS) ran 2-4 % slower than this form; an ablation puts ~30 of its
 // ~95 us (C4) in the fixed costs (row statistics, partial-output stores, the combine pass).
+// BF16X6 (round 6, the "fwd6" policy): V is DMA'd as the in-projection's fp32 rows (the same 4 dp bytes per key
+// as an x2 row, so the same LDS image size), its 32-column chunk halves XOR-swizzled by key-row bit 3, and the
+// V^T fragments are read as 8 ds_read_b32 per lane and split into hi / mid / lo bf16 planes in registers; P is
+// split three ways too, and each term is the six products mm, hl, lh, hm, mh, hh (fp32-accurate).
 #include "u2gnn_common.h"
 
 #include <type_traits>
@@ -67,16 +71,21 @@ __device__ __forceinline__ void dma16(const char *base, int off, unsigned m0) {
 // LDS byte address of a shared object (a link-time constant)
 __device__ __forceinline__ unsigned lds_addr(const void *p) { return (unsigned)(size_t)(const lds_void *)p; }
 
-template <int DP, int NT = FA_NT>
+// fp32 V image (BF16X6): 16-B chunk c of key row r stored at c ^ (8 ((r >> 3) & 1)), i.e. rows 8..15 (mod 16)
+// swap the two 128-B halves of every 256-B column group: the 8 ds_read_b32 of a fragment have lanes l < 32
+// reading key row k and lanes l >= 32 row k + 8, which then fall in opposite 32-bank halves
+__device__ __forceinline__ int kr_swz6(int krow) { return ((krow >> 3) & 1) << 7; }
+
+template <int DP, int NPL, int NT = FA_NT>
 __device__ __forceinline__ void issue_v(const char *vbase, int64_t ld_bytes, unsigned img, int tid, int w) {
-    constexpr int RB = 4 * DP;                      // bytes per k-row
+    constexpr int RB = 4 * DP;                      // bytes per k-row (x2: hi + lo bf16; x6: fp32)
     constexpr int NI = FA_BN * RB / (16 * NT);     // DMA instructions per thread
     static_assert(NI * 16 * NT == FA_BN * RB, "V tile / threads");
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
         const int b = (i * NT + tid) * 16;
         const int kr = b / RB, pb = b % RB;
-        dma16(vbase, (int)(kr * ld_bytes) + (pb ^ kr_swz(kr)), img + (i * NT + 64 * w) * 16);
+        dma16(vbase, (int)(kr * ld_bytes) + (pb ^ (NPL == 3 ? kr_swz6(kr) : kr_swz(kr))), img + (i * NT + 64 * w) * 16);
     }
 }
 
@@ -133,6 +142,41 @@ __device__ __forceinline__ void v_frag(const char *img, const VBase &B, int dt, 
     lo = __builtin_bit_cast(bf16x8, vl);
 }
 
+// BF16X6: the V^T fragment of d tile dt, k step ks (lane: d = 32 dt + l % 32, keys 16 ks + 8 (l / 32) + e) from
+// the fp32 image as 8 ds_read_b32, split into three bf16 planes.  base[dt & 1] = this lane's byte offset
+// (v_base6); every other term is a compile-time offset
+template <int DP>
+__device__ __forceinline__ void v_base6(int lane, int (&base)[2]) {
+    const int li = lane & 31, h = lane >> 5;
+    // key row 16 ks + 8 h + e, chunk (8 dt + li / 4) ^ 8 h = 8 (dt ^ h) + li / 4
+    base[0] = 8 * h * 4 * DP + 128 * h + 4 * li;
+    base[1] = 8 * h * 4 * DP - 128 * h + 4 * li;
+}
+
+template <int DP>
+__device__ __forceinline__ void v_frag6(const char *img, const int (&base)[2], int dt, int ks, bf16x8 &hi, bf16x8 &mid,
+                                        bf16x8 &lo) {
+    const char *a = img + base[dt & 1] + 128 * dt + ks * 64 * DP;
+    float x[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) x[e] = *reinterpret_cast<const float *>(a + e * 4 * DP);
+    unsigned h[4], m[4], l[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) split3(x[2 * i], x[2 * i + 1], h[i], m[i], l[i]);
+    hi = __builtin_bit_cast(bf16x8, h);
+    mid = __builtin_bit_cast(bf16x8, m);
+    lo = __builtin_bit_cast(bf16x8, l);
+}
+
+__device__ __forceinline__ void split8_3(const float *x, bf16x8 &hi, bf16x8 &mid, bf16x8 &lo) {
+    unsigned h[4], m[4], l[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) split3(x[2 * i], x[2 * i + 1], h[i], m[i], l[i]);
+    hi = __builtin_bit_cast(bf16x8, h);
+    mid = __builtin_bit_cast(bf16x8, m);
+    lo = __builtin_bit_cast(bf16x8, l);
+}
+
 __device__ __forceinline__ void split8(const float *x, bf16x8 &hi, bf16x8 &lo) {
     unsigned h[4], l[4];
 #pragma unroll
@@ -147,8 +191,9 @@ struct SpvP {
     const float *rowpart;  // EPI_STORE_ROWSTAT partials: [rows_pad][ld_rowpart] (max, sum) pairs
     int64_t ld_rowpart;
     int32_t ngroups;
-    const __bf16 *qkv2;    // x2 [rows_pad][ldq2]
+    const __bf16 *qkv2;    // x2 [rows_pad][ldq2]; BF16X6: the fp32 in-projection output [rows_pad][ldq2 floats]
     int64_t ldq2;
+    int64_t ld_vbytes;     // bytes per row of qkv2
     float *Pd;             // signed image [rows_pad][ldp]
     int64_t ldp;
     float *Opart;          // [nsplit][rows_pad][dp]
@@ -212,7 +257,8 @@ struct PRow {
     float *prow;
 };
 
-__device__ __forceinline__ void p_half(const PRow &R, const char *simg, int kb, int ks, bf16x8 &ph, bf16x8 &pl) {
+template <int NPL>
+__device__ __forceinline__ void p_half(const PRow &R, const char *simg, int kb, int ks, bf16x8 (&pp)[3]) {
     const int c = 4 * ks + 2 * R.h;   // logical 16-B chunk of the row
     const char *rowp = simg + R.r * 128;
     const float4 a = *reinterpret_cast<const float4 *>(rowp + ((c ^ s_swz(R.r)) << 4));
@@ -241,37 +287,63 @@ __device__ __forceinline__ void p_half(const PRow &R, const char *simg, int kb, 
 #else
     if (img[0] == 123.f) *dst = img[1] + img[2] + img[3] + img[4] + img[5] + img[6] + img[7];
 #endif
-    split8(pv, ph, pl);
+    if constexpr (NPL == 3) split8_3(pv, pp[0], pp[1], pp[2]);
+    else split8(pv, pp[0], pp[1]);
 }
 
-__device__ __forceinline__ void p_block(const PRow &R, const char *simg, int kb, bf16x8 (&ph)[2], bf16x8 (&pl)[2]) {
+template <int NPL>
+__device__ __forceinline__ void p_block(const PRow &R, const char *simg, int kb, bf16x8 (&pp)[2][3]) {
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) p_half(R, simg, kb, ks, ph[ks], pl[ks]);
+    for (int ks = 0; ks < 2; ++ks) p_half<NPL>(R, simg, kb, ks, pp[ks]);
 }
 
 // O^T += V^T . P over one block (V image vimg, P operands ph / pl); fragments of d tile t + 1 are read
 // while the products of tile t run
-template <int DP, bool X3>
-__device__ __forceinline__ void pv_block(const char *vimg, const VBase &vb, const bf16x8 (&ph)[2],
-                                         const bf16x8 (&pl)[2], f32x16 (&o)[DP / 32]) {
+template <int DP, int NPL>
+__device__ __forceinline__ void pv_block(const char *vimg, const VBase &vb, const int (&vb6)[2], const bf16x8 (&pp)[2][3],
+                                         f32x16 (&o)[DP / 32]) {
     constexpr int DT = DP / 32;
-    bf16x8 vh[2][2], vl[2][2];
-    v_frag<DP>(vimg, vb, 0, 0, vh[0][0], vl[0][0]);
-    v_frag<DP>(vimg, vb, 0, 1, vh[0][1], vl[0][1]);
+    if constexpr (NPL == 3) {
+        // bf16x6: one d tile's fragments at a time (ks 1's reads and splits under ks 0's six products; a second
+        // buffer for tile t + 1 spilled at dp = 384)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)   // (k step outermost: ks 0's P planes die before ks 1's tiles)
+#pragma unroll
+            for (int t = 0; t < DT; ++t) {   // smallest terms first: mm, hl, lh, hm, mh, then hh
+                bf16x8 f[3];
+                v_frag6<DP>(vimg, vb6, t, ks, f[0], f[1], f[2]);
+                const bf16x8(&q)[3] = pp[ks];
+                o[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f[1], q[1], o[t], 0, 0, 0);
+                o[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f[0], q[2], o[t], 0, 0, 0);
+                o[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f[2], q[0], o[t], 0, 0, 0);
+                o[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f[0], q[1], o[t], 0, 0, 0);
+                o[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f[1], q[0], o[t], 0, 0, 0);
+                o[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f[0], q[0], o[t], 0, 0, 0);
+            }
+        return;
+    }
+    bf16x8 v[2][2][3];   // [buffer][ks][plane]
+    auto frag = [&](int t, int ks, bf16x8 (&f)[3]) __attribute__((always_inline)) {
+        v_frag<DP>(vimg, vb, t, ks, f[0], f[1]);
+    };
+    frag(0, 0, v[0][0]);
+    frag(0, 1, v[0][1]);
 #pragma unroll
     for (int t = 0; t < DT; ++t) {
         const int cur = t & 1;
         if (t + 1 < DT) {
-            v_frag<DP>(vimg, vb, t + 1, 0, vh[cur ^ 1][0], vl[cur ^ 1][0]);
-            v_frag<DP>(vimg, vb, t + 1, 1, vh[cur ^ 1][1], vl[cur ^ 1][1]);
+            frag(t + 1, 0, v[cur ^ 1][0]);
+            frag(t + 1, 1, v[cur ^ 1][1]);
         }
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
-            if constexpr (X3) {
-                o[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vh[cur][ks], pl[ks], o[t], 0, 0, 0);
-                o[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vl[cur][ks], ph[ks], o[t], 0, 0, 0);
+            const bf16x8(&f)[3] = v[cur][ks];
+            const bf16x8(&q)[3] = pp[ks];
+            if constexpr (NPL >= 2) {
+                o[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f[0], q[1], o[t], 0, 0, 0);
+                o[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f[1], q[0], o[t], 0, 0, 0);
             }
-            o[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vh[cur][ks], ph[ks], o[t], 0, 0, 0);
+            o[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f[0], q[0], o[t], 0, 0, 0);
         }
     }
 }
@@ -300,7 +372,8 @@ __device__ __forceinline__ void spv_block(int id, int total, int qblocks, int &q
     qb = pos - split * qblocks;
 }
 
-template <int DP, bool X3>
+// NPL: bf16 planes per operand -- 1 (bf16), 2 (bf16x3: x2 V rows), 3 (bf16x6: fp32 V rows)
+template <int DP, int NPL>
 __global__ void __launch_bounds__(FA_NT, 1) attn_softmax_pv_kernel(SpvP P) {
     constexpr int DT = DP / 32;              // 32-wide d tiles of O
     constexpr int VIMG = FA_BN * 4 * DP;     // bytes of one V image
@@ -320,8 +393,9 @@ __global__ void __launch_bounds__(FA_NT, 1) attn_softmax_pv_kernel(SpvP P) {
     const int query = qrow0 + R.r;
     const int kb0 = split * P.kb_per_split;
     const int kb1 = min(kb0 + P.kb_per_split, P.kb_valid);
-    const int64_t ld_bytes = P.ldq2 * 2, lds_bytes = P.lds * 4;
-    const char *vcol = reinterpret_cast<const char *>(P.qkv2) + 8 * DP;   // x2 byte offset of V
+    const int64_t ld_bytes = P.ld_vbytes, lds_bytes = P.lds * 4;
+    // byte offset of V (column 2 dp): 2 dp x2 columns of 4 B (hi + lo), or 2 dp fp32 columns -- 8 DP either way
+    const char *vcol = reinterpret_cast<const char *>(P.qkv2) + 8 * DP;
     const char *srow0 = reinterpret_cast<const char *>(P.S + (int64_t)qrow0 * P.lds);
     const bool qvalid = query < P.n_valid;
     float M = 0.f, inv = 0.f;
@@ -339,6 +413,8 @@ __global__ void __launch_bounds__(FA_NT, 1) attn_softmax_pv_kernel(SpvP P) {
     R.rkey = u2gnn_row_key(seed, (uint32_t)query);
     R.prow = P.Pd + (int64_t)query * P.ldp;
     const VBase vb = v_base<DP>(lane);
+    int vb6[2];
+    v_base6<DP>(lane, vb6);
 
     f32x16 o[DT];
 #pragma unroll
@@ -351,12 +427,12 @@ __global__ void __launch_bounds__(FA_NT, 1) attn_softmax_pv_kernel(SpvP P) {
     // S(kb+1) for the current iteration and receives V(kb+1) and S(kb+2) by DMA.  The stages are separate
     // LDS objects and the loop is unrolled by two, so every access names its stage at compile time.
     auto issue_vt = [&](int kb, unsigned img) __attribute__((always_inline)) {
-        issue_v<DP>(vcol + (int64_t)kb * FA_BN * ld_bytes, ld_bytes, img, tid, w);
+        issue_v<DP, NPL>(vcol + (int64_t)kb * FA_BN * ld_bytes, ld_bytes, img, tid, w);
     };
     auto issue_st = [&](int kb, unsigned img) __attribute__((always_inline)) {
         issue_s(srow0 + (int64_t)kb * FA_BN * 4, lds_bytes, img, tid, w);
     };
-    bf16x8 ph[2], pl[2];
+    bf16x8 pp[2][3];   // [ks][plane]
     // an iteration that also forms the next block's P (kb + 1 < kb1)
     auto body = [&](auto stage, int kb) __attribute__((always_inline)) {
         constexpr int STG = decltype(stage)::value;
@@ -369,26 +445,29 @@ __global__ void __launch_bounds__(FA_NT, 1) attn_softmax_pv_kernel(SpvP P) {
         issue_vt(kb + 1, lds_addr(STG ? vst0 : vst1));
         if (kb + 2 < kb1) issue_st(kb + 2, lds_addr(STG ? sst1 : sst0));
 #endif
-        bf16x8 nh[2], nl[2];
+        bf16x8 np[2][3];
 #ifndef SPV_NO_P
-        p_block(R, STG ? sst0 : sst1, kb + 1, nh, nl);
+        p_block<NPL>(R, STG ? sst0 : sst1, kb + 1, np);
 #else
-        nh[0] = ph[1], nh[1] = ph[0], nl[0] = pl[1], nl[1] = pl[0];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) np[0][q] = pp[1][q], np[1][q] = pp[0][q];
 #endif
 #ifndef SPV_NO_MFMA
-        pv_block<DP, X3>(STG ? vst1 : vst0, vb, ph, pl, o);
+        pv_block<DP, NPL>(STG ? vst1 : vst0, vb, vb6, pp, o);
 #endif
 #ifndef SPV_NO_HINT
-        interleave_hint<(X3 ? 6 : 2) * DT, X3 ? 6 : 18>();
+        if constexpr (NPL != 3) interleave_hint<(NPL == 2 ? 6 : 2) * DT, NPL == 2 ? 6 : 18>();
 #endif
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) ph[ks] = nh[ks], pl[ks] = nl[ks];
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+            for (int q = 0; q < 3; ++q) pp[ks][q] = np[ks][q];
     };
     auto last = [&](auto stage) __attribute__((always_inline)) {
         constexpr int STG = decltype(stage)::value;
         wait_vm<4>();
         __builtin_amdgcn_s_barrier();
-        pv_block<DP, X3>(STG ? vst1 : vst0, vb, ph, pl, o);
+        pv_block<DP, NPL>(STG ? vst1 : vst0, vb, vb6, pp, o);
     };
     if (kb0 < kb1) {
         issue_vt(kb0, lds_addr(vst0));
@@ -396,7 +475,7 @@ __global__ void __launch_bounds__(FA_NT, 1) attn_softmax_pv_kernel(SpvP P) {
         if (kb0 + 1 < kb1) issue_st(kb0 + 1, lds_addr(sst1));
         wait_vm<0>();
         __builtin_amdgcn_s_barrier();
-        p_block(R, sst0, kb0, ph, pl);
+        p_block<NPL>(R, sst0, kb0, pp);
         int kb = kb0;
         for (; kb + 2 < kb1; kb += 2) {
             body(std::integral_constant<int, 0>(), kb);
@@ -482,12 +561,14 @@ inline int spv_nsplit(int64_t n_valid) {
 }
 
 template <int DP>
-void launch_spv(const SpvP &P, bool x3, hipStream_t st) {
+void launch_spv(const SpvP &P, int npl, hipStream_t st) {
     const dim3 grid((unsigned)(P.qblocks * P.nsplit));
-    if (x3)
-        hipLaunchKernelGGL((attn_softmax_pv_kernel<DP, true>), grid, dim3(FA_NT), 0, st, P);
+    if (npl == 3)
+        hipLaunchKernelGGL((attn_softmax_pv_kernel<DP, 3>), grid, dim3(FA_NT), 0, st, P);
+    else if (npl == 2)
+        hipLaunchKernelGGL((attn_softmax_pv_kernel<DP, 2>), grid, dim3(FA_NT), 0, st, P);
     else
-        hipLaunchKernelGGL((attn_softmax_pv_kernel<DP, false>), grid, dim3(FA_NT), 0, st, P);
+        hipLaunchKernelGGL((attn_softmax_pv_kernel<DP, 1>), grid, dim3(FA_NT), 0, st, P);
 }
 
 }  // namespace
@@ -504,9 +585,11 @@ int u2gnn_attn_softmax_pv(const float *S, int64_t lds, const float *rowpart, int
                           float *ws, int64_t ws_floats, int64_t n_valid, int64_t rows_pad, float p, uint64_t seed,
                           int32_t precision, void *stream) {
     if (!S || !rowpart || !qkv2 || !Pd || !O || !ws || n_valid < 1 || rows_pad < n_valid || rows_pad % FA_BM ||
-        !(p < 1.f) || p < 0.f || (precision != U2GNN_PREC_BF16X3 && precision != U2GNN_PREC_BF16))
+        !(p < 1.f) || p < 0.f ||
+        (precision != U2GNN_PREC_BF16X3 && precision != U2GNN_PREC_BF16 && precision != U2GNN_PREC_BF16X6))
         return U2GNN_E_ARG;
-    if (dp < 64 || dp > 384 || dp % 64 || ldq2 < 6 * dp || (ldq2 & 7) || lds < rows_pad || (lds & 3) ||
+    const bool x6 = precision == U2GNN_PREC_BF16X6;   // qkv2 = the fp32 in-projection output, ldq2 in floats
+    if (dp < 64 || dp > 384 || dp % 64 || ldq2 < (x6 ? 3 : 6) * dp || (ldq2 & (x6 ? 3 : 7)) || lds < rows_pad || (lds & 3) ||
         ldp < rows_pad || (ldp & 3) || ldo < dp || (ldo & 3) || ngroups < 2 || (ngroups & 1) ||
         ld_rowpart < ngroups || (ld_rowpart & 1) || ngroups > INT32_MAX)
         return U2GNN_E_ARG;
@@ -514,7 +597,8 @@ int u2gnn_attn_softmax_pv(const float *S, int64_t lds, const float *rowpart, int
         ((uintptr_t)rowpart & 15) || ((uintptr_t)ws & 15))
         return U2GNN_E_ALIGN;
     // 32-bit byte offsets inside one block's DMA sources
-    if ((int64_t)FA_BM * lds * 4 >= INT32_MAX || (int64_t)FA_BN * ldq2 * 2 >= INT32_MAX) return U2GNN_E_SHAPE;
+    const int64_t ld_vbytes = ldq2 * (x6 ? 4 : 2);
+    if ((int64_t)FA_BM * lds * 4 >= INT32_MAX || (int64_t)FA_BN * ld_vbytes >= INT32_MAX) return U2GNN_E_SHAPE;
     const int64_t need = u2gnn_attn_softmax_pv_ws_floats(n_valid, rows_pad, dp);
     if (need < 0 || ws_floats < need) return U2GNN_E_ARG;
     SpvP P;
@@ -525,6 +609,7 @@ int u2gnn_attn_softmax_pv(const float *S, int64_t lds, const float *rowpart, int
     P.ngroups = (int32_t)ngroups;
     P.qkv2 = static_cast<const __bf16 *>(qkv2);
     P.ldq2 = ldq2;
+    P.ld_vbytes = ld_vbytes;
     P.Pd = Pd;
     P.ldp = ldp;
     P.Opart = ws;
@@ -545,14 +630,16 @@ int u2gnn_attn_softmax_pv(const float *S, int64_t lds, const float *rowpart, int
     P.seed = seed;
     P.epoch = u2gnn_cur_epoch();
     hipStream_t st = u2gnn_stream(stream);
-    const bool x3 = precision == U2GNN_PREC_BF16X3;
+    const int npl = x6 ? 3 : precision == U2GNN_PREC_BF16X3 ? 2 : 1;
     switch (dp) {
-        case 64: launch_spv<64>(P, x3, st); break;
-        case 128: launch_spv<128>(P, x3, st); break;
-        case 192: launch_spv<192>(P, x3, st); break;
-        case 256: launch_spv<256>(P, x3, st); break;
-        case 320: launch_spv<320>(P, x3, st); break;
-        default: launch_spv<384>(P, x3, st); break;
+#ifndef SPV_ONLY384   // (kernel experiments: build the dp = 384 instances only)
+        case 64: launch_spv<64>(P, npl, st); break;
+        case 128: launch_spv<128>(P, npl, st); break;
+        case 192: launch_spv<192>(P, npl, st); break;
+        case 256: launch_spv<256>(P, npl, st); break;
+        case 320: launch_spv<320>(P, npl, st); break;
+#endif
+        default: launch_spv<384>(P, npl, st); break;
     }
     const int rc = u2gnn_launch_status();
     if (rc != U2GNN_OK || P.direct) return rc;

@@ -487,6 +487,9 @@ int64_t ffn2_split(int64_t dp, bool mfma, int64_t Np, int64_t ffp) {
 // them), then 128x128 (the same per-element sums: same bits; engine.qk_tile mirrors the rule)
 int qk_tile(int64_t Np) { return (Np % 256 == 0 && (Np / 256) * (Np / 128) >= 256) ? 256 : 128; }
 
+// (bf16x6 -- the fwd6 policy -- keeps the three-pass form: its fused kernel, u2gnn_attn_softmax_pv with BF16X6, ran
+// the C4 step at 3.42 / 3.43 ms against 3.40 unfused, and its exp2-based probabilities moved one boundary ReLU unit
+// of the test seed's step across 0)
 bool fused_attn(const Dims &D) {
     return !D.window && !small_attn(D) && D.prec_fwd != U2GNN_PREC_F32 && D.prec_fwd != U2GNN_PREC_BF16X6 &&
            D.dp <= 384;
@@ -518,8 +521,10 @@ int layer_fwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
     const bool plan = W.plan();
     Ctx c = carve_ctx(need_ctx ? CA : W, D, drop);
     const bool fused = fused_attn(D);
-    // the in-projection output again in x2 format: the V tiles the fused softmax.P.V kernel reads
-    void *qkv2 = fused ? static_cast<void *>(W.take<uint16_t>(Np * 6 * dp)) : nullptr;
+    // the in-projection output again in x2 format: the V tiles the fused softmax.P.V kernel reads (bf16x6: it reads
+    // the fp32 output itself and splits V in registers, no copy)
+    const bool x6 = prec == U2GNN_PREC_BF16X6;
+    void *qkv2 = fused && !x6 ? static_cast<void *>(W.take<uint16_t>(Np * 6 * dp)) : nullptr;
     // a3.1 in-projection (+bias, Q scaled by 1/sqrt(d)); the small-width attention does its own
     if (!small_attn(D)) {
         G g(X, w->W_in, c.QKV, Np, 3 * dp, dp, dp, dp, 3 * dp, prec);
@@ -533,7 +538,7 @@ int layer_fwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
         g.a.alpha = (float)(1.0 / std::sqrt((double)d));
         g.a.scale_cols = dp;
         // the x2 copy the fused softmax.P.V kernel reads: its V block only (Q and K are never read in x2)
-        if (fused) g.a.Cx2 = qkv2, g.a.ldcx2 = 6 * dp, g.a.cx2_col0 = (int32_t)(2 * dp);
+        if (fused && !x6) g.a.Cx2 = qkv2, g.a.ldcx2 = 6 * dp, g.a.cx2_col0 = (int32_t)(2 * dp);
         U2GNN_TRY(g.run(st, plan));
     }
     const float *Q = c.QKV, *Kt = Q ? Q + dp : nullptr, *V = Q ? Q + 2 * dp : nullptr;   // (no image: small path)
@@ -568,9 +573,9 @@ int layer_fwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
         }
         if (!plan) {
             probe_mark(U2GNN_ROLE_PV, false, st, plan);
-            U2GNN_TRY(u2gnn_attn_softmax_pv(c.Pd, Np, rowpart, ld_rp, groups, qkv2, 6 * dp, dp, c.Pd, Np, c.O, dp,
-                                            pv_ws, u2gnn_attn_softmax_pv_ws_floats(N, Np, dp), N, Np, pd, s->attn,
-                                            prec, st));
+            U2GNN_TRY(u2gnn_attn_softmax_pv(c.Pd, Np, rowpart, ld_rp, groups, x6 ? static_cast<const void *>(c.QKV) : qkv2,
+                                            x6 ? 3 * dp : 6 * dp, dp, c.Pd, Np, c.O, dp, pv_ws,
+                                            u2gnn_attn_softmax_pv_ws_floats(N, Np, dp), N, Np, pd, s->attn, prec, st));
             probe_mark(U2GNN_ROLE_PV, true, st, plan);
         }
     } else {

@@ -377,9 +377,10 @@ def mid_tail(d: int, dp: int, Np: int) -> bool:
 
 
 def fused_attn(dp: int, prec_qk: str, prec_pv: str) -> bool:
-    """Node-axis attention forward through the fused softmax.P.V kernel: the bf16 / bf16x3 matrix-core
-    precisions, dp <= 384 (encoder_layer.cpp fused_attn)."""
-    return prec_qk not in ("fp32", "bf16x6") and prec_pv not in ("fp32", "bf16x6") and dp <= 384
+    """Node-axis attention forward through the fused softmax.P.V kernel: Q K^T with the row-statistics epilogue
+    (bf16, bf16x3 or bf16x6) and P.V in bf16 / bf16x3, dp <= 384 (encoder_layer.cpp fused_attn: the fwd6 policy keeps
+    the three-pass form; the kernel's bf16x6 P.V is a tested capability, measured no faster)."""
+    return prec_qk != "fp32" and prec_pv in ("bf16", "bf16x3") and dp <= 384
 
 
 def _attn_split(Q, Kt, V, N, Np, dp, pd, seeds, prec, att, dev):
@@ -414,7 +415,8 @@ def encoder_layer_forward(X: torch.Tensor, w: PackedLayer, p: LayerParams, dims:
     QKV = QKV2 = None
     if not small:   # (the small-width attention projects into its own compact context)
         QKV = torch.empty(Np, 3 * dp, device=dev, dtype=f32)
-        QKV2 = torch.empty(Np, 6 * dp, device=dev, dtype=torch.bfloat16) if fused else None   # x2 copy for P.V
+        # x2 copy of V for the fused P.V (bf16x6 P.V reads the fp32 output itself)
+        QKV2 = torch.empty(Np, 6 * dp, device=dev, dtype=torch.bfloat16) if fused and _rp("pv", prec) != "bf16x6" else None
         K.gemm(X, w.W_in, QKV, Np, 3 * dp, dp, dp, dp, 3 * dp, trans_b=True, epilogue=E.EPI_BIAS, bias=w.b_in,
                alpha=1.0 / math.sqrt(d), scale_cols=dp, precision=_rp("in_proj", prec), flops=6.0 * N * d * d,
                tile=256 if (_rp("in_proj", prec) != "fp32" and Np % 256 == 0 and (Np // 256) * (3 * dp // 128) >= BIG_TILE_BLOCKS) else 0,
@@ -435,8 +437,9 @@ def encoder_layer_forward(X: torch.Tensor, w: PackedLayer, p: LayerParams, dims:
                rowpart=rowpart, n_valid=N, precision=_rp("qk", prec), flops=att, tile=qk_tile(Np))
         ws = torch.empty(K.attn_softmax_pv_ws_floats(N, Np, dp), device=dev, dtype=f32)
         O = torch.empty(Np, dp, device=dev, dtype=f32)
-        K.attn_softmax_pv(Pd, Np, rowpart, Np // 64, QKV2, 6 * dp, dp, Pd, Np, O, dp, ws, N, Np, pd,
-                          seeds.get(SITE_ATTN, 0), precision=_rp("pv", prec))
+        x6 = _rp("pv", prec) == "bf16x6"
+        K.attn_softmax_pv(Pd, Np, rowpart, Np // 64, QKV if x6 else QKV2, 3 * dp if x6 else 6 * dp, dp, Pd, Np, O, dp,
+                          ws, N, Np, pd, seeds.get(SITE_ATTN, 0), precision=_rp("pv", prec))
         del QKV2, rowpart, ws
     else:
         Pd, O = _attn_split(Q, Kt, V, N, Np, dp, pd, seeds, prec, att, dev)

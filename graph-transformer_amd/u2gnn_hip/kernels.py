@@ -428,7 +428,8 @@ def attn_softmax_pv_ws_floats(n_valid, rows_pad, dp):
 def attn_softmax_pv(S, lds, rowpart, ngroups, qkv2, ldq2, dp, Pd, ldp, O, ldo, ws, n_valid, rows_pad, p, seed,
                     precision="bf16x3"):
     """ABI v10: signed probability image Pd and O = dropout(P) V from the scores S, the EPI_STORE_ROWSTAT
-    row partials ``rowpart`` (float32 [rows, >= 2*ngroups]) and the x2 in-projection output qkv2 (bfloat16)."""
+    row partials ``rowpart`` (float32 [rows, >= 2*ngroups]) and the x2 in-projection output qkv2 (bfloat16); with
+    precision "bf16x6" (ABI v17) qkv2 is the fp32 in-projection output and ldq2 its row length in floats."""
     _dev(S, rowpart, qkv2, Pd, O, ws)
     check(hip_lib().u2gnn_attn_softmax_pv(_p(S), int(lds), _p(rowpart), int(rowpart.stride(0)) // 2, int(ngroups),
                                           _p(qkv2), int(ldq2), int(dp), _p(Pd), int(ldp), _p(O), int(ldo), _p(ws),

@@ -414,7 +414,9 @@ int u2gnn_index_zero_rows(const int64_t *idx, int64_t n_rows, float *dst, int64_
  * keep(seed, m, n) (the hash of every dropout site); it writes the signed image Pd = keep ? P/(1-p) : -P
  * (zero for padded rows / keys; what EPI_ATTN_DS_SIGNED and the clamped P^T.dO read) and
  * O = Pd_kept . V on the matrix cores (precision BF16X3: split-bf16, 3 products; BF16: 1), V read from qkv2
- * (the in-projection output in x2 format, [rows_pad][ldq2] bf16, V = columns 2dp .. 3dp).  dp in {64, 128,
+ * (the in-projection output in x2 format, [rows_pad][ldq2] bf16, V = columns 2dp .. 3dp).  ABI v17, precision
+ * BF16X6: qkv2 is the fp32 in-projection output itself ([rows_pad][ldq2] float, ldq2 >= 3 dp, V = columns
+ * 2dp .. 3dp), P and V split three ways in registers, 6 products (fp32-accurate).  dp in {64, 128,
  * ..., 384}, rows_pad % 128 == 0, ngroups and ld_rowpart even, rowpart 16-byte aligned; S columns >= n_valid
  * hold -inf (as EPI_STORE_ROWSTAT writes them); S and Pd may alias (the image is written over the scores).
  * ws: u2gnn_attn_softmax_pv_ws_floats(n_valid, rows_pad, dp) floats (per key range partial outputs). */

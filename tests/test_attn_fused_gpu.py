@@ -142,3 +142,41 @@ def test_softmax_pv_rejects_bad_shapes():
         K.attn_softmax_pv(S, Np, rp, 3, Q2, 6 * dp, dp, S, Np, O, dp, ws, N, Np, 0.5, 1)
     with pytest.raises(_lib.U2GNNNativeError):   # fp32 is the split path's precision
         K.attn_softmax_pv(S, Np, rp, G, Q2, 6 * dp, dp, S, Np, O, dp, ws, N, Np, 0.5, 1, precision="fp32")
+
+
+@pytest.mark.parametrize("Np,N,dp", [(256, 230, 64), (128, 100, 384), (1280, 1100, 128), (512, 500, 384),
+                                     (2048, 1999, 192), (4864, 4776, 384), (384, 257, 256), (640, 640, 320)])
+@pytest.mark.parametrize("p", [0.5, 0.0])
+def test_softmax_pv_bf16x6(Np, N, dp, p):
+    """ABI v17 BF16X6: V straight from the fp32 in-projection output (ldq2 = 3 dp floats), P and V split three
+    ways in registers: O within fp32 rounding of the fp64 reference (an order below bf16x3's), and the signed
+    image bit for bit the bf16x3 kernel's (the same P and keep decisions)."""
+    seed = 4242
+    S = _mk(Np, Np, seed=7, scale=2.0)
+    S[:, N:] = float("-inf")
+    V = _mk(Np, dp, seed=9)
+    rp = _partials(S, N, Np)
+    rs = _ref_rowstat(S, N, Np)
+    QKV = _mk(Np, 3 * dp, seed=11)
+    QKV[:, 2 * dp:] = V
+    ws = torch.empty(K.attn_softmax_pv_ws_floats(N, Np, dp), device=DEV)
+    X6, O6 = S.clone(), torch.full((Np, dp), float("nan"), device=DEV)
+    K.attn_softmax_pv(X6, Np, rp, Np // 64, QKV, 3 * dp, dp, X6, Np, O6, dp, ws, N, Np, p, seed, precision="bf16x6")
+    X3, O3 = S.clone(), torch.full((Np, dp), float("nan"), device=DEV)
+    K.attn_softmax_pv(X3, Np, rp, Np // 64, _qkv2(V, Np, dp), 6 * dp, dp, X3, Np, O3, dp, ws, N, Np, p, seed,
+                      precision="bf16x3")
+    torch.cuda.synchronize()
+    assert torch.equal(X6, X3)
+    s = S[:N, :N].double()
+    P = torch.exp(s - rs[:N, 0:1]) * rs[:N, 1:2]
+    keep = K.dropout_mask(seed, Np, Np, p).bool()[:N, :N] if p > 0 else torch.ones_like(P, dtype=torch.bool)
+    img = torch.where(keep, P / (1.0 - p), -P)
+    # the reference from the kernel's own fp32 image (P carries exp2 / rounding of its own): the products' error only
+    O_ref = X6[:N, :N].double().clamp_min(0) @ V[:N].double()
+    O_ref_p = img.clamp_min(0) @ V[:N].double()
+    e6 = ((O6[:N].double() - O_ref).abs().max() / O_ref.abs().max()).item()
+    e3 = ((O3[:N].double() - O_ref).abs().max() / O_ref.abs().max()).item()
+    assert e6 < 1e-6, e6
+    assert e6 * 4 < e3, (e6, e3)
+    assert ((O6[:N].double() - O_ref_p).abs().max() / O_ref_p.abs().max()).item() < 2e-6
+    assert (O6[N:] == 0).all()

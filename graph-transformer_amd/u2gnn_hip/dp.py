@@ -19,11 +19,84 @@ in rank order: the dense all-reduce's result at a fraction of its bytes.
 """
 from __future__ import annotations
 
+import atexit
 import contextlib
+import ctypes
+import os
 from typing import Dict, List, Optional, Tuple
 
 import numpy as np
 import torch
+
+
+class _UniqueId(ctypes.Structure):
+    _fields_ = [("internal", ctypes.c_char * 128)]   # ncclUniqueId (rccl.h: NCCL_UNIQUE_ID_BYTES)
+
+
+_NCCL_FLOAT32, _NCCL_SUM, _NCCL_AVG = 7, 0, 4
+
+
+class RcclComm:
+    """An RCCL communicator of the process group's ranks, driven directly through torch's own librccl (ctypes):
+    ncclAllReduce is enqueued on the stream that wrote the gradients, in its order -- no c10d work objects and no
+    event hand-offs between that stream, an RCCL stream and the main stream.  (Through c10d each collective
+    recorded and waited on events -- system-scope releases on this ROCm -- and the overlapped all-reduce cost
+    +2.7 % of the C4 step at one rank with no reduction kernel at all; profiles/r06/dp_overhead_ab.txt.)  The
+    unique id travels over the existing process group once, at construction."""
+
+    def __init__(self, group=None):
+        import torch.distributed as dist
+        self.lib = ctypes.CDLL(os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so"))
+        self.lib.ncclGetErrorString.restype = ctypes.c_char_p
+        self.lib.ncclAllReduce.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
+                                           ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+        self.world, rank = dist.get_world_size(group), dist.get_rank(group)
+        uid = _UniqueId()
+        if rank == 0:
+            self._check(self.lib.ncclGetUniqueId(ctypes.byref(uid)), "ncclGetUniqueId")
+        dev = torch.device("cuda", torch.cuda.current_device())
+        t = torch.frombuffer(bytearray(ctypes.string_at(ctypes.addressof(uid), 128)), dtype=torch.uint8).to(dev)
+        dist.broadcast(t, dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+        raw = bytes(t.cpu().numpy().tobytes())
+        ctypes.memmove(ctypes.addressof(uid), raw, 128)
+        self.comm = ctypes.c_void_p()
+        self._check(self.lib.ncclCommInitRank(ctypes.byref(self.comm), self.world, uid, rank), "ncclCommInitRank")
+        atexit.register(self.close)
+
+    def _check(self, rc: int, what: str) -> None:
+        if rc != 0:
+            raise RuntimeError(f"{what}: {self.lib.ncclGetErrorString(rc).decode()} ({rc})")
+
+    def all_reduce(self, t: torch.Tensor, average: bool, stream: Optional["torch.cuda.Stream"] = None) -> None:
+        """In place over the contiguous fp32 tensor t, on `stream` (default: the current one)."""
+        st = stream if stream is not None else torch.cuda.current_stream()
+        op = _NCCL_AVG if average else _NCCL_SUM
+        self._check(self.lib.ncclAllReduce(ctypes.c_void_p(t.data_ptr()), ctypes.c_void_p(t.data_ptr()), t.numel(),
+                                           _NCCL_FLOAT32, op, self.comm, ctypes.c_void_p(st.cuda_stream)),
+                    "ncclAllReduce")
+
+    def close(self) -> None:
+        if self.comm:
+            self.lib.ncclCommDestroy(self.comm)
+            self.comm = ctypes.c_void_p()
+
+
+_NATIVE_RCCL = [os.environ.get("U2GNN_NATIVE_RCCL", "1") != "0"]   # (env: the c10d path for A/B only)
+
+
+def native_rccl() -> bool:
+    return _NATIVE_RCCL[0]
+
+
+def _avg_op(dist, group):
+    """ReduceOp.AVG where it pays: RCCL with more than one rank (ncclAvg pre-multiplies 1/world inside the ring
+    reduction, so no separate scaling pass over the gradient buffer), else None -- SUM and the callers scale by
+    1/world only when world > 1.  (At one rank SUM in place launches nothing while AVG runs RCCL's one-rank
+    pre-multiply kernel over every bucket: 5 x 14 us per C4 step, profiles/r06/dp_overhead_ab.txt.)"""
+    try:
+        return dist.ReduceOp.AVG if dist.get_backend(group) == "nccl" and dist.get_world_size(group) > 1 else None
+    except (RuntimeError, ValueError):
+        return None
 
 
 def rank_batches(loader, world: int, rank: int, n_steps: int) -> List:
@@ -47,15 +120,18 @@ class GradAllReduce:
         self.group = group
         self.world = dist.get_world_size(group)
         self.bucket = max(1, int(bucket_mb * (1 << 20) // 4))
+        self.avg = _avg_op(dist, group)
 
     def __call__(self, flat) -> None:
         g = flat.gflat
         handles = []
+        op = self.avg if self.avg is not None else self.dist.ReduceOp.SUM
         for o in range(0, g.numel(), self.bucket):
-            handles.append(self.dist.all_reduce(g[o:o + self.bucket], group=self.group, async_op=True))
+            handles.append(self.dist.all_reduce(g[o:o + self.bucket], op=op, group=self.group, async_op=True))
         for h in handles:
             h.wait()
-        g.mul_(1.0 / self.world)
+        if self.avg is None and self.world > 1:
+            g.mul_(1.0 / self.world)
 
 
 class OverlappedGradAllReduce:
@@ -69,6 +145,10 @@ class OverlappedGradAllReduce:
 
     Wiring: ``stack.grad_ready = ar.layer_done`` (EncoderStack calls it with the layer's
     parameter-name prefix and the stream that wrote its gradients) and ``trainer.grad_sync = ar``.
+
+    With RCCL (round 6) the collectives go straight to librccl (RcclComm) on the stream that wrote the region
+    -- the side stream, which the backward joins before the optimizer -- and the head's regions on the main
+    stream: no c10d events, and ncclAvg instead of the scaling pass at world > 1.  gloo keeps the c10d form.
     """
 
     def __init__(self, flat, group=None):
@@ -85,6 +165,12 @@ class OverlappedGradAllReduce:
             self.span[name] = (lo, lo + g.numel())
         self.pending: List = []
         self.launched: List[Tuple[int, int]] = []
+        # RCCL: the average inside the collective (ncclAvg) -- no scaling pass over the 20.7 MB buffer at the
+        # step's end; gloo: sum, then the scaling pass
+        self.avg = _avg_op(dist, group)
+        self.op = self.avg if self.avg is not None else dist.ReduceOp.SUM
+        # RCCL: the collectives issued natively, in the order of the streams that wrote the gradients
+        self.rccl = RcclComm(group) if dist.get_backend(group) == "nccl" and native_rccl() else None
 
     def region(self, prefix: str) -> Tuple[int, int]:
         """Element range [lo, hi) of the parameters named prefix*, which must be contiguous."""
@@ -106,9 +192,13 @@ class OverlappedGradAllReduce:
     def layer_done(self, prefix: str, stream: Optional["torch.cuda.Stream"] = None) -> None:
         lo, hi = self.region(prefix)
         g = self.flat.gflat
+        if self.rccl is not None:   # on the gradients' own stream: it is joined by the backward's end
+            self.rccl.all_reduce(g[lo:hi], self.avg is not None, stream)
+            self.launched.append((lo, hi))
+            return
         ctx = torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
         with ctx:
-            self.pending.append(self.dist.all_reduce(g[lo:hi], group=self.group, async_op=True))
+            self.pending.append(self.dist.all_reduce(g[lo:hi], op=self.op, group=self.group, async_op=True))
         self.launched.append((lo, hi))
 
     def __call__(self, flat) -> None:
@@ -116,13 +206,17 @@ class OverlappedGradAllReduce:
         o = 0
         for lo, hi in sorted(self.launched) + [(g.numel(), g.numel())]:
             if lo > o:   # a region no layer_done covered (head parameters, padding)
-                self.pending.append(self.dist.all_reduce(g[o:lo], group=self.group, async_op=True))
+                if self.rccl is not None:
+                    self.rccl.all_reduce(g[o:lo], self.avg is not None)
+                else:
+                    self.pending.append(self.dist.all_reduce(g[o:lo], op=self.op, group=self.group, async_op=True))
             o = max(o, hi)
         for h in self.pending:
             h.wait()
         self.pending.clear()
         self.launched.clear()
-        g.mul_(1.0 / self.world)
+        if self.avg is None and self.world > 1:
+            g.mul_(1.0 / self.world)
 
 
 def broadcast_params(flat, src: int = 0, group=None) -> None:
@@ -173,10 +267,12 @@ class UnSupGradSync:
     def __call__(self, flat) -> None:
         g = flat.gflat
         regions = [(0, self.lo), (self.hi, g.numel())]
+        avg = _avg_op(self.dist, self.group)
         for a, b in regions:
             if b > a:
-                self.dist.all_reduce(g[a:b], group=self.group)
-                g[a:b].mul_(1.0 / self.world)
+                self.dist.all_reduce(g[a:b], op=avg if avg is not None else self.dist.ReduceOp.SUM, group=self.group)
+                if avg is None and self.world > 1:
+                    g[a:b].mul_(1.0 / self.world)
 
     def _flat(self, kind: str, rows: int, D: int, device) -> torch.Tensor:
         """[2 * rows + rows * D] float32: the ids (int64 bits) then the rows, one all-gather per kind."""

@@ -26,6 +26,14 @@ import time
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path[:0] = [os.path.join(REPO, "graph-transformer_amd"), REPO]
 
+if int(os.environ.get("WORLD_SIZE", "1")) > 1 or "--force-dist" in sys.argv:
+    # a process-group rank: 16 HIP hardware queues, so that RCCL's streams do not share the main / side streams'
+    # queues (C4 at one rank, overlapped all-reduce: +2.2 % over no process group with 16, +2.6-3.4 % with 8;
+    # profiles/r06/dp_overhead_ab.txt).  Before the HIP runtime starts.
+    _q = os.environ.get("GPU_MAX_HW_QUEUES", "")
+    if not _q.isdigit() or int(_q) < 16:
+        os.environ["GPU_MAX_HW_QUEUES"] = "16"
+
 import u2gnn_hip  # noqa: E402,F401  (before the HIP runtime starts: GPU_MAX_HW_QUEUES, see ensure_hw_queues)
 import numpy as np  # noqa: E402
 import torch  # noqa: E402

@@ -19,73 +19,11 @@ in rank order: the dense all-reduce's result at a fraction of its bytes.
 """
 from __future__ import annotations
 
-import atexit
 import contextlib
-import ctypes
-import os
 from typing import Dict, List, Optional, Tuple
 
 import numpy as np
 import torch
-
-
-class _UniqueId(ctypes.Structure):
-    _fields_ = [("internal", ctypes.c_char * 128)]   # ncclUniqueId (rccl.h: NCCL_UNIQUE_ID_BYTES)
-
-
-_NCCL_FLOAT32, _NCCL_SUM, _NCCL_AVG = 7, 0, 4
-
-
-class RcclComm:
-    """An RCCL communicator of the process group's ranks, driven directly through torch's own librccl (ctypes):
-    ncclAllReduce is enqueued on the stream that wrote the gradients, in its order -- no c10d work objects and no
-    event hand-offs between that stream, an RCCL stream and the main stream.  (Through c10d each collective
-    recorded and waited on events -- system-scope releases on this ROCm -- and the overlapped all-reduce cost
-    +2.7 % of the C4 step at one rank with no reduction kernel at all; profiles/r06/dp_overhead_ab.txt.)  The
-    unique id travels over the existing process group once, at construction."""
-
-    def __init__(self, group=None):
-        import torch.distributed as dist
-        self.lib = ctypes.CDLL(os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so"))
-        self.lib.ncclGetErrorString.restype = ctypes.c_char_p
-        self.lib.ncclAllReduce.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
-                                           ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
-        self.world, rank = dist.get_world_size(group), dist.get_rank(group)
-        uid = _UniqueId()
-        if rank == 0:
-            self._check(self.lib.ncclGetUniqueId(ctypes.byref(uid)), "ncclGetUniqueId")
-        dev = torch.device("cuda", torch.cuda.current_device())
-        t = torch.frombuffer(bytearray(ctypes.string_at(ctypes.addressof(uid), 128)), dtype=torch.uint8).to(dev)
-        dist.broadcast(t, dist.get_global_rank(group, 0) if group is not None else 0, group=group)
-        raw = bytes(t.cpu().numpy().tobytes())
-        ctypes.memmove(ctypes.addressof(uid), raw, 128)
-        self.comm = ctypes.c_void_p()
-        self._check(self.lib.ncclCommInitRank(ctypes.byref(self.comm), self.world, uid, rank), "ncclCommInitRank")
-        atexit.register(self.close)
-
-    def _check(self, rc: int, what: str) -> None:
-        if rc != 0:
-            raise RuntimeError(f"{what}: {self.lib.ncclGetErrorString(rc).decode()} ({rc})")
-
-    def all_reduce(self, t: torch.Tensor, average: bool, stream: Optional["torch.cuda.Stream"] = None) -> None:
-        """In place over the contiguous fp32 tensor t, on `stream` (default: the current one)."""
-        st = stream if stream is not None else torch.cuda.current_stream()
-        op = _NCCL_AVG if average else _NCCL_SUM
-        self._check(self.lib.ncclAllReduce(ctypes.c_void_p(t.data_ptr()), ctypes.c_void_p(t.data_ptr()), t.numel(),
-                                           _NCCL_FLOAT32, op, self.comm, ctypes.c_void_p(st.cuda_stream)),
-                    "ncclAllReduce")
-
-    def close(self) -> None:
-        if self.comm:
-            self.lib.ncclCommDestroy(self.comm)
-            self.comm = ctypes.c_void_p()
-
-
-_NATIVE_RCCL = [os.environ.get("U2GNN_NATIVE_RCCL", "1") != "0"]   # (env: the c10d path for A/B only)
-
-
-def native_rccl() -> bool:
-    return _NATIVE_RCCL[0]
 
 
 def _avg_op(dist, group):
@@ -146,12 +84,13 @@ class OverlappedGradAllReduce:
     Wiring: ``stack.grad_ready = ar.layer_done`` (EncoderStack calls it with the layer's
     parameter-name prefix and the stream that wrote its gradients) and ``trainer.grad_sync = ar``.
 
-    With RCCL (round 6) the collectives go straight to librccl (RcclComm) on the stream that wrote the region
-    -- the side stream, which the backward joins before the optimizer -- and the head's regions on the main
-    stream: no c10d events, and ncclAvg instead of the scaling pass at world > 1.  gloo keeps the c10d form.
+    RCCL at world > 1: ncclAvg (the 1/world folded into the ring reduction) instead of the scaling pass.  (Measured
+    and not kept, round 6: the collectives issued straight to torch's librccl through ctypes on the gradients' own
+    stream, no c10d events -- 4.82 vs 3.36 ms per C4 step at one rank, the host blocked ~190 us in each call;
+    profiles/r06/dp_overhead_ab.txt.)
     """
 
-    def __init__(self, flat, group=None):
+    def __init__(self, flat, group=None, bucket_mb: float = 4.0, layer_prefix: str = "u2gnn_layers."):
         import torch.distributed as dist
         self.dist = dist
         self.group = group
@@ -165,12 +104,26 @@ class OverlappedGradAllReduce:
             self.span[name] = (lo, lo + g.numel())
         self.pending: List = []
         self.launched: List[Tuple[int, int]] = []
+        # Adjacent layer regions go out together until a bucket holds >= bucket_mb; the backward visits the layers in
+        # descending flat order, so each new region ends where the bucket begins.  The parameters after the last
+        # layer (the head, written before the encoder backward starts) join the first bucket.  Default 4 MB: every
+        # C4 layer (5.2 MB) its own collective -- at one rank 2 buckets of 2 layers measured the same as 5
+        # collectives (+74 vs +72-85 us over no process group, profiles/r06/dp_overhead_ab.txt), and at N ranks a
+        # smaller last bucket is less exposed after the backward.
+        self.bucket = max(1, int(bucket_mb * (1 << 20) // 4))
+        layers = {n[:n.index(".layers.") + len(".layers.")] + n.split(".layers.")[1].split(".")[0]
+                  for n in flat.names if n.startswith(layer_prefix) and ".layers." in n}
+        self.n_layers = len(layers)
+        enc_hi = max((b for n, (a, b) in self.span.items() if n.startswith(layer_prefix)), default=0)
+        self.tail = (self._align_end(enc_hi), flat.gflat.numel())   # [head parameters, end)
+        self.acc: Optional[Tuple[int, int]] = None
+        self.acc_stream = None
+        self.calls = 0
         # RCCL: the average inside the collective (ncclAvg) -- no scaling pass over the 20.7 MB buffer at the
         # step's end; gloo: sum, then the scaling pass
         self.avg = _avg_op(dist, group)
         self.op = self.avg if self.avg is not None else dist.ReduceOp.SUM
-        # RCCL: the collectives issued natively, in the order of the streams that wrote the gradients
-        self.rccl = RcclComm(group) if dist.get_backend(group) == "nccl" and native_rccl() else None
+
 
     def region(self, prefix: str) -> Tuple[int, int]:
         """Element range [lo, hi) of the parameters named prefix*, which must be contiguous."""
@@ -189,27 +142,37 @@ class OverlappedGradAllReduce:
         nxt = [a for a, _ in self.span.values() if a >= hi]
         return min(nxt) if nxt else self.flat.gflat.numel()
 
-    def layer_done(self, prefix: str, stream: Optional["torch.cuda.Stream"] = None) -> None:
-        lo, hi = self.region(prefix)
+    def _issue(self, lo: int, hi: int, stream) -> None:
         g = self.flat.gflat
-        if self.rccl is not None:   # on the gradients' own stream: it is joined by the backward's end
-            self.rccl.all_reduce(g[lo:hi], self.avg is not None, stream)
-            self.launched.append((lo, hi))
-            return
         ctx = torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
         with ctx:
             self.pending.append(self.dist.all_reduce(g[lo:hi], op=self.op, group=self.group, async_op=True))
         self.launched.append((lo, hi))
 
+    def layer_done(self, prefix: str, stream: Optional["torch.cuda.Stream"] = None) -> None:
+        lo, hi = self.region(prefix)
+        self.calls += 1
+        if self.acc is None and self.calls == 1 and hi == self.tail[0] and self.tail[1] > self.tail[0]:
+            hi = self.tail[1]   # the head's gradients: complete before the encoder backward, adjacent
+        if self.acc is not None and hi != self.acc[0]:   # not adjacent: send what is held
+            self._issue(*self.acc, self.acc_stream)
+            self.acc = None
+        self.acc = (lo, self.acc[1] if self.acc is not None else hi)
+        self.acc_stream = stream   # ordered after every earlier write (the side stream forks from the main one)
+        if self.acc[1] - self.acc[0] >= self.bucket or self.calls >= self.n_layers:
+            self._issue(*self.acc, self.acc_stream)
+            self.acc = None
+
     def __call__(self, flat) -> None:
         g = flat.gflat
+        if self.acc is not None:   # (a backward that visited fewer layers than the stack holds)
+            self._issue(*self.acc, self.acc_stream)
+            self.acc = None
+        self.calls = 0
         o = 0
         for lo, hi in sorted(self.launched) + [(g.numel(), g.numel())]:
             if lo > o:   # a region no layer_done covered (head parameters, padding)
-                if self.rccl is not None:
-                    self.rccl.all_reduce(g[o:lo], self.avg is not None)
-                else:
-                    self.pending.append(self.dist.all_reduce(g[o:lo], op=self.op, group=self.group, async_op=True))
+                self.pending.append(self.dist.all_reduce(g[o:lo], op=self.op, group=self.group, async_op=True))
             o = max(o, hi)
         for h in self.pending:
             h.wait()

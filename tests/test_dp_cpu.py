@@ -52,13 +52,20 @@ def _worker(rank, world, port, out_dir):
     GradAllReduce(bucket_mb=0.001)(f2)
     g_after = f2.gflat.clone()
     f2.gflat.copy_(mine_g)
-    ar = OverlappedGradAllReduce(f2)
-    for l in reversed(range(2)):
-        for t in reversed(range(2)):
-            ar.layer_done(f"u2gnn_layers.{l}.layers.{t}.")
-    ar(f2)
-    assert torch.equal(f2.gflat, g_after)
-    assert not ar.pending and not ar.launched
+    # buckets of adjacent layers (round 6): one bucket for this small model (the default 9 MB), a bucket per layer
+    # (tiny), and every layer pair; the head joins the first bucket; twice each (the step resets the counters)
+    for mb in (9.0, 1e-5, 0.02):
+        ar = OverlappedGradAllReduce(f2, bucket_mb=mb)
+        for rep in range(2):
+            f2.gflat.copy_(mine_g)
+            for l in reversed(range(2)):
+                for t in reversed(range(2)):
+                    ar.layer_done(f"u2gnn_layers.{l}.layers.{t}.")
+            n_coll = len(ar.pending)
+            ar(f2)
+            assert torch.equal(f2.gflat, g_after), mb
+            assert not ar.pending and not ar.launched
+            assert n_coll == {9.0: 1, 1e-5: 4}.get(mb, n_coll), (mb, n_coll)
     np.savez(os.path.join(out_dir, f"r{rank}.npz"), g=flat.gflat.numpy(), p=flat.flat.numpy(),
              ix=np.concatenate([x.input_x.ravel() for x in mine]))
     dist.destroy_process_group()

@@ -26,6 +26,20 @@
 
 #include "u2gnn_common.h"
 
+// Phase stamps of the fused kernels (experiment builds only: -DSX_STAMPS, tools/sl_stamps.py): thread 0 of a
+// workgroup records the constant-rate wall clock (100 MHz) at phase boundaries; read back by u2gnn_dbg_sx_stamps.
+#ifdef SX_STAMPS
+__device__ unsigned long long g_sx_stamps[2][4096][16];
+#define SX_STAMP(kern, k)                                                                                            \
+    do {                                                                                                           \
+        if (threadIdx.x == 0 && blockIdx.x < 4096) g_sx_stamps[kern][blockIdx.x][k] = (unsigned long long)wall_clock64(); \
+    } while (0)
+#else
+#define SX_STAMP(kern, k) \
+    do {                  \
+    } while (0)
+#endif
+
 namespace {
 
 constexpr int SA_WAVES = 8;    // rows (forward, dQ) or key rows (dK / dV) per 512-thread workgroup
@@ -35,6 +49,10 @@ constexpr int SA_NT = 64 * SA_WAVES;
 template <int DM> constexpr int sa_kt_f() { return 4096 / DM > 256 ? 4096 / DM / 256 * 256 : 256; }   // 128-key rounds per wave
 template <int DM> constexpr int sa_kt_b() { return 2048 / DM > 128 ? 2048 / DM / 128 * 128 : 128; }   // 64-query rounds per wave
 constexpr float SA_LOG2E = 1.4426950408889634f;
+// 2^x as one v_exp_f32: exp2f adds a 6-instruction rescue of results below 2^-126 (round 6: the walks are
+// VALU-issue-bound, SQ_INSTS_VALU); softmax terms that small are flushed to 0 -- they are below fp32 resolution of
+// the row sums they would join (every row sum holds its maximum term, exp2(0) = 1).  exp2(-inf) = 0 as before.
+__device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
 // waves per SIMD the register budget is sized for: 4 (128 VGPRs) up to DM = 16, 2 (256) beyond, where the row's
 // q, o / dq / dk, dv arrays alone take 2-3 DM registers (the 128 cap spilled them to scratch)
 template <int DM> constexpr int sa_min_waves() { return DM <= 12 ? 4 : 2; }
@@ -116,11 +134,16 @@ __device__ __forceinline__ float lane_col(const float (&x)[DM], int c) {
 constexpr int SA_SPL = 2, SA_RB = SA_WAVES / SA_SPL;
 
 // Staging of records [t0, t0 + KT) of a compact [Np][W] array (W = WA + WB + WC, each a multiple of 4) into the
-// LDS arrays a [KT][WA], b [KT][WB], c [KT][WC]; records at or past Np are zeros.  In two halves: tile_load
+// LDS arrays a [KT][WA], b [KT][WB], c [KT][WC]; records at or past Np are zeros.  PS (pair split): record t goes to
+// row ps_row(t) = (t & 1) KT / 2 + t / 2, so a lane walking the key pair (2 c, 2 c + 1) with c = base + lane reads
+// two rows that are consecutive across the lanes (16-byte stride at DM = 4: no LDS bank conflicts; the natural
+// order put the lanes 32 bytes apart).  In two halves: tile_load
 // issues every global load of the tile into registers (SA_PER float4 per thread, all in flight together) and
 // tile_store writes them to LDS -- so the next tile's loads run under this tile's compute, and a tile costs one
 // load latency instead of one per loop iteration (a load -> ds_write loop waits on every load).
-template <int KT, int WA, int WB, int WC>
+template <int KT> __device__ __forceinline__ int ps_row(int t) { return (t & 1) * (KT / 2) + (t >> 1); }
+
+template <int KT, int WA, int WB, int WC, bool PS = false>
 struct Tile {
     static constexpr int W4 = (WA + WB + WC) / 4, NE = KT * W4, PER = (NE + SA_NT - 1) / SA_NT;
     float4 v[PER];
@@ -137,7 +160,7 @@ struct Tile {
         for (int i = 0; i < PER; ++i) {
             const int e = threadIdx.x + i * SA_NT;
             if (e >= NE) break;
-            const int t = e / W4, k = 4 * (e % W4);
+            const int t = PS ? ps_row<KT>(e / W4) : e / W4, k = 4 * (e % W4);
             if (k < WA) *reinterpret_cast<float4 *>(&a[t][k]) = v[i];
             else if (k < WA + WB) *reinterpret_cast<float4 *>(&b[t][k - WA]) = v[i];
             else *reinterpret_cast<float4 *>(c + t * WC + k - WA - WB) = v[i];
@@ -221,15 +244,18 @@ __global__ void __launch_bounds__(SA_NT, sa_min_waves<DM>()) sa_fwd_kernel(SaP P
     const bool drop = P.p > 0.f;
     const uint32_t thr = u2gnn_keep_thr(P.p), rk = u2gnn_row_key(seed, (uint32_t)i);
     float m = -INFINITY, l = 0.f;
-    Tile<SA_KT, DM, DM, 0> tl;
+    if (TAIL) SX_STAMP(0, 0);
+    Tile<SA_KT, DM, DM, 0, true> tl;
     tl.load(kvc, 0, P.Np);
     for (int t0 = 0; t0 < P.N; t0 += SA_KT) {
         __syncthreads();
         tl.store(ks, vs, nullptr);
         __syncthreads();
+        if (TAIL && t0 == 0) SX_STAMP(0, 1);
         if (t0 + SA_KT < P.N) tl.load(kvc, t0 + SA_KT, P.Np);   // the next tile, in flight under this one
         if (!live) continue;
-        // this wave's keys of the tile: pairs (t0 + sp PART + 128 h + 2 lane, +1); CU / 2 pairs per rescale
+        // this wave's keys of the tile: pairs (t0 + sp PART + 128 h + 2 lane, +1), LDS rows ps_row; CU / 2 pairs per
+        // rescale
 #pragma unroll 1
         for (int h0 = 0; h0 < NP; h0 += CU / 2) {
             float s[CU];
@@ -237,13 +263,13 @@ __global__ void __launch_bounds__(SA_NT, sa_min_waves<DM>()) sa_fwd_kernel(SaP P
 #pragma unroll
             for (int u = 0; u < CU; ++u) {
                 const int t = sp * PART + 128 * (h0 + u / 2) + 2 * lane + (u & 1);
-                const float x = dot_lds<DM>(q, ks[t]) * SA_LOG2E;   // rows past N are zeros: finite
+                const float x = dot_lds<DM>(q, ks[ps_row<SA_KT>(t)]) * SA_LOG2E;   // rows past N are zeros: finite
                 s[u] = (h0 + u / 2 < NP && t0 + t < P.N) ? x : -INFINITY;
                 cm = fmaxf(cm, s[u]);
             }
             if (cm == -INFINITY) continue;   // none of this lane's keys in the chunk
             const float mn = fmaxf(m, cm);
-            const float sc = exp2f(m - mn);  // m = -inf: 0
+            const float sc = fexp2(m - mn);  // m = -inf: 0
             l *= sc;
 #pragma unroll
             for (int c = 0; c < DM; ++c) o[c] *= sc;
@@ -255,28 +281,25 @@ __global__ void __launch_bounds__(SA_NT, sa_min_waves<DM>()) sa_fwd_kernel(SaP P
                     const uint32_t hh = u2gnn_pair_hash(rk, (uint32_t)(t0 + t) >> 1);
                     k0 = u2gnn_keep_lo(hh, thr), k1 = u2gnn_keep_hi(hh, thr);
                 }
-                const float e0 = exp2f(s[u] - mn), e1 = exp2f(s[u + 1] - mn);   // 0 past N
+                const float e0 = fexp2(s[u] - mn), e1 = fexp2(s[u + 1] - mn);   // 0 past N
                 l += e0 + e1;
                 const float a0 = k0 ? e0 : 0.f, a1 = k1 ? e1 : 0.f;
-                const int tt = h0 + u / 2 < NP ? t : 0;   // (a0 = a1 = 0 there)
+                const int tt = ps_row<SA_KT>(h0 + u / 2 < NP ? t : 0);   // (a0 = a1 = 0 there)
 #pragma unroll
-                for (int c = 0; c < DM; ++c) o[c] = fmaf(a1, vs[tt + 1][c], fmaf(a0, vs[tt][c], o[c]));
+                for (int c = 0; c < DM; ++c) o[c] = fmaf(a1, vs[tt + SA_KT / 2][c], fmaf(a0, vs[tt][c], o[c]));
             }
             m = mn;
         }
     }
-    // butterfly merge of the 64 lanes' (m, l, o): every lane ends with the same values
+    if (TAIL) SX_STAMP(0, 2);
+    // merge of the 64 lanes' (m, l, o): the wave's maximum first, each lane rescales to it once, then plain
+    // butterfly sums (one exp per lane instead of two per butterfly level); every lane ends with the same values
+    {
+        const float M = wave_max(m);
+        const float f = m == -INFINITY ? 0.f : fexp2(m - M);   // (M = -inf only with every lane empty)
+        l = wave_sum(l * f);
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        const float m2 = __shfl_xor(m, off, 64), l2 = __shfl_xor(l, off, 64);
-        const float M = fmaxf(m, m2);
-        const float f1 = m == -INFINITY ? 0.f : exp2f(m - M), f2 = m2 == -INFINITY ? 0.f : exp2f(m2 - M);
-        l = l * f1 + l2 * f2;
-#pragma unroll
-        for (int c = 0; c < DM; ++c) {
-            const float o2 = __shfl_xor(o[c], off, 64);
-            o[c] = o[c] * f1 + o2 * f2;
-        }
+        for (int c = 0; c < DM; ++c) o[c] = wave_sum(o[c] * f);
         m = M;
     }
     // then the row's SA_SPL waves, in wave order
@@ -287,6 +310,7 @@ __global__ void __launch_bounds__(SA_NT, sa_min_waves<DM>()) sa_fwd_kernel(SaP P
         for (int c = 0; c < DM; ++c) xw[rw][sp][2 + c] = o[c];
     }
     __syncthreads();
+    if (TAIL) SX_STAMP(0, 3);
     const bool fin = sp == 0 && i < P.Np;   // the row's finishing wave
     if (!TAIL && !fin) return;
     float of[DM];   // fin: the row of O
@@ -302,7 +326,7 @@ __global__ void __launch_bounds__(SA_NT, sa_min_waves<DM>()) sa_fwd_kernel(SaP P
         if (M != -INFINITY) {
 #pragma unroll
             for (int x = 0; x < SA_SPL; ++x) {
-                const float f = xw[rw][x][0] == -INFINITY ? 0.f : exp2f(xw[rw][x][0] - M);
+                const float f = xw[rw][x][0] == -INFINITY ? 0.f : fexp2(xw[rw][x][0] - M);
                 L = fmaf(xw[rw][x][1], f, L);
 #pragma unroll
                 for (int c = 0; c < DM; ++c) o[c] = fmaf(xw[rw][x][2 + c], f, o[c]);
@@ -321,8 +345,10 @@ __global__ void __launch_bounds__(SA_NT, sa_min_waves<DM>()) sa_fwd_kernel(SaP P
         }
     }
     if constexpr (TAIL) {
+        SX_STAMP(0, 4);
         __shared__ __attribute__((aligned(16))) float tsm[tail_smem_floats<DM>()];
         tail_fwd_rows<DM>(T, i, rw, sp, of, fin, tsm);
+        SX_STAMP(0, 9);
     }
 }
 
@@ -347,8 +373,10 @@ __global__ void __launch_bounds__(SA_NT, sa_min_waves<DM>()) sa_bwd_q_kernel(SaP
 #pragma unroll
     for (int c = 0; c < DM; ++c) q[c] = g[c] = dq[c] = 0.f;
     if constexpr (TAIL) {   // dO and delta of the row from the tail backward (every wave of the row)
+        SX_STAMP(1, 0);
         __shared__ __attribute__((aligned(16))) float tsm[tail_smem_floats<DM>()];
         tail_bwd_rows<DM>(T, i, rw, sp, sp == 0 && i < P.Np, g, dl, tsm);
+        SX_STAMP(1, 1);
     }
     if (live) {
         load_row<DM>(sa_qc<DM>(P.ctx, P.Np) + (int64_t)i * DM, q);
@@ -368,12 +396,13 @@ __global__ void __launch_bounds__(SA_NT, sa_min_waves<DM>()) sa_bwd_q_kernel(SaP
         *reinterpret_cast<float4 *>(r + 2 * DM) = make_float4(M, iL, dl, __uint_as_float(rk));
     }
     const float *kvc = sa_kvc<DM>(P.ctx, P.Np);
-    Tile<SA_KT, DM, DM, 0> tl;
+    Tile<SA_KT, DM, DM, 0, true> tl;
     tl.load(kvc, 0, P.Np);
     for (int t0 = 0; t0 < P.N; t0 += SA_KT) {
         __syncthreads();
         tl.store(ks, vs, nullptr);
         __syncthreads();
+        if (TAIL && t0 == 0) SX_STAMP(1, 2);
         if (t0 + SA_KT < P.N) tl.load(kvc, t0 + SA_KT, P.Np);
         if (!live) continue;
 #pragma unroll 2
@@ -386,14 +415,16 @@ __global__ void __launch_bounds__(SA_NT, sa_min_waves<DM>()) sa_bwd_q_kernel(SaP
             }
 #pragma unroll
             for (int x = 0; x < 2; ++x) {
+                const int r = x * (SA_KT / 2) + (t >> 1);   // ps_row(t + x)
                 // rows past N are zeros in LDS: their pr is masked to 0 below
-                const float pr = t0 + t + x < P.N ? exp2f(dot_lds<DM>(q, ks[t + x]) * SA_LOG2E - M) * iL : 0.f;
-                const float ds = pr * (((x ? kp1 : kp0) ? dot_lds<DM>(g, vs[t + x]) * s1p : 0.f) - dl);
+                const float pr = t0 + t + x < P.N ? fexp2(dot_lds<DM>(q, ks[r]) * SA_LOG2E - M) * iL : 0.f;
+                const float ds = pr * (((x ? kp1 : kp0) ? dot_lds<DM>(g, vs[r]) * s1p : 0.f) - dl);
 #pragma unroll
-                for (int c = 0; c < DM; ++c) dq[c] = fmaf(ds, ks[t + x][c], dq[c]);
+                for (int c = 0; c < DM; ++c) dq[c] = fmaf(ds, ks[r][c], dq[c]);
             }
         }
     }
+    if (TAIL) SX_STAMP(1, 3);
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1)
 #pragma unroll
@@ -412,6 +443,7 @@ __global__ void __launch_bounds__(SA_NT, sa_min_waves<DM>()) sa_bwd_q_kernel(SaP
     }
     float *row = P.out + (int64_t)i * P.ld_out;   // the Q block of dQKV
     for (int c = lane; c < P.dp; c += 64) row[c] = (live && c < P.d) ? lane_col<DM>(dq, c) * P.q_scale : 0.f;
+    if (TAIL) SX_STAMP(1, 4);
 }
 
 // ---- backward dK, dV: SA_SPL waves per KP key rows, the waves and lanes splitting the queries -------------
@@ -480,7 +512,7 @@ __global__ void __launch_bounds__(SA_NT, sa_min_waves<DM>()) sa_bwd_kv_kernel(Sa
                 float sq = 0.f, sg = 0.f;
 #pragma unroll
                 for (int c = 0; c < DM; ++c) sq = fmaf(k[x][c], qt[c], sq), sg = fmaf(v[x][c], gt[c], sg);
-                const float pr = exp2f(sq * SA_LOG2E - r.x) * r.y;
+                const float pr = fexp2(sq * SA_LOG2E - r.x) * r.y;
                 const float ds = pr * ((kp[x] ? sg * s1p : 0.f) - r.z);
                 const float pd = kp[x] ? pr * s1p : 0.f;
 #pragma unroll
@@ -696,8 +728,9 @@ struct Stage {
             if (e < N1 && h0 + h < P.ffp) a[i] = *reinterpret_cast<const float4 *>(P.a.W1 + (int64_t)(h0 + h) * P.dp + k);
         }
 #pragma unroll
-        for (int i = 0; i < P2; ++i) {   // W2 row k, 4 consecutive hidden units: coalesced
-            const int e = threadIdx.x + i * LS_NT, k = e / (HC / 4), h = 4 * (e % (HC / 4));
+        for (int i = 0; i < P2; ++i) {   // W2 row k, 4 consecutive hidden units (DM rows side by side: their
+            // transposed LDS stores below spread over DM x more banks than a row-major walk; 16-way -> 4-way at DM = 4)
+            const int e = threadIdx.x + i * LS_NT, k = e % DM, h = 4 * (e / DM);
             b[i] = z;
             if (e < N2 && h0 + h < P.ffp) b[i] = *reinterpret_cast<const float4 *>(P.a.W2 + (int64_t)k * P.ffp + h0 + h);
         }
@@ -716,7 +749,7 @@ struct Stage {
         }
 #pragma unroll
         for (int i = 0; i < P2; ++i) {
-            const int e = threadIdx.x + i * LS_NT, k = e / (HC / 4), h = 4 * (e % (HC / 4));
+            const int e = threadIdx.x + i * LS_NT, k = e % DM, h = 4 * (e / DM);
             if (e < N2) w2s[h][k] = b[i].x, w2s[h + 1][k] = b[i].y, w2s[h + 2][k] = b[i].z, w2s[h + 3][k] = b[i].w;
         }
 #pragma unroll
@@ -1027,7 +1060,7 @@ template <int DM> constexpr int tail_smem_floats() { return 2 * ls_hc<DM>() * DM
 template <int DM>
 __device__ void tail_fwd_rows(const LsP &T, int i, int rw, int sp, const float (&of)[DM], bool fin, float *smem) {
     static_assert(LS_NT == SA_NT, "the tail's staging runs on the attention workgroup");
-    constexpr int HC = ls_hc<DM>(), NU = HC / 64;
+    constexpr int HC = ls_hc<DM>(), NPR = (HC / 2 + 63) / 64;   // 64-lane rounds of unit pairs per chunk
     float (*w1s)[DM] = reinterpret_cast<float (*)[DM]>(smem);
     float (*w2s)[DM] = reinterpret_cast<float (*)[DM]>(smem + HC * DM);
     float *b1s = smem + 2 * HC * DM;
@@ -1067,6 +1100,7 @@ __device__ void tail_fwd_rows(const LsP &T, int i, int rw, int sp, const float (
         if (lane < DM) xs[rw][lane] = x1;
     }
     __syncthreads();
+    SX_STAMP(0, 5);
     float xv[DM], zp[DM];
 #pragma unroll
     for (int k = 0; k < DM; ++k) xv[k] = xs[rw][k], zp[k] = 0.f;
@@ -1079,28 +1113,50 @@ __device__ void tail_fwd_rows(const LsP &T, int i, int rw, int sp, const float (
         __syncthreads();
         sg.store(w1s, w2s, b1s);
         __syncthreads();
-#pragma unroll 4
-        for (int k = sp; k < NU; k += SA_SPL) {
-            const int h = 64 * k + lane;
-            if (h0 + h >= T.ffp) break;
-            float w1[DM], w2[DM];
+        if (h0 == 0) SX_STAMP(0, 6);
+        // unit pairs (h, h + 1), h = 2 (64 k + lane): one dropout hash per pair gives both keep bits, Hd written as
+        // float2 (round 6: a hash per unit was a fifth of the kernel's VALU issue)
+#pragma unroll 2
+        for (int k = sp; k < NPR; k += SA_SPL) {
+            const int h = 2 * (64 * k + lane);
+            if (h >= HC || h0 + h >= T.ffp) break;   // (ffp even: h + 1 < ffp too)
+            float a0 = b1s[h], a1 = b1s[h + 1];
 #pragma unroll
             for (int c = 0; c < DM; c += 4) {
-                const float4 t = *reinterpret_cast<const float4 *>(&w1s[h][c]);
-                w1[c] = t.x, w1[c + 1] = t.y, w1[c + 2] = t.z, w1[c + 3] = t.w;
-                const float4 q = *reinterpret_cast<const float4 *>(&w2s[h][c]);
-                w2[c] = q.x, w2[c + 1] = q.y, w2[c + 2] = q.z, w2[c + 3] = q.w;
+                const float4 t0 = *reinterpret_cast<const float4 *>(&w1s[h][c]);
+                const float4 t1 = *reinterpret_cast<const float4 *>(&w1s[h + 1][c]);
+                a0 = fmaf(xv[c], t0.x, a0), a0 = fmaf(xv[c + 1], t0.y, a0), a0 = fmaf(xv[c + 2], t0.z, a0);
+                a0 = fmaf(xv[c + 3], t0.w, a0);
+                a1 = fmaf(xv[c], t1.x, a1), a1 = fmaf(xv[c + 1], t1.y, a1), a1 = fmaf(xv[c + 2], t1.z, a1);
+                a1 = fmaf(xv[c + 3], t1.w, a1);
             }
-            const bool keep = !drop || u2gnn_keep_rk(rkf, (uint32_t)(h0 + h), thr);
-            ffn_unit_fwd<DM>(xv, w1, w2, b1s[h], keep, ks, live, hrow + h0 + h, zp);
+            bool k0 = true, k1 = true;
+            if (drop) {
+                const uint32_t hh = u2gnn_pair_hash(rkf, (uint32_t)(h0 + h) >> 1);
+                k0 = u2gnn_keep_lo(hh, thr), k1 = u2gnn_keep_hi(hh, thr);
+            }
+            a0 = (live && k0) ? fmaxf(a0, 0.f) * ks : 0.f;
+            a1 = (live && k1) ? fmaxf(a1, 0.f) * ks : 0.f;
+            *reinterpret_cast<float2 *>(hrow + h0 + h) = make_float2(a0, a1);
+#pragma unroll
+            for (int c = 0; c < DM; c += 4) {
+                const float4 q0 = *reinterpret_cast<const float4 *>(&w2s[h][c]);
+                const float4 q1 = *reinterpret_cast<const float4 *>(&w2s[h + 1][c]);
+                zp[c] = fmaf(a1, q1.x, fmaf(a0, q0.x, zp[c]));
+                zp[c + 1] = fmaf(a1, q1.y, fmaf(a0, q0.y, zp[c + 1]));
+                zp[c + 2] = fmaf(a1, q1.z, fmaf(a0, q0.z, zp[c + 2]));
+                zp[c + 3] = fmaf(a1, q1.w, fmaf(a0, q0.w, zp[c + 3]));
+            }
         }
     }
+    SX_STAMP(0, 7);
 #pragma unroll
     for (int k = 0; k < DM; ++k) zp[k] = wsum(zp[k]);
     if (lane == 0)
 #pragma unroll
         for (int k = 0; k < DM; ++k) xz[rw][sp][k] = zp[k];
     __syncthreads();
+    SX_STAMP(0, 8);
     if (!fin) return;
 #pragma unroll
     for (int k = 0; k < DM; ++k) {
@@ -1149,6 +1205,7 @@ __device__ void tail_bwd_rows(const LsP &T, int i, int rw, int sp, bool fin, flo
         if (lane < DM) fs[rw][lane] = df;
     }
     __syncthreads();
+    SX_STAMP(1, 5);
     float fv[DM], xp[DM];
 #pragma unroll
     for (int k = 0; k < DM; ++k) fv[k] = fs[rw][k], xp[k] = 0.f;
@@ -1166,6 +1223,7 @@ __device__ void tail_bwd_rows(const LsP &T, int i, int rw, int sp, bool fin, flo
         __syncthreads();
         sg.store(w1s, w2s, nullptr);
         __syncthreads();
+        if (h0 == 0) SX_STAMP(1, 6);
 #pragma unroll 4
         for (int u = 0; u < NW; ++u) {
             const int k = sp + SA_SPL * u, h = 64 * k + lane;
@@ -1181,12 +1239,14 @@ __device__ void tail_bwd_rows(const LsP &T, int i, int rw, int sp, bool fin, flo
             ffn_unit_bwd<DM>(fv, w1, w2, hvs[u], ks, live, dhrow + h0 + h, xp);
         }
     }
+    SX_STAMP(1, 7);
 #pragma unroll
     for (int k = 0; k < DM; ++k) xp[k] = wsum(xp[k]);
     if (lane == 0)
 #pragma unroll
         for (int k = 0; k < DM; ++k) xz[rw][sp][k] = xp[k];
     __syncthreads();
+    SX_STAMP(1, 8);
     if (fin) {
 #pragma unroll
         for (int k = 0; k < DM; ++k) {
@@ -1315,6 +1375,12 @@ int small_bwd_launch(const SaP &P, const LsP &T, hipStream_t st) {
 }  // namespace
 
 extern "C" {
+
+#ifdef SX_STAMPS
+int u2gnn_dbg_sx_stamps(unsigned long long *host, int64_t n) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_sx_stamps), (size_t)n * 8) == hipSuccess ? U2GNN_OK : U2GNN_E_ARG;
+}
+#endif
 
 int u2gnn_layer_tail_small_fwd(const u2gnn_small_tail_args *a, void *stream) { return ls_run(a, false, stream); }
 

@@ -40,6 +40,10 @@ __device__ unsigned long long g_sx_stamps[2][4096][16];
     } while (0)
 #endif
 
+#ifndef SX_BWD_ORDER
+#define SX_BWD_ORDER 1
+#endif
+
 namespace {
 
 constexpr int SA_WAVES = 8;    // rows (forward, dQ) or key rows (dK / dV) per 512-thread workgroup
@@ -55,7 +59,7 @@ constexpr float SA_LOG2E = 1.4426950408889634f;
 __device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
 // waves per SIMD the register budget is sized for: 4 (128 VGPRs) up to DM = 16, 2 (256) beyond, where the row's
 // q, o / dq / dk, dv arrays alone take 2-3 DM registers (the 128 cap spilled them to scratch)
-template <int DM> constexpr int sa_min_waves() { return DM <= 12 ? 4 : 2; }
+template <int DM> constexpr int sa_min_waves() { return DM <= 8 ? 4 : 2; }
 
 // Layouts (all fp32; DM = d rounded up to a multiple of 4 up to 24, else 32):
 //   ctx (the forward's saved context, u2gnn_attn_small_ctx_floats):  st [Np][2] = (M in log2 units, 1/L) |
@@ -86,6 +90,12 @@ struct SaP {
 };
 
 template <int DM> __host__ __device__ constexpr int sa_rq() { return 2 * DM + 4; }
+
+// 16 bytes from p (a valid, clamped address), zeroed where !ok -- the load is issued whatever ok is
+__device__ __forceinline__ float4 ld4z(const float *p, bool ok) {
+    const float4 t = *reinterpret_cast<const float4 *>(p);
+    return make_float4(ok ? t.x : 0.f, ok ? t.y : 0.f, ok ? t.z : 0.f, ok ? t.w : 0.f);
+}
 __host__ __device__ inline float *sa_st(float *ctx) { return ctx; }
 template <int DM> __host__ __device__ inline float *sa_qc(float *ctx, int64_t Np) { return ctx + 2 * Np; }
 template <int DM> __host__ __device__ inline float *sa_kvc(float *ctx, int64_t Np) { return ctx + (2 + DM) * Np; }
@@ -212,10 +222,17 @@ struct LsP {
     u2gnn_small_tail_args a;
 };
 
+template <int DM, int HC, bool BIAS> struct Stage;
+template <int DM> struct TailRowF;
+template <int DM> struct TailRowB;
+template <int DM> constexpr int ls_nw() { return (ls_hc<DM>() / 64 + SA_SPL - 1) / SA_SPL; }   // units per lane per chunk
+template <int DM>
+__device__ void tail_hd_load(const LsP &T, int i, int sp, int h0, float (&hvs)[ls_nw<DM>()]);
 template <int DM> __device__ void tail_fwd_rows(const LsP &T, int i, int rw, int sp, const float (&of)[DM], bool fin,
-                                                float *smem);
-template <int DM> __device__ void tail_bwd_rows(const LsP &T, int i, int rw, int sp, bool fin, float (&g)[DM],
-                                                float &dl, float *smem);
+                                                const TailRowF<DM> &rp, Stage<DM, ls_hc<DM>(), true> &sg, float *smem);
+template <int DM> __device__ void tail_bwd_rows(const LsP &T, int i, int rw, int sp, bool fin, const TailRowB<DM> &rp,
+                                                Stage<DM, ls_hc<DM>(), false> &sg, float (&hvs)[ls_nw<DM>()],
+                                                float (&g)[DM], float &dl, float *smem);
 template <int DM> constexpr int tail_smem_floats();
 
 // ---- forward: one query row per SA_SPL waves -------------------------------------------------------------
@@ -247,6 +264,9 @@ __global__ void __launch_bounds__(SA_NT, sa_min_waves<DM>()) sa_fwd_kernel(SaP P
     if (TAIL) SX_STAMP(0, 0);
     Tile<SA_KT, DM, DM, 0, true> tl;
     tl.load(kvc, 0, P.Np);
+    [[maybe_unused]] TailRowF<DM> rp;   // TAIL: the row operands of the tail, in flight under the walk
+    if constexpr (TAIL)
+        if (sp == 0) rp.load(T, i);
     for (int t0 = 0; t0 < P.N; t0 += SA_KT) {
         __syncthreads();
         tl.store(ks, vs, nullptr);
@@ -292,6 +312,9 @@ __global__ void __launch_bounds__(SA_NT, sa_min_waves<DM>()) sa_fwd_kernel(SaP P
         }
     }
     if (TAIL) SX_STAMP(0, 2);
+    // TAIL: the tail's first weight chunk, in flight under the merge and the out-projection / LayerNorm1
+    [[maybe_unused]] Stage<DM, ls_hc<DM>(), true> sg;
+    if constexpr (TAIL) sg.load(T, 0);
     // merge of the 64 lanes' (m, l, o): the wave's maximum first, each lane rescales to it once, then plain
     // butterfly sums (one exp per lane instead of two per butterfly level); every lane ends with the same values
     {
@@ -347,7 +370,7 @@ __global__ void __launch_bounds__(SA_NT, sa_min_waves<DM>()) sa_fwd_kernel(SaP P
     if constexpr (TAIL) {
         SX_STAMP(0, 4);
         __shared__ __attribute__((aligned(16))) float tsm[tail_smem_floats<DM>()];
-        tail_fwd_rows<DM>(T, i, rw, sp, of, fin, tsm);
+        tail_fwd_rows<DM>(T, i, rw, sp, of, fin, rp, sg, tsm);
         SX_STAMP(0, 9);
     }
 }
@@ -375,7 +398,17 @@ __global__ void __launch_bounds__(SA_NT, sa_min_waves<DM>()) sa_bwd_q_kernel(SaP
     if constexpr (TAIL) {   // dO and delta of the row from the tail backward (every wave of the row)
         SX_STAMP(1, 0);
         __shared__ __attribute__((aligned(16))) float tsm[tail_smem_floats<DM>()];
-        tail_bwd_rows<DM>(T, i, rw, sp, sp == 0 && i < P.Np, g, dl, tsm);
+        const bool fin = sp == 0 && i < P.Np;
+        Stage<DM, ls_hc<DM>(), false> sg;   // every operand of the tail's first chunk, issued together
+        float hvs[ls_nw<DM>()];
+        TailRowB<DM> rp;
+        rp.load(T, i);   // (every wave: the LayerNorm2^T operands are the first loads in flight)
+#if SX_BWD_ORDER
+        __builtin_amdgcn_sched_barrier(0);
+#endif
+        sg.load(T, 0);
+        tail_hd_load<DM>(T, i, sp, 0, hvs);
+        tail_bwd_rows<DM>(T, i, rw, sp, fin, rp, sg, hvs, g, dl, tsm);
         SX_STAMP(1, 1);
     }
     if (live) {
@@ -719,26 +752,24 @@ struct Stage {
     static constexpr int C4 = DM / 4, N1 = HC * C4, N2 = DM * (HC / 4), N3 = BIAS ? HC / 4 : 0;
     static constexpr int P1 = (N1 + LS_NT - 1) / LS_NT, P2 = (N2 + LS_NT - 1) / LS_NT, P3 = (N3 + LS_NT - 1) / LS_NT;
     float4 a[P1], b[P2], c[P3 > 0 ? P3 : 1];
+    // every load unconditional from a clamped address, zeroed after (ld4z): the form "zero, then load under a
+    // branch" compiled to one s_waitcnt vmcnt(0) per load in the fused kernels (tools/isa_waits.py)
     __device__ __forceinline__ void load(const LsP &P, int h0) {
-        const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
         for (int i = 0; i < P1; ++i) {
             const int e = threadIdx.x + i * LS_NT, h = e / C4, k = 4 * (e % C4);
-            a[i] = z;
-            if (e < N1 && h0 + h < P.ffp) a[i] = *reinterpret_cast<const float4 *>(P.a.W1 + (int64_t)(h0 + h) * P.dp + k);
+            a[i] = ld4z(P.a.W1 + (int64_t)min(h0 + h, P.ffp - 1) * P.dp + k, e < N1 && h0 + h < P.ffp);
         }
 #pragma unroll
         for (int i = 0; i < P2; ++i) {   // W2 row k, 4 consecutive hidden units (DM rows side by side: their
             // transposed LDS stores below spread over DM x more banks than a row-major walk; 16-way -> 4-way at DM = 4)
             const int e = threadIdx.x + i * LS_NT, k = e % DM, h = 4 * (e / DM);
-            b[i] = z;
-            if (e < N2 && h0 + h < P.ffp) b[i] = *reinterpret_cast<const float4 *>(P.a.W2 + (int64_t)k * P.ffp + h0 + h);
+            b[i] = ld4z(P.a.W2 + (int64_t)k * P.ffp + min(h0 + h, P.ffp - 4), e < N2 && h0 + h < P.ffp);
         }
 #pragma unroll
         for (int i = 0; i < P3; ++i) {
             const int e = threadIdx.x + i * LS_NT, h = 4 * e;
-            c[i] = z;
-            if (e < N3 && h0 + h < P.ffp) c[i] = *reinterpret_cast<const float4 *>(P.a.b1 + h0 + h);
+            c[i] = ld4z(P.a.b1 + min(h0 + h, P.ffp - 4), e < N3 && h0 + h < P.ffp);
         }
     }
     __device__ __forceinline__ void store(float (*w1s)[DM], float (*w2s)[DM], float *b1s) const {
@@ -761,24 +792,31 @@ struct Stage {
 };
 
 // post-LN of one row held as lane c < d: returns y_c (0 past d), the row's mean and 1/std
-__device__ __forceinline__ float ln_row(float z, int lane, int d, float eps, const float *gamma, const float *beta,
-                                        float &mu, float &rs) {
+__device__ __forceinline__ float ln_row_v(float z, int lane, int d, float eps, float gam, float bet, float &mu,
+                                          float &rs) {   // (gam, bet: column lane's gamma, beta)
     const bool ok = lane < d;
     const float v = ok ? z : 0.f;
     mu = wsum(v) / (float)d;
     const float t = ok ? v - mu : 0.f;
     rs = rsqrtf(wsum(t * t) / (float)d + eps);
-    const int c = ok ? lane : 0;   // gamma, beta: unpadded [d]
-    return ok ? t * rs * gamma[c] + beta[c] : 0.f;
+    return ok ? t * rs * gam + bet : 0.f;
+}
+__device__ __forceinline__ float ln_row(float z, int lane, int d, float eps, const float *gamma, const float *beta,
+                                        float &mu, float &rs) {
+    const int c = lane < d ? lane : 0;   // gamma, beta: unpadded [d]
+    return ln_row_v(z, lane, d, eps, gamma[c], beta[c], mu, rs);
 }
 
 // LN backward of one row (lane c < d): dz = rs (g - mean(g) - xh mean(g xh)), g = dy gamma, xh = (z - mu) rs
-__device__ __forceinline__ float ln_row_bwd(float dy, float z, float mu, float rs, int lane, int d, const float *gamma) {
+__device__ __forceinline__ float ln_row_bwd_v(float dy, float z, float mu, float rs, int lane, int d, float gam) {
     const bool ok = lane < d;
     const float xh = ok ? (z - mu) * rs : 0.f;
-    const float g = ok ? dy * gamma[ok ? lane : 0] : 0.f;
+    const float g = ok ? dy * gam : 0.f;
     const float m1 = wsum(g) / (float)d, m2 = wsum(g * xh) / (float)d;
     return ok ? rs * (g - m1 - xh * m2) : 0.f;
+}
+__device__ __forceinline__ float ln_row_bwd(float dy, float z, float mu, float rs, int lane, int d, const float *gamma) {
+    return ln_row_bwd_v(dy, z, mu, rs, lane, d, gamma[lane < d ? lane : 0]);
 }
 
 // Two work splits.  STAGED (large N, e.g. C5's 2048 rows): 8 rows per workgroup, one wave per row, the weights
@@ -990,7 +1028,10 @@ __global__ void __launch_bounds__(LS_NT, ls_min_waves<DM>()) ls_bwd_kernel(LsP P
             sg.load(P, h0);
             float hvs[NU];   // this row's ReLU image of the chunk, loaded with the weights
 #pragma unroll
-            for (int u = 0; u < NU; ++u) hvs[u] = h0 + 64 * u + lane < P.ffp ? hrow[h0 + 64 * u + lane] : 0.f;
+            for (int u = 0; u < NU; ++u) {   // (unconditional loads, clamped: see Stage::load)
+                const float v = hrow[min(h0 + 64 * u + lane, P.ffp - 1)];
+                hvs[u] = h0 + 64 * u + lane < P.ffp ? v : 0.f;
+            }
             __syncthreads();
             sg.store(w1s, w2s, nullptr);
             __syncthreads();
@@ -1057,8 +1098,67 @@ __global__ void __launch_bounds__(LS_NT, ls_min_waves<DM>()) ls_bwd_kernel(LsP P
 // sums are taken in another order (per wave, then across the two waves).
 template <int DM> constexpr int tail_smem_floats() { return 2 * ls_hc<DM>() * DM + ls_hc<DM>() + SA_RB * (4 * DM + 4); }
 
+// The tail's global operands are issued ahead of the phase that uses them (round 6, tools/sl_stamps.py: each
+// dependent global round trip cost about a microsecond of the workgroup's chain): the row operands (TailRowF /
+// TailRowB) at kernel start; forward, the first weight chunk (Stage) right after the walk, under the lane merge,
+// the O row and LayerNorm1; backward, the first chunk and the row's ReLU image together with the row operands.
+// forward row operands, lane c < d: W_o row c, b_o[c], X[i][c], b2[c], the LayerNorm gammas / betas of column c
 template <int DM>
-__device__ void tail_fwd_rows(const LsP &T, int i, int rw, int sp, const float (&of)[DM], bool fin, float *smem) {
+struct TailRowF {
+    float wo[DM], bo, x, g1, e1, b2, g2, e2;
+    __device__ __forceinline__ void load(const LsP &T, int i) {
+        const int lane = threadIdx.x & 63, cw = lane < DM ? lane : 0, c = lane < T.d ? lane : 0;
+        const u2gnn_small_tail_args &A = T.a;
+#pragma unroll
+        for (int k = 0; k < DM; k += 4) {
+            const float4 t = *reinterpret_cast<const float4 *>(A.W_o + (int64_t)cw * T.dp + k);
+            wo[k] = t.x, wo[k + 1] = t.y, wo[k + 2] = t.z, wo[k + 3] = t.w;
+        }
+        bo = A.b_o[lane], x = A.X[(int64_t)i * T.dp + lane], b2 = A.b2[lane];   // (dp == 64: one column per lane)
+        g1 = A.n1_w[c], e1 = A.n1_b[c], g2 = A.n2_w[c], e2 = A.n2_b[c];
+    }
+};
+
+// backward row operands, lane c: dX2, Z2, Z1, O of column c, the row statistics, the LayerNorm gammas, W_o column c
+template <int DM>
+struct TailRowB {
+    float dx2, z2, mu2, rs2, g2, z1, mu1, rs1, g1, o, woc[DM];
+    __device__ __forceinline__ void load(const LsP &T, int i) {
+        const int lane = threadIdx.x & 63, kc = lane < DM ? lane : 0, c = lane < T.d ? lane : 0;
+        const u2gnn_small_tail_args &A = T.a;
+        const int64_t ro = (int64_t)i * T.dp;
+        dx2 = A.dX2[ro + lane], z2 = A.Z2[ro + lane], z1 = A.Z1[ro + lane], o = A.O[ro + lane];
+        mu2 = A.mean2[i], rs2 = A.rstd2[i], mu1 = A.mean1[i], rs1 = A.rstd1[i];
+        g2 = A.n2_w[c], g1 = A.n1_w[c];
+#pragma unroll
+        for (int k = 0; k < DM; ++k) woc[k] = A.W_o[(int64_t)k * T.dp + kc];
+    }
+};
+
+// the row's ReLU image Hd over this wave's units of chunk h0
+template <int DM>
+__device__ void tail_hd_load(const LsP &T, int i, int sp, int h0, float (&hvs)[ls_nw<DM>()]) {
+    constexpr int NU = ls_hc<DM>() / 64;
+    const int lane = threadIdx.x & 63;
+    const float *hrow = T.a.Hd + (int64_t)i * T.ffp;
+    // every load issued unconditionally (clamped index, masked after): a conditional load into a zeroed register
+    // compiled to load -> s_waitcnt vmcnt(0) per unit, a memory round trip each (tools/isa_waits.py)
+    float v[ls_nw<DM>()];
+#pragma unroll
+    for (int u = 0; u < ls_nw<DM>(); ++u) {
+        const int k = sp + SA_SPL * u, h = 64 * k + lane;
+        v[u] = hrow[min(h0 + h, T.ffp - 1)];
+    }
+#pragma unroll
+    for (int u = 0; u < ls_nw<DM>(); ++u) {
+        const int k = sp + SA_SPL * u, h = 64 * k + lane;
+        hvs[u] = (k < NU && h0 + h < T.ffp) ? v[u] : 0.f;
+    }
+}
+
+template <int DM>
+__device__ void tail_fwd_rows(const LsP &T, int i, int rw, int sp, const float (&of)[DM], bool fin,
+                              const TailRowF<DM> &rp, Stage<DM, ls_hc<DM>(), true> &sg, float *smem) {
     static_assert(LS_NT == SA_NT, "the tail's staging runs on the attention workgroup");
     constexpr int HC = ls_hc<DM>(), NPR = (HC / 2 + 63) / 64;   // 64-lane rounds of unit pairs per chunk
     float (*w1s)[DM] = reinterpret_cast<float (*)[DM]>(smem);
@@ -1079,20 +1179,13 @@ __device__ void tail_fwd_rows(const LsP &T, int i, int rw, int sp, const float (
     if (fin) {
         float z1 = 0.f, mu1 = 0.f, rs1 = 0.f;
         if (live) {
-            float wo[DM];
-            const int cw = lane < DM ? lane : 0;
-#pragma unroll
-            for (int k = 0; k < DM; k += 4) {
-                const float4 t = *reinterpret_cast<const float4 *>(A.W_o + (int64_t)cw * T.dp + k);
-                wo[k] = t.x, wo[k + 1] = t.y, wo[k + 2] = t.z, wo[k + 3] = t.w;
-            }
             float acc = 0.f;
 #pragma unroll
-            for (int k = 0; k < DM; ++k) acc = fmaf(of[k], wo[k], acc);
-            float v = acc + A.b_o[lane];
+            for (int k = 0; k < DM; ++k) acc = fmaf(of[k], rp.wo[k], acc);
+            float v = acc + rp.bo;
             if (drop) v = u2gnn_keep(s1, (uint32_t)i, (uint32_t)lane, T.p) ? v * ks : 0.f;
-            z1 = lane < T.d ? v + A.X[ro + lane] : 0.f;
-            x1 = ln_row(z1, lane, T.d, T.eps, A.n1_w, A.n1_b, mu1, rs1);
+            z1 = lane < T.d ? v + rp.x : 0.f;
+            x1 = ln_row_v(z1, lane, T.d, T.eps, rp.g1, rp.e1, mu1, rs1);
         }
         A.Z1[ro + lane] = z1;
         A.X1[ro + lane] = x1;
@@ -1108,11 +1201,10 @@ __device__ void tail_fwd_rows(const LsP &T, int i, int rw, int sp, const float (
     const uint32_t rkf = u2gnn_row_key(sff, (uint32_t)i);
     float *hrow = A.Hd + (int64_t)i * T.ffp;
     for (int h0 = 0; h0 < T.ffp; h0 += HC) {
-        Stage<DM, HC, true> sg;
-        sg.load(T, h0);
-        __syncthreads();
+        if (h0) __syncthreads();   // the previous chunk's readers are done
         sg.store(w1s, w2s, b1s);
         __syncthreads();
+        if (h0 + HC < T.ffp) sg.load(T, h0 + HC);   // the next chunk, in flight under this one
         if (h0 == 0) SX_STAMP(0, 6);
         // unit pairs (h, h + 1), h = 2 (64 k + lane): one dropout hash per pair gives both keep bits, Hd written as
         // float2 (round 6: a hash per unit was a fifth of the kernel's VALU issue)
@@ -1167,20 +1259,23 @@ __device__ void tail_fwd_rows(const LsP &T, int i, int rw, int sp, const float (
     }
     float z2 = 0.f, x2 = 0.f, mu2 = 0.f, rs2 = 0.f;
     if (live) {
-        float v = pick<DM>(zp, lane) + A.b2[lane];
+        float v = pick<DM>(zp, lane) + rp.b2;
         if (drop) v = u2gnn_keep(s2, (uint32_t)i, (uint32_t)lane, T.p) ? v * ks : 0.f;
         z2 = lane < T.d ? v + x1 : 0.f;
-        x2 = ln_row(z2, lane, T.d, T.eps, A.n2_w, A.n2_b, mu2, rs2);
+        x2 = ln_row_v(z2, lane, T.d, T.eps, rp.g2, rp.e2, mu2, rs2);
     }
     A.Z2[ro + lane] = z2;
     A.X2[ro + lane] = x2;
     if (lane == 0) A.mean2[i] = mu2, A.rstd2[i] = rs2;
 }
 
-// the tail backward of the row; on return every wave of the row holds its dO row (g) and delta (dl)
+// the tail backward of the row; on return every wave of the row holds its dO row (g) and delta (dl).  sg, hvs: the
+// first chunk's weights and this wave's units of the row's ReLU image, already in flight
 template <int DM>
-__device__ void tail_bwd_rows(const LsP &T, int i, int rw, int sp, bool fin, float (&g)[DM], float &dl, float *smem) {
-    constexpr int HC = ls_hc<DM>(), NU = HC / 64, NW = (NU + SA_SPL - 1) / SA_SPL;
+__device__ void tail_bwd_rows(const LsP &T, int i, int rw, int sp, bool fin, const TailRowB<DM> &rp,
+                              Stage<DM, ls_hc<DM>(), false> &sg, float (&hvs)[ls_nw<DM>()], float (&g)[DM], float &dl,
+                              float *smem) {
+    constexpr int HC = ls_hc<DM>(), NU = HC / 64, NW = ls_nw<DM>();
     float (*w1s)[DM] = reinterpret_cast<float (*)[DM]>(smem);
     float (*w2s)[DM] = reinterpret_cast<float (*)[DM]>(smem + HC * DM);
     float (*fs)[DM] = reinterpret_cast<float (*)[DM]>(smem + 2 * HC * DM);
@@ -1198,7 +1293,7 @@ __device__ void tail_bwd_rows(const LsP &T, int i, int rw, int sp, bool fin, flo
     if (fin) {
         float df = 0.f;
         if (live) {
-            dz2 = ln_row_bwd(A.dX2[ro + lane], A.Z2[ro + lane], A.mean2[i], A.rstd2[i], lane, T.d, A.n2_w);
+            dz2 = ln_row_bwd_v(rp.dx2, rp.z2, rp.mu2, rp.rs2, lane, T.d, rp.g2);
             df = (drop && lane < T.d) ? (u2gnn_keep(s2, (uint32_t)i, (uint32_t)lane, T.p) ? dz2 * ks : 0.f) : dz2;
         }
         A.dF[ro + lane] = df;
@@ -1209,20 +1304,18 @@ __device__ void tail_bwd_rows(const LsP &T, int i, int rw, int sp, bool fin, flo
     float fv[DM], xp[DM];
 #pragma unroll
     for (int k = 0; k < DM; ++k) fv[k] = fs[rw][k], xp[k] = 0.f;
-    const float *hrow = A.Hd + (int64_t)i * T.ffp;
     float *dhrow = A.dH + (int64_t)i * T.ffp;
     for (int h0 = 0; h0 < T.ffp; h0 += HC) {
-        Stage<DM, HC, false> sg;
-        sg.load(T, h0);
-        float hvs[NW];   // this wave's units of the row's ReLU image, loaded with the weights
-#pragma unroll
-        for (int u = 0; u < NW; ++u) {
-            const int h = 64 * (sp + SA_SPL * u) + lane;
-            hvs[u] = (sp + SA_SPL * u < NU && h0 + h < T.ffp) ? hrow[h0 + h] : 0.f;
-        }
-        __syncthreads();
+        if (h0) __syncthreads();   // the previous chunk's readers are done
         sg.store(w1s, w2s, nullptr);
         __syncthreads();
+        float hc[NW];
+#pragma unroll
+        for (int u = 0; u < NW; ++u) hc[u] = hvs[u];
+        if (h0 + HC < T.ffp) {   // the next chunk, in flight under this one
+            sg.load(T, h0 + HC);
+            tail_hd_load<DM>(T, i, sp, h0 + HC, hvs);
+        }
         if (h0 == 0) SX_STAMP(1, 6);
 #pragma unroll 4
         for (int u = 0; u < NW; ++u) {
@@ -1236,7 +1329,7 @@ __device__ void tail_bwd_rows(const LsP &T, int i, int rw, int sp, bool fin, flo
                 const float4 q = *reinterpret_cast<const float4 *>(&w2s[h][c]);
                 w2[c] = q.x, w2[c + 1] = q.y, w2[c + 2] = q.z, w2[c + 3] = q.w;
             }
-            ffn_unit_bwd<DM>(fv, w1, w2, hvs[u], ks, live, dhrow + h0 + h, xp);
+            ffn_unit_bwd<DM>(fv, w1, w2, hc[u], ks, live, dhrow + h0 + h, xp);
         }
     }
     SX_STAMP(1, 7);
@@ -1258,17 +1351,16 @@ __device__ void tail_bwd_rows(const LsP &T, int i, int rw, int sp, bool fin, flo
         float dx1 = 0.f, dz1 = 0.f, da = 0.f, dov = 0.f, dlt = 0.f;
         if (live) {
             dx1 = lane < T.d ? dz2 + pick<DM>(xp, lane) : 0.f;
-            dz1 = ln_row_bwd(dx1, A.Z1[ro + lane], A.mean1[i], A.rstd1[i], lane, T.d, A.n1_w);
+            dz1 = ln_row_bwd_v(dx1, rp.z1, rp.mu1, rp.rs1, lane, T.d, rp.g1);
             da = (drop && lane < T.d) ? (u2gnn_keep(s1, (uint32_t)i, (uint32_t)lane, T.p) ? dz1 * ks : 0.f) : dz1;
             float av[DM];
 #pragma unroll
             for (int k = 0; k < DM; ++k) av[k] = __shfl(da, k, 64);
-            const int kc = lane < DM ? lane : 0;
             float acc = 0.f;
 #pragma unroll
-            for (int c = 0; c < DM; ++c) acc = fmaf(av[c], A.W_o[(int64_t)c * T.dp + kc], acc);
+            for (int c = 0; c < DM; ++c) acc = fmaf(av[c], rp.woc[c], acc);
             dov = lane < T.d ? acc : 0.f;
-            dlt = wsum(dov * A.O[ro + lane]);
+            dlt = wsum(dov * rp.o);
         }
         A.dX1[ro + lane] = dx1;
         A.dX[ro + lane] = dz1;

@@ -197,7 +197,15 @@ __device__ __forceinline__ float4 slab_sum4(const float *p, int n_slab, int64_t 
         a = add4(a, l[0]), b = add4(b, l[1]), e = add4(e, l[2]), f = add4(f, l[3]);
         z += 4;
     }
-    for (; z < n_slab; ++z) a = add4(a, ld4(p + (int64_t)z * slab_stride));
+    if (z < n_slab) {   // the last 1-3 slices: loaded together from clamped addresses, then added in order (a loop
+        // here waited out one memory round trip per slice, tools/isa_waits.py)
+        const int z1 = min(z + 1, n_slab - 1), z2 = min(z + 2, n_slab - 1);
+        const float4 l0 = ld4(p + (int64_t)z * slab_stride), l1 = ld4(p + (int64_t)z1 * slab_stride);
+        const float4 l2 = ld4(p + (int64_t)z2 * slab_stride);
+        a = add4(a, l0);
+        if (z + 1 < n_slab) a = add4(a, l1);
+        if (z + 2 < n_slab) a = add4(a, l2);
+    }
     return add4(add4(a, b), add4(e, f));
 }
 
@@ -224,14 +232,20 @@ __device__ __forceinline__ void slab_reduce_body(const float *src, int n_slab, i
         *reinterpret_cast<float4 *>(o) = v;
     } else {
         const float x[4] = {t.x, t.y, t.z, t.w};
+        float *orow = dst + rr * ld_dst;
+        int64_t cc[4];
+        bool vc[4];
+        float ov[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            bool vc;
-            const int64_t cc = blk_map(c + q, cbp, cbr, &vc);
-            if (!vc) continue;
-            float *o = dst + rr * ld_dst + cc;
-            *o = accumulate ? *o + alpha * x[q] : alpha * x[q];
-        }
+        for (int q = 0; q < 4; ++q) cc[q] = blk_map(c + q, cbp, cbr, &vc[q]);
+        // the four old values loaded before any store (blk_map is injective: no aliasing; clamped addresses): a
+        // load -> store per column waited out four dependent memory round trips
+        if (accumulate)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) ov[q] = orow[vc[q] ? cc[q] : 0];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if (vc[q]) orow[cc[q]] = accumulate ? ov[q] + alpha * x[q] : alpha * x[q];
     }
 }
 

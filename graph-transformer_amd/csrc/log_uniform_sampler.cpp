@@ -4,6 +4,8 @@
 #include "u2gnn_lus.h"
 
 #include <cmath>
+#include <cstdlib>
+#include <functional>
 #include <new>
 #include <random>
 #include <unordered_map>
@@ -11,16 +13,103 @@
 #include <vector>
 
 namespace {
+// Bump allocator for one draw's unordered_set (nodes and bucket arrays; freeing is a no-op, the arena is
+// rewound per call).  The set's iteration order depends only on its hash policy and insertion sequence,
+// never on the allocator, so the ids and their order are unchanged; what goes is a malloc / free per try
+// (emplace builds the node before it finds a duplicate).  Blocks are kept across calls.
+struct Arena {
+    std::vector<char *> blocks;
+    size_t blk = 0, off = 0;
+    static constexpr size_t BLOCK = 1 << 20;
+    void *get(size_t bytes, size_t align) {
+        if (bytes > BLOCK) throw std::bad_alloc();
+        off = (off + align - 1) & ~(align - 1);
+        if (blocks.empty() || off + bytes > BLOCK) {
+            if (!blocks.empty()) ++blk;
+            if (blk == blocks.size()) {
+                char *b = static_cast<char *>(std::malloc(BLOCK));
+                if (!b) throw std::bad_alloc();
+                blocks.push_back(b);
+            }
+            off = 0;
+        }
+        void *p = blocks[blk] + off;
+        off += bytes;
+        return p;
+    }
+    void rewind() { blk = 0, off = 0; }
+    ~Arena() {
+        for (char *b : blocks) std::free(b);
+    }
+};
+
+template <class T>
+struct ArenaAlloc {
+    using value_type = T;
+    Arena *a;
+    explicit ArenaAlloc(Arena *a_) : a(a_) {}
+    template <class U>
+    ArenaAlloc(const ArenaAlloc<U> &o) : a(o.a) {}
+    T *allocate(size_t n) { return static_cast<T *>(a->get(n * sizeof(T), alignof(T))); }
+    void deallocate(T *, size_t) {}
+    template <class U>
+    bool operator==(const ArenaAlloc<U> &o) const { return a == o.a; }
+    template <class U>
+    bool operator!=(const ArenaAlloc<U> &o) const { return a != o.a; }
+};
+using IdSet = std::unordered_set<long, std::hash<long>, std::equal_to<long>, ArenaAlloc<long>>;
+
 struct Sampler {
     int64_t n;
     std::minstd_rand0 engine;                    // == std::default_random_engine (libstdc++)
     std::uniform_real_distribution<double> uni;  // [0, 1)
     std::vector<float> prob;
+    Arena arena;
+    std::vector<int64_t> pytab;                  // sample_pyset's table
     Sampler(int64_t n_, uint32_t seed) : n(n_), engine(seed), uni(0.0, 1.0), prob((size_t)n_) {
         const double lr = std::log((double)(n_ + 1));
         for (int64_t i = 0; i < n_; ++i) prob[(size_t)i] = (float)((std::log((double)(i + 2)) - std::log((double)(i + 1))) / lr);
     }
     long draw(double log_n) { return std::lround(std::exp(uni(engine) * log_n)) - 1; }
+};
+
+// CPython's set of non-negative ints (Objects/setobject.c, 3.x: hash(i) = i, 8-slot start, 9 linear probes then
+// perturbed probing, resize to 4 x used once fill * 5 >= mask * 3, rehash in table order): the order of
+// list(set(ids)) for distinct ids inserted in the given order -- what the reference's Cython binding
+// returns (a Python set built from the C++ unordered_set, then list()).  tests/test_sampler_cpu.py checks it
+// against this interpreter's own set on thousands of draws.
+struct PySetOrder {
+    static constexpr int64_t EMPTY = -1;
+    static constexpr size_t LINEAR_PROBES = 9, PERTURB_SHIFT = 5;
+    std::vector<int64_t> &tab;
+    size_t mask = 7, fill = 0;
+    explicit PySetOrder(std::vector<int64_t> &t) : tab(t) { tab.assign(8, EMPTY); }
+    static void put(std::vector<int64_t> &t, size_t mask, int64_t key) {
+        size_t perturb = (size_t)key, i = (size_t)key & mask;
+        while (true) {
+            const size_t probes = i + LINEAR_PROBES <= mask ? LINEAR_PROBES : 0;
+            for (size_t j = 0; j <= probes; ++j)
+                if (t[i + j] == EMPTY) {
+                    t[i + j] = key;
+                    return;
+                }
+            perturb >>= PERTURB_SHIFT;
+            i = (i * 5 + 1 + perturb) & mask;
+        }
+    }
+    void add(int64_t key) {   // key not yet present
+        put(tab, mask, key);
+        ++fill;
+        if (fill * 5 < mask * 3) return;
+        const size_t minused = fill > 50000 ? fill * 2 : fill * 4;
+        size_t newsize = 8;
+        while (newsize <= minused) newsize <<= 1;
+        std::vector<int64_t> nt(newsize, EMPTY);
+        for (int64_t k : tab)
+            if (k != EMPTY) put(nt, newsize - 1, k);
+        tab.swap(nt);
+        mask = newsize - 1;
+    }
 };
 }  // namespace
 
@@ -41,7 +130,8 @@ int u2gnn_lus_sample(void *h, size_t size, int64_t *out_ids, int32_t *num_tries)
     auto *s = static_cast<Sampler *>(h);
     if (!s || (!out_ids && size) || !num_tries || (int64_t)size > s->n) return -1;
     try {
-        std::unordered_set<long> data;
+        s->arena.rewind();
+        IdSet data(ArenaAlloc<long>(&s->arena));
         const double log_n = std::log((double)s->n);
         int32_t tries = 0;
         while (data.size() != size) {
@@ -56,6 +146,22 @@ int u2gnn_lus_sample(void *h, size_t size, int64_t *out_ids, int32_t *num_tries)
         return -2;
     } catch (...) {
         return -1;
+    }
+}
+
+int u2gnn_lus_sample_pyset(void *h, size_t size, int64_t *out_ids, int32_t *num_tries) {
+    auto *s = static_cast<Sampler *>(h);
+    const int rc = u2gnn_lus_sample(h, size, out_ids, num_tries);
+    if (rc != 0) return rc;
+    try {
+        PySetOrder ps(s->pytab);
+        for (size_t i = 0; i < size; ++i) ps.add(out_ids[i]);
+        size_t k = 0;
+        for (int64_t v : s->pytab)
+            if (v != PySetOrder::EMPTY) out_ids[k++] = v;
+        return 0;
+    } catch (const std::bad_alloc &) {
+        return -2;
     }
 }
 

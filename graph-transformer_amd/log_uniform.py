@@ -48,9 +48,16 @@ class LogUniformSampler(object):
 
     def sample_set_order(self, size):
         """ids in the order the reference returns them: its Cython binding converts the C++
-        unordered_set into a Python set (inserting in C++ iteration order) before list()."""
-        ids, nt = self.sample_ids(size)
-        return np.asarray(list(set(ids.tolist())), dtype=np.int64), nt
+        unordered_set into a Python set (inserting in C++ iteration order) before list() -- that
+        set order computed natively (u2gnn_lus_sample_pyset; equal to list(set(sample_ids order)),
+        tests/test_sampler_pyset_cpu.py)."""
+        out = np.empty(int(size), dtype=np.int64)
+        nt = ctypes.c_int32()
+        rc = self._lib.u2gnn_lus_sample_pyset(self._h, int(size), _ptr(out), ctypes.byref(nt))
+        if rc != 0:
+            raise ValueError(f"sample({size}) rejected (N={self.N}); the reference would not terminate"
+                             if rc == -1 else f"sampler error {rc}")
+        return out, nt.value
 
     def sample(self, size, labels):
         """log_uniform.pyx:29-34: (sample ids, true expected counts, sample expected counts)."""

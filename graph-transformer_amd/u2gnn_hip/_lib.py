@@ -208,6 +208,7 @@ _LUS_SIGS = {
     "u2gnn_lus_create": ([I64, c_uint32], VP),
     "u2gnn_lus_destroy": ([VP], None),
     "u2gnn_lus_sample": ([VP, c_size_t, VP, POINTER(c_int32)], c_int32),
+    "u2gnn_lus_sample_pyset": ([VP, c_size_t, VP, POINTER(c_int32)], c_int32),
     "u2gnn_lus_expected_count": ([VP, c_int32, VP, c_size_t, VP], c_int32),
     "u2gnn_lus_probability": ([VP, I64], c_float),
     "u2gnn_lus_sample_unique": ([VP, c_size_t, VP, c_size_t, VP], c_int32),

@@ -26,6 +26,10 @@ void *u2gnn_lus_create(int64_t range_max, uint32_t seed);
 void u2gnn_lus_destroy(void *h);
 /* sample(size) (Log_Uniform_Sampler.cpp:57-71): `size` distinct ids in unordered_set order. */
 int u2gnn_lus_sample(void *h, size_t size, int64_t *out_ids, int32_t *num_tries);
+/* sample(size) as the reference's Python binding returns it (log_uniform.pyx:24-27 converts the unordered_set
+ * into a Python set, then list()): the same ids in CPython set order -- list(set(u2gnn_lus_sample's ids)) without
+ * the interpreter round trip (round 6: that conversion was about half of the per-step sampler time). */
+int u2gnn_lus_sample_pyset(void *h, size_t size, int64_t *out_ids, int32_t *num_tries);
 /* expected_count (Log_Uniform_Sampler.cpp:23-32) */
 int u2gnn_lus_expected_count(void *h, int32_t num_tries, const int64_t *ids, size_t n, float *out);
 /* probability (Log_Uniform_Sampler.cpp:18-21) */

@@ -1012,23 +1012,57 @@ __global__ void __launch_bounds__(256) slab_bias_drop_resid_ln_kernel(
     const int l = threadIdx.x & 63;
     if (row >= rows_pad) return;
     const bool live = row < rows_valid;   // padding rows: Z, Y, mean, rstd all 0
-    float zz[CPL];
+    // the column groups' loads of one 4-slab round issued together, bias and residual before the rounds (round 6:
+    // a round per column group, then the remainder slab by slab, each waited out a memory round trip,
+    // tools/isa_waits.py); the sums per column are the same, in the same order
+    float zz[CPL], a[CPL], b[CPL], e[CPL], f[CPL], bi[CPL], re[CPL], gm[CPL], bt[CPL];
+    const float *q = src + row * ld_src + l;
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) {
+        const int cc = l + 64 * k < d ? l + 64 * k : (int)d - 1;
+        a[k] = b[k] = e[k] = f[k] = 0.f;
+        bi[k] = bias[l + 64 * k];
+        re[k] = resid[row * ld_res + l + 64 * k];
+        gm[k] = gamma[cc], bt[k] = beta[cc];
+    }
+    int z = 0;
+    for (; z + 4 <= n_slab; z += 4) {
+        float t[CPL][4];
+#pragma unroll
+        for (int k = 0; k < CPL; ++k)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) t[k][j] = q[(int64_t)(z + j) * slab_stride + 64 * k];
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) a[k] += t[k][0], b[k] += t[k][1], e[k] += t[k][2], f[k] += t[k][3];
+    }
+    if (z < n_slab) {   // the last 1-3 slabs: clamped loads together, then added in slab order
+        const int z1 = min(z + 1, n_slab - 1), z2 = min(z + 2, n_slab - 1);
+        float t[CPL][3];
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) {
+            t[k][0] = q[(int64_t)z * slab_stride + 64 * k];
+            t[k][1] = q[(int64_t)z1 * slab_stride + 64 * k];
+            t[k][2] = q[(int64_t)z2 * slab_stride + 64 * k];
+        }
+#pragma unroll
+        for (int k = 0; k < CPL; ++k)   // (consumed here: keeps the compiler from sinking a load into its branch)
+            asm volatile("" ::"v"(t[k][0]), "v"(t[k][1]), "v"(t[k][2]));
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) {
+            a[k] += t[k][0];
+            if (z + 1 < n_slab) a[k] += t[k][1];
+            if (z + 2 < n_slab) a[k] += t[k][2];
+        }
+    }
     float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) asm volatile("" ::"v"(gm[k]), "v"(bt[k]));   // (loaded with the slabs: see above)
 #pragma unroll
     for (int k = 0; k < CPL; ++k) {
         const int c = l + 64 * k;
-        const float *q = src + row * ld_src + c;
-        float a = 0.f, b = 0.f, e = 0.f, f = 0.f;
-        int z = 0;
-        for (; z + 4 <= n_slab; z += 4) {
-            const float l0 = q[(int64_t)z * slab_stride], l1 = q[(int64_t)(z + 1) * slab_stride];
-            const float l2 = q[(int64_t)(z + 2) * slab_stride], l3 = q[(int64_t)(z + 3) * slab_stride];
-            a += l0, b += l1, e += l2, f += l3;
-        }
-        for (; z < n_slab; ++z) a += q[(int64_t)z * slab_stride];
-        float x = ((a + b) + (e + f)) + bias[c];
+        float x = ((a[k] + b[k]) + (e[k] + f[k])) + bi[k];
         if (p > 0.f) x = u2gnn_keep(seed, (uint32_t)row, (uint32_t)c, p) ? x * (1.f / (1.f - p)) : 0.f;
-        zz[k] = x + resid[row * ld_res + c];
+        zz[k] = x + re[k];
         Z[row * ldz + c] = live ? zz[k] : 0.f;
         s += c < d ? zz[k] : 0.f;
     }
@@ -1043,8 +1077,7 @@ __global__ void __launch_bounds__(256) slab_bias_drop_resid_ln_kernel(
 #pragma unroll
     for (int k = 0; k < CPL; ++k) {
         const int c = l + 64 * k;
-        const int cc = c < d ? c : (int)d - 1;
-        Y[row * ldy + c] = (live && c < d) ? (zz[k] - mu) * rs * gamma[cc] + beta[cc] : 0.f;
+        Y[row * ldy + c] = (live && c < d) ? (zz[k] - mu) * rs * gm[k] + bt[k] : 0.f;
     }
     if (l == 0) {
         mean[row] = live ? mu : 0.f;

@@ -141,7 +141,10 @@ __device__ __forceinline__ float lane_col(const float (&x)[DM], int c) {
 // Work split inside a 512-thread workgroup: SA_RB rows (forward, dQ: query rows; dK / dV: key rows), each
 // taken by SA_SPL waves that split the tile between them (wave s: the s-th part), lanes splitting each part;
 // a row's partial results merge across its lanes (butterfly) and then across its waves (LDS).
-constexpr int SA_SPL = 2, SA_RB = SA_WAVES / SA_SPL;
+#ifndef SA_SPL_
+#define SA_SPL_ 2   // (A/B: -DSA_SPL_=1 builds one wave per row, 8 rows per workgroup)
+#endif
+constexpr int SA_SPL = SA_SPL_, SA_RB = SA_WAVES / SA_SPL;
 
 // Staging of records [t0, t0 + KT) of a compact [Np][W] array (W = WA + WB + WC, each a multiple of 4) into the
 // LDS arrays a [KT][WA], b [KT][WB], c [KT][WC]; records at or past Np are zeros.  PS (pair split): record t goes to

@@ -145,6 +145,13 @@ __device__ __forceinline__ float lane_col(const float (&x)[DM], int c) {
 #define SA_SPL_ 2   // (A/B: -DSA_SPL_=1 builds one wave per row, 8 rows per workgroup)
 #endif
 constexpr int SA_SPL = SA_SPL_, SA_RB = SA_WAVES / SA_SPL;
+// the fused forward (attention + tail, rows_pad >= 1024) at DM = 4 takes one wave per row, 8 rows per workgroup: half the
+// workgroups, each staging the keys and the weight chunk once for 8 rows (round 6, C5 shape: 16.7 vs 18.0 us at
+// N = 1 914, 30.2 vs 38.5 at 3 900 per layer forward; the backward keeps 2, tools/small_layer_bench.py)
+#ifndef SA_FWD_SPL_
+#define SA_FWD_SPL_ 1
+#endif
+constexpr int SA_FWD_SPL = SA_FWD_SPL_;
 
 // Staging of records [t0, t0 + KT) of a compact [Np][W] array (W = WA + WB + WC, each a multiple of 4) into the
 // LDS arrays a [KT][WA], b [KT][WB], c [KT][WC]; records at or past Np are zeros.  PS (pair split): record t goes to
@@ -231,30 +238,32 @@ template <int DM> struct TailRowB;
 template <int DM> constexpr int ls_nw() { return (ls_hc<DM>() / 64 + SA_SPL - 1) / SA_SPL; }   // units per lane per chunk
 template <int DM>
 __device__ void tail_hd_load(const LsP &T, int i, int sp, int h0, float (&hvs)[ls_nw<DM>()]);
-template <int DM> __device__ void tail_fwd_rows(const LsP &T, int i, int rw, int sp, const float (&of)[DM], bool fin,
-                                                const TailRowF<DM> &rp, Stage<DM, ls_hc<DM>(), true> &sg, float *smem);
+template <int DM, int SPL> __device__ void tail_fwd_rows(const LsP &T, int i, int rw, int sp, const float (&of)[DM],
+                                                         bool fin, const TailRowF<DM> &rp,
+                                                         Stage<DM, ls_hc<DM>(), true> &sg, float *smem);
 template <int DM> __device__ void tail_bwd_rows(const LsP &T, int i, int rw, int sp, bool fin, const TailRowB<DM> &rp,
                                                 Stage<DM, ls_hc<DM>(), false> &sg, float (&hvs)[ls_nw<DM>()],
                                                 float (&g)[DM], float &dl, float *smem);
-template <int DM> constexpr int tail_smem_floats();
+template <int DM, int SPL = SA_SPL> constexpr int tail_smem_floats();
 
 // ---- forward: one query row per SA_SPL waves -------------------------------------------------------------
 // TAIL (ABI u2gnn_layer_small_fwd, rows_pad >= 1024): the same workgroup then runs the row-local tail of its
 // SA_RB rows (tail_fwd_rows): the attention output O never makes a round trip before its out-projection
-template <int DM, bool TAIL>
+template <int DM, bool TAIL, int SPL = SA_SPL>
 __global__ void __launch_bounds__(SA_NT, sa_min_waves<DM>()) sa_fwd_kernel(SaP P, LsP T) {
+    constexpr int RB = SA_WAVES / SPL;   // rows per workgroup
     constexpr int SA_KT = sa_kt_f<DM>();
-    constexpr int PART = SA_KT / SA_SPL, NP = PART / 128;   // keys per wave per tile; key pairs per lane
+    constexpr int PART = SA_KT / SPL, NP = PART / 128;   // keys per wave per tile; key pairs per lane
     // keys per lane between rescales (their K rows are live in registers), at most the wave's part of the tile
     // (2 NP keys per lane): a larger chunk would index ks past the tile for DM >= 8
     constexpr int CU = (DM <= 8 ? 8 : 4) < 2 * NP ? (DM <= 8 ? 8 : 4) : 2 * NP;
     static_assert(NP >= 1 && PART % 128 == 0, "a wave's part of the key tile: whole 128-key rounds");
     __shared__ __attribute__((aligned(16))) float ks[SA_KT][DM];
     __shared__ __attribute__((aligned(16))) float vs[SA_KT][DM];
-    __shared__ float xw[SA_RB][SA_SPL][2 + DM];
+    __shared__ float xw[RB][SPL][2 + DM];
     const uint64_t seed = u2gnn_seed(P.seed, P.epoch);
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, rw = w % SA_RB, sp = w / SA_RB;
-    const int i = blockIdx.x * SA_RB + rw;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, rw = w % RB, sp = w / RB;
+    const int i = blockIdx.x * RB + rw;
     const bool live = i < P.N;
     const float *kvc = sa_kvc<DM>(P.ctx, P.Np);
     float q[DM], o[DM];
@@ -328,7 +337,7 @@ __global__ void __launch_bounds__(SA_NT, sa_min_waves<DM>()) sa_fwd_kernel(SaP P
         for (int c = 0; c < DM; ++c) o[c] = wave_sum(o[c] * f);
         m = M;
     }
-    // then the row's SA_SPL waves, in wave order
+    // then the row's SPL waves, in wave order
     if (lane == 0) {
         xw[rw][sp][0] = m;
         xw[rw][sp][1] = l;
@@ -345,13 +354,13 @@ __global__ void __launch_bounds__(SA_NT, sa_min_waves<DM>()) sa_fwd_kernel(SaP P
     if (fin) {
         float M = xw[rw][0][0];
 #pragma unroll
-        for (int x = 1; x < SA_SPL; ++x) M = fmaxf(M, xw[rw][x][0]);
+        for (int x = 1; x < SPL; ++x) M = fmaxf(M, xw[rw][x][0]);
         float L = 0.f;
 #pragma unroll
         for (int c = 0; c < DM; ++c) o[c] = 0.f;
         if (M != -INFINITY) {
 #pragma unroll
-            for (int x = 0; x < SA_SPL; ++x) {
+            for (int x = 0; x < SPL; ++x) {
                 const float f = xw[rw][x][0] == -INFINITY ? 0.f : fexp2(xw[rw][x][0] - M);
                 L = fmaf(xw[rw][x][1], f, L);
 #pragma unroll
@@ -372,8 +381,8 @@ __global__ void __launch_bounds__(SA_NT, sa_min_waves<DM>()) sa_fwd_kernel(SaP P
     }
     if constexpr (TAIL) {
         SX_STAMP(0, 4);
-        __shared__ __attribute__((aligned(16))) float tsm[tail_smem_floats<DM>()];
-        tail_fwd_rows<DM>(T, i, rw, sp, of, fin, rp, sg, tsm);
+        __shared__ __attribute__((aligned(16))) float tsm[tail_smem_floats<DM, SPL>()];
+        tail_fwd_rows<DM, SPL>(T, i, rw, sp, of, fin, rp, sg, tsm);
         SX_STAMP(0, 9);
     }
 }
@@ -1099,7 +1108,9 @@ __global__ void __launch_bounds__(LS_NT, ls_min_waves<DM>()) ls_bwd_kernel(LsP P
 // sp + SA_SPL, ...), the waves' partial sums combined in wave order; the row's finishing wave (sp 0) runs the
 // row prologue / epilogue.  Same arithmetic per unit as ls_fwd_kernel / ls_bwd_kernel; the hidden-unit partial
 // sums are taken in another order (per wave, then across the two waves).
-template <int DM> constexpr int tail_smem_floats() { return 2 * ls_hc<DM>() * DM + ls_hc<DM>() + SA_RB * (4 * DM + 4); }
+template <int DM, int SPL> constexpr int tail_smem_floats() {
+    return 2 * ls_hc<DM>() * DM + ls_hc<DM>() + SA_WAVES / SPL * (4 * DM + 4);
+}
 
 // The tail's global operands are issued ahead of the phase that uses them (round 6, tools/sl_stamps.py: each
 // dependent global round trip cost about a microsecond of the workgroup's chain): the row operands (TailRowF /
@@ -1159,16 +1170,17 @@ __device__ void tail_hd_load(const LsP &T, int i, int sp, int h0, float (&hvs)[l
     }
 }
 
-template <int DM>
+template <int DM, int SPL>
 __device__ void tail_fwd_rows(const LsP &T, int i, int rw, int sp, const float (&of)[DM], bool fin,
                               const TailRowF<DM> &rp, Stage<DM, ls_hc<DM>(), true> &sg, float *smem) {
     static_assert(LS_NT == SA_NT, "the tail's staging runs on the attention workgroup");
+    constexpr int RB = SA_WAVES / SPL;
     constexpr int HC = ls_hc<DM>(), NPR = (HC / 2 + 63) / 64;   // 64-lane rounds of unit pairs per chunk
     float (*w1s)[DM] = reinterpret_cast<float (*)[DM]>(smem);
     float (*w2s)[DM] = reinterpret_cast<float (*)[DM]>(smem + HC * DM);
     float *b1s = smem + 2 * HC * DM;
     float (*xs)[DM] = reinterpret_cast<float (*)[DM]>(b1s + HC);
-    float (*xz)[SA_SPL][DM] = reinterpret_cast<float (*)[SA_SPL][DM]>(b1s + HC + SA_RB * DM);
+    float (*xz)[SPL][DM] = reinterpret_cast<float (*)[SPL][DM]>(b1s + HC + RB * DM);
     const int lane = threadIdx.x & 63;
     const bool live = i < T.N;
     const u2gnn_small_tail_args &A = T.a;
@@ -1212,7 +1224,7 @@ __device__ void tail_fwd_rows(const LsP &T, int i, int rw, int sp, const float (
         // unit pairs (h, h + 1), h = 2 (64 k + lane): one dropout hash per pair gives both keep bits, Hd written as
         // float2 (round 6: a hash per unit was a fifth of the kernel's VALU issue)
 #pragma unroll 2
-        for (int k = sp; k < NPR; k += SA_SPL) {
+        for (int k = sp; k < NPR; k += SPL) {
             const int h = 2 * (64 * k + lane);
             if (h >= HC || h0 + h >= T.ffp) break;   // (ffp even: h + 1 < ffp too)
             float a0 = b1s[h], a1 = b1s[h + 1];
@@ -1257,7 +1269,7 @@ __device__ void tail_fwd_rows(const LsP &T, int i, int rw, int sp, const float (
     for (int k = 0; k < DM; ++k) {
         float t = xz[rw][0][k];
 #pragma unroll
-        for (int y = 1; y < SA_SPL; ++y) t += xz[rw][y][k];
+        for (int y = 1; y < SPL; ++y) t += xz[rw][y][k];
         zp[k] = t;
     }
     float z2 = 0.f, x2 = 0.f, mu2 = 0.f, rs2 = 0.f;
@@ -1444,8 +1456,10 @@ int small_fwd_launch(const SaP &P, const LsP &T, hipStream_t st) {
     const int64_t nt = (int64_t)P.Np * 3 * (DM / 4);
     hipLaunchKernelGGL(sa_proj_kernel<DM>, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, st, P);
     const dim3 grid((unsigned)((P.Np + SA_RB - 1) / SA_RB));
-    if (P.Np >= SMALL_FUSE_ROWS) {
-        hipLaunchKernelGGL((sa_fwd_kernel<DM, true>), grid, dim3(SA_NT), 0, st, P, T);
+    if (P.Np >= SMALL_FUSE_ROWS) {   // (DM = 4: one wave per row, SA_FWD_SPL; wider rows spill registers there)
+        constexpr int FS = DM <= 4 ? SA_FWD_SPL : SA_SPL, RBF = SA_WAVES / FS;
+        hipLaunchKernelGGL((sa_fwd_kernel<DM, true, FS>), dim3((unsigned)((P.Np + RBF - 1) / RBF)), dim3(SA_NT), 0, st, P,
+                           T);
     } else {
         hipLaunchKernelGGL((sa_fwd_kernel<DM, false>), grid, dim3(SA_NT), 0, st, P, LsP{});
         hipLaunchKernelGGL((ls_fwd_kernel<DM, true>), dim3((unsigned)P.Np), dim3(LS_NT), 0, st, T);

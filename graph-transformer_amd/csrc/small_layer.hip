@@ -152,6 +152,13 @@ constexpr int SA_SPL = SA_SPL_, SA_RB = SA_WAVES / SA_SPL;
 #define SA_FWD_SPL_ 1
 #endif
 constexpr int SA_FWD_SPL = SA_FWD_SPL_;
+#ifndef SA_BWD_SPL_
+#define SA_BWD_SPL_ 2   // (A/B: 1 = the fused tail backward + dQ walk at one wave per row, SA_BWD_MINW waves per SIMD)
+#endif
+#ifndef SA_BWD_MINW
+#define SA_BWD_MINW 2
+#endif
+constexpr int SA_BWD_SPL = SA_BWD_SPL_;
 
 // Staging of records [t0, t0 + KT) of a compact [Np][W] array (W = WA + WB + WC, each a multiple of 4) into the
 // LDS arrays a [KT][WA], b [KT][WB], c [KT][WC]; records at or past Np are zeros.  PS (pair split): record t goes to
@@ -235,15 +242,16 @@ struct LsP {
 template <int DM, int HC, bool BIAS> struct Stage;
 template <int DM> struct TailRowF;
 template <int DM> struct TailRowB;
-template <int DM> constexpr int ls_nw() { return (ls_hc<DM>() / 64 + SA_SPL - 1) / SA_SPL; }   // units per lane per chunk
-template <int DM>
-__device__ void tail_hd_load(const LsP &T, int i, int sp, int h0, float (&hvs)[ls_nw<DM>()]);
+template <int DM, int SPL = SA_SPL> constexpr int ls_nw() { return (ls_hc<DM>() / 64 + SPL - 1) / SPL; }   // units per lane per chunk
+template <int DM, int SPL>
+__device__ void tail_hd_load(const LsP &T, int i, int sp, int h0, float (&hvs)[ls_nw<DM, SPL>()]);
 template <int DM, int SPL> __device__ void tail_fwd_rows(const LsP &T, int i, int rw, int sp, const float (&of)[DM],
                                                          bool fin, const TailRowF<DM> &rp,
                                                          Stage<DM, ls_hc<DM>(), true> &sg, float *smem);
-template <int DM> __device__ void tail_bwd_rows(const LsP &T, int i, int rw, int sp, bool fin, const TailRowB<DM> &rp,
-                                                Stage<DM, ls_hc<DM>(), false> &sg, float (&hvs)[ls_nw<DM>()],
-                                                float (&g)[DM], float &dl, float *smem);
+template <int DM, int SPL> __device__ void tail_bwd_rows(const LsP &T, int i, int rw, int sp, bool fin,
+                                                         const TailRowB<DM> &rp, Stage<DM, ls_hc<DM>(), false> &sg,
+                                                         float (&hvs)[ls_nw<DM, SPL>()], float (&g)[DM], float &dl,
+                                                         float *smem);
 template <int DM, int SPL = SA_SPL> constexpr int tail_smem_floats();
 
 // ---- forward: one query row per SA_SPL waves -------------------------------------------------------------
@@ -390,17 +398,19 @@ __global__ void __launch_bounds__(SA_NT, sa_min_waves<DM>()) sa_fwd_kernel(SaP P
 // ---- backward dQ: one query row per SA_SPL waves; also the row's record for dK / dV -----------------------
 // TAIL (ABI u2gnn_layer_small_bwd, rows_pad >= 1024): the workgroup first runs the row-local tail backward of
 // its SA_RB rows (tail_bwd_rows), whose dO row and delta then feed the dQ walk from LDS
-template <int DM, bool TAIL>
-__global__ void __launch_bounds__(SA_NT, sa_min_waves<DM>()) sa_bwd_q_kernel(SaP P, LsP T) {
+template <int DM, bool TAIL, int SPL = SA_SPL>
+__global__ void __launch_bounds__(SA_NT, SPL == 1 ? SA_BWD_MINW : sa_min_waves<DM>()) sa_bwd_q_kernel(SaP P,
+                                                                                                         LsP T) {
+    constexpr int RB = SA_WAVES / SPL;   // rows per workgroup
     constexpr int SA_KT = sa_kt_f<DM>();
-    constexpr int PART = SA_KT / SA_SPL, NP = PART / 128;
+    constexpr int PART = SA_KT / SPL, NP = PART / 128;
     static_assert(NP >= 1 && PART % 128 == 0, "a wave's part of the key tile: whole 128-key rounds");
     __shared__ __attribute__((aligned(16))) float ks[SA_KT][DM];
     __shared__ __attribute__((aligned(16))) float vs[SA_KT][DM];
-    __shared__ float xw[SA_RB][SA_SPL][DM];
+    __shared__ float xw[RB][SPL][DM];
     const uint64_t seed = u2gnn_seed(P.seed, P.epoch);
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, rw = w % SA_RB, sp = w / SA_RB;
-    const int i = blockIdx.x * SA_RB + rw;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, rw = w % RB, sp = w / RB;
+    const int i = blockIdx.x * RB + rw;
     const bool live = i < P.N;
     const float *st = sa_st(P.ctx);
     float q[DM], g[DM], dq[DM];
@@ -409,18 +419,18 @@ __global__ void __launch_bounds__(SA_NT, sa_min_waves<DM>()) sa_bwd_q_kernel(SaP
     for (int c = 0; c < DM; ++c) q[c] = g[c] = dq[c] = 0.f;
     if constexpr (TAIL) {   // dO and delta of the row from the tail backward (every wave of the row)
         SX_STAMP(1, 0);
-        __shared__ __attribute__((aligned(16))) float tsm[tail_smem_floats<DM>()];
+        __shared__ __attribute__((aligned(16))) float tsm[tail_smem_floats<DM, SPL>()];
         const bool fin = sp == 0 && i < P.Np;
         Stage<DM, ls_hc<DM>(), false> sg;   // every operand of the tail's first chunk, issued together
-        float hvs[ls_nw<DM>()];
+        float hvs[ls_nw<DM, SPL>()];
         TailRowB<DM> rp;
         rp.load(T, i);   // (every wave: the LayerNorm2^T operands are the first loads in flight)
 #if SX_BWD_ORDER
         __builtin_amdgcn_sched_barrier(0);
 #endif
         sg.load(T, 0);
-        tail_hd_load<DM>(T, i, sp, 0, hvs);
-        tail_bwd_rows<DM>(T, i, rw, sp, fin, rp, sg, hvs, g, dl, tsm);
+        tail_hd_load<DM, SPL>(T, i, sp, 0, hvs);
+        tail_bwd_rows<DM, SPL>(T, i, rw, sp, fin, rp, sg, hvs, g, dl, tsm);
         SX_STAMP(1, 1);
     }
     if (live) {
@@ -483,7 +493,7 @@ __global__ void __launch_bounds__(SA_NT, sa_min_waves<DM>()) sa_bwd_q_kernel(SaP
     for (int c = 0; c < DM; ++c) {
         float t = xw[rw][0][c];
 #pragma unroll
-        for (int x = 1; x < SA_SPL; ++x) t += xw[rw][x][c];
+        for (int x = 1; x < SPL; ++x) t += xw[rw][x][c];
         dq[c] = t;
     }
     float *row = P.out + (int64_t)i * P.ld_out;   // the Q block of dQKV
@@ -1150,22 +1160,22 @@ struct TailRowB {
 };
 
 // the row's ReLU image Hd over this wave's units of chunk h0
-template <int DM>
-__device__ void tail_hd_load(const LsP &T, int i, int sp, int h0, float (&hvs)[ls_nw<DM>()]) {
+template <int DM, int SPL>
+__device__ void tail_hd_load(const LsP &T, int i, int sp, int h0, float (&hvs)[ls_nw<DM, SPL>()]) {
     constexpr int NU = ls_hc<DM>() / 64;
     const int lane = threadIdx.x & 63;
     const float *hrow = T.a.Hd + (int64_t)i * T.ffp;
     // every load issued unconditionally (clamped index, masked after): a conditional load into a zeroed register
     // compiled to load -> s_waitcnt vmcnt(0) per unit, a memory round trip each (tools/isa_waits.py)
-    float v[ls_nw<DM>()];
+    float v[ls_nw<DM, SPL>()];
 #pragma unroll
-    for (int u = 0; u < ls_nw<DM>(); ++u) {
-        const int k = sp + SA_SPL * u, h = 64 * k + lane;
+    for (int u = 0; u < ls_nw<DM, SPL>(); ++u) {
+        const int k = sp + SPL * u, h = 64 * k + lane;
         v[u] = hrow[min(h0 + h, T.ffp - 1)];
     }
 #pragma unroll
-    for (int u = 0; u < ls_nw<DM>(); ++u) {
-        const int k = sp + SA_SPL * u, h = 64 * k + lane;
+    for (int u = 0; u < ls_nw<DM, SPL>(); ++u) {
+        const int k = sp + SPL * u, h = 64 * k + lane;
         hvs[u] = (k < NU && h0 + h < T.ffp) ? v[u] : 0.f;
     }
 }
@@ -1286,16 +1296,16 @@ __device__ void tail_fwd_rows(const LsP &T, int i, int rw, int sp, const float (
 
 // the tail backward of the row; on return every wave of the row holds its dO row (g) and delta (dl).  sg, hvs: the
 // first chunk's weights and this wave's units of the row's ReLU image, already in flight
-template <int DM>
+template <int DM, int SPL>
 __device__ void tail_bwd_rows(const LsP &T, int i, int rw, int sp, bool fin, const TailRowB<DM> &rp,
-                              Stage<DM, ls_hc<DM>(), false> &sg, float (&hvs)[ls_nw<DM>()], float (&g)[DM], float &dl,
+                              Stage<DM, ls_hc<DM>(), false> &sg, float (&hvs)[ls_nw<DM, SPL>()], float (&g)[DM], float &dl,
                               float *smem) {
-    constexpr int HC = ls_hc<DM>(), NU = HC / 64, NW = ls_nw<DM>();
+    constexpr int HC = ls_hc<DM>(), NU = HC / 64, NW = ls_nw<DM, SPL>(), RB = SA_WAVES / SPL;
     float (*w1s)[DM] = reinterpret_cast<float (*)[DM]>(smem);
     float (*w2s)[DM] = reinterpret_cast<float (*)[DM]>(smem + HC * DM);
     float (*fs)[DM] = reinterpret_cast<float (*)[DM]>(smem + 2 * HC * DM);
-    float (*xz)[SA_SPL][DM] = reinterpret_cast<float (*)[SA_SPL][DM]>(smem + 2 * HC * DM + SA_RB * DM);
-    float (*gs)[DM + 4] = reinterpret_cast<float (*)[DM + 4]>(smem + 2 * HC * DM + SA_RB * DM * (1 + SA_SPL));
+    float (*xz)[SPL][DM] = reinterpret_cast<float (*)[SPL][DM]>(smem + 2 * HC * DM + RB * DM);
+    float (*gs)[DM + 4] = reinterpret_cast<float (*)[DM + 4]>(smem + 2 * HC * DM + RB * DM * (1 + SPL));
     const int lane = threadIdx.x & 63;
     const bool live = i < T.N;
     const u2gnn_small_tail_args &A = T.a;
@@ -1329,12 +1339,12 @@ __device__ void tail_bwd_rows(const LsP &T, int i, int rw, int sp, bool fin, con
         for (int u = 0; u < NW; ++u) hc[u] = hvs[u];
         if (h0 + HC < T.ffp) {   // the next chunk, in flight under this one
             sg.load(T, h0 + HC);
-            tail_hd_load<DM>(T, i, sp, h0 + HC, hvs);
+            tail_hd_load<DM, SPL>(T, i, sp, h0 + HC, hvs);
         }
         if (h0 == 0) SX_STAMP(1, 6);
 #pragma unroll 4
         for (int u = 0; u < NW; ++u) {
-            const int k = sp + SA_SPL * u, h = 64 * k + lane;
+            const int k = sp + SPL * u, h = 64 * k + lane;
             if (k >= NU || h0 + h >= T.ffp) break;
             float w1[DM], w2[DM];
 #pragma unroll
@@ -1360,7 +1370,7 @@ __device__ void tail_bwd_rows(const LsP &T, int i, int rw, int sp, bool fin, con
         for (int k = 0; k < DM; ++k) {
             float t = xz[rw][0][k];
 #pragma unroll
-            for (int y = 1; y < SA_SPL; ++y) t += xz[rw][y][k];
+            for (int y = 1; y < SPL; ++y) t += xz[rw][y][k];
             xp[k] = t;
         }
         float dx1 = 0.f, dz1 = 0.f, da = 0.f, dov = 0.f, dlt = 0.f;
@@ -1471,7 +1481,9 @@ template <int DM>
 int small_bwd_launch(const SaP &P, const LsP &T, hipStream_t st) {
     const dim3 grid((unsigned)((P.Np + SA_RB - 1) / SA_RB));
     if (P.Np >= SMALL_FUSE_ROWS) {
-        hipLaunchKernelGGL((sa_bwd_q_kernel<DM, true>), grid, dim3(SA_NT), 0, st, P, T);
+        constexpr int BS = DM <= 4 ? SA_BWD_SPL : SA_SPL, RBB = SA_WAVES / BS;
+        hipLaunchKernelGGL((sa_bwd_q_kernel<DM, true, BS>), dim3((unsigned)((P.Np + RBB - 1) / RBB)), dim3(SA_NT), 0, st,
+                           P, T);
     } else {
         hipLaunchKernelGGL((ls_bwd_kernel<DM, true>), dim3((unsigned)P.Np), dim3(LS_NT), 0, st, T);
         hipLaunchKernelGGL((sa_bwd_q_kernel<DM, false>), grid, dim3(SA_NT), 0, st, P, LsP{});

@@ -568,10 +568,15 @@ __global__ void __launch_bounds__(256) attn_softmax_kernel(const float *S, int64
         const bool in = c < n_pad;
         float pv[4], pdv[4];
         bool kp[4];
+        // one finaliser per column pair (c % 4 == 0: pairs c / 2 and c / 2 + 1), the same bits as u2gnn_keep_rk per
+        // column (round 6: the per-column form hashed every pair twice; the hash's two quarter-rate multiplies made
+        // it a third of this kernel's VALU issue)
+        const uint32_t h0 = u2gnn_pair_hash(rkey, (uint32_t)(c >> 1)), h1 = u2gnn_pair_hash(rkey, (uint32_t)(c >> 1) + 1u);
+        kp[0] = u2gnn_keep_lo(h0, thr), kp[1] = u2gnn_keep_hi(h0, thr);
+        kp[2] = u2gnn_keep_lo(h1, thr), kp[3] = u2gnn_keep_hi(h1, thr);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             pv[j] = e[i][j] * inv;
-            kp[j] = u2gnn_keep_rk(rkey, (uint32_t)(c + j), thr);
             pdv[j] = kp[j] ? pv[j] * ks : (sgn ? -pv[j] : 0.f);
         }
         if (in) {

@@ -42,17 +42,30 @@ static_assert(MT_RB == 4, "the butterfly below reduces 16 weight rows x 4 activa
 // (output o = 4 i + r) are reduced by one transpose butterfly -- at step s the lanes with bit 5-s set keep the
 // upper half of their outputs and trade the lower half with lane ^ (32 >> s): 63 shuffles instead of 64 wave
 // sums -- after which lane l holds output l complete.  Fixed order: deterministic.
+// The 16 weight rows of one batch, loaded ahead of their phase (round 6): every load unconditional from a clamped
+// address (rows i >= valid and elements k >= klim read a valid word and are zeroed at use), so a kernel can issue
+// all its phases' weights with the first loads and pay one memory round trip instead of one per phase
 template <int CPLK>
-__device__ __forceinline__ float dot16x4(const float *W, int64_t ldw, int i0, int valid, int klim, const float *xs,
-                                         int ldx, int lane) {
+struct W16 {
+    float v[16][CPLK];
+    int valid, klim;
+    __device__ __forceinline__ void load(const float *W, int64_t ldw, int i0, int valid_, int klim_, int lane) {
+        valid = valid_, klim = klim_;
+        const int il = valid_ > 0 ? valid_ - 1 : 0, kl = klim_ > 0 ? klim_ - 1 : 0;
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+#pragma unroll
+            for (int m = 0; m < CPLK; ++m) v[i][m] = W[(int64_t)(i0 + min(i, il)) * ldw + min(lane + 64 * m, kl)];
+    }
+};
+
+template <int CPLK>
+__device__ __forceinline__ float dot16x4w(const W16<CPLK> &W, const float *xs, int ldx, int lane) {
     float wv[16][CPLK];
 #pragma unroll
     for (int i = 0; i < 16; ++i)
 #pragma unroll
-        for (int m = 0; m < CPLK; ++m) {
-            const int k = lane + 64 * m;
-            wv[i][m] = (i < valid && k < klim) ? W[(int64_t)(i0 + i) * ldw + k] : 0.f;
-        }
+        for (int m = 0; m < CPLK; ++m) wv[i][m] = (i < W.valid && lane + 64 * m < W.klim) ? W.v[i][m] : 0.f;
     float xv[MT_RB][CPLK];
 #pragma unroll
     for (int r = 0; r < MT_RB; ++r)
@@ -80,6 +93,14 @@ __device__ __forceinline__ float dot16x4(const float *W, int64_t ldw, int i0, in
         }
     }
     return v[0];
+}
+
+template <int CPLK>
+__device__ __forceinline__ float dot16x4(const float *W, int64_t ldw, int i0, int valid, int klim, const float *xs,
+                                         int ldx, int lane) {
+    W16<CPLK> w;
+    w.load(W, ldw, i0, valid, klim, lane);
+    return dot16x4w<CPLK>(w, xs, ldx, lane);
 }
 
 // the waves' partial sums of one row in a fixed pairwise order
@@ -112,21 +133,38 @@ __global__ void __launch_bounds__(MT_NT) mid_tail_fwd_kernel(MtP P) {
     const float ks = drop ? 1.f / (1.f - A.p) : 1.f;
     const uint32_t thr = u2gnn_keep_thr(A.p);
     const uint64_t s1 = u2gnn_seed(A.seed_drop1, P.epoch), sff = u2gnn_seed(A.seed_dropff, P.epoch);
+    const int lr = lane & 3, li = lane >> 2;   // the (activation row, weight row) of this lane's butterfly output
+    const int h0 = ch * MT_HC, nu = min(MT_HC, ffp - h0);
+    // every global operand of the wave's first batch in each phase, issued together with the O rows (round 6: the
+    // phases' weight, bias and residual loads were seven dependent memory round trips, tools/isa_waits.py)
+    // (dp <= 128: the three weight batches fit the registers; wider rows load each batch at its phase)
+    constexpr bool PF = CPL <= 2;
+    W16<CPL> wo_p, w1_p;
+    W16<MT_HC / 64> w2_p;
+    if constexpr (PF) {
+        wo_p.load(A.W_o, DP, 16 * w, d - 16 * w, DP, lane);
+        w1_p.load(A.W1, DP, h0 + 16 * w, nu - 16 * w, DP, lane);
+        w2_p.load(A.W2 + h0, ffp, 16 * w, DP - 16 * w, nu, lane);
+    }
+    const float bo_p = A.b_o[min(16 * w + li, DP - 1)], x_p = A.X[(int64_t)(r0 + lr) * DP + min(16 * w + li, DP - 1)];
+    const float b1_p = A.b1[min(h0 + 16 * w + li, ffp - 1)];
+    const float g1 = A.n1_w[min(t, d - 1)], b1n = A.n1_b[min(t, d - 1)];
     for (int e = t; e < MT_RB * DP / 4; e += MT_NT) {
         const int r = e / (DP / 4), k = 4 * (e % (DP / 4));
         *reinterpret_cast<float4 *>(&os[r][k]) = mt_ld4(A.O + (int64_t)(r0 + r) * DP + k);
     }
     __syncthreads();
-    const int lr = lane & 3, li = lane >> 2;   // the (activation row, weight row) of this lane's butterfly output
     // a3.3: z1[c] = drop1(sum_k O[k] W_o[c][k] + b_o[c]) + x[c]; wave w takes the 16-column batches w, w + NW, ...
     for (int b = w; b < DP / 16; b += NW) {
         const int c = 16 * b + li, row = r0 + lr;
-        float v = dot16x4<CPL>(A.W_o, DP, 16 * b, d - 16 * b, DP, &os[0][0], DP, lane);
+        const bool first = b == w;   // (bias and residual prefetched; the weights too when PF)
+        float v = (PF && first) ? dot16x4w<CPL>(wo_p, &os[0][0], DP, lane)
+                        : dot16x4<CPL>(A.W_o, DP, 16 * b, d - 16 * b, DP, &os[0][0], DP, lane);
         float z = 0.f;
         if (c < d && row < N) {
-            v += A.b_o[c];
+            v += first ? bo_p : A.b_o[c];
             if (drop) v = u2gnn_keep(s1, (uint32_t)row, (uint32_t)c, A.p) ? v * ks : 0.f;
-            z = v + A.X[(int64_t)row * DP + c];
+            z = v + (first ? x_p : A.X[(int64_t)row * DP + c]);
         }
         zs[lr][c] = z;
     }
@@ -155,12 +193,11 @@ __global__ void __launch_bounds__(MT_NT) mid_tail_fwd_kernel(MtP P) {
 #pragma unroll
     for (int r = 0; r < MT_RB; ++r)
         rs[r] = rsqrtf(wsum_fixed<NW>(red[r]) / (float)d + A.eps);
-    const float g1 = c < d ? A.n1_w[c] : 0.f, b1n = c < d ? A.n1_b[c] : 0.f;
 #pragma unroll
     for (int r = 0; r < MT_RB; ++r) {
         const int row = r0 + r;
         const bool live = row < N;
-        const float x1 = (live && c < d) ? (z[r] - mu[r]) * rs[r] * g1 + b1n : 0.f;
+        const float x1 = (live && c < d) ? (z[r] - mu[r]) * rs[r] * g1 + b1n : 0.f;   // (g1, b1n: column t's)
         if (c < DP) {
             xs[r][c] = x1;
             if (ch == 0) {
@@ -175,12 +212,13 @@ __global__ void __launch_bounds__(MT_NT) mid_tail_fwd_kernel(MtP P) {
     }
     __syncthreads();
     // a3.4 FFN1: h_j = dropff(relu(sum_k x1[k] W1[j][k] + b1[j])) for the chunk's units j, 16-unit batches
-    const int h0 = ch * MT_HC, nu = min(MT_HC, ffp - h0);
     for (int b = w; b < MT_HC / 16; b += NW) {
         const int u = 16 * b + li, j = h0 + u, row = r0 + lr;
-        float h = dot16x4<CPL>(A.W1, DP, h0 + 16 * b, nu - 16 * b, DP, &xs[0][0], DP, lane);
+        const bool first = b == w;
+        float h = (PF && first) ? dot16x4w<CPL>(w1_p, &xs[0][0], DP, lane)
+                        : dot16x4<CPL>(A.W1, DP, h0 + 16 * b, nu - 16 * b, DP, &xs[0][0], DP, lane);
         if (u < nu && row < N) {
-            h = fmaxf(h + A.b1[j], 0.f);
+            h = fmaxf(h + (first ? b1_p : A.b1[j]), 0.f);
             if (drop) h = u2gnn_keep_rk(u2gnn_row_key(sff, (uint32_t)row), (uint32_t)j, thr) ? h * ks : 0.f;
         } else {
             h = 0.f;
@@ -199,7 +237,8 @@ __global__ void __launch_bounds__(MT_NT) mid_tail_fwd_kernel(MtP P) {
     // batches, lanes along the units
     for (int b = w; b < DP / 16; b += NW) {
         const int cc = 16 * b + li;
-        const float v = dot16x4<MT_HC / 64>(A.W2 + h0, ffp, 16 * b, DP - 16 * b, nu, &hs[0][0], MT_HC, lane);
+        const float v = (PF && b == w) ? dot16x4w<MT_HC / 64>(w2_p, &hs[0][0], MT_HC, lane)
+                               : dot16x4<MT_HC / 64>(A.W2 + h0, ffp, 16 * b, DP - 16 * b, nu, &hs[0][0], MT_HC, lane);
         P.slabs[((int64_t)ch * rows_pad + r0 + lr) * DP + cc] = v;
     }
 }

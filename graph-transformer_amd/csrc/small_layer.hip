@@ -50,8 +50,18 @@ constexpr int SA_WAVES = 8;    // rows (forward, dQ) or key rows (dK / dV) per 5
 constexpr int SA_NT = 64 * SA_WAVES;
 // keys (forward, dQ) / queries (dK, dV) staged in LDS per tile: 32 KB of K and V (16-34 KB of query
 // records): two to four workgroups per CU
-template <int DM> constexpr int sa_kt_f() { return 4096 / DM > 256 ? 4096 / DM / 256 * 256 : 256; }   // 128-key rounds per wave
-template <int DM> constexpr int sa_kt_b() { return 2048 / DM > 128 ? 2048 / DM / 128 * 128 : 128; }   // 64-query rounds per wave
+#ifndef SA_KT4_F
+#define SA_KT4_F 0   // (A/B: key-tile size of the DM = 4 forward / dQ walks; 0 = the formula below)
+#endif
+#ifndef SA_KT4_B
+#define SA_KT4_B 0   // (A/B: query-tile size of the DM = 4 dK / dV walk)
+#endif
+template <int DM> constexpr int sa_kt_f() {   // 128-key rounds per wave
+    return DM == 4 && SA_KT4_F ? SA_KT4_F : 4096 / DM > 256 ? 4096 / DM / 256 * 256 : 256;
+}
+template <int DM> constexpr int sa_kt_b() {   // 64-query rounds per wave
+    return DM == 4 && SA_KT4_B ? SA_KT4_B : 2048 / DM > 128 ? 2048 / DM / 128 * 128 : 128;
+}
 constexpr float SA_LOG2E = 1.4426950408889634f;
 // 2^x as one v_exp_f32: exp2f adds a 6-instruction rescue of results below 2^-126 (round 6: the walks are
 // VALU-issue-bound, SQ_INSTS_VALU); softmax terms that small are flushed to 0 -- they are below fp32 resolution of
@@ -1459,7 +1469,10 @@ int ls_run(const u2gnn_small_tail_args *a, bool bwd, void *stream) {
 // ---- a whole small-width layer (ABI u2gnn_layer_small_fwd / _bwd): fused where the rows allow --------------
 // rows_pad >= 1024 (the tail's STAGED split): attention forward + tail in one launch, tail backward + the dQ walk
 // in one launch; below that the tail's DIRECT split keeps its own launches
-constexpr int64_t SMALL_FUSE_ROWS = 1024;   // (C5: fused 0.541 / 0.543 vs separate 0.587 / 0.594 ms, one session)
+#ifndef SMALL_FUSE_ROWS_
+#define SMALL_FUSE_ROWS_ 1024
+#endif
+constexpr int64_t SMALL_FUSE_ROWS = SMALL_FUSE_ROWS_;   // (C5: fused 0.541 / 0.543 vs separate 0.587 / 0.594 ms, one session)
 
 template <int DM>
 int small_fwd_launch(const SaP &P, const LsP &T, hipStream_t st) {

@@ -99,6 +99,9 @@ def parse():
                     help="C4 at N=1: also run the other BASELINE configs (c5, c2, c3) in the same process and "
                          "report each as an object of the C4 line (0 = skip)")
     ap.add_argument("--config-steps", type=int, default=30, help="timed steps of each embedded config line")
+    ap.add_argument("--neighbors-line", type=int, default=1,
+                    help="C4 at N=1: also time the paper-semantics neighbour attention (--attention neighbors) in a "
+                         "child process and report it as the 'neighbors' object (0 = skip)")
     ap.add_argument("--workload", default="c4", choices=["c4", "c5", "c2", "c3"],
                     help="c4 = U2GNN-Sup COLLAB (the headline metric); c5 = U2GNN-UnSup REDDIT-M5K (HBM-bound); "
                          "c2 = U2GNN-Sup IMDBBINARY, c3 = U2GNN-UnSup PTC (BASELINE configs[1], [2]: real data, "
@@ -811,6 +814,29 @@ def run_small(args):
     return out
 
 
+def neighbors_line(args):
+    """The paper-semantics neighbour attention (--attention neighbors: every node attends
+    over its own k+1 sampled neighbours, csrc/window_attn.hip) on the same C4 batches, timed by this script in a
+    child process (its own HIP context; this process has released its cached memory) -- the line that process
+    prints, reduced to its timing fields."""
+    import subprocess
+    torch.cuda.empty_cache()
+    cmd = [sys.executable, os.path.abspath(__file__), "--attention", "neighbors", "--steps", "10", "--warmup", "3",
+           "--configs", "0", "--neighbors-line", "0", "--cpu-baseline", "0", "--fp32-steps", "0", "--pipeline-steps",
+           "0", "--no-roofline", "--precision", args.precision]
+    t0 = time.perf_counter()
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+        line = json.loads(r.stdout.strip().splitlines()[-1])
+    except (subprocess.TimeoutExpired, ValueError, IndexError) as e:
+        return {"error": f"{type(e).__name__}: {str(e)[:200]}"}
+    keep = ("metric", "value", "unit", "ms_per_step", "steps", "warmup", "dtype", "config", "host_issue_ms_per_step")
+    out = {k: line[k] for k in keep if k in line}
+    out["run_s"] = round(time.perf_counter() - t0, 1)
+    out["command"] = " ".join(["python", "bench.py"] + cmd[2:])
+    return out
+
+
 def largest_kernel(workload):
     """The largest kernel (device time) of a workload's step from the committed kernel-trace summary of THIS build
     (profiles/<round>/*_<workload>_kstats.json, tools/wl_trace.sh), or a note."""
@@ -1074,6 +1100,8 @@ def main():
             sub["run_s"] = round(time.perf_counter() - t0, 1)
             out[wl] = sub
             torch.cuda.empty_cache()
+    if rank == 0 and world == 1 and args.neighbors_line and args.attention == "nodes" and not args.force_dist:
+        out["neighbors"] = neighbors_line(args)
     if rank == 0:
         emit(out)
     if dist is not None:

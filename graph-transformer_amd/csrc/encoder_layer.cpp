@@ -59,6 +59,7 @@ Dims make_dims(const u2gnn_layer_dims *a) {
     D.prec_fwd = a->precision;
     if (a->precision == U2GNN_PREC_BF16X3 && (a->flags & U2GNN_LAYER_FWD_F32)) D.prec_fwd = U2GNN_PREC_F32;
     if (a->precision == U2GNN_PREC_BF16X3 && (a->flags & U2GNN_LAYER_FWD_X6)) D.prec_fwd = U2GNN_PREC_BF16X6;
+    if (a->precision == U2GNN_PREC_BF16X3 && (a->flags & U2GNN_LAYER_FWD_H3)) D.prec_fwd = U2GNN_PREC_F16X3;
     D.deep_wgrad = (a->flags & U2GNN_LAYER_DEEP_WGRAD) != 0;
     D.window = a->window;
     return D;
@@ -156,6 +157,15 @@ void probe_mark(int role, bool end, hipStream_t st, bool plan) {
     if (end) ++g_probe.n;
 }
 
+// f16x3 operand pre-scale exponents (u2gnn_hip.h h3_exp_a / h3_exp_b; kernels.H3_EXP / h3_prob_exp mirror them):
+// activations and weights by 2^6, the probability image (entries ~1/N, at most 1/(1-p)) by 2^(15 - ceil(log2(1/(1-p))))
+constexpr int32_t kH3Exp = 6;
+int32_t h3_prob_exp(float pd) {
+    int32_t e = 15;
+    for (float m = 1.f / (1.f - pd); m > 1.f; m *= 0.5f) --e;
+    return e;
+}
+
 struct G {   // one GEMM launch (defaults = plain store)
     u2gnn_gemm_args a;
     G(const float *A, const float *B, float *C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
@@ -166,6 +176,7 @@ struct G {   // one GEMM launch (defaults = plain store)
         a.split_k = 1;
         a.alpha = 1.f;
         a.precision = prec;
+        if (prec == U2GNN_PREC_F16X3) a.h3_exp_a = a.h3_exp_b = kH3Exp;
     }
     G &ta() { a.trans_a = 1; return *this; }
     G &tb() { a.trans_b = 1; return *this; }
@@ -231,7 +242,7 @@ int gemm_split(Arena &W, const Dims &D, const float *A, const float *B, float *C
                int64_t lda, int64_t ldb, int64_t ldc, bool ta, float alpha, bool accumulate, const int64_t *rblk,
                const int64_t *cblk, bool deep, hipStream_t st, bool clamp_a = false, int prec = -1, int role = 0,
                hipStream_t red_st = nullptr, Defer *df = nullptr, float **slabs_out = nullptr,
-               int64_t *nslab_out = nullptr) {
+               int64_t *nslab_out = nullptr, int32_t h3_exp_a = kH3Exp) {
     if (prec < 0) prec = D.prec;
     const bool f32 = prec == U2GNN_PREC_F32;
     const int64_t bk = f32 ? 16 : 32;
@@ -248,6 +259,7 @@ int gemm_split(Arena &W, const Dims &D, const float *A, const float *B, float *C
         if (ta) g.ta();
         g.a.alpha = alpha;
         g.a.clamp_a = clamp_a;
+        if (prec == U2GNN_PREC_F16X3) g.a.h3_exp_a = h3_exp_a;
         const bool big = M % 256 == 0 && N % 128 == 0 && (M / 256) * (N / 128) >= U2GNN_BIG_TILE_BLOCKS;
         g.epi(accumulate ? U2GNN_EPI_ACCUM : U2GNN_EPI_STORE).tile(big ? 256 : 64);
         probe_mark(role, false, st, plan);
@@ -291,6 +303,7 @@ int gemm_split(Arena &W, const Dims &D, const float *A, const float *B, float *C
         if (ta) g.ta();
         g.a.alpha = alpha;
         g.a.clamp_a = clamp_a;
+        if (prec == U2GNN_PREC_F16X3) g.a.h3_exp_a = h3_exp_a;
         g.epi(accumulate ? U2GNN_EPI_ACCUM : U2GNN_EPI_STORE).tile(t_group);
         if (df && df->gemms && !accumulate) {
             df->gemm.push_back(g.a);
@@ -308,6 +321,7 @@ int gemm_split(Arena &W, const Dims &D, const float *A, const float *B, float *C
     g.a.split_k = (int32_t)split;
     g.a.slab_stride = M * N;
     g.a.clamp_a = clamp_a;
+    if (prec == U2GNN_PREC_F16X3) g.a.h3_exp_a = h3_exp_a;
     g.tile(t_group);
     const int64_t rb0 = rblk ? rblk[0] : M, rb1 = rblk ? rblk[1] : M;
     const int64_t cb0 = cblk ? cblk[0] : N, cb1 = cblk ? cblk[1] : N;
@@ -492,7 +506,7 @@ int qk_tile(int64_t Np) { return (Np % 256 == 0 && (Np / 256) * (Np / 128) >= 25
 // of the test seed's step across 0)
 bool fused_attn(const Dims &D) {
     return !D.window && !small_attn(D) && D.prec_fwd != U2GNN_PREC_F32 && D.prec_fwd != U2GNN_PREC_BF16X6 &&
-           D.dp <= 384;
+           D.prec_fwd != U2GNN_PREC_F16X3 && D.dp <= 384;
 }
 
 // the row-local tail of a small-width layer (u2gnn_layer_tail_small_*, small_layer.hip): every precision when the
@@ -592,7 +606,8 @@ int layer_fwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
             U2GNN_TRY(u2gnn_attn_softmax_fwd(S, Np, drop ? nullptr : c.Pd, c.Pd, Np, N, Np, N, Np, pd, s->attn,
                                              nullptr, 0, st));
         U2GNN_TRY(gemm_split(W, D, c.Pd, V, c.O, Np, dp, Np, Np, 3 * dp, dp, false, 1.f, false, nullptr, nullptr,
-                             false, st, drop, prec, U2GNN_ROLE_PV));
+                             false, st, drop, prec, U2GNN_ROLE_PV, nullptr, nullptr, nullptr, nullptr,
+                             h3_prob_exp(pd)));
     }
     if (small_attn(D)) {
         // a3.3 + a3.4: run by u2gnn_layer_small_fwd above
@@ -823,11 +838,12 @@ int layer_bwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
     return (W.overflow || CA.overflow) ? U2GNN_E_ARG : U2GNN_OK;
 }
 
+constexpr int32_t FWD_FLAGS = U2GNN_LAYER_FWD_F32 | U2GNN_LAYER_FWD_X6 | U2GNN_LAYER_FWD_H3;
 bool dims_ok(const u2gnn_layer_dims *a) {
     return a && a->N >= 1 && a->d >= 1 && a->ff >= 1 && rup(a->d, 64) <= 1024 &&
            (a->precision == U2GNN_PREC_F32 || a->precision == U2GNN_PREC_BF16X3 || a->precision == U2GNN_PREC_BF16) &&
-           ((a->flags & (U2GNN_LAYER_FWD_F32 | U2GNN_LAYER_FWD_X6)) == 0 || a->precision == U2GNN_PREC_BF16X3) &&
-           (a->flags & (U2GNN_LAYER_FWD_F32 | U2GNN_LAYER_FWD_X6)) != (U2GNN_LAYER_FWD_F32 | U2GNN_LAYER_FWD_X6) &&
+           ((a->flags & FWD_FLAGS) == 0 || a->precision == U2GNN_PREC_BF16X3) &&
+           __builtin_popcount((unsigned)(a->flags & FWD_FLAGS)) <= 1 &&   // at most one forward policy
            a->window >= 0 && a->window <= 32 && (a->window == 0 || a->N % a->window == 0);
 }
 

@@ -20,6 +20,7 @@
 //   * split-K writes fp32 partial slabs (deterministic; reduced by u2gnn_slab_reduce).
 #include "gemm_common.h"
 
+#include <cmath>
 #include <cstring>
 
 
@@ -257,20 +258,28 @@ __device__ __forceinline__ void g2r_bf(__amdgpu_buffer_rsrc_t rs, const int (&vo
     }
 }
 
-// NPL bf16 planes of each staged element (1: bf16, 2: hi / lo of bf16x3, 3: hi / mid / lo of bf16x6), plane q
-// at p0 + q * pst
+// NPL: the planes of each staged element (1: bf16, 2: hi / lo of bf16x3, 3: hi / mid / lo of bf16x6,
+// NPL_F16X3: fp16 hi / lo), plane q at p0 + q * pst
+constexpr int NPL_F16X3 = 4;
+template <int NPL> constexpr int nplanes() { return NPL == NPL_F16X3 ? 2 : NPL; }
 template <int NPL>
 __device__ __forceinline__ void split_planes(float x0, float x1, unsigned (&o)[3]) {
     if constexpr (NPL == 3) split3(x0, x1, o[0], o[1], o[2]);
+    else if constexpr (NPL == NPL_F16X3) split2h(x0, x1, o[0], o[1]);
     else split2<NPL == 2>(x0, x1, o[0], o[1]);
 }
 
 template <int R, int BK, int LDK, bool T, int NPL, int NT, bool CLAMP = false>
-__device__ __forceinline__ void r2s_bf(__bf16 *p0, int pst, int tid, const float4 (&v_)[R * BK / (4 * NT)]) {
+__device__ __forceinline__ void r2s_bf(__bf16 *p0, int pst, int tid, const float4 (&v_)[R * BK / (4 * NT)],
+                                       float sc = 1.f) {
     constexpr int NF = R * BK / (4 * NT);
     float4 v[NF];
 #pragma unroll
     for (int i = 0; i < NF; ++i) v[i] = CLAMP ? clamp0(v_[i]) : v_[i];
+    if constexpr (NPL == NPL_F16X3) {   // the operand's pre-scale (a power of two: exact)
+#pragma unroll
+        for (int i = 0; i < NF; ++i) v[i] = make_float4(v[i].x * sc, v[i].y * sc, v[i].z * sc, v[i].w * sc);
+    }
 #ifdef U2GNN_EXP_NOSTAGE
     return;
 #endif
@@ -294,7 +303,7 @@ __device__ __forceinline__ void r2s_bf(__bf16 *p0, int pst, int tid, const float
         split_planes<NPL>(v[i].x, v[i].y, a);
         split_planes<NPL>(v[i].z, v[i].w, b);
 #pragma unroll
-        for (int q = 0; q < NPL; ++q) *reinterpret_cast<uint2 *>(p0 + q * pst + o) = make_uint2(a[q], b[q]);
+        for (int q = 0; q < nplanes<NPL>(); ++q) *reinterpret_cast<uint2 *>(p0 + q * pst + o) = make_uint2(a[q], b[q]);
     }
 }
 
@@ -321,9 +330,9 @@ __device__ __forceinline__ bf16x8 ld_frag(const __bf16 *img, int r0, int ks, int
 
 // The main loop and epilogue of one output tile (tile coordinates from the caller: the plain launch's
 // XCD-aware map, or the grouped launch's job walk).
-// bf16 planes held per staged operand: two for bf16 / bf16x3 (the bf16 kind leaves its second plane unused, so
-// both kinds share one LDS layout), three for bf16x6
-template <int NPL> constexpr int planes_of() { return NPL < 2 ? 2 : NPL; }
+// 16-bit planes held per staged operand: two for bf16 / bf16x3 (the bf16 kind leaves its second plane unused, so
+// both kinds share one LDS layout) and f16x3, three for bf16x6
+template <int NPL> constexpr int planes_of() { return NPL < 2 ? 2 : nplanes<NPL>(); }
 // bf16 elements of the kernel's LDS image (two stages of the planes of both operands)
 template <int BM, int BN, int BK, bool TA, bool TB, int NPL = 2>
 constexpr int bf16_smem_elems() {
@@ -432,15 +441,16 @@ __device__ __forceinline__ void gemm_bf16_body(const GemmP &P, int tmi, int tni,
         const __bf16 *Bh = Ah + PL * AE;
 #pragma unroll
         for (int ks = 0; ks < BK / 16; ++ks) {
-            bf16x8 a[NPL][TM], b[NPL][TN];
+            constexpr int NP = nplanes<NPL>();
+            bf16x8 a[NP][TM], b[NP][TN];
 #pragma unroll
             for (int i = 0; i < TM; ++i)
 #pragma unroll
-                for (int q = 0; q < NPL; ++q) a[q][i] = ld_frag<BM, LDK, TA>(Ah + q * AE, wm * WTM + i * 32, ks, lane);
+                for (int q = 0; q < NP; ++q) a[q][i] = ld_frag<BM, LDK, TA>(Ah + q * AE, wm * WTM + i * 32, ks, lane);
 #pragma unroll
             for (int j = 0; j < TN; ++j)
 #pragma unroll
-                for (int q = 0; q < NPL; ++q) b[q][j] = ld_frag<BN, LDK, !TB>(Bh + q * BE, wn * WTN + j * 32, ks, lane);
+                for (int q = 0; q < NP; ++q) b[q][j] = ld_frag<BN, LDK, !TB>(Bh + q * BE, wn * WTN + j * 32, ks, lane);
 #pragma unroll
             for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -448,17 +458,24 @@ __device__ __forceinline__ void gemm_bf16_body(const GemmP &P, int tmi, int tni,
                     // B fragment first: the accumulator holds the tile transposed, so each lane
                     // owns 4 consecutive output columns of one row (16-byte epilogue accesses).
                     // Smallest terms first: bf16x6 mid.mid, hi.lo, lo.hi, hi.mid, mid.hi; bf16x3 hi.lo, lo.hi;
-                    // then hi.hi
-                    if constexpr (NPL == 3) {
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[1][j], a[1][i], acc[i][j], 0, 0, 0);
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[0][j], a[2][i], acc[i][j], 0, 0, 0);
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[2][j], a[0][i], acc[i][j], 0, 0, 0);
+                    // then hi.hi (f16x3: hi.lo, lo.hi, hi.hi on the fp16 matrix cores, same fragment layout)
+                    if constexpr (NPL == NPL_F16X3) {
+                        const auto h = [](bf16x8 v) { return __builtin_bit_cast(f16x8, v); };
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(h(b[0][j]), h(a[1][i]), acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(h(b[1][j]), h(a[0][i]), acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(h(b[0][j]), h(a[0][i]), acc[i][j], 0, 0, 0);
+                    } else {
+                        if constexpr (NPL == 3) {
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[1][j], a[1][i], acc[i][j], 0, 0, 0);
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[0][j], a[2][i], acc[i][j], 0, 0, 0);
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[2][j], a[0][i], acc[i][j], 0, 0, 0);
+                        }
+                        if constexpr (NPL >= 2) {
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[0][j], a[1][i], acc[i][j], 0, 0, 0);
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[1][j], a[0][i], acc[i][j], 0, 0, 0);
+                        }
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[0][j], a[0][i], acc[i][j], 0, 0, 0);
                     }
-                    if constexpr (NPL >= 2) {
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[0][j], a[1][i], acc[i][j], 0, 0, 0);
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[1][j], a[0][i], acc[i][j], 0, 0, 0);
-                    }
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[0][j], a[0][i], acc[i][j], 0, 0, 0);
                 }
         }
     };
@@ -487,27 +504,33 @@ __device__ __forceinline__ void gemm_bf16_body(const GemmP &P, int tmi, int tni,
         g2r_bf<NFB>(rsB, voB, (0) * kstepB, rb0);
         g2r_bf<NFA>(rsA, voA, (min(1, nk - 1)) * kstepA, ra1);
         g2r_bf<NFB>(rsB, voB, (min(1, nk - 1)) * kstepB, rb1);
-        r2s_bf<BM, BK, LDK, TA, NPL, NT, CLAMP>(stage(0), AE, tid, ra0);
-        r2s_bf<BN, BK, LDK, !TB, NPL, NT>(stage(0) + PL * AE, BE, tid, rb0);
+        r2s_bf<BM, BK, LDK, TA, NPL, NT, CLAMP>(stage(0), AE, tid, ra0, P.h3_sa);
+        r2s_bf<BN, BK, LDK, !TB, NPL, NT>(stage(0) + PL * AE, BE, tid, rb0, P.h3_sb);
         __syncthreads();
         for (int t = 0; t < nk; t += 2) {
             if constexpr (kStageA) g2r_bf<NFA>(rsA, voA, (min(t + 2, nk - 1)) * kstepA, ra0);
             if constexpr (kStageB) g2r_bf<NFB>(rsB, voB, (min(t + 2, nk - 1)) * kstepB, rb0);
             compute(stage(0));
-            if constexpr (kStageA) r2s_bf<BM, BK, LDK, TA, NPL, NT, CLAMP>(stage(1), AE, tid, ra1);
-            if constexpr (kStageB) r2s_bf<BN, BK, LDK, !TB, NPL, NT>(stage(1) + PL * AE, BE, tid, rb1);
+            if constexpr (kStageA) r2s_bf<BM, BK, LDK, TA, NPL, NT, CLAMP>(stage(1), AE, tid, ra1, P.h3_sa);
+            if constexpr (kStageB) r2s_bf<BN, BK, LDK, !TB, NPL, NT>(stage(1) + PL * AE, BE, tid, rb1, P.h3_sb);
             U2GNN_LOOP_SYNC();
             if (t + 1 < nk) {
                 if constexpr (kStageA) g2r_bf<NFA>(rsA, voA, (min(t + 3, nk - 1)) * kstepA, ra1);
                 if constexpr (kStageB) g2r_bf<NFB>(rsB, voB, (min(t + 3, nk - 1)) * kstepB, rb1);
                 compute(stage(1));
-                if constexpr (kStageA) r2s_bf<BM, BK, LDK, TA, NPL, NT, CLAMP>(stage(0), AE, tid, ra0);
-                if constexpr (kStageB) r2s_bf<BN, BK, LDK, !TB, NPL, NT>(stage(0) + PL * AE, BE, tid, rb0);
+                if constexpr (kStageA) r2s_bf<BM, BK, LDK, TA, NPL, NT, CLAMP>(stage(0), AE, tid, ra0, P.h3_sa);
+                if constexpr (kStageB) r2s_bf<BN, BK, LDK, !TB, NPL, NT>(stage(0) + PL * AE, BE, tid, rb0, P.h3_sb);
                 U2GNN_LOOP_SYNC();
             }
         }
     }
 
+    if constexpr (NPL == NPL_F16X3) {   // undo the operand pre-scales (exact)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) acc[i][j] *= P.h3_inv;
+    }
     if constexpr (DSL) {
         ds_lds_store(P, P.C + (int64_t)zi * P.slab_stride, acc, m0 + wm * WTM, n0 + wn * WTN, wave, lane, smem, dsl);
         return;
@@ -538,6 +561,18 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_bf16x6_kernel(GemmP P) {
     int tmi, tni, zi;
     tile_coords(P.gm, P.gn, tmi, tni, zi);
     gemm_bf16_body<BM, BN, WM, WN, 16, TA, TB, EPI, 3, CLAMP>(P, tmi, tni, zi, smem);
+}
+
+// U2GNN_PREC_F16X3: the bf16x3 body over two fp16 planes per operand (fp16 MFMA), the forward products only
+template <int BM, int BN, int WM, int WN, int BK, bool TA, bool TB, int EPI, bool CLAMP>
+__global__ void __launch_bounds__(64 * WM * WN) gemm_f16x3_kernel(GemmP P) {
+    if constexpr (EPI == U2GNN_EPI_BIAS_DROP_RESID || EPI == U2GNN_EPI_BIAS_RELU_DROP ||
+                  EPI == U2GNN_EPI_BIAS_DROP_RESID_LN)
+        P.seed = u2gnn_seed(P.seed, P.epoch);   // graph replay: device-resident seed epoch
+    __shared__ __attribute__((aligned(16))) __bf16 smem[bf16_smem_elems<BM, BN, BK, TA, TB, NPL_F16X3>()];
+    int tmi, tni, zi;
+    tile_coords(P.gm, P.gn, tmi, tni, zi);
+    gemm_bf16_body<BM, BN, WM, WN, BK, TA, TB, EPI, NPL_F16X3, CLAMP>(P, tmi, tni, zi, smem);
 }
 
 // Grouped launch (u2gnn_gemm_group): several STORE products of one tile shape, each A^T B (the weight
@@ -586,6 +621,10 @@ void launch_kernel(const GemmP &P, dim3 grid, hipStream_t st) {
     } else if constexpr (KIND == U2GNN_PREC_BF16X6) {
         constexpr int WM = BM == 256 ? 4 : 2, WN = 2;
         hipLaunchKernelGGL((gemm_bf16x6_kernel<BM, BN, WM, WN, TA, TB, EPI, CLAMP>), grid, dim3(64 * WM * WN), 0, st, P);
+    } else if constexpr (KIND == U2GNN_PREC_F16X3) {
+        constexpr int WM = BM == 256 ? 4 : 2, WN = 2;
+        hipLaunchKernelGGL((gemm_f16x3_kernel<BM, BN, WM, WN, CFG_BK<VAR>, TA, TB, EPI, CLAMP>), grid,
+                           dim3(64 * WM * WN), 0, st, P);
     } else {
         constexpr int WM = BM == 256 ? 4 : 2, WN = 2;   // 256x128 tiles run 8 waves (4x2)
         hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, WM, WN, CFG_BK<VAR>, TA, TB, EPI,
@@ -594,7 +633,9 @@ void launch_kernel(const GemmP &P, dim3 grid, hipStream_t st) {
     }
 }
 
-// the epilogues the bf16x6 kernels are built for (the forward products; u2gnn_gemm refuses the others)
+// the kinds built for the forward products only (A never transposed, x6_epi's epilogues)
+constexpr bool fwd_kind(int k) { return k == U2GNN_PREC_BF16X6 || k == U2GNN_PREC_F16X3; }
+// the epilogues the bf16x6 / f16x3 kernels are built for (the forward products; u2gnn_gemm refuses the others)
 constexpr bool x6_epi(int e) {
     return e == U2GNN_EPI_STORE || e == U2GNN_EPI_BIAS || e == U2GNN_EPI_BIAS_DROP_RESID ||
            e == U2GNN_EPI_BIAS_RELU_DROP || e == U2GNN_EPI_ACCUM || e == U2GNN_EPI_STORE_ROWSTAT ||
@@ -613,11 +654,11 @@ int launch_epi(const GemmP &P, int epi, int split, bool clamp_a, hipStream_t st)
             return u2gnn_launch_status();
         }
     }
-    if (KIND == U2GNN_PREC_BF16X6 && !x6_epi(epi)) return U2GNN_E_ARG;
+    if (fwd_kind(KIND) && !x6_epi(epi)) return U2GNN_E_ARG;
     switch (epi) {
 #define U2GNN_CASE(E)                                                                    \
     case E:                                                                              \
-        if constexpr (KIND != U2GNN_PREC_BF16X6 || x6_epi(E)) launch_kernel<KIND, BM, BN, VAR, TA, TB, E>(P, grid, st); \
+        if constexpr (!fwd_kind(KIND) || x6_epi(E)) launch_kernel<KIND, BM, BN, VAR, TA, TB, E>(P, grid, st); \
         break;
         U2GNN_CASE(U2GNN_EPI_STORE)
         U2GNN_CASE(U2GNN_EPI_BIAS)
@@ -635,7 +676,7 @@ int launch_epi(const GemmP &P, int epi, int split, bool clamp_a, hipStream_t st)
                 return U2GNN_E_ARG;
             break;
         case U2GNN_EPI_ATTN_DS_SIGNED:   // delta as STORE_ROWDOT partials: its own instantiation
-            if constexpr (KIND == U2GNN_PREC_BF16X6) return U2GNN_E_ARG;
+            if constexpr (fwd_kind(KIND)) return U2GNN_E_ARG;
             else if (P.rowvec_parts > 1)
                 launch_kernel<KIND, BM, BN, VAR, TA, TB, EPI_DS_SIGNED_PARTS>(P, grid, st);
             else
@@ -657,7 +698,7 @@ template <int KIND, int BM, int BN, int VAR = 0>
 int launch_layout(const GemmP &P, bool ta, bool tb, int epi, int split, bool clamp_a, hipStream_t st) {
     if (!ta && tb) return launch_epi<KIND, BM, BN, VAR, false, true>(P, epi, split, clamp_a, st);
     if (!ta && !tb) return launch_epi<KIND, BM, BN, VAR, false, false>(P, epi, split, clamp_a, st);
-    if constexpr (KIND != U2GNN_PREC_BF16X6)   // (bf16x6: the forward products, A never transposed)
+    if constexpr (!fwd_kind(KIND))   // (bf16x6 / f16x3: the forward products, A never transposed)
         if (ta && !tb) return launch_epi<KIND, BM, BN, VAR, true, false>(P, epi, split, clamp_a, st);
     return U2GNN_E_ARG;  // A^T B^T is never needed by the encoder
 }
@@ -696,9 +737,13 @@ int gemm_plan(const u2gnn_gemm_args *a, GemmPlan &G) {
     if (a->M <= 0 || a->N <= 0 || a->K <= 0) return U2GNN_E_ARG;
     if (a->epilogue < 0 || a->epilogue > U2GNN_EPI_STORE_ROWSTAT) return U2GNN_E_ARG;
     const int prec = a->precision;
-    if (prec != U2GNN_PREC_F32 && prec != U2GNN_PREC_BF16X3 && prec != U2GNN_PREC_BF16 && prec != U2GNN_PREC_BF16X6)
+    if (prec != U2GNN_PREC_F32 && prec != U2GNN_PREC_BF16X3 && prec != U2GNN_PREC_BF16 && prec != U2GNN_PREC_BF16X6 &&
+        prec != U2GNN_PREC_F16X3)
         return U2GNN_E_ARG;
-    if (prec == U2GNN_PREC_BF16X6 && (a->trans_a || !x6_epi(a->epilogue))) return U2GNN_E_ARG;
+    if (fwd_kind(prec) && (a->trans_a || !x6_epi(a->epilogue))) return U2GNN_E_ARG;
+    if (prec == U2GNN_PREC_F16X3 ? (a->h3_exp_a < -24 || a->h3_exp_a > 24 || a->h3_exp_b < -24 || a->h3_exp_b > 24)
+                                 : (a->h3_exp_a != 0 || a->h3_exp_b != 0))
+        return U2GNN_E_ARG;
     const int split = a->split_k < 1 ? 1 : a->split_k;
     if (split > 1 && (a->epilogue != U2GNN_EPI_STORE || a->Cx2 || !a->C)) return U2GNN_E_ARG;
     if (!al16(a->A) || !al16(a->B) || (a->lda & 3) || (a->ldb & 3)) return U2GNN_E_ALIGN;
@@ -804,6 +849,9 @@ int gemm_plan(const u2gnn_gemm_args *a, GemmPlan &G) {
     P.ld_rowpart = a->ld_rowpart;
     P.rowvec_parts = a->rowvec_parts;
     P.ld_rowvec = a->ld_rowvec;
+    P.h3_sa = std::ldexp(1.f, a->h3_exp_a);
+    P.h3_sb = std::ldexp(1.f, a->h3_exp_b);
+    P.h3_inv = std::ldexp(1.f, -(a->h3_exp_a + a->h3_exp_b));
     if (e == U2GNN_EPI_BIAS_DROP_RESID_LN) {   // N == 64: the tile rule above picked 64
         P.ln_gamma = a->ln_gamma;
         P.ln_beta = a->ln_beta;
@@ -822,6 +870,8 @@ int gemm_plan(const u2gnn_gemm_args *a, GemmPlan &G) {
 }
 
 int gemm_launch(const u2gnn_gemm_args *a, GemmPlan &G, hipStream_t st) {
+    if (G.prec == U2GNN_PREC_F16X3)
+        return launch_tile<U2GNN_PREC_F16X3>(G.P, G.tile, G.ta, G.tb, G.epi, G.split, G.clamp, st);
     if (G.prec == U2GNN_PREC_BF16X6)
         return launch_tile<U2GNN_PREC_BF16X6>(G.P, G.tile, G.ta, G.tb, G.epi, G.split, G.clamp, st);
     if (G.prec == U2GNN_PREC_BF16X3)
@@ -864,7 +914,7 @@ extern "C" int u2gnn_gemm_group(const u2gnn_gemm_args *args, int32_t n, void *st
     // one launch when every job runs the same grouped kernel
     bool same = n > 1;
     for (int32_t i = 0; i < n && same; ++i)
-        same = G[i].prec == G[0].prec && G[i].prec != U2GNN_PREC_F32 && G[i].prec != U2GNN_PREC_BF16X6 &&
+        same = G[i].prec == G[0].prec && G[i].prec != U2GNN_PREC_F32 && !fwd_kind(G[i].prec) &&
                G[i].tile == G[0].tile &&
                (G[i].tile == 64 || G[i].tile == 129 || G[i].tile == 256) && !G[i].tb && G[i].epi == U2GNN_EPI_STORE &&
                (G[i].ta || !G[i].clamp);

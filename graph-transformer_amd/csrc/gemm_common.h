@@ -41,6 +41,7 @@ struct GemmP {
     int64_t ld_rowpart;
     int32_t rowvec_parts;
     int64_t ld_rowvec;
+    float h3_sa, h3_sb, h3_inv;   // f16x3: operand pre-scales 2^h3_exp_a, 2^h3_exp_b and the result's 2^-(sum)
 };
 
 

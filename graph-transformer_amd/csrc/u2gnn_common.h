@@ -125,6 +125,17 @@ __device__ __forceinline__ void split3(float x0, float x1, unsigned &h, unsigned
     asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(l) : "v"(s0), "v"(s1));
 }
 
+// (x0, x1) -> packed fp16 pairs hi, lo with hi = fp16_rne(x), lo = fp16_rne(x - hi) (U2GNN_PREC_F16X3): the
+// residual is exact in fp32, so the pair carries 22 significant bits of x (fewer where lo is subnormal)
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ void split2h(float x0, float x1, unsigned &h, unsigned &l) {
+    const f16x2 hv = {(_Float16)x0, (_Float16)x1};
+    const f16x2 lv = {(_Float16)(x0 - (float)hv.x), (_Float16)(x1 - (float)hv.y)};
+    h = __builtin_bit_cast(unsigned, hv);
+    l = __builtin_bit_cast(unsigned, lv);
+}
+
 // x2 store of four consecutive columns (col % 4 == 0): hi at 16*(col/8) + col%8, lo 8 further
 __device__ __forceinline__ void store_x2_4(__bf16 *Cx2, int64_t ldcx2, int row, int col, float4 o) {
     unsigned h0, h1, l0, l1;

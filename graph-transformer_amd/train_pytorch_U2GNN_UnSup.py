@@ -44,7 +44,7 @@ parser.add_argument("--num_timesteps", default=1, type=int, help="Timestep T ~ N
 parser.add_argument("--ff_hidden_size", default=1024, type=int, help="The hidden size for the feedforward layer")
 parser.add_argument("--num_neighbors", default=4, type=int, help="")
 parser.add_argument('--fold_idx', type=int, default=1, help='The fold index. 0-9.')
-parser.add_argument("--precision", default="fp32", choices=["fp32", "bf16x3", "mixed", "bf16", "fwd32", "fwd6"],
+parser.add_argument("--precision", default="fp32", choices=["fp32", "bf16x3", "mixed", "bf16", "fwd32", "fwd6", "fwdh"],
                     help="matrix-core precision (MI355X): fp32 exact, bf16x3 split-bf16 (~fp32), mixed (bf16x3 "
                          "with the attention-backward dS/dQ/dK products in bf16), bf16")
 parser.add_argument("--attention", default="nodes", choices=["nodes", "neighbors"],

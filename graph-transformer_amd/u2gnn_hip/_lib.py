@@ -30,8 +30,8 @@ ERRORS = {-1: "bad argument", -2: "misaligned pointer / leading dimension", -3: 
 
 EPI_STORE, EPI_BIAS, EPI_BIAS_DROP_RESID, EPI_BIAS_RELU_DROP, EPI_RELU_DROP_BWD, EPI_ACCUM, EPI_ATTN_DS, \
     EPI_ATTN_DS_SIGNED, EPI_ATTN_DS_RECOMP, EPI_BIAS_DROP_RESID_LN, EPI_STORE_ROWDOT, EPI_STORE_ROWSTAT = range(12)
-ABI_VERSION = 17   # include/u2gnn_hip.h U2GNN_ABI_VERSION
-PREC_F32, PREC_BF16X3, PREC_BF16, PREC_BF16X6 = 0, 1, 2, 3
+ABI_VERSION = 18   # include/u2gnn_hip.h U2GNN_ABI_VERSION
+PREC_F32, PREC_BF16X3, PREC_BF16, PREC_BF16X6, PREC_F16X3 = 0, 1, 2, 3, 4
 
 
 class GemmArgs(ctypes.Structure):
@@ -63,6 +63,7 @@ class GemmArgs(ctypes.Structure):
         # ABI v8: delta = rowsum(dO * O) from the dO GEMM's epilogue (STORE_ROWDOT -> ATTN_DS_SIGNED)
         ("rowpart", c_void_p), ("ld_rowpart", c_int64),
         ("rowvec_parts", c_int32), ("rowvec_reserved", c_int32), ("ld_rowvec", c_int64),
+        ("h3_exp_a", c_int32), ("h3_exp_b", c_int32),   # ABI v18: f16x3 operand pre-scales
     ]
 
 
@@ -121,6 +122,7 @@ LAYER_DEEP_WGRAD = 1
 LAYER_ATTN_BWD_BF16 = 2   # precision "mixed": dS, dQ, dK on plain bf16 (ABI v5)
 LAYER_FWD_F32 = 4         # precision "fwd32": forward products exact fp32, backward bf16x3 (ABI v14)
 LAYER_FWD_X6 = 8          # precision "fwd6": forward products bf16x6 (three-plane split), backward bf16x3 (ABI v17)
+LAYER_FWD_H3 = 16         # precision "fwdh": forward products f16x3 (two-plane fp16 split), backward bf16x3 (ABI v18)
 ROLE_QK, ROLE_PV, ROLE_DS, ROLE_DV, ROLE_DQ, ROLE_DK = range(1, 7)   # u2gnn_probe_arm roles
 
 I64, F32, VP, I32 = c_int64, c_float, c_void_p, c_int32

@@ -254,7 +254,8 @@ ROLE_PREC: Dict[str, str] = {}
 # precision "fwd32": the forward products exact fp32 (so the forward's ReLU decisions carry fp32 rounding
 # only), the backward bf16x3 (u2gnn_hip.h U2GNN_LAYER_FWD_F32); precision "fwd6": the
 # forward products on the three-plane bf16x6 split (fp32-accurate products at 6/16 of the bf16 MFMA rate instead
-# of 1/16), the backward bf16x3 (U2GNN_LAYER_FWD_X6)
+# of 1/16), the backward bf16x3 (U2GNN_LAYER_FWD_X6); precision "fwdh": the forward products on the two-plane fp16
+# split f16x3 (~2^-21 per product at the bf16x3 rate), the backward bf16x3 (U2GNN_LAYER_FWD_H3)
 FWD_ROLES = ("in_proj", "qk", "pv", "out_proj", "ffn1", "ffn2")
 
 
@@ -268,17 +269,20 @@ def _rp(role: str, prec: str) -> str:
         return "fp32" if role in FWD_ROLES else "bf16x3"
     if prec == "fwd6":
         return "bf16x6" if role in FWD_ROLES else "bf16x3"
+    if prec == "fwdh":
+        return "f16x3" if role in FWD_ROLES else "bf16x3"
     return "bf16" if (prec == "bf16x3" and role in ROLE_BF16) else prec
 
 
 def _gemm_split(A, B, C, M, N, Kd, lda, ldb, ldc, trans_a=False, trans_b=False, alpha=1.0, accumulate=False,
-                prec="fp32", rblk=None, cblk=None, target=448, flops=None, deep=False, clamp_a=False, target256=240):
+                prec="fp32", rblk=None, cblk=None, target=448, flops=None, deep=False, clamp_a=False, target256=240,
+                h3_exp=None):
     """C (+)= alpha * op(A) . op(B) with deterministic split-K: when the tile grid alone would
     leave most of the 256 CUs idle (skinny outputs with a deep node dimension: P.V, Pd^T.dO,
     dS.K, dS^T.Q, the weight gradients, dH.W1, dQKV.W_in), the depth is cut into fp32 slabs
     (>= 4 K-tiles each, ~target workgroups) and one streaming pass sums them into C — applying
     alpha, accumulation and an optional padded->real block map (rblk, cblk).  clamp_a: A is the
-    signed probability image (read as Pd)."""
+    signed probability image (read as Pd).  h3_exp: the f16x3 operand pre-scales (kernels.gemm)."""
     bk = 16 if prec == "fp32" else 32
     # tiny: an accumulating product of <= 16 tiles and <= 16 K steps (C2's dX += dQKV W_in) as one short launch
     tiny = accumulate and Kd <= 512 and (M // 64) * (N // 64) <= 16
@@ -289,7 +293,7 @@ def _gemm_split(A, B, C, M, N, Kd, lda, ldb, ldc, trans_a=False, trans_b=False, 
         K.gemm(A, B, C, M, N, Kd, lda, ldb, ldc, trans_a=trans_a, trans_b=trans_b, alpha=alpha,
                epilogue=E.EPI_ACCUM if accumulate else E.EPI_STORE, precision=prec,
                tile=256 if (M % 256 == 0 and N % 128 == 0 and (M // 256) * (N // 128) >= BIG_TILE_BLOCKS) else 64,
-               flops=flops, clamp_a=clamp_a)
+               flops=flops, clamp_a=clamp_a, h3_exp=h3_exp)
         return
     if prec != "fp32" and M % 256 == 0 and N % 128 == 0 and (M // 256) * (N // 128) >= 32:
         # 256x128 blocks (8 waves, one block per CU): the skinny attention products
@@ -306,11 +310,11 @@ def _gemm_split(A, B, C, M, N, Kd, lda, ldb, ldc, trans_a=False, trans_b=False, 
     if split == 1 and not mapped:
         K.gemm(A, B, C, M, N, Kd, lda, ldb, ldc, trans_a=trans_a, trans_b=trans_b, alpha=alpha,
                epilogue=E.EPI_ACCUM if accumulate else E.EPI_STORE, precision=prec, tile=t, flops=flops,
-               clamp_a=clamp_a)
+               clamp_a=clamp_a, h3_exp=h3_exp)
         return
     slabs = torch.empty(split, M, N, device=C.device, dtype=torch.float32)
     K.gemm(A, B, slabs, M, N, Kd, lda, ldb, N, trans_a=trans_a, trans_b=trans_b, split_k=split, slab_stride=M * N,
-           precision=prec, tile=t, flops=flops, clamp_a=clamp_a)
+           precision=prec, tile=t, flops=flops, clamp_a=clamp_a, h3_exp=h3_exp)
     K.slab_reduce(slabs, split, M * N, M, N, N, rblk or (M, M), cblk or (N, N), C, ldc, alpha=alpha,
                   accumulate=accumulate)
 
@@ -336,12 +340,12 @@ def in_bias_grad(dQKV, Np, dp, d, out):
 
 
 def _gemm_nodes_k(A, B, C, M, N, Kd, lda, ldb, ldc, trans_a=False, alpha=1.0, prec="fp32", flops=None,
-                  clamp_a=False, grouped=False):
+                  clamp_a=False, grouped=False, h3_exp=None):
     """The skinny attention products whose depth is the node dimension (N = dp, K = Np).  grouped: dQ / dK,
     which the native executor issues as one grouped launch -- half the 256x128 block target each
     (encoder_layer.cpp gemm_split), so both paths cut the same split-K slabs."""
     _gemm_split(A, B, C, M, N, Kd, lda, ldb, ldc, trans_a=trans_a, alpha=alpha, prec=prec, flops=flops,
-                clamp_a=clamp_a, target256=120 if grouped else 240)
+                clamp_a=clamp_a, target256=120 if grouped else 240, h3_exp=h3_exp)
 
 
 def ffn2_split(dp: int, mfma: bool, Np: int, ffp: int) -> int:
@@ -396,7 +400,8 @@ def _attn_split(Q, Kt, V, N, Np, dp, pd, seeds, prec, att, dev):
     K.attn_softmax_fwd(S, Np, None if pd > 0 else Pd, Pd, Np, N, Np, N, Np, pd, seeds.get(SITE_ATTN, 0))
     del S
     O = torch.empty(Np, dp, device=dev, dtype=f32)
-    _gemm_nodes_k(Pd, V, O, Np, dp, Np, Np, 3 * dp, dp, prec=_rp("pv", prec), flops=att, clamp_a=pd > 0)
+    _gemm_nodes_k(Pd, V, O, Np, dp, Np, Np, 3 * dp, dp, prec=_rp("pv", prec), flops=att, clamp_a=pd > 0,
+                  h3_exp=(K.h3_prob_exp(pd), K.H3_EXP))   # (f16x3: the probability image's pre-scale)
     return Pd, O
 
 

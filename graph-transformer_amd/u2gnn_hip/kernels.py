@@ -13,7 +13,8 @@ import torch
 from . import _lib
 from ._lib import check, hip_lib
 
-PREC = {"fp32": _lib.PREC_F32, "bf16x3": _lib.PREC_BF16X3, "bf16": _lib.PREC_BF16, "bf16x6": _lib.PREC_BF16X6}
+PREC = {"fp32": _lib.PREC_F32, "bf16x3": _lib.PREC_BF16X3, "bf16": _lib.PREC_BF16, "bf16x6": _lib.PREC_BF16X6,
+        "f16x3": _lib.PREC_F16X3}
 
 
 def _p(t):
@@ -65,14 +66,31 @@ def gemm_symbol(precision, M, N, split_k, tile, trans_a, trans_b, epilogue, clam
     bm, bn, wm, bk = {256: (256, 128, 4, 32), 129: (128, 128, 2, 16)}.get(tile, (tile, tile, 2, 32))
     if precision == "bf16x6":   # three-plane kernel, 16-deep K step on every tile
         return f"gemm_bf16x6_kernel<{bm}, {bn}, {wm}, 2, {b(trans_a)}, {b(trans_b)}, {int(epilogue)}, {b(clamp_a)}>"
+    if precision == "f16x3":   # two fp16 planes, the bf16x3 K steps
+        return (f"gemm_f16x3_kernel<{bm}, {bn}, {wm}, 2, {bk}, {b(trans_a)}, {b(trans_b)}, {int(epilogue)}, "
+                f"{b(clamp_a)}>")
     return (f"gemm_bf16_kernel<{bm}, {bn}, {wm}, 2, {bk}, {b(trans_a)}, {b(trans_b)}, {int(epilogue)}, "
             f"{b(precision == 'bf16x3')}, {b(clamp_a)}>")   # the C++ template instance as rocprofv3 names it
+
+
+# f16x3 operand pre-scale exponents of the layer executor (encoder_layer.cpp kH3Exp / h3_prob_exp): activations
+# and weights (typical magnitudes 2^-5 .. 2^0) by 2^6; the probability image P (entries ~1/N, at most 1/(1-p)) by
+# 2^(15 - ceil(log2(1/(1-p)))), so that its largest entry stays below fp16's 65504 and its typical ones keep 22 bits
+H3_EXP = 6
+
+
+def h3_prob_exp(p_drop):
+    e, m = 15, 1.0 / (1.0 - float(p_drop))
+    while m > 1.0:
+        m *= 0.5
+        e -= 1
+    return e
 
 
 def gemm(A, B, C, M, N, K, lda, ldb, ldc, trans_a=False, trans_b=False, epilogue=_lib.EPI_STORE, split_k=1,
          slab_stride=0, bias=None, aux0=None, aux1=None, rowvec=None, ld_aux=0, alpha=1.0, scale_cols=0, p_drop=0.0,
          seed=0, precision="fp32", tile=0, flops=None, keep=None, clamp_a=False, Cx2=None, ldcx2=0, cx2_col0=0,
-         n_valid=0, ln=None, rowpart=None):
+         n_valid=0, ln=None, rowpart=None, h3_exp=None):
     """C[M,N] (epilogue) sum_k A(m,k) B(k,n).  A/B/C may be views (pointer arithmetic via
     storage offsets is done by torch's data_ptr()).  ``flops``: algorithmic FLOPs of the
     launch for the roofline recorder (None = not recorded).  ``clamp_a``: A elements below +0 are read
@@ -81,7 +99,8 @@ def gemm(A, B, C, M, N, K, lda, ldb, ldc, trans_a=False, trans_b=False, epilogue
     then be None.  ``n_valid``: the STORE_ROWSTAT epilogue's real keys.  ``ln`` =
     (gamma, beta, Y, ldy, mean, rstd, d, rows, eps): the EPI_BIAS_DROP_RESID_LN LayerNorm (N == 64).
     ``rowpart`` [N/64, >= M]: the EPI_STORE_ROWDOT row partials (ABI v8).  A 2-D ``rowvec`` [P, >= M]
-    gives ATTN_DS_SIGNED the sum of its P partials per row (in row order of ``rowvec``)."""
+    gives ATTN_DS_SIGNED the sum of its P partials per row (in row order of ``rowvec``).  ``h3_exp`` = (ea, eb):
+    the f16x3 operand pre-scale exponents (ABI v18; None: H3_EXP for both, the layer executor's default)."""
     rec = REC.enabled and flops is not None
     if rec:
         ev0 = torch.cuda.Event(enable_timing=True)
@@ -89,7 +108,7 @@ def gemm(A, B, C, M, N, K, lda, ldb, ldc, trans_a=False, trans_b=False, epilogue
         ev0.record()
     a = _gemm_args(A, B, C, M, N, K, lda, ldb, ldc, trans_a, trans_b, epilogue, split_k, slab_stride, bias, aux0,
                    aux1, rowvec, ld_aux, alpha, scale_cols, p_drop, seed, precision, tile, keep, clamp_a, Cx2, ldcx2,
-                   cx2_col0, n_valid, ln, rowpart)
+                   cx2_col0, n_valid, ln, rowpart, h3_exp)
     check(hip_lib().u2gnn_gemm(ctypes.byref(a), _s()), "u2gnn_gemm")
     if rec:
         ev1.record()
@@ -111,7 +130,7 @@ def gemm_group(calls):
 def _gemm_args(A, B, C, M, N, K, lda, ldb, ldc, trans_a=False, trans_b=False, epilogue=_lib.EPI_STORE, split_k=1,
                slab_stride=0, bias=None, aux0=None, aux1=None, rowvec=None, ld_aux=0, alpha=1.0, scale_cols=0,
                p_drop=0.0, seed=0, precision="fp32", tile=0, keep=None, clamp_a=False, Cx2=None, ldcx2=0,
-               cx2_col0=0, n_valid=0, ln=None, rowpart=None):
+               cx2_col0=0, n_valid=0, ln=None, rowpart=None, h3_exp=None):
     _dev(A, B, C, Cx2)
     if A.dtype != torch.float32 or B.dtype != torch.float32:
         # pre-split (x2) operands were the removed round-1/2 experiments (gemm.hip rejects them)
@@ -148,6 +167,10 @@ def _gemm_args(A, B, C, M, N, K, lda, ldb, ldc, trans_a=False, trans_b=False, ep
         _dev(keep)
         a.keep, a.ld_keep = keep.data_ptr(), keep.stride(0)
     a.clamp_a = int(bool(clamp_a))
+    if h3_exp is not None:
+        a.h3_exp_a, a.h3_exp_b = int(h3_exp[0]), int(h3_exp[1])
+    elif a.precision == _lib.PREC_F16X3:
+        a.h3_exp_a = a.h3_exp_b = H3_EXP
     if ln is not None:
         gam, bet, Y, ldy, mean, rstd, d_real, rows, eps = ln
         _dev(gam, bet, Y, mean, rstd)

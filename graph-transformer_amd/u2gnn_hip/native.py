@@ -46,6 +46,8 @@ def _dims(N: int, d: int, ff: int, prec: str, deep_wgrad: bool, window: int = 0)
         prec, flags = "bf16x3", flags | _lib.LAYER_FWD_F32
     elif prec == "fwd6":   # bf16x6 forward products, bf16x3 backward (engine.FWD_ROLES)
         prec, flags = "bf16x3", flags | _lib.LAYER_FWD_X6
+    elif prec == "fwdh":   # f16x3 forward products, bf16x3 backward (engine.FWD_ROLES)
+        prec, flags = "bf16x3", flags | _lib.LAYER_FWD_H3
     return LayerDims(int(N), int(d), int(ff), PREC[prec], flags, int(window), 0)
 
 

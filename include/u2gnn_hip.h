@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define U2GNN_ABI_VERSION 17
+#define U2GNN_ABI_VERSION 18
 
 #define U2GNN_OK 0
 #define U2GNN_E_ARG (-1)    /* bad size / null pointer */
@@ -84,6 +84,11 @@ extern "C" {
                                hh + hm + mh + hl + lh + mm on bf16 MFMA, fp32 accum (~2^-26 per product,
                                the fp32 products' accuracy at 6/16 of the bf16 rate).  16-deep K step on
                                every tile; A not transposed (the forward products' layouts) */
+#define U2GNN_PREC_F16X3 4  /* ABI v18: two-way fp16 split x = hi + lo, hi = fp16_rne(x), lo = fp16_rne(x - hi)
+                               (11 + 11 significant bits), hh + hl + lh on fp16 MFMA, fp32 accum (~2^-21 per
+                               product at the bf16x3 rate).  |x| < 65504 (hi overflows to inf beyond); x small
+                               enough that lo is subnormal keeps an absolute error <= 2^-25.  The forward
+                               products' epilogues and layouts, as U2GNN_PREC_BF16X6 */
 
 typedef struct u2gnn_gemm_args {
     const float *A;       /* trans_a=0: A[m*lda+k]   trans_a=1: A[k*lda+m] */
@@ -146,6 +151,13 @@ typedef struct u2gnn_gemm_args {
                              q order (fp32-operand kernels only) */
     int32_t rowvec_reserved;
     int64_t ld_rowvec;
+    /* ---- ABI v18: U2GNN_PREC_F16X3 operand pre-scales ---- */
+    int32_t h3_exp_a, h3_exp_b;   /* A and B are multiplied by 2^h3_exp_a / 2^h3_exp_b before the fp16 split and the
+                                     result by 2^-(h3_exp_a + h3_exp_b) before the epilogue (exact): a scale that
+                                     puts an operand's typical magnitude near 2^3 keeps lo normal (22 bits) for
+                                     elements down to 2^-9 of it (the layer executor: 6 for activations and
+                                     weights, 15 - ceil(log2(1/(1-p))) for the probability image, whose entries
+                                     are ~1/N).  Within [-24, 24]; must be 0 for the other precisions */
 } u2gnn_gemm_args;
 
 /* ---- library ------------------------------------------------------------------ */
@@ -545,6 +557,10 @@ int u2gnn_window_attn_bwd(const float *QKV, int64_t ldq, int32_t W, int32_t dp, 
 /* precision "fwd6" (ABI v17): with precision == U2GNN_PREC_BF16X3, every FORWARD product runs on the three-plane
  * split U2GNN_PREC_BF16X6 (fp32-accurate products on bf16 MFMA); the backward stays bf16x3.  Excludes FWD_F32 */
 #define U2GNN_LAYER_FWD_X6 8
+/* precision "fwdh" (ABI v18): with precision == U2GNN_PREC_BF16X3, every FORWARD product runs on the two-plane
+ * fp16 split U2GNN_PREC_F16X3 (~2^-21 per product at the bf16x3 rate); the backward stays bf16x3.  Excludes
+ * FWD_F32 and FWD_X6 */
+#define U2GNN_LAYER_FWD_H3 16
 typedef struct u2gnn_layer_dims {
     int64_t N, d, ff;      /* real rows (nodes; window mode: nodes * window tokens), model width, FFN width */
     int32_t precision;     /* U2GNN_PREC_* */

@@ -23,7 +23,7 @@ def test_libraries_export_every_header_symbol(header, loader):
     missing = [s for s in syms if not hasattr(lib, s)]
     assert not missing, missing
     if loader == "hip_lib":
-        assert lib.u2gnn_abi_version() == _lib.ABI_VERSION == 17
+        assert lib.u2gnn_abi_version() == _lib.ABI_VERSION == 18
 
 
 def test_kernel_wrappers_refuse_host_tensors():

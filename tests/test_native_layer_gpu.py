@@ -29,7 +29,7 @@ def _zeros_like_params(p: LayerParams) -> LayerParams:
 # softmax.P.V, FFN2 split-K + slab LayerNorm at dp = 192 / 128, the tiny direct dX1 product (ff = 256)
 @pytest.mark.parametrize("N,d,ff", [(300, 67, 128), (1000, 367, 1024), (300, 19, 128), (1920, 4, 1024),
                                     (80, 136, 1024), (100, 100, 256)])
-@pytest.mark.parametrize("prec", ["bf16x3", "fp32", "mixed", "fwd32", "fwd6"])
+@pytest.mark.parametrize("prec", ["bf16x3", "fp32", "mixed", "fwd32", "fwd6", "fwdh"])
 @pytest.mark.parametrize("train", [True, False])
 @pytest.mark.parametrize("side", [False, True])
 def test_native_layer_matches_python_orchestration(N, d, ff, prec, train, side):

@@ -7,8 +7,8 @@ reproduced on the GPU, so the oracle restatement is run with the exact masks the
 parameter gradient, the clip norm and the parameters after clip_grad_norm_(0.5) + Adam.
 
 Cases: the reference-golden batches mutag_sup_L2T2 (L = 2, T = 2) and imdbb_sup (C2), and one full C4 batch
-(N ~ 4.8K, d = 367, T = 4) -- in fp32, fwd6 (the bench's precision: bf16x6 forward products, bf16x3
-backward), bf16x3 and fwd32 (exact forward, bf16x3 backward).  Tolerance TOL = 1e-3 (north_star) on max|ours - oracle| / max(1, max|oracle|) for EVERY quantity,
+(N ~ 4.8K, d = 367, T = 4) -- in fp32, fwdh (the bench's precision: pre-scaled f16x3 forward products, bf16x3
+backward), fwd6 (bf16x6 forward products, bf16x3 backward), bf16x3 and fwd32 (exact forward, bf16x3 backward).  Tolerance TOL = 1e-3 (north_star) on max|ours - oracle| / max(1, max|oracle|) for EVERY quantity,
 with no per-quantity exceptions; why the gradients are compared against the oracle run with the GPU's own
 ReLU decisions, and what bounds the decisions themselves, is in tests/train_parity_util.py and DESIGN.md
 section 7.  U2GNN_PARITY_REPORT=<path> appends the measured errors as JSON lines (profiles/ evidence)."""
@@ -66,7 +66,7 @@ def _gpu_step(m, flat, b, C, seed, native_on):
     return scores.detach().cpu().clone(), float(loss.item()), grads, ctx["stack"]
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16x3", "fwd32", "fwd6"])
+@pytest.mark.parametrize("precision", ["fp32", "bf16x3", "fwd32", "fwd6", "fwdh"])
 @pytest.mark.parametrize("name", ["mutag_sup_L2T2", "imdbb_sup", "c4"])
 def test_train_mode_step_matches_oracle_with_kernel_masks(golden_dir, name, precision):
     from oracle import u2gnn_oracle as O

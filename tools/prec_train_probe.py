@@ -29,6 +29,7 @@ POLICIES = {   # name -> (layer precision, role overrides)
     "x6_proj": ("bf16x3", {r: "bf16x6" for r in ("in_proj", "out_proj", "ffn1", "ffn2")}),
     "x6_all": ("bf16x3", {r: "bf16x6" for r in FWD}),
     "fwd6": ("fwd6", {}),
+    "fwdh": ("fwdh", {}),
     "x6_nopv": ("bf16x3", {r: "bf16x6" for r in ("in_proj", "qk", "out_proj", "ffn1", "ffn2")}),
     "x6_noqk": ("bf16x3", {r: "bf16x6" for r in ("in_proj", "pv", "out_proj", "ffn1", "ffn2")}),
 }

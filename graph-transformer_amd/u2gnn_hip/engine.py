@@ -401,7 +401,8 @@ def _attn_split(Q, Kt, V, N, Np, dp, pd, seeds, prec, att, dev):
     del S
     O = torch.empty(Np, dp, device=dev, dtype=f32)
     _gemm_nodes_k(Pd, V, O, Np, dp, Np, Np, 3 * dp, dp, prec=_rp("pv", prec), flops=att, clamp_a=pd > 0,
-                  h3_exp=(K.h3_prob_exp(pd), K.H3_EXP))   # (f16x3: the probability image's pre-scale)
+                  h3_exp=(K.h3_prob_exp(pd), K.H3_EXP) if _rp("pv", prec) == "f16x3" else None)
+    # (f16x3: the probability image's pre-scale, encoder_layer.cpp h3_prob_exp)
     return Pd, O
 
 

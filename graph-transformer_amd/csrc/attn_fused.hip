@@ -26,6 +26,7 @@
 // V^T fragments are read as 8 ds_read_b32 per lane and split into hi / mid / lo bf16 planes in registers; P is
 // split three ways too, and each term is the six products mm, hl, lh, hm, mh, hh (fp32-accurate).
 #include "u2gnn_common.h"
+#include <cmath>
 
 #include <type_traits>
 
@@ -168,6 +169,14 @@ __device__ __forceinline__ void v_frag6(const char *img, const int (&base)[2], i
     lo = __builtin_bit_cast(bf16x8, l);
 }
 
+__device__ __forceinline__ void split8_h(const float *x, float sc, bf16x8 &hi, bf16x8 &lo) {
+    unsigned h[4], l[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) split2h(x[2 * i] * sc, x[2 * i + 1] * sc, h[i], l[i]);
+    hi = __builtin_bit_cast(bf16x8, h);
+    lo = __builtin_bit_cast(bf16x8, l);
+}
+
 __device__ __forceinline__ void split8_3(const float *x, bf16x8 &hi, bf16x8 &mid, bf16x8 &lo) {
     unsigned h[4], m[4], l[4];
 #pragma unroll
@@ -204,6 +213,7 @@ struct SpvP {
     float p;
     uint64_t seed;
     const uint64_t *epoch;
+    float h3_sp, h3_inv;   // F16X3: the pre-scale of P (a power of two) and the inverse of P's and V's
 };
 
 // (m, l) <- the log-sum-exp merge with (m2, l2); -inf maxima (empty groups) contribute nothing
@@ -252,7 +262,7 @@ __device__ __forceinline__ void row_stat(const SpvP &P, int query, int h, float 
 // both reach exp2(-inf) = 0.
 struct PRow {
     int r, h;
-    float mb, inv, sc;
+    float mb, inv, sc, hsc;   // hsc: F16X3 pre-scale of the kept probabilities
     uint32_t rkey, thr;
     float *prow;
 };
@@ -288,6 +298,7 @@ __device__ __forceinline__ void p_half(const PRow &R, const char *simg, int kb, 
     if (img[0] == 123.f) *dst = img[1] + img[2] + img[3] + img[4] + img[5] + img[6] + img[7];
 #endif
     if constexpr (NPL == 3) split8_3(pv, pp[0], pp[1], pp[2]);
+    else if constexpr (NPL == 4) split8_h(pv, R.hsc, pp[0], pp[1]);
     else split8(pv, pp[0], pp[1]);
 }
 
@@ -339,11 +350,18 @@ __device__ __forceinline__ void pv_block(const char *vimg, const VBase &vb, cons
         for (int ks = 0; ks < 2; ++ks) {
             const bf16x8(&f)[3] = v[cur][ks];
             const bf16x8(&q)[3] = pp[ks];
-            if constexpr (NPL >= 2) {
-                o[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f[0], q[1], o[t], 0, 0, 0);
-                o[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f[1], q[0], o[t], 0, 0, 0);
+            if constexpr (NPL == 4) {   // f16x3: the x2 rows hold fp16 planes (U2GNN_H3_X2_EXP), P split likewise
+                const auto h = [](bf16x8 v) { return __builtin_bit_cast(f16x8, v); };
+                o[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(h(f[0]), h(q[1]), o[t], 0, 0, 0);
+                o[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(h(f[1]), h(q[0]), o[t], 0, 0, 0);
+                o[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(h(f[0]), h(q[0]), o[t], 0, 0, 0);
+            } else {
+                if constexpr (NPL >= 2) {
+                    o[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f[0], q[1], o[t], 0, 0, 0);
+                    o[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f[1], q[0], o[t], 0, 0, 0);
+                }
+                o[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f[0], q[0], o[t], 0, 0, 0);
             }
-            o[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f[0], q[0], o[t], 0, 0, 0);
         }
     }
 }
@@ -372,7 +390,8 @@ __device__ __forceinline__ void spv_block(int id, int total, int qblocks, int &q
     qb = pos - split * qblocks;
 }
 
-// NPL: bf16 planes per operand -- 1 (bf16), 2 (bf16x3: x2 V rows), 3 (bf16x6: fp32 V rows)
+// NPL: planes per operand -- 1 (bf16), 2 (bf16x3: x2 V rows), 3 (bf16x6: fp32 V rows), 4 (f16x3: x2 rows of fp16
+// planes, U2GNN_H3_X2_EXP)
 template <int DP, int NPL>
 __global__ void __launch_bounds__(FA_NT, 1) attn_softmax_pv_kernel(SpvP P) {
     constexpr int DT = DP / 32;              // 32-wide d tiles of O
@@ -410,6 +429,7 @@ __global__ void __launch_bounds__(FA_NT, 1) attn_softmax_pv_kernel(SpvP P) {
     R.inv = qvalid ? inv : 0.f;
     R.thr = u2gnn_keep_thr(P.p);
     R.sc = P.p > 0.f ? 1.f / (1.f - P.p) : 1.f;
+    R.hsc = P.h3_sp;
     R.rkey = u2gnn_row_key(seed, (uint32_t)query);
     R.prow = P.Pd + (int64_t)query * P.ldp;
     const VBase vb = v_base<DP>(lane);
@@ -456,7 +476,7 @@ __global__ void __launch_bounds__(FA_NT, 1) attn_softmax_pv_kernel(SpvP P) {
         pv_block<DP, NPL>(STG ? vst1 : vst0, vb, vb6, pp, o);
 #endif
 #ifndef SPV_NO_HINT
-        if constexpr (NPL != 3) interleave_hint<(NPL == 2 ? 6 : 2) * DT, NPL == 2 ? 6 : 18>();
+        if constexpr (NPL != 3) interleave_hint<(NPL == 1 ? 2 : 6) * DT, NPL == 1 ? 18 : NPL == 4 ? 8 : 6>();
 #endif
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
@@ -491,6 +511,10 @@ __global__ void __launch_bounds__(FA_NT, 1) attn_softmax_pv_kernel(SpvP P) {
     // ---- partial O of this key range: O^T lane layout = query l%32, d = 32 t + 8 g + 4 h .. +3
     // (direct: one key range and one query block cover everything -- O itself, padded rows 0 via P = 0)
     float *orow = P.direct ? P.O + (int64_t)query * P.ldo : P.Opart + ((int64_t)split * P.rows_pad + query) * DP;
+    if constexpr (NPL == 4) {   // undo the pre-scales (exact)
+#pragma unroll
+        for (int t = 0; t < DT; ++t) o[t] *= P.h3_inv;
+    }
 #ifndef SPV_NO_OSTORE
 #pragma unroll
     for (int t = 0; t < DT; ++t)
@@ -563,7 +587,9 @@ inline int spv_nsplit(int64_t n_valid) {
 template <int DP>
 void launch_spv(const SpvP &P, int npl, hipStream_t st) {
     const dim3 grid((unsigned)(P.qblocks * P.nsplit));
-    if (npl == 3)
+    if (npl == 4)
+        hipLaunchKernelGGL((attn_softmax_pv_kernel<DP, 4>), grid, dim3(FA_NT), 0, st, P);
+    else if (npl == 3)
         hipLaunchKernelGGL((attn_softmax_pv_kernel<DP, 3>), grid, dim3(FA_NT), 0, st, P);
     else if (npl == 2)
         hipLaunchKernelGGL((attn_softmax_pv_kernel<DP, 2>), grid, dim3(FA_NT), 0, st, P);
@@ -586,7 +612,8 @@ int u2gnn_attn_softmax_pv(const float *S, int64_t lds, const float *rowpart, int
                           int32_t precision, void *stream) {
     if (!S || !rowpart || !qkv2 || !Pd || !O || !ws || n_valid < 1 || rows_pad < n_valid || rows_pad % FA_BM ||
         !(p < 1.f) || p < 0.f ||
-        (precision != U2GNN_PREC_BF16X3 && precision != U2GNN_PREC_BF16 && precision != U2GNN_PREC_BF16X6))
+        (precision != U2GNN_PREC_BF16X3 && precision != U2GNN_PREC_BF16 && precision != U2GNN_PREC_BF16X6 &&
+         precision != U2GNN_PREC_F16X3))
         return U2GNN_E_ARG;
     const bool x6 = precision == U2GNN_PREC_BF16X6;   // qkv2 = the fp32 in-projection output, ldq2 in floats
     if (dp < 64 || dp > 384 || dp % 64 || ldq2 < (x6 ? 3 : 6) * dp || (ldq2 & (x6 ? 3 : 7)) || lds < rows_pad || (lds & 3) ||
@@ -629,8 +656,14 @@ int u2gnn_attn_softmax_pv(const float *S, int64_t lds, const float *rowpart, int
     P.p = p;
     P.seed = seed;
     P.epoch = u2gnn_cur_epoch();
+    // f16x3: V arrives pre-scaled by 2^U2GNN_H3_X2_EXP in its fp16 x2 rows; the kept probabilities (at most
+    // 1/(1-p)) are scaled by 2^(15 - ceil(log2(1/(1-p)))) before their split (encoder_layer.cpp h3_prob_exp)
+    int ep = 15;
+    for (float m = p > 0.f ? 1.f / (1.f - p) : 1.f; m > 1.f; m *= 0.5f) --ep;
+    P.h3_sp = std::ldexp(1.f, ep);
+    P.h3_inv = std::ldexp(1.f, -(ep + U2GNN_H3_X2_EXP));
     hipStream_t st = u2gnn_stream(stream);
-    const int npl = x6 ? 3 : precision == U2GNN_PREC_BF16X3 ? 2 : 1;
+    const int npl = precision == U2GNN_PREC_F16X3 ? 4 : x6 ? 3 : precision == U2GNN_PREC_BF16X3 ? 2 : 1;
     switch (dp) {
 #ifndef SPV_ONLY384   // (kernel experiments: build the dp = 384 instances only)
         case 64: launch_spv<64>(P, npl, st); break;

@@ -501,12 +501,16 @@ int64_t ffn2_split(int64_t dp, bool mfma, int64_t Np, int64_t ffp) {
 // them), then 128x128 (the same per-element sums: same bits; engine.qk_tile mirrors the rule)
 int qk_tile(int64_t Np) { return (Np % 256 == 0 && (Np / 256) * (Np / 128) >= 256) ? 256 : 128; }
 
-// (bf16x6 -- the fwd6 policy -- keeps the three-pass form: its fused kernel, u2gnn_attn_softmax_pv with BF16X6, ran
+// (f16x3 -- the fwdh policy -- runs fused: V as fp16 x2 rows from the in-projection, 3.024 vs 3.052 ms three-pass,
+// profiles/r06/h3g_fused_ab.txt; bf16x6 -- the fwd6 policy -- keeps the three-pass form: its fused kernel, ran
 // the C4 step at 3.42 / 3.43 ms against 3.40 unfused, and its exp2-based probabilities moved one boundary ReLU unit
 // of the test seed's step across 0)
 bool fused_attn(const Dims &D) {
+#ifdef U2GNN_EXP_H3_UNFUSED   // (A/B: the fwdh policy on the three-pass forward)
+    if (D.prec_fwd == U2GNN_PREC_F16X3) return false;
+#endif
     return !D.window && !small_attn(D) && D.prec_fwd != U2GNN_PREC_F32 && D.prec_fwd != U2GNN_PREC_BF16X6 &&
-           D.prec_fwd != U2GNN_PREC_F16X3 && D.dp <= 384;
+           D.dp <= 384;
 }
 
 // the row-local tail of a small-width layer (u2gnn_layer_tail_small_*, small_layer.hip): every precision when the

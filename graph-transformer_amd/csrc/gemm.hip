@@ -844,6 +844,7 @@ int gemm_plan(const u2gnn_gemm_args *a, GemmPlan &G) {
     P.Cx2 = static_cast<__bf16 *>(a->Cx2);
     P.ldcx2 = a->ldcx2;
     P.cx2_col0 = a->cx2_col0;
+    P.cx2_h3 = prec == U2GNN_PREC_F16X3 ? std::ldexp(1.f, U2GNN_H3_X2_EXP) : 0.f;
     P.n_valid = (int32_t)a->n_valid;
     P.rowpart = a->rowpart;
     P.ld_rowpart = a->ld_rowpart;

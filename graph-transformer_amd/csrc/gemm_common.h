@@ -28,6 +28,7 @@ struct GemmP {
     __bf16 *Cx2;          // non-null: the epilogue also writes C in x2 format
     int64_t ldcx2;        // bf16 elements
     int32_t cx2_col0;     // Cx2 receives columns >= cx2_col0 only
+    float cx2_h3;         // 0: bf16 x2; > 0 (f16x3 kind): fp16 hi / lo of cx2_h3 * C (u2gnn_hip.h U2GNN_H3_X2_EXP)
     int32_t n_valid;   // STORE_ROWSTAT: real keys (columns >= n_valid are masked)
     const uint64_t *epoch;      // seed epoch at launch (u2gnn_set_seed_epoch): seed ^= *epoch * golden
     // EPI_BIAS_DROP_RESID_LN: the post-LayerNorm of the row-complete 64-column result
@@ -222,7 +223,10 @@ __device__ __forceinline__ float store_slice(const GemmP &P, float *C, const f32
                                          acc[i][j][4 * g + 3]);
             const float4 o = epilogue4<EPI>(P, row, col, v, e.a[j][g], e.b[j][g], e.kb[j][g], dl);
             if (P.C) *reinterpret_cast<float4 *>(C + (int64_t)row * P.ldc + col) = o;
-            if (P.Cx2 && col >= P.cx2_col0) store_x2_4(P.Cx2, P.ldcx2, row, col, o);
+            if (P.Cx2 && col >= P.cx2_col0) {
+                if (P.cx2_h3 > 0.f) store_x2h_4(P.Cx2, P.ldcx2, row, col, o, P.cx2_h3);
+                else store_x2_4(P.Cx2, P.ldcx2, row, col, o);
+            }
             if constexpr (EPI == U2GNN_EPI_STORE_ROWDOT) {
                 const float4 x = e.a[j][g];
                 rs += o.x * x.x + o.y * x.y + o.z * x.z + o.w * x.w;

@@ -136,6 +136,16 @@ __device__ __forceinline__ void split2h(float x0, float x1, unsigned &h, unsigne
     l = __builtin_bit_cast(unsigned, lv);
 }
 
+// x2 store of four consecutive columns in the f16x3 form: fp16 hi / lo of sc * o (the same layout)
+__device__ __forceinline__ void store_x2h_4(__bf16 *Cx2, int64_t ldcx2, int row, int col, float4 o, float sc) {
+    unsigned h0, h1, l0, l1;
+    split2h(o.x * sc, o.y * sc, h0, l0);
+    split2h(o.z * sc, o.w * sc, h1, l1);
+    __bf16 *b = Cx2 + (int64_t)row * ldcx2 + 2 * (col & ~7) + (col & 7);
+    *reinterpret_cast<uint2 *>(b) = make_uint2(h0, h1);
+    *reinterpret_cast<uint2 *>(b + 8) = make_uint2(l0, l1);
+}
+
 // x2 store of four consecutive columns (col % 4 == 0): hi at 16*(col/8) + col%8, lo 8 further
 __device__ __forceinline__ void store_x2_4(__bf16 *Cx2, int64_t ldcx2, int row, int col, float4 o) {
     unsigned h0, h1, l0, l1;

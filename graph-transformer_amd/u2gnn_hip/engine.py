@@ -382,9 +382,9 @@ def mid_tail(d: int, dp: int, Np: int) -> bool:
 
 def fused_attn(dp: int, prec_qk: str, prec_pv: str) -> bool:
     """Node-axis attention forward through the fused softmax.P.V kernel: Q K^T with the row-statistics epilogue
-    (bf16, bf16x3 or bf16x6) and P.V in bf16 / bf16x3, dp <= 384 (encoder_layer.cpp fused_attn: the fwd6 policy keeps
+    (bf16, bf16x3, bf16x6 or f16x3) and P.V in bf16 / bf16x3 / f16x3, dp <= 384 (encoder_layer.cpp fused_attn: the fwd6 policy keeps
     the three-pass form; the kernel's bf16x6 P.V is a tested capability, measured no faster)."""
-    return prec_qk != "fp32" and prec_pv in ("bf16", "bf16x3") and dp <= 384
+    return prec_qk != "fp32" and prec_pv in ("bf16", "bf16x3", "f16x3") and dp <= 384
 
 
 def _attn_split(Q, Kt, V, N, Np, dp, pd, seeds, prec, att, dev):
@@ -422,6 +422,7 @@ def encoder_layer_forward(X: torch.Tensor, w: PackedLayer, p: LayerParams, dims:
     if not small:   # (the small-width attention projects into its own compact context)
         QKV = torch.empty(Np, 3 * dp, device=dev, dtype=f32)
         # x2 copy of V for the fused P.V (bf16x6 P.V reads the fp32 output itself)
+        # (f16x3: fp16 planes of 2^U2GNN_H3_X2_EXP V in the same layout)
         QKV2 = torch.empty(Np, 6 * dp, device=dev, dtype=torch.bfloat16) if fused and _rp("pv", prec) != "bf16x6" else None
         K.gemm(X, w.W_in, QKV, Np, 3 * dp, dp, dp, dp, 3 * dp, trans_b=True, epilogue=E.EPI_BIAS, bias=w.b_in,
                alpha=1.0 / math.sqrt(d), scale_cols=dp, precision=_rp("in_proj", prec), flops=6.0 * N * d * d,

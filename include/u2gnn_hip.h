@@ -428,7 +428,10 @@ int u2gnn_index_zero_rows(const int64_t *idx, int64_t n_rows, float *dst, int64_
  * O = Pd_kept . V on the matrix cores (precision BF16X3: split-bf16, 3 products; BF16: 1), V read from qkv2
  * (the in-projection output in x2 format, [rows_pad][ldq2] bf16, V = columns 2dp .. 3dp).  ABI v17, precision
  * BF16X6: qkv2 is the fp32 in-projection output itself ([rows_pad][ldq2] float, ldq2 >= 3 dp, V = columns
- * 2dp .. 3dp), P and V split three ways in registers, 6 products (fp32-accurate).  dp in {64, 128,
+ * 2dp .. 3dp), P and V split three ways in registers, 6 products (fp32-accurate).  ABI v18, precision F16X3:
+ * qkv2 in x2 layout holding fp16 planes of 2^U2GNN_H3_X2_EXP times the in-projection output (what an F16X3 GEMM
+ * writes to Cx2), P scaled by 2^(15 - ceil(log2(1/(1-p)))) and split into fp16 hi / lo, 3 fp16 products, O
+ * scaled back (f16x3 accuracy).  dp in {64, 128,
  * ..., 384}, rows_pad % 128 == 0, ngroups and ld_rowpart even, rowpart 16-byte aligned; S columns >= n_valid
  * hold -inf (as EPI_STORE_ROWSTAT writes them); S and Pd may alias (the image is written over the scores).
  * ws: u2gnn_attn_softmax_pv_ws_floats(n_valid, rows_pad, dp) floats (per key range partial outputs). */
@@ -561,6 +564,9 @@ int u2gnn_window_attn_bwd(const float *QKV, int64_t ldq, int32_t W, int32_t dp, 
  * fp16 split U2GNN_PREC_F16X3 (~2^-21 per product at the bf16x3 rate); the backward stays bf16x3.  Excludes
  * FWD_F32 and FWD_X6 */
 #define U2GNN_LAYER_FWD_H3 16
+/* ABI v18: with precision U2GNN_PREC_F16X3, a GEMM's x2 output (Cx2) holds fp16 hi / lo of 2^U2GNN_H3_X2_EXP * C in
+ * the x2 layout (the in-projection's V block for the f16x3 softmax.P.V, which takes that scale back out) */
+#define U2GNN_H3_X2_EXP 6
 typedef struct u2gnn_layer_dims {
     int64_t N, d, ff;      /* real rows (nodes; window mode: nodes * window tokens), model width, FFN width */
     int32_t precision;     /* U2GNN_PREC_* */

@@ -180,3 +180,43 @@ def test_softmax_pv_bf16x6(Np, N, dp, p):
     assert e6 * 4 < e3, (e6, e3)
     assert ((O6[:N].double() - O_ref_p).abs().max() / O_ref_p.abs().max()).item() < 2e-6
     assert (O6[N:] == 0).all()
+
+
+def x2h(X, scale_exp=6):
+    """The f16x3 x2 image of fp32 X (u2gnn_hip.h U2GNN_H3_X2_EXP): per 8 columns fp16 hi then lo of 2^6 X."""
+    x = X.float() * 2.0 ** scale_exp
+    hi = x.half()
+    lo = (x - hi.float()).half()
+    R, C = X.shape
+    img = torch.stack([hi.view(R, C // 8, 8), lo.view(R, C // 8, 8)], dim=2).reshape(R, 2 * C)
+    return img.view(torch.int16).view(torch.bfloat16)
+
+
+@pytest.mark.parametrize("Np,N,dp", [(256, 230, 64), (128, 100, 384), (1280, 1100, 128), (512, 500, 384),
+                                     (2048, 1999, 192), (4864, 4776, 384), (384, 257, 256), (640, 640, 320)])
+@pytest.mark.parametrize("p", [0.5, 0.0])
+def test_softmax_pv_f16x3(Np, N, dp, p):
+    """ABI v18 F16X3: V as x2 rows of fp16 planes of 2^6 V (the in-projection's f16x3 x2 output), P pre-scaled by
+    2^h3_prob_exp(p) and split in registers: O well below bf16x3's error against the fp64 product of the kernel's
+    own image, and the signed image bit for bit the bf16x3 kernel's (the same P and keep decisions)."""
+    seed = 4243
+    S = _mk(Np, Np, seed=17, scale=2.0)
+    S[:, N:] = float("-inf")
+    V = _mk(Np, dp, seed=19)
+    rp = _partials(S, N, Np)
+    QKV = _mk(Np, 3 * dp, seed=21)
+    QKV[:, 2 * dp:] = V
+    ws = torch.empty(K.attn_softmax_pv_ws_floats(N, Np, dp), device=DEV)
+    Xh, Oh = S.clone(), torch.full((Np, dp), float("nan"), device=DEV)
+    K.attn_softmax_pv(Xh, Np, rp, Np // 64, x2h(QKV), 6 * dp, dp, Xh, Np, Oh, dp, ws, N, Np, p, seed, precision="f16x3")
+    X3, O3 = S.clone(), torch.full((Np, dp), float("nan"), device=DEV)
+    K.attn_softmax_pv(X3, Np, rp, Np // 64, _qkv2(V, Np, dp), 6 * dp, dp, X3, Np, O3, dp, ws, N, Np, p, seed,
+                      precision="bf16x3")
+    torch.cuda.synchronize()
+    assert torch.equal(Xh, X3)
+    O_ref = Xh[:N, :N].double().clamp_min(0) @ V[:N].double()
+    eh = ((Oh[:N].double() - O_ref).abs().max() / O_ref.abs().max()).item()
+    e3 = ((O3[:N].double() - O_ref).abs().max() / O_ref.abs().max()).item()
+    assert eh < 4e-6, eh
+    assert eh * 4 < e3, (eh, e3)
+    assert (Oh[N:] == 0).all()

@@ -175,3 +175,19 @@ def test_h3_refuses_the_backward_layouts_and_epilogues():
         K.gemm(A, B, C, M, N, Kd, Kd, N, N, epilogue=_lib.EPI_RELU_DROP_BWD, aux0=C, ld_aux=N, precision="f16x3")
     with pytest.raises(U2GNNNativeError):   # not a multiple of the 32-deep K step
         K.gemm(A, B, C, M, N, 112, Kd, N, N, precision="f16x3")
+
+
+def test_h3_x2_output_is_fp16_planes_of_scaled_result():
+    """with precision f16x3 the x2 output (Cx2) holds fp16 hi / lo of 2^U2GNN_H3_X2_EXP * C (the f16x3 fused
+    softmax.P.V's V operand), bit for bit the planes of the stored C; columns below cx2_col0 untouched"""
+    from test_attn_fused_gpu import x2h
+    M, N, Kd = 256, 192, 128
+    A, B = _mk(M, Kd, seed=81), _mk(N, Kd, seed=82)
+    bias = _mk(N, seed=83)
+    C = torch.empty(M, N, device=DEV)
+    Cx2 = torch.zeros(M, 2 * N, device=DEV, dtype=torch.bfloat16)
+    K.gemm(A, B, C, M, N, Kd, Kd, Kd, N, trans_b=True, epilogue=_lib.EPI_BIAS, bias=bias, precision="f16x3", tile=64,
+           Cx2=Cx2, ldcx2=2 * N, cx2_col0=64)
+    ref = x2h(C)
+    assert torch.equal(Cx2[:, 128:].view(torch.int16), ref[:, 128:].view(torch.int16))
+    assert (Cx2[:, :128].view(torch.int16) == 0).all()

@@ -17,10 +17,10 @@ for rep in 1 2; do
       U2GNN_HIP_LIB=$L GB_ONLY="$ONLY" timeout -k 10 200 python tools/gemm_bench.py bf16x3 2>/dev/null | sed "s/^/$v /" || exit 1
     fi
     if [ -n "${WL:-}" ]; then
-      U2GNN_HIP_LIB=$L timeout -k 10 200 python bench.py --workload $WL --steps 30 --warmup 5 --cpu-baseline 0 > gpurun_out/ab_$v.json 2>gpurun_out/ab_$v.err || exit 1
+      U2GNN_HIP_LIB=$L timeout -k 10 200 python bench.py --workload $WL --steps 30 --warmup 5 --cpu-baseline 0 --neighbors-line 0 > gpurun_out/ab_$v.json 2>gpurun_out/ab_$v.err || exit 1
     else
     NR=--no-roofline; [ -n "${PROBE:-}" ] && NR=""
-    U2GNN_HIP_LIB=$L timeout -k 10 200 python bench.py --configs 0 --steps 30 --warmup 5 --cpu-baseline 0 --fp32-steps 0 --pipeline-steps 0 $NR > gpurun_out/ab_$v.json 2>gpurun_out/ab_$v.err || exit 1
+    U2GNN_HIP_LIB=$L timeout -k 10 200 python bench.py --configs 0 --steps 30 --warmup 5 --cpu-baseline 0 --fp32-steps 0 --pipeline-steps 0 --neighbors-line 0 $NR > gpurun_out/ab_$v.json 2>gpurun_out/ab_$v.err || exit 1
     fi
     python -c "import json;d=json.load(open('gpurun_out/ab_$v.json'));r=d.get('roofline') or {};print('$v', 'step_ms', d['ms_per_step'], d['final_loss'], 'probe_us', r.get('avg_launch_us'))"
   done

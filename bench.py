@@ -296,7 +296,7 @@ def attn_kernel_roofline(args, role, ms, n, used, d, per_step, K, LIB):
     from u2gnn_hip.engine import row_pad, rup
     Np0, dp = row_pad(used[0].N), rup(d, 64)
     pk = probe_precision(args.precision, role)
-    fused = pk in ("bf16x3", "bf16") and dp <= 384   # encoder_layer.cpp fused_attn (fwd6: the three-pass forward)
+    fused = pk in ("bf16x3", "bf16", "f16x3") and dp <= 384 and Np0 >= 1024   # encoder_layer.cpp fused_attn (fwd6: three-pass)
     prods = 2.0 if role == "dq" else 1.0   # the grouped dQ + dK launch
     fl = float(sum(per_step * prods * 2.0 * b.N * b.N * d for b in used))
     if role == "ds":
@@ -308,7 +308,7 @@ def attn_kernel_roofline(args, role, ms, n, used, d, per_step, K, LIB):
     elif role == "qk":
         sym = K.gemm_symbol(pk, Np0, Np0, 1, 256, False, True, LIB.EPI_STORE_ROWSTAT if fused else LIB.EPI_STORE)
     else:
-        sym = f"attn_softmax_pv_kernel<{dp}, {2 if pk == 'bf16x3' else 1}>" if fused else \
+        sym = f"attn_softmax_pv_kernel<{dp}, {dict(bf16x3=2, f16x3=4).get(pk, 1)}>" if fused else \
             K.gemm_symbol(pk, Np0, dp, 4, 256, False, False, LIB.EPI_STORE, clamp_a=True)
     ach = fl / (ms * 1e-3) / 1e12
     peak = PEAK[pk]

@@ -504,10 +504,16 @@ int qk_tile(int64_t Np) { return (Np % 256 == 0 && (Np / 256) * (Np / 128) >= 25
 // (f16x3 -- the fwdh policy -- runs fused: V as fp16 x2 rows from the in-projection, 3.024 vs 3.052 ms three-pass,
 // profiles/r06/h3g_fused_ab.txt; bf16x6 -- the fwd6 policy -- keeps the three-pass form: its fused kernel, ran
 // the C4 step at 3.42 / 3.43 ms against 3.40 unfused, and its exp2-based probabilities moved one boundary ReLU unit
-// of the test seed's step across 0)
+// of the test seed's step across 0).  Few rows (C2's IMDBBINARY batches, Np = 128: ONE
+// workgroup walks every key) run the three-pass form, whose GEMM tiles spread over more CUs: C2 fwdh 0.424 ms
+// three-pass (r6h) vs 0.460 fused (r6i); engine.FUSED_MIN_NP mirrors the bound
+constexpr int64_t kFusedMinNp = 1024;
 bool fused_attn(const Dims &D) {
 #ifdef U2GNN_EXP_H3_UNFUSED   // (A/B: the fwdh policy on the three-pass forward)
     if (D.prec_fwd == U2GNN_PREC_F16X3) return false;
+#endif
+#ifndef U2GNN_EXP_FUSED_ANY_NP   // (A/B: the fused form at every row count, as up to r6i)
+    if (D.Np < kFusedMinNp) return false;
 #endif
     return !D.window && !small_attn(D) && D.prec_fwd != U2GNN_PREC_F32 && D.prec_fwd != U2GNN_PREC_BF16X6 &&
            D.dp <= 384;

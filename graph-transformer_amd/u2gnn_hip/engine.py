@@ -380,11 +380,15 @@ def mid_tail(d: int, dp: int, Np: int) -> bool:
     return d > SMALL_ATTN_MAX_D and dp <= 256 and Np <= 512
 
 
-def fused_attn(dp: int, prec_qk: str, prec_pv: str) -> bool:
+FUSED_MIN_NP = 1024   # encoder_layer.cpp kFusedMinNp
+
+
+def fused_attn(dp: int, prec_qk: str, prec_pv: str, Np: int = FUSED_MIN_NP) -> bool:
     """Node-axis attention forward through the fused softmax.P.V kernel: Q K^T with the row-statistics epilogue
-    (bf16, bf16x3, bf16x6 or f16x3) and P.V in bf16 / bf16x3 / f16x3, dp <= 384 (encoder_layer.cpp fused_attn: the fwd6 policy keeps
-    the three-pass form; the kernel's bf16x6 P.V is a tested capability, measured no faster)."""
-    return prec_qk != "fp32" and prec_pv in ("bf16", "bf16x3", "f16x3") and dp <= 384
+    (bf16, bf16x3, bf16x6 or f16x3) and P.V in bf16 / bf16x3 / f16x3, dp <= 384, Np >= FUSED_MIN_NP
+    (encoder_layer.cpp fused_attn: fewer rows run the three-pass form; the fwd6 policy keeps the three-pass form,
+    the kernel's bf16x6 P.V is a tested capability, measured no faster)."""
+    return prec_qk != "fp32" and prec_pv in ("bf16", "bf16x3", "f16x3") and dp <= 384 and Np >= FUSED_MIN_NP
 
 
 def _attn_split(Q, Kt, V, N, Np, dp, pd, seeds, prec, att, dev):
@@ -417,7 +421,7 @@ def encoder_layer_forward(X: torch.Tensor, w: PackedLayer, p: LayerParams, dims:
     dev = X.device
     f32 = torch.float32
     small = small_attn(d)
-    fused = not small and fused_attn(dp, _rp("qk", prec), _rp("pv", prec))
+    fused = not small and fused_attn(dp, _rp("qk", prec), _rp("pv", prec), Np)
     QKV = QKV2 = None
     if not small:   # (the small-width attention projects into its own compact context)
         QKV = torch.empty(Np, 3 * dp, device=dev, dtype=f32)

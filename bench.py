@@ -69,8 +69,8 @@ def parse():
     ap.add_argument("--num-hidden-layers", type=int, default=1)
     ap.add_argument("--precision", default="fwdh", choices=["fp32", "bf16x3", "mixed", "bf16", "fwd32", "fwd6", "fwdh"],
                     help="fwdh (default, round 6) = forward products on the two-plane fp16 split f16x3 (22-bit "
-                         "pre-scaled operands), backward bf16x3: the train-mode ReLU decisions carry near-fp32 rounding "
-                         "at +3 %% over bf16x3 (DESIGN.md section 7.1); fwd6 = forward products on the three-plane "
+                         "pre-scaled operands), backward bf16x3: the train-mode ReLU decisions carry fp32-class rounding "
+                         "at +2 %% over bf16x3 (DESIGN.md section 7.1); fwd6 = forward products on the three-plane "
                          "bf16x6 split (fp32-accurate, +16 %%); "
                          "bf16x3 = every product split-bf16; mixed = bf16x3 with the attention-backward dS/dQ/dK "
                          "products on plain bf16 (experiment: +4 %% at C4, outside the 1e-3 bound on the MUTAG L2T2 golden)")
@@ -394,7 +394,7 @@ WHAT_PREC = {"fp32": "the same training step with every matrix-core product in e
              "fwd6": "the same training step with the forward products on the three-plane bf16x6 split (fp32-accurate) "
                      "and the backward in bf16x3",
              "fwdh": "the same training step with the forward products on the two-plane fp16 split f16x3 (~2^-21 per "
-                     "product at the bf16x3 rate) and the backward in bf16x3"}
+                     "product at the bf16x3 rate, fused softmax.P.V) and the backward in bf16x3"}
 
 
 def exact_line(args, batches, sd0, dev, d, C, precision="fp32"):
@@ -1060,12 +1060,13 @@ def main():
            "roofline": roof, "gather": None, "cpu_baseline": None,
            "parity": {"tolerance": "max|ours - reference| / max(1, max|reference|) <= 1e-3 (north_star)",
                       "fwdh_train_c4": "the headline policy (round 6, late): forward products on the two-plane fp16 split "
-                                       "f16x3 (22-bit operands, pre-scaled out of fp16's subnormals), backward bf16x3.  "
-                                       "Train mode at the test seed (tests/test_train_parity_gpu.py): every output, "
-                                       "gradient and post-Adam parameter within 1e-3 of the PLAIN oracle (5.5e-5, no "
-                                       "flips).  Over 8 dropout seeds (profiles/r06/h3b_prec.jsonl): 0-4 ReLU decisions "
-                                       "per step differ from the fp32 oracle's (total 12; fwd6 9, bf16x3 100); 3 of 8 "
-                                       "seeds hold every gradient within 1e-3 (fwd6 2, fwd32 4)",
+                                       "f16x3 (22-bit operands, pre-scaled out of fp16's subnormals) with the fused "
+                                       "softmax.P.V, backward bf16x3.  Train mode at the test seed "
+                                       "(tests/test_train_parity_gpu.py): every output, gradient and post-Adam parameter "
+                                       "within 1e-3 of the PLAIN oracle (4.1e-5, no flips).  Over 8 dropout seeds "
+                                       "(profiles/r06/h3g_prec_fused.jsonl): 0-2 ReLU decisions per step differ from the "
+                                       "fp32 oracle's (total 5; fwd32 6, fwd6 9, bf16x3 100); 5 of 8 seeds hold every "
+                                       "gradient within 1e-3 (fwd32 4, fwd6 2)",
                       "fwd6_train_c4": "(the 'fwd6' object) forward products on the three-plane bf16x6 split "
                                        "(fp32-accurate), backward bf16x3.  Train mode at the test seed "
                                        "(tests/test_train_parity_gpu.py): every output, gradient and post-Adam parameter "

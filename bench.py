@@ -1066,7 +1066,9 @@ def main():
                                        "within 1e-3 of the PLAIN oracle (4.1e-5, no flips).  Over 8 dropout seeds "
                                        "(profiles/r06/h3g_prec_fused.jsonl): 0-2 ReLU decisions per step differ from the "
                                        "fp32 oracle's (total 5; fwd32 6, fwd6 9, bf16x3 100); 5 of 8 seeds hold every "
-                                       "gradient within 1e-3 (fwd32 4, fwd6 2)",
+                                       "gradient within 1e-3 (fwd32 4, fwd6 2); over 16 seeds "
+                                       "(profiles/r06/prec_train_16seeds.jsonl) fwdh 7, fwd32 6, fwd6 4, the oracle's "
+                                       "own fp32 vs float64 9",
                       "fwd6_train_c4": "(the 'fwd6' object) forward products on the three-plane bf16x6 split "
                                        "(fp32-accurate), backward bf16x3.  Train mode at the test seed "
                                        "(tests/test_train_parity_gpu.py): every output, gradient and post-Adam parameter "

@@ -30,6 +30,8 @@ POLICIES = {   # name -> (layer precision, role overrides)
     "x6_all": ("bf16x3", {r: "bf16x6" for r in FWD}),
     "fwd6": ("fwd6", {}),
     "fwdh": ("fwdh", {}),
+    "fwdh_3pass": ("fwdh", {}),   # the three-pass attention forward (engine.FUSED_MIN_NP raised for this policy)
+    "fwd32": ("fwd32", {}),
     "x6_nopv": ("bf16x3", {r: "bf16x6" for r in ("in_proj", "qk", "out_proj", "ffn1", "ffn2")}),
     "x6_noqk": ("bf16x3", {r: "bf16x6" for r in ("in_proj", "pv", "out_proj", "ffn1", "ffn2")}),
 }
@@ -59,6 +61,7 @@ def main():
         if a == "--policies":
             only = sys.argv[i + 1].split(",")
     native.set_enabled(False)
+    fused_min_np = engine.FUSED_MIN_NP
     dev = "cuda"
     torch.set_num_threads(min(16, os.cpu_count()))
     np.random.seed(123)
@@ -146,6 +149,7 @@ def main():
                 continue
             engine.ROLE_PREC.clear()
             engine.ROLE_PREC.update(roles)
+            engine.FUSED_MIN_NP = 1 << 30 if pname.endswith("_3pass") else fused_min_np
             m = TransformerU2GNN(d, ff, C, T, 0.5, L, precision=base)
             m.load_state_dict(sd0)
             m = m.to(dev).train()

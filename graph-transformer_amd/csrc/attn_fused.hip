@@ -172,7 +172,7 @@ __device__ __forceinline__ void v_frag6(const char *img, const int (&base)[2], i
 __device__ __forceinline__ void split8_h(const float *x, float sc, bf16x8 &hi, bf16x8 &lo) {
     unsigned h[4], l[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) split2h(x[2 * i] * sc, x[2 * i + 1] * sc, h[i], l[i]);
+    for (int i = 0; i < 4; ++i) split2h(x[2 * i], x[2 * i + 1], sc, h[i], l[i]);
     hi = __builtin_bit_cast(bf16x8, h);
     lo = __builtin_bit_cast(bf16x8, l);
 }

@@ -263,9 +263,9 @@ __device__ __forceinline__ void g2r_bf(__amdgpu_buffer_rsrc_t rs, const int (&vo
 constexpr int NPL_F16X3 = 4;
 template <int NPL> constexpr int nplanes() { return NPL == NPL_F16X3 ? 2 : NPL; }
 template <int NPL>
-__device__ __forceinline__ void split_planes(float x0, float x1, unsigned (&o)[3]) {
+__device__ __forceinline__ void split_planes(float x0, float x1, float sc, unsigned (&o)[3]) {
     if constexpr (NPL == 3) split3(x0, x1, o[0], o[1], o[2]);
-    else if constexpr (NPL == NPL_F16X3) split2h(x0, x1, o[0], o[1]);
+    else if constexpr (NPL == NPL_F16X3) split2h(x0, x1, sc, o[0], o[1]);   // (the pre-scale inside the split)
     else split2<NPL == 2>(x0, x1, o[0], o[1]);
 }
 
@@ -276,10 +276,6 @@ __device__ __forceinline__ void r2s_bf(__bf16 *p0, int pst, int tid, const float
     float4 v[NF];
 #pragma unroll
     for (int i = 0; i < NF; ++i) v[i] = CLAMP ? clamp0(v_[i]) : v_[i];
-    if constexpr (NPL == NPL_F16X3) {   // the operand's pre-scale (a power of two: exact)
-#pragma unroll
-        for (int i = 0; i < NF; ++i) v[i] = make_float4(v[i].x * sc, v[i].y * sc, v[i].z * sc, v[i].w * sc);
-    }
 #ifdef U2GNN_EXP_NOSTAGE
     return;
 #endif
@@ -300,8 +296,8 @@ __device__ __forceinline__ void r2s_bf(__bf16 *p0, int pst, int tid, const float
             o = (kg * NF + i) * (R + 32) + mg * 4;
         }
         unsigned a[3], b[3];
-        split_planes<NPL>(v[i].x, v[i].y, a);
-        split_planes<NPL>(v[i].z, v[i].w, b);
+        split_planes<NPL>(v[i].x, v[i].y, sc, a);
+        split_planes<NPL>(v[i].z, v[i].w, sc, b);
 #pragma unroll
         for (int q = 0; q < nplanes<NPL>(); ++q) *reinterpret_cast<uint2 *>(p0 + q * pst + o) = make_uint2(a[q], b[q]);
     }

@@ -98,8 +98,11 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
 // (x0, x1) -> packed bf16 hi pair and, for SPLIT, the packed bf16 residual pair:
-// one v_cvt_pk_bf16_f32, two bit ops, two subtractions, one more cvt_pk (3 VALU / element).
+// one v_cvt_pk_bf16_f32, two bit ops, one packed subtraction (v_pk_add_f32: both residuals, exact), one more
+// cvt_pk (5 VALU per pair; two scalar subtractions made it 6, the same bits).
 template <bool SPLIT>
 __device__ __forceinline__ void split2(float x0, float x1, unsigned &h, unsigned &l) {
     // opaque to the optimizer: otherwise it re-derives bf16(x0) with a second cvt instead of
@@ -109,8 +112,8 @@ __device__ __forceinline__ void split2(float x0, float x1, unsigned &h, unsigned
 #endif
     asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(h) : "v"(x0), "v"(x1));
     if constexpr (SPLIT) {
-        const float l0 = x0 - __uint_as_float(h << 16), l1 = x1 - __uint_as_float(h & 0xffff0000u);
-        l = __builtin_bit_cast(unsigned, bf16x2{(__bf16)l0, (__bf16)l1});
+        const f32x2 r = f32x2{x0, x1} - f32x2{__uint_as_float(h << 16), __uint_as_float(h & 0xffff0000u)};
+        l = __builtin_bit_cast(unsigned, bf16x2{(__bf16)r.x, (__bf16)r.y});
     }
 }
 
@@ -127,20 +130,24 @@ __device__ __forceinline__ void split3(float x0, float x1, unsigned &h, unsigned
 
 // (x0, x1) -> packed fp16 pairs hi, lo with hi = fp16_rne(x), lo = fp16_rne(x - hi) (U2GNN_PREC_F16X3): the
 // residual is exact in fp32, so the pair carries 22 significant bits of x (fewer where lo is subnormal)
-typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-__device__ __forceinline__ void split2h(float x0, float x1, unsigned &h, unsigned &l) {
-    const f16x2 hv = {(_Float16)x0, (_Float16)x1};
-    const f16x2 lv = {(_Float16)(x0 - (float)hv.x), (_Float16)(x1 - (float)hv.y)};
-    h = __builtin_bit_cast(unsigned, hv);
-    l = __builtin_bit_cast(unsigned, lv);
+// ... of the pre-scaled pair (s x0, s x1), s a power of two: hi = fp16_rne(s x) and lo = fp16_rne(s x - hi), each one
+// mixed-precision fma (v_fma_mix{lo,hi}_f16: the product and the difference exact, one rounding), 4 VALU per pair --
+// the compiler's form of the same arithmetic formed hi twice (mix + mul + cvt_pk) and took 7, the same bits
+__device__ __forceinline__ void split2h(float x0, float x1, float s, unsigned &h, unsigned &l) {
+    asm("v_fma_mixlo_f16 %0, %1, %2, 0\n\t"
+        "v_fma_mixhi_f16 %0, %1, %3, 0"
+        : "=&v"(h) : "v"(s), "v"(x0), "v"(x1));
+    asm("v_fma_mixlo_f16 %0, %1, %2, -%4 op_sel_hi:[0,0,1]\n\t"
+        "v_fma_mixhi_f16 %0, %1, %3, -%4 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+        : "=&v"(l) : "v"(s), "v"(x0), "v"(x1), "v"(h));
 }
 
 // x2 store of four consecutive columns in the f16x3 form: fp16 hi / lo of sc * o (the same layout)
 __device__ __forceinline__ void store_x2h_4(__bf16 *Cx2, int64_t ldcx2, int row, int col, float4 o, float sc) {
     unsigned h0, h1, l0, l1;
-    split2h(o.x * sc, o.y * sc, h0, l0);
-    split2h(o.z * sc, o.w * sc, h1, l1);
+    split2h(o.x, o.y, sc, h0, l0);
+    split2h(o.z, o.w, sc, h1, l1);
     __bf16 *b = Cx2 + (int64_t)row * ldcx2 + 2 * (col & ~7) + (col & 7);
     *reinterpret_cast<uint2 *>(b) = make_uint2(h0, h1);
     *reinterpret_cast<uint2 *>(b + 8) = make_uint2(l0, l1);

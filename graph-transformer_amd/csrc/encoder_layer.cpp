@@ -555,8 +555,11 @@ int layer_fwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
         // 256x128 blocks from 3 waves of them on (token-sized rows, neighbour mode), the default tile
         // rule below that: C4's 19 x 9 blocks of 256x128 leave a third of the CUs idle, its 76 x 18 64-tile
         // blocks run the step 0.8 % faster (3/3 reps, profiles/r02/qkv_tile_ab.txt; bit-identical).
-        const int qkv_tile = (prec != U2GNN_PREC_F32 && Np % 256 == 0 &&
-                              (Np / 256) * (3 * dp / 128) >= U2GNN_BIG_TILE_BLOCKS) ? 256 : 0;
+        int qkv_tile = (prec != U2GNN_PREC_F32 && Np % 256 == 0 &&
+                        (Np / 256) * (3 * dp / 128) >= U2GNN_BIG_TILE_BLOCKS) ? 256 : 0;
+#ifdef U2GNN_EXP_QKV256   // (A/B: 256x128 blocks for every in-projection with Np % 256 == 0)
+        if (prec != U2GNN_PREC_F32 && Np % 256 == 0) qkv_tile = 256;
+#endif
         g.tb().epi(U2GNN_EPI_BIAS).tile(qkv_tile);
         g.a.bias = w->b_in;
         g.a.alpha = (float)(1.0 / std::sqrt((double)d));
@@ -647,6 +650,9 @@ int layer_fwd(const Dims &D, const u2gnn_layer_params *w, const u2gnn_layer_seed
         {
             G g(c.X1, w->W1, c.Hd, Np, ffp, dp, dp, dp, ffp, prec);
             g.tb().epi(U2GNN_EPI_BIAS_RELU_DROP);
+#ifdef U2GNN_EXP_FFN1_256   // (A/B: FFN1 on 256x128 blocks)
+            if (prec != U2GNN_PREC_F32 && Np % 256 == 0 && ffp % 128 == 0) g.tile(256);
+#endif
             g.a.bias = w->b1, g.a.p_drop = pd, g.a.seed = s->dropff;
             U2GNN_TRY(g.run(st, plan));
         }
